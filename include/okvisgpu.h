@@ -1,0 +1,274 @@
+/*
+ * okvisgpu.h — C ABI of the MI355X-native sliding-window bundle-adjustment backend.
+ *
+ * This is the drop-in boundary that replaces `::ceres::Solve(options_, problem_.get(), &summary_)`
+ * inside `okvis::ViGraph::optimise()` (reference: okvis_ceres/src/ViGraph.cpp:1844-1890, the call
+ * itself at :1884). Everything the reference hands to Ceres through the `::ceres::Problem` subset
+ *  is handed over here as plain structure-of-arrays host buffers; the library copies
+ * them to device memory, solves on the GPU, and writes the optimised parameter blocks back into
+ * the SAME caller-owned host arrays (the reference's in-place ParameterBlock semantics,
+ * okvis_ceres/include/okvis/ceres/PoseParameterBlock.hpp:62-78).
+ *
+ * Conventions (all FP64, host memory, caller-owned; the library never frees caller memory):
+ *   pose / extrinsics block : [t_x t_y t_z q_x q_y q_z q_w]   (PoseParameterBlock, 7 doubles)
+ *   speed-and-bias block    : [v(3) b_g(3) b_a(3)]            (SpeedAndBiasParameterBlock, 9)
+ *   landmark block          : [x y z w] homogeneous            (HomogeneousPointParameterBlock, 4)
+ *   time stamps             : int64 nanoseconds (okvis::Time sec/nsec, okvis_time/.../Time.hpp:124)
+ *
+ * No C++ exceptions cross this boundary. Every entry point returns an okvisgpu_status; the text
+ * of the last error of a context is available from okvisgpu_last_error().
+ *
+ * Threading (SURVEY.md §8b "Threading"): one okvisgpu_ctx per graph (realtime graph, full graph);
+ * each context owns one HIP stream and its device buffers. Entry points are re-entrant across
+ * contexts, not within one.
+ */
+#ifndef OKVISGPU_H_
+#define OKVISGPU_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OKVISGPU_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- status codes */
+typedef enum okvisgpu_status {
+  OKVISGPU_OK = 0,
+  OKVISGPU_ERR_INVALID_ARGUMENT = 1,
+  OKVISGPU_ERR_UNSUPPORTED = 2,     /* a problem feature the GPU path does not implement yet */
+  OKVISGPU_ERR_DEVICE = 3,          /* HIP runtime error / no device / kernel image missing   */
+  OKVISGPU_ERR_OUT_OF_MEMORY = 4,
+  OKVISGPU_ERR_NO_PROBLEM = 5,
+  OKVISGPU_ERR_NUMERICAL = 6
+} okvisgpu_status;
+
+/* ---------------------------------------------------------------- enums mirroring Ceres/okvis */
+typedef enum okvisgpu_distortion {
+  OKVISGPU_DIST_NONE = 0,           /* okvis_cv/.../NoDistortion.hpp */
+  OKVISGPU_DIST_RADTAN = 1,         /* okvis_cv/.../implementation/RadialTangentialDistortion.hpp:70-137 */
+  OKVISGPU_DIST_EQUIDISTANT = 2     /* okvis_cv/.../implementation/EquidistantDistortion.hpp:67-188 */
+} okvisgpu_distortion;
+
+typedef enum okvisgpu_linear_solver {
+  OKVISGPU_DENSE_SCHUR = 0          /* ViSlamBackend.cpp:877 realtime graph */
+} okvisgpu_linear_solver;
+
+typedef enum okvisgpu_tr_strategy {
+  OKVISGPU_DOGLEG = 0               /* ViGraph.cpp:249 (traditional dogleg) */
+} okvisgpu_tr_strategy;
+
+typedef enum okvisgpu_termination {  /* ::ceres::TerminationType subset */
+  OKVISGPU_CONVERGENCE = 0,
+  OKVISGPU_NO_CONVERGENCE = 1,
+  OKVISGPU_FAILURE = 2,
+  OKVISGPU_USER_SUCCESS = 3         /* CeresIterationCallback time limit (CeresIterationCallback.cpp:30-38) */
+} okvisgpu_termination;
+
+/* ---------------------------------------------------------------- problem description */
+typedef struct okvisgpu_camera {
+  int32_t distortion;               /* okvisgpu_distortion */
+  int32_t width, height;
+  double fu, fv, cu, cv;            /* PinholeCamera intrinsics (PinholeCamera.hpp:288-366) */
+  double dist[4];                   /* radtan: k1 k2 p1 p2 ; equidistant: k1 k2 k3 k4 */
+} okvisgpu_camera;
+
+typedef struct okvisgpu_imu_params { /* okvis::ImuParameters subset, okvis_common/.../Parameters.hpp:89-105 */
+  double a_max, g_max;
+  double sigma_g_c, sigma_a_c, sigma_gw_c, sigma_aw_c;
+  double g;
+} okvisgpu_imu_params;
+
+/* Size (doubles) of one ImuError's persistent preintegration state (in/out, see imu_state). Layout:
+ *  [0]       redo counter (0 => never integrated; first Evaluate integrates, ImuError.cpp:837)
+ *  [1]       redo_ flag
+ *  [2..5]    Delta_q (x y z w)        [6..14]   C_integral (row-major)
+ *  [15..23]  C_doubleintegral         [24..26]  acc_integral
+ *  [27..29]  acc_doubleintegral       [30..38]  dalpha_db_g
+ *  [39..47]  dv_db_g                  [48..56]  dp_db_g
+ *  [57..65]  speedAndBiases_ref_ (9)  [66..290] squareRootInformation_ (15x15 row-major)
+ *  [291]     steps integrated by the last redo (informational)                               */
+#define OKVISGPU_IMU_STATE_DOUBLES 292
+
+typedef struct okvisgpu_problem {
+  /* --- parameter blocks (written back in place by okvisgpu_solve / okvisgpu_get_params) */
+  int32_t n_poses;
+  double* poses;                    /* [n_poses][7] T_WS                                       */
+  const uint8_t* pose_constant;     /* [n_poses] 1 = SetParameterBlockConstant (may be NULL)    */
+  int32_t n_speed_biases;
+  double* speed_biases;             /* [n_speed_biases][9]                                     */
+  const uint8_t* speed_bias_constant;
+  int32_t n_landmarks;
+  double* landmarks;                /* [n_landmarks][4]                                        */
+  const uint8_t* landmark_constant;
+  int32_t n_cameras;
+  const okvisgpu_camera* cameras;   /* [n_cameras]                                             */
+  const double* extrinsics;         /* [n_cameras][7] T_SC — constant (do_extrinsics: false)    */
+
+  /* --- ReprojectionError<PinholeCamera<D>> residual blocks (ViGraph.hpp:307-352) */
+  int32_t n_observations;
+  const int32_t* obs_pose;          /* [n_obs] pose block index                                */
+  const int32_t* obs_landmark;      /* [n_obs] landmark block index                            */
+  const int32_t* obs_camera;        /* [n_obs] camera / extrinsics index                       */
+  const double* obs_keypoint;       /* [n_obs][2] measurement_                                 */
+  const double* obs_sqrt_info;      /* [n_obs][4] squareRootInformation_ = LLT(info).L^T, row-major
+                                       (ReprojectionError.hpp:49-57; info = 64/size^2 I)         */
+  const uint8_t* obs_cauchy;        /* [n_obs] 1 = CauchyLoss(1.0) (ViGraph.cpp:235), NULL = all */
+
+  /* --- ImuError residual blocks (ImuError.cpp:797-1003), parameter order (pose0, sb0, pose1, sb1) */
+  int32_t n_imu;
+  const int32_t* imu_blocks;        /* [n_imu][4] pose0 sb0 pose1 sb1                           */
+  const int64_t* imu_t0_ns;         /* [n_imu]                                                  */
+  const int64_t* imu_t1_ns;         /* [n_imu]                                                  */
+  const int32_t* imu_sample_begin;  /* [n_imu+1] CSR into the sample arrays                     */
+  const int64_t* imu_sample_t_ns;   /* [n_samples]                                              */
+  const double* imu_sample_gyr_acc; /* [n_samples][6] gyroscopes(3) accelerometers(3)           */
+  okvisgpu_imu_params imu_params;
+  double* imu_state;                /* [n_imu][OKVISGPU_IMU_STATE_DOUBLES] in/out, NULL = fresh  */
+
+  /* --- PoseError priors (PoseError.cpp:73-125) */
+  int32_t n_pose_priors;
+  const int32_t* pose_prior_block;  /* [n] pose index                                           */
+  const double* pose_prior_meas;    /* [n][7]                                                   */
+  const double* pose_prior_sqrt_info; /* [n][36] row-major                                      */
+
+  /* --- SpeedAndBiasError priors (SpeedAndBiasError.cpp:67-101) */
+  int32_t n_sb_priors;
+  const int32_t* sb_prior_block;
+  const double* sb_prior_meas;      /* [n][9]                                                   */
+  const double* sb_prior_sqrt_info; /* [n][81] row-major                                        */
+} okvisgpu_problem;
+
+/* ---------------------------------------------------------------- solver options / summary */
+typedef struct okvisgpu_options {   /* ::ceres::Solver::Options fields okvis sets or relies on */
+  int32_t max_num_iterations;       /* ViGraph.cpp:1856                                         */
+  int32_t linear_solver;            /* okvisgpu_linear_solver                                   */
+  int32_t trust_region_strategy;    /* okvisgpu_tr_strategy                                     */
+  int32_t jacobi_scaling;           /* Ceres default true                                       */
+  double function_tolerance;        /* 1e-6 default; 1e-3 for the first full-graph pass          */
+  double gradient_tolerance;        /* 1e-10                                                    */
+  double parameter_tolerance;       /* 1e-8                                                     */
+  double initial_trust_region_radius; /* 1e4                                                    */
+  double max_trust_region_radius;   /* 1e16                                                     */
+  double min_trust_region_radius;   /* 1e-32                                                    */
+  double min_relative_decrease;     /* 1e-3                                                     */
+  double min_lm_diagonal;           /* 1e-6                                                     */
+  double max_lm_diagonal;           /* 1e32                                                     */
+  int32_t max_num_consecutive_invalid_steps; /* 5                                               */
+  double time_limit_s;              /* <0: none (ViGraph::setOptimisationTimeLimit)              */
+  int32_t min_iterations;           /* CeresIterationCallback iterationMinimum_                  */
+  int32_t redo_propagation_always;  /* ImuError::redoPropagationAlways (ViSlamBackend.cpp:2036)  */
+  int32_t num_threads;              /* host threads (reference path / host evaluation)          */
+  int32_t verbose;
+} okvisgpu_options;
+
+typedef struct okvisgpu_summary {   /* ::ceres::Solver::Summary subset */
+  double initial_cost;
+  double final_cost;
+  int32_t num_iterations;           /* iterations performed, excluding iteration 0              */
+  int32_t num_successful_steps;     /* Ceres counts iteration 0 as successful                    */
+  int32_t num_unsuccessful_steps;
+  int32_t termination_type;         /* okvisgpu_termination                                     */
+  double total_time_s;              /* wall time of okvisgpu_solve for this batch               */
+  double final_radius;
+  double final_mu;
+} okvisgpu_summary;
+
+/* ---------------------------------------------------------------- context */
+typedef struct okvisgpu_ctx okvisgpu_ctx;
+
+int okvisgpu_abi_version(void);
+void okvisgpu_default_options(okvisgpu_options* options);
+int okvisgpu_device_count(int32_t* count);
+int okvisgpu_ctx_create(int32_t device, okvisgpu_ctx** ctx);
+int okvisgpu_ctx_destroy(okvisgpu_ctx* ctx);
+const char* okvisgpu_last_error(const okvisgpu_ctx* ctx);
+
+/* Upload a batch of independent windows (one window = one okvis::ViGraph problem). The structure
+ * (residual blocks, parameter blocks, constant flags) is analysed once here. The problem structs
+ * and the arrays they point to must stay valid until the next okvisgpu_set_problems() call,
+ * because okvisgpu_solve() writes results back into them. */
+int okvisgpu_set_problems(okvisgpu_ctx* ctx, const okvisgpu_problem* problems, int32_t n_windows);
+
+/* Re-upload only parameter values (and imu_state) from the host arrays (after the caller changed
+ * estimates between solves, e.g. ViSlamBackend re-initialising states). */
+int okvisgpu_update_params(okvisgpu_ctx* ctx);
+
+/* SetParameterBlockConstant / SetParameterBlockVariable between solves (freeze / unfreeze:
+ * ViGraphEstimator.cpp:216-331). kind: 0 pose, 1 speed/bias, 2 landmark. Takes effect at the next
+ * okvisgpu_solve (the reduced-system structure is rebuilt on the host, values stay on device). */
+int okvisgpu_set_block_constant(okvisgpu_ctx* ctx, int32_t window, int32_t kind, int32_t index,
+                                int32_t is_constant);
+
+/* ::ceres::Solve equivalent for every window in the batch. summaries: [n_windows] (may be NULL).
+ * Results are written back into the caller's parameter arrays (and imu_state when provided). */
+int okvisgpu_solve(okvisgpu_ctx* ctx, const okvisgpu_options* options, okvisgpu_summary* summaries);
+
+/* Copy device parameter values back into the caller's host arrays without solving. */
+int okvisgpu_get_params(okvisgpu_ctx* ctx);
+
+/* ---------------------------------------------------------------- evaluation entry points
+ * (::ceres::Problem::Evaluate / EvaluateResidualBlock analogues; also the parity-test hooks)
+ *
+ * okvisgpu_evaluate: total cost 1/2 sum rho(|r|^2) of window w at the current device parameters.
+ */
+int okvisgpu_evaluate(okvisgpu_ctx* ctx, int32_t window, double* cost);
+
+/* Linearise window w at the current parameters and eliminate the landmarks (DENSE_SCHUR):
+ *   S   = H_ff - H_fl H_ll^-1 H_lf,   rhs = g_f - H_fl H_ll^-1 g_l,   g = J^T r (Cauchy-corrected)
+ * with Jacobi scaling (if jacobi_scaling) and the dogleg LM diagonal D = diag(J^T J)^(1/2)*sqrt(mu)
+ * exactly as the solver's first Gauss-Newton solve would form them. Outputs (host, may be NULL):
+ *   S   [dim*dim] row-major (full symmetric), rhs [dim], cost [1], dim_out [1].
+ * The reduced ordering is: for i = 0 .. max(n_poses, n_speed_biases)-1: pose i (6, if variable)
+ * then speed/bias i (9, if variable). */
+int okvisgpu_linearize_reduce(okvisgpu_ctx* ctx, int32_t window, int32_t jacobi_scaling, double mu,
+                              double* S, double* rhs, double* cost, int32_t* dim_out);
+
+/* Raw per-residual evaluation for parity tests (EvaluateWithMinimalJacobians semantics, no loss):
+ *   reprojection: r [n_obs][2], J_pose [n_obs][2][6], J_landmark [n_obs][2][3] (minimal, row-major)
+ *   imu:          r [n_imu][15], J [n_imu][15][30] minimal columns (pose0 6, sb0 9, pose1 6, sb1 9)
+ * Any output pointer may be NULL. The IMU call updates the factor's preintegration state exactly as
+ * ImuError::EvaluateWithMinimalJacobians does (ImuError.cpp:833-859). */
+int okvisgpu_eval_reprojection(okvisgpu_ctx* ctx, int32_t window, double* r, double* J_pose,
+                               double* J_landmark);
+int okvisgpu_eval_imu(okvisgpu_ctx* ctx, int32_t window, int32_t redo_always, double* r, double* J);
+
+/* ---------------------------------------------------------------- synthetic windows
+ * Host-side generator of the synthetic sliding windows the benchmark is quoted on:
+ * EuRoC stereo rig (config/euroc/okvis2.yaml:2-32), smooth sinusoidal 6-DoF trajectory
+ * (okvis_ceres/test/TestImuError.cpp:86-185 style), 200 Hz IMU, landmarks in a 2-20 m band,
+ * observations with N(0,1px^2) noise and information 64/8^2 = I, perturbed initial states, priors as
+ * ViGraph::addStatesInitialise (ViGraph.cpp:347-370), Cauchy(1) on every reprojection.
+ * std::mt19937_64(seed). No GPU is touched. */
+typedef struct okvisgpu_synth_config {
+  int32_t n_keyframes;              /* S10: 10, S50: 50 */
+  int32_t n_landmarks;              /* S10: 500, S50: 2000 */
+  int32_t n_observations;           /* S10: 4000, S50: 16000 */
+  int32_t max_obs_per_landmark;     /* 20 */
+  double kf_dt_s;                   /* 0.1 */
+  double imu_rate_hz;               /* 200 */
+  double pixel_noise;               /* 1.0 */
+  double init_sigma_pos, init_sigma_rot, init_sigma_lm, init_sigma_vel; /* 0.05 0.01 0.05 0.02 */
+  uint64_t seed;
+} okvisgpu_synth_config;
+
+typedef struct okvisgpu_synth_window okvisgpu_synth_window;  /* owns all arrays of one problem */
+
+void okvisgpu_synth_default_config(okvisgpu_synth_config* cfg, int32_t n_keyframes,
+                                   int32_t n_landmarks, int32_t n_observations, uint64_t seed);
+int okvisgpu_synth_create(const okvisgpu_synth_config* cfg, okvisgpu_synth_window** out);
+/* The problem view into the window's arrays (valid until destroy). */
+const okvisgpu_problem* okvisgpu_synth_problem(okvisgpu_synth_window* w);
+/* Ground truth: poses [n_kf][7], landmarks [n_lm][4], speed_biases [n_kf][9] (may be NULL). */
+int okvisgpu_synth_ground_truth(const okvisgpu_synth_window* w, double* poses, double* landmarks,
+                                double* speed_biases);
+/* Reset the problem's parameter arrays (and imu_state) to the generated initial estimate. */
+int okvisgpu_synth_reset(okvisgpu_synth_window* w);
+void okvisgpu_synth_destroy(okvisgpu_synth_window* w);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif /* OKVISGPU_H_ */

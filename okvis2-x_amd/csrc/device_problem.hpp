@@ -1,0 +1,190 @@
+// device_problem.hpp — HBM layout of a batch of sliding windows and the per-window trust-region
+// state. One flat, window-concatenated array per quantity so that every kernel covers the whole
+// batch in one launch (batch index = window; SURVEY.md §8e "replicas only" sharding).
+//
+// Index spaces (all global over the batch):
+//   pose p in [0, n_pose)   sb s in [0, n_sb)   landmark l in [0, n_lm)   obs o in [0, n_obs)
+//   visit v in [0, n_visit) : maximal run of observations of ONE landmark from ONE pose (stereo
+//                             pairs of a keyframe aggregate into one visit); obs sorted by
+//                             (window, landmark, pose, camera)
+//   imu factor f in [0, n_imu)
+//   f-vector index: the reduced ("camera") system of window w occupies [foff[w], foff[w]+fdim[w])
+//   S of window w: dense row-major fpad[w] x fpad[w] at soff[w] (lower triangle used), padded to a
+//   multiple of 64 with identity on the padded diagonal.
+#pragma once
+
+#include <cstdint>
+
+namespace okg {
+
+constexpr int kTile = 64;             // Cholesky tile (one 64x64 FP64 tile = 32 KiB of LDS)
+constexpr int kImuLin = 15 + 15 * 30; // per-IMU-factor linearisation record: r[15], J[15][30]
+constexpr int kImuState = 292;        // == OKVISGPU_IMU_STATE_DOUBLES
+
+// Linearisation record per observation (structure of arrays, plane-major):
+//   plane 0-1: r (Cauchy-corrected)   plane 2-13: J_pose 2x6   plane 14-19: J_lm 2x3
+constexpr int kObsLin = 20;
+
+// contribution record types for the reduced-system assembly
+enum ContribType : int32_t {
+  C_VISIT = 0,      // a = visit: Hpp / gp of the visit (pose diagonal block)
+  C_PAIR = 1,       // a = visit i, b = visit j (same landmark): - W_i V^-1 W_j^T
+  C_IMU = 2,        // a = factor, b = column offset of row block, c = column offset of col block
+  C_PPRIOR = 3,     // a = pose prior
+  C_SBPRIOR = 4     // a = sb prior
+};
+
+struct Contrib {
+  int32_t type, a, b, c;
+};
+
+struct WinState {
+  double radius, mu;
+  double x_cost, cand_cost, fixed_cost, initial_cost, min_cost;
+  double x_norm, step_norm;
+  double alpha, dogleg_step_norm, model_cost_change;
+  double grad_max_norm, grad_norm;
+  double jv2, jvr;                 // reductions of the last J*v pass
+  int32_t xcur, lcur;              // current parameter set / linearisation buffer (0/1)
+  int32_t need_gn;                 // !DoglegStrategy::reuse_
+  int32_t done, termination;
+  int32_t iteration, num_succ, num_unsucc, consecutive_invalid;
+  int32_t gn_failed;               // Cholesky / 3x3 inverse failure in this GN attempt
+  int32_t eval_cand;               // candidate must be evaluated this iteration
+  int32_t step_valid;
+  int32_t accepted;
+  int32_t pad_[3];
+};
+
+// Options mirrored on the device (okvisgpu_options subset used inside kernels).
+struct DevOptions {
+  int32_t max_num_iterations;
+  int32_t jacobi_scaling;
+  int32_t max_num_consecutive_invalid_steps;
+  int32_t redo_propagation_always;
+  double function_tolerance, gradient_tolerance, parameter_tolerance;
+  double initial_radius, max_radius, min_radius;
+  double min_relative_decrease, min_lm_diagonal, max_lm_diagonal;
+};
+
+struct DevProblem {
+  int32_t n_win, n_pose, n_sb, n_lm, n_obs, n_visit, n_imu, n_pprior, n_sbprior, n_cam;
+  int32_t n_fblock, n_pair;
+  int32_t max_fpad, max_tiles;     // largest padded reduced dimension / its 64-tile count
+  int64_t obs_stride;              // plane stride of the obs linearisation SoA (>= n_obs)
+
+  // --- parameters, two sets (current / candidate), ambient
+  double* pose[2];                 // [n_pose][7]
+  double* sb[2];                   // [n_sb][9]
+  double* lm[2];                   // [n_lm][4]
+  const double* extr;              // [n_cam][7]
+  const double* cam;               // [n_cam][9]: dist, fu, fv, cu, cv, d0..d3 (dist as double)
+
+  // --- per-block window id and reduced-system offsets (-1: not a free f-block / e-block)
+  const int32_t* pose_win;         // [n_pose]
+  const int32_t* sb_win;
+  const int32_t* lm_win;
+  const int32_t* pose_f;           // [n_pose] offset in the window's f-vector, -1 if not free
+  const int32_t* sb_f;             // [n_sb]
+  const uint8_t* lm_free;          // [n_lm] 1 = e-block
+  const uint8_t* pose_active;      // [n_pose] active (free & used) — included in norms / Plus
+  const uint8_t* sb_active;
+
+  // --- observations (sorted)
+  const int32_t* obs_pose;         // global pose index
+  const int32_t* obs_lm;           // global landmark index
+  const int32_t* obs_cam;          // global camera index
+  const int32_t* obs_win;
+  const uint8_t* obs_flags;        // bit0 cauchy, bit1 fixed (all blocks constant)
+  const double* obs_kp;            // [n_obs][2]
+  const double* obs_L;             // [n_obs][4]
+  double* obs_lin[2];              // [kObsLin][obs_stride]
+  double* obs_cost[2];             // [n_obs]
+  double* obs_jv;                  // [2][n_obs]: (Jv)^2, (Jv).r
+
+  // --- landmarks / visits
+  const int32_t* lm_visit_begin;   // [n_lm+1] visits of landmark l
+  const int32_t* visit_pose;       // [n_visit]
+  const int32_t* visit_obs_begin;  // [n_visit+1]
+  const int32_t* visit_lm;         // [n_visit]
+  double* lm_V;                    // [n_lm][6]  sum J_l^T J_l (unscaled, sym packed 00 01 02 11 12 22)
+  double* lm_g;                    // [n_lm][3]  J_l^T r
+  double* lm_Vinv;                 // [n_lm][6]  (s V s + D^2)^-1
+  double* lm_z;                    // [n_lm][3]  Vinv (s g)
+  double* visit_W;                 // [n_visit][18] J_p^T J_l (unscaled)
+  double* visit_H;                 // [n_visit][21] J_p^T J_p (unscaled, sym packed)
+  double* visit_g;                 // [n_visit][6]  J_p^T r
+
+  // --- IMU factors
+  const int32_t* imu_blocks;       // [n_imu][4] global pose0 sb0 pose1 sb1
+  const int32_t* imu_win;
+  const uint8_t* imu_flags;        // bit1 fixed
+  const int64_t* imu_t0;
+  const int64_t* imu_t1;
+  const int32_t* imu_sbegin;       // [n_imu+1]
+  const int64_t* imu_ts;
+  const double* imu_ga;            // [n_samples][6]
+  const double* imu_par;           // [n_win][7]: a_max g_max sigma_g_c sigma_a_c sigma_gw_c sigma_aw_c g
+  double* imu_state;               // [n_imu][kImuState]
+  double* imu_lin[2];              // [n_imu][kImuLin]
+  double* imu_cost[2];             // [n_imu]
+  double* imu_jv;                  // [2][n_imu]
+
+  // --- priors
+  const int32_t* pp_block;         // [n_pprior] global pose
+  const int32_t* pp_win;
+  const double* pp_meas;           // [n][7]
+  const double* pp_L;              // [n][36]
+  double* pp_lin[2];               // [n][6 + 36]
+  double* pp_cost[2];
+  double* pp_jv;                   // [2][n]
+  const int32_t* sbp_block;
+  const int32_t* sbp_win;
+  const double* sbp_meas;          // [n][9]
+  const double* sbp_L;             // [n][81]
+  double* sbp_lin[2];              // [n][9 + 81]
+  double* sbp_cost[2];
+  double* sbp_jv;
+
+  // --- reduced system structure
+  const int32_t* win_foff;         // [n_win]
+  const int32_t* win_fdim;
+  const int32_t* win_fpad;
+  const int64_t* win_soff;         // [n_win] offset of S
+  const int32_t* win_pose_range;   // [n_win][2]
+  const int32_t* win_sb_range;
+  const int32_t* win_lm_range;
+  const int32_t* win_obs_range;
+  const int32_t* win_imu_range;
+  const int32_t* win_pp_range;
+  const int32_t* win_sbp_range;
+  const int32_t* fb_win;           // [n_fblock] window
+  const int32_t* fb_kind;          // 0 pose / 1 sb
+  const int32_t* fb_index;         // global pose / sb index
+  const int32_t* fb_off;           // offset in the window's f-vector
+  const int32_t* fb_cbegin;        // [n_fblock+1] gradient / diagonal contributions (C_VISIT, C_IMU, priors)
+  const Contrib* fb_contrib;
+  const int32_t* pair_win;         // [n_pair]
+  const int32_t* pair_fi;          // global f-block index (row, fi >= fj)
+  const int32_t* pair_fj;
+  const int32_t* pair_cbegin;      // [n_pair+1]
+  const Contrib* pair_contrib;
+
+  // --- f-vectors (window-concatenated, reduced ordering) and landmark vectors
+  double* S;                       // sum over windows fpad^2
+  double* sF;   double* sL;        // Jacobi scaling (fixed at iteration 0)
+  double* diagF; double* diagL;    // dogleg diagonal_
+  double* hdF;                     // unscaled diag(H_ff)
+  double* gF;   double* gL;        // unscaled gradient J^T r
+  double* rhsF;                    // Schur rhs / forward-substitution workspace
+  double* yF;   double* yL;        // GN solution (Jacobi-scaled space)
+  double* gnF;  double* gnL;       // gauss_newton_step_ (dogleg-scaled)
+  double* dgF;  double* dgL;       // gradient_ (dogleg-scaled)
+  double* vF;   double* vL;        // J*v operand (Jacobi-scaled space)
+  double* stepF; double* stepL;    // trust-region step (Jacobi-scaled space)
+
+  WinState* st;                    // [n_win]
+  DevOptions opt;
+};
+
+}  // namespace okg

@@ -1,0 +1,554 @@
+// kernels_control.hip — the trust-region loop on the device (no host round trip per iteration).
+//
+// Restates ceres::internal::TrustRegionMinimizer + DoglegStrategy (TRADITIONAL_DOGLEG) as used by
+// okvis (ViGraph.cpp:249, ViSlamBackend.cpp:877) [ext-Ceres, un-vendored; see DESIGN.md]:
+//   k_jv        per residual block: J*v with the Jacobi scaling applied on the fly; emits
+//               (Jv)^2 and (Jv).r for the Cauchy point (|J g|^2) and the model cost change.
+//   k_reduce    one workgroup per window, fixed-order tree reductions (bitwise reproducible):
+//               costs, Cauchy alpha, model_cost_change (+ the step-validity bookkeeping), and the
+//               candidate acceptance test (parameter / function tolerance, relative decrease,
+//               radius and mu updates).
+//   k_gradnorm  |x - Plus(x, -g)|_inf / _2 and |x| after every accepted step.
+//   k_dogleg    one workgroup per window: LM-failure retries of the GN step, the traditional
+//               dogleg interpolation, delta = step .* jacobi_scaling and the manifold Plus into
+//               the candidate parameter set.
+#include <cfloat>
+
+#include "device_problem.hpp"
+#include "launch.hpp"
+#include "okvisgpu_math.hpp"
+
+namespace okg {
+
+constexpr int kRB = 256;  // reduction workgroup size
+
+__device__ __forceinline__ double blockSum(double v, double* sh) {
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int s = kRB / 2; s > 0; s >>= 1) {
+    if (t < s) sh[t] += sh[t + s];
+    __syncthreads();
+  }
+  const double r = sh[0];
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ double blockMax(double v, double* sh) {
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int s = kRB / 2; s > 0; s >>= 1) {
+    if (t < s) sh[t] = fmax(sh[t], sh[t + s]);
+    __syncthreads();
+  }
+  const double r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ bool jvSelect(const DevProblem& P, int w, int mode) {
+  const WinState& s = P.st[w];
+  if (s.done) return false;
+  if (mode == R_JV_CAUCHY) return s.need_gn && !s.gn_failed;
+  return s.step_valid == 2;
+}
+
+__global__ __launch_bounds__(256) void k_jv(DevProblem P, int mode) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const double* vF = (mode == R_JV_CAUCHY) ? P.vF : P.stepF;
+  const double* vL = (mode == R_JV_CAUCHY) ? P.vL : P.stepL;
+  if (t < P.n_obs) {
+    const int o = t;
+    const int w = P.obs_win[o];
+    if (!jvSelect(P, w, mode)) return;
+    double a = 0.0, b = 0.0;
+    if (!(P.obs_flags[o] & 2)) {
+      const int lb = P.st[w].lcur;
+      const double* lin = P.obs_lin[lb];
+      const int64_t S = P.obs_stride;
+      const int pf = P.pose_f[P.obs_pose[o]];
+      const int l = P.obs_lm[o];
+      double vp[6] = {0, 0, 0, 0, 0, 0}, vl[3] = {0, 0, 0};
+      if (pf >= 0) {
+        const size_t base = (size_t)P.win_foff[w] + pf;
+        for (int c = 0; c < 6; ++c) vp[c] = P.sF[base + c] * vF[base + c];
+      }
+      if (P.lm_free[l])
+        for (int c = 0; c < 3; ++c) vl[c] = P.sL[3 * (size_t)l + c] * vL[3 * (size_t)l + c];
+      for (int r = 0; r < 2; ++r) {
+        double jv = 0.0;
+        for (int c = 0; c < 6; ++c) jv += lin[(2 + r * 6 + c) * S + o] * vp[c];
+        for (int c = 0; c < 3; ++c) jv += lin[(14 + r * 3 + c) * S + o] * vl[c];
+        a += jv * jv;
+        b += jv * lin[r * S + o];
+      }
+    }
+    P.obs_jv[o] = a;
+    P.obs_jv[(size_t)P.n_obs + o] = b;
+    return;
+  }
+  int u = t - P.n_obs;
+  if (u < P.n_imu) {
+    const int f = u;
+    const int w = P.imu_win[f];
+    if (!jvSelect(P, w, mode)) return;
+    double a = 0.0, b = 0.0;
+    if (!(P.imu_flags[f] & 2)) {
+      const int lb = P.st[w].lcur;
+      const double* L = P.imu_lin[lb] + (size_t)f * kImuLin;
+      const int* blk = P.imu_blocks + 4 * f;
+      double v[30];
+      const size_t foff = P.win_foff[w];
+      const int offs[4] = {P.pose_f[blk[0]], P.sb_f[blk[1]], P.pose_f[blk[2]], P.sb_f[blk[3]]};
+      const int cols[4] = {0, 6, 15, 21}, ns[4] = {6, 9, 6, 9};
+      for (int q = 0; q < 4; ++q)
+        for (int c = 0; c < ns[q]; ++c)
+          v[cols[q] + c] = offs[q] >= 0 ? P.sF[foff + offs[q] + c] * vF[foff + offs[q] + c] : 0.0;
+      for (int r = 0; r < 15; ++r) {
+        double jv = 0.0;
+        for (int c = 0; c < 30; ++c) jv += L[15 + r * 30 + c] * v[c];
+        a += jv * jv;
+        b += jv * L[r];
+      }
+    }
+    P.imu_jv[f] = a;
+    P.imu_jv[(size_t)P.n_imu + f] = b;
+    return;
+  }
+  u -= P.n_imu;
+  if (u < P.n_pprior) {
+    const int i = u;
+    const int w = P.pp_win[i];
+    if (!jvSelect(P, w, mode)) return;
+    double a = 0.0, b = 0.0;
+    const int pf = P.pose_f[P.pp_block[i]];
+    if (pf >= 0) {
+      const double* L = P.pp_lin[P.st[w].lcur] + 42 * (size_t)i;
+      const size_t base = (size_t)P.win_foff[w] + pf;
+      for (int r = 0; r < 6; ++r) {
+        double jv = 0.0;
+        for (int c = 0; c < 6; ++c) jv += L[6 + r * 6 + c] * P.sF[base + c] * vF[base + c];
+        a += jv * jv;
+        b += jv * L[r];
+      }
+    }
+    P.pp_jv[i] = a;
+    P.pp_jv[(size_t)P.n_pprior + i] = b;
+    return;
+  }
+  u -= P.n_pprior;
+  if (u < P.n_sbprior) {
+    const int i = u;
+    const int w = P.sbp_win[i];
+    if (!jvSelect(P, w, mode)) return;
+    double a = 0.0, b = 0.0;
+    const int sf = P.sb_f[P.sbp_block[i]];
+    if (sf >= 0) {
+      const double* L = P.sbp_lin[P.st[w].lcur] + 90 * (size_t)i;
+      const size_t base = (size_t)P.win_foff[w] + sf;
+      for (int r = 0; r < 9; ++r) {
+        double jv = 0.0;
+        for (int c = 0; c < 9; ++c) jv += L[9 + r * 9 + c] * P.sF[base + c] * vF[base + c];
+        a += jv * jv;
+        b += jv * L[r];
+      }
+    }
+    P.sbp_jv[i] = a;
+    P.sbp_jv[(size_t)P.n_sbprior + i] = b;
+  }
+}
+
+// Bookkeeping common to every iteration end (FinalizeIterationAndCheckIfMinimizerCanContinue):
+// iteration cap, then the trust-region radius floor. (The gradient test follows the next
+// gradient evaluation: k_gradnorm.)
+__device__ void finalizeIteration(const DevProblem& P, WinState& s) {
+  if (s.done) return;
+  if (s.iteration >= P.opt.max_num_iterations) {
+    s.done = 1;
+    s.termination = 1;  // NO_CONVERGENCE
+    return;
+  }
+  if (s.radius <= P.opt.min_radius) {
+    s.done = 1;
+    s.termination = 0;  // CONVERGENCE
+  }
+}
+
+__global__ __launch_bounds__(kRB) void k_reduce(DevProblem P, int mode) {
+  const int w = blockIdx.x;
+  WinState& s = P.st[w];
+  if (s.done) return;
+  __shared__ double sh[kRB];
+  const int t = threadIdx.x;
+  const int ob = P.win_obs_range[2 * w], oe = P.win_obs_range[2 * w + 1];
+  const int ib = P.win_imu_range[2 * w], ie = P.win_imu_range[2 * w + 1];
+  const int pb = P.win_pp_range[2 * w], pe = P.win_pp_range[2 * w + 1];
+  const int sbb = P.win_sbp_range[2 * w], sbe = P.win_sbp_range[2 * w + 1];
+
+  if (mode == R_COST_INIT || mode == R_COST_CAND) {
+    if (mode == R_COST_CAND && !s.eval_cand) return;
+    const int lb = (mode == R_COST_CAND) ? 1 - s.lcur : s.lcur;
+    double c = 0.0, cf = 0.0;
+    for (int o = ob + t; o < oe; o += kRB) {
+      if (P.obs_flags[o] & 2) cf += P.obs_cost[lb][o];
+      else c += P.obs_cost[lb][o];
+    }
+    for (int f = ib + t; f < ie; f += kRB) {
+      if (P.imu_flags[f] & 2) cf += P.imu_cost[lb][f];
+      else c += P.imu_cost[lb][f];
+    }
+    for (int i = pb + t; i < pe; i += kRB) {
+      if (P.pose_f[P.pp_block[i]] < 0) cf += P.pp_cost[lb][i];
+      else c += P.pp_cost[lb][i];
+    }
+    for (int i = sbb + t; i < sbe; i += kRB) {
+      if (P.sb_f[P.sbp_block[i]] < 0) cf += P.sbp_cost[lb][i];
+      else c += P.sbp_cost[lb][i];
+    }
+    c = blockSum(c, sh);
+    cf = blockSum(cf, sh);
+    if (t != 0) return;
+    if (mode == R_COST_CAND) {
+      // fixed residuals are not re-evaluated at candidates; their cost is fixed_cost
+    }
+    if (mode == R_COST_INIT) {
+      s.x_cost = c;
+      s.fixed_cost = cf;
+      s.initial_cost = c + cf;
+      s.min_cost = c;
+      return;
+    }
+    // ------------------------------------------------ candidate acceptance (per iteration)
+    s.cand_cost = c;
+    s.eval_cand = 0;
+    s.step_valid = 0;
+    // ParameterToleranceReached / FunctionToleranceReached: return without finalising the iteration
+    if (s.step_norm <= P.opt.parameter_tolerance * (s.x_norm + P.opt.parameter_tolerance)) {
+      s.done = 1;
+      s.termination = 0;
+      s.iteration -= 1;
+      return;
+    }
+    if (fabs(s.x_cost - c) <= P.opt.function_tolerance * s.x_cost) {
+      s.done = 1;
+      s.termination = 0;
+      s.iteration -= 1;
+      return;
+    }
+    const double rel = isfinite(c) ? (s.x_cost - c) / s.model_cost_change : -DBL_MAX;
+    if (rel > P.opt.min_relative_decrease) {
+      // HandleSuccessfulStep + DoglegStrategy::StepAccepted
+      s.xcur = 1 - s.xcur;
+      s.lcur = 1 - s.lcur;
+      s.x_cost = c;
+      if (c < s.min_cost) s.min_cost = c;
+      s.accepted = 1;
+      s.num_succ += 1;
+      if (rel < 0.25) s.radius *= 0.5;
+      if (rel > 0.75) s.radius = fmax(s.radius, 3.0 * s.dogleg_step_norm);
+      s.radius = fmin(s.radius, P.opt.max_radius);
+      s.mu = fmax(1e-8, 2.0 * s.mu / 10.0);
+      s.need_gn = 1;
+    } else {
+      // HandleUnsuccessfulStep + StepRejected
+      s.num_unsucc += 1;
+      s.radius *= 0.5;
+      s.need_gn = 0;
+    }
+    finalizeIteration(P, s);
+    return;
+  }
+
+  // J*v reductions
+  if (mode == R_JV_CAUCHY && !(s.need_gn && !s.gn_failed)) return;
+  if (mode == R_JV_STEP && s.step_valid != 2) return;
+  double a = 0.0, b = 0.0;
+  for (int o = ob + t; o < oe; o += kRB) { a += P.obs_jv[o]; b += P.obs_jv[(size_t)P.n_obs + o]; }
+  for (int f = ib + t; f < ie; f += kRB) { a += P.imu_jv[f]; b += P.imu_jv[(size_t)P.n_imu + f]; }
+  for (int i = pb + t; i < pe; i += kRB) { a += P.pp_jv[i]; b += P.pp_jv[(size_t)P.n_pprior + i]; }
+  for (int i = sbb + t; i < sbe; i += kRB) { a += P.sbp_jv[i]; b += P.sbp_jv[(size_t)P.n_sbprior + i]; }
+  a = blockSum(a, sh);
+  b = blockSum(b, sh);
+  if (mode == R_JV_CAUCHY) {
+    // |gradient_|^2 over the window (f-vector + free landmarks)
+    double g2 = 0.0;
+    const int fo = P.win_foff[w], fd = P.win_fdim[w];
+    for (int e = t; e < fd; e += kRB) g2 += P.dgF[fo + e] * P.dgF[fo + e];
+    const int lbg = P.win_lm_range[2 * w], lnd = P.win_lm_range[2 * w + 1];
+    for (int l = lbg + t; l < lnd; l += kRB)
+      if (P.lm_free[l])
+        for (int c = 0; c < 3; ++c) g2 += P.dgL[3 * (size_t)l + c] * P.dgL[3 * (size_t)l + c];
+    g2 = blockSum(g2, sh);
+    if (t == 0) {
+      s.jv2 = a;
+      s.alpha = g2 / a;
+    }
+    return;
+  }
+  if (t != 0) return;
+  // model_cost_change = -(J step).(r + J step / 2)
+  s.jv2 = a;
+  s.jvr = b;
+  s.model_cost_change = -(b + 0.5 * a);
+  if (s.model_cost_change > 0.0) {
+    s.step_valid = 1;
+    s.consecutive_invalid = 0;
+    s.eval_cand = 1;
+  } else {
+    // HandleInvalidStep + DoglegStrategy::StepIsInvalid
+    s.step_valid = 0;
+    s.eval_cand = 0;
+    s.num_unsucc += 1;
+    if (++s.consecutive_invalid >= P.opt.max_num_consecutive_invalid_steps) {
+      s.done = 1;
+      s.termination = 2;  // FAILURE
+      return;
+    }
+    s.mu *= 10.0;
+    s.need_gn = 1;
+    finalizeIteration(P, s);
+  }
+}
+
+// |x - Plus(x, -g)| and |x| over the window's active blocks; gradient tolerance test.
+__global__ __launch_bounds__(kRB) void k_gradnorm(DevProblem P, int lin_mode) {
+  const int w = blockIdx.x;
+  WinState& s = P.st[w];
+  if (s.done) return;
+  if (lin_mode == 1 && !s.accepted) return;
+  __shared__ double sh[kRB];
+  const int t = threadIdx.x;
+  const int xs = s.xcur;
+  const int foff = P.win_foff[w];
+  double mx = 0.0, g2 = 0.0, x2 = 0.0;
+  const int p0 = P.win_pose_range[2 * w], p1 = P.win_pose_range[2 * w + 1];
+  for (int p = p0 + t; p < p1; p += kRB) {
+    if (!P.pose_active[p]) continue;
+    const double* x = P.pose[xs] + 7 * (size_t)p;
+    for (int k = 0; k < 7; ++k) x2 += x[k] * x[k];
+    const int pf = P.pose_f[p];
+    const double* g = P.gF + foff + pf;
+    double xp[7];
+    for (int k = 0; k < 3; ++k) xp[k] = x[k] + (-g[k]);
+    const Q dq = deltaQ(-g[3], -g[4], -g[5]);
+    const Q q = qnormalize(qmul(dq, qnormalize(Q{x[3], x[4], x[5], x[6]})));
+    xp[3] = q.x; xp[4] = q.y; xp[5] = q.z; xp[6] = q.w;
+    for (int k = 0; k < 7; ++k) {
+      const double d = x[k] - xp[k];
+      mx = fmax(mx, fabs(d));
+      g2 += d * d;
+    }
+  }
+  const int s0 = P.win_sb_range[2 * w], s1 = P.win_sb_range[2 * w + 1];
+  for (int b = s0 + t; b < s1; b += kRB) {
+    if (!P.sb_active[b]) continue;
+    const double* x = P.sb[xs] + 9 * (size_t)b;
+    const double* g = P.gF + foff + P.sb_f[b];
+    for (int k = 0; k < 9; ++k) {
+      x2 += x[k] * x[k];
+      const double d = x[k] - (x[k] + (-g[k]));
+      mx = fmax(mx, fabs(d));
+      g2 += d * d;
+    }
+  }
+  const int l0 = P.win_lm_range[2 * w], l1 = P.win_lm_range[2 * w + 1];
+  for (int l = l0 + t; l < l1; l += kRB) {
+    if (!P.lm_free[l]) continue;
+    const double* x = P.lm[xs] + 4 * (size_t)l;
+    const double* g = P.lm_g + 3 * (size_t)l;
+    for (int k = 0; k < 4; ++k) x2 += x[k] * x[k];
+    for (int k = 0; k < 3; ++k) {
+      const double d = x[k] - (x[k] + (-g[k]));
+      mx = fmax(mx, fabs(d));
+      g2 += d * d;
+    }
+  }
+  mx = blockMax(mx, sh);
+  g2 = blockSum(g2, sh);
+  x2 = blockSum(x2, sh);
+  if (t != 0) return;
+  s.grad_max_norm = mx;
+  s.grad_norm = sqrt(g2);
+  s.x_norm = sqrt(x2);
+  if (lin_mode == 0 && s.iteration >= P.opt.max_num_iterations) {
+    s.done = 1;
+    s.termination = 1;
+    return;
+  }
+  if (mx <= P.opt.gradient_tolerance) {
+    s.done = 1;
+    s.termination = 0;
+    return;
+  }
+  if (lin_mode == 0 && s.radius <= P.opt.min_radius) {
+    s.done = 1;
+    s.termination = 0;
+  }
+}
+
+// One workgroup per window: GN failure handling, traditional dogleg step, Plus into X[1-xcur].
+__global__ __launch_bounds__(kRB) void k_dogleg(DevProblem P) {
+  const int w = blockIdx.x;
+  WinState& s = P.st[w];
+  if (s.done) return;
+  __shared__ double sh[kRB];
+  __shared__ int sflag;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    sflag = 0;
+    s.accepted = 0;
+    if (s.need_gn) {
+      if (s.gn_failed) {
+        // ComputeGaussNewtonStep: mu *= 10 and retry within the same iteration while mu < max_mu
+        s.gn_failed = 0;
+        s.mu *= 10.0;
+        if (s.mu < 1.0) {
+          sflag = 1;  // retry next pass, iteration not consumed
+        } else {
+          // LINEAR_SOLVER_FAILURE -> invalid step (HandleInvalidStep, StepIsInvalid)
+          s.iteration += 1;
+          s.num_unsucc += 1;
+          if (++s.consecutive_invalid >= P.opt.max_num_consecutive_invalid_steps) {
+            s.done = 1;
+            s.termination = 2;
+          } else {
+            s.mu *= 10.0;
+            s.need_gn = 1;
+            finalizeIteration(P, s);
+          }
+          sflag = 1;
+        }
+      } else {
+        s.need_gn = 0;  // reuse_ = true until the step is accepted / invalid
+      }
+    }
+    if (!sflag) s.iteration += 1;
+  }
+  __syncthreads();
+  if (sflag) return;
+  const int foff = P.win_foff[w], fd = P.win_fdim[w];
+  const int l0 = P.win_lm_range[2 * w], l1 = P.win_lm_range[2 * w + 1];
+  // pass 1: norms
+  double gg = 0.0, nn = 0.0, gn = 0.0;
+  for (int e = t; e < fd; e += kRB) {
+    const double a = P.dgF[foff + e], b = P.gnF[foff + e];
+    gg += a * a;
+    nn += b * b;
+    gn += a * b;
+  }
+  for (int l = l0 + t; l < l1; l += kRB) {
+    if (!P.lm_free[l]) continue;
+    for (int c = 0; c < 3; ++c) {
+      const double a = P.dgL[3 * (size_t)l + c], b = P.gnL[3 * (size_t)l + c];
+      gg += a * a;
+      nn += b * b;
+      gn += a * b;
+    }
+  }
+  gg = blockSum(gg, sh);
+  nn = blockSum(nn, sh);
+  gn = blockSum(gn, sh);
+  const double gradient_norm = sqrt(gg), gauss_newton_norm = sqrt(nn);
+  const double radius = s.radius, alpha = s.alpha;
+  // step = ca * gradient_ + cb * gauss_newton_step_  (then divided by diagonal_)
+  double ca, cb;
+  int dcase;
+  if (gauss_newton_norm <= radius) {
+    ca = 0.0; cb = 1.0; dcase = 1;
+  } else if (gradient_norm * alpha >= radius) {
+    ca = -(radius / gradient_norm); cb = 0.0; dcase = 2;
+  } else {
+    const double b_dot_a = -alpha * gn;
+    const double a_squared_norm = (alpha * gradient_norm) * (alpha * gradient_norm);
+    const double b_minus_a_squared_norm = a_squared_norm - 2 * b_dot_a + gauss_newton_norm * gauss_newton_norm;
+    const double c = b_dot_a - a_squared_norm;
+    const double d = sqrt(c * c + b_minus_a_squared_norm * (radius * radius - a_squared_norm));
+    const double beta = (c <= 0) ? (d - c) / b_minus_a_squared_norm : (radius * radius - a_squared_norm) / (d + c);
+    ca = -alpha * (1.0 - beta);
+    cb = beta;
+    dcase = 3;
+  }
+  // pass 2: step, delta, Plus, |x - x_cand|
+  const int xs = s.xcur, xd = 1 - s.xcur;
+  double sn2 = 0.0, dn2 = 0.0;
+  const int p0 = P.win_pose_range[2 * w], p1 = P.win_pose_range[2 * w + 1];
+  for (int p = p0 + t; p < p1; p += kRB) {
+    const int pf = P.pose_f[p];
+    if (pf < 0) continue;
+    double delta[6];
+    for (int c = 0; c < 6; ++c) {
+      const size_t i = (size_t)foff + pf + c;
+      const double v = ca * P.dgF[i] + cb * P.gnF[i];
+      dn2 += v * v;
+      const double st = v / P.diagF[i];
+      P.stepF[i] = st;
+      delta[c] = st * P.sF[i];
+    }
+    const double* x = P.pose[xs] + 7 * (size_t)p;
+    double* y = P.pose[xd] + 7 * (size_t)p;
+    const Q dq = deltaQ(delta[3], delta[4], delta[5]);
+    const Q q = qnormalize(qmul(dq, qnormalize(Q{x[3], x[4], x[5], x[6]})));
+    double yv[7] = {x[0] + delta[0], x[1] + delta[1], x[2] + delta[2], q.x, q.y, q.z, q.w};
+    for (int k = 0; k < 7; ++k) {
+      y[k] = yv[k];
+      sn2 += (x[k] - yv[k]) * (x[k] - yv[k]);
+    }
+  }
+  const int b0 = P.win_sb_range[2 * w], b1 = P.win_sb_range[2 * w + 1];
+  for (int b = b0 + t; b < b1; b += kRB) {
+    const int sf = P.sb_f[b];
+    if (sf < 0) continue;
+    const double* x = P.sb[xs] + 9 * (size_t)b;
+    double* y = P.sb[xd] + 9 * (size_t)b;
+    for (int c = 0; c < 9; ++c) {
+      const size_t i = (size_t)foff + sf + c;
+      const double v = ca * P.dgF[i] + cb * P.gnF[i];
+      dn2 += v * v;
+      const double st = v / P.diagF[i];
+      P.stepF[i] = st;
+      const double yv = x[c] + st * P.sF[i];
+      y[c] = yv;
+      sn2 += (x[c] - yv) * (x[c] - yv);
+    }
+  }
+  for (int l = l0 + t; l < l1; l += kRB) {
+    if (!P.lm_free[l]) continue;
+    const double* x = P.lm[xs] + 4 * (size_t)l;
+    double* y = P.lm[xd] + 4 * (size_t)l;
+    for (int c = 0; c < 3; ++c) {
+      const size_t i = 3 * (size_t)l + c;
+      const double v = ca * P.dgL[i] + cb * P.gnL[i];
+      dn2 += v * v;
+      const double st = v / P.diagL[i];
+      P.stepL[i] = st;
+      const double yv = x[c] + st * P.sL[i];
+      y[c] = yv;
+      sn2 += (x[c] - yv) * (x[c] - yv);
+    }
+    y[3] = x[3];
+  }
+  sn2 = blockSum(sn2, sh);
+  dn2 = blockSum(dn2, sh);
+  if (t == 0) {
+    s.dogleg_step_norm = (dcase == 1) ? gauss_newton_norm : (dcase == 2) ? radius : sqrt(dn2);
+    s.step_norm = sqrt(sn2);
+    s.step_valid = 2;  // pending the model-cost test
+  }
+}
+
+void launch_jv(const DevProblem& P, int mode, hipStream_t s) {
+  const int n = P.n_obs + P.n_imu + P.n_pprior + P.n_sbprior;
+  if (n > 0) hipLaunchKernelGGL(k_jv, dim3((n + 255) / 256), dim3(256), 0, s, P, mode);
+}
+void launch_reduce(const DevProblem& P, int mode, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce, dim3(P.n_win), dim3(kRB), 0, s, P, mode);
+}
+void launch_gradnorm(const DevProblem& P, int lin_mode, hipStream_t s) {
+  hipLaunchKernelGGL(k_gradnorm, dim3(P.n_win), dim3(kRB), 0, s, P, lin_mode);
+}
+void launch_dogleg(const DevProblem& P, hipStream_t s) {
+  hipLaunchKernelGGL(k_dogleg, dim3(P.n_win), dim3(kRB), 0, s, P);
+}
+
+}  // namespace okg

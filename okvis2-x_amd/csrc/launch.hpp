@@ -1,0 +1,30 @@
+// launch.hpp — host-side launchers of the gfx950 kernels (one stream, graph-capturable: no
+// allocation, no synchronisation, no host reads inside any launcher).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "device_problem.hpp"
+
+namespace okg {
+
+// evaluation (kernels_eval.hip); mode 0 current, 1 candidate, 2 initial
+void launch_eval(const DevProblem& P, int mode, hipStream_t s);
+
+// landmark / reduced-system kernels (kernels_schur.hip); lin_mode 0 = init, 1 = accepted only
+void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t s);
+void launch_gn_reduce(const DevProblem& P, hipStream_t s);    // lm_prep + zero S + assemble
+void launch_gn_backsub(const DevProblem& P, hipStream_t s);   // landmark back substitution + gn vectors
+
+// dense factorisation (kernels_chol.hip)
+void launch_cholesky(const DevProblem& P, int max_tiles, hipStream_t s);
+void launch_trsv(const DevProblem& P, hipStream_t s);
+
+// trust-region control (kernels_control.hip)
+enum ReduceMode { R_COST_INIT = 0, R_COST_CAND = 1, R_JV_CAUCHY = 2, R_JV_STEP = 3 };
+void launch_reduce(const DevProblem& P, int mode, hipStream_t s);
+void launch_jv(const DevProblem& P, int mode, hipStream_t s);     // mode: R_JV_CAUCHY / R_JV_STEP
+void launch_gradnorm(const DevProblem& P, int lin_mode, hipStream_t s);
+void launch_dogleg(const DevProblem& P, hipStream_t s);
+
+}  // namespace okg

@@ -1,0 +1,200 @@
+// okvisgpu_math.hpp — FP64 small-matrix / quaternion / camera helpers for the HIP kernels
+// (and the host-side synthetic generator). Register-resident, fully unrolled.
+//
+// Conventions follow the reference's Eigen usage: quaternion coefficients (x, y, z, w), Hamilton
+// product, Eigen::QuaternionBase::toRotationMatrix(). Formulas cite the okvis source they restate.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdint>
+
+#define OKG_HD __host__ __device__ __forceinline__
+
+namespace okg {
+
+struct Q {
+  double x, y, z, w;
+};
+
+OKG_HD Q qmul(const Q& a, const Q& b) {
+  return Q{a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y, a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z,
+           a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x, a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z};
+}
+OKG_HD Q qnormalize(const Q& q) {
+  const double n = sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+  return Q{q.x / n, q.y / n, q.z / n, q.w / n};
+}
+OKG_HD Q qinv(const Q& q) {  // Eigen Quaternion::inverse (conjugate / squared norm)
+  const double n2 = q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w;
+  return Q{-q.x / n2, -q.y / n2, -q.z / n2, q.w / n2};
+}
+// Eigen toRotationMatrix; R row-major [9]
+OKG_HD void qrot(const Q& q, double R[9]) {
+  const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
+  const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+  const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+  const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+  R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+  R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+  R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+}
+// okvis::kinematics::plus(q) (operators.hpp:64-76), 4x4 row-major
+OKG_HD void qplusM(const Q& q, double M[16]) {
+  M[0] = q.w;  M[1] = -q.z; M[2] = q.y;   M[3] = q.x;
+  M[4] = q.z;  M[5] = q.w;  M[6] = -q.x;  M[7] = q.y;
+  M[8] = -q.y; M[9] = q.x;  M[10] = q.w;  M[11] = q.z;
+  M[12] = -q.x; M[13] = -q.y; M[14] = -q.z; M[15] = q.w;
+}
+// okvis::kinematics::oplus(q) (operators.hpp:78-90)
+OKG_HD void qoplusM(const Q& q, double M[16]) {
+  M[0] = q.w;  M[1] = q.z;  M[2] = -q.y;  M[3] = q.x;
+  M[4] = -q.z; M[5] = q.w;  M[6] = q.x;   M[7] = q.y;
+  M[8] = q.y;  M[9] = -q.x; M[10] = q.w;  M[11] = q.z;
+  M[12] = -q.x; M[13] = -q.y; M[14] = -q.z; M[15] = q.w;
+}
+
+// kinematics::sinc / ode::sinc (Transformation.hpp:30-43, ode.hpp:34-46)
+OKG_HD double sinc(double x) {
+  if (fabs(x) > 1.0e-6) return sin(x) / x;
+  const double x_2 = x * x, x_4 = x_2 * x_2, x_6 = x_2 * x_2 * x_2;
+  return 1.0 - (1.0 / 6.0) * x_2 + (1.0 / 120.0) * x_4 - (1.0 / 5040.0) * x_6;
+}
+// kinematics::deltaQ (Transformation.hpp:45-52)
+OKG_HD Q deltaQ(double a0, double a1, double a2) {
+  const double halfnorm = 0.5 * sqrt(a0 * a0 + a1 * a1 + a2 * a2);
+  const double s = sinc(halfnorm) * 0.5;
+  return Q{s * a0, s * a1, s * a2, cos(halfnorm)};
+}
+
+// 3x3 row-major helpers
+OKG_HD void mm3(const double A[9], const double B[9], double C[9]) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) C[r * 3 + c] = A[r * 3 + 0] * B[0 * 3 + c] + A[r * 3 + 1] * B[1 * 3 + c] + A[r * 3 + 2] * B[2 * 3 + c];
+}
+OKG_HD void mv3(const double A[9], const double v[3], double o[3]) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r) o[r] = A[r * 3 + 0] * v[0] + A[r * 3 + 1] * v[1] + A[r * 3 + 2] * v[2];
+}
+OKG_HD void mtv3(const double A[9], const double v[3], double o[3]) {  // A^T v
+#pragma unroll
+  for (int r = 0; r < 3; ++r) o[r] = A[0 * 3 + r] * v[0] + A[1 * 3 + r] * v[1] + A[2 * 3 + r] * v[2];
+}
+OKG_HD void crossMx(const double v[3], double C[9]) {
+  C[0] = 0.0;   C[1] = -v[2]; C[2] = v[1];
+  C[3] = v[2];  C[4] = 0.0;   C[5] = -v[0];
+  C[6] = -v[1]; C[7] = v[0];  C[8] = 0.0;
+}
+// kinematics::rightJacobian (Transformation.hpp:55-67)
+OKG_HD void rightJacobian(const double p[3], double J[9]) {
+  const double Phi = sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
+  double X[9], X2[9];
+  crossMx(p, X);
+  mm3(X, X, X2);
+  double a, b;
+  if (Phi < 1.0e-4) {
+    a = -0.5;
+    b = 1.0 / 6.0;
+  } else {
+    const double Phi2 = Phi * Phi, Phi3 = Phi2 * Phi;
+    a = -(1.0 - cos(Phi)) / Phi2;
+    b = (Phi - sin(Phi)) / Phi3;
+  }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) J[i] = a * X[i] + b * X2[i];
+  J[0] += 1.0; J[4] += 1.0; J[8] += 1.0;
+}
+
+// okvis::Duration::toSec of a signed nanosecond difference (Duration.hpp:107-109)
+OKG_HD double durToSec(int64_t dns) {
+  int64_t sec = dns / 1000000000LL;
+  int64_t nsec = dns % 1000000000LL;
+  if (nsec < 0) { nsec += 1000000000LL; sec -= 1; }
+  return (double)sec + 1e-9 * (double)nsec;
+}
+
+// ------------------------------------------------------------------ camera (okvis_cv)
+struct Cam {
+  int dist;
+  double fu, fv, cu, cv;
+  double d0, d1, d2, d3;
+};
+
+// distortion_.distort (RadialTangentialDistortion.hpp:89-137, EquidistantDistortion.hpp:87-188)
+OKG_HD void distort(const Cam& c, double u0, double u1, double& o0, double& o1, double Jd[4], bool wantJ) {
+  if (c.dist == 1) {
+    const double k1 = c.d0, k2 = c.d1, p1 = c.d2, p2 = c.d3;
+    const double mx_u = u0 * u0, my_u = u1 * u1, mxy_u = u0 * u1;
+    const double rho_u = mx_u + my_u;
+    const double rad = k1 * rho_u + k2 * rho_u * rho_u;
+    o0 = u0 + u0 * rad + 2.0 * p1 * mxy_u + p2 * (rho_u + 2.0 * mx_u);
+    o1 = u1 + u1 * rad + 2.0 * p2 * mxy_u + p1 * (rho_u + 2.0 * my_u);
+    if (wantJ) {
+      Jd[0] = 1 + rad + k1 * 2.0 * mx_u + k2 * rho_u * 4 * mx_u + 2.0 * p1 * u1 + 6 * p2 * u0;
+      Jd[2] = k1 * 2.0 * u0 * u1 + k2 * 4 * rho_u * u0 * u1 + p1 * 2.0 * u0 + 2.0 * p2 * u1;
+      Jd[1] = Jd[2];
+      Jd[3] = 1 + rad + k1 * 2.0 * my_u + k2 * rho_u * 4 * my_u + 6 * p1 * u1 + 2.0 * p2 * u0;
+    }
+  } else if (c.dist == 2) {
+    const double k1 = c.d0, k2 = c.d1, k3 = c.d2, k4 = c.d3;
+    const double r2 = u0 * u0 + u1 * u1;
+    const double r = sqrt(r2);
+    const double th = atan(r);
+    const double th2 = th * th, th4 = th2 * th2, th6 = th4 * th2, th8 = th4 * th4;
+    const double poly = 1.0 + k1 * th2 + k2 * th4 + k3 * th6 + k4 * th8;
+    const double thd = th * poly;
+    const double s = (r > 1e-8) ? thd / r : 1.0;
+    o0 = s * u0;
+    o1 = s * u1;
+    if (wantJ) {
+      if (r > 1e-8) {
+        // d(s*u)/du = s I + u (ds/dr) u^T / r ; ds/dr = (dthd/dth * dth/dr * r - thd) / r^2
+        const double dpoly = 2.0 * k1 * th + 4.0 * k2 * th2 * th + 6.0 * k3 * th4 * th + 8.0 * k4 * th6 * th;
+        const double dthd = poly + th * dpoly;
+        const double dth_dr = 1.0 / (1.0 + r2);
+        const double ds = (dthd * dth_dr * r - thd) / r2;
+        const double f = ds / r;
+        Jd[0] = s + f * u0 * u0;
+        Jd[1] = f * u0 * u1;
+        Jd[2] = Jd[1];
+        Jd[3] = s + f * u1 * u1;
+      } else {
+        Jd[0] = 1; Jd[1] = 0; Jd[2] = 0; Jd[3] = 1;
+      }
+    }
+  } else {
+    o0 = u0;
+    o1 = u1;
+    if (wantJ) { Jd[0] = 1; Jd[1] = 0; Jd[2] = 0; Jd[3] = 1; }
+  }
+}
+
+// PinholeCamera::projectHomogeneous (PinholeCamera.hpp:497-518) -> project (:288-366).
+// J: 2x3 point Jacobian (the 4th homogeneous column is zero). kp/J = 0 when |z| < 1e-12.
+OKG_HD void projectHomogeneous(const Cam& c, double x, double y, double z, double w, double kp[2],
+                               double J[6], bool wantJ) {
+  if (w < 0) { x = -x; y = -y; z = -z; }
+  if (fabs(z) < 1.0e-12) {
+    kp[0] = kp[1] = 0.0;
+    if (wantJ) for (int i = 0; i < 6; ++i) J[i] = 0.0;
+    return;
+  }
+  const double rz = 1.0 / z;
+  const double rz2 = rz * rz;
+  double d0, d1, Jd[4];
+  distort(c, x * rz, y * rz, d0, d1, Jd, wantJ);
+  if (wantJ) {
+    J[0] = c.fu * Jd[0] * rz;
+    J[1] = c.fu * Jd[1] * rz;
+    J[2] = -c.fu * (x * Jd[0] + y * Jd[1]) * rz2;
+    J[3] = c.fv * Jd[2] * rz;
+    J[4] = c.fv * Jd[3] * rz;
+    J[5] = -c.fv * (x * Jd[2] + y * Jd[3]) * rz2;
+  }
+  kp[0] = c.fu * d0 + c.cu;
+  kp[1] = c.fv * d1 + c.cv;
+}
+
+}  // namespace okg

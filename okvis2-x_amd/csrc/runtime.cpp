@@ -1,0 +1,1033 @@
+// runtime.cpp — host runtime of the okvisgpu C ABI (include/okvisgpu.h).
+//
+// The drop-in replacement for `::ceres::Solve(options_, problem_.get(), &summary_)` in
+// okvis::ViGraph::optimise (okvis_ceres/src/ViGraph.cpp:1844-1890): structure analysis of each
+// window (residual blocks, constant flags, Schur ordering with landmarks as e-blocks, the
+// reduced-system contribution lists), one HBM arena per context, upload, and the trust-region
+// iteration as a captured hipGraph that is replayed max_num_iterations times with every decision
+// taken on the device (kernels_control.hip). The host synchronises once per solve (plus once per
+// iteration only when a CeresIterationCallback-style time limit is requested).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/okvisgpu.h"
+#include "device_problem.hpp"
+#include "launch.hpp"
+
+using namespace okg;
+
+namespace {
+
+struct HipError {
+  std::string msg;
+  int code;
+};
+
+#define HIPCHK(x)                                                                             \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess)                                                                     \
+      throw HipError{std::string(#x) + ": " + hipGetErrorString(e_),                          \
+                     e_ == hipErrorOutOfMemory ? OKVISGPU_ERR_OUT_OF_MEMORY : OKVISGPU_ERR_DEVICE}; \
+  } while (0)
+
+struct ArgError {
+  std::string msg;
+};
+
+double nowS() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Host mirror of everything uploaded (built by analyse()).
+struct HostBatch {
+  int n_win = 0;
+  std::vector<const okvisgpu_problem*> probs;
+  // bases per window
+  std::vector<int> pose_base, sb_base, lm_base, cam_base, obs_base, imu_base, pp_base, sbp_base, sample_base;
+  // parameters (initial copies)
+  std::vector<double> pose, sb, lm, extr, cam;
+  std::vector<int32_t> pose_win, sb_win, lm_win, pose_f, sb_f;
+  std::vector<uint8_t> lm_free, pose_active, sb_active;
+  // obs (sorted) + permutation to the caller's order (within the window)
+  std::vector<int32_t> obs_pose, obs_lm, obs_cam, obs_win, obs_orig;
+  std::vector<uint8_t> obs_flags;
+  std::vector<double> obs_kp, obs_L;
+  // visits
+  std::vector<int32_t> lm_visit_begin, visit_pose, visit_obs_begin, visit_lm;
+  // imu
+  std::vector<int32_t> imu_blocks, imu_win, imu_sbegin;
+  std::vector<uint8_t> imu_flags;
+  std::vector<int64_t> imu_t0, imu_t1, imu_ts;
+  std::vector<double> imu_ga, imu_par, imu_state;
+  // priors
+  std::vector<int32_t> pp_block, pp_win, sbp_block, sbp_win;
+  std::vector<double> pp_meas, pp_L, sbp_meas, sbp_L;
+  // reduced structure
+  std::vector<int32_t> win_foff, win_fdim, win_fpad;
+  std::vector<int64_t> win_soff;
+  std::vector<int32_t> win_pose_range, win_sb_range, win_lm_range, win_obs_range, win_imu_range, win_pp_range,
+      win_sbp_range;
+  std::vector<int32_t> fb_win, fb_kind, fb_index, fb_off, fb_cbegin;
+  std::vector<Contrib> fb_contrib;
+  std::vector<int32_t> pair_win, pair_fi, pair_fj, pair_cbegin;
+  std::vector<Contrib> pair_contrib;
+  int64_t s_total = 0;
+  int f_total = 0;
+  int max_fpad = 0;
+};
+
+template <class T>
+void appendN(std::vector<T>& v, const T* src, size_t n) {
+  if (n) v.insert(v.end(), src, src + n);
+}
+
+void validate(const okvisgpu_problem* p, int w) {
+  auto bad = [&](const std::string& m) { throw ArgError{"window " + std::to_string(w) + ": " + m}; };
+  if (p->n_poses < 0 || p->n_speed_biases < 0 || p->n_landmarks < 0 || p->n_observations < 0 || p->n_imu < 0 ||
+      p->n_pose_priors < 0 || p->n_sb_priors < 0 || p->n_cameras < 0)
+    bad("negative count");
+  if (p->n_poses && !p->poses) bad("poses == NULL");
+  if (p->n_speed_biases && !p->speed_biases) bad("speed_biases == NULL");
+  if (p->n_landmarks && !p->landmarks) bad("landmarks == NULL");
+  if (p->n_observations) {
+    if (!p->obs_pose || !p->obs_landmark || !p->obs_camera || !p->obs_keypoint || !p->obs_sqrt_info)
+      bad("observation arrays missing");
+    if (!p->cameras || !p->extrinsics) bad("cameras / extrinsics missing");
+    for (int o = 0; o < p->n_observations; ++o) {
+      if (p->obs_pose[o] < 0 || p->obs_pose[o] >= p->n_poses) bad("obs_pose out of range");
+      if (p->obs_landmark[o] < 0 || p->obs_landmark[o] >= p->n_landmarks) bad("obs_landmark out of range");
+      if (p->obs_camera[o] < 0 || p->obs_camera[o] >= p->n_cameras) bad("obs_camera out of range");
+    }
+  }
+  for (int c = 0; c < p->n_cameras; ++c)
+    if (p->cameras[c].distortion < 0 || p->cameras[c].distortion > 2) bad("unknown distortion model");
+  if (p->n_imu) {
+    if (!p->imu_blocks || !p->imu_t0_ns || !p->imu_t1_ns || !p->imu_sample_begin || !p->imu_sample_t_ns ||
+        !p->imu_sample_gyr_acc)
+      bad("imu arrays missing");
+    for (int f = 0; f < p->n_imu; ++f) {
+      const int* b = &p->imu_blocks[4 * f];
+      if (b[0] < 0 || b[0] >= p->n_poses || b[2] < 0 || b[2] >= p->n_poses || b[1] < 0 ||
+          b[1] >= p->n_speed_biases || b[3] < 0 || b[3] >= p->n_speed_biases)
+        bad("imu block index out of range");
+      if (p->imu_sample_begin[f + 1] < p->imu_sample_begin[f]) bad("imu_sample_begin not monotone");
+    }
+  }
+  for (int i = 0; i < p->n_pose_priors; ++i)
+    if (p->pose_prior_block[i] < 0 || p->pose_prior_block[i] >= p->n_poses) bad("pose prior block out of range");
+  for (int i = 0; i < p->n_sb_priors; ++i)
+    if (p->sb_prior_block[i] < 0 || p->sb_prior_block[i] >= p->n_speed_biases) bad("sb prior block out of range");
+}
+
+// Build the batch. `constOverride` carries okvisgpu_set_block_constant() edits.
+void analyse(const std::vector<const okvisgpu_problem*>& probs,
+             const std::map<std::tuple<int, int, int>, int>& constOverride, HostBatch& B) {
+  B = HostBatch();
+  B.n_win = (int)probs.size();
+  B.probs = probs;
+  for (int w = 0; w < B.n_win; ++w) {
+    const okvisgpu_problem* p = probs[w];
+    validate(p, w);
+    const int pb = (int)B.pose_win.size(), sbb = (int)B.sb_win.size(), lb = (int)B.lm_win.size();
+    const int cb = (int)(B.cam.size() / 9), ob = (int)B.obs_win.size(), ib = (int)B.imu_win.size();
+    const int ppb = (int)B.pp_win.size(), sbpb = (int)B.sbp_win.size();
+    B.pose_base.push_back(pb); B.sb_base.push_back(sbb); B.lm_base.push_back(lb); B.cam_base.push_back(cb);
+    B.obs_base.push_back(ob); B.imu_base.push_back(ib); B.pp_base.push_back(ppb); B.sbp_base.push_back(sbpb);
+    auto isConst = [&](int kind, int idx, const uint8_t* flags) {
+      auto it = constOverride.find(std::make_tuple(w, kind, idx));
+      if (it != constOverride.end()) return it->second != 0;
+      return flags ? flags[idx] != 0 : false;
+    };
+    std::vector<uint8_t> pc(p->n_poses), sc(p->n_speed_biases), lc(p->n_landmarks);
+    for (int i = 0; i < p->n_poses; ++i) pc[i] = isConst(0, i, p->pose_constant);
+    for (int i = 0; i < p->n_speed_biases; ++i) sc[i] = isConst(1, i, p->speed_bias_constant);
+    for (int i = 0; i < p->n_landmarks; ++i) lc[i] = isConst(2, i, p->landmark_constant);
+    // parameters
+    appendN(B.pose, p->poses, (size_t)7 * p->n_poses);
+    appendN(B.sb, p->speed_biases, (size_t)9 * p->n_speed_biases);
+    appendN(B.lm, p->landmarks, (size_t)4 * p->n_landmarks);
+    for (int c = 0; c < p->n_cameras; ++c) {
+      const okvisgpu_camera& k = p->cameras[c];
+      const double cv[9] = {(double)k.distortion, k.fu, k.fv, k.cu, k.cv, k.dist[0], k.dist[1], k.dist[2], k.dist[3]};
+      appendN(B.cam, cv, 9);
+      appendN(B.extr, &p->extrinsics[7 * c], 7);
+    }
+    for (int i = 0; i < p->n_poses; ++i) B.pose_win.push_back(w);
+    for (int i = 0; i < p->n_speed_biases; ++i) B.sb_win.push_back(w);
+    for (int i = 0; i < p->n_landmarks; ++i) B.lm_win.push_back(w);
+    // active blocks: free and used by a residual block that is not entirely constant
+    std::vector<uint8_t> pa(p->n_poses, 0), sa(p->n_speed_biases, 0), la(p->n_landmarks, 0);
+    std::vector<uint8_t> ofix(p->n_observations), ifix(p->n_imu);
+    for (int o = 0; o < p->n_observations; ++o) {
+      const int ps = p->obs_pose[o], l = p->obs_landmark[o];
+      ofix[o] = pc[ps] && lc[l];
+      if (!pc[ps]) pa[ps] = 1;
+      if (!lc[l]) la[l] = 1;
+    }
+    for (int f = 0; f < p->n_imu; ++f) {
+      const int* b = &p->imu_blocks[4 * f];
+      ifix[f] = pc[b[0]] && sc[b[1]] && pc[b[2]] && sc[b[3]];
+      if (!pc[b[0]]) pa[b[0]] = 1;
+      if (!sc[b[1]]) sa[b[1]] = 1;
+      if (!pc[b[2]]) pa[b[2]] = 1;
+      if (!sc[b[3]]) sa[b[3]] = 1;
+    }
+    for (int i = 0; i < p->n_pose_priors; ++i)
+      if (!pc[p->pose_prior_block[i]]) pa[p->pose_prior_block[i]] = 1;
+    for (int i = 0; i < p->n_sb_priors; ++i)
+      if (!sc[p->sb_prior_block[i]]) sa[p->sb_prior_block[i]] = 1;
+    // f-blocks in the reduced ordering: pose i, then speed/bias i
+    std::vector<int> posef(p->n_poses, -1), sbf(p->n_speed_biases, -1), poseFb(p->n_poses, -1),
+        sbFb(p->n_speed_biases, -1);
+    int fo = 0;
+    const int nmax = std::max(p->n_poses, p->n_speed_biases);
+    const int fbBase = (int)B.fb_win.size();
+    for (int i = 0; i < nmax; ++i) {
+      if (i < p->n_poses && pa[i]) {
+        posef[i] = fo;
+        poseFb[i] = (int)B.fb_win.size();
+        B.fb_win.push_back(w); B.fb_kind.push_back(0); B.fb_index.push_back(pb + i); B.fb_off.push_back(fo);
+        fo += 6;
+      }
+      if (i < p->n_speed_biases && sa[i]) {
+        sbf[i] = fo;
+        sbFb[i] = (int)B.fb_win.size();
+        B.fb_win.push_back(w); B.fb_kind.push_back(1); B.fb_index.push_back(sbb + i); B.fb_off.push_back(fo);
+        fo += 9;
+      }
+    }
+    for (int i = 0; i < p->n_poses; ++i) { B.pose_f.push_back(posef[i]); B.pose_active.push_back(pa[i]); }
+    for (int i = 0; i < p->n_speed_biases; ++i) { B.sb_f.push_back(sbf[i]); B.sb_active.push_back(sa[i]); }
+    for (int i = 0; i < p->n_landmarks; ++i) B.lm_free.push_back(la[i]);
+    const int fpad = ((fo + kTile - 1) / kTile) * kTile;
+    B.win_foff.push_back(B.f_total);
+    B.win_fdim.push_back(fo);
+    B.win_fpad.push_back(fpad);
+    B.win_soff.push_back(B.s_total);
+    B.f_total += fo;
+    B.s_total += (int64_t)fpad * fpad;
+    B.max_fpad = std::max(B.max_fpad, fpad);
+
+    // observations sorted by (landmark, pose, camera, original index)
+    std::vector<int> order(p->n_observations);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+      if (p->obs_landmark[a] != p->obs_landmark[b]) return p->obs_landmark[a] < p->obs_landmark[b];
+      if (p->obs_pose[a] != p->obs_pose[b]) return p->obs_pose[a] < p->obs_pose[b];
+      return p->obs_camera[a] < p->obs_camera[b];
+    });
+    // visits and landmark -> visit ranges
+    const int vBase = (int)B.visit_pose.size();
+    std::vector<int> lmVisitBegin(p->n_landmarks + 1, 0);
+    std::vector<std::vector<int>> visitsAtPose(p->n_poses);
+    {
+      int prevL = -1, prevP = -1;
+      std::vector<int> vcount(p->n_landmarks, 0);
+      for (int k = 0; k < p->n_observations; ++k) {
+        const int o = order[k];
+        const int l = p->obs_landmark[o], ps = p->obs_pose[o];
+        B.obs_pose.push_back(pb + ps);
+        B.obs_lm.push_back(lb + l);
+        B.obs_cam.push_back(cb + p->obs_camera[o]);
+        B.obs_win.push_back(w);
+        B.obs_orig.push_back(o);
+        uint8_t fl = 0;
+        if (p->obs_cauchy ? p->obs_cauchy[o] != 0 : true) fl |= 1;
+        if (ofix[o]) fl |= 2;
+        B.obs_flags.push_back(fl);
+        appendN(B.obs_kp, &p->obs_keypoint[2 * o], 2);
+        appendN(B.obs_L, &p->obs_sqrt_info[4 * o], 4);
+        if (l != prevL || ps != prevP) {
+          B.visit_pose.push_back(pb + ps);
+          B.visit_lm.push_back(lb + l);
+          B.visit_obs_begin.push_back(ob + k);
+          visitsAtPose[ps].push_back((int)B.visit_pose.size() - 1);
+          vcount[l]++;
+          prevL = l;
+          prevP = ps;
+        }
+      }
+      int acc = vBase;
+      for (int l = 0; l < p->n_landmarks; ++l) {
+        lmVisitBegin[l] = acc;
+        acc += vcount[l];
+      }
+      lmVisitBegin[p->n_landmarks] = acc;
+      for (int l = 0; l < p->n_landmarks; ++l) B.lm_visit_begin.push_back(lmVisitBegin[l]);
+    }
+    // imu
+    const int sBase = (int)B.imu_ts.size();
+    for (int f = 0; f < p->n_imu; ++f) {
+      const int* b = &p->imu_blocks[4 * f];
+      const int32_t gb[4] = {pb + b[0], sbb + b[1], pb + b[2], sbb + b[3]};
+      appendN(B.imu_blocks, gb, 4);
+      B.imu_win.push_back(w);
+      B.imu_flags.push_back(ifix[f] ? 2 : 0);
+      B.imu_t0.push_back(p->imu_t0_ns[f]);
+      B.imu_t1.push_back(p->imu_t1_ns[f]);
+      B.imu_sbegin.push_back(sBase + p->imu_sample_begin[f] - p->imu_sample_begin[0]);
+    }
+    if (p->n_imu) {
+      const int s0 = p->imu_sample_begin[0], s1 = p->imu_sample_begin[p->n_imu];
+      appendN(B.imu_ts, &p->imu_sample_t_ns[s0], (size_t)(s1 - s0));
+      appendN(B.imu_ga, &p->imu_sample_gyr_acc[6 * (size_t)s0], (size_t)6 * (s1 - s0));
+    }
+    {
+      const okvisgpu_imu_params& ip = p->imu_params;
+      const double par[7] = {ip.a_max, ip.g_max, ip.sigma_g_c, ip.sigma_a_c, ip.sigma_gw_c, ip.sigma_aw_c, ip.g};
+      appendN(B.imu_par, par, 7);
+    }
+    for (int f = 0; f < p->n_imu; ++f) {
+      if (p->imu_state) appendN(B.imu_state, &p->imu_state[(size_t)f * OKVISGPU_IMU_STATE_DOUBLES], OKVISGPU_IMU_STATE_DOUBLES);
+      else B.imu_state.insert(B.imu_state.end(), OKVISGPU_IMU_STATE_DOUBLES, 0.0);
+    }
+    // priors
+    for (int i = 0; i < p->n_pose_priors; ++i) {
+      B.pp_block.push_back(pb + p->pose_prior_block[i]);
+      B.pp_win.push_back(w);
+      appendN(B.pp_meas, &p->pose_prior_meas[7 * i], 7);
+      appendN(B.pp_L, &p->pose_prior_sqrt_info[36 * i], 36);
+    }
+    for (int i = 0; i < p->n_sb_priors; ++i) {
+      B.sbp_block.push_back(sbb + p->sb_prior_block[i]);
+      B.sbp_win.push_back(w);
+      appendN(B.sbp_meas, &p->sb_prior_meas[9 * i], 9);
+      appendN(B.sbp_L, &p->sb_prior_sqrt_info[81 * i], 81);
+    }
+    // ranges
+    const int r_pose[2] = {pb, pb + p->n_poses}, r_sb[2] = {sbb, sbb + p->n_speed_biases},
+              r_lm[2] = {lb, lb + p->n_landmarks}, r_obs[2] = {ob, ob + p->n_observations},
+              r_imu[2] = {ib, ib + p->n_imu}, r_pp[2] = {ppb, ppb + p->n_pose_priors},
+              r_sbp[2] = {sbpb, sbpb + p->n_sb_priors};
+    appendN(B.win_pose_range, r_pose, 2); appendN(B.win_sb_range, r_sb, 2); appendN(B.win_lm_range, r_lm, 2);
+    appendN(B.win_obs_range, r_obs, 2); appendN(B.win_imu_range, r_imu, 2); appendN(B.win_pp_range, r_pp, 2);
+    appendN(B.win_sbp_range, r_sbp, 2);
+
+    // ---- f-block gradient / diagonal contribution lists
+    const int nFb = (int)B.fb_win.size() - fbBase;
+    std::vector<std::vector<Contrib>> fbc(nFb);
+    for (int i = 0; i < p->n_poses; ++i) {
+      if (poseFb[i] < 0) continue;
+      for (int v : visitsAtPose[i]) fbc[poseFb[i] - fbBase].push_back(Contrib{C_VISIT, v, la[B.visit_lm[v] - lb], 0});
+    }
+    const int imuCol[4] = {0, 6, 15, 21};
+    for (int f = 0; f < p->n_imu; ++f) {
+      if (ifix[f]) continue;
+      const int* b = &p->imu_blocks[4 * f];
+      const int fbs[4] = {poseFb[b[0]], sbFb[b[1]], poseFb[b[2]], sbFb[b[3]]};
+      for (int q = 0; q < 4; ++q)
+        if (fbs[q] >= 0) fbc[fbs[q] - fbBase].push_back(Contrib{C_IMU, ib + f, imuCol[q], imuCol[q]});
+    }
+    for (int i = 0; i < p->n_pose_priors; ++i) {
+      const int fb = poseFb[p->pose_prior_block[i]];
+      if (fb >= 0) fbc[fb - fbBase].push_back(Contrib{C_PPRIOR, ppb + i, 0, 0});
+    }
+    for (int i = 0; i < p->n_sb_priors; ++i) {
+      const int fb = sbFb[p->sb_prior_block[i]];
+      if (fb >= 0) fbc[fb - fbBase].push_back(Contrib{C_SBPRIOR, sbpb + i, 0, 0});
+    }
+    for (int k = 0; k < nFb; ++k) {
+      B.fb_cbegin.push_back((int)B.fb_contrib.size());
+      B.fb_contrib.insert(B.fb_contrib.end(), fbc[k].begin(), fbc[k].end());
+    }
+    // ---- block pairs (fi >= fj by reduced offset) and their contribution lists
+    std::map<std::pair<int, int>, std::vector<Contrib>> pairs;
+    auto key = [&](int fa, int fb2) {  // row = larger offset
+      return B.fb_off[fa] >= B.fb_off[fb2] ? std::make_pair(fa, fb2) : std::make_pair(fb2, fa);
+    };
+    for (int i = 0; i < p->n_poses; ++i) {
+      if (poseFb[i] < 0) continue;
+      auto& lst = pairs[std::make_pair(poseFb[i], poseFb[i])];
+      for (int v : visitsAtPose[i]) {
+        const int l = B.visit_lm[v] - lb;
+        lst.push_back(Contrib{C_VISIT, v, la[l], 0});
+      }
+    }
+    for (int l = 0; l < p->n_landmarks; ++l) {
+      if (!la[l]) continue;
+      const int v0 = lmVisitBegin[l], v1 = lmVisitBegin[l + 1];
+      for (int va = v0; va < v1; ++va) {
+        const int fa = poseFb[B.visit_pose[va] - pb];
+        if (fa < 0) continue;
+        for (int vb = v0; vb < v1; ++vb) {
+          const int fb2 = poseFb[B.visit_pose[vb] - pb];
+          if (fb2 < 0) continue;
+          if (B.fb_off[fa] < B.fb_off[fb2]) continue;  // each unordered pair once, row >= col
+          pairs[std::make_pair(fa, fb2)].push_back(Contrib{C_PAIR, va, vb, 0});
+        }
+      }
+    }
+    for (int f = 0; f < p->n_imu; ++f) {
+      if (ifix[f]) continue;
+      const int* b = &p->imu_blocks[4 * f];
+      const int fbs[4] = {poseFb[b[0]], sbFb[b[1]], poseFb[b[2]], sbFb[b[3]]};
+      for (int u = 0; u < 4; ++u)
+        for (int v = 0; v < 4; ++v) {
+          if (fbs[u] < 0 || fbs[v] < 0) continue;
+          if (B.fb_off[fbs[u]] < B.fb_off[fbs[v]]) continue;
+          pairs[key(fbs[u], fbs[v])].push_back(Contrib{C_IMU, ib + f, imuCol[u], imuCol[v]});
+        }
+    }
+    for (int i = 0; i < p->n_pose_priors; ++i) {
+      const int fb = poseFb[p->pose_prior_block[i]];
+      if (fb >= 0) pairs[std::make_pair(fb, fb)].push_back(Contrib{C_PPRIOR, ppb + i, 0, 0});
+    }
+    for (int i = 0; i < p->n_sb_priors; ++i) {
+      const int fb = sbFb[p->sb_prior_block[i]];
+      if (fb >= 0) pairs[std::make_pair(fb, fb)].push_back(Contrib{C_SBPRIOR, sbpb + i, 0, 0});
+    }
+    // diagonal pairs must exist for every f-block (they carry the damping, diag and rhs)
+    for (int k = fbBase; k < (int)B.fb_win.size(); ++k) pairs[std::make_pair(k, k)];
+    for (auto& kv : pairs) {
+      B.pair_win.push_back(w);
+      B.pair_fi.push_back(kv.first.first);
+      B.pair_fj.push_back(kv.first.second);
+      B.pair_cbegin.push_back((int)B.pair_contrib.size());
+      B.pair_contrib.insert(B.pair_contrib.end(), kv.second.begin(), kv.second.end());
+    }
+  }
+  B.lm_visit_begin.push_back((int)B.visit_pose.size());
+  B.visit_obs_begin.push_back((int)B.obs_win.size());
+  B.imu_sbegin.push_back((int)B.imu_ts.size());
+  B.fb_cbegin.push_back((int)B.fb_contrib.size());
+  B.pair_cbegin.push_back((int)B.pair_contrib.size());
+}
+
+// A single hipMalloc arena carved into the device arrays.
+struct Arena {
+  char* base = nullptr;
+  size_t size = 0, used = 0;
+  std::vector<std::pair<size_t, size_t>> plan;
+  size_t reserve(size_t bytes) {
+    const size_t off = (size + 255) & ~size_t(255);
+    size = off + std::max<size_t>(bytes, 8);
+    return off;
+  }
+  template <class T>
+  T* at(size_t off) const { return reinterpret_cast<T*>(base + off); }
+};
+
+}  // namespace
+
+struct okvisgpu_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string last_error;
+  HostBatch B;
+  std::vector<const okvisgpu_problem*> probs;
+  std::map<std::tuple<int, int, int>, int> constOverride;
+  bool structureDirty = false;
+  DevProblem P{};
+  void* arena = nullptr;
+  size_t arenaBytes = 0;
+  hipGraphExec_t iterGraph = nullptr;
+  bool haveProblem = false;
+
+  ~okvisgpu_ctx() {
+    if (iterGraph) (void)hipGraphExecDestroy(iterGraph);
+    if (arena) (void)hipFree(arena);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  void dropGraph() {
+    if (iterGraph) {
+      (void)hipGraphExecDestroy(iterGraph);
+      iterGraph = nullptr;
+    }
+  }
+
+  void build() {
+    analyse(probs, constOverride, B);
+    dropGraph();
+    if (arena) {
+      HIPCHK(hipFree(arena));
+      arena = nullptr;
+    }
+    Arena A;
+    DevProblem& D = P;
+    D = DevProblem{};
+    D.n_win = B.n_win;
+    D.n_pose = (int)B.pose_win.size();
+    D.n_sb = (int)B.sb_win.size();
+    D.n_lm = (int)B.lm_win.size();
+    D.n_obs = (int)B.obs_win.size();
+    D.n_visit = (int)B.visit_pose.size();
+    D.n_imu = (int)B.imu_win.size();
+    D.n_pprior = (int)B.pp_win.size();
+    D.n_sbprior = (int)B.sbp_win.size();
+    D.n_cam = (int)(B.cam.size() / 9);
+    D.n_fblock = (int)B.fb_win.size();
+    D.n_pair = (int)B.pair_win.size();
+    D.max_fpad = B.max_fpad;
+    D.max_tiles = B.max_fpad / kTile;
+    D.obs_stride = ((int64_t)D.n_obs + 63) / 64 * 64;
+    // ---- plan
+    struct Up { size_t off; const void* src; size_t bytes; };
+    std::vector<Up> ups;
+    auto upl = [&](const auto& vec) -> size_t {
+      using T = typename std::decay_t<decltype(vec)>::value_type;
+      const size_t bytes = vec.size() * sizeof(T);
+      const size_t off = A.reserve(bytes);
+      ups.push_back(Up{off, vec.data(), bytes});
+      return off;
+    };
+    auto scratch = [&](size_t bytes) { return A.reserve(bytes); };
+    const size_t o_pose0 = upl(B.pose), o_pose1 = upl(B.pose), o_sb0 = upl(B.sb), o_sb1 = upl(B.sb);
+    const size_t o_lm0 = upl(B.lm), o_lm1 = upl(B.lm), o_extr = upl(B.extr), o_cam = upl(B.cam);
+    const size_t o_pose_win = upl(B.pose_win), o_sb_win = upl(B.sb_win), o_lm_win = upl(B.lm_win);
+    const size_t o_pose_f = upl(B.pose_f), o_sb_f = upl(B.sb_f), o_lm_free = upl(B.lm_free);
+    const size_t o_pose_act = upl(B.pose_active), o_sb_act = upl(B.sb_active);
+    const size_t o_obs_pose = upl(B.obs_pose), o_obs_lm = upl(B.obs_lm), o_obs_cam = upl(B.obs_cam),
+                 o_obs_win = upl(B.obs_win), o_obs_flags = upl(B.obs_flags), o_obs_kp = upl(B.obs_kp),
+                 o_obs_L = upl(B.obs_L);
+    const size_t o_obs_lin0 = scratch(sizeof(double) * kObsLin * D.obs_stride);
+    const size_t o_obs_lin1 = scratch(sizeof(double) * kObsLin * D.obs_stride);
+    const size_t o_obs_cost0 = scratch(sizeof(double) * D.n_obs), o_obs_cost1 = scratch(sizeof(double) * D.n_obs);
+    const size_t o_obs_jv = scratch(sizeof(double) * 2 * D.n_obs);
+    const size_t o_lmvb = upl(B.lm_visit_begin), o_vpose = upl(B.visit_pose), o_vob = upl(B.visit_obs_begin),
+                 o_vlm = upl(B.visit_lm);
+    const size_t o_lmV = scratch(sizeof(double) * 6 * D.n_lm), o_lmg = scratch(sizeof(double) * 3 * D.n_lm),
+                 o_lmVi = scratch(sizeof(double) * 9 * D.n_lm), o_lmz = scratch(sizeof(double) * 3 * D.n_lm);
+    const size_t o_vW = scratch(sizeof(double) * 18 * D.n_visit), o_vH = scratch(sizeof(double) * 21 * D.n_visit),
+                 o_vg = scratch(sizeof(double) * 6 * D.n_visit);
+    const size_t o_imu_blocks = upl(B.imu_blocks), o_imu_win = upl(B.imu_win), o_imu_flags = upl(B.imu_flags),
+                 o_imu_t0 = upl(B.imu_t0), o_imu_t1 = upl(B.imu_t1), o_imu_sb = upl(B.imu_sbegin),
+                 o_imu_ts = upl(B.imu_ts), o_imu_ga = upl(B.imu_ga), o_imu_par = upl(B.imu_par),
+                 o_imu_state = upl(B.imu_state);
+    const size_t o_imu_lin0 = scratch(sizeof(double) * kImuLin * D.n_imu),
+                 o_imu_lin1 = scratch(sizeof(double) * kImuLin * D.n_imu);
+    const size_t o_imu_cost0 = scratch(sizeof(double) * D.n_imu), o_imu_cost1 = scratch(sizeof(double) * D.n_imu),
+                 o_imu_jv = scratch(sizeof(double) * 2 * D.n_imu);
+    const size_t o_pp_block = upl(B.pp_block), o_pp_win = upl(B.pp_win), o_pp_meas = upl(B.pp_meas),
+                 o_pp_L = upl(B.pp_L);
+    const size_t o_pp_lin0 = scratch(sizeof(double) * 42 * D.n_pprior), o_pp_lin1 = scratch(sizeof(double) * 42 * D.n_pprior),
+                 o_pp_cost0 = scratch(sizeof(double) * D.n_pprior), o_pp_cost1 = scratch(sizeof(double) * D.n_pprior),
+                 o_pp_jv = scratch(sizeof(double) * 2 * D.n_pprior);
+    const size_t o_sbp_block = upl(B.sbp_block), o_sbp_win = upl(B.sbp_win), o_sbp_meas = upl(B.sbp_meas),
+                 o_sbp_L = upl(B.sbp_L);
+    const size_t o_sbp_lin0 = scratch(sizeof(double) * 90 * D.n_sbprior),
+                 o_sbp_lin1 = scratch(sizeof(double) * 90 * D.n_sbprior),
+                 o_sbp_cost0 = scratch(sizeof(double) * D.n_sbprior), o_sbp_cost1 = scratch(sizeof(double) * D.n_sbprior),
+                 o_sbp_jv = scratch(sizeof(double) * 2 * D.n_sbprior);
+    const size_t o_wfoff = upl(B.win_foff), o_wfdim = upl(B.win_fdim), o_wfpad = upl(B.win_fpad),
+                 o_wsoff = upl(B.win_soff), o_wpr = upl(B.win_pose_range), o_wsr = upl(B.win_sb_range),
+                 o_wlr = upl(B.win_lm_range), o_wor = upl(B.win_obs_range), o_wir = upl(B.win_imu_range),
+                 o_wppr = upl(B.win_pp_range), o_wsbpr = upl(B.win_sbp_range);
+    const size_t o_fbw = upl(B.fb_win), o_fbk = upl(B.fb_kind), o_fbi = upl(B.fb_index), o_fbo = upl(B.fb_off),
+                 o_fbcb = upl(B.fb_cbegin), o_fbc = upl(B.fb_contrib);
+    const size_t o_pw = upl(B.pair_win), o_pfi = upl(B.pair_fi), o_pfj = upl(B.pair_fj), o_pcb = upl(B.pair_cbegin),
+                 o_pc = upl(B.pair_contrib);
+    const size_t nf = std::max(1, B.f_total), nl3 = std::max<size_t>(1, (size_t)3 * D.n_lm);
+    const size_t o_S = scratch(sizeof(double) * std::max<int64_t>(1, B.s_total));
+    size_t of[10], ol[7];
+    for (int i = 0; i < 10; ++i) of[i] = scratch(sizeof(double) * nf);
+    for (int i = 0; i < 7; ++i) ol[i] = scratch(sizeof(double) * nl3);
+    const size_t o_st = scratch(sizeof(WinState) * D.n_win);
+    // ---- allocate + upload
+    HIPCHK(hipMalloc(&arena, A.size));
+    arenaBytes = A.size;
+    char* base = static_cast<char*>(arena);
+    HIPCHK(hipMemsetAsync(arena, 0, A.size, stream));
+    for (const Up& u : ups)
+      if (u.bytes) HIPCHK(hipMemcpyAsync(base + u.off, u.src, u.bytes, hipMemcpyHostToDevice, stream));
+    auto dp = [&](size_t off) { return reinterpret_cast<double*>(base + off); };
+    auto ip = [&](size_t off) { return reinterpret_cast<int32_t*>(base + off); };
+    auto lp = [&](size_t off) { return reinterpret_cast<int64_t*>(base + off); };
+    auto up = [&](size_t off) { return reinterpret_cast<uint8_t*>(base + off); };
+    D.pose[0] = dp(o_pose0); D.pose[1] = dp(o_pose1); D.sb[0] = dp(o_sb0); D.sb[1] = dp(o_sb1);
+    D.lm[0] = dp(o_lm0); D.lm[1] = dp(o_lm1); D.extr = dp(o_extr); D.cam = dp(o_cam);
+    D.pose_win = ip(o_pose_win); D.sb_win = ip(o_sb_win); D.lm_win = ip(o_lm_win);
+    D.pose_f = ip(o_pose_f); D.sb_f = ip(o_sb_f); D.lm_free = up(o_lm_free);
+    D.pose_active = up(o_pose_act); D.sb_active = up(o_sb_act);
+    D.obs_pose = ip(o_obs_pose); D.obs_lm = ip(o_obs_lm); D.obs_cam = ip(o_obs_cam); D.obs_win = ip(o_obs_win);
+    D.obs_flags = up(o_obs_flags); D.obs_kp = dp(o_obs_kp); D.obs_L = dp(o_obs_L);
+    D.obs_lin[0] = dp(o_obs_lin0); D.obs_lin[1] = dp(o_obs_lin1);
+    D.obs_cost[0] = dp(o_obs_cost0); D.obs_cost[1] = dp(o_obs_cost1); D.obs_jv = dp(o_obs_jv);
+    D.lm_visit_begin = ip(o_lmvb); D.visit_pose = ip(o_vpose); D.visit_obs_begin = ip(o_vob); D.visit_lm = ip(o_vlm);
+    D.lm_V = dp(o_lmV); D.lm_g = dp(o_lmg); D.lm_Vinv = dp(o_lmVi); D.lm_z = dp(o_lmz);
+    D.visit_W = dp(o_vW); D.visit_H = dp(o_vH); D.visit_g = dp(o_vg);
+    D.imu_blocks = ip(o_imu_blocks); D.imu_win = ip(o_imu_win); D.imu_flags = up(o_imu_flags);
+    D.imu_t0 = lp(o_imu_t0); D.imu_t1 = lp(o_imu_t1); D.imu_sbegin = ip(o_imu_sb); D.imu_ts = lp(o_imu_ts);
+    D.imu_ga = dp(o_imu_ga); D.imu_par = dp(o_imu_par); D.imu_state = dp(o_imu_state);
+    D.imu_lin[0] = dp(o_imu_lin0); D.imu_lin[1] = dp(o_imu_lin1);
+    D.imu_cost[0] = dp(o_imu_cost0); D.imu_cost[1] = dp(o_imu_cost1); D.imu_jv = dp(o_imu_jv);
+    D.pp_block = ip(o_pp_block); D.pp_win = ip(o_pp_win); D.pp_meas = dp(o_pp_meas); D.pp_L = dp(o_pp_L);
+    D.pp_lin[0] = dp(o_pp_lin0); D.pp_lin[1] = dp(o_pp_lin1); D.pp_cost[0] = dp(o_pp_cost0);
+    D.pp_cost[1] = dp(o_pp_cost1); D.pp_jv = dp(o_pp_jv);
+    D.sbp_block = ip(o_sbp_block); D.sbp_win = ip(o_sbp_win); D.sbp_meas = dp(o_sbp_meas); D.sbp_L = dp(o_sbp_L);
+    D.sbp_lin[0] = dp(o_sbp_lin0); D.sbp_lin[1] = dp(o_sbp_lin1); D.sbp_cost[0] = dp(o_sbp_cost0);
+    D.sbp_cost[1] = dp(o_sbp_cost1); D.sbp_jv = dp(o_sbp_jv);
+    D.win_foff = ip(o_wfoff); D.win_fdim = ip(o_wfdim); D.win_fpad = ip(o_wfpad); D.win_soff = lp(o_wsoff);
+    D.win_pose_range = ip(o_wpr); D.win_sb_range = ip(o_wsr); D.win_lm_range = ip(o_wlr);
+    D.win_obs_range = ip(o_wor); D.win_imu_range = ip(o_wir); D.win_pp_range = ip(o_wppr);
+    D.win_sbp_range = ip(o_wsbpr);
+    D.fb_win = ip(o_fbw); D.fb_kind = ip(o_fbk); D.fb_index = ip(o_fbi); D.fb_off = ip(o_fbo);
+    D.fb_cbegin = ip(o_fbcb); D.fb_contrib = reinterpret_cast<const Contrib*>(base + o_fbc);
+    D.pair_win = ip(o_pw); D.pair_fi = ip(o_pfi); D.pair_fj = ip(o_pfj); D.pair_cbegin = ip(o_pcb);
+    D.pair_contrib = reinterpret_cast<const Contrib*>(base + o_pc);
+    D.S = dp(o_S);
+    double** fv[10] = {&D.sF, &D.diagF, &D.hdF, &D.gF, &D.rhsF, &D.yF, &D.gnF, &D.dgF, &D.vF, &D.stepF};
+    for (int i = 0; i < 10; ++i) *fv[i] = dp(of[i]);
+    double** lv[7] = {&D.sL, &D.diagL, &D.stepL, &D.yL, &D.gnL, &D.dgL, &D.vL};
+    for (int i = 0; i < 7; ++i) *lv[i] = dp(ol[i]);
+    D.gL = D.lm_g;  // the landmark gradient is the accumulated J_l^T r
+    D.st = reinterpret_cast<WinState*>(base + o_st);
+    HIPCHK(hipStreamSynchronize(stream));
+    haveProblem = true;
+    structureDirty = false;
+  }
+
+  void setOptions(const okvisgpu_options& o) {
+    DevOptions& d = P.opt;
+    d.max_num_iterations = o.max_num_iterations;
+    d.jacobi_scaling = o.jacobi_scaling;
+    d.max_num_consecutive_invalid_steps = o.max_num_consecutive_invalid_steps;
+    d.redo_propagation_always = o.redo_propagation_always;
+    d.function_tolerance = o.function_tolerance;
+    d.gradient_tolerance = o.gradient_tolerance;
+    d.parameter_tolerance = o.parameter_tolerance;
+    d.initial_radius = o.initial_trust_region_radius;
+    d.max_radius = o.max_trust_region_radius;
+    d.min_radius = o.min_trust_region_radius;
+    d.min_relative_decrease = o.min_relative_decrease;
+    d.min_lm_diagonal = o.min_lm_diagonal;
+    d.max_lm_diagonal = o.max_lm_diagonal;
+  }
+
+  void resetStates(double mu) {
+    std::vector<WinState> s(P.n_win);
+    for (auto& x : s) {
+      std::memset(&x, 0, sizeof(x));
+      x.radius = P.opt.initial_radius;
+      x.mu = mu;
+      x.need_gn = 1;
+      x.termination = OKVISGPU_NO_CONVERGENCE;
+    }
+    HIPCHK(hipMemcpyAsync(P.st, s.data(), sizeof(WinState) * s.size(), hipMemcpyHostToDevice, stream));
+  }
+
+  // Upload current host parameter values into both parameter sets (+ IMU state).
+  void uploadParams() {
+    std::vector<double> pose, sb, lm, imu;
+    for (int w = 0; w < B.n_win; ++w) {
+      const okvisgpu_problem* p = probs[w];
+      appendN(pose, p->poses, (size_t)7 * p->n_poses);
+      appendN(sb, p->speed_biases, (size_t)9 * p->n_speed_biases);
+      appendN(lm, p->landmarks, (size_t)4 * p->n_landmarks);
+      for (int f = 0; f < p->n_imu; ++f) {
+        if (p->imu_state) appendN(imu, &p->imu_state[(size_t)f * OKVISGPU_IMU_STATE_DOUBLES], OKVISGPU_IMU_STATE_DOUBLES);
+        else imu.insert(imu.end(), OKVISGPU_IMU_STATE_DOUBLES, 0.0);
+      }
+    }
+    for (int k = 0; k < 2; ++k) {
+      if (!pose.empty()) HIPCHK(hipMemcpyAsync(P.pose[k], pose.data(), pose.size() * 8, hipMemcpyHostToDevice, stream));
+      if (!sb.empty()) HIPCHK(hipMemcpyAsync(P.sb[k], sb.data(), sb.size() * 8, hipMemcpyHostToDevice, stream));
+      if (!lm.empty()) HIPCHK(hipMemcpyAsync(P.lm[k], lm.data(), lm.size() * 8, hipMemcpyHostToDevice, stream));
+    }
+    if (!imu.empty()) HIPCHK(hipMemcpyAsync(P.imu_state, imu.data(), imu.size() * 8, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+  }
+
+  // Write device results back into the caller's arrays (parameter set xcur of each window).
+  void downloadParams(const std::vector<WinState>& st) {
+    const size_t np = 7 * (size_t)P.n_pose, ns = 9 * (size_t)P.n_sb, nl = 4 * (size_t)P.n_lm;
+    std::vector<double> pose[2], sb[2], lm[2], imu((size_t)P.n_imu * kImuState);
+    for (int k = 0; k < 2; ++k) {
+      pose[k].resize(np); sb[k].resize(ns); lm[k].resize(nl);
+      if (np) HIPCHK(hipMemcpyAsync(pose[k].data(), P.pose[k], np * 8, hipMemcpyDeviceToHost, stream));
+      if (ns) HIPCHK(hipMemcpyAsync(sb[k].data(), P.sb[k], ns * 8, hipMemcpyDeviceToHost, stream));
+      if (nl) HIPCHK(hipMemcpyAsync(lm[k].data(), P.lm[k], nl * 8, hipMemcpyDeviceToHost, stream));
+    }
+    if (!imu.empty()) HIPCHK(hipMemcpyAsync(imu.data(), P.imu_state, imu.size() * 8, hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    for (int w = 0; w < B.n_win; ++w) {
+      const okvisgpu_problem* p = probs[w];
+      const int x = st.empty() ? 0 : st[w].xcur;
+      std::memcpy(p->poses, &pose[x][7 * (size_t)B.pose_base[w]], sizeof(double) * 7 * p->n_poses);
+      std::memcpy(p->speed_biases, &sb[x][9 * (size_t)B.sb_base[w]], sizeof(double) * 9 * p->n_speed_biases);
+      std::memcpy(p->landmarks, &lm[x][4 * (size_t)B.lm_base[w]], sizeof(double) * 4 * p->n_landmarks);
+      if (p->imu_state && p->n_imu)
+        std::memcpy(p->imu_state, &imu[(size_t)B.imu_base[w] * kImuState],
+                    sizeof(double) * kImuState * p->n_imu);
+    }
+  }
+
+  std::vector<WinState> readStates() {
+    std::vector<WinState> s(P.n_win);
+    HIPCHK(hipMemcpyAsync(s.data(), P.st, sizeof(WinState) * s.size(), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipStreamSynchronize(stream));
+    return s;
+  }
+
+  void launchInit(int evalMode) {
+    launch_eval(P, evalMode, stream);
+    launch_reduce(P, R_COST_INIT, stream);
+    launch_linearization_blocks(P, 0, stream);
+    launch_gradnorm(P, 0, stream);
+    HIPCHK(hipGetLastError());
+  }
+
+  void launchIteration() {
+    launch_gn_reduce(P, stream);
+    launch_cholesky(P, P.max_tiles, stream);
+    launch_trsv(P, stream);
+    launch_gn_backsub(P, stream);
+    launch_jv(P, R_JV_CAUCHY, stream);
+    launch_reduce(P, R_JV_CAUCHY, stream);
+    launch_dogleg(P, stream);
+    launch_jv(P, R_JV_STEP, stream);
+    launch_reduce(P, R_JV_STEP, stream);
+    launch_eval(P, 1, stream);
+    launch_reduce(P, R_COST_CAND, stream);
+    launch_linearization_blocks(P, 1, stream);
+    launch_gradnorm(P, 1, stream);
+  }
+
+  void ensureGraph() {
+    if (iterGraph) return;
+    hipGraph_t g;
+    HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+    launchIteration();
+    HIPCHK(hipStreamEndCapture(stream, &g));
+    HIPCHK(hipGraphInstantiate(&iterGraph, g, nullptr, nullptr, 0));
+    HIPCHK(hipGraphDestroy(g));
+  }
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(okvisgpu_ctx* c, int code, const std::string& m) {
+  if (c) c->last_error = m;
+  g_err = m;
+  return code;
+}
+
+template <class F>
+int guarded(okvisgpu_ctx* c, F f) {
+  try {
+    return f();
+  } catch (const HipError& e) {
+    return fail(c, e.code, e.msg);
+  } catch (const ArgError& e) {
+    return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, e.msg);
+  } catch (const std::bad_alloc&) {
+    return fail(c, OKVISGPU_ERR_OUT_OF_MEMORY, "host allocation failed");
+  } catch (const std::exception& e) {
+    return fail(c, OKVISGPU_ERR_DEVICE, e.what());
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int okvisgpu_abi_version(void) { return OKVISGPU_ABI_VERSION; }
+
+void okvisgpu_default_options(okvisgpu_options* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->max_num_iterations = 50;  // ::ceres::Solver::Options default
+  o->linear_solver = OKVISGPU_DENSE_SCHUR;
+  o->trust_region_strategy = OKVISGPU_DOGLEG;
+  o->jacobi_scaling = 1;
+  o->function_tolerance = 1e-6;
+  o->gradient_tolerance = 1e-10;
+  o->parameter_tolerance = 1e-8;
+  o->initial_trust_region_radius = 1e4;
+  o->max_trust_region_radius = 1e16;
+  o->min_trust_region_radius = 1e-32;
+  o->min_relative_decrease = 1e-3;
+  o->min_lm_diagonal = 1e-6;
+  o->max_lm_diagonal = 1e32;
+  o->max_num_consecutive_invalid_steps = 5;
+  o->time_limit_s = -1.0;
+  o->min_iterations = 0;
+  o->redo_propagation_always = 0;
+  o->num_threads = 1;
+  o->verbose = 0;
+}
+
+int okvisgpu_device_count(int32_t* count) {
+  if (!count) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return OKVISGPU_OK;
+}
+
+int okvisgpu_ctx_create(int32_t device, okvisgpu_ctx** out) {
+  if (!out) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(nullptr, OKVISGPU_ERR_DEVICE, "no HIP device");
+  if (device < 0 || device >= n) return fail(nullptr, OKVISGPU_ERR_INVALID_ARGUMENT, "bad device index");
+  auto* c = new okvisgpu_ctx();
+  c->device = device;
+  const int rc = guarded(c, [&]() {
+    HIPCHK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+      throw HipError{std::string("okvisgpu is built for gfx950 only; device is ") + prop.gcnArchName,
+                     OKVISGPU_ERR_DEVICE};
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    return (int)OKVISGPU_OK;
+  });
+  if (rc != OKVISGPU_OK) {
+    delete c;
+    return rc;
+  }
+  *out = c;
+  return OKVISGPU_OK;
+}
+
+int okvisgpu_ctx_destroy(okvisgpu_ctx* c) {
+  if (!c) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  (void)hipSetDevice(c->device);
+  delete c;
+  return OKVISGPU_OK;
+}
+
+const char* okvisgpu_last_error(const okvisgpu_ctx* c) { return c ? c->last_error.c_str() : g_err.c_str(); }
+
+int okvisgpu_set_problems(okvisgpu_ctx* c, const okvisgpu_problem* problems, int32_t n) {
+  if (!c || !problems || n <= 0) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "set_problems: bad arguments");
+  return guarded(c, [&]() {
+    HIPCHK(hipSetDevice(c->device));
+    c->probs.clear();
+    for (int i = 0; i < n; ++i) c->probs.push_back(&problems[i]);
+    c->constOverride.clear();
+    c->build();
+    return (int)OKVISGPU_OK;
+  });
+}
+
+int okvisgpu_update_params(okvisgpu_ctx* c) {
+  if (!c) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
+  return guarded(c, [&]() {
+    HIPCHK(hipSetDevice(c->device));
+    c->uploadParams();
+    return (int)OKVISGPU_OK;
+  });
+}
+
+int okvisgpu_set_block_constant(okvisgpu_ctx* c, int32_t window, int32_t kind, int32_t index, int32_t is_const) {
+  if (!c) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
+  if (window < 0 || window >= (int)c->probs.size() || kind < 0 || kind > 2)
+    return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "set_block_constant: bad window/kind");
+  const okvisgpu_problem* p = c->probs[window];
+  const int n = kind == 0 ? p->n_poses : kind == 1 ? p->n_speed_biases : p->n_landmarks;
+  if (index < 0 || index >= n) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "set_block_constant: bad index");
+  c->constOverride[std::make_tuple(window, kind, index)] = is_const ? 1 : 0;
+  c->structureDirty = true;
+  return OKVISGPU_OK;
+}
+
+int okvisgpu_get_params(okvisgpu_ctx* c) {
+  if (!c) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
+  return guarded(c, [&]() {
+    HIPCHK(hipSetDevice(c->device));
+    c->downloadParams(c->readStates());
+    return (int)OKVISGPU_OK;
+  });
+}
+
+int okvisgpu_solve(okvisgpu_ctx* c, const okvisgpu_options* o, okvisgpu_summary* sums) {
+  if (!c || !o) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
+  if (o->linear_solver != OKVISGPU_DENSE_SCHUR || o->trust_region_strategy != OKVISGPU_DOGLEG)
+    return fail(c, OKVISGPU_ERR_UNSUPPORTED, "only DENSE_SCHUR + DOGLEG is implemented on the GPU path");
+  if (o->max_num_iterations < 0) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "max_num_iterations < 0");
+  return guarded(c, [&]() {
+    HIPCHK(hipSetDevice(c->device));
+    const double t0 = nowS();
+    if (c->structureDirty) {
+      // freeze / unfreeze changed the free set: re-analyse with the caller's current values
+      c->build();
+    }
+    c->setOptions(*o);
+    c->dropGraph();  // options are baked into the captured kernel arguments
+    c->uploadParams();
+    c->resetStates(1e-8);
+    c->launchInit(2);
+    c->ensureGraph();
+    const bool timed = o->time_limit_s >= 0.0;
+    int replays = 0;
+    const int maxReplays = std::max(1, o->max_num_iterations) * 8 + 8;
+    double iterStart = nowS();
+    if (!timed) {
+      for (int k = 0; k < o->max_num_iterations; ++k) HIPCHK(hipGraphLaunch(c->iterGraph, c->stream));
+      replays = o->max_num_iterations;
+    }
+    std::vector<WinState> st = c->readStates();
+    while (true) {
+      bool allDone = true;
+      for (auto& s : st) allDone = allDone && s.done;
+      if (allDone || replays >= maxReplays) break;
+      if (timed) {
+        // CeresIterationCallback (CeresIterationCallback.cpp:30-38): stop once the next iteration
+        // would exceed the budget, after the minimum number of iterations.
+        const double now = nowS();
+        const double iterTime = now - iterStart, cum = now - t0;
+        bool changed = false;
+        for (auto& s : st)
+          if (!s.done && replays > 0 && s.iteration >= o->min_iterations && cum + iterTime > o->time_limit_s) {
+            s.done = 1;
+            s.termination = OKVISGPU_USER_SUCCESS;
+            changed = true;
+          }
+        if (changed) {
+          HIPCHK(hipMemcpyAsync(c->P.st, st.data(), sizeof(WinState) * st.size(), hipMemcpyHostToDevice, c->stream));
+          continue;
+        }
+        iterStart = nowS();
+      }
+      HIPCHK(hipGraphLaunch(c->iterGraph, c->stream));
+      ++replays;
+      st = c->readStates();
+    }
+    c->downloadParams(st);
+    const double t1 = nowS();
+    if (sums) {
+      for (int w = 0; w < c->P.n_win; ++w) {
+        const WinState& s = st[w];
+        okvisgpu_summary& S = sums[w];
+        std::memset(&S, 0, sizeof(S));
+        S.initial_cost = s.initial_cost;
+        S.final_cost = std::min(s.min_cost, s.x_cost) + s.fixed_cost;
+        S.num_iterations = s.iteration;
+        S.num_successful_steps = s.num_succ + 1;
+        S.num_unsuccessful_steps = s.num_unsucc;
+        S.termination_type = s.done ? s.termination : OKVISGPU_NO_CONVERGENCE;
+        S.total_time_s = t1 - t0;
+        S.final_radius = s.radius;
+        S.final_mu = s.mu;
+      }
+    }
+    return (int)OKVISGPU_OK;
+  });
+}
+
+int okvisgpu_evaluate(okvisgpu_ctx* c, int32_t window, double* cost) {
+  if (!c) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
+  if (window < 0 || window >= c->P.n_win) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "bad window");
+  return guarded(c, [&]() {
+    HIPCHK(hipSetDevice(c->device));
+    okvisgpu_options o;
+    okvisgpu_default_options(&o);
+    c->setOptions(o);
+    c->resetStates(1e-8);
+    launch_eval(c->P, 2, c->stream);
+    launch_reduce(c->P, R_COST_INIT, c->stream);
+    HIPCHK(hipGetLastError());
+    auto st = c->readStates();
+    if (cost) *cost = st[window].x_cost + st[window].fixed_cost;
+    return (int)OKVISGPU_OK;
+  });
+}
+
+int okvisgpu_linearize_reduce(okvisgpu_ctx* c, int32_t window, int32_t jacobi_scaling, double mu, double* S,
+                              double* rhs, double* cost, int32_t* dim_out) {
+  if (!c) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
+  if (window < 0 || window >= c->P.n_win) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "bad window");
+  return guarded(c, [&]() {
+    HIPCHK(hipSetDevice(c->device));
+    okvisgpu_options o;
+    okvisgpu_default_options(&o);
+    o.jacobi_scaling = jacobi_scaling;
+    c->setOptions(o);
+    c->resetStates(mu);
+    c->launchInit(2);
+    launch_gn_reduce(c->P, c->stream);
+    HIPCHK(hipGetLastError());
+    auto st = c->readStates();
+    const int fdim = c->B.win_fdim[window], fpad = c->B.win_fpad[window];
+    if (dim_out) *dim_out = fdim;
+    if (cost) *cost = st[window].x_cost + st[window].fixed_cost;
+    if (S && fdim) {
+      std::vector<double> full((size_t)fpad * fpad);
+      HIPCHK(hipMemcpy(full.data(), c->P.S + c->B.win_soff[window], full.size() * 8, hipMemcpyDeviceToHost));
+      for (int r = 0; r < fdim; ++r)
+        for (int q = 0; q <= r; ++q) {
+          S[(size_t)r * fdim + q] = full[(size_t)r * fpad + q];
+          S[(size_t)q * fdim + r] = full[(size_t)r * fpad + q];
+        }
+    }
+    if (rhs && fdim)
+      HIPCHK(hipMemcpy(rhs, c->P.rhsF + c->B.win_foff[window], sizeof(double) * fdim, hipMemcpyDeviceToHost));
+    if (st[window].gn_failed) return fail(c, OKVISGPU_ERR_NUMERICAL, "landmark block not positive definite");
+    return (int)OKVISGPU_OK;
+  });
+}
+
+int okvisgpu_eval_reprojection(okvisgpu_ctx* c, int32_t window, double* r, double* Jp, double* Jl) {
+  if (!c) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
+  if (window < 0 || window >= c->P.n_win) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "bad window");
+  return guarded(c, [&]() {
+    HIPCHK(hipSetDevice(c->device));
+    c->resetStates(1e-8);
+    launch_eval(c->P, 3, c->stream);
+    HIPCHK(hipGetLastError());
+    const int64_t S = c->P.obs_stride;
+    std::vector<double> lin((size_t)kObsLin * S);
+    HIPCHK(hipMemcpyAsync(lin.data(), c->P.obs_lin[0], lin.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    const int ob = c->B.obs_base[window], n = c->probs[window]->n_observations;
+    for (int k = 0; k < n; ++k) {
+      const int g = ob + k, o = c->B.obs_orig[g];
+      if (r) for (int i = 0; i < 2; ++i) r[2 * o + i] = lin[(size_t)i * S + g];
+      if (Jp) for (int i = 0; i < 12; ++i) Jp[12 * o + i] = lin[(size_t)(2 + i) * S + g];
+      if (Jl) for (int i = 0; i < 6; ++i) Jl[6 * o + i] = lin[(size_t)(14 + i) * S + g];
+    }
+    return (int)OKVISGPU_OK;
+  });
+}
+
+int okvisgpu_eval_imu(okvisgpu_ctx* c, int32_t window, int32_t redo_always, double* r, double* J) {
+  if (!c) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
+  if (window < 0 || window >= c->P.n_win) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "bad window");
+  return guarded(c, [&]() {
+    HIPCHK(hipSetDevice(c->device));
+    okvisgpu_options o;
+    okvisgpu_default_options(&o);
+    o.redo_propagation_always = redo_always;
+    c->setOptions(o);
+    c->resetStates(1e-8);
+    launch_eval(c->P, 3, c->stream);
+    HIPCHK(hipGetLastError());
+    const int n = c->probs[window]->n_imu, ib = c->B.imu_base[window];
+    std::vector<double> lin((size_t)kImuLin * std::max(1, n));
+    if (n) HIPCHK(hipMemcpyAsync(lin.data(), c->P.imu_lin[0] + (size_t)ib * kImuLin, (size_t)kImuLin * n * 8,
+                                 hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int f = 0; f < n; ++f) {
+      if (r) for (int i = 0; i < 15; ++i) r[15 * f + i] = lin[(size_t)f * kImuLin + i];
+      if (J) for (int i = 0; i < 450; ++i) J[450 * (size_t)f + i] = lin[(size_t)f * kImuLin + 15 + i];
+    }
+    // keep the caller's ImuError state in sync (the evaluation may have re-integrated)
+    c->downloadParams(c->readStates());
+    return (int)OKVISGPU_OK;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,301 @@
+"""ctypes binding of the okvisgpu C ABI (include/okvisgpu.h).
+
+The product is the C-ABI shared library ``okvis2-x_amd/libokvisgpu.so`` (HIP kernels for gfx950 +
+C++ host runtime). This module only marshals structs for tests, the benchmark and Python callers;
+it contains no solver logic and no CPU fallback: if the library (or its GPU code object) is
+missing, every call fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.path.join(PKG_ROOT, "libokvisgpu.so")
+
+IMU_STATE_DOUBLES = 292
+
+DIST_NONE, DIST_RADTAN, DIST_EQUIDISTANT = 0, 1, 2
+TERMINATION = {0: "CONVERGENCE", 1: "NO_CONVERGENCE", 2: "FAILURE", 3: "USER_SUCCESS"}
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+_lp = C.POINTER(C.c_int64)
+_up = C.POINTER(C.c_uint8)
+
+
+class Camera(C.Structure):
+    _fields_ = [("distortion", C.c_int32), ("width", C.c_int32), ("height", C.c_int32),
+                ("fu", C.c_double), ("fv", C.c_double), ("cu", C.c_double), ("cv", C.c_double),
+                ("dist", C.c_double * 4)]
+
+
+class ImuParams(C.Structure):
+    _fields_ = [("a_max", C.c_double), ("g_max", C.c_double), ("sigma_g_c", C.c_double),
+                ("sigma_a_c", C.c_double), ("sigma_gw_c", C.c_double), ("sigma_aw_c", C.c_double),
+                ("g", C.c_double)]
+
+
+class Problem(C.Structure):
+    _fields_ = [
+        ("n_poses", C.c_int32), ("poses", _dp), ("pose_constant", _up),
+        ("n_speed_biases", C.c_int32), ("speed_biases", _dp), ("speed_bias_constant", _up),
+        ("n_landmarks", C.c_int32), ("landmarks", _dp), ("landmark_constant", _up),
+        ("n_cameras", C.c_int32), ("cameras", C.POINTER(Camera)), ("extrinsics", _dp),
+        ("n_observations", C.c_int32), ("obs_pose", _ip), ("obs_landmark", _ip), ("obs_camera", _ip),
+        ("obs_keypoint", _dp), ("obs_sqrt_info", _dp), ("obs_cauchy", _up),
+        ("n_imu", C.c_int32), ("imu_blocks", _ip), ("imu_t0_ns", _lp), ("imu_t1_ns", _lp),
+        ("imu_sample_begin", _ip), ("imu_sample_t_ns", _lp), ("imu_sample_gyr_acc", _dp),
+        ("imu_params", ImuParams), ("imu_state", _dp),
+        ("n_pose_priors", C.c_int32), ("pose_prior_block", _ip), ("pose_prior_meas", _dp),
+        ("pose_prior_sqrt_info", _dp),
+        ("n_sb_priors", C.c_int32), ("sb_prior_block", _ip), ("sb_prior_meas", _dp),
+        ("sb_prior_sqrt_info", _dp),
+    ]
+
+
+class Options(C.Structure):
+    _fields_ = [
+        ("max_num_iterations", C.c_int32), ("linear_solver", C.c_int32),
+        ("trust_region_strategy", C.c_int32), ("jacobi_scaling", C.c_int32),
+        ("function_tolerance", C.c_double), ("gradient_tolerance", C.c_double),
+        ("parameter_tolerance", C.c_double), ("initial_trust_region_radius", C.c_double),
+        ("max_trust_region_radius", C.c_double), ("min_trust_region_radius", C.c_double),
+        ("min_relative_decrease", C.c_double), ("min_lm_diagonal", C.c_double),
+        ("max_lm_diagonal", C.c_double), ("max_num_consecutive_invalid_steps", C.c_int32),
+        ("time_limit_s", C.c_double), ("min_iterations", C.c_int32),
+        ("redo_propagation_always", C.c_int32), ("num_threads", C.c_int32), ("verbose", C.c_int32),
+    ]
+
+
+class Summary(C.Structure):
+    _fields_ = [("initial_cost", C.c_double), ("final_cost", C.c_double),
+                ("num_iterations", C.c_int32), ("num_successful_steps", C.c_int32),
+                ("num_unsuccessful_steps", C.c_int32), ("termination_type", C.c_int32),
+                ("total_time_s", C.c_double), ("final_radius", C.c_double), ("final_mu", C.c_double)]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["termination"] = TERMINATION.get(self.termination_type, "?")
+        return d
+
+
+class SynthConfig(C.Structure):
+    _fields_ = [("n_keyframes", C.c_int32), ("n_landmarks", C.c_int32), ("n_observations", C.c_int32),
+                ("max_obs_per_landmark", C.c_int32), ("kf_dt_s", C.c_double), ("imu_rate_hz", C.c_double),
+                ("pixel_noise", C.c_double), ("init_sigma_pos", C.c_double), ("init_sigma_rot", C.c_double),
+                ("init_sigma_lm", C.c_double), ("init_sigma_vel", C.c_double), ("seed", C.c_uint64)]
+
+
+# Exported symbols of include/okvisgpu.h (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = [
+    "okvisgpu_abi_version", "okvisgpu_default_options", "okvisgpu_device_count", "okvisgpu_ctx_create",
+    "okvisgpu_ctx_destroy", "okvisgpu_last_error", "okvisgpu_set_problems", "okvisgpu_update_params",
+    "okvisgpu_set_block_constant", "okvisgpu_solve", "okvisgpu_get_params", "okvisgpu_evaluate",
+    "okvisgpu_linearize_reduce", "okvisgpu_eval_reprojection", "okvisgpu_eval_imu",
+    "okvisgpu_synth_default_config", "okvisgpu_synth_create", "okvisgpu_synth_problem",
+    "okvisgpu_synth_ground_truth", "okvisgpu_synth_reset", "okvisgpu_synth_destroy",
+]
+
+_lib = None
+
+
+def lib():
+    """Load libokvisgpu.so (fails loudly if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"okvisgpu: {LIB_PATH} missing — build it with `make -C okvis2-x_amd`")
+        L = C.CDLL(LIB_PATH)
+        L.okvisgpu_abi_version.restype = C.c_int
+        L.okvisgpu_default_options.argtypes = [C.POINTER(Options)]
+        L.okvisgpu_device_count.argtypes = [_ip]
+        L.okvisgpu_ctx_create.argtypes = [C.c_int32, C.POINTER(C.c_void_p)]
+        L.okvisgpu_ctx_destroy.argtypes = [C.c_void_p]
+        L.okvisgpu_last_error.argtypes = [C.c_void_p]
+        L.okvisgpu_last_error.restype = C.c_char_p
+        L.okvisgpu_set_problems.argtypes = [C.c_void_p, C.POINTER(Problem), C.c_int32]
+        L.okvisgpu_update_params.argtypes = [C.c_void_p]
+        L.okvisgpu_set_block_constant.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_int32]
+        L.okvisgpu_solve.argtypes = [C.c_void_p, C.POINTER(Options), C.POINTER(Summary)]
+        L.okvisgpu_get_params.argtypes = [C.c_void_p]
+        L.okvisgpu_evaluate.argtypes = [C.c_void_p, C.c_int32, _dp]
+        L.okvisgpu_linearize_reduce.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_double, _dp, _dp, _dp, _ip]
+        L.okvisgpu_eval_reprojection.argtypes = [C.c_void_p, C.c_int32, _dp, _dp, _dp]
+        L.okvisgpu_eval_imu.argtypes = [C.c_void_p, C.c_int32, C.c_int32, _dp, _dp]
+        L.okvisgpu_synth_default_config.argtypes = [C.POINTER(SynthConfig), C.c_int32, C.c_int32, C.c_int32, C.c_uint64]
+        L.okvisgpu_synth_create.argtypes = [C.POINTER(SynthConfig), C.POINTER(C.c_void_p)]
+        L.okvisgpu_synth_problem.argtypes = [C.c_void_p]
+        L.okvisgpu_synth_problem.restype = C.POINTER(Problem)
+        L.okvisgpu_synth_ground_truth.argtypes = [C.c_void_p, _dp, _dp, _dp]
+        L.okvisgpu_synth_reset.argtypes = [C.c_void_p]
+        L.okvisgpu_synth_destroy.argtypes = [C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def default_options(**kw) -> Options:
+    o = Options()
+    lib().okvisgpu_default_options(C.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+def dptr(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_dp)
+
+
+class OkvisGpuError(RuntimeError):
+    pass
+
+
+class SynthWindow:
+    """A synthetic sliding window (owned by the C library)."""
+
+    def __init__(self, n_kf=10, n_lm=500, n_obs=4000, seed=20251015, **overrides):
+        cfg = SynthConfig()
+        lib().okvisgpu_synth_default_config(C.byref(cfg), n_kf, n_lm, n_obs, seed)
+        for k, v in overrides.items():
+            setattr(cfg, k, v)
+        h = C.c_void_p()
+        rc = lib().okvisgpu_synth_create(C.byref(cfg), C.byref(h))
+        if rc != 0:
+            raise OkvisGpuError(f"okvisgpu_synth_create failed ({rc})")
+        self.handle = h
+        self.cfg = cfg
+
+    @property
+    def problem(self) -> Problem:
+        return lib().okvisgpu_synth_problem(self.handle).contents
+
+    def problem_ptr(self):
+        return lib().okvisgpu_synth_problem(self.handle)
+
+    def reset(self):
+        lib().okvisgpu_synth_reset(self.handle)
+
+    def ground_truth(self):
+        p = self.problem
+        poses = np.zeros((p.n_poses, 7))
+        lms = np.zeros((p.n_landmarks, 4))
+        sbs = np.zeros((p.n_speed_biases, 9))
+        lib().okvisgpu_synth_ground_truth(self.handle, dptr(poses), dptr(lms), dptr(sbs))
+        return poses, lms, sbs
+
+    # views into the (mutable) parameter arrays
+    def poses(self):
+        p = self.problem
+        return np.ctypeslib.as_array(p.poses, shape=(p.n_poses, 7))
+
+    def speed_biases(self):
+        p = self.problem
+        return np.ctypeslib.as_array(p.speed_biases, shape=(p.n_speed_biases, 9))
+
+    def landmarks(self):
+        p = self.problem
+        return np.ctypeslib.as_array(p.landmarks, shape=(p.n_landmarks, 4))
+
+    def imu_state(self):
+        p = self.problem
+        return np.ctypeslib.as_array(p.imu_state, shape=(p.n_imu, IMU_STATE_DOUBLES))
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                lib().okvisgpu_synth_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+class Context:
+    """One okvisgpu_ctx (one HIP stream + device buffers) holding a batch of windows."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        rc = lib().okvisgpu_ctx_create(device, C.byref(h))
+        if rc != 0:
+            raise OkvisGpuError(f"okvisgpu_ctx_create({device}) failed with status {rc}")
+        self.h = h
+        self._keep = None
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = lib().okvisgpu_last_error(self.h)
+            raise OkvisGpuError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def set_problems(self, problems):
+        arr = (Problem * len(problems))(*problems)
+        self._keep = (arr, problems)
+        self._check(lib().okvisgpu_set_problems(self.h, arr, len(problems)), "okvisgpu_set_problems")
+
+    def update_params(self):
+        self._check(lib().okvisgpu_update_params(self.h), "okvisgpu_update_params")
+
+    def set_block_constant(self, window, kind, index, is_constant):
+        self._check(lib().okvisgpu_set_block_constant(self.h, window, kind, index, int(is_constant)),
+                    "okvisgpu_set_block_constant")
+
+    def solve(self, options: Optional[Options] = None, n_windows: int = 1):
+        o = options or default_options()
+        sums = (Summary * n_windows)()
+        self._check(lib().okvisgpu_solve(self.h, C.byref(o), sums), "okvisgpu_solve")
+        return [s.as_dict() for s in sums]
+
+    def get_params(self):
+        self._check(lib().okvisgpu_get_params(self.h), "okvisgpu_get_params")
+
+    def evaluate(self, window=0):
+        c = C.c_double()
+        self._check(lib().okvisgpu_evaluate(self.h, window, C.byref(c)), "okvisgpu_evaluate")
+        return c.value
+
+    def linearize_reduce(self, window=0, jacobi_scaling=True, mu=0.0, dim_hint=None):
+        dim = C.c_int32()
+        cost = C.c_double()
+        self._check(lib().okvisgpu_linearize_reduce(self.h, window, int(jacobi_scaling), mu, None, None,
+                                                     C.byref(cost), C.byref(dim)), "linearize_reduce(dim)")
+        n = dim.value
+        S = np.zeros((n, n))
+        rhs = np.zeros(n)
+        self._check(lib().okvisgpu_linearize_reduce(self.h, window, int(jacobi_scaling), mu, dptr(S), dptr(rhs),
+                                                     C.byref(cost), C.byref(dim)), "linearize_reduce")
+        return S, rhs, cost.value
+
+    def eval_reprojection(self, n_obs, window=0):
+        r = np.zeros((n_obs, 2))
+        Jp = np.zeros((n_obs, 2, 6))
+        Jl = np.zeros((n_obs, 2, 3))
+        self._check(lib().okvisgpu_eval_reprojection(self.h, window, dptr(r), dptr(Jp), dptr(Jl)),
+                    "eval_reprojection")
+        return r, Jp, Jl
+
+    def eval_imu(self, n_imu, window=0, redo_always=False):
+        r = np.zeros((n_imu, 15))
+        J = np.zeros((n_imu, 15, 30))
+        self._check(lib().okvisgpu_eval_imu(self.h, window, int(redo_always), dptr(r), dptr(J)), "eval_imu")
+        return r, J
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().okvisgpu_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def device_count() -> int:
+    n = C.c_int32(0)
+    rc = lib().okvisgpu_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
