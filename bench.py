@@ -1,0 +1,273 @@
+#!/usr/bin/env python3
+"""bench.py — Gauss-Newton (dogleg trust-region) iterations/s of the MI355X okvis_ceres backend.
+
+Metric (BASELINE.json): "Gauss-Newton iters/sec on 50-KF/2000-landmark window; ATE vs CPU ref".
+A step = one trust-region iteration (Ceres semantics: linearise + Schur-reduce + LLT + dogleg +
+candidate evaluation + accept/reject) of EVERY window in the job's batch of independent synthetic
+S50 windows (50 keyframes, 2,000 landmarks, 16,000 reprojections, 49 IMU factors).
+value = (windows x timed iterations) / wall time of the timed region, max over ranks
+(window-iterations per second, whole job). Strong scaling: the total window count is fixed and
+split across ranks (one process per GPU, no data-path collective).
+
+All tolerances are set to 0 so every timed iteration does real work (the K-iteration protocol of
+BASELINE.md); inputs are resident in HBM before the timed region.
+
+Also reported: the single-window latency mode (1 window on 1 GPU), per-kernel device time of one
+iteration (HIP events on the context's stream), the roofline of the dominant kernel, accuracy (ATE
+of window 0 vs ground truth for GPU and CPU oracle, max pose deviation GPU vs CPU), and the CPU
+baseline = the repo's CPU restatement (oracle/liboracle.so, "port") timed on this host.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "okvis2-x_amd"))
+import okvisgpu as og  # noqa: E402
+
+FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (spec; SURVEY.md §8d, not in the gfx950 guide)
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+SEED0 = 20251015
+
+CONFIGS = {
+    "s50": dict(n_kf=50, n_lm=2000, n_obs=16000),
+    "s10": dict(n_kf=10, n_lm=500, n_obs=4000),
+}
+
+
+def bench_options(max_iter):
+    # all tolerances 0: every iteration is performed (BASELINE.md timing protocol)
+    return og.default_options(max_num_iterations=max_iter, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+
+
+def make_windows(cfg, indices):
+    return [og.SynthWindow(cfg["n_kf"], cfg["n_lm"], cfg["n_obs"], seed=SEED0 + i) for i in indices]
+
+
+def ate(P, gt):
+    """SE(3)-aligned RMSE of keyframe positions (Horn/Umeyama without scale)."""
+    a, b = P[:, :3], gt[:, :3]
+    ma, mb = a.mean(0), b.mean(0)
+    H = (a - ma).T @ (b - mb)
+    U, _, Vt = np.linalg.svd(H)
+    D = np.eye(3)
+    D[2, 2] = np.sign(np.linalg.det(Vt.T @ U.T))
+    R = Vt.T @ D @ U.T
+    aligned = (R @ (a - ma).T).T + mb
+    return float(np.sqrt(np.mean(np.sum((aligned - b) ** 2, axis=1))))
+
+
+def chol_update_flops(fdims, n_tiles):
+    """Algorithmic FLOPs of all k_chol_update launches of one GN iteration (2*64^3 per tile)."""
+    tot = 0
+    for fd in fdims:
+        T = (fd + 63) // 64
+        for k in range(T):
+            m = T - k - 1
+            tot += m * (m + 1) // 2 * 2 * 64 ** 3
+    return tot
+
+
+def run_cpu_baseline(cfg, iters, threads, reps):
+    """Oracle (CPU restatement, `port`) on window 0, same protocol; median of `reps` runs after one
+    warm-up. Bounded sample: one window."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import _oracle  # noqa: E402  (bench.py's cpu_baseline leg is an allowed oracle user)
+    w = make_windows(cfg, [0])[0]
+    opts = bench_options(iters)
+    opts.num_threads = threads
+    times = []
+    for r in range(reps + 1):
+        w.reset()
+        t0 = time.perf_counter()
+        s = _oracle.solve(w.problem_ptr(), opts)
+        if r > 0:
+            times.append(time.perf_counter() - t0)
+    return w, s, float(np.median(times))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--windows", type=int, default=64, help="total windows in the job (strong scaling)")
+    ap.add_argument("--config", default="s50", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-threads", type=int, default=3, help="realtime_num_threads (okvis2.yaml:93)")
+    ap.add_argument("--cpu-iters", type=int, default=None, help="default: warmup + steps")
+    ap.add_argument("--cpu-reps", type=int, default=5, help="median of this many timed runs after 1 warm-up")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-latency", action="store_true")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl")
+        dist = tdist
+    else:
+        import torch
+    cfg = CONFIGS[args.config]
+
+    # ---- this rank's share of the fixed total (strong scaling)
+    per = [args.windows // world + (1 if r < args.windows % world else 0) for r in range(world)]
+    start = sum(per[:rank])
+    mine = list(range(start, start + per[rank]))
+    windows = make_windows(cfg, mine)
+    ctx = og.Context(local_rank)
+    ctx.set_problems([w.problem for w in windows])
+    total_iters = args.warmup + args.steps
+    opts = bench_options(total_iters)
+
+    ctx.solve_begin(opts)
+    ctx.solve_iterate(args.warmup)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ctx.solve_iterate(args.steps)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    sums = ctx.solve_end(len(windows))
+    elapsed = t1 - t0
+    early = sum(1 for s in sums if s["num_iterations"] < total_iters)
+    gn_frac = float(np.mean([(s["num_successful_steps"] - 1) / max(1, s["num_iterations"]) for s in sums]))
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        e = torch.tensor([early], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(e, op=dist.ReduceOp.SUM)
+        early = int(e.item())
+
+    value = args.windows * args.steps / elapsed
+    result = {
+        "metric": "Gauss-Newton iters/sec on 50-KF/2000-landmark window; ATE vs CPU ref",
+        "value": value,
+        "unit": "window-iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (EuRoC stereo rig, 200 Hz IMU, seeded windows; SURVEY.md §8d)",
+        "config": {
+            "workload": f"{args.windows} independent {args.config.upper()} windows "
+                        f"({cfg['n_kf']} KF / {cfg['n_lm']} landmarks / {cfg['n_obs']} reprojections, "
+                        f"{cfg['n_kf'] - 1} IMU factors), DENSE_SCHUR + DOGLEG, all tolerances 0",
+            "windows_total": args.windows,
+            "windows_per_gpu": per[rank],
+            "parallelism": f"replicas x{world} (one window batch per GPU, no collective in the loop)",
+        },
+    }
+
+    if args.cpu_iters is None:
+        args.cpu_iters = total_iters
+    if rank == 0:
+        result["early_terminated_windows"] = early
+        result["frac_iterations_with_gn_solve"] = gn_frac
+        # ---- single-window latency mode (1 window, this GPU)
+        if not args.no_latency:
+            w1 = make_windows(cfg, [0])
+            c1 = og.Context(local_rank)
+            c1.set_problems([w1[0].problem])
+            c1.solve_begin(opts)
+            c1.solve_iterate(args.warmup)
+            c1.synchronize()
+            a = time.perf_counter()
+            c1.solve_iterate(args.steps)
+            c1.synchronize()
+            b = time.perf_counter()
+            s1 = c1.solve_end(1)[0]
+            result["single_window"] = {"iters_per_s": args.steps / (b - a), "ms_per_iter": (b - a) / args.steps * 1e3,
+                                       "final_cost": s1["final_cost"]}
+            gpu_pose_w0 = w1[0].poses().copy()
+            gt_p, _, _ = w1[0].ground_truth()
+            c1.close()
+        # ---- per-kernel device time of one iteration + roofline of the dominant kernel
+        if not args.no_profile:
+            cp = og.Context(local_rank)
+            cp.set_problems([w.problem for w in windows])
+            for w in windows:
+                w.reset()
+            cp.update_params()
+            cp.solve_begin(opts)
+            cp.solve_iterate(args.warmup)
+            ph = cp.profile_iteration()
+            cp.solve_end(len(windows))
+            cp.close()
+            result["kernel_ms_per_iteration"] = {k: round(v, 4) for k, v in ph.items()}
+            fdims = [15 * cfg["n_kf"]] * len(windows)
+            flops = chol_update_flops(fdims, None)
+            upd_ms = ph["chol_update"]
+            n_launch = (fdims[0] + 63) // 64 - 1
+            dominant = max(ph, key=ph.get)
+            result["roofline"] = {
+                "kernel": "k_chol_update (reduced-camera block multiply, v_mfma_f64_16x16x4_f64)",
+                "bound": "mfma",
+                "achieved": flops / (upd_ms * 1e-3) / 1e12 if upd_ms > 0 else None,
+                "peak": FP64_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": (flops / (upd_ms * 1e-3) / 1e12) / FP64_MFMA_PEAK_TFLOPS if upd_ms > 0 else None,
+                "traffic": None,
+                "flops_per_iteration": flops,
+                "launches_per_iteration": n_launch,
+                "avg_launch_ms": upd_ms / max(1, n_launch),
+                "dominant_kernel_by_time": dominant,
+            }
+            # eval kernel: algorithmic HBM bytes per observation
+            eo = ph["eval_obs"]
+            n_obs = cfg["n_obs"] * len(windows)
+            bytes_obs = n_obs * (2 * 8 + 4 * 8 + 3 * 4 + 1 + 20 * 8 + 8)
+            result["roofline_eval_obs"] = {"bound": "hbm", "achieved": bytes_obs / (eo * 1e-3) / 1e9 if eo > 0 else None,
+                                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                           "frac": bytes_obs / (eo * 1e-3) / 1e9 / HBM_PEAK_GBS if eo > 0 else None,
+                                           "bytes_per_launch": bytes_obs}
+        # ---- CPU baseline (oracle restatement timed on this host) + accuracy vs CPU
+        if not args.no_cpu:
+            wc, sc, dt = run_cpu_baseline(cfg, args.cpu_iters, args.cpu_threads, args.cpu_reps)
+            result["cpu_baseline"] = {
+                "value": args.cpu_iters / dt,
+                "unit": "iters/s (single window)",
+                "cores": args.cpu_threads,
+                "kind": "port",
+                "sample": f"1 {args.config.upper()} window x {args.cpu_iters} iterations, median of "
+                          f"{args.cpu_reps} runs (oracle/liboracle.so, {args.cpu_threads} threads, same options)",
+                "wall_s": dt,
+            }
+            if not args.no_latency and args.cpu_iters == total_iters:
+                P0 = wc.poses()
+                result["accuracy"] = {
+                    "ate_gpu_m": ate(gpu_pose_w0, gt_p), "ate_cpu_m": ate(P0, gt_p),
+                    "max_pose_dev_gpu_vs_cpu_m": float(np.abs(gpu_pose_w0[:, :3] - P0[:, :3]).max()),
+                    "final_cost_gpu": result["single_window"]["final_cost"], "final_cost_cpu": sc["final_cost"],
+                }
+            if not args.no_latency:
+                result["single_window"]["speedup_vs_cpu"] = result["single_window"]["iters_per_s"] / (args.cpu_iters / dt)
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -205,6 +205,27 @@ int okvisgpu_set_block_constant(okvisgpu_ctx* ctx, int32_t window, int32_t kind,
  * Results are written back into the caller's parameter arrays (and imu_state when provided). */
 int okvisgpu_solve(okvisgpu_ctx* ctx, const okvisgpu_options* options, okvisgpu_summary* summaries);
 
+/* Split form of okvisgpu_solve (okvisgpu_solve == begin + iterate(max_num_iterations) + end):
+ *   begin   upload the caller's parameter values, iteration 0 (initial evaluation, Jacobi scaling,
+ *           gradient norms) and instantiate the captured iteration graph;
+ *   iterate enqueue n trust-region iterations on the context's stream (asynchronous; windows that
+ *           have terminated skip all work);
+ *   end     synchronise, finish windows that spent iterations on LM-regularisation retries, write
+ *           results back into the caller's arrays and fill the summaries.
+ * okvisgpu_synchronize waits for the context's stream. */
+int okvisgpu_solve_begin(okvisgpu_ctx* ctx, const okvisgpu_options* options);
+int okvisgpu_solve_iterate(okvisgpu_ctx* ctx, int32_t n);
+int okvisgpu_solve_end(okvisgpu_ctx* ctx, okvisgpu_summary* summaries);
+int okvisgpu_synchronize(okvisgpu_ctx* ctx);
+
+/* Device time per kernel of ONE trust-region iteration launched eagerly (not from the graph) on
+ * the context's stream, bracketed by HIP events; must follow okvisgpu_solve_begin (it advances the
+ * solve by one iteration). phase_ms[OKVISGPU_N_PHASES] (ms, summed over the launches of that
+ * kernel in the iteration); phase i is named by okvisgpu_phase_name(i). */
+#define OKVISGPU_N_PHASES 19
+int okvisgpu_profile_iteration(okvisgpu_ctx* ctx, double* phase_ms);
+const char* okvisgpu_phase_name(int32_t phase);
+
 /* Copy device parameter values back into the caller's host arrays without solving. */
 int okvisgpu_get_params(okvisgpu_ctx* ctx);
 

@@ -201,11 +201,17 @@ __global__ __launch_bounds__(256) void k_trsv(DevProblem P) {
   for (int e = t; e < fdim; e += 256) P.yF[(size_t)foff + e] = y[e];
 }
 
+void launch_chol_panel(const DevProblem& P, int k, hipStream_t s) {
+  hipLaunchKernelGGL(k_chol_panel, dim3(P.max_tiles - k, P.n_win), dim3(256), 0, s, P, k);
+}
+void launch_chol_update(const DevProblem& P, int k, hipStream_t s) {
+  const int m = P.max_tiles - k - 1;
+  if (m > 0) hipLaunchKernelGGL(k_chol_update, dim3(m * (m + 1) / 2, P.n_win), dim3(256), 0, s, P, k);
+}
 void launch_cholesky(const DevProblem& P, int max_tiles, hipStream_t s) {
   for (int k = 0; k < max_tiles; ++k) {
-    hipLaunchKernelGGL(k_chol_panel, dim3(max_tiles - k, P.n_win), dim3(256), 0, s, P, k);
-    const int m = max_tiles - k - 1;
-    if (m > 0) hipLaunchKernelGGL(k_chol_update, dim3(m * (m + 1) / 2, P.n_win), dim3(256), 0, s, P, k);
+    launch_chol_panel(P, k, s);
+    launch_chol_update(P, k, s);
   }
 }
 

@@ -682,11 +682,20 @@ __global__ __launch_bounds__(64) void k_eval_priors(DevProblem P, int mode) {
 }
 
 // ------------------------------------------------------------------------------------ launchers
-void launch_eval(const DevProblem& P, int mode, hipStream_t s) {
+void launch_eval_obs(const DevProblem& P, int mode, hipStream_t s) {
   if (P.n_obs > 0) hipLaunchKernelGGL(k_eval_obs, dim3((P.n_obs + 255) / 256), dim3(256), 0, s, P, mode);
+}
+void launch_eval_imu(const DevProblem& P, int mode, hipStream_t s) {
   if (P.n_imu > 0) hipLaunchKernelGGL(k_eval_imu, dim3(P.n_imu), dim3(64), 0, s, P, mode);
+}
+void launch_eval_priors(const DevProblem& P, int mode, hipStream_t s) {
   const int np = P.n_pprior + P.n_sbprior;
   if (np > 0) hipLaunchKernelGGL(k_eval_priors, dim3((np + 63) / 64), dim3(64), 0, s, P, mode);
+}
+void launch_eval(const DevProblem& P, int mode, hipStream_t s) {
+  launch_eval_obs(P, mode, s);
+  launch_eval_imu(P, mode, s);
+  launch_eval_priors(P, mode, s);
 }
 
 }  // namespace okg

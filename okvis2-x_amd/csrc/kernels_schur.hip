@@ -387,21 +387,40 @@ __global__ __launch_bounds__(256) void k_gn_finalize(DevProblem P) {
 }
 
 // ------------------------------------------------------------------------------------ launchers
-void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
+void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
   if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_blocks, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P, lin_mode);
+}
+void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s) {
   if (P.n_fblock > 0) hipLaunchKernelGGL(k_fgrad, dim3((P.n_fblock + 63) / 64), dim3(64), 0, s, P, lin_mode);
 }
-
-void launch_gn_reduce(const DevProblem& P, hipStream_t s) {
+void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
+  launch_lm_blocks(P, lin_mode, s);
+  launch_fgrad(P, lin_mode, s);
+}
+void launch_lm_prep(const DevProblem& P, hipStream_t s) {
   if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_prep, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P);
-  hipLaunchKernelGGL(k_zero_S, dim3(512, P.n_win), dim3(256), 0, s, P);
+}
+void launch_zero_S(const DevProblem& P, hipStream_t s) {
+  if (P.max_fpad > 0) hipLaunchKernelGGL(k_zero_S, dim3(512, P.n_win), dim3(256), 0, s, P);
+}
+void launch_assemble(const DevProblem& P, hipStream_t s) {
   if (P.n_pair > 0) hipLaunchKernelGGL(k_assemble, dim3(P.n_pair), dim3(128), 0, s, P);
 }
-
-void launch_gn_backsub(const DevProblem& P, hipStream_t s) {
+void launch_gn_reduce(const DevProblem& P, hipStream_t s) {
+  launch_lm_prep(P, s);
+  launch_zero_S(P, s);
+  launch_assemble(P, s);
+}
+void launch_lm_backsub(const DevProblem& P, hipStream_t s) {
   if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_backsub, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P);
+}
+void launch_gn_finalize(const DevProblem& P, hipStream_t s) {
   const int n = P.n_fblock + P.n_lm;
   if (n > 0) hipLaunchKernelGGL(k_gn_finalize, dim3((n + 255) / 256), dim3(256), 0, s, P);
+}
+void launch_gn_backsub(const DevProblem& P, hipStream_t s) {
+  launch_lm_backsub(P, s);
+  launch_gn_finalize(P, s);
 }
 
 }  // namespace okg

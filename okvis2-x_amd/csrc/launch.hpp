@@ -8,16 +8,28 @@
 
 namespace okg {
 
-// evaluation (kernels_eval.hip); mode 0 current, 1 candidate, 2 initial
+// evaluation (kernels_eval.hip); mode 0 current, 1 candidate, 2 initial, 3 initial without loss
 void launch_eval(const DevProblem& P, int mode, hipStream_t s);
+void launch_eval_obs(const DevProblem& P, int mode, hipStream_t s);
+void launch_eval_imu(const DevProblem& P, int mode, hipStream_t s);
+void launch_eval_priors(const DevProblem& P, int mode, hipStream_t s);
 
 // landmark / reduced-system kernels (kernels_schur.hip); lin_mode 0 = init, 1 = accepted only
 void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_gn_reduce(const DevProblem& P, hipStream_t s);    // lm_prep + zero S + assemble
 void launch_gn_backsub(const DevProblem& P, hipStream_t s);   // landmark back substitution + gn vectors
+void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s);
+void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s);
+void launch_lm_prep(const DevProblem& P, hipStream_t s);
+void launch_zero_S(const DevProblem& P, hipStream_t s);
+void launch_assemble(const DevProblem& P, hipStream_t s);
+void launch_lm_backsub(const DevProblem& P, hipStream_t s);
+void launch_gn_finalize(const DevProblem& P, hipStream_t s);
 
 // dense factorisation (kernels_chol.hip)
 void launch_cholesky(const DevProblem& P, int max_tiles, hipStream_t s);
+void launch_chol_panel(const DevProblem& P, int k, hipStream_t s);
+void launch_chol_update(const DevProblem& P, int k, hipStream_t s);
 void launch_trsv(const DevProblem& P, hipStream_t s);
 
 // trust-region control (kernels_control.hip)

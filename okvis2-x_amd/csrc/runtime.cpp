@@ -433,6 +433,30 @@ struct okvisgpu_ctx {
   size_t arenaBytes = 0;
   hipGraphExec_t iterGraph = nullptr;
   bool haveProblem = false;
+  // split-solve state
+  bool inSolve = false;
+  okvisgpu_options opts{};
+  int replays = 0;
+  double solveT0 = 0.0;
+
+  void fillSummaries(const std::vector<WinState>& st, okvisgpu_summary* sums) {
+    if (!sums) return;
+    const double t1 = nowS();
+    for (int w = 0; w < P.n_win; ++w) {
+      const WinState& s = st[w];
+      okvisgpu_summary& S = sums[w];
+      std::memset(&S, 0, sizeof(S));
+      S.initial_cost = s.initial_cost;
+      S.final_cost = std::min(s.min_cost, s.x_cost) + s.fixed_cost;
+      S.num_iterations = s.iteration;
+      S.num_successful_steps = s.num_succ + 1;  // Ceres counts iteration 0
+      S.num_unsuccessful_steps = s.num_unsucc;
+      S.termination_type = s.done ? s.termination : OKVISGPU_NO_CONVERGENCE;
+      S.total_time_s = t1 - solveT0;
+      S.final_radius = s.radius;
+      S.final_mu = s.mu;
+    }
+  }
 
   ~okvisgpu_ctx() {
     if (iterGraph) (void)hipGraphExecDestroy(iterGraph);
@@ -848,78 +872,174 @@ int okvisgpu_get_params(okvisgpu_ctx* c) {
   });
 }
 
-int okvisgpu_solve(okvisgpu_ctx* c, const okvisgpu_options* o, okvisgpu_summary* sums) {
+static int checkSolveOptions(okvisgpu_ctx* c, const okvisgpu_options* o) {
   if (!c || !o) return OKVISGPU_ERR_INVALID_ARGUMENT;
   if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
   if (o->linear_solver != OKVISGPU_DENSE_SCHUR || o->trust_region_strategy != OKVISGPU_DOGLEG)
     return fail(c, OKVISGPU_ERR_UNSUPPORTED, "only DENSE_SCHUR + DOGLEG is implemented on the GPU path");
   if (o->max_num_iterations < 0) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "max_num_iterations < 0");
+  return OKVISGPU_OK;
+}
+
+int okvisgpu_solve_begin(okvisgpu_ctx* c, const okvisgpu_options* o) {
+  const int rc = checkSolveOptions(c, o);
+  if (rc != OKVISGPU_OK) return rc;
   return guarded(c, [&]() {
     HIPCHK(hipSetDevice(c->device));
-    const double t0 = nowS();
-    if (c->structureDirty) {
-      // freeze / unfreeze changed the free set: re-analyse with the caller's current values
-      c->build();
-    }
+    c->solveT0 = nowS();
+    c->opts = *o;
+    c->replays = 0;
+    if (c->structureDirty) c->build();  // freeze / unfreeze changed the free set
     c->setOptions(*o);
     c->dropGraph();  // options are baked into the captured kernel arguments
     c->uploadParams();
     c->resetStates(1e-8);
     c->launchInit(2);
     c->ensureGraph();
-    const bool timed = o->time_limit_s >= 0.0;
-    int replays = 0;
-    const int maxReplays = std::max(1, o->max_num_iterations) * 8 + 8;
-    double iterStart = nowS();
-    if (!timed) {
-      for (int k = 0; k < o->max_num_iterations; ++k) HIPCHK(hipGraphLaunch(c->iterGraph, c->stream));
-      replays = o->max_num_iterations;
-    }
+    c->inSolve = true;
+    return (int)OKVISGPU_OK;
+  });
+}
+
+int okvisgpu_solve_iterate(okvisgpu_ctx* c, int32_t n) {
+  if (!c || n < 0) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  if (!c->inSolve) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "solve_iterate without solve_begin");
+  return guarded(c, [&]() {
+    for (int k = 0; k < n; ++k) HIPCHK(hipGraphLaunch(c->iterGraph, c->stream));
+    c->replays += n;
+    return (int)OKVISGPU_OK;
+  });
+}
+
+int okvisgpu_synchronize(okvisgpu_ctx* c) {
+  if (!c) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  return guarded(c, [&]() {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return (int)OKVISGPU_OK;
+  });
+}
+
+int okvisgpu_solve_end(okvisgpu_ctx* c, okvisgpu_summary* sums) {
+  if (!c) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  if (!c->inSolve) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "solve_end without solve_begin");
+  return guarded(c, [&]() {
+    const okvisgpu_options& o = c->opts;
+    const int maxReplays = std::max(1, o.max_num_iterations) * 8 + 8;
     std::vector<WinState> st = c->readStates();
-    while (true) {
+    // windows that consumed passes on mu-retries (ComputeGaussNewtonStep loop) finish here
+    while (c->replays < maxReplays) {
       bool allDone = true;
       for (auto& s : st) allDone = allDone && s.done;
-      if (allDone || replays >= maxReplays) break;
-      if (timed) {
-        // CeresIterationCallback (CeresIterationCallback.cpp:30-38): stop once the next iteration
-        // would exceed the budget, after the minimum number of iterations.
-        const double now = nowS();
-        const double iterTime = now - iterStart, cum = now - t0;
-        bool changed = false;
-        for (auto& s : st)
-          if (!s.done && replays > 0 && s.iteration >= o->min_iterations && cum + iterTime > o->time_limit_s) {
-            s.done = 1;
-            s.termination = OKVISGPU_USER_SUCCESS;
-            changed = true;
-          }
-        if (changed) {
-          HIPCHK(hipMemcpyAsync(c->P.st, st.data(), sizeof(WinState) * st.size(), hipMemcpyHostToDevice, c->stream));
-          continue;
-        }
-        iterStart = nowS();
-      }
+      if (allDone) break;
       HIPCHK(hipGraphLaunch(c->iterGraph, c->stream));
-      ++replays;
+      ++c->replays;
       st = c->readStates();
     }
     c->downloadParams(st);
-    const double t1 = nowS();
-    if (sums) {
-      for (int w = 0; w < c->P.n_win; ++w) {
-        const WinState& s = st[w];
-        okvisgpu_summary& S = sums[w];
-        std::memset(&S, 0, sizeof(S));
-        S.initial_cost = s.initial_cost;
-        S.final_cost = std::min(s.min_cost, s.x_cost) + s.fixed_cost;
-        S.num_iterations = s.iteration;
-        S.num_successful_steps = s.num_succ + 1;
-        S.num_unsuccessful_steps = s.num_unsucc;
-        S.termination_type = s.done ? s.termination : OKVISGPU_NO_CONVERGENCE;
-        S.total_time_s = t1 - t0;
-        S.final_radius = s.radius;
-        S.final_mu = s.mu;
+    c->inSolve = false;
+    c->fillSummaries(st, sums);
+    return (int)OKVISGPU_OK;
+  });
+}
+
+int okvisgpu_solve(okvisgpu_ctx* c, const okvisgpu_options* o, okvisgpu_summary* sums) {
+  int rc = okvisgpu_solve_begin(c, o);
+  if (rc != OKVISGPU_OK) return rc;
+  if (o->time_limit_s < 0.0) {
+    rc = okvisgpu_solve_iterate(c, o->max_num_iterations);
+    if (rc != OKVISGPU_OK) return rc;
+    return okvisgpu_solve_end(c, sums);
+  }
+  // CeresIterationCallback (CeresIterationCallback.cpp:30-38): after the minimum number of
+  // iterations, stop once the next iteration would exceed the time budget.
+  return guarded(c, [&]() {
+    std::vector<WinState> st = c->readStates();
+    double iterStart = nowS();
+    const int maxReplays = std::max(1, o->max_num_iterations) * 8 + 8;
+    while (c->replays < maxReplays) {
+      bool allDone = true;
+      for (auto& s : st) allDone = allDone && s.done;
+      if (allDone) break;
+      const double now = nowS();
+      const double iterTime = now - iterStart, cum = now - c->solveT0;
+      bool changed = false;
+      for (auto& s : st)
+        if (!s.done && c->replays > 0 && s.iteration >= o->min_iterations && cum + iterTime > o->time_limit_s) {
+          s.done = 1;
+          s.termination = OKVISGPU_USER_SUCCESS;
+          changed = true;
+        }
+      if (changed) {
+        HIPCHK(hipMemcpyAsync(c->P.st, st.data(), sizeof(WinState) * st.size(), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        continue;
       }
+      iterStart = nowS();
+      HIPCHK(hipGraphLaunch(c->iterGraph, c->stream));
+      ++c->replays;
+      st = c->readStates();
     }
+    c->downloadParams(st);
+    c->inSolve = false;
+    c->fillSummaries(st, sums);
+    return (int)OKVISGPU_OK;
+  });
+}
+
+static const char* kPhaseNames[OKVISGPU_N_PHASES] = {
+    "lm_prep", "zero_S", "assemble", "chol_panel", "chol_update", "trsv", "lm_backsub", "gn_finalize",
+    "jv_cauchy", "reduce_cauchy", "dogleg", "jv_step", "reduce_step", "eval_obs", "eval_imu",
+    "eval_priors", "reduce_cand", "lin_blocks", "gradnorm"};
+
+const char* okvisgpu_phase_name(int32_t i) { return (i >= 0 && i < OKVISGPU_N_PHASES) ? kPhaseNames[i] : ""; }
+
+int okvisgpu_profile_iteration(okvisgpu_ctx* c, double* ms) {
+  if (!c || !ms) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  if (!c->inSolve) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "profile_iteration needs solve_begin");
+  return guarded(c, [&]() {
+    const DevProblem& P = c->P;
+    hipStream_t s = c->stream;
+    std::vector<hipEvent_t> ev;
+    std::vector<int> phaseOf;
+    auto mark = [&](int phase) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      HIPCHK(hipEventRecord(e, s));
+      ev.push_back(e);
+      phaseOf.push_back(phase);
+    };
+    mark(-1);
+    launch_lm_prep(P, s); mark(0);
+    launch_zero_S(P, s); mark(1);
+    launch_assemble(P, s); mark(2);
+    for (int k = 0; k < P.max_tiles; ++k) {
+      launch_chol_panel(P, k, s); mark(3);
+      launch_chol_update(P, k, s); mark(4);
+    }
+    launch_trsv(P, s); mark(5);
+    launch_lm_backsub(P, s); mark(6);
+    launch_gn_finalize(P, s); mark(7);
+    launch_jv(P, R_JV_CAUCHY, s); mark(8);
+    launch_reduce(P, R_JV_CAUCHY, s); mark(9);
+    launch_dogleg(P, s); mark(10);
+    launch_jv(P, R_JV_STEP, s); mark(11);
+    launch_reduce(P, R_JV_STEP, s); mark(12);
+    launch_eval_obs(P, 1, s); mark(13);
+    launch_eval_imu(P, 1, s); mark(14);
+    launch_eval_priors(P, 1, s); mark(15);
+    launch_reduce(P, R_COST_CAND, s); mark(16);
+    launch_linearization_blocks(P, 1, s); mark(17);
+    launch_gradnorm(P, 1, s); mark(18);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    for (int i = 0; i < OKVISGPU_N_PHASES; ++i) ms[i] = 0.0;
+    for (size_t i = 1; i < ev.size(); ++i) {
+      float t = 0.f;
+      HIPCHK(hipEventElapsedTime(&t, ev[i - 1], ev[i]));
+      ms[phaseOf[i]] += t;
+    }
+    for (auto e : ev) (void)hipEventDestroy(e);
+    c->replays += 1;
     return (int)OKVISGPU_OK;
   });
 }

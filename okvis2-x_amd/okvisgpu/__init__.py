@@ -100,7 +100,10 @@ EXPORTED_SYMBOLS = [
     "okvisgpu_linearize_reduce", "okvisgpu_eval_reprojection", "okvisgpu_eval_imu",
     "okvisgpu_synth_default_config", "okvisgpu_synth_create", "okvisgpu_synth_problem",
     "okvisgpu_synth_ground_truth", "okvisgpu_synth_reset", "okvisgpu_synth_destroy",
+    "okvisgpu_solve_begin", "okvisgpu_solve_iterate", "okvisgpu_solve_end", "okvisgpu_synchronize",
+    "okvisgpu_profile_iteration", "okvisgpu_phase_name",
 ]
+N_PHASES = 19
 
 _lib = None
 
@@ -135,6 +138,13 @@ def lib():
         L.okvisgpu_synth_ground_truth.argtypes = [C.c_void_p, _dp, _dp, _dp]
         L.okvisgpu_synth_reset.argtypes = [C.c_void_p]
         L.okvisgpu_synth_destroy.argtypes = [C.c_void_p]
+        L.okvisgpu_solve_begin.argtypes = [C.c_void_p, C.POINTER(Options)]
+        L.okvisgpu_solve_iterate.argtypes = [C.c_void_p, C.c_int32]
+        L.okvisgpu_solve_end.argtypes = [C.c_void_p, C.POINTER(Summary)]
+        L.okvisgpu_synchronize.argtypes = [C.c_void_p]
+        L.okvisgpu_profile_iteration.argtypes = [C.c_void_p, _dp]
+        L.okvisgpu_phase_name.argtypes = [C.c_int32]
+        L.okvisgpu_phase_name.restype = C.c_char_p
         _lib = L
     return _lib
 
@@ -248,6 +258,26 @@ class Context:
         sums = (Summary * n_windows)()
         self._check(lib().okvisgpu_solve(self.h, C.byref(o), sums), "okvisgpu_solve")
         return [s.as_dict() for s in sums]
+
+    def solve_begin(self, options: Options):
+        self._opts = options
+        self._check(lib().okvisgpu_solve_begin(self.h, C.byref(options)), "okvisgpu_solve_begin")
+
+    def solve_iterate(self, n: int):
+        self._check(lib().okvisgpu_solve_iterate(self.h, n), "okvisgpu_solve_iterate")
+
+    def synchronize(self):
+        self._check(lib().okvisgpu_synchronize(self.h), "okvisgpu_synchronize")
+
+    def solve_end(self, n_windows: int = 1):
+        sums = (Summary * n_windows)()
+        self._check(lib().okvisgpu_solve_end(self.h, sums), "okvisgpu_solve_end")
+        return [s.as_dict() for s in sums]
+
+    def profile_iteration(self):
+        ms = np.zeros(N_PHASES)
+        self._check(lib().okvisgpu_profile_iteration(self.h, dptr(ms)), "okvisgpu_profile_iteration")
+        return {lib().okvisgpu_phase_name(i).decode(): float(ms[i]) for i in range(N_PHASES)}
 
     def get_params(self):
         self._check(lib().okvisgpu_get_params(self.h), "okvisgpu_get_params")
