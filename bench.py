@@ -97,7 +97,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--windows", type=int, default=64, help="total windows in the job (strong scaling)")
+    ap.add_argument("--windows", type=int, default=512, help="total windows in the job (strong scaling)")
     ap.add_argument("--config", default="s50", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-threads", type=int, default=3, help="realtime_num_threads (okvis2.yaml:93)")
     ap.add_argument("--cpu-iters", type=int, default=None, help="default: warmup + steps")
@@ -202,6 +202,14 @@ def main():
                                        "final_cost": s1["final_cost"]}
             gpu_pose_w0 = w1[0].poses().copy()
             gt_p, _, _ = w1[0].ground_truth()
+            if not args.no_profile:
+                w1[0].reset()
+                c1.update_params()
+                c1.solve_begin(opts)
+                c1.solve_iterate(args.warmup)
+                ph1 = c1.profile_iteration()
+                c1.solve_end(1)
+                result["single_window"]["kernel_ms_per_iteration"] = {k: round(v, 4) for k, v in ph1.items()}
             c1.close()
         # ---- per-kernel device time of one iteration + roofline of the dominant kernel
         if not args.no_profile:

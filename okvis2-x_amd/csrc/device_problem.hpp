@@ -68,6 +68,7 @@ struct DevOptions {
 };
 
 struct DevProblem {
+  const DevProblem* self;          // device-resident copy of this descriptor (what kernels receive)
   int32_t n_win, n_pose, n_sb, n_lm, n_obs, n_visit, n_imu, n_pprior, n_sbprior, n_cam;
   int32_t n_fblock, n_pair;
   int32_t max_fpad, max_tiles;     // largest padded reduced dimension / its 64-tile count
@@ -109,11 +110,13 @@ struct DevProblem {
   const int32_t* visit_lm;         // [n_visit]
   double* lm_V;                    // [n_lm][6]  sum J_l^T J_l (unscaled, sym packed 00 01 02 11 12 22)
   double* lm_g;                    // [n_lm][3]  J_l^T r
-  double* lm_Vinv;                 // [n_lm][6]  (s V s + D^2)^-1
+  double* lm_Vinv;                 // [n_lm][9]  (s V s + D^2)^-1
   double* lm_z;                    // [n_lm][3]  Vinv (s g)
   double* visit_W;                 // [n_visit][18] J_p^T J_l (unscaled)
   double* visit_H;                 // [n_visit][21] J_p^T J_p (unscaled, sym packed)
   double* visit_g;                 // [n_visit][6]  J_p^T r
+  double* visit_UY;                // [n_visit][36] U = s_p W s_l (6x3) | Y = U Vinv (6x3)   (per GN solve)
+  double* visit_uz;                // [n_visit][6]  U z
 
   // --- IMU factors
   const int32_t* imu_blocks;       // [n_imu][4] global pose0 sb0 pose1 sb1
@@ -172,6 +175,21 @@ struct DevProblem {
 
   // --- f-vectors (window-concatenated, reduced ordering) and landmark vectors
   double* S;                       // sum over windows fpad^2
+  double* Linv;                    // per window (fpad/64) inverses of the 64x64 diagonal factors
+  const int64_t* win_linvoff;      // [n_win] offset into Linv
+  // tile-level symbolic factorisation (host analysis): the reduced camera matrix of a sliding
+  // window is block-banded and LLT creates no fill outside its envelope, so only structurally
+  // non-zero 64x64 tiles are zeroed, factored and updated (bitwise identical to the dense LLT).
+  const int32_t* chol_panel_items;   // (w, i) pairs; panel k items in [chol_panel_begin[k], ...[k+1])
+  const int32_t* chol_panel_begin;   // [max_tiles + 1]
+  const int32_t* chol_upd_items;     // (w, i, j) triples for the trailing update of panel k
+  const int32_t* chol_upd_begin;     // [max_tiles + 1]
+  const int32_t* tile_items;         // (w, i, j) every structurally non-zero tile (i >= j)
+  int32_t n_tiles;
+  const int32_t* h_panel_begin;      // host copies of the begin arrays (launch sizes)
+  const int32_t* h_upd_begin;
+  double* fwdF;                    // per window fpad: forward-substitution work vector
+  const int64_t* win_fwdoff;       // [n_win] offset into fwdF
   double* sF;   double* sL;        // Jacobi scaling (fixed at iteration 0)
   double* diagF; double* diagL;    // dogleg diagonal_
   double* hdF;                     // unscaled diag(H_ff)

@@ -54,7 +54,8 @@ __device__ __forceinline__ bool jvSelect(const DevProblem& P, int w, int mode) {
   return s.step_valid == 2;
 }
 
-__global__ __launch_bounds__(256) void k_jv(DevProblem P, int mode) {
+__global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp, int mode) {
+  const DevProblem& P = *Pp;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const double* vF = (mode == R_JV_CAUCHY) ? P.vF : P.stepF;
   const double* vL = (mode == R_JV_CAUCHY) ? P.vL : P.stepL;
@@ -175,7 +176,8 @@ __device__ void finalizeIteration(const DevProblem& P, WinState& s) {
   }
 }
 
-__global__ __launch_bounds__(kRB) void k_reduce(DevProblem P, int mode) {
+__global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ Pp, int mode) {
+  const DevProblem& P = *Pp;
   const int w = blockIdx.x;
   WinState& s = P.st[w];
   if (s.done) return;
@@ -312,7 +314,8 @@ __global__ __launch_bounds__(kRB) void k_reduce(DevProblem P, int mode) {
 }
 
 // |x - Plus(x, -g)| and |x| over the window's active blocks; gradient tolerance test.
-__global__ __launch_bounds__(kRB) void k_gradnorm(DevProblem P, int lin_mode) {
+__global__ __launch_bounds__(kRB) void k_gradnorm(const DevProblem* __restrict__ Pp, int lin_mode) {
+  const DevProblem& P = *Pp;
   const int w = blockIdx.x;
   WinState& s = P.st[w];
   if (s.done) return;
@@ -388,7 +391,8 @@ __global__ __launch_bounds__(kRB) void k_gradnorm(DevProblem P, int lin_mode) {
 }
 
 // One workgroup per window: GN failure handling, traditional dogleg step, Plus into X[1-xcur].
-__global__ __launch_bounds__(kRB) void k_dogleg(DevProblem P) {
+__global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
   const int w = blockIdx.x;
   WinState& s = P.st[w];
   if (s.done) return;
@@ -539,16 +543,16 @@ __global__ __launch_bounds__(kRB) void k_dogleg(DevProblem P) {
 
 void launch_jv(const DevProblem& P, int mode, hipStream_t s) {
   const int n = P.n_obs + P.n_imu + P.n_pprior + P.n_sbprior;
-  if (n > 0) hipLaunchKernelGGL(k_jv, dim3((n + 255) / 256), dim3(256), 0, s, P, mode);
+  if (n > 0) hipLaunchKernelGGL(k_jv, dim3((n + 255) / 256), dim3(256), 0, s, P.self, mode);
 }
 void launch_reduce(const DevProblem& P, int mode, hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce, dim3(P.n_win), dim3(kRB), 0, s, P, mode);
+  hipLaunchKernelGGL(k_reduce, dim3(P.n_win), dim3(kRB), 0, s, P.self, mode);
 }
 void launch_gradnorm(const DevProblem& P, int lin_mode, hipStream_t s) {
-  hipLaunchKernelGGL(k_gradnorm, dim3(P.n_win), dim3(kRB), 0, s, P, lin_mode);
+  hipLaunchKernelGGL(k_gradnorm, dim3(P.n_win), dim3(kRB), 0, s, P.self, lin_mode);
 }
 void launch_dogleg(const DevProblem& P, hipStream_t s) {
-  hipLaunchKernelGGL(k_dogleg, dim3(P.n_win), dim3(kRB), 0, s, P);
+  hipLaunchKernelGGL(k_dogleg, dim3(P.n_win), dim3(kRB), 0, s, P.self);
 }
 
 }  // namespace okg

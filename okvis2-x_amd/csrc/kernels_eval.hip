@@ -41,7 +41,8 @@ __device__ __forceinline__ bool evalSelect(const DevProblem& P, int w, int mode,
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_eval_obs(DevProblem P, int mode) {
+__global__ __launch_bounds__(256) void k_eval_obs(const DevProblem* __restrict__ Pp, int mode) {
+  const DevProblem& P = *Pp;
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= P.n_obs) return;
   const int w = P.obs_win[o];
@@ -251,7 +252,8 @@ __device__ void jacobiEigen16(double* A, double* V, double* rot, int lane) {
 
 }  // namespace
 
-__global__ __launch_bounds__(64) void k_eval_imu(DevProblem P, int mode) {
+__global__ __launch_bounds__(64) void k_eval_imu(const DevProblem* __restrict__ Pp, int mode) {
+  const DevProblem& P = *Pp;
   const int f = blockIdx.x;
   if (f >= P.n_imu) return;
   const int w = P.imu_win[f];
@@ -622,7 +624,8 @@ __global__ __launch_bounds__(64) void k_eval_imu(DevProblem P, int mode) {
 }
 
 // ------------------------------------------------------------------------------------ priors
-__global__ __launch_bounds__(64) void k_eval_priors(DevProblem P, int mode) {
+__global__ __launch_bounds__(64) void k_eval_priors(const DevProblem* __restrict__ Pp, int mode) {
+  const DevProblem& P = *Pp;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t < P.n_pprior) {
     const int i = t;
@@ -683,14 +686,14 @@ __global__ __launch_bounds__(64) void k_eval_priors(DevProblem P, int mode) {
 
 // ------------------------------------------------------------------------------------ launchers
 void launch_eval_obs(const DevProblem& P, int mode, hipStream_t s) {
-  if (P.n_obs > 0) hipLaunchKernelGGL(k_eval_obs, dim3((P.n_obs + 255) / 256), dim3(256), 0, s, P, mode);
+  if (P.n_obs > 0) hipLaunchKernelGGL(k_eval_obs, dim3((P.n_obs + 255) / 256), dim3(256), 0, s, P.self, mode);
 }
 void launch_eval_imu(const DevProblem& P, int mode, hipStream_t s) {
-  if (P.n_imu > 0) hipLaunchKernelGGL(k_eval_imu, dim3(P.n_imu), dim3(64), 0, s, P, mode);
+  if (P.n_imu > 0) hipLaunchKernelGGL(k_eval_imu, dim3(P.n_imu), dim3(64), 0, s, P.self, mode);
 }
 void launch_eval_priors(const DevProblem& P, int mode, hipStream_t s) {
   const int np = P.n_pprior + P.n_sbprior;
-  if (np > 0) hipLaunchKernelGGL(k_eval_priors, dim3((np + 63) / 64), dim3(64), 0, s, P, mode);
+  if (np > 0) hipLaunchKernelGGL(k_eval_priors, dim3((np + 63) / 64), dim3(64), 0, s, P.self, mode);
 }
 void launch_eval(const DevProblem& P, int mode, hipStream_t s) {
   launch_eval_obs(P, mode, s);

@@ -40,7 +40,8 @@ __device__ __forceinline__ bool linSelect(const DevProblem& P, int w, int lin_mo
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_lm_blocks(DevProblem P, int lin_mode) {
+__global__ __launch_bounds__(256) void k_lm_blocks(const DevProblem* __restrict__ Pp, int lin_mode) {
+  const DevProblem& P = *Pp;
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= P.n_lm) return;
   const int w = P.lm_win[l];
@@ -110,20 +111,26 @@ __device__ __forceinline__ const double* imuLin(const DevProblem& P, int lb, int
   return P.imu_lin[lb] + (size_t)f * kImuLin;
 }
 
-__global__ __launch_bounds__(64) void k_fgrad(DevProblem P, int lin_mode) {
-  const int fb = blockIdx.x * blockDim.x + threadIdx.x;
+// One wavefront per f-block: lanes stride over the contribution list, then a fixed xor-tree
+// reduction (deterministic).
+__global__ __launch_bounds__(64) void k_fgrad(const DevProblem* __restrict__ Pp, int lin_mode) {
+  const DevProblem& P = *Pp;
+  const int fb = blockIdx.x;
   if (fb >= P.n_fblock) return;
   const int w = P.fb_win[fb];
   if (!linSelect(P, w, lin_mode)) return;
+  const int lane = threadIdx.x;
   const int lb = P.st[w].lcur;
   const int n = P.fb_kind[fb] == 0 ? 6 : 9;
   double g[9], hd[9];
+#pragma unroll
   for (int c = 0; c < 9; ++c) { g[c] = 0.0; hd[c] = 0.0; }
-  for (int k = P.fb_cbegin[fb]; k < P.fb_cbegin[fb + 1]; ++k) {
+  for (int k = P.fb_cbegin[fb] + lane; k < P.fb_cbegin[fb + 1]; k += 64) {
     const Contrib cb = P.fb_contrib[k];
     if (cb.type == C_VISIT) {
       const double* H = P.visit_H + 21 * (size_t)cb.a;
       const double* gp = P.visit_g + 6 * (size_t)cb.a;
+#pragma unroll
       for (int c = 0; c < 6; ++c) { g[c] += gp[c]; hd[c] += H[sym6(c, c)]; }
     } else if (cb.type == C_IMU) {
       const double* L = imuLin(P, lb, cb.a);
@@ -163,6 +170,14 @@ __global__ __launch_bounds__(64) void k_fgrad(DevProblem P, int lin_mode) {
       }
     }
   }
+#pragma unroll
+  for (int c = 0; c < 9; ++c)
+#pragma unroll
+    for (int sh = 32; sh > 0; sh >>= 1) {
+      g[c] += __shfl_xor(g[c], sh, 64);
+      hd[c] += __shfl_xor(hd[c], sh, 64);
+    }
+  if (lane != 0) return;
   const size_t base = (size_t)P.win_foff[w] + P.fb_off[fb];
   for (int c = 0; c < n; ++c) {
     P.gF[base + c] = g[c];
@@ -176,7 +191,8 @@ __device__ __forceinline__ bool gnSelect(const DevProblem& P, int w) {
   return !s.done && s.need_gn && !s.gn_failed;
 }
 
-__global__ __launch_bounds__(256) void k_lm_prep(DevProblem P) {
+__global__ __launch_bounds__(256) void k_lm_prep(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= P.n_lm) return;
   if (!P.lm_free[l]) return;
@@ -234,28 +250,58 @@ __global__ __launch_bounds__(256) void k_lm_prep(DevProblem P) {
   double sg[3] = {s[0] * g[0], s[1] * g[1], s[2] * g[2]};
   double* Vi = P.lm_Vinv + 9 * (size_t)l;
   for (int i = 0; i < 9; ++i) Vi[i] = inv[i];
-  for (int a = 0; a < 3; ++a)
-    P.lm_z[3 * (size_t)l + a] = inv[a * 3 + 0] * sg[0] + inv[a * 3 + 1] * sg[1] + inv[a * 3 + 2] * sg[2];
-}
-
-__global__ __launch_bounds__(256) void k_zero_S(DevProblem P) {
-  const int w = blockIdx.y;
-  if (!gnSelect(P, w)) return;
-  const int fpad = P.win_fpad[w], fdim = P.win_fdim[w];
-  const int64_t n = (int64_t)fpad * fpad;
-  double* S = P.S + P.win_soff[w];
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-    const int r = (int)(e / fpad), c = (int)(e % fpad);
-    if (c > r) continue;
-    S[e] = (r == c && r >= fdim) ? 1.0 : 0.0;
+  double z[3];
+  for (int a = 0; a < 3; ++a) {
+    z[a] = inv[a * 3 + 0] * sg[0] + inv[a * 3 + 1] * sg[1] + inv[a * 3 + 2] * sg[2];
+    P.lm_z[3 * (size_t)l + a] = z[a];
+  }
+  // per visit (free pose): U = s_p W s_l, Y = U Vinv, uz = U z — the operands of the Schur terms
+  const int foff = P.win_foff[w];
+  for (int v = P.lm_visit_begin[l]; v < P.lm_visit_begin[l + 1]; ++v) {
+    const int pf = P.pose_f[P.visit_pose[v]];
+    if (pf < 0) continue;
+    const double* W = P.visit_W + 18 * (size_t)v;
+    double* UY = P.visit_UY + 36 * (size_t)v;
+    double* uz = P.visit_uz + 6 * (size_t)v;
+    for (int r = 0; r < 6; ++r) {
+      const double sp = P.sF[(size_t)foff + pf + r];
+      const double u0 = sp * W[r * 3 + 0] * s[0], u1 = sp * W[r * 3 + 1] * s[1], u2 = sp * W[r * 3 + 2] * s[2];
+      UY[r * 3 + 0] = u0; UY[r * 3 + 1] = u1; UY[r * 3 + 2] = u2;
+      for (int b = 0; b < 3; ++b) UY[18 + r * 3 + b] = u0 * inv[0 * 3 + b] + u1 * inv[1 * 3 + b] + u2 * inv[2 * 3 + b];
+      uz[r] = u0 * z[0] + u1 * z[1] + u2 * z[2];
+    }
   }
 }
 
-__global__ __launch_bounds__(128) void k_assemble(DevProblem P) {
+// Clears the structurally non-zero tiles of S (one workgroup per tile; padded diagonal = 1). Zero
+// tiles are never written by the factorisation and stay zero from the initial arena clear.
+__global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
+  const int item = blockIdx.x;
+  const int w = P.tile_items[3 * item], ti = P.tile_items[3 * item + 1], tj = P.tile_items[3 * item + 2];
+  if (!gnSelect(P, w)) return;
+  const int fpad = P.win_fpad[w], fdim = P.win_fdim[w];
+  double* S = P.S + P.win_soff[w];
+  for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
+    const int r = ti * kTile + (e >> 6), c = tj * kTile + (e & 63);
+    S[(int64_t)r * fpad + c] = (r == c && r >= fdim) ? 1.0 : 0.0;
+  }
+}
+
+// One workgroup per non-zero f-block pair; contributions are processed in chunks of 64 whose
+// operands (visit H / uz, or the Y_i, U_j pair of a landmark) are first staged into LDS with
+// coalesced loads, so the per-entry accumulation reads only LDS (no dependent global chains).
+constexpr int kChunk = 64;
+constexpr int kStage = 36;
+
+__global__ __launch_bounds__(128) void k_assemble(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
   const int k = blockIdx.x;
   if (k >= P.n_pair) return;
   const int w = P.pair_win[k];
   if (!gnSelect(P, w)) return;
+  __shared__ double stage[kChunk * kStage];
+  __shared__ Contrib sc[kChunk];
   const int lb = P.st[w].lcur;
   const double mu = P.st[w].mu;
   const int fi = P.pair_fi[k], fj = P.pair_fj[k];
@@ -264,43 +310,62 @@ __global__ __launch_bounds__(128) void k_assemble(DevProblem P) {
   const int offi = P.fb_off[fi], offj = P.fb_off[fj];
   const int t = threadIdx.x;
   const int cb = P.pair_cbegin[k], ce = P.pair_cbegin[k + 1];
-  if (t < ni * nj) {
-    const int r = t / nj, c = t % nj;
-    double H = 0.0, schur = 0.0;
-    for (int q = cb; q < ce; ++q) {
-      const Contrib C = P.pair_contrib[q];
-      if (C.type == C_VISIT) {
-        H += P.visit_H[21 * (size_t)C.a + sym6(r, c)];
-      } else if (C.type == C_PAIR) {
-        const int l = P.visit_lm[C.a];
-        const double* sl = P.sL + 3 * (size_t)l;
-        const double* Vi = P.lm_Vinv + 9 * (size_t)l;
-        const double* wi = P.visit_W + 18 * (size_t)C.a + 3 * r;
-        const double* wj = P.visit_W + 18 * (size_t)C.b + 3 * c;
-        const double a0 = wi[0] * sl[0], a1 = wi[1] * sl[1], a2 = wi[2] * sl[2];
-        const double b0 = wj[0] * sl[0], b1 = wj[1] * sl[1], b2 = wj[2] * sl[2];
-        schur += a0 * (Vi[0] * b0 + Vi[1] * b1 + Vi[2] * b2) + a1 * (Vi[3] * b0 + Vi[4] * b1 + Vi[5] * b2) +
-                 a2 * (Vi[6] * b0 + Vi[7] * b1 + Vi[8] * b2);
+  const bool entry = t < ni * nj;
+  const int r = entry ? t / nj : 0, c = entry ? t % nj : 0;
+  const bool diag = (fi == fj);
+  double H = 0.0, schur = 0.0, uzacc = 0.0;
+  for (int c0 = cb; c0 < ce; c0 += kChunk) {
+    const int nc = min(kChunk, ce - c0);
+    __syncthreads();
+    if (t < nc) sc[t] = P.pair_contrib[c0 + t];
+    __syncthreads();
+    for (int e = t; e < nc * kStage; e += 128) {
+      const int q = e / kStage, x = e - q * kStage;
+      const Contrib C = sc[q];
+      double v = 0.0;
+      if (C.type == C_PAIR) v = (x < 18) ? P.visit_UY[36 * (size_t)C.a + 18 + x] : P.visit_UY[36 * (size_t)C.b + x - 18];
+      else if (C.type == C_VISIT) v = (x < 21) ? P.visit_H[21 * (size_t)C.a + x]
+                                    : (x < 27 && C.b) ? P.visit_uz[6 * (size_t)C.a + x - 21] : 0.0;
+      stage[e] = v;
+    }
+    __syncthreads();
+    for (int q = 0; q < nc; ++q) {
+      const Contrib C = sc[q];  // uniform across the workgroup
+      const double* st = stage + q * kStage;
+      if (C.type == C_PAIR) {
+        if (entry) schur += st[r * 3 + 0] * st[18 + c * 3 + 0] + st[r * 3 + 1] * st[18 + c * 3 + 1] +
+                            st[r * 3 + 2] * st[18 + c * 3 + 2];
+      } else if (C.type == C_VISIT) {
+        if (entry) H += st[sym6(r, c)];
+        if (diag && t < ni) uzacc += st[21 + t];
       } else if (C.type == C_IMU) {
-        const double* L = imuLin(P, lb, C.a) + 15;
-        double s = 0;
-        for (int k2 = 0; k2 < 15; ++k2) s += L[k2 * 30 + C.b + r] * L[k2 * 30 + C.c + c];
-        H += s;
+        if (entry) {
+          const double* L = imuLin(P, lb, C.a) + 15;
+          double s2 = 0;
+          for (int k2 = 0; k2 < 15; ++k2) s2 += L[k2 * 30 + C.b + r] * L[k2 * 30 + C.c + c];
+          H += s2;
+        }
       } else if (C.type == C_PPRIOR) {
-        const double* L = P.pp_lin[lb] + 42 * (size_t)C.a + 6;
-        double s = 0;
-        for (int k2 = 0; k2 < 6; ++k2) s += L[k2 * 6 + r] * L[k2 * 6 + c];
-        H += s;
+        if (entry) {
+          const double* L = P.pp_lin[lb] + 42 * (size_t)C.a + 6;
+          double s2 = 0;
+          for (int k2 = 0; k2 < 6; ++k2) s2 += L[k2 * 6 + r] * L[k2 * 6 + c];
+          H += s2;
+        }
       } else if (C.type == C_SBPRIOR) {
-        const double* L = P.sbp_lin[lb] + 90 * (size_t)C.a + 9;
-        double s = 0;
-        for (int k2 = 0; k2 < 9; ++k2) s += L[k2 * 9 + r] * L[k2 * 9 + c];
-        H += s;
+        if (entry) {
+          const double* L = P.sbp_lin[lb] + 90 * (size_t)C.a + 9;
+          double s2 = 0;
+          for (int k2 = 0; k2 < 9; ++k2) s2 += L[k2 * 9 + r] * L[k2 * 9 + c];
+          H += s2;
+        }
       }
     }
+  }
+  if (entry) {
     const double si = P.sF[(size_t)foff + offi + r], sj = P.sF[(size_t)foff + offj + c];
-    double val = si * sj * H - si * sj * schur;
-    if (fi == fj && r == c) {
+    double val = si * sj * H - schur;
+    if (diag && r == c) {
       const double dg = sqrt(fmin(fmax(si * si * P.hdF[(size_t)foff + offi + r], P.opt.min_lm_diagonal),
                                   P.opt.max_lm_diagonal));
       P.diagF[(size_t)foff + offi + r] = dg;
@@ -309,26 +374,15 @@ __global__ __launch_bounds__(128) void k_assemble(DevProblem P) {
     }
     P.S[P.win_soff[w] + (int64_t)(offi + r) * P.win_fpad[w] + offj + c] = val;
   }
-  if (fi == fj && t < ni) {
-    // Schur rhs: s_i (g_i - sum_visits W (s_l z_l))
-    const int r = t;
-    double acc = 0.0;
-    for (int q = cb; q < ce; ++q) {
-      const Contrib C = P.pair_contrib[q];
-      if (C.type == C_VISIT && C.b) {
-        const int l = P.visit_lm[C.a];
-        const double* sl = P.sL + 3 * (size_t)l;
-        const double* z = P.lm_z + 3 * (size_t)l;
-        const double* wr = P.visit_W + 18 * (size_t)C.a + 3 * r;
-        acc += wr[0] * sl[0] * z[0] + wr[1] * sl[1] * z[1] + wr[2] * sl[2] * z[2];
-      }
-    }
-    const size_t idx = (size_t)foff + offi + r;
-    P.rhsF[idx] = P.sF[idx] * P.gF[idx] - P.sF[idx] * acc;
+  if (diag && t < ni) {
+    // Schur rhs: s_i g_i - sum_visits U_v z_l
+    const size_t idx = (size_t)foff + offi + t;
+    P.rhsF[idx] = P.sF[idx] * P.gF[idx] - uzacc;
   }
 }
 
-__global__ __launch_bounds__(256) void k_lm_backsub(DevProblem P) {
+__global__ __launch_bounds__(256) void k_lm_backsub(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= P.n_lm) return;
   if (!P.lm_free[l]) return;
@@ -341,11 +395,10 @@ __global__ __launch_bounds__(256) void k_lm_backsub(DevProblem P) {
   for (int v = P.lm_visit_begin[l]; v < P.lm_visit_begin[l + 1]; ++v) {
     const int pf = P.pose_f[P.visit_pose[v]];
     if (pf < 0) continue;
-    const double* W = P.visit_W + 18 * (size_t)v;
+    const double* U = P.visit_UY + 36 * (size_t)v;  // U = s_p W s_l
     for (int rr = 0; rr < 6; ++rr) {
-      const size_t idx = (size_t)foff + pf + rr;
-      const double sy = P.sF[idx] * P.yF[idx];
-      for (int a = 0; a < 3; ++a) rhs[a] -= W[rr * 3 + a] * s[a] * sy;
+      const double y = P.yF[(size_t)foff + pf + rr];
+      for (int a = 0; a < 3; ++a) rhs[a] -= U[rr * 3 + a] * y;
     }
   }
   const double* Vi = P.lm_Vinv + 9 * (size_t)l;
@@ -355,7 +408,8 @@ __global__ __launch_bounds__(256) void k_lm_backsub(DevProblem P) {
 
 // gauss_newton_step_ = -diagonal_ .* y ; gradient_ = s .* g / diagonal_ ; v = gradient_ / diagonal_
 // (DoglegStrategy::ComputeGradient / ComputeCauchyPoint / ComputeGaussNewtonStep)
-__global__ __launch_bounds__(256) void k_gn_finalize(DevProblem P) {
+__global__ __launch_bounds__(256) void k_gn_finalize(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t < P.n_fblock) {
     const int w = P.fb_win[t];
@@ -388,23 +442,23 @@ __global__ __launch_bounds__(256) void k_gn_finalize(DevProblem P) {
 
 // ------------------------------------------------------------------------------------ launchers
 void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
-  if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_blocks, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P, lin_mode);
+  if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_blocks, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P.self, lin_mode);
 }
 void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s) {
-  if (P.n_fblock > 0) hipLaunchKernelGGL(k_fgrad, dim3((P.n_fblock + 63) / 64), dim3(64), 0, s, P, lin_mode);
+  if (P.n_fblock > 0) hipLaunchKernelGGL(k_fgrad, dim3(P.n_fblock), dim3(64), 0, s, P.self, lin_mode);
 }
 void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
   launch_lm_blocks(P, lin_mode, s);
   launch_fgrad(P, lin_mode, s);
 }
 void launch_lm_prep(const DevProblem& P, hipStream_t s) {
-  if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_prep, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P);
+  if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_prep, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P.self);
 }
 void launch_zero_S(const DevProblem& P, hipStream_t s) {
-  if (P.max_fpad > 0) hipLaunchKernelGGL(k_zero_S, dim3(512, P.n_win), dim3(256), 0, s, P);
+  if (P.n_tiles > 0) hipLaunchKernelGGL(k_zero_S, dim3(P.n_tiles), dim3(256), 0, s, P.self);
 }
 void launch_assemble(const DevProblem& P, hipStream_t s) {
-  if (P.n_pair > 0) hipLaunchKernelGGL(k_assemble, dim3(P.n_pair), dim3(128), 0, s, P);
+  if (P.n_pair > 0) hipLaunchKernelGGL(k_assemble, dim3(P.n_pair), dim3(128), 0, s, P.self);
 }
 void launch_gn_reduce(const DevProblem& P, hipStream_t s) {
   launch_lm_prep(P, s);
@@ -412,11 +466,11 @@ void launch_gn_reduce(const DevProblem& P, hipStream_t s) {
   launch_assemble(P, s);
 }
 void launch_lm_backsub(const DevProblem& P, hipStream_t s) {
-  if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_backsub, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P);
+  if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_backsub, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P.self);
 }
 void launch_gn_finalize(const DevProblem& P, hipStream_t s) {
   const int n = P.n_fblock + P.n_lm;
-  if (n > 0) hipLaunchKernelGGL(k_gn_finalize, dim3((n + 255) / 256), dim3(256), 0, s, P);
+  if (n > 0) hipLaunchKernelGGL(k_gn_finalize, dim3((n + 255) / 256), dim3(256), 0, s, P.self);
 }
 void launch_gn_backsub(const DevProblem& P, hipStream_t s) {
   launch_lm_backsub(P, s);

@@ -75,14 +75,17 @@ struct HostBatch {
   std::vector<double> pp_meas, pp_L, sbp_meas, sbp_L;
   // reduced structure
   std::vector<int32_t> win_foff, win_fdim, win_fpad;
-  std::vector<int64_t> win_soff;
+  std::vector<int64_t> win_soff, win_linvoff, win_fwdoff;
   std::vector<int32_t> win_pose_range, win_sb_range, win_lm_range, win_obs_range, win_imu_range, win_pp_range,
       win_sbp_range;
   std::vector<int32_t> fb_win, fb_kind, fb_index, fb_off, fb_cbegin;
   std::vector<Contrib> fb_contrib;
   std::vector<int32_t> pair_win, pair_fi, pair_fj, pair_cbegin;
+  std::vector<int32_t> chol_panel_items, chol_panel_begin, chol_upd_items, chol_upd_begin, tile_items;
   std::vector<Contrib> pair_contrib;
-  int64_t s_total = 0;
+  int64_t s_total = 0, linv_total = 0, fwd_total = 0;
+  std::vector<std::vector<uint8_t>> tileNz;
+  std::vector<int> tileT;
   int f_total = 0;
   int max_fpad = 0;
 };
@@ -215,8 +218,12 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     B.win_fdim.push_back(fo);
     B.win_fpad.push_back(fpad);
     B.win_soff.push_back(B.s_total);
+    B.win_linvoff.push_back(B.linv_total);
+    B.win_fwdoff.push_back(B.fwd_total);
+    B.fwd_total += fpad;
     B.f_total += fo;
     B.s_total += (int64_t)fpad * fpad;
+    B.linv_total += (int64_t)(fpad / kTile) * kTile * kTile;
     B.max_fpad = std::max(B.max_fpad, fpad);
 
     // observations sorted by (landmark, pose, camera, original index)
@@ -389,6 +396,26 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     }
     // diagonal pairs must exist for every f-block (they carry the damping, diag and rhs)
     for (int k = fbBase; k < (int)B.fb_win.size(); ++k) pairs[std::make_pair(k, k)];
+    // tile-level structure of S and its symbolic LLT (fill within the envelope)
+    {
+      const int T = fpad / kTile;
+      std::vector<uint8_t> nz((size_t)T * T, 0);
+      for (int i = 0; i < T; ++i) nz[(size_t)i * T + i] = 1;
+      for (auto& kv : pairs) {
+        const int fa = kv.first.first, fb2 = kv.first.second;
+        const int na = B.fb_kind[fa] == 0 ? 6 : 9, nb = B.fb_kind[fb2] == 0 ? 6 : 9;
+        for (int ti = B.fb_off[fa] / kTile; ti <= (B.fb_off[fa] + na - 1) / kTile; ++ti)
+          for (int tj = B.fb_off[fb2] / kTile; tj <= (B.fb_off[fb2] + nb - 1) / kTile; ++tj)
+            nz[(size_t)std::max(ti, tj) * T + std::min(ti, tj)] = 1;
+      }
+      for (int k = 0; k < T; ++k)
+        for (int i = k + 1; i < T; ++i)
+          if (nz[(size_t)i * T + k])
+            for (int j = k + 1; j <= i; ++j)
+              if (nz[(size_t)j * T + k]) nz[(size_t)i * T + j] = 1;
+      B.tileNz.push_back(nz);
+      B.tileT.push_back(T);
+    }
     for (auto& kv : pairs) {
       B.pair_win.push_back(w);
       B.pair_fi.push_back(kv.first.first);
@@ -396,6 +423,31 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       B.pair_cbegin.push_back((int)B.pair_contrib.size());
       B.pair_contrib.insert(B.pair_contrib.end(), kv.second.begin(), kv.second.end());
     }
+  }
+  // per-panel work lists over the whole batch
+  const int maxT = B.max_fpad / kTile;
+  for (int k = 0; k <= maxT; ++k) {
+    B.chol_panel_begin.push_back((int)B.chol_panel_items.size() / 2);
+    B.chol_upd_begin.push_back((int)B.chol_upd_items.size() / 3);
+    if (k == maxT) break;
+    for (int w = 0; w < B.n_win; ++w) {
+      const int T = B.tileT[w];
+      const auto& nz = B.tileNz[w];
+      for (int i = k + 1; i < T; ++i)
+        if (nz[(size_t)i * T + k]) { B.chol_panel_items.push_back(w); B.chol_panel_items.push_back(i); }
+      for (int i = k + 1; i < T; ++i)
+        if (nz[(size_t)i * T + k])
+          for (int j = k + 1; j <= i; ++j)
+            if (nz[(size_t)j * T + k]) {
+              B.chol_upd_items.push_back(w); B.chol_upd_items.push_back(i); B.chol_upd_items.push_back(j);
+            }
+    }
+  }
+  for (int w = 0; w < B.n_win; ++w) {
+    const int T = B.tileT[w];
+    for (int i = 0; i < T; ++i)
+      for (int j = 0; j <= i; ++j)
+        if (B.tileNz[w][(size_t)i * T + j]) { B.tile_items.push_back(w); B.tile_items.push_back(i); B.tile_items.push_back(j); }
   }
   B.lm_visit_begin.push_back((int)B.visit_pose.size());
   B.visit_obs_begin.push_back((int)B.obs_win.size());
@@ -524,7 +576,8 @@ struct okvisgpu_ctx {
     const size_t o_lmV = scratch(sizeof(double) * 6 * D.n_lm), o_lmg = scratch(sizeof(double) * 3 * D.n_lm),
                  o_lmVi = scratch(sizeof(double) * 9 * D.n_lm), o_lmz = scratch(sizeof(double) * 3 * D.n_lm);
     const size_t o_vW = scratch(sizeof(double) * 18 * D.n_visit), o_vH = scratch(sizeof(double) * 21 * D.n_visit),
-                 o_vg = scratch(sizeof(double) * 6 * D.n_visit);
+                 o_vg = scratch(sizeof(double) * 6 * D.n_visit),
+                 o_vUY = scratch(sizeof(double) * 36 * D.n_visit), o_vuz = scratch(sizeof(double) * 6 * D.n_visit);
     const size_t o_imu_blocks = upl(B.imu_blocks), o_imu_win = upl(B.imu_win), o_imu_flags = upl(B.imu_flags),
                  o_imu_t0 = upl(B.imu_t0), o_imu_t1 = upl(B.imu_t1), o_imu_sb = upl(B.imu_sbegin),
                  o_imu_ts = upl(B.imu_ts), o_imu_ga = upl(B.imu_ga), o_imu_par = upl(B.imu_par),
@@ -545,19 +598,24 @@ struct okvisgpu_ctx {
                  o_sbp_cost0 = scratch(sizeof(double) * D.n_sbprior), o_sbp_cost1 = scratch(sizeof(double) * D.n_sbprior),
                  o_sbp_jv = scratch(sizeof(double) * 2 * D.n_sbprior);
     const size_t o_wfoff = upl(B.win_foff), o_wfdim = upl(B.win_fdim), o_wfpad = upl(B.win_fpad),
-                 o_wsoff = upl(B.win_soff), o_wpr = upl(B.win_pose_range), o_wsr = upl(B.win_sb_range),
+                 o_wsoff = upl(B.win_soff), o_wlinv = upl(B.win_linvoff), o_wfwd = upl(B.win_fwdoff), o_wpr = upl(B.win_pose_range), o_wsr = upl(B.win_sb_range),
                  o_wlr = upl(B.win_lm_range), o_wor = upl(B.win_obs_range), o_wir = upl(B.win_imu_range),
                  o_wppr = upl(B.win_pp_range), o_wsbpr = upl(B.win_sbp_range);
     const size_t o_fbw = upl(B.fb_win), o_fbk = upl(B.fb_kind), o_fbi = upl(B.fb_index), o_fbo = upl(B.fb_off),
                  o_fbcb = upl(B.fb_cbegin), o_fbc = upl(B.fb_contrib);
     const size_t o_pw = upl(B.pair_win), o_pfi = upl(B.pair_fi), o_pfj = upl(B.pair_fj), o_pcb = upl(B.pair_cbegin),
                  o_pc = upl(B.pair_contrib);
+    const size_t o_cpi = upl(B.chol_panel_items), o_cpb = upl(B.chol_panel_begin), o_cui = upl(B.chol_upd_items),
+                 o_cub = upl(B.chol_upd_begin), o_ti = upl(B.tile_items);
     const size_t nf = std::max(1, B.f_total), nl3 = std::max<size_t>(1, (size_t)3 * D.n_lm);
     const size_t o_S = scratch(sizeof(double) * std::max<int64_t>(1, B.s_total));
+    const size_t o_Linv = scratch(sizeof(double) * std::max<int64_t>(1, B.linv_total));
+    const size_t o_fwd = scratch(sizeof(double) * std::max<int64_t>(1, B.fwd_total));
     size_t of[10], ol[7];
     for (int i = 0; i < 10; ++i) of[i] = scratch(sizeof(double) * nf);
     for (int i = 0; i < 7; ++i) ol[i] = scratch(sizeof(double) * nl3);
     const size_t o_st = scratch(sizeof(WinState) * D.n_win);
+    const size_t o_self = scratch(sizeof(DevProblem));
     // ---- allocate + upload
     HIPCHK(hipMalloc(&arena, A.size));
     arenaBytes = A.size;
@@ -581,6 +639,7 @@ struct okvisgpu_ctx {
     D.lm_visit_begin = ip(o_lmvb); D.visit_pose = ip(o_vpose); D.visit_obs_begin = ip(o_vob); D.visit_lm = ip(o_vlm);
     D.lm_V = dp(o_lmV); D.lm_g = dp(o_lmg); D.lm_Vinv = dp(o_lmVi); D.lm_z = dp(o_lmz);
     D.visit_W = dp(o_vW); D.visit_H = dp(o_vH); D.visit_g = dp(o_vg);
+    D.visit_UY = dp(o_vUY); D.visit_uz = dp(o_vuz);
     D.imu_blocks = ip(o_imu_blocks); D.imu_win = ip(o_imu_win); D.imu_flags = up(o_imu_flags);
     D.imu_t0 = lp(o_imu_t0); D.imu_t1 = lp(o_imu_t1); D.imu_sbegin = ip(o_imu_sb); D.imu_ts = lp(o_imu_ts);
     D.imu_ga = dp(o_imu_ga); D.imu_par = dp(o_imu_par); D.imu_state = dp(o_imu_state);
@@ -600,16 +659,35 @@ struct okvisgpu_ctx {
     D.fb_cbegin = ip(o_fbcb); D.fb_contrib = reinterpret_cast<const Contrib*>(base + o_fbc);
     D.pair_win = ip(o_pw); D.pair_fi = ip(o_pfi); D.pair_fj = ip(o_pfj); D.pair_cbegin = ip(o_pcb);
     D.pair_contrib = reinterpret_cast<const Contrib*>(base + o_pc);
+    D.chol_panel_items = ip(o_cpi); D.chol_panel_begin = ip(o_cpb);
+    D.chol_upd_items = ip(o_cui); D.chol_upd_begin = ip(o_cub);
+    D.tile_items = ip(o_ti);
+    D.n_tiles = (int)(B.tile_items.size() / 3);
+    D.h_panel_begin = B.chol_panel_begin.data();
+    D.h_upd_begin = B.chol_upd_begin.data();
     D.S = dp(o_S);
+    D.Linv = dp(o_Linv);
+    D.win_linvoff = lp(o_wlinv);
+    D.fwdF = dp(o_fwd);
+    D.win_fwdoff = lp(o_wfwd);
     double** fv[10] = {&D.sF, &D.diagF, &D.hdF, &D.gF, &D.rhsF, &D.yF, &D.gnF, &D.dgF, &D.vF, &D.stepF};
     for (int i = 0; i < 10; ++i) *fv[i] = dp(of[i]);
     double** lv[7] = {&D.sL, &D.diagL, &D.stepL, &D.yL, &D.gnL, &D.dgL, &D.vL};
     for (int i = 0; i < 7; ++i) *lv[i] = dp(ol[i]);
     D.gL = D.lm_g;  // the landmark gradient is the accumulated J_l^T r
     D.st = reinterpret_cast<WinState*>(base + o_st);
+    D.self = reinterpret_cast<const DevProblem*>(base + o_self);
     HIPCHK(hipStreamSynchronize(stream));
+    uploadDescriptor();
     haveProblem = true;
     structureDirty = false;
+  }
+
+  // Kernels read the descriptor through one pointer to device memory (a 1.3 KB by-value kernarg is
+  // re-fetched field by field on every dependent access).
+  void uploadDescriptor() {
+    HIPCHK(hipMemcpyAsync(const_cast<DevProblem*>(P.self), &P, sizeof(DevProblem), hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
   }
 
   void setOptions(const okvisgpu_options& o) {
@@ -627,6 +705,7 @@ struct okvisgpu_ctx {
     d.min_relative_decrease = o.min_relative_decrease;
     d.min_lm_diagonal = o.min_lm_diagonal;
     d.max_lm_diagonal = o.max_lm_diagonal;
+    uploadDescriptor();
   }
 
   void resetStates(double mu) {
