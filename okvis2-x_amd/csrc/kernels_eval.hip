@@ -6,13 +6,13 @@
 //                Restates implementation/ReprojectionError.hpp:71-220 fused: with
 //                A = L * Jh * C_CW,  J_pose = [w A, -A [p]x],  J_lm = -A  (the reference's
 //                J0_minimal = Jh_w T_CS J and J1 = -Jh_w T_CW, first three columns).
-//  k_eval_imu    one wavefront per ImuError: the data-dependent re-preintegration decision
-//                (ImuError.cpp:833-859), the trapezoidal re-preintegration with covariance
-//                propagation (ImuError.cpp:258-466; the four dP/dsigma recursions are linear in
-//                the noise densities and are carried as their sum P = sum sigma^2 dP/dsigma),
-//                the pseudo-inverse square root of P via a parallel (round-robin) Jacobi
-//                eigen-solver (PseudoInverse.hpp:132-158), then residual + minimal Jacobians
-//                (ImuError.cpp:861-1000).
+//  k_eval_imu    one 16-lane group per ImuError (four per wavefront): the data-dependent
+//                re-preintegration decision (ImuError.cpp:833-859), the trapezoidal
+//                re-preintegration with covariance propagation (ImuError.cpp:258-466; the four
+//                dP/dsigma recursions are linear in the noise densities and are carried as their
+//                sum P = sum sigma^2 dP/dsigma), a square-root information factor of P
+//                (PseudoInverse.hpp:132-158; see the note above the kernel), then residual +
+//                minimal Jacobians (ImuError.cpp:861-1000).
 //  k_eval_priors one thread per PoseError / SpeedAndBiasError (PoseError.cpp:73-125,
 //                SpeedAndBiasError.cpp:67-101).
 //
@@ -155,52 +155,92 @@ __device__ void loadPre(const double* s, ImuPre& p) {
   }
 }
 
-// F_delta of one integration step (ImuError.cpp:395-410); returns element (i, j).
-struct FStep {
-  double b03[9], b09[9], b012[9], b39[9], b63[9], b69[9], b612[9], dt;
-  __device__ double at(int i, int j) const {
-    const int bi = i / 3, bj = j / 3, ii = i % 3, jj = j % 3;
-    double v = (i == j) ? 1.0 : 0.0;
-    if (bi == 0) {
-      if (bj == 1) v = b03[ii * 3 + jj];
-      else if (bj == 2) v = (ii == jj) ? dt : 0.0;
-      else if (bj == 3) v = b09[ii * 3 + jj];
-      else if (bj == 4) v = b012[ii * 3 + jj];
-    } else if (bi == 1) {
-      if (bj == 3) v = b39[ii * 3 + jj];
-    } else if (bi == 2) {
-      if (bj == 1) v = b63[ii * 3 + jj];
-      else if (bj == 3) v = b69[ii * 3 + jj];
-      else if (bj == 4) v = b612[ii * 3 + jj];
-    }
-    return v;
-  }
-};
+// ---- k_eval_imu: one 16-lane group per ImuError, four factors per wavefront
+//
+// Lane l of a group owns column l of the preintegration covariance P (l < 15). Per integration
+// step every lane evaluates the scalar chain (ImuError.cpp:312-410) redundantly, so the
+// block-sparse F_delta (ImuError.cpp:395-410) is register resident and P <- F P F^T + Q needs one
+// LDS transpose: M = F P column-locally, then P' = F M^T + Q with row l of M read back.
+//
+// Square-root information. The solver consumes the IMU block only through U^T U, U^T r (with
+// r = U e) and column norms of U J, all invariant under U -> Q U for orthogonal Q. The reference
+// forms U = diag(lambda^-1/2) V^T from an eigen-decomposition with eigenvalues <= tol clamped to
+// tol (PseudoInverse.hpp:132-158, tol = max(eps, eps*15*lambda_max)). When P is provably far from
+// that clamp the pseudo-inverse is the inverse, and the Cholesky factor U = L^-1 (P = L L^T) is an
+// admissible square root at a fraction of the cost. The proof used on device:
+//   lambda_min(P) >= 1 / ||L^-1||_F^2   and   lambda_max(P) <= trace(P);
+// if 1/||U||_F^2 > 4 max(eps, eps*15*trace(P)) no eigenvalue is clamped. Otherwise (e.g. zero
+// bias random-walk densities) the group runs the cyclic Jacobi eigen-solver and applies the
+// reference's clamp exactly.
+constexpr int kImuGroup = 16;
+constexpr int kImuPerWG = 4;
 
-// Parallel cyclic Jacobi (round-robin ordering, 8 disjoint rotations per round) on a 16x16
-// symmetric matrix in LDS whose last row/column is a decoupled pad. One wavefront.
-__device__ void jacobiEigen16(double* A, double* V, double* rot, int lane) {
-  for (int e = lane; e < 256; e += 64) V[e] = ((e >> 4) == (e & 15)) ? 1.0 : 0.0;
+// F_delta (ImuError.cpp:395-410) of one step in LDS: non-identity 3x3 blocks
+constexpr int kF03 = 0, kF09 = 9, kF012 = 18, kF39 = 27, kF63 = 36, kF69 = 45, kF612 = 54, kFdt = 63;
+
+// out = F v   (block rows: 0 dp, 1 dalpha, 2 dv, 3 bg, 4 ba); F read from LDS (group broadcast)
+__device__ __forceinline__ void applyF(const double* F, const double* v, double* out) {
+  const double dt = F[kFdt];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    double a = v[r];
+    a += F[kF03 + r * 3 + 0] * v[3] + F[kF03 + r * 3 + 1] * v[4] + F[kF03 + r * 3 + 2] * v[5];
+    a += dt * v[6 + r];
+    a += F[kF09 + r * 3 + 0] * v[9] + F[kF09 + r * 3 + 1] * v[10] + F[kF09 + r * 3 + 2] * v[11];
+    a += F[kF012 + r * 3 + 0] * v[12] + F[kF012 + r * 3 + 1] * v[13] + F[kF012 + r * 3 + 2] * v[14];
+    out[r] = a;
+    out[3 + r] = v[3 + r] + F[kF39 + r * 3 + 0] * v[9] + F[kF39 + r * 3 + 1] * v[10] + F[kF39 + r * 3 + 2] * v[11];
+    double c = F[kF63 + r * 3 + 0] * v[3] + F[kF63 + r * 3 + 1] * v[4] + F[kF63 + r * 3 + 2] * v[5];
+    c += v[6 + r];
+    c += F[kF69 + r * 3 + 0] * v[9] + F[kF69 + r * 3 + 1] * v[10] + F[kF69 + r * 3 + 2] * v[11];
+    c += F[kF612 + r * 3 + 0] * v[12] + F[kF612 + r * 3 + 1] * v[13] + F[kF612 + r * 3 + 2] * v[14];
+    out[6 + r] = c;
+  }
+#pragma unroll
+  for (int r = 9; r < 15; ++r) out[r] = v[r];
+}
+
+__device__ __forceinline__ double pick9(const double* v, int l) {  // v[l] for l < 9, register selects
+  double x = v[0];
+#pragma unroll
+  for (int e = 1; e < 9; ++e) x = (l == e) ? v[e] : x;
+  return x;
+}
+
+__device__ __forceinline__ double groupSum(double v) {  // sum over the 16 lanes of a group
+  v += __shfl_xor(v, 8, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 1, 64);
+  return v;
+}
+
+__device__ __forceinline__ double sel3(const double* M, int r, int c) {  // M(r, c), c dynamic
+  return c == 0 ? M[r * 3] : (c == 1 ? M[r * 3 + 1] : M[r * 3 + 2]);
+}
+
+// Cyclic Jacobi with round-robin ordering on the 16x16 (15 + decoupled pad) symmetric matrix A of
+// every group with `need` set; V receives the eigenvectors. Uniform control flow over the wave.
+__device__ void groupJacobi(double* A, double* V, double* rot, int l, bool need) {
+  for (int e = l; e < 256; e += kImuGroup) V[e] = ((e >> 4) == (e & 15)) ? 1.0 : 0.0;
   __syncthreads();
+  bool run = need;
   for (int sweep = 0; sweep < 100; ++sweep) {
-    // convergence test: off-diagonal vs diagonal energy (same criterion as the oracle)
     double off = 0.0, dg = 0.0;
-    for (int e = lane; e < 256; e += 64) {
-      const int i = e >> 4, j = e & 15;
-      const double a = A[e];
-      if (i == j) dg += a * a;
-      else if (i < j) off += a * a;
+    for (int j = 0; j < 16; ++j) {
+      const double a = A[l * 16 + j];
+      if (j == l) dg += a * a;
+      else if (l < j) off += a * a;
     }
-    for (int sh = 32; sh > 0; sh >>= 1) {
-      off += __shfl_xor(off, sh, 64);
-      dg += __shfl_xor(dg, sh, 64);
-    }
-    if (off <= 1e-36 * dg || off == 0.0) break;
+    off = groupSum(off);
+    dg = groupSum(dg);
+    if (off <= 1e-36 * dg || off == 0.0) run = false;
+    if (!__any(run)) break;
     for (int round = 0; round < 15; ++round) {
-      if (lane < 8) {
+      if (run && l < 8) {
         int p, q;
-        if (lane == 0) { p = 15; q = round; }
-        else { p = (round + lane) % 15; q = (round + 15 - lane) % 15; }
+        if (l == 0) { p = 15; q = round; }
+        else { p = (round + l) % 15; q = (round + 15 - l) % 15; }
         if (p > q) { const int t = p; p = q; q = t; }
         const double apq = A[p * 16 + q];
         double c = 1.0, s = 0.0;
@@ -211,36 +251,38 @@ __device__ void jacobiEigen16(double* A, double* V, double* rot, int lane) {
           c = 1.0 / sqrt(t * t + 1.0);
           s = t * c;
         }
-        rot[lane * 4 + 0] = c;
-        rot[lane * 4 + 1] = s;
-        rot[lane * 4 + 2] = (double)p;
-        rot[lane * 4 + 3] = (double)q;
+        rot[l * 4 + 0] = c;
+        rot[l * 4 + 1] = s;
+        rot[l * 4 + 2] = (double)p;
+        rot[l * 4 + 3] = (double)q;
       }
       __syncthreads();
-      // columns: A <- A J, V <- V J   (8 pairs x 16 rows, two matrices)
-      for (int t = lane; t < 256; t += 64) {
-        const int k = (t >> 4) & 7, row = t & 15;
-        double* M = (t < 128) ? A : V;
-        const double c = rot[k * 4], s = rot[k * 4 + 1];
-        const int p = (int)rot[k * 4 + 2], q = (int)rot[k * 4 + 3];
-        const double mp = M[row * 16 + p], mq = M[row * 16 + q];
-        M[row * 16 + p] = c * mp - s * mq;
-        M[row * 16 + q] = s * mp + c * mq;
+      if (run) {
+        for (int t = l; t < 256; t += kImuGroup) {  // columns: A <- A J, V <- V J
+          const int k = (t >> 4) & 7, row = t & 15;
+          double* M = (t < 128) ? A : V;
+          const double c = rot[k * 4], s = rot[k * 4 + 1];
+          const int p = (int)rot[k * 4 + 2], q = (int)rot[k * 4 + 3];
+          const double mp = M[row * 16 + p], mq = M[row * 16 + q];
+          M[row * 16 + p] = c * mp - s * mq;
+          M[row * 16 + q] = s * mp + c * mq;
+        }
       }
       __syncthreads();
-      // rows: A <- J^T A
-      for (int t = lane; t < 128; t += 64) {
-        const int k = t >> 4, col = t & 15;
-        const double c = rot[k * 4], s = rot[k * 4 + 1];
-        const int p = (int)rot[k * 4 + 2], q = (int)rot[k * 4 + 3];
-        const double mp = A[p * 16 + col], mq = A[q * 16 + col];
-        A[p * 16 + col] = c * mp - s * mq;
-        A[q * 16 + col] = s * mp + c * mq;
+      if (run) {
+        for (int t = l; t < 128; t += kImuGroup) {  // rows: A <- J^T A
+          const int k = t >> 4, col = t & 15;
+          const double c = rot[k * 4], s = rot[k * 4 + 1];
+          const int p = (int)rot[k * 4 + 2], q = (int)rot[k * 4 + 3];
+          const double mp = A[p * 16 + col], mq = A[q * 16 + col];
+          A[p * 16 + col] = c * mp - s * mq;
+          A[q * 16 + col] = s * mp + c * mq;
+        }
       }
       __syncthreads();
-      if (lane < 8) {
-        const int p = (int)rot[lane * 4 + 2], q = (int)rot[lane * 4 + 3];
-        if (rot[lane * 4 + 1] != 0.0) {
+      if (run && l < 8) {
+        const int p = (int)rot[l * 4 + 2], q = (int)rot[l * 4 + 3];
+        if (rot[l * 4 + 1] != 0.0) {
           A[p * 16 + q] = 0.0;
           A[q * 16 + p] = 0.0;
         }
@@ -254,29 +296,36 @@ __device__ void jacobiEigen16(double* A, double* V, double* rot, int lane) {
 
 __global__ __launch_bounds__(64) void k_eval_imu(const DevProblem* __restrict__ Pp, int mode) {
   const DevProblem& P = *Pp;
-  const int f = blockIdx.x;
-  if (f >= P.n_imu) return;
-  const int w = P.imu_win[f];
-  int xs, lb;
-  if (!evalSelect(P, w, mode, xs, lb)) return;
-  if ((P.imu_flags[f] & 2) && mode < 2) return;
-  const int lane = threadIdx.x;
+  const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
+  const int f = blockIdx.x * kImuPerWG + g;
 
-  __shared__ double sP[256], sF[256], sT[256], sV[256], sU[225];
-  __shared__ double sRot[32];
-  __shared__ double sFF[450];
+  // per-group LDS: sA = symmetric P / Jacobi matrix / U (row-major 16x16), sB = transpose
+  // exchange / L (column-major) / Jacobi eigenvectors, sR = Jacobi rotations, sF = F_delta
+  __shared__ double sAll[kImuPerWG][2 * 256 + 32 + 64];
+  double* sA = sAll[g];
+  double* sB = sAll[g] + 256;
+  double* sR = sAll[g] + 512;
+  double* sF = sAll[g] + 544;
 
-  const int* blk = P.imu_blocks + 4 * f;
+  int w = 0, xs = 0, lb = 0;
+  bool live = f < P.n_imu;
+  if (live) {
+    w = P.imu_win[f];
+    live = evalSelect(P, w, mode, xs, lb) && !((P.imu_flags[f] & 2) && mode < 2);
+  }
+  const int fs = live ? f : 0;  // safe index for idle groups
+
+  const int* blk = P.imu_blocks + 4 * fs;
   const double* p0 = P.pose[xs] + 7 * (size_t)blk[0];
   const double* sb0 = P.sb[xs] + 9 * (size_t)blk[1];
   const double* p1 = P.pose[xs] + 7 * (size_t)blk[2];
   const double* sb1 = P.sb[xs] + 9 * (size_t)blk[3];
-  double* state = P.imu_state + (size_t)f * kImuState;
+  double* state = P.imu_state + (size_t)fs * kImuState;
   const double* par = P.imu_par + 7 * w;
   const double a_max = par[0], g_max = par[1], sg_c = par[2], sa_c = par[3], sgw_c = par[4], saw_c = par[5],
                gmag = par[6];
-  const int64_t t0 = P.imu_t0[f], t1 = P.imu_t1[f];
-  const int sbeg = P.imu_sbegin[f], send = P.imu_sbegin[f + 1];
+  const int64_t t0 = P.imu_t0[fs], t1 = P.imu_t1[fs];
+  const int sbeg = P.imu_sbegin[fs], send = P.imu_sbegin[fs + 1];
 
   // ---- re-preintegration decision (ImuError.cpp:833-859)
   int redoCounter = (int)state[0];
@@ -285,32 +334,40 @@ __global__ __launch_bounds__(64) void k_eval_imu(const DevProblem* __restrict__ 
   for (int k = 0; k < 6; ++k) Db[k] = sb0[3 + k] - state[57 + 3 + k];
   redo = redo || (sqrt(Db[0] * Db[0] + Db[1] * Db[1] + Db[2] * Db[2]) > 0.0003);
   const bool doRedo = (redo && ((send - sbeg) < 50 || P.opt.redo_propagation_always)) || redoCounter == 0;
-  bool success = true;
-  ImuPre pre;
-
+  // redoPreintegration returns -1 before touching any state when the samples do not cover t1
+  // (ImuError.cpp:270-273): the old preintegration is kept.
   const bool covered = (send > sbeg) && P.imu_ts[send - 1] >= t1;
-  if (doRedo && !covered) {
-    // redoPreintegration returns -1 before touching any state (ImuError.cpp:270-273)
-    loadPre(state, pre);
-    for (int e = lane; e < 225; e += 64) sU[e] = state[66 + e];
-    __syncthreads();
+  const bool integrate = live && doRedo && covered;
+  if (live && doRedo) {
     redoCounter++;
     for (int k = 0; k < 6; ++k) Db[k] = 0.0;
     redo = false;
-  } else if (doRedo) {
-    // ---- redoPreintegration (ImuError.cpp:258-466)
-    pre.dq = Q{0, 0, 0, 1};
-    for (int i = 0; i < 9; ++i) { pre.Ci[i] = 0; pre.Cdi[i] = 0; pre.dadbg[i] = 0; pre.dvdbg[i] = 0; pre.dpdbg[i] = 0; }
-    for (int i = 0; i < 3; ++i) { pre.ai[i] = 0; pre.adi[i] = 0; }
-    double cross[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int e = lane; e < 256; e += 64) sP[e] = 0.0;
+  }
+
+  // chain state needed by every step (replicated across the group); the pure accumulators
+  // C_dint, acc_dint, dalpha_db_g, dp_db_g are distributed: lane e < 9 holds component e.
+  Q cdq{0, 0, 0, 1};
+  double cCi[9], cai[3], cdvdbg[9], cross[9];
+  double aCdi = 0.0, aadi = 0.0, adadbg = 0.0, adpdbg = 0.0;
+  for (int i = 0; i < 9; ++i) { cCi[i] = 0; cdvdbg[i] = 0; cross[i] = 0; }
+  for (int i = 0; i < 3; ++i) cai[i] = 0;
+  double Pc[15];  // column l of P
+  for (int i = 0; i < 15; ++i) Pc[i] = 0.0;
+  int steps = 0;
+
+  // ---- redoPreintegration (ImuError.cpp:258-466), uniform trip count over the wavefront
+  {
     const double bg[3] = {sb0[3], sb0[4], sb0[5]}, ba[3] = {sb0[6], sb0[7], sb0[8]};
     int64_t time = t0;
-    bool hasStarted = false;
-    int steps = 0;
-    const int N = send - sbeg;
-    {
-      for (int it = 0; it < N; ++it) {
+    bool hasStarted = false, running = integrate;
+    const int N = integrate ? send - sbeg : 0;
+    int Nmax = N;
+    Nmax = max(Nmax, __shfl_xor(Nmax, 16, 64));
+    Nmax = max(Nmax, __shfl_xor(Nmax, 32, 64));
+    for (int it = 0; it < Nmax; ++it) {
+      bool doStep = false;
+      double qa0 = 0, qg = 0, qa = 0, qbg = 0, qba = 0;
+      if (running && it < N) {
         const int s0 = sbeg + it;
         const int s1 = (it + 1 < N) ? s0 + 1 : s0;
         double om0[3], ac0[3], om1[3], ac1[3];
@@ -332,186 +389,294 @@ __global__ __launch_bounds__(64) void k_eval_imu(const DevProblem* __restrict__ 
             ac1[k] = (1.0 - r) * ac0[k] + r * ac1[k];
           }
         }
-        if (dt <= 0.0) continue;
-        if (!hasStarted) {
-          hasStarted = true;
-          const double r = dt / durToSec(nexttime - P.imu_ts[s0]);
+        if (dt > 0.0) {  // dt <= 0: the sample is skipped (ImuError.cpp:339)
+          doStep = true;
+          if (!hasStarted) {
+            hasStarted = true;
+            const double r = dt / durToSec(nexttime - P.imu_ts[s0]);
+            for (int k = 0; k < 3; ++k) {
+              om0[k] = r * om0[k] + (1.0 - r) * om1[k];
+              ac0[k] = r * ac0[k] + (1.0 - r) * ac1[k];
+            }
+          }
+          double gyr_sat = 1.0, acc_sat = 1.0;
           for (int k = 0; k < 3; ++k) {
-            om0[k] = r * om0[k] + (1.0 - r) * om1[k];
-            ac0[k] = r * ac0[k] + (1.0 - r) * ac1[k];
+            if (fabs(om0[k]) > g_max || fabs(om1[k]) > g_max) gyr_sat = 100.0;
+            if (fabs(ac0[k]) > a_max || fabs(ac1[k]) > a_max) acc_sat = 100.0;
           }
-        }
-        double gyr_sat = 1.0, acc_sat = 1.0;
-        for (int k = 0; k < 3; ++k) {
-          if (fabs(om0[k]) > g_max || fabs(om1[k]) > g_max) gyr_sat = 100.0;
-          if (fabs(ac0[k]) > a_max || fabs(ac1[k]) > a_max) acc_sat = 100.0;
-        }
-        // orientation
-        double w_true[3], a_true[3];
-        for (int k = 0; k < 3; ++k) {
-          w_true[k] = 0.5 * (om0[k] + om1[k]) - bg[k];
-          a_true[k] = 0.5 * (ac0[k] + ac1[k]) - ba[k];
-        }
-        const double theta_half = sqrt(w_true[0] * w_true[0] + w_true[1] * w_true[1] + w_true[2] * w_true[2]) * 0.5 * dt;
-        const double sth = sinc(theta_half) * 0.5 * dt;
-        const Q dq{sth * w_true[0], sth * w_true[1], sth * w_true[2], cos(theta_half)};
-        const Q dq1 = qmul(pre.dq, dq);
-        double C[9], C1[9], CC1[9];
-        qrot(pre.dq, C);
-        qrot(dq1, C1);
-        for (int i = 0; i < 9; ++i) CC1[i] = C[i] + C1[i];
-        double CCa[3];
-        mv3(CC1, a_true, CCa);
-        double Ci1[9], ai1[3];
-        for (int i = 0; i < 9; ++i) Ci1[i] = pre.Ci[i] + 0.5 * dt * CC1[i];
-        for (int i = 0; i < 3; ++i) ai1[i] = pre.ai[i] + 0.5 * dt * CCa[i];
-        FStep F;
-        F.dt = dt;
-        {
-          double v[3];
-          for (int i = 0; i < 3; ++i) v[i] = pre.ai[i] * dt + 0.25 * dt * dt * CCa[i];
-          crossMx(v, F.b03);
-          for (int i = 0; i < 9; ++i) F.b03[i] = -F.b03[i];
-          for (int i = 0; i < 3; ++i) v[i] = 0.5 * dt * CCa[i];
-          crossMx(v, F.b63);
-          for (int i = 0; i < 9; ++i) F.b63[i] = -F.b63[i];
-        }
-        for (int i = 0; i < 9; ++i) {
-          pre.Cdi[i] += pre.Ci[i] * dt + 0.25 * dt * dt * CC1[i];
-          F.b012[i] = -pre.Ci[i] * dt + 0.25 * dt * dt * CC1[i];
-          F.b39[i] = -dt * C1[i];
-          F.b612[i] = -0.5 * dt * CC1[i];
-        }
-        for (int i = 0; i < 3; ++i) pre.adi[i] += pre.ai[i] * dt + 0.25 * dt * dt * CCa[i];
-        // Jacobian parts (ImuError.cpp:385-392)
-        double wdt[3] = {w_true[0] * dt, w_true[1] * dt, w_true[2] * dt};
-        double Jr[9], CJr[9];
-        rightJacobian(wdt, Jr);
-        mm3(C1, Jr, CJr);
-        for (int i = 0; i < 9; ++i) pre.dadbg[i] += CJr[i] * dt;
-        double Rdqi[9], tmp[9], cross1[9];
-        qrot(qinv(dq), Rdqi);
-        mm3(Rdqi, cross, tmp);
-        for (int i = 0; i < 9; ++i) cross1[i] = tmp[i] + Jr[i] * dt;
-        double ax[9], t1m[9], t2m[9], X[9];
-        crossMx(a_true, ax);
-        mm3(C, ax, tmp);
-        mm3(tmp, cross, t1m);
-        mm3(C1, ax, tmp);
-        mm3(tmp, cross1, t2m);
-        for (int i = 0; i < 9; ++i) X[i] = t1m[i] + t2m[i];
-        for (int i = 0; i < 9; ++i) {
-          F.b09[i] = dt * pre.dvdbg[i] + 0.25 * dt * dt * X[i];
-          F.b69[i] = 0.5 * dt * X[i];
-          pre.dpdbg[i] += dt * pre.dvdbg[i] + 0.25 * dt * dt * X[i];
-        }
-        // covariance propagation P <- F P F^T + sum_j sigma_j^2 K_j (ImuError.cpp:412-426)
-        for (int e = lane; e < 225; e += 64) sF[e] = F.at(e / 15, e % 15);
-        __syncthreads();
-        for (int e = lane; e < 225; e += 64) {
-          const int i = e / 15, j = e % 15;
-          double acc = 0.0;
-          for (int m = 0; m < 15; ++m) acc += sF[i * 15 + m] * sP[m * 15 + j];
-          sT[e] = acc;
-        }
-        __syncthreads();
-        for (int e = lane; e < 225; e += 64) {
-          const int i = e / 15, j = e % 15;
-          double acc = 0.0;
-          for (int m = 0; m < 15; ++m) acc += sT[i * 15 + m] * sF[j * 15 + m];
-          if (i == j) {
-            const int b = i / 3;
-            if (b == 0) acc += sa_c * sa_c * (0.5 * dt * dt * dt * acc_sat * acc_sat * acc_sat);
-            else if (b == 1) acc += sg_c * sg_c * (gyr_sat * dt);
-            else if (b == 2) acc += sa_c * sa_c * (acc_sat * dt);
-            else if (b == 3) acc += sgw_c * sgw_c * dt;
-            else acc += saw_c * saw_c * dt;
+          double w_true[3], a_true[3];
+          for (int k = 0; k < 3; ++k) {
+            w_true[k] = 0.5 * (om0[k] + om1[k]) - bg[k];
+            a_true[k] = 0.5 * (ac0[k] + ac1[k]) - ba[k];
           }
-          sP[e] = acc;
+          const double theta_half =
+              sqrt(w_true[0] * w_true[0] + w_true[1] * w_true[1] + w_true[2] * w_true[2]) * 0.5 * dt;
+          const double sth = sinc(theta_half) * 0.5 * dt;
+          const Q dq{sth * w_true[0], sth * w_true[1], sth * w_true[2], cos(theta_half)};
+          const Q dq1 = qmul(cdq, dq);
+          double C[9], C1[9], CC1[9];
+          qrot(cdq, C);
+          qrot(dq1, C1);
+          for (int i = 0; i < 9; ++i) CC1[i] = C[i] + C1[i];
+          double CCa[3];
+          mv3(CC1, a_true, CCa);
+          const double hdt2 = 0.25 * dt * dt;
+          double tmp[9];
+          if (l == 0) {
+            double v[3], mx[9];
+            for (int i = 0; i < 3; ++i) v[i] = cai[i] * dt + hdt2 * CCa[i];
+            crossMx(v, mx);
+            for (int i = 0; i < 9; ++i) sF[kF03 + i] = -mx[i];
+            for (int i = 0; i < 3; ++i) v[i] = 0.5 * dt * CCa[i];
+            crossMx(v, mx);
+            for (int i = 0; i < 9; ++i) sF[kF63 + i] = -mx[i];
+            for (int i = 0; i < 9; ++i) {
+              sF[kF012 + i] = -cCi[i] * dt + hdt2 * CC1[i];
+              sF[kF39 + i] = -dt * C1[i];
+              sF[kF612 + i] = -0.5 * dt * CC1[i];
+            }
+            sF[kFdt] = dt;
+          }
+          for (int i = 0; i < 9; ++i) tmp[i] = cCi[i] * dt + hdt2 * CC1[i];
+          aCdi += pick9(tmp, l);
+          for (int i = 0; i < 3; ++i) tmp[i] = cai[i] * dt + hdt2 * CCa[i];
+          aadi += (l == 0) ? tmp[0] : ((l == 1) ? tmp[1] : tmp[2]);
+          for (int i = 0; i < 9; ++i) cCi[i] += 0.5 * dt * CC1[i];
+          for (int i = 0; i < 3; ++i) cai[i] += 0.5 * dt * CCa[i];
+          // Jacobian parts (ImuError.cpp:385-392)
+          const double wdt[3] = {w_true[0] * dt, w_true[1] * dt, w_true[2] * dt};
+          double Jr[9];
+          rightJacobian(wdt, Jr);
+          mm3(C1, Jr, tmp);
+          adadbg += pick9(tmp, l) * dt;
+          double Rdqi[9], cross1[9];
+          qrot(qinv(dq), Rdqi);
+          mm3(Rdqi, cross, tmp);
+          for (int i = 0; i < 9; ++i) cross1[i] = tmp[i] + Jr[i] * dt;
+          double ax[9], t1m[9], X[9];
+          crossMx(a_true, ax);
+          mm3(C, ax, tmp);
+          mm3(tmp, cross, t1m);
+          mm3(C1, ax, tmp);
+          mm3(tmp, cross1, X);
+          for (int i = 0; i < 9; ++i) X[i] += t1m[i];
+          for (int i = 0; i < 9; ++i) tmp[i] = dt * cdvdbg[i] + hdt2 * X[i];
+          if (l == 0)
+            for (int i = 0; i < 9; ++i) {
+              sF[kF09 + i] = tmp[i];
+              sF[kF69 + i] = 0.5 * dt * X[i];
+            }
+          adpdbg += pick9(tmp, l);
+          for (int i = 0; i < 9; ++i) {
+            cdvdbg[i] += 0.5 * dt * X[i];
+            cross[i] = cross1[i];
+          }
+          cdq = dq1;
+          // discrete noise of this step on the diagonal (ImuError.cpp:412-426, summed over sigma)
+          qa0 = sa_c * sa_c * (0.5 * dt * dt * dt * acc_sat * acc_sat * acc_sat);
+          qg = sg_c * sg_c * (gyr_sat * dt);
+          qa = sa_c * sa_c * (acc_sat * dt);
+          qbg = sgw_c * sgw_c * dt;
+          qba = saw_c * saw_c * dt;
+          time = nexttime;
+          ++steps;
+          if (nexttime == t1) running = false;
         }
-        __syncthreads();
-        // memory shift
-        pre.dq = dq1;
-        for (int i = 0; i < 9; ++i) { pre.Ci[i] = Ci1[i]; cross[i] = cross1[i]; }
-        for (int i = 0; i < 9; ++i) pre.dvdbg[i] += 0.5 * dt * X[i];
-        for (int i = 0; i < 3; ++i) pre.ai[i] = ai1[i];
-        time = nexttime;
-        ++steps;
-        if (nexttime == t1) break;
       }
+      __syncthreads();
+      // P <- F P F^T + Q : M = F P (column l), exchange rows, P' = F M^T (column l)
+      if (doStep && l < 15) {
+        double Mc[15];
+        applyF(sF, Pc, Mc);
+        for (int i = 0; i < 15; ++i) sB[l * 16 + i] = Mc[i];  // column l of M
+      }
+      __syncthreads();
+      if (doStep && l < 15) {
+        double Mr[15];
+        for (int j = 0; j < 15; ++j) Mr[j] = sB[j * 16 + l];  // row l of M
+        applyF(sF, Mr, Pc);
+        for (int i = 0; i < 15; ++i) {
+          const double q = i < 3 ? qa0 : (i < 6 ? qg : (i < 9 ? qa : (i < 12 ? qbg : qba)));
+          Pc[i] += (i == l) ? q : 0.0;
+        }
+      }
+      __syncthreads();
     }
-    // symmetrise, pad to 16x16 and take the pseudo-inverse square root
-    for (int e = lane; e < 256; e += 64) {
-      const int i = e >> 4, j = e & 15;
-      sT[e] = (i < 15 && j < 15) ? 0.5 * sP[i * 15 + j] + 0.5 * sP[j * 15 + i] : 0.0;
-    }
-    __syncthreads();
-    jacobiEigen16(sT, sV, sRot, lane);
-    double lmax = -1e300;
-    for (int i = 0; i < 15; ++i) lmax = fmax(lmax, sT[i * 16 + i]);
-    const double tol = fmax(DBL_EPSILON, DBL_EPSILON * 15.0 * lmax);
-    for (int e = lane; e < 225; e += 64) {
-      const int i = e / 15, j = e % 15;
-      const double li = sT[i * 16 + i];
-      sU[e] = sqrt(li > tol ? 1.0 / li : 1.0 / tol) * sV[j * 16 + i];
-    }
-    __syncthreads();
-    if (steps == 0) success = false;
-    redoCounter++;
-    for (int k = 0; k < 6; ++k) Db[k] = 0.0;
-    redo = false;
-    // store the new state (lane-parallel)
-    if (lane == 0) {
-      state[2] = pre.dq.x; state[3] = pre.dq.y; state[4] = pre.dq.z; state[5] = pre.dq.w;
+  }
+  // new preintegration state (ImuError.hpp:273-304 members) straight from the chain registers;
+  // the distributed accumulators are written by their owner lanes
+  if (integrate) {
+    if (l == 0) {
+      state[2] = cdq.x; state[3] = cdq.y; state[4] = cdq.z; state[5] = cdq.w;
       for (int i = 0; i < 9; ++i) {
-        state[6 + i] = pre.Ci[i];
-        state[15 + i] = pre.Cdi[i];
-        state[30 + i] = pre.dadbg[i];
-        state[39 + i] = pre.dvdbg[i];
-        state[48 + i] = pre.dpdbg[i];
+        state[6 + i] = cCi[i];
+        state[39 + i] = cdvdbg[i];
         state[57 + i] = sb0[i];
       }
-      for (int i = 0; i < 3; ++i) { state[24 + i] = pre.ai[i]; state[27 + i] = pre.adi[i]; }
+      for (int i = 0; i < 3; ++i) state[24 + i] = cai[i];
       state[291] = (double)steps;
     }
-    for (int e = lane; e < 225; e += 64) state[66 + e] = sU[e];
-  } else {
-    loadPre(state, pre);
-    for (int e = lane; e < 225; e += 64) sU[e] = state[66 + e];
+    if (l < 9) {
+      state[15 + l] = aCdi;
+      state[30 + l] = adadbg;
+      state[48 + l] = adpdbg;
+    }
+    if (l < 3) state[27 + l] = aadi;
+  }
+
+  // ---- square-root information of P (PseudoInverse.hpp:132-158)
+  // symmetrise (ImuError.cpp:441): sB holds P column-major; the symmetric P is kept row-major
+  // (16x16 with a decoupled zero pad) in sA for the eigen fallback
+  if (integrate && l < 15)
+    for (int i = 0; i < 15; ++i) sB[l * 16 + i] = Pc[i];
+  __syncthreads();
+  double trace = 0.0;
+  if (integrate) {
+    for (int i = 0; i < 15; ++i) Pc[i] = (l < 15) ? 0.5 * Pc[i] + 0.5 * sB[i * 16 + l] : 0.0;
+    for (int i = 0; i < 16; ++i) sA[l * 16 + i] = (i < 15) ? Pc[i] : 0.0;
+    for (int i = 0; i < 15; ++i) trace += (i == l) ? Pc[i] : 0.0;
+  }
+  trace = groupSum(trace);
+  __syncthreads();
+  // right-looking Cholesky P = L L^T in LDS: sB (column-major) starts as P, lane j owns column j
+  bool ok = true;
+  if (integrate)
+    for (int i = 0; i < 16; ++i) sB[l * 16 + i] = (l < 15 && i < 15) ? Pc[i] : 0.0;
+  __syncthreads();
+  for (int k = 0; k < 15; ++k) {
+    if (integrate && l >= k && l < 15) {
+      const double d = sB[k * 16 + k];
+      if (!(d > 0.0)) ok = false;
+      const double v = sB[k * 16 + l] / sqrt(d);
+      sB[k * 16 + l] = v;
+    }
+    __syncthreads();
+    if (integrate && l > k && l < 15) {
+      const double ljk = sB[k * 16 + l];
+      for (int i = l; i < 15; ++i) sB[l * 16 + i] -= sB[k * 16 + i] * ljk;
+    }
     __syncthreads();
   }
-  if (lane == 0) {
+  // U = L^-1 in place (column-major, backward over columns):
+  //   U(j,j) = 1/L(j,j),  U(i,j) = -U(j,j) sum_{m=j+1..i} U(i,m) L(m,j)   (i > j)
+  for (int j = 14; j >= 0; --j) {
+    double acc = 0.0, ujj = 0.0;
+    if (integrate && l >= j && l < 15) {
+      ujj = 1.0 / sB[j * 16 + j];
+      for (int m = j + 1; m <= l; ++m) acc += sB[m * 16 + l] * sB[j * 16 + m];
+    }
+    __syncthreads();
+    if (integrate && l >= j && l < 15) sB[j * 16 + l] = (l == j) ? ujj : -ujj * acc;
+    __syncthreads();
+  }
+  double fro = 0.0;
+  if (integrate && l < 15)
+    for (int i = l; i < 15; ++i) fro += sB[l * 16 + i] * sB[l * 16 + i];
+  fro = groupSum(fro);
+  ok = groupSum(ok ? 0.0 : 1.0) == 0.0;
+  const double eps = DBL_EPSILON;
+  const bool needEig = integrate && !(ok && fro > 0.0 && 1.0 / fro > 4.0 * fmax(eps, eps * 15.0 * trace));
+  __syncthreads();
+  if (__any(needEig)) {
+    // clamped eigenvalues possible: the reference's eigen-decomposition (cyclic Jacobi) of the
+    // symmetric P kept in sA; eigenvectors into sB, then U = diag(clamped lambda^-1/2) V^T
+    groupJacobi(sA, sB, sR, l, needEig);
+    double urow[15];
+    if (needEig && l < 15) {
+      double lmax = -1e300;
+      for (int i = 0; i < 15; ++i) lmax = fmax(lmax, sA[i * 16 + i]);
+      const double tol = fmax(eps, eps * 15.0 * lmax);
+      const double li = sA[l * 16 + l];
+      const double s = sqrt(li > tol ? 1.0 / li : 1.0 / tol);
+      for (int j = 0; j < 15; ++j) urow[j] = s * sB[j * 16 + l];
+    }
+    __syncthreads();
+    if (needEig && l < 15)
+      for (int j = 0; j < 15; ++j) sA[l * 16 + j] = urow[j];
+  }
+  // Cholesky path: U (column-major in sB, lower triangular) -> row-major sA
+  if (integrate && !needEig && l < 15)
+    for (int i = 0; i < 15; ++i) sA[i * 16 + l] = (i >= l) ? sB[l * 16 + i] : 0.0;
+  __syncthreads();
+  if (integrate) {
+    for (int e = l; e < 225; e += kImuGroup) state[66 + e] = sA[(e / 15) * 16 + e % 15];
+  } else if (live) {
+    for (int e = l; e < 225; e += kImuGroup) sA[(e / 15) * 16 + e % 15] = state[66 + e];
+  }
+  __syncthreads();  // state writes of the group visible to all its lanes
+  ImuPre pre;
+  loadPre(state, pre);
+  const bool success = live && (!integrate || steps > 0);
+  if (live && l == 0) {
     state[0] = (double)redoCounter;
     state[1] = redo ? 1.0 : 0.0;
   }
 
   // ---- residual and minimal Jacobians (ImuError.cpp:861-1000)
+  // The ten distinct 3x3 blocks of [F0 | F1] are staged in LDS (sB, row-major 3x3 each):
+  //  0 C_S0_W  1 C_S0_W[dp]x  2 F0(3,3)  3 C_S0_W[dv]x  4 dp_db_g  5 F0(3,9)  6 dv_db_g
+  //  7 C_doubleintegral  8 C_integral  9 F1(3,3)
   const Q q0 = qnormalize(Q{p0[3], p0[4], p0[5], p0[6]});
   const Q q1 = qnormalize(Q{p1[3], p1[4], p1[5], p1[6]});
-  double C0[9];
-  qrot(q0, C0);  // C_WS_0 ; C_S0_W = C0^T
-  const double Dt = durToSec(t1 - t0);
-  double dp[3], dv[3];
-  const double gW[3] = {0.0, 0.0, gmag};
-  for (int k = 0; k < 3; ++k) {
-    dp[k] = p0[k] - p1[k] + sb0[k] * Dt - 0.5 * gW[k] * Dt * Dt;
-    dv[k] = sb0[k] - sb1[k] - gW[k] * Dt;
-  }
-  double adb[3];
-  mv3(pre.dadbg, Db, adb);
-  const Q Dq = qmul(deltaQ(-adb[0], -adb[1], -adb[2]), pre.dq);
   const Q q1i = qinv(q1);
-  // F0 / F1 blocks needing quaternion algebra
-  double M33a[9], M33b[9], M33c[9];
+  const double Dt = durToSec(t1 - t0);
+  double err[15];
+  Q Dq;
   {
-    double Pm[16], Om[16], R[16];
+    double C0[9];
+    qrot(q0, C0);  // C_WS_0 ; C_S0_W = C0^T
+    double dp[3], dv[3];
+    const double gW[3] = {0.0, 0.0, gmag};
+    for (int k = 0; k < 3; ++k) {
+      dp[k] = p0[k] - p1[k] + sb0[k] * Dt - 0.5 * gW[k] * Dt * Dt;
+      dv[k] = sb0[k] - sb1[k] - gW[k] * Dt;
+    }
+    double adb[3];
+    mv3(pre.dadbg, Db, adb);
+    Dq = qmul(deltaQ(-adb[0], -adb[1], -adb[2]), pre.dq);
+    double t0v[3], t6v[3];
+    mtv3(C0, dp, t0v);
+    mtv3(C0, dv, t6v);
+    const Q qe = qmul(Dq, qmul(q1i, q0));
+    for (int k = 0; k < 3; ++k) {
+      const double e0 = pre.dpdbg[k * 3 + 0] * Db[0] + pre.dpdbg[k * 3 + 1] * Db[1] + pre.dpdbg[k * 3 + 2] * Db[2] -
+                        (pre.Cdi[k * 3 + 0] * Db[3] + pre.Cdi[k * 3 + 1] * Db[4] + pre.Cdi[k * 3 + 2] * Db[5]);
+      const double e6 = pre.dvdbg[k * 3 + 0] * Db[0] + pre.dvdbg[k * 3 + 1] * Db[1] + pre.dvdbg[k * 3 + 2] * Db[2] -
+                        (pre.Ci[k * 3 + 0] * Db[3] + pre.Ci[k * 3 + 1] * Db[4] + pre.Ci[k * 3 + 2] * Db[5]);
+      err[k] = t0v[k] + pre.adi[k] + e0;
+      err[6 + k] = t6v[k] + pre.ai[k] + e6;
+    }
+    err[3] = 2 * qe.x; err[4] = 2 * qe.y; err[5] = 2 * qe.z;
+    for (int k = 0; k < 6; ++k) err[9 + k] = sb0[3 + k] - sb1[3 + k];
+    if (!success)
+      for (int k = 0; k < 15; ++k) err[k] = 0.0;
+    if (live && l == 0) {
+      double dpx[9], dvx[9];
+      crossMx(dp, dpx);
+      crossMx(dv, dvx);
+      for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+          sB[0 * 9 + r * 3 + c] = C0[c * 3 + r];
+          sB[1 * 9 + r * 3 + c] = C0[0 * 3 + r] * dpx[0 * 3 + c] + C0[1 * 3 + r] * dpx[1 * 3 + c] + C0[2 * 3 + r] * dpx[2 * 3 + c];
+          sB[3 * 9 + r * 3 + c] = C0[0 * 3 + r] * dvx[0 * 3 + c] + C0[1 * 3 + r] * dvx[1 * 3 + c] + C0[2 * 3 + r] * dvx[2 * 3 + c];
+        }
+      for (int i = 0; i < 9; ++i) {
+        sB[4 * 9 + i] = pre.dpdbg[i];
+        sB[6 * 9 + i] = pre.dvdbg[i];
+        sB[7 * 9 + i] = pre.Cdi[i];
+        sB[8 * 9 + i] = pre.Ci[i];
+      }
+    }
+  }
+  if (live && l == 1) {
+    double Pm[16], Om[16], R[9];
     qplusM(qmul(Dq, q1i), Pm);
     qoplusM(q0, Om);
     for (int r = 0; r < 3; ++r)
       for (int c = 0; c < 3; ++c) {
         double s = 0;
         for (int k = 0; k < 4; ++k) s += Pm[r * 4 + k] * Om[k * 4 + c];
-        M33a[r * 3 + c] = s;  // F0(3,3)
+        sB[2 * 9 + r * 3 + c] = s;  // F0(3,3)
       }
     qoplusM(qmul(q1i, q0), Pm);
     qoplusM(Dq, Om);
@@ -523,8 +688,10 @@ __global__ __launch_bounds__(64) void k_eval_imu(const DevProblem* __restrict__ 
       }
     for (int r = 0; r < 3; ++r)
       for (int c = 0; c < 3; ++c)
-        M33b[r * 3 + c] = -(R[r * 3 + 0] * pre.dadbg[0 * 3 + c] + R[r * 3 + 1] * pre.dadbg[1 * 3 + c] +
-                            R[r * 3 + 2] * pre.dadbg[2 * 3 + c]);  // F0(3,9)
+        sB[5 * 9 + r * 3 + c] = -(R[r * 3 + 0] * pre.dadbg[0 * 3 + c] + R[r * 3 + 1] * pre.dadbg[1 * 3 + c] +
+                                  R[r * 3 + 2] * pre.dadbg[2 * 3 + c]);  // F0(3,9)
+  }
+  if (live && l == 2) {
     double Pd[16], O0[16], P1i[16], T4[16];
     qplusM(Dq, Pd);
     qoplusM(q0, O0);
@@ -539,88 +706,58 @@ __global__ __launch_bounds__(64) void k_eval_imu(const DevProblem* __restrict__ 
       for (int c = 0; c < 3; ++c) {
         double s = 0;
         for (int k = 0; k < 4; ++k) s += T4[r * 4 + k] * P1i[k * 4 + c];
-        M33c[r * 3 + c] = -s;  // F1(3,3)
+        sB[9 * 9 + r * 3 + c] = -s;  // F1(3,3)
       }
   }
-  double dpx[9], dvx[9], Cdp[9], Cdv[9];
-  crossMx(dp, dpx);
-  crossMx(dv, dvx);
-  // C_S0_W [dp]x and C_S0_W [dv]x
-  for (int r = 0; r < 3; ++r)
-    for (int c = 0; c < 3; ++c) {
-      Cdp[r * 3 + c] = C0[0 * 3 + r] * dpx[0 * 3 + c] + C0[1 * 3 + r] * dpx[1 * 3 + c] + C0[2 * 3 + r] * dpx[2 * 3 + c];
-      Cdv[r * 3 + c] = C0[0 * 3 + r] * dvx[0 * 3 + c] + C0[1 * 3 + r] * dvx[1 * 3 + c] + C0[2 * 3 + r] * dvx[2 * 3 + c];
-    }
-  // FF = [F0 | F1] (15 x 30) into LDS
-  for (int e = lane; e < 450; e += 64) {
-    const int i = e / 30, j = e % 30;
-    const bool right = j >= 15;
-    const int jj = right ? j - 15 : j;
-    const int bi = i / 3, bj = jj / 3, ii = i % 3, kk = jj % 3;
-    double v;
-    if (!right) {
-      v = (i == jj) ? 1.0 : 0.0;
-      if (bi == 0) {
-        if (bj == 0) v = C0[kk * 3 + ii];
-        else if (bj == 1) v = Cdp[ii * 3 + kk];
-        else if (bj == 2) v = C0[kk * 3 + ii] * Dt;
-        else if (bj == 3) v = pre.dpdbg[ii * 3 + kk];
-        else v = -pre.Cdi[ii * 3 + kk];
-      } else if (bi == 1) {
-        if (bj == 1) v = M33a[ii * 3 + kk];
-        else if (bj == 3) v = M33b[ii * 3 + kk];
-      } else if (bi == 2) {
-        if (bj == 1) v = Cdv[ii * 3 + kk];
-        else if (bj == 2) v = C0[kk * 3 + ii];
-        else if (bj == 3) v = pre.dvdbg[ii * 3 + kk];
-        else if (bj == 4) v = -pre.Ci[ii * 3 + kk];
-      }
-    } else {
-      v = (i == jj) ? -1.0 : 0.0;
-      if (bi == 0 && bj == 0) v = -C0[kk * 3 + ii];
-      else if (bi == 1 && bj == 1) v = M33c[ii * 3 + kk];
-      else if (bi == 2 && bj == 2) v = -C0[kk * 3 + ii];
-    }
-    sFF[e] = v;
-  }
-  __syncthreads();
-  // error vector (every lane computes it; 15 doubles)
-  double err[15];
-  {
-    double t0v[3], t6v[3];
-    mtv3(C0, dp, t0v);
-    mtv3(C0, dv, t6v);
-    const Q qe = qmul(Dq, qmul(q1i, q0));
-    for (int k = 0; k < 3; ++k) {
-      // F0.block<3,6>(0,9) * Db = dp_db_g Db_g - C_dint Db_a ; F0.block<3,6>(6,9) * Db = dv_db_g Db_g - C_int Db_a
-      const double e0 = pre.dpdbg[k * 3 + 0] * Db[0] + pre.dpdbg[k * 3 + 1] * Db[1] + pre.dpdbg[k * 3 + 2] * Db[2] -
-                        (pre.Cdi[k * 3 + 0] * Db[3] + pre.Cdi[k * 3 + 1] * Db[4] + pre.Cdi[k * 3 + 2] * Db[5]);
-      const double e6 = pre.dvdbg[k * 3 + 0] * Db[0] + pre.dvdbg[k * 3 + 1] * Db[1] + pre.dvdbg[k * 3 + 2] * Db[2] -
-                        (pre.Ci[k * 3 + 0] * Db[3] + pre.Ci[k * 3 + 1] * Db[4] + pre.Ci[k * 3 + 2] * Db[5]);
-      err[k] = t0v[k] + pre.adi[k] + e0;
-      err[6 + k] = t6v[k] + pre.ai[k] + e6;
-    }
-    err[3] = 2 * qe.x; err[4] = 2 * qe.y; err[5] = 2 * qe.z;
-    for (int k = 0; k < 6; ++k) err[9 + k] = sb0[3 + k] - sb1[3 + k];
-    if (!success)
-      for (int k = 0; k < 15; ++k) err[k] = 0.0;
-  }
-  double* lin = P.imu_lin[lb] + (size_t)f * kImuLin;
+  const size_t fl = live ? (size_t)f : 0;
+  double* lin = P.imu_lin[lb] + fl * kImuLin;
   double rr = 0.0;
-  if (lane < 15) {
-    for (int k = 0; k < 15; ++k) rr += sU[lane * 15 + k] * err[k];
-    lin[lane] = rr;
+  if (live && l < 15) {
+    for (int k = 0; k < 15; ++k) rr += sA[l * 16 + k] * err[k];
+    lin[l] = rr;
   }
-  for (int e = lane; e < 450; e += 64) {
-    const int i = e / 30, j = e % 30;
-    double acc = 0.0;
-    if (success)
-      for (int k = 0; k < 15; ++k) acc += sU[i * 15 + k] * sFF[k * 30 + j];
-    lin[15 + e] = acc;
+  const double c2 = groupSum(l < 15 ? rr * rr : 0.0);
+  if (live && l == 0) P.imu_cost[lb][f] = 0.5 * c2;
+  __syncthreads();
+  // J = U [F0 | F1]; lane l computes columns l and l + 16 of the 15 x 30 Jacobian. Column j of
+  // [F0 | F1] has at most three non-zero 3-blocks: (block row, staged block, sign, or identity).
+  if (live) {
+    for (int pass = 0; pass < 2; ++pass) {
+      const int j = l + 16 * pass;
+      if (j >= 30) break;
+      const bool right = j >= 15;
+      const int jj = right ? j - 15 : j, bj = jj / 3, c = jj % 3;
+      int nt = 0, trow[3], tblk[3];
+      double tsc[3];
+      auto add = [&](int row, int blk, double sc) { trow[nt] = row; tblk[nt] = blk; tsc[nt] = sc; ++nt; };
+      if (!right) {
+        if (bj == 0) add(0, 0, 1.0);
+        else if (bj == 1) { add(0, 1, 1.0); add(3, 2, 1.0); add(6, 3, 1.0); }
+        else if (bj == 2) { add(0, 0, Dt); add(6, 0, 1.0); }
+        else if (bj == 3) { add(0, 4, 1.0); add(3, 5, 1.0); add(6, 6, 1.0); }
+        else { add(0, 7, -1.0); add(6, 8, -1.0); }
+      } else {
+        if (bj == 0) add(0, 0, -1.0);
+        else if (bj == 1) add(3, 9, 1.0);
+        else if (bj == 2) add(6, 0, -1.0);
+      }
+      // identity / minus-identity blocks on the bias rows
+      const int idrow = (bj >= 3) ? 3 * bj + c : -1;
+      const double idv = right ? -1.0 : 1.0;
+      for (int i = 0; i < 15; ++i) {
+        double acc = 0.0;
+        if (success) {
+          for (int t = 0; t < nt; ++t) {
+            const double* Bk = sB + tblk[t] * 9;
+            const double* Ui = sA + i * 16 + trow[t];
+            acc += tsc[t] * (Ui[0] * Bk[0 * 3 + c] + Ui[1] * Bk[1 * 3 + c] + Ui[2] * Bk[2 * 3 + c]);
+          }
+          if (idrow >= 0) acc += idv * sA[i * 16 + idrow];
+        }
+        lin[15 + i * 30 + j] = acc;
+      }
+    }
   }
-  double c2 = (lane < 15) ? rr * rr : 0.0;
-  for (int sh = 32; sh > 0; sh >>= 1) c2 += __shfl_xor(c2, sh, 64);
-  if (lane == 0) P.imu_cost[lb][f] = 0.5 * c2;
 }
 
 // ------------------------------------------------------------------------------------ priors
@@ -689,7 +826,7 @@ void launch_eval_obs(const DevProblem& P, int mode, hipStream_t s) {
   if (P.n_obs > 0) hipLaunchKernelGGL(k_eval_obs, dim3((P.n_obs + 255) / 256), dim3(256), 0, s, P.self, mode);
 }
 void launch_eval_imu(const DevProblem& P, int mode, hipStream_t s) {
-  if (P.n_imu > 0) hipLaunchKernelGGL(k_eval_imu, dim3(P.n_imu), dim3(64), 0, s, P.self, mode);
+  if (P.n_imu > 0) hipLaunchKernelGGL(k_eval_imu, dim3((P.n_imu + kImuPerWG - 1) / kImuPerWG), dim3(64), 0, s, P.self, mode);
 }
 void launch_eval_priors(const DevProblem& P, int mode, hipStream_t s) {
   const int np = P.n_pprior + P.n_sbprior;

@@ -49,6 +49,26 @@ def test_imu_functor_invariants(og, oracle, gpu_ctx):
         assert abs(r[f] @ r[f] - r0[f] @ r0[f]) <= 1e-7 * (r0[f] @ r0[f]) + 1e-12
 
 
+def test_imu_functor_pseudo_inverse(og, oracle, gpu_ctx):
+    """Zero bias random-walk densities make the preintegrated covariance singular, so the
+    square-root information takes the clamped eigen-decomposition branch of
+    PseudoInverse::symmSqrtU (PseudoInverse.hpp:132-158) instead of the Cholesky shortcut."""
+    w = _window(og)
+    p = w.problem
+    p.imu_params.sigma_gw_c = 0.0
+    p.imu_params.sigma_aw_c = 0.0
+    gpu_ctx.set_problems([p])
+    r, J = gpu_ctx.eval_imu(p.n_imu)
+    w.reset()
+    r0, J0 = oracle.eval_imu(w.problem_ptr(), p.n_imu)
+    for f in range(p.n_imu):
+        H, H0 = J[f].T @ J[f], J0[f].T @ J0[f]
+        g, g0 = J[f].T @ r[f], J0[f].T @ r0[f]
+        assert np.linalg.norm(H - H0) <= 1e-6 * np.linalg.norm(H0)
+        assert np.linalg.norm(g - g0) <= 1e-6 * np.linalg.norm(g0) + 1e-9
+        assert abs(r[f] @ r[f] - r0[f] @ r0[f]) <= 1e-6 * (r0[f] @ r0[f]) + 1e-12
+
+
 @pytest.mark.parametrize("mu", [0.0, 1e-8, 1e-2])
 def test_linearize_reduce_parity(og, oracle, gpu_ctx, mu):
     w = _window(og)
