@@ -24,6 +24,8 @@ constexpr int kImuState = 292;        // == OKVISGPU_IMU_STATE_DOUBLES
 // Linearisation record per observation (structure of arrays, plane-major):
 //   plane 0-1: r (Cauchy-corrected)   plane 2-13: J_pose 2x6   plane 14-19: J_lm 2x3
 constexpr int kObsLin = 20;
+constexpr int kVisitLin = 54;
+constexpr int kVisitUY = 42;
 
 // contribution record types for the reduced-system assembly
 enum ContribType : int32_t {
@@ -37,6 +39,7 @@ enum ContribType : int32_t {
 struct Contrib {
   int32_t type, a, b, c;
 };
+
 
 struct WinState {
   double radius, mu;
@@ -112,11 +115,9 @@ struct DevProblem {
   double* lm_g;                    // [n_lm][3]  J_l^T r
   double* lm_Vinv;                 // [n_lm][9]  (s V s + D^2)^-1
   double* lm_z;                    // [n_lm][3]  Vinv (s g)
-  double* visit_W;                 // [n_visit][18] J_p^T J_l (unscaled)
-  double* visit_H;                 // [n_visit][21] J_p^T J_p (unscaled, sym packed)
-  double* visit_g;                 // [n_visit][6]  J_p^T r
-  double* visit_UY;                // [n_visit][36] U = s_p W s_l (6x3) | Y = U Vinv (6x3)   (per GN solve)
-  double* visit_uz;                // [n_visit][6]  U z
+  double* visit_lin;               // [n_visit][kVisitLin] W = J_p^T J_l (18) | H = J_p^T J_p (21, sym packed)
+                                   //   | g = J_p^T r (6) | V part J_l^T J_l (6) | J_l^T r (3)   (unscaled)
+  double* visit_UY;                // [n_visit][kVisitUY] U = s_p W s_l (6x3) | Y = U Vinv (6x3) | U z (6)
 
   // --- IMU factors
   const int32_t* imu_blocks;       // [n_imu][4] global pose0 sb0 pose1 sb1
@@ -167,10 +168,14 @@ struct DevProblem {
   const int32_t* fb_off;           // offset in the window's f-vector
   const int32_t* fb_cbegin;        // [n_fblock+1] gradient / diagonal contributions (C_VISIT, C_IMU, priors)
   const Contrib* fb_contrib;
+  const int32_t* asm_pp_items;      // pose-pose pairs, one per wavefront, XCD-grouped order (-1 = pad)
+  const int32_t* asm_sb_items;      // pairs with a speed/bias block, one per wavefront
+  int32_t n_asm_pp, n_asm_sb;
   const int32_t* pair_win;         // [n_pair]
   const int32_t* pair_fi;          // global f-block index (row, fi >= fj)
   const int32_t* pair_fj;
   const int32_t* pair_cbegin;      // [n_pair+1]
+  const int32_t* pair_runs;        // [n_pair][2] start of the landmark-pair run, start of the factor run
   const Contrib* pair_contrib;
 
   // --- f-vectors (window-concatenated, reduced ordering) and landmark vectors

@@ -215,9 +215,6 @@ __device__ __forceinline__ double groupSum(double v) {  // sum over the 16 lanes
   return v;
 }
 
-__device__ __forceinline__ double sel3(const double* M, int r, int c) {  // M(r, c), c dynamic
-  return c == 0 ? M[r * 3] : (c == 1 ? M[r * 3 + 1] : M[r * 3 + 2]);
-}
 
 // Cyclic Jacobi with round-robin ordering on the 16x16 (15 + decoupled pad) symmetric matrix A of
 // every group with `need` set; V receives the eigenvectors. Uniform control flow over the wave.

@@ -2,18 +2,22 @@
 //
 // The reduced ("camera") system of a window is formed exactly as Ceres' SchurEliminator does for
 // e-blocks = landmarks, but organised for the GPU:
-//   k_lm_blocks   one thread per landmark: per-visit blocks W = J_p^T J_l, H_pp = J_p^T J_p,
-//                 g_p = J_p^T r and per-landmark V = J_l^T J_l, g_l = J_l^T r from the stored
-//                 linearisation (unscaled; the Jacobi scaling is applied by the consumers).
-//   k_fgrad       one thread per f-block (pose / speed-bias): unscaled gradient and diag(H_ff),
-//                 and at iteration 0 the Jacobi scaling 1/(1+sqrt(diag)).
+//   k_visit_lin   one thread per (landmark, pose) visit: W = J_p^T J_l, H_pp = J_p^T J_p,
+//                 g_p = J_p^T r and the visit's share of V = J_l^T J_l, g_l = J_l^T r from the
+//                 stored linearisation (unscaled; the Jacobi scaling is applied by consumers).
+//                 Visit records are AoS, staged through LDS for coalesced stores.
+//   k_lm_lin      one thread per landmark: V, g_l over its visits; iteration 0: Jacobi scaling.
+//   k_fgrad       one wavefront per f-block (pose / speed-bias): unscaled gradient and
+//                 diag(H_ff), and at iteration 0 the Jacobi scaling 1/(1+sqrt(diag)).
 //   k_lm_prep     one thread per landmark: (s V s + D^2)^-1 via 3x3 LLT (InvertPSDMatrix), z.
-//   k_zero_S      clears the dense lower triangle (padded diagonal = 1).
-//   k_assemble    one workgroup per non-zero f-block pair (i >= j): every entry is a fixed-order
-//                 sum over that pair's contribution list — visits, landmark pairs (the
-//                 W_i V^-1 W_j^T Schur terms), IMU / prior J^T J sub-blocks — so the reduction is
+//   k_visit_prep  one thread per visit: U = s_p W s_l, Y = U V^-1, U z.
+//   k_zero_S      clears the structurally non-zero tiles of S (padded diagonal = 1).
+//   k_assemble_pp one wavefront per pose-pose block pair (i >= j), one entry per lane: a
+//                 fixed-order sum over the pair's contributions — visits, landmark pairs (the
+//                 Y_i U_j^T Schur terms), IMU / prior J^T J sub-blocks — so the reduction is
 //                 deterministic without atomics; diagonal pairs also emit the Schur rhs and the
 //                 dogleg diagonal.
+//   k_assemble_sb one wavefront per block pair involving a speed/bias block (one entry per lane).
 //   k_lm_backsub  one thread per landmark: y_l = V^-1 (g_l - W^T y_f).
 //   k_gn_finalize Gauss-Newton step / dogleg gradient in the dogleg-scaled space.
 #include <cfloat>
@@ -40,70 +44,106 @@ __device__ __forceinline__ bool linSelect(const DevProblem& P, int w, int lin_mo
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_lm_blocks(const DevProblem* __restrict__ Pp, int lin_mode) {
+// One thread per (landmark, pose) visit: the 1-2 reprojection residuals of the visit give the
+// pose-landmark blocks W = J_p^T J_l, H = J_p^T J_p, g = J_p^T r and the visit's share of the
+// landmark block (V, J_l^T r). The 64 visit records of a workgroup (contiguous AoS in HBM) are
+// staged in LDS and stored with coalesced writes.
+constexpr int kVisitWG = 64;
+
+__global__ __launch_bounds__(kVisitWG) void k_visit_lin(const DevProblem* __restrict__ Pp, int lin_mode) {
+  const DevProblem& P = *Pp;
+  __shared__ double buf[kVisitWG * kVisitLin];
+  __shared__ int sel[kVisitWG];
+  const int t = threadIdx.x;
+  const int v0 = blockIdx.x * kVisitWG, v = v0 + t;
+  bool act = false;
+  double W[18], H[21], gp[6], V[6], gl[3];
+#pragma unroll
+  for (int i = 0; i < 18; ++i) W[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 21; ++i) H[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) { gp[i] = 0.0; V[i] = 0.0; }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) gl[i] = 0.0;
+  if (v < P.n_visit) {
+    const int l = P.visit_lm[v];
+    const int w = P.lm_win[l];
+    act = linSelect(P, w, lin_mode);
+    if (act) {
+      const bool lfree = P.lm_free[l] != 0;
+      const bool pf = P.pose_f[P.visit_pose[v]] >= 0;
+      const double* lin = P.obs_lin[P.st[w].lcur];
+      const int64_t S = P.obs_stride;
+      for (int o = P.visit_obs_begin[v]; o < P.visit_obs_begin[v + 1]; ++o) {
+        if (P.obs_flags[o] & 2) continue;
+        double r[2], Jp[12], Jl[6];
+        r[0] = lin[0 * S + o];
+        r[1] = lin[1 * S + o];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) Jp[k] = lin[(2 + k) * S + o];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) Jl[k] = lin[(14 + k) * S + o];
+        if (lfree) {
+#pragma unroll
+          for (int a2 = 0; a2 < 3; ++a2) {
+            gl[a2] += Jl[a2] * r[0] + Jl[3 + a2] * r[1];
+#pragma unroll
+            for (int b2 = a2; b2 < 3; ++b2) V[sym3(a2, b2)] += Jl[a2] * Jl[b2] + Jl[3 + a2] * Jl[3 + b2];
+          }
+        }
+        if (pf) {
+#pragma unroll
+          for (int a2 = 0; a2 < 6; ++a2) {
+            gp[a2] += Jp[a2] * r[0] + Jp[6 + a2] * r[1];
+#pragma unroll
+            for (int b2 = a2; b2 < 6; ++b2) H[sym6(a2, b2)] += Jp[a2] * Jp[b2] + Jp[6 + a2] * Jp[6 + b2];
+            if (lfree)
+#pragma unroll
+              for (int b2 = 0; b2 < 3; ++b2) W[a2 * 3 + b2] += Jp[a2] * Jl[b2] + Jp[6 + a2] * Jl[3 + b2];
+          }
+        }
+      }
+    }
+  }
+  double* my = buf + t * kVisitLin;
+#pragma unroll
+  for (int i = 0; i < 18; ++i) my[i] = W[i];
+#pragma unroll
+  for (int i = 0; i < 21; ++i) my[18 + i] = H[i];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) { my[39 + i] = gp[i]; my[45 + i] = V[i]; }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) my[51 + i] = gl[i];
+  sel[t] = act ? 1 : 0;
+  __syncthreads();
+  const int nv = min(kVisitWG, P.n_visit - v0);
+  double* dst = P.visit_lin + (size_t)v0 * kVisitLin;
+  for (int e = t; e < nv * kVisitLin; e += kVisitWG)
+    if (sel[e / kVisitLin]) dst[e] = buf[e];
+}
+
+// One thread per landmark: V = sum over visits, J_l^T r, and (iteration 0) the landmark's Jacobi
+// scaling 1 / (1 + sqrt(diag(V)))  (TrustRegionMinimizer / ScaledJacobian).
+__global__ __launch_bounds__(256) void k_lm_lin(const DevProblem* __restrict__ Pp, int lin_mode) {
   const DevProblem& P = *Pp;
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= P.n_lm) return;
+  if (l >= P.n_lm || !P.lm_free[l]) return;
   const int w = P.lm_win[l];
   if (!linSelect(P, w, lin_mode)) return;
-  const int vb = P.lm_visit_begin[l], ve = P.lm_visit_begin[l + 1];
-  if (vb == ve) return;
-  const int lb = P.st[w].lcur;
-  const bool lfree = P.lm_free[l] != 0;
-  const double* lin = P.obs_lin[lb];
-  const int64_t S = P.obs_stride;
   double V[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-  for (int v = vb; v < ve; ++v) {
-    const bool pf = P.pose_f[P.visit_pose[v]] >= 0;
-    double W[18], H[21], gp[6];
-    for (int i = 0; i < 18; ++i) W[i] = 0.0;
-    for (int i = 0; i < 21; ++i) H[i] = 0.0;
-    for (int i = 0; i < 6; ++i) gp[i] = 0.0;
-    for (int o = P.visit_obs_begin[v]; o < P.visit_obs_begin[v + 1]; ++o) {
-      if (P.obs_flags[o] & 2) continue;
-      double r[2], Jp[12], Jl[6];
-      r[0] = lin[0 * S + o];
-      r[1] = lin[1 * S + o];
+  for (int v = P.lm_visit_begin[l]; v < P.lm_visit_begin[l + 1]; ++v) {
+    const double* src = P.visit_lin + (size_t)v * kVisitLin + 45;
 #pragma unroll
-      for (int k = 0; k < 12; ++k) Jp[k] = lin[(2 + k) * S + o];
+    for (int i = 0; i < 6; ++i) V[i] += src[i];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) Jl[k] = lin[(14 + k) * S + o];
-      if (lfree) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-          g[a] += Jl[a] * r[0] + Jl[3 + a] * r[1];
-#pragma unroll
-          for (int b = a; b < 3; ++b) V[sym3(a, b)] += Jl[a] * Jl[b] + Jl[3 + a] * Jl[3 + b];
-        }
-      }
-      if (pf) {
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-          gp[a] += Jp[a] * r[0] + Jp[6 + a] * r[1];
-#pragma unroll
-          for (int b = a; b < 6; ++b) H[sym6(a, b)] += Jp[a] * Jp[b] + Jp[6 + a] * Jp[6 + b];
-          if (lfree)
-#pragma unroll
-            for (int b = 0; b < 3; ++b) W[a * 3 + b] += Jp[a] * Jl[b] + Jp[6 + a] * Jl[3 + b];
-        }
-      }
-    }
-    if (pf) {
-      double* Wd = P.visit_W + 18 * (size_t)v;
-      double* Hd = P.visit_H + 21 * (size_t)v;
-      double* gd = P.visit_g + 6 * (size_t)v;
-      for (int i = 0; i < 18; ++i) Wd[i] = W[i];
-      for (int i = 0; i < 21; ++i) Hd[i] = H[i];
-      for (int i = 0; i < 6; ++i) gd[i] = gp[i];
-    }
+    for (int i = 0; i < 3; ++i) g[i] += src[6 + i];
   }
-  if (lfree) {
-    for (int i = 0; i < 6; ++i) P.lm_V[6 * (size_t)l + i] = V[i];
-    for (int i = 0; i < 3; ++i) P.lm_g[3 * (size_t)l + i] = g[i];
-    if (lin_mode == 0)  // Jacobi scaling fixed at iteration 0 (TrustRegionMinimizer)
-      for (int a = 0; a < 3; ++a)
-        P.sL[3 * (size_t)l + a] = P.opt.jacobi_scaling ? 1.0 / (1.0 + sqrt(V[sym3(a, a)])) : 1.0;
-  }
+  for (int i = 0; i < 6; ++i) P.lm_V[6 * (size_t)l + i] = V[i];
+  for (int i = 0; i < 3; ++i) P.lm_g[3 * (size_t)l + i] = g[i];
+  if (lin_mode == 0)  // Jacobi scaling fixed at iteration 0 (TrustRegionMinimizer)
+    for (int a = 0; a < 3; ++a)
+      P.sL[3 * (size_t)l + a] = P.opt.jacobi_scaling ? 1.0 / (1.0 + sqrt(V[sym3(a, a)])) : 1.0;
 }
 
 // contribution helpers -------------------------------------------------------------------------
@@ -128,8 +168,8 @@ __global__ __launch_bounds__(64) void k_fgrad(const DevProblem* __restrict__ Pp,
   for (int k = P.fb_cbegin[fb] + lane; k < P.fb_cbegin[fb + 1]; k += 64) {
     const Contrib cb = P.fb_contrib[k];
     if (cb.type == C_VISIT) {
-      const double* H = P.visit_H + 21 * (size_t)cb.a;
-      const double* gp = P.visit_g + 6 * (size_t)cb.a;
+      const double* H = P.visit_lin + (size_t)cb.a * kVisitLin + 18;
+      const double* gp = H + 21;
 #pragma unroll
       for (int c = 0; c < 6; ++c) { g[c] += gp[c]; hd[c] += H[sym6(c, c)]; }
     } else if (cb.type == C_IMU) {
@@ -255,22 +295,61 @@ __global__ __launch_bounds__(256) void k_lm_prep(const DevProblem* __restrict__ 
     z[a] = inv[a * 3 + 0] * sg[0] + inv[a * 3 + 1] * sg[1] + inv[a * 3 + 2] * sg[2];
     P.lm_z[3 * (size_t)l + a] = z[a];
   }
-  // per visit (free pose): U = s_p W s_l, Y = U Vinv, uz = U z — the operands of the Schur terms
-  const int foff = P.win_foff[w];
-  for (int v = P.lm_visit_begin[l]; v < P.lm_visit_begin[l + 1]; ++v) {
-    const int pf = P.pose_f[P.visit_pose[v]];
-    if (pf < 0) continue;
-    const double* W = P.visit_W + 18 * (size_t)v;
-    double* UY = P.visit_UY + 36 * (size_t)v;
-    double* uz = P.visit_uz + 6 * (size_t)v;
-    for (int r = 0; r < 6; ++r) {
-      const double sp = P.sF[(size_t)foff + pf + r];
-      const double u0 = sp * W[r * 3 + 0] * s[0], u1 = sp * W[r * 3 + 1] * s[1], u2 = sp * W[r * 3 + 2] * s[2];
-      UY[r * 3 + 0] = u0; UY[r * 3 + 1] = u1; UY[r * 3 + 2] = u2;
-      for (int b = 0; b < 3; ++b) UY[18 + r * 3 + b] = u0 * inv[0 * 3 + b] + u1 * inv[1 * 3 + b] + u2 * inv[2 * 3 + b];
-      uz[r] = u0 * z[0] + u1 * z[1] + u2 * z[2];
-    }
+}
+
+// One thread per visit with a free pose and landmark: U = s_p W s_l, Y = U Vinv, U z — the
+// operands of the Schur terms. W is staged in / the 42-double records staged out through LDS.
+__global__ __launch_bounds__(kVisitWG) void k_visit_prep(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
+  __shared__ double bufW[kVisitWG * 18];
+  __shared__ double bufO[kVisitWG * kVisitUY];
+  __shared__ int sel[kVisitWG];
+  const int t = threadIdx.x;
+  const int v0 = blockIdx.x * kVisitWG, v = v0 + t;
+  const int nv = min(kVisitWG, P.n_visit - v0);
+  for (int e = t; e < nv * 18; e += kVisitWG) {
+    const int q = e / 18;
+    bufW[e] = P.visit_lin[(size_t)(v0 + q) * kVisitLin + (e - q * 18)];
   }
+  bool act = false;
+  int l = 0, w = 0, pf = -1;
+  if (v < P.n_visit) {
+    l = P.visit_lm[v];
+    w = P.lm_win[l];
+    act = gnSelect(P, w);
+    pf = P.pose_f[P.visit_pose[v]];
+  }
+  __syncthreads();
+  double* out = bufO + t * kVisitUY;
+  if (act && pf >= 0 && P.lm_free[l]) {
+    const double* W = bufW + t * 18;
+    const double* sl = P.sL + 3 * (size_t)l;
+    const double* inv = P.lm_Vinv + 9 * (size_t)l;
+    const double* z = P.lm_z + 3 * (size_t)l;
+    const double s0 = sl[0], s1 = sl[1], s2 = sl[2];
+    double iv[9], zz[3];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) iv[i] = inv[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) zz[i] = z[i];
+    const double* sp = P.sF + (size_t)P.win_foff[w] + pf;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const double spr = sp[r];
+      const double u0 = spr * W[r * 3 + 0] * s0, u1 = spr * W[r * 3 + 1] * s1, u2 = spr * W[r * 3 + 2] * s2;
+      out[r * 3 + 0] = u0; out[r * 3 + 1] = u1; out[r * 3 + 2] = u2;
+#pragma unroll
+      for (int b2 = 0; b2 < 3; ++b2) out[18 + r * 3 + b2] = u0 * iv[0 * 3 + b2] + u1 * iv[1 * 3 + b2] + u2 * iv[2 * 3 + b2];
+      out[36 + r] = u0 * zz[0] + u1 * zz[1] + u2 * zz[2];
+    }
+  } else {
+    for (int i = 0; i < kVisitUY; ++i) out[i] = 0.0;
+  }
+  sel[t] = act ? 1 : 0;
+  __syncthreads();
+  double* dst = P.visit_UY + (size_t)v0 * kVisitUY;
+  for (int e = t; e < nv * kVisitUY; e += kVisitWG)
+    if (sel[e / kVisitUY]) dst[e] = bufO[e];
 }
 
 // Clears the structurally non-zero tiles of S (one workgroup per tile; padded diagonal = 1). Zero
@@ -288,96 +367,171 @@ __global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ P
   }
 }
 
-// One workgroup per non-zero f-block pair; contributions are processed in chunks of 64 whose
-// operands (visit H / uz, or the Y_i, U_j pair of a landmark) are first staged into LDS with
-// coalesced loads, so the per-entry accumulation reads only LDS (no dependent global chains).
-constexpr int kChunk = 64;
-constexpr int kStage = 36;
+// Assembly of the reduced camera matrix S = s (J_f^T J_f - J_f^T J_l V^-1 J_l^T J_f) s + D^2 and of
+// its rhs, one wavefront per block pair (SchurEliminator::Eliminate restated pair-major so that
+// every entry is a fixed-order sum; no atomics).
+//
+// k_assemble_pp: pose-pose pairs; lane e < 36 owns entry (e / 6, e % 6) and sums the pair's
+// contribution runs in list order (visits, landmark pairs, factor blocks). Contribution
+// descriptors are wave-uniform (scalar loads); operand loads of kBatch contributions are issued
+// before they are consumed so that each lane keeps several independent loads in flight.
+constexpr int kBatch = 8;
 
-__global__ __launch_bounds__(128) void k_assemble(const DevProblem* __restrict__ Pp) {
+__global__ __launch_bounds__(256) void k_assemble_pp(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
-  const int k = blockIdx.x;
-  if (k >= P.n_pair) return;
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= P.n_asm_pp) return;
+  const int k = P.asm_pp_items[item];
+  if (k < 0) return;
   const int w = P.pair_win[k];
   if (!gnSelect(P, w)) return;
-  __shared__ double stage[kChunk * kStage];
-  __shared__ Contrib sc[kChunk];
+  const int e = lane < 36 ? lane : 0;
+  const int r = e / 6, q = e - 6 * (e / 6);
+  const int hs = sym6(r, q);
+  const int cb = P.pair_cbegin[k], pb = P.pair_runs[2 * k], ob = P.pair_runs[2 * k + 1], ce = P.pair_cbegin[k + 1];
+  const auto pc = gmem(P.pair_contrib);
+  const auto vlin = gmem(P.visit_lin);
+  const auto vuy = gmem(P.visit_UY);
+  double H = 0.0, schur = 0.0, uz = 0.0;
+  // visits (diagonal pairs): H_v and U_v z_l. Lanes 0..kBatch-1 fetch the batch's descriptors,
+  // readlane makes them wave-uniform; out-of-range slots reuse the first descriptor and are
+  // zero-weighted, so the operand loads are branch-free and issued back to back.
+  for (int c0 = cb; c0 < pb; c0 += kBatch) {
+    const int myc = min(c0 + (lane & (kBatch - 1)), pb - 1);
+    const int ma = pc[myc].a, mb = pc[myc].b;
+    double h[kBatch], z[kBatch];
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u) {
+      const int a = __builtin_amdgcn_readlane(ma, u);
+      h[u] = vlin[(size_t)a * kVisitLin + 18 + hs];
+      z[u] = vuy[(size_t)a * kVisitUY + 36 + (lane & 7) % 6];
+    }
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u) {
+      const bool valid = c0 + u < pb;
+      const bool withz = __builtin_amdgcn_readlane(mb, u) != 0;
+      H += valid ? h[u] : 0.0;
+      uz += (valid && withz) ? z[u] : 0.0;
+    }
+  }
+  // landmark pairs: Y_a U_b^T
+  for (int c0 = pb; c0 < ob; c0 += kBatch) {
+    const int myc = min(c0 + (lane & (kBatch - 1)), ob - 1);
+    const int ma = pc[myc].a, mb = pc[myc].b;
+    double y[kBatch][3], x[kBatch][3];
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u) {
+      const int a = __builtin_amdgcn_readlane(ma, u), b = __builtin_amdgcn_readlane(mb, u);
+      const auto Y = vuy + (size_t)a * kVisitUY + 18 + r * 3;
+      const auto U = vuy + (size_t)b * kVisitUY + q * 3;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        y[u][i] = Y[i];
+        x[u][i] = U[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u) {
+      const double t = y[u][0] * x[u][0] + y[u][1] * x[u][1] + y[u][2] * x[u][2];
+      schur += (c0 + u < ob) ? t : 0.0;
+    }
+  }
+  // factor blocks (IMU, pose prior): J^T J sub-blocks
   const int lb = P.st[w].lcur;
-  const double mu = P.st[w].mu;
+  for (int c = ob; c < ce; ++c) {
+    const Contrib C = P.pair_contrib[c];
+    if (C.type == C_IMU) {
+      const double* L = imuLin(P, lb, C.a) + 15;
+      double s2 = 0;
+      for (int k2 = 0; k2 < 15; ++k2) s2 += L[k2 * 30 + C.b + r] * L[k2 * 30 + C.c + q];
+      H += s2;
+    } else if (C.type == C_PPRIOR) {
+      const double* L = P.pp_lin[lb] + 42 * (size_t)C.a + 6;
+      double s2 = 0;
+      for (int k2 = 0; k2 < 6; ++k2) s2 += L[k2 * 6 + r] * L[k2 * 6 + q];
+      H += s2;
+    }
+  }
+  const int fi = P.pair_fi[k], fj = P.pair_fj[k];
+  const int foff = P.win_foff[w];
+  const int offi = P.fb_off[fi], offj = P.fb_off[fj];
+  const bool diag = fi == fj;
+  if (lane < 36) {
+    const double si = P.sF[(size_t)foff + offi + r], sj = P.sF[(size_t)foff + offj + q];
+    double val = si * sj * H - schur;
+    if (diag && r == q) {
+      const size_t idx = (size_t)foff + offi + r;
+      const double dg = sqrt(fmin(fmax(si * si * P.hdF[idx], P.opt.min_lm_diagonal), P.opt.max_lm_diagonal));
+      P.diagF[idx] = dg;
+      const double d = dg * sqrt(P.st[w].mu);
+      val += d * d;
+    }
+    P.S[P.win_soff[w] + (int64_t)(offi + r) * P.win_fpad[w] + offj + q] = val;
+  }
+  if (diag && lane < 6) {
+    // Schur rhs: s_i g_i - sum_visits U_v z_l
+    const size_t idx = (size_t)foff + offi + lane;
+    P.rhsF[idx] = P.sF[idx] * P.gF[idx] - uz;
+  }
+}
+
+// k_assemble_sb: pairs with a speed/bias block (6x9, 9x9): few contributions (IMU factors,
+// speed/bias priors), one entry per lane.
+__global__ __launch_bounds__(256) void k_assemble_sb(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= P.n_asm_sb) return;
+  const int k = P.asm_sb_items[item];
+  const int w = P.pair_win[k];
+  if (!gnSelect(P, w)) return;
+  const int lb = P.st[w].lcur;
   const int fi = P.pair_fi[k], fj = P.pair_fj[k];
   const int ni = P.fb_kind[fi] == 0 ? 6 : 9, nj = P.fb_kind[fj] == 0 ? 6 : 9;
   const int foff = P.win_foff[w];
   const int offi = P.fb_off[fi], offj = P.fb_off[fj];
-  const int t = threadIdx.x;
+  const bool diag = fi == fj;
   const int cb = P.pair_cbegin[k], ce = P.pair_cbegin[k + 1];
-  const bool entry = t < ni * nj;
-  const int r = entry ? t / nj : 0, c = entry ? t % nj : 0;
-  const bool diag = (fi == fj);
-  double H = 0.0, schur = 0.0, uzacc = 0.0;
-  for (int c0 = cb; c0 < ce; c0 += kChunk) {
-    const int nc = min(kChunk, ce - c0);
-    __syncthreads();
-    if (t < nc) sc[t] = P.pair_contrib[c0 + t];
-    __syncthreads();
-    for (int e = t; e < nc * kStage; e += 128) {
-      const int q = e / kStage, x = e - q * kStage;
-      const Contrib C = sc[q];
-      double v = 0.0;
-      if (C.type == C_PAIR) v = (x < 18) ? P.visit_UY[36 * (size_t)C.a + 18 + x] : P.visit_UY[36 * (size_t)C.b + x - 18];
-      else if (C.type == C_VISIT) v = (x < 21) ? P.visit_H[21 * (size_t)C.a + x]
-                                    : (x < 27 && C.b) ? P.visit_uz[6 * (size_t)C.a + x - 21] : 0.0;
-      stage[e] = v;
-    }
-    __syncthreads();
-    for (int q = 0; q < nc; ++q) {
-      const Contrib C = sc[q];  // uniform across the workgroup
-      const double* st = stage + q * kStage;
-      if (C.type == C_PAIR) {
-        if (entry) schur += st[r * 3 + 0] * st[18 + c * 3 + 0] + st[r * 3 + 1] * st[18 + c * 3 + 1] +
-                            st[r * 3 + 2] * st[18 + c * 3 + 2];
-      } else if (C.type == C_VISIT) {
-        if (entry) H += st[sym6(r, c)];
-        if (diag && t < ni) uzacc += st[21 + t];
-      } else if (C.type == C_IMU) {
-        if (entry) {
-          const double* L = imuLin(P, lb, C.a) + 15;
-          double s2 = 0;
-          for (int k2 = 0; k2 < 15; ++k2) s2 += L[k2 * 30 + C.b + r] * L[k2 * 30 + C.c + c];
-          H += s2;
-        }
-      } else if (C.type == C_PPRIOR) {
-        if (entry) {
-          const double* L = P.pp_lin[lb] + 42 * (size_t)C.a + 6;
-          double s2 = 0;
-          for (int k2 = 0; k2 < 6; ++k2) s2 += L[k2 * 6 + r] * L[k2 * 6 + c];
-          H += s2;
-        }
+  double* S = P.S + P.win_soff[w];
+  const int ld = P.win_fpad[w];
+  const double smu = sqrt(P.st[w].mu);
+  for (int e = lane; e < ni * nj; e += 64) {
+    const int r = e / nj, q = e - r * nj;
+    double H = 0.0;
+    for (int c = cb; c < ce; ++c) {
+      const Contrib C = P.pair_contrib[c];
+      if (C.type == C_IMU) {
+        const double* L = imuLin(P, lb, C.a) + 15;
+        double s2 = 0;
+        for (int k2 = 0; k2 < 15; ++k2) s2 += L[k2 * 30 + C.b + r] * L[k2 * 30 + C.c + q];
+        H += s2;
       } else if (C.type == C_SBPRIOR) {
-        if (entry) {
-          const double* L = P.sbp_lin[lb] + 90 * (size_t)C.a + 9;
-          double s2 = 0;
-          for (int k2 = 0; k2 < 9; ++k2) s2 += L[k2 * 9 + r] * L[k2 * 9 + c];
-          H += s2;
-        }
+        const double* L = P.sbp_lin[lb] + 90 * (size_t)C.a + 9;
+        double s2 = 0;
+        for (int k2 = 0; k2 < 9; ++k2) s2 += L[k2 * 9 + r] * L[k2 * 9 + q];
+        H += s2;
+      } else if (C.type == C_PPRIOR) {
+        const double* L = P.pp_lin[lb] + 42 * (size_t)C.a + 6;
+        double s2 = 0;
+        for (int k2 = 0; k2 < 6; ++k2) s2 += L[k2 * 6 + r] * L[k2 * 6 + q];
+        H += s2;
       }
     }
-  }
-  if (entry) {
-    const double si = P.sF[(size_t)foff + offi + r], sj = P.sF[(size_t)foff + offj + c];
-    double val = si * sj * H - schur;
-    if (diag && r == c) {
-      const double dg = sqrt(fmin(fmax(si * si * P.hdF[(size_t)foff + offi + r], P.opt.min_lm_diagonal),
-                                  P.opt.max_lm_diagonal));
-      P.diagF[(size_t)foff + offi + r] = dg;
-      const double d = dg * sqrt(mu);
+    const double si = P.sF[(size_t)foff + offi + r], sj = P.sF[(size_t)foff + offj + q];
+    double val = si * sj * H;
+    if (diag && r == q) {
+      const size_t idx = (size_t)foff + offi + r;
+      const double dg = sqrt(fmin(fmax(si * si * P.hdF[idx], P.opt.min_lm_diagonal), P.opt.max_lm_diagonal));
+      P.diagF[idx] = dg;
+      const double d = dg * smu;
       val += d * d;
     }
-    P.S[P.win_soff[w] + (int64_t)(offi + r) * P.win_fpad[w] + offj + c] = val;
+    S[(int64_t)(offi + r) * ld + offj + q] = val;
   }
-  if (diag && t < ni) {
-    // Schur rhs: s_i g_i - sum_visits U_v z_l
-    const size_t idx = (size_t)foff + offi + t;
-    P.rhsF[idx] = P.sF[idx] * P.gF[idx] - uzacc;
+  if (diag && lane < ni) {
+    const size_t idx = (size_t)foff + offi + lane;
+    P.rhsF[idx] = P.sF[idx] * P.gF[idx];
   }
 }
 
@@ -395,7 +549,7 @@ __global__ __launch_bounds__(256) void k_lm_backsub(const DevProblem* __restrict
   for (int v = P.lm_visit_begin[l]; v < P.lm_visit_begin[l + 1]; ++v) {
     const int pf = P.pose_f[P.visit_pose[v]];
     if (pf < 0) continue;
-    const double* U = P.visit_UY + 36 * (size_t)v;  // U = s_p W s_l
+    const double* U = P.visit_UY + (size_t)v * kVisitUY;  // U = s_p W s_l
     for (int rr = 0; rr < 6; ++rr) {
       const double y = P.yF[(size_t)foff + pf + rr];
       for (int a = 0; a < 3; ++a) rhs[a] -= U[rr * 3 + a] * y;
@@ -442,7 +596,9 @@ __global__ __launch_bounds__(256) void k_gn_finalize(const DevProblem* __restric
 
 // ------------------------------------------------------------------------------------ launchers
 void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
-  if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_blocks, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P.self, lin_mode);
+  if (P.n_visit > 0)
+    hipLaunchKernelGGL(k_visit_lin, dim3((P.n_visit + kVisitWG - 1) / kVisitWG), dim3(kVisitWG), 0, s, P.self, lin_mode);
+  if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_lin, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P.self, lin_mode);
 }
 void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s) {
   if (P.n_fblock > 0) hipLaunchKernelGGL(k_fgrad, dim3(P.n_fblock), dim3(64), 0, s, P.self, lin_mode);
@@ -453,12 +609,15 @@ void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t 
 }
 void launch_lm_prep(const DevProblem& P, hipStream_t s) {
   if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_prep, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P.self);
+  if (P.n_visit > 0)
+    hipLaunchKernelGGL(k_visit_prep, dim3((P.n_visit + kVisitWG - 1) / kVisitWG), dim3(kVisitWG), 0, s, P.self);
 }
 void launch_zero_S(const DevProblem& P, hipStream_t s) {
   if (P.n_tiles > 0) hipLaunchKernelGGL(k_zero_S, dim3(P.n_tiles), dim3(256), 0, s, P.self);
 }
 void launch_assemble(const DevProblem& P, hipStream_t s) {
-  if (P.n_pair > 0) hipLaunchKernelGGL(k_assemble, dim3(P.n_pair), dim3(128), 0, s, P.self);
+  if (P.n_asm_pp > 0) hipLaunchKernelGGL(k_assemble_pp, dim3((P.n_asm_pp + 3) / 4), dim3(256), 0, s, P.self);
+  if (P.n_asm_sb > 0) hipLaunchKernelGGL(k_assemble_sb, dim3((P.n_asm_sb + 3) / 4), dim3(256), 0, s, P.self);
 }
 void launch_gn_reduce(const DevProblem& P, hipStream_t s) {
   launch_lm_prep(P, s);

@@ -13,6 +13,15 @@
 
 namespace okg {
 
+// Pointers loaded from the device descriptor are generic (flat) to the compiler; re-qualifying
+// them as global lets it emit global_load (vmcnt only) and batch independent loads.
+template <typename T>
+using gptr = const __attribute__((address_space(1))) T*;
+template <typename T>
+__device__ __forceinline__ gptr<T> gmem(const T* p) {
+  return (gptr<T>)p;
+}
+
 struct Q {
   double x, y, z, w;
 };

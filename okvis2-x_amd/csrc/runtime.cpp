@@ -17,6 +17,7 @@
 #include <map>
 #include <memory>
 #include <numeric>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -80,7 +81,8 @@ struct HostBatch {
       win_sbp_range;
   std::vector<int32_t> fb_win, fb_kind, fb_index, fb_off, fb_cbegin;
   std::vector<Contrib> fb_contrib;
-  std::vector<int32_t> pair_win, pair_fi, pair_fj, pair_cbegin;
+  std::vector<int32_t> pair_win, pair_fi, pair_fj, pair_cbegin, pair_runs;
+  std::vector<int32_t> asm_pp_items, asm_sb_items;
   std::vector<int32_t> chol_panel_items, chol_panel_begin, chol_upd_items, chol_upd_begin, tile_items;
   std::vector<Contrib> pair_contrib;
   int64_t s_total = 0, linv_total = 0, fwd_total = 0;
@@ -421,6 +423,20 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       B.pair_fi.push_back(kv.first.first);
       B.pair_fj.push_back(kv.first.second);
       B.pair_cbegin.push_back((int)B.pair_contrib.size());
+      // contributions are grouped by kind (visits, landmark pairs, then factor blocks); the
+      // kernels stream each run separately
+      {
+        const int base = (int)B.pair_contrib.size();
+        int np = 0, nv = 0;
+        for (const Contrib& c : kv.second) { nv += c.type == C_VISIT; np += c.type == C_PAIR; }
+        for (size_t i = 0; i < kv.second.size(); ++i) {
+          const int t = kv.second[i].type;
+          const bool ok = (int)i < nv ? t == C_VISIT : ((int)i < nv + np ? t == C_PAIR : (t != C_VISIT && t != C_PAIR));
+          if (!ok) throw std::logic_error("pair contribution runs out of order");
+        }
+        B.pair_runs.push_back(base + nv);
+        B.pair_runs.push_back(base + nv + np);
+      }
       B.pair_contrib.insert(B.pair_contrib.end(), kv.second.begin(), kv.second.end());
     }
   }
@@ -442,6 +458,31 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
               B.chol_upd_items.push_back(w); B.chol_upd_items.push_back(i); B.chol_upd_items.push_back(j);
             }
     }
+  }
+  // assembly work lists: pose-pose pairs (one wavefront each, 4 per workgroup) are grouped so
+  // that workgroups b, b+8, ... (one XCD under round-robin placement; speed only) walk the pairs of
+  // the same windows and share their visit blocks in that XCD's L2
+  {
+    constexpr int kWavesPerWG = 4, kXcd = 8;
+    const int nq = B.n_win >= kXcd ? kXcd : 1;
+    std::vector<std::vector<int32_t>> q(nq);
+    for (int k = 0; k < (int)B.pair_win.size(); ++k) {
+      const bool pp = B.fb_kind[B.pair_fi[k]] == 0 && B.fb_kind[B.pair_fj[k]] == 0;
+      if (pp) q[B.pair_win[k] % nq].push_back(k);
+      else B.asm_sb_items.push_back(k);
+    }
+    std::vector<size_t> pos(nq, 0);
+    bool more = true;
+    while (more) {
+      more = false;
+      for (int x = 0; x < nq; ++x)
+        for (int i = 0; i < kWavesPerWG; ++i) {
+          const bool has = pos[x] < q[x].size();
+          B.asm_pp_items.push_back(has ? q[x][pos[x]++] : -1);
+        }
+      for (int x = 0; x < nq; ++x) more = more || pos[x] < q[x].size();
+    }
+    while (!B.asm_pp_items.empty() && B.asm_pp_items.back() < 0) B.asm_pp_items.pop_back();
   }
   for (int w = 0; w < B.n_win; ++w) {
     const int T = B.tileT[w];
@@ -575,9 +616,8 @@ struct okvisgpu_ctx {
                  o_vlm = upl(B.visit_lm);
     const size_t o_lmV = scratch(sizeof(double) * 6 * D.n_lm), o_lmg = scratch(sizeof(double) * 3 * D.n_lm),
                  o_lmVi = scratch(sizeof(double) * 9 * D.n_lm), o_lmz = scratch(sizeof(double) * 3 * D.n_lm);
-    const size_t o_vW = scratch(sizeof(double) * 18 * D.n_visit), o_vH = scratch(sizeof(double) * 21 * D.n_visit),
-                 o_vg = scratch(sizeof(double) * 6 * D.n_visit),
-                 o_vUY = scratch(sizeof(double) * 36 * D.n_visit), o_vuz = scratch(sizeof(double) * 6 * D.n_visit);
+    const size_t o_vlin = scratch(sizeof(double) * kVisitLin * D.n_visit),
+                 o_vUY = scratch(sizeof(double) * kVisitUY * D.n_visit);
     const size_t o_imu_blocks = upl(B.imu_blocks), o_imu_win = upl(B.imu_win), o_imu_flags = upl(B.imu_flags),
                  o_imu_t0 = upl(B.imu_t0), o_imu_t1 = upl(B.imu_t1), o_imu_sb = upl(B.imu_sbegin),
                  o_imu_ts = upl(B.imu_ts), o_imu_ga = upl(B.imu_ga), o_imu_par = upl(B.imu_par),
@@ -605,6 +645,8 @@ struct okvisgpu_ctx {
                  o_fbcb = upl(B.fb_cbegin), o_fbc = upl(B.fb_contrib);
     const size_t o_pw = upl(B.pair_win), o_pfi = upl(B.pair_fi), o_pfj = upl(B.pair_fj), o_pcb = upl(B.pair_cbegin),
                  o_pc = upl(B.pair_contrib);
+    const size_t o_pruns = upl(B.pair_runs);
+    const size_t o_app = upl(B.asm_pp_items), o_asb = upl(B.asm_sb_items);
     const size_t o_cpi = upl(B.chol_panel_items), o_cpb = upl(B.chol_panel_begin), o_cui = upl(B.chol_upd_items),
                  o_cub = upl(B.chol_upd_begin), o_ti = upl(B.tile_items);
     const size_t nf = std::max(1, B.f_total), nl3 = std::max<size_t>(1, (size_t)3 * D.n_lm);
@@ -638,8 +680,7 @@ struct okvisgpu_ctx {
     D.obs_cost[0] = dp(o_obs_cost0); D.obs_cost[1] = dp(o_obs_cost1); D.obs_jv = dp(o_obs_jv);
     D.lm_visit_begin = ip(o_lmvb); D.visit_pose = ip(o_vpose); D.visit_obs_begin = ip(o_vob); D.visit_lm = ip(o_vlm);
     D.lm_V = dp(o_lmV); D.lm_g = dp(o_lmg); D.lm_Vinv = dp(o_lmVi); D.lm_z = dp(o_lmz);
-    D.visit_W = dp(o_vW); D.visit_H = dp(o_vH); D.visit_g = dp(o_vg);
-    D.visit_UY = dp(o_vUY); D.visit_uz = dp(o_vuz);
+    D.visit_lin = dp(o_vlin); D.visit_UY = dp(o_vUY);
     D.imu_blocks = ip(o_imu_blocks); D.imu_win = ip(o_imu_win); D.imu_flags = up(o_imu_flags);
     D.imu_t0 = lp(o_imu_t0); D.imu_t1 = lp(o_imu_t1); D.imu_sbegin = ip(o_imu_sb); D.imu_ts = lp(o_imu_ts);
     D.imu_ga = dp(o_imu_ga); D.imu_par = dp(o_imu_par); D.imu_state = dp(o_imu_state);
@@ -659,6 +700,9 @@ struct okvisgpu_ctx {
     D.fb_cbegin = ip(o_fbcb); D.fb_contrib = reinterpret_cast<const Contrib*>(base + o_fbc);
     D.pair_win = ip(o_pw); D.pair_fi = ip(o_pfi); D.pair_fj = ip(o_pfj); D.pair_cbegin = ip(o_pcb);
     D.pair_contrib = reinterpret_cast<const Contrib*>(base + o_pc);
+    D.pair_runs = ip(o_pruns);
+    D.asm_pp_items = ip(o_app); D.asm_sb_items = ip(o_asb);
+    D.n_asm_pp = (int)B.asm_pp_items.size(); D.n_asm_sb = (int)B.asm_sb_items.size();
     D.chol_panel_items = ip(o_cpi); D.chol_panel_begin = ip(o_cpb);
     D.chol_upd_items = ip(o_cui); D.chol_upd_begin = ip(o_cub);
     D.tile_items = ip(o_ti);
