@@ -12,11 +12,11 @@
 //   k_lm_prep     one thread per landmark: (s V s + D^2)^-1 via 3x3 LLT (InvertPSDMatrix), z.
 //   k_visit_prep  one thread per visit: U = s_p W s_l, Y = U V^-1, U z.
 //   k_zero_S      clears the structurally non-zero tiles of S (padded diagonal = 1).
-//   k_assemble_pp one wavefront per pose-pose block pair (i >= j), one entry per lane: a
-//                 fixed-order sum over the pair's contributions — visits, landmark pairs (the
-//                 Y_i U_j^T Schur terms), IMU / prior J^T J sub-blocks — so the reduction is
-//                 deterministic without atomics; diagonal pairs also emit the Schur rhs and the
-//                 dogleg diagonal.
+//   k_assemble_pp one wavefront per pose-pose block pair (i >= j): 8 groups of 6 lanes (one per
+//                 row) sum fixed, interleaved subsets of the pair's contributions — visits,
+//                 landmark pairs (the Y_i U_j^T Schur terms), IMU / prior J^T J sub-blocks — and
+//                 a fixed tree combines the groups, so the sum is deterministic without atomics;
+//                 diagonal pairs also emit the Schur rhs and the dogleg diagonal.
 //   k_assemble_sb one wavefront per block pair involving a speed/bias block (one entry per lane).
 //   k_lm_backsub  one thread per landmark: y_l = V^-1 (g_l - W^T y_f).
 //   k_gn_finalize Gauss-Newton step / dogleg gradient in the dogleg-scaled space.
@@ -371,11 +371,12 @@ __global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ P
 // its rhs, one wavefront per block pair (SchurEliminator::Eliminate restated pair-major so that
 // every entry is a fixed-order sum; no atomics).
 //
-// k_assemble_pp: pose-pose pairs; lane e < 36 owns entry (e / 6, e % 6) and sums the pair's
-// contribution runs in list order (visits, landmark pairs, factor blocks). Contribution
-// descriptors are wave-uniform (scalar loads); operand loads of kBatch contributions are issued
-// before they are consumed so that each lane keeps several independent loads in flight.
-constexpr int kBatch = 8;
+// k_assemble_pp: pose-pose pairs. The wavefront is split into 8 groups of 6 lanes; lane
+// (g, r) accumulates row r of the 6x6 block over the contributions c with (c - run start) % 8 ==
+// g (fixed assignment), then a fixed 3-step tree over the groups sums the rows — deterministic
+// without atomics. Each group loads a contribution's U (or H) once for its 6 lanes plus each lane
+// its own Y row, and two steps of descriptors/operands are in flight per lane.
+constexpr int kGroups = 8;
 
 __global__ __launch_bounds__(256) void k_assemble_pp(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
@@ -386,80 +387,85 @@ __global__ __launch_bounds__(256) void k_assemble_pp(const DevProblem* __restric
   if (k < 0) return;
   const int w = P.pair_win[k];
   if (!gnSelect(P, w)) return;
-  const int e = lane < 36 ? lane : 0;
-  const int r = e / 6, q = e - 6 * (e / 6);
-  const int hs = sym6(r, q);
+  const int g = lane / 6, r = lane - 6 * (lane / 6);
+  const bool inGroup = g < kGroups;
   const int cb = P.pair_cbegin[k], pb = P.pair_runs[2 * k], ob = P.pair_runs[2 * k + 1], ce = P.pair_cbegin[k + 1];
   const auto pc = gmem(P.pair_contrib);
   const auto vlin = gmem(P.visit_lin);
   const auto vuy = gmem(P.visit_UY);
-  double H = 0.0, schur = 0.0, uz = 0.0;
-  // visits (diagonal pairs): H_v and U_v z_l. Lanes 0..kBatch-1 fetch the batch's descriptors,
-  // readlane makes them wave-uniform; out-of-range slots reuse the first descriptor and are
-  // zero-weighted, so the operand loads are branch-free and issued back to back.
-  for (int c0 = cb; c0 < pb; c0 += kBatch) {
-    const int myc = min(c0 + (lane & (kBatch - 1)), pb - 1);
-    const int ma = pc[myc].a, mb = pc[myc].b;
-    double h[kBatch], z[kBatch];
+  double H[6], Sc[6], uz = 0.0;
 #pragma unroll
-    for (int u = 0; u < kBatch; ++u) {
-      const int a = __builtin_amdgcn_readlane(ma, u);
-      h[u] = vlin[(size_t)a * kVisitLin + 18 + hs];
-      z[u] = vuy[(size_t)a * kVisitUY + 36 + (lane & 7) % 6];
-    }
+  for (int q = 0; q < 6; ++q) { H[q] = 0.0; Sc[q] = 0.0; }
+  const int g0 = inGroup ? g : 1 << 29;  // lanes 48..63 idle
+  // visits (diagonal pairs): row r of H_v, and (U_v z_l)_r
+  for (int c0 = cb + g0; c0 < pb; c0 += 2 * kGroups) {
+    const int c1 = c0 + kGroups;
+    const bool v1 = c1 < pb;
+    const Contrib C0 = pc[c0], C1 = pc[v1 ? c1 : c0];
+    const auto H0 = vlin + (size_t)C0.a * kVisitLin + 18, H1 = vlin + (size_t)C1.a * kVisitLin + 18;
+    double h0[6], h1[6];
 #pragma unroll
-    for (int u = 0; u < kBatch; ++u) {
-      const bool valid = c0 + u < pb;
-      const bool withz = __builtin_amdgcn_readlane(mb, u) != 0;
-      H += valid ? h[u] : 0.0;
-      uz += (valid && withz) ? z[u] : 0.0;
+    for (int q = 0; q < 6; ++q) { h0[q] = H0[sym6(r, q)]; h1[q] = H1[sym6(r, q)]; }
+    const double z0 = vuy[(size_t)C0.a * kVisitUY + 36 + r], z1 = vuy[(size_t)C1.a * kVisitUY + 36 + r];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) H[q] += h0[q] + (v1 ? h1[q] : 0.0);
+    uz += (C0.b ? z0 : 0.0) + ((v1 && C1.b) ? z1 : 0.0);
+  }
+  // landmark pairs: row r of Y_a U_b^T
+  for (int c0 = pb + g0; c0 < ob; c0 += 2 * kGroups) {
+    const int c1 = c0 + kGroups;
+    const bool v1 = c1 < ob;
+    const Contrib C0 = pc[c0], C1 = pc[v1 ? c1 : c0];
+    const auto Y0 = vuy + (size_t)C0.a * kVisitUY + 18 + 3 * r, Y1 = vuy + (size_t)C1.a * kVisitUY + 18 + 3 * r;
+    const auto U0 = vuy + (size_t)C0.b * kVisitUY, U1 = vuy + (size_t)C1.b * kVisitUY;
+    double y0[3], y1[3], u0[18], u1[18];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { y0[i] = Y0[i]; y1[i] = Y1[i]; }
+#pragma unroll
+    for (int i = 0; i < 18; ++i) { u0[i] = U0[i]; u1[i] = U1[i]; }
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const double t0 = y0[0] * u0[3 * q] + y0[1] * u0[3 * q + 1] + y0[2] * u0[3 * q + 2];
+      const double t1 = y1[0] * u1[3 * q] + y1[1] * u1[3 * q + 1] + y1[2] * u1[3 * q + 2];
+      Sc[q] += t0 + (v1 ? t1 : 0.0);
     }
   }
-  // landmark pairs: Y_a U_b^T
-  for (int c0 = pb; c0 < ob; c0 += kBatch) {
-    const int myc = min(c0 + (lane & (kBatch - 1)), ob - 1);
-    const int ma = pc[myc].a, mb = pc[myc].b;
-    double y[kBatch][3], x[kBatch][3];
-#pragma unroll
-    for (int u = 0; u < kBatch; ++u) {
-      const int a = __builtin_amdgcn_readlane(ma, u), b = __builtin_amdgcn_readlane(mb, u);
-      const auto Y = vuy + (size_t)a * kVisitUY + 18 + r * 3;
-      const auto U = vuy + (size_t)b * kVisitUY + q * 3;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        y[u][i] = Y[i];
-        x[u][i] = U[i];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kBatch; ++u) {
-      const double t = y[u][0] * x[u][0] + y[u][1] * x[u][1] + y[u][2] * x[u][2];
-      schur += (c0 + u < ob) ? t : 0.0;
-    }
-  }
-  // factor blocks (IMU, pose prior): J^T J sub-blocks
+  // factor blocks (IMU, pose prior): row r of J_i^T J_j
   const int lb = P.st[w].lcur;
-  for (int c = ob; c < ce; ++c) {
-    const Contrib C = P.pair_contrib[c];
-    if (C.type == C_IMU) {
-      const double* L = imuLin(P, lb, C.a) + 15;
-      double s2 = 0;
-      for (int k2 = 0; k2 < 15; ++k2) s2 += L[k2 * 30 + C.b + r] * L[k2 * 30 + C.c + q];
-      H += s2;
-    } else if (C.type == C_PPRIOR) {
-      const double* L = P.pp_lin[lb] + 42 * (size_t)C.a + 6;
-      double s2 = 0;
-      for (int k2 = 0; k2 < 6; ++k2) s2 += L[k2 * 6 + r] * L[k2 * 6 + q];
-      H += s2;
+  for (int c = ob + g0; c < ce; c += kGroups) {
+    const Contrib C = pc[c];
+    const double* L;
+    int rows, ld, ci, cj;
+    if (C.type == C_IMU) { L = imuLin(P, lb, C.a) + 15; rows = 15; ld = 30; ci = C.b; cj = C.c; }
+    else { L = P.pp_lin[lb] + 42 * (size_t)C.a + 6; rows = 6; ld = 6; ci = 0; cj = 0; }
+    for (int k2 = 0; k2 < rows; ++k2) {
+      const double jr = L[k2 * ld + ci + r];
+#pragma unroll
+      for (int q = 0; q < 6; ++q) H[q] += jr * L[k2 * ld + cj + q];
     }
   }
+  // fixed tree over the groups: g += g + 4, g += g + 2, g += g + 1
+#pragma unroll
+  for (int d = 4; d >= 1; d >>= 1) {
+    const int src = min(lane + 6 * d, 63);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      H[q] += __shfl(H[q], src, 64);
+      Sc[q] += __shfl(Sc[q], src, 64);
+    }
+    uz += __shfl(uz, src, 64);
+  }
+  if (lane >= 6) return;
   const int fi = P.pair_fi[k], fj = P.pair_fj[k];
   const int foff = P.win_foff[w];
   const int offi = P.fb_off[fi], offj = P.fb_off[fj];
   const bool diag = fi == fj;
-  if (lane < 36) {
-    const double si = P.sF[(size_t)foff + offi + r], sj = P.sF[(size_t)foff + offj + q];
-    double val = si * sj * H - schur;
+  const double si = P.sF[(size_t)foff + offi + r];
+  double* Srow = P.S + P.win_soff[w] + (int64_t)(offi + r) * P.win_fpad[w] + offj;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const double sj = P.sF[(size_t)foff + offj + q];
+    double val = si * sj * H[q] - Sc[q];
     if (diag && r == q) {
       const size_t idx = (size_t)foff + offi + r;
       const double dg = sqrt(fmin(fmax(si * si * P.hdF[idx], P.opt.min_lm_diagonal), P.opt.max_lm_diagonal));
@@ -467,11 +473,11 @@ __global__ __launch_bounds__(256) void k_assemble_pp(const DevProblem* __restric
       const double d = dg * sqrt(P.st[w].mu);
       val += d * d;
     }
-    P.S[P.win_soff[w] + (int64_t)(offi + r) * P.win_fpad[w] + offj + q] = val;
+    Srow[q] = val;
   }
-  if (diag && lane < 6) {
+  if (diag) {
     // Schur rhs: s_i g_i - sum_visits U_v z_l
-    const size_t idx = (size_t)foff + offi + lane;
+    const size_t idx = (size_t)foff + offi + r;
     P.rhsF[idx] = P.sF[idx] * P.gF[idx] - uz;
   }
 }

@@ -15,8 +15,13 @@ namespace okg {
 
 // Pointers loaded from the device descriptor are generic (flat) to the compiler; re-qualifying
 // them as global lets it emit global_load (vmcnt only) and batch independent loads.
+#if defined(__HIP_DEVICE_COMPILE__)
 template <typename T>
 using gptr = const __attribute__((address_space(1))) T*;
+#else
+template <typename T>
+using gptr = const T*;
+#endif
 template <typename T>
 __device__ __forceinline__ gptr<T> gmem(const T* p) {
   return (gptr<T>)p;
