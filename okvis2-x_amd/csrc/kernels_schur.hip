@@ -5,7 +5,6 @@
 //   k_visit_lin   one thread per (landmark, pose) visit: W = J_p^T J_l, H_pp = J_p^T J_p,
 //                 g_p = J_p^T r and the visit's share of V = J_l^T J_l, g_l = J_l^T r from the
 //                 stored linearisation (unscaled; the Jacobi scaling is applied by consumers).
-//                 Visit records are AoS, staged through LDS for coalesced stores.
 //   k_lm_lin      one thread per landmark: V, g_l over its visits; iteration 0: Jacobi scaling.
 //   k_fgrad       one wavefront per f-block (pose / speed-bias): unscaled gradient and
 //                 diag(H_ff), and at iteration 0 the Jacobi scaling 1/(1+sqrt(diag)).
@@ -46,81 +45,53 @@ __device__ __forceinline__ bool linSelect(const DevProblem& P, int w, int lin_mo
 
 // One thread per (landmark, pose) visit: the 1-2 reprojection residuals of the visit give the
 // pose-landmark blocks W = J_p^T J_l, H = J_p^T J_p, g = J_p^T r and the visit's share of the
-// landmark block (V, J_l^T r). The 64 visit records of a workgroup (contiguous AoS in HBM) are
-// staged in LDS and stored with coalesced writes.
-constexpr int kVisitWG = 64;
-
-__global__ __launch_bounds__(kVisitWG) void k_visit_lin(const DevProblem* __restrict__ Pp, int lin_mode) {
+// landmark block (V, J_l^T r): one 54-double AoS record per visit (16-byte stores, merged in L2).
+__global__ __launch_bounds__(256) void k_visit_lin(const DevProblem* __restrict__ Pp, int lin_mode) {
   const DevProblem& P = *Pp;
-  __shared__ double buf[kVisitWG * kVisitLin];
-  __shared__ int sel[kVisitWG];
-  const int t = threadIdx.x;
-  const int v0 = blockIdx.x * kVisitWG, v = v0 + t;
-  bool act = false;
-  double W[18], H[21], gp[6], V[6], gl[3];
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= P.n_visit) return;
+  const int l = P.visit_lm[v];
+  const int w = P.lm_win[l];
+  if (!linSelect(P, w, lin_mode)) return;
+  double o[kVisitLin];  // W 0..17 | H 18..38 | g 39..44 | V 45..50 | g_l 51..53
 #pragma unroll
-  for (int i = 0; i < 18; ++i) W[i] = 0.0;
+  for (int i = 0; i < kVisitLin; ++i) o[i] = 0.0;
+  const bool lfree = P.lm_free[l] != 0;
+  const bool pf = P.pose_f[P.visit_pose[v]] >= 0;
+  const auto lin = gmem(P.obs_lin[P.st[w].lcur]);
+  const int64_t S = P.obs_stride;
+  for (int ob = P.visit_obs_begin[v]; ob < P.visit_obs_begin[v + 1]; ++ob) {
+    if (P.obs_flags[ob] & 2) continue;
+    double r[2], Jp[12], Jl[6];
+    r[0] = lin[0 * S + ob];
+    r[1] = lin[1 * S + ob];
 #pragma unroll
-  for (int i = 0; i < 21; ++i) H[i] = 0.0;
+    for (int k = 0; k < 12; ++k) Jp[k] = lin[(2 + k) * S + ob];
 #pragma unroll
-  for (int i = 0; i < 6; ++i) { gp[i] = 0.0; V[i] = 0.0; }
+    for (int k = 0; k < 6; ++k) Jl[k] = lin[(14 + k) * S + ob];
+    if (lfree) {
 #pragma unroll
-  for (int i = 0; i < 3; ++i) gl[i] = 0.0;
-  if (v < P.n_visit) {
-    const int l = P.visit_lm[v];
-    const int w = P.lm_win[l];
-    act = linSelect(P, w, lin_mode);
-    if (act) {
-      const bool lfree = P.lm_free[l] != 0;
-      const bool pf = P.pose_f[P.visit_pose[v]] >= 0;
-      const double* lin = P.obs_lin[P.st[w].lcur];
-      const int64_t S = P.obs_stride;
-      for (int o = P.visit_obs_begin[v]; o < P.visit_obs_begin[v + 1]; ++o) {
-        if (P.obs_flags[o] & 2) continue;
-        double r[2], Jp[12], Jl[6];
-        r[0] = lin[0 * S + o];
-        r[1] = lin[1 * S + o];
+      for (int a2 = 0; a2 < 3; ++a2) {
+        o[51 + a2] += Jl[a2] * r[0] + Jl[3 + a2] * r[1];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) Jp[k] = lin[(2 + k) * S + o];
+        for (int b2 = a2; b2 < 3; ++b2) o[45 + sym3(a2, b2)] += Jl[a2] * Jl[b2] + Jl[3 + a2] * Jl[3 + b2];
+      }
+    }
+    if (pf) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) Jl[k] = lin[(14 + k) * S + o];
-        if (lfree) {
+      for (int a2 = 0; a2 < 6; ++a2) {
+        o[39 + a2] += Jp[a2] * r[0] + Jp[6 + a2] * r[1];
 #pragma unroll
-          for (int a2 = 0; a2 < 3; ++a2) {
-            gl[a2] += Jl[a2] * r[0] + Jl[3 + a2] * r[1];
+        for (int b2 = a2; b2 < 6; ++b2) o[18 + sym6(a2, b2)] += Jp[a2] * Jp[b2] + Jp[6 + a2] * Jp[6 + b2];
+        if (lfree)
 #pragma unroll
-            for (int b2 = a2; b2 < 3; ++b2) V[sym3(a2, b2)] += Jl[a2] * Jl[b2] + Jl[3 + a2] * Jl[3 + b2];
-          }
-        }
-        if (pf) {
-#pragma unroll
-          for (int a2 = 0; a2 < 6; ++a2) {
-            gp[a2] += Jp[a2] * r[0] + Jp[6 + a2] * r[1];
-#pragma unroll
-            for (int b2 = a2; b2 < 6; ++b2) H[sym6(a2, b2)] += Jp[a2] * Jp[b2] + Jp[6 + a2] * Jp[6 + b2];
-            if (lfree)
-#pragma unroll
-              for (int b2 = 0; b2 < 3; ++b2) W[a2 * 3 + b2] += Jp[a2] * Jl[b2] + Jp[6 + a2] * Jl[3 + b2];
-          }
-        }
+          for (int b2 = 0; b2 < 3; ++b2) o[a2 * 3 + b2] += Jp[a2] * Jl[b2] + Jp[6 + a2] * Jl[3 + b2];
       }
     }
   }
-  double* my = buf + t * kVisitLin;
+  double2* out = reinterpret_cast<double2*>(P.visit_lin + (size_t)v * kVisitLin);
 #pragma unroll
-  for (int i = 0; i < 18; ++i) my[i] = W[i];
-#pragma unroll
-  for (int i = 0; i < 21; ++i) my[18 + i] = H[i];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) { my[39 + i] = gp[i]; my[45 + i] = V[i]; }
-#pragma unroll
-  for (int i = 0; i < 3; ++i) my[51 + i] = gl[i];
-  sel[t] = act ? 1 : 0;
-  __syncthreads();
-  const int nv = min(kVisitWG, P.n_visit - v0);
-  double* dst = P.visit_lin + (size_t)v0 * kVisitLin;
-  for (int e = t; e < nv * kVisitLin; e += kVisitWG)
-    if (sel[e / kVisitLin]) dst[e] = buf[e];
+  for (int i = 0; i < kVisitLin / 2; ++i) out[i] = double2{o[2 * i], o[2 * i + 1]};
 }
 
 // One thread per landmark: V = sum over visits, J_l^T r, and (iteration 0) the landmark's Jacobi
@@ -298,58 +269,47 @@ __global__ __launch_bounds__(256) void k_lm_prep(const DevProblem* __restrict__ 
 }
 
 // One thread per visit with a free pose and landmark: U = s_p W s_l, Y = U Vinv, U z — the
-// operands of the Schur terms. W is staged in / the 42-double records staged out through LDS.
-__global__ __launch_bounds__(kVisitWG) void k_visit_prep(const DevProblem* __restrict__ Pp) {
+// operands of the Schur terms (42-double AoS records; 16-byte stores, merged in L2).
+__global__ __launch_bounds__(256) void k_visit_prep(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
-  __shared__ double bufW[kVisitWG * 18];
-  __shared__ double bufO[kVisitWG * kVisitUY];
-  __shared__ int sel[kVisitWG];
-  const int t = threadIdx.x;
-  const int v0 = blockIdx.x * kVisitWG, v = v0 + t;
-  const int nv = min(kVisitWG, P.n_visit - v0);
-  for (int e = t; e < nv * 18; e += kVisitWG) {
-    const int q = e / 18;
-    bufW[e] = P.visit_lin[(size_t)(v0 + q) * kVisitLin + (e - q * 18)];
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v >= P.n_visit) return;
+  const int l = P.visit_lm[v];
+  const int w = P.lm_win[l];
+  if (!gnSelect(P, w)) return;
+  const int pf = P.pose_f[P.visit_pose[v]];
+  double2* out = reinterpret_cast<double2*>(P.visit_UY + (size_t)v * kVisitUY);
+  if (pf < 0 || !P.lm_free[l]) {
+#pragma unroll
+    for (int i = 0; i < kVisitUY / 2; ++i) out[i] = double2{0.0, 0.0};
+    return;
   }
-  bool act = false;
-  int l = 0, w = 0, pf = -1;
-  if (v < P.n_visit) {
-    l = P.visit_lm[v];
-    w = P.lm_win[l];
-    act = gnSelect(P, w);
-    pf = P.pose_f[P.visit_pose[v]];
+  const auto W = gmem(P.visit_lin + (size_t)v * kVisitLin);
+  const auto sl = gmem(P.sL + 3 * (size_t)l);
+  const auto inv = gmem(P.lm_Vinv + 9 * (size_t)l);
+  const auto z = gmem(P.lm_z + 3 * (size_t)l);
+  const auto sp = gmem(P.sF + (size_t)P.win_foff[w] + pf);
+  double w18[18], iv[9], zz[3], s3[3], spr[6];
+#pragma unroll
+  for (int i = 0; i < 18; ++i) w18[i] = W[i];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) iv[i] = inv[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) { zz[i] = z[i]; s3[i] = sl[i]; }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) spr[i] = sp[i];
+  double o[kVisitUY];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const double u0 = spr[r] * w18[r * 3 + 0] * s3[0], u1 = spr[r] * w18[r * 3 + 1] * s3[1],
+                 u2 = spr[r] * w18[r * 3 + 2] * s3[2];
+    o[r * 3 + 0] = u0; o[r * 3 + 1] = u1; o[r * 3 + 2] = u2;
+#pragma unroll
+    for (int b2 = 0; b2 < 3; ++b2) o[18 + r * 3 + b2] = u0 * iv[0 * 3 + b2] + u1 * iv[1 * 3 + b2] + u2 * iv[2 * 3 + b2];
+    o[36 + r] = u0 * zz[0] + u1 * zz[1] + u2 * zz[2];
   }
-  __syncthreads();
-  double* out = bufO + t * kVisitUY;
-  if (act && pf >= 0 && P.lm_free[l]) {
-    const double* W = bufW + t * 18;
-    const double* sl = P.sL + 3 * (size_t)l;
-    const double* inv = P.lm_Vinv + 9 * (size_t)l;
-    const double* z = P.lm_z + 3 * (size_t)l;
-    const double s0 = sl[0], s1 = sl[1], s2 = sl[2];
-    double iv[9], zz[3];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) iv[i] = inv[i];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) zz[i] = z[i];
-    const double* sp = P.sF + (size_t)P.win_foff[w] + pf;
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      const double spr = sp[r];
-      const double u0 = spr * W[r * 3 + 0] * s0, u1 = spr * W[r * 3 + 1] * s1, u2 = spr * W[r * 3 + 2] * s2;
-      out[r * 3 + 0] = u0; out[r * 3 + 1] = u1; out[r * 3 + 2] = u2;
-#pragma unroll
-      for (int b2 = 0; b2 < 3; ++b2) out[18 + r * 3 + b2] = u0 * iv[0 * 3 + b2] + u1 * iv[1 * 3 + b2] + u2 * iv[2 * 3 + b2];
-      out[36 + r] = u0 * zz[0] + u1 * zz[1] + u2 * zz[2];
-    }
-  } else {
-    for (int i = 0; i < kVisitUY; ++i) out[i] = 0.0;
-  }
-  sel[t] = act ? 1 : 0;
-  __syncthreads();
-  double* dst = P.visit_UY + (size_t)v0 * kVisitUY;
-  for (int e = t; e < nv * kVisitUY; e += kVisitWG)
-    if (sel[e / kVisitUY]) dst[e] = bufO[e];
+  for (int i = 0; i < kVisitUY / 2; ++i) out[i] = double2{o[2 * i], o[2 * i + 1]};
 }
 
 // Clears the structurally non-zero tiles of S (one workgroup per tile; padded diagonal = 1). Zero
@@ -603,7 +563,7 @@ __global__ __launch_bounds__(256) void k_gn_finalize(const DevProblem* __restric
 // ------------------------------------------------------------------------------------ launchers
 void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
   if (P.n_visit > 0)
-    hipLaunchKernelGGL(k_visit_lin, dim3((P.n_visit + kVisitWG - 1) / kVisitWG), dim3(kVisitWG), 0, s, P.self, lin_mode);
+    hipLaunchKernelGGL(k_visit_lin, dim3((P.n_visit + 255) / 256), dim3(256), 0, s, P.self, lin_mode);
   if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_lin, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P.self, lin_mode);
 }
 void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s) {
@@ -616,7 +576,7 @@ void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t 
 void launch_lm_prep(const DevProblem& P, hipStream_t s) {
   if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_prep, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P.self);
   if (P.n_visit > 0)
-    hipLaunchKernelGGL(k_visit_prep, dim3((P.n_visit + kVisitWG - 1) / kVisitWG), dim3(kVisitWG), 0, s, P.self);
+    hipLaunchKernelGGL(k_visit_prep, dim3((P.n_visit + 255) / 256), dim3(256), 0, s, P.self);
 }
 void launch_zero_S(const DevProblem& P, hipStream_t s) {
   if (P.n_tiles > 0) hipLaunchKernelGGL(k_zero_S, dim3(P.n_tiles), dim3(256), 0, s, P.self);
