@@ -63,33 +63,74 @@ def ate(P, gt):
     return float(np.sqrt(np.mean(np.sum((aligned - b) ** 2, axis=1))))
 
 
-def chol_update_flops(fdims, n_tiles):
-    """Algorithmic FLOPs of all k_chol_update launches of one GN iteration (2*64^3 per tile)."""
-    tot = 0
-    for fd in fdims:
-        T = (fd + 63) // 64
-        for k in range(T):
-            m = T - k - 1
-            tot += m * (m + 1) // 2 * 2 * 64 ** 3
-    return tot
+# kernels timed for the roofline table (include/okvisgpu.h okvisgpu_time_kernel)
+ROOFLINE_KERNELS = ["k_assemble_pp", "k_assemble_sb", "k_chol_update", "k_potrf_inv", "k_panel", "k_visit_lin",
+                    "k_visit_prep", "k_eval_imu", "k_eval_obs", "k_jv", "k_trsv", "k_fgrad"]
+PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
 
-def run_cpu_baseline(cfg, iters, threads, reps):
-    """Oracle (CPU restatement, `port`) on window 0, same protocol; median of `reps` runs after one
-    warm-up. Bounded sample: one window."""
+def rank_windows(total, world, rank):
+    """This rank's share of the fixed total window count (strong scaling)."""
+    per = [total // world + (1 if r < total % world else 0) for r in range(world)]
+    start = sum(per[:rank])
+    return list(range(start, start + per[rank]))
+
+
+def aggregate(dist, elapsed, early, device):
+    """Max of the timed region over ranks, sum of early-terminated windows (the only exchange)."""
+    if dist is None:
+        return elapsed, early
+    import torch
+    t = torch.tensor([elapsed, float(early)], dtype=torch.float64, device=device)
+    tmax, tsum = t.clone(), t.clone()
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+    return float(tmax[0].item()), int(tsum[1].item())
+
+
+def roofline_table(ctx, reps):
+    """Per-kernel device time (HIP events on the context's stream, `reps` back-to-back launches of
+    one iteration's worth on the resident data) and achieved rate of its algorithmic work."""
+    table = {}
+    for name in ROOFLINE_KERNELS:
+        ms, work, bound = ctx.time_kernel(name, reps)
+        rate = work / (ms * 1e-3) / (1e9 if bound == "hbm" else 1e12) if ms > 0 else 0.0
+        peak = HBM_PEAK_GBS if bound == "hbm" else FP64_MFMA_PEAK_TFLOPS
+        table[name] = {"ms": ms, "bound": bound, "work": work, "achieved": rate, "peak": peak, "frac": rate / peak}
+    return table
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per iteration of `kernel` from the committed rocprofv3 --pmc summary
+    (scripts/pmc_traffic.py: FETCH_SIZE x 2 per the gfx950 calibration + WRITE_SIZE), or None."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            d = json.load(f)
+        return d["kernels"][kernel]["bytes_per_iteration"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def run_cpu_baseline(cfg, iters, threads, n_windows, reps):
+    """Oracle (CPU restatement, `port`) on the first `n_windows` windows of the workload, same
+    options and iteration count; median over `reps` timed passes after one warm-up pass. Bounded
+    sample of the same workload, reported in the metric's unit (window-iterations/s)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import _oracle  # noqa: E402  (bench.py's cpu_baseline leg is an allowed oracle user)
-    w = make_windows(cfg, [0])[0]
+    ws = make_windows(cfg, range(n_windows))
     opts = bench_options(iters)
     opts.num_threads = threads
-    times = []
+    times, s0 = [], None
     for r in range(reps + 1):
-        w.reset()
         t0 = time.perf_counter()
-        s = _oracle.solve(w.problem_ptr(), opts)
+        for i, w in enumerate(ws):
+            w.reset()
+            s = _oracle.solve(w.problem_ptr(), opts)
+            if i == 0:
+                s0 = s
         if r > 0:
             times.append(time.perf_counter() - t0)
-    return w, s, float(np.median(times))
+    return ws[0], s0, float(np.median(times))
 
 
 def main():
@@ -101,7 +142,9 @@ def main():
     ap.add_argument("--config", default="s50", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-threads", type=int, default=3, help="realtime_num_threads (okvis2.yaml:93)")
     ap.add_argument("--cpu-iters", type=int, default=None, help="default: warmup + steps")
-    ap.add_argument("--cpu-reps", type=int, default=5, help="median of this many timed runs after 1 warm-up")
+    ap.add_argument("--cpu-reps", type=int, default=3, help="median of this many timed passes after 1 warm-up")
+    ap.add_argument("--cpu-windows", type=int, default=8, help="windows in the CPU baseline sample")
+    ap.add_argument("--kernel-reps", type=int, default=5, help="repetitions per kernel in the roofline table")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
@@ -110,21 +153,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
     dist = None
     if world > 1:
-        import torch
         import torch.distributed as tdist
         torch.cuda.set_device(local_rank)
         tdist.init_process_group("nccl")
         dist = tdist
-    else:
-        import torch
     cfg = CONFIGS[args.config]
 
     # ---- this rank's share of the fixed total (strong scaling)
-    per = [args.windows // world + (1 if r < args.windows % world else 0) for r in range(world)]
-    start = sum(per[:rank])
-    mine = list(range(start, start + per[rank]))
+    mine = rank_windows(args.windows, world, rank)
     windows = make_windows(cfg, mine)
     ctx = og.Context(local_rank)
     ctx.set_problems([w.problem for w in windows])
@@ -148,13 +187,7 @@ def main():
     elapsed = t1 - t0
     early = sum(1 for s in sums if s["num_iterations"] < total_iters)
     gn_frac = float(np.mean([(s["num_successful_steps"] - 1) / max(1, s["num_iterations"]) for s in sums]))
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        e = torch.tensor([early], dtype=torch.float64, device=f"cuda:{local_rank}")
-        dist.all_reduce(e, op=dist.ReduceOp.SUM)
-        early = int(e.item())
+    elapsed, early = aggregate(dist, elapsed, early, f"cuda:{local_rank}")
 
     value = args.windows * args.steps / elapsed
     result = {
@@ -175,7 +208,7 @@ def main():
                         f"({cfg['n_kf']} KF / {cfg['n_lm']} landmarks / {cfg['n_obs']} reprojections, "
                         f"{cfg['n_kf'] - 1} IMU factors), DENSE_SCHUR + DOGLEG, all tolerances 0",
             "windows_total": args.windows,
-            "windows_per_gpu": per[rank],
+            "windows_per_gpu": len(mine),
             "parallelism": f"replicas x{world} (one window batch per GPU, no collective in the loop)",
         },
     }
@@ -211,55 +244,34 @@ def main():
                 c1.solve_end(1)
                 result["single_window"]["kernel_ms_per_iteration"] = {k: round(v, 4) for k, v in ph1.items()}
             c1.close()
-        # ---- per-kernel device time of one iteration + roofline of the dominant kernel
+        # ---- roofline: per-kernel device time on the resident batch, dominant kernel by time
         if not args.no_profile:
-            cp = og.Context(local_rank)
-            cp.set_problems([w.problem for w in windows])
-            for w in windows:
-                w.reset()
-            cp.update_params()
-            cp.solve_begin(opts)
-            cp.solve_iterate(args.warmup)
-            ph = cp.profile_iteration()
-            cp.solve_end(len(windows))
-            cp.close()
-            result["kernel_ms_per_iteration"] = {k: round(v, 4) for k, v in ph.items()}
-            fdims = [15 * cfg["n_kf"]] * len(windows)
-            flops = chol_update_flops(fdims, None)
-            upd_ms = ph["chol_update"]
-            n_launch = (fdims[0] + 63) // 64 - 1
-            dominant = max(ph, key=ph.get)
+            table = roofline_table(ctx, args.kernel_reps)
+            dominant = max(table, key=lambda k: table[k]["ms"])
+            d = table[dominant]
+            traffic = pmc_traffic(dominant)
             result["roofline"] = {
-                "kernel": "k_chol_update (reduced-camera block multiply, v_mfma_f64_16x16x4_f64)",
-                "bound": "mfma",
-                "achieved": flops / (upd_ms * 1e-3) / 1e12 if upd_ms > 0 else None,
-                "peak": FP64_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": (flops / (upd_ms * 1e-3) / 1e12) / FP64_MFMA_PEAK_TFLOPS if upd_ms > 0 else None,
-                "traffic": None,
-                "flops_per_iteration": flops,
-                "launches_per_iteration": n_launch,
-                "avg_launch_ms": upd_ms / max(1, n_launch),
-                "dominant_kernel_by_time": dominant,
+                "kernel": dominant, "bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"],
+                "unit": "GB/s" if d["bound"] == "hbm" else "TFLOP/s", "frac": d["frac"],
+                "traffic": traffic,
+                "work_per_iteration": d["work"], "ms_per_iteration": d["ms"],
+                "method": f"HIP events on the context stream, {args.kernel_reps} launches of one iteration's "
+                          "worth on the resident batch; work = algorithmic bytes/FLOPs (DESIGN.md §4); traffic = "
+                          "rocprofv3 --pmc HBM bytes per iteration from profiles/pmc_traffic.json",
             }
-            # eval kernel: algorithmic HBM bytes per observation
-            eo = ph["eval_obs"]
-            n_obs = cfg["n_obs"] * len(windows)
-            bytes_obs = n_obs * (2 * 8 + 4 * 8 + 3 * 4 + 1 + 20 * 8 + 8)
-            result["roofline_eval_obs"] = {"bound": "hbm", "achieved": bytes_obs / (eo * 1e-3) / 1e9 if eo > 0 else None,
-                                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                           "frac": bytes_obs / (eo * 1e-3) / 1e9 / HBM_PEAK_GBS if eo > 0 else None,
-                                           "bytes_per_launch": bytes_obs}
+            result["kernels"] = {k: {"ms": round(v["ms"], 4), "bound": v["bound"], "achieved": round(v["achieved"], 2),
+                                     "frac": round(v["frac"], 4)} for k, v in table.items()}
         # ---- CPU baseline (oracle restatement timed on this host) + accuracy vs CPU
         if not args.no_cpu:
-            wc, sc, dt = run_cpu_baseline(cfg, args.cpu_iters, args.cpu_threads, args.cpu_reps)
+            wc, sc, dt = run_cpu_baseline(cfg, args.cpu_iters, args.cpu_threads, args.cpu_windows, args.cpu_reps)
             result["cpu_baseline"] = {
-                "value": args.cpu_iters / dt,
-                "unit": "iters/s (single window)",
+                "value": args.cpu_windows * args.cpu_iters / dt,
+                "unit": "window-iterations/s",
                 "cores": args.cpu_threads,
                 "kind": "port",
-                "sample": f"1 {args.config.upper()} window x {args.cpu_iters} iterations, median of "
-                          f"{args.cpu_reps} runs (oracle/liboracle.so, {args.cpu_threads} threads, same options)",
+                "sample": f"{args.cpu_windows} {args.config.upper()} windows x {args.cpu_iters} iterations each, "
+                          f"median of {args.cpu_reps} passes after 1 warm-up (oracle/liboracle.so, "
+                          f"{args.cpu_threads} threads = realtime_num_threads, same options)",
                 "wall_s": dt,
             }
             if not args.no_latency and args.cpu_iters == total_iters:
@@ -270,7 +282,9 @@ def main():
                     "final_cost_gpu": result["single_window"]["final_cost"], "final_cost_cpu": sc["final_cost"],
                 }
             if not args.no_latency:
-                result["single_window"]["speedup_vs_cpu"] = result["single_window"]["iters_per_s"] / (args.cpu_iters / dt)
+                cpu_single = args.cpu_iters * args.cpu_windows / dt
+                result["single_window"]["speedup_vs_cpu"] = result["single_window"]["iters_per_s"] / cpu_single
+            result["speedup_vs_cpu_baseline"] = value / result["cpu_baseline"]["value"]
         print(json.dumps(result), flush=True)
     ctx.close()
     if dist:

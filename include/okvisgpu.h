@@ -226,6 +226,17 @@ int okvisgpu_synchronize(okvisgpu_ctx* ctx);
 int okvisgpu_profile_iteration(okvisgpu_ctx* ctx, double* phase_ms);
 const char* okvisgpu_phase_name(int32_t phase);
 
+/* Measurement hooks (not part of the reference interface; used by bench.py's roofline).
+ * okvisgpu_time_kernel re-arms every window of the last finished solve (call after
+ * okvisgpu_solve_end / okvisgpu_solve; the solve state is scratch afterwards) and launches one
+ * iteration's worth of kernel `kernel` `reps` times on the context's stream between HIP events.
+ * avg_ms = device time per repetition; work = algorithmic work of one repetition over the whole
+ * batch (compulsory HBM bytes if *bound == 0, FP64 FLOPs if *bound == 1). */
+int okvisgpu_kernel_count(void);
+const char* okvisgpu_kernel_name(int32_t kernel);
+int okvisgpu_time_kernel(okvisgpu_ctx* ctx, int32_t kernel, int32_t reps, double* avg_ms, double* work,
+                         int32_t* bound);
+
 /* Copy device parameter values back into the caller's host arrays without solving. */
 int okvisgpu_get_params(okvisgpu_ctx* ctx);
 

@@ -309,10 +309,16 @@ __global__ __launch_bounds__(256) void k_trsv(const DevProblem* __restrict__ Pp)
   for (int e = t; e < fdim; e += 256) P.yF[(size_t)foff + e] = y[e];
 }
 
-void launch_chol_panel(const DevProblem& P, int k, hipStream_t s) {
+void launch_potrf(const DevProblem& P, int k, hipStream_t s) {
   hipLaunchKernelGGL(k_potrf_inv, dim3(P.n_win), dim3(256), 0, s, P.self, k);
+}
+void launch_panel(const DevProblem& P, int k, hipStream_t s) {
   const int n = P.h_panel_begin[k + 1] - P.h_panel_begin[k];
   if (n > 0) hipLaunchKernelGGL(k_panel, dim3(n), dim3(256), 0, s, P.self, k);
+}
+void launch_chol_panel(const DevProblem& P, int k, hipStream_t s) {
+  launch_potrf(P, k, s);
+  launch_panel(P, k, s);
 }
 void launch_chol_update(const DevProblem& P, int k, hipStream_t s) {
   const int n = P.h_upd_begin[k + 1] - P.h_upd_begin[k];

@@ -561,9 +561,21 @@ __global__ __launch_bounds__(256) void k_gn_finalize(const DevProblem* __restric
 }
 
 // ------------------------------------------------------------------------------------ launchers
-void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
+void launch_visit_lin(const DevProblem& P, int lin_mode, hipStream_t s) {
   if (P.n_visit > 0)
     hipLaunchKernelGGL(k_visit_lin, dim3((P.n_visit + 255) / 256), dim3(256), 0, s, P.self, lin_mode);
+}
+void launch_visit_prep(const DevProblem& P, hipStream_t s) {
+  if (P.n_visit > 0) hipLaunchKernelGGL(k_visit_prep, dim3((P.n_visit + 255) / 256), dim3(256), 0, s, P.self);
+}
+void launch_assemble_pp(const DevProblem& P, hipStream_t s) {
+  if (P.n_asm_pp > 0) hipLaunchKernelGGL(k_assemble_pp, dim3((P.n_asm_pp + 3) / 4), dim3(256), 0, s, P.self);
+}
+void launch_assemble_sb(const DevProblem& P, hipStream_t s) {
+  if (P.n_asm_sb > 0) hipLaunchKernelGGL(k_assemble_sb, dim3((P.n_asm_sb + 3) / 4), dim3(256), 0, s, P.self);
+}
+void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
+  launch_visit_lin(P, lin_mode, s);
   if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_lin, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P.self, lin_mode);
 }
 void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s) {
@@ -575,15 +587,14 @@ void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t 
 }
 void launch_lm_prep(const DevProblem& P, hipStream_t s) {
   if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_prep, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P.self);
-  if (P.n_visit > 0)
-    hipLaunchKernelGGL(k_visit_prep, dim3((P.n_visit + 255) / 256), dim3(256), 0, s, P.self);
+  launch_visit_prep(P, s);
 }
 void launch_zero_S(const DevProblem& P, hipStream_t s) {
   if (P.n_tiles > 0) hipLaunchKernelGGL(k_zero_S, dim3(P.n_tiles), dim3(256), 0, s, P.self);
 }
 void launch_assemble(const DevProblem& P, hipStream_t s) {
-  if (P.n_asm_pp > 0) hipLaunchKernelGGL(k_assemble_pp, dim3((P.n_asm_pp + 3) / 4), dim3(256), 0, s, P.self);
-  if (P.n_asm_sb > 0) hipLaunchKernelGGL(k_assemble_sb, dim3((P.n_asm_sb + 3) / 4), dim3(256), 0, s, P.self);
+  launch_assemble_pp(P, s);
+  launch_assemble_sb(P, s);
 }
 void launch_gn_reduce(const DevProblem& P, hipStream_t s) {
   launch_lm_prep(P, s);

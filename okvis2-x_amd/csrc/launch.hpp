@@ -24,12 +24,18 @@ void launch_lm_prep(const DevProblem& P, hipStream_t s);
 void launch_zero_S(const DevProblem& P, hipStream_t s);
 void launch_assemble(const DevProblem& P, hipStream_t s);
 void launch_lm_backsub(const DevProblem& P, hipStream_t s);
+void launch_assemble_pp(const DevProblem& P, hipStream_t s);
+void launch_assemble_sb(const DevProblem& P, hipStream_t s);
+void launch_visit_lin(const DevProblem& P, int lin_mode, hipStream_t s);
+void launch_visit_prep(const DevProblem& P, hipStream_t s);
 void launch_gn_finalize(const DevProblem& P, hipStream_t s);
 
 // dense factorisation (kernels_chol.hip)
 void launch_cholesky(const DevProblem& P, int max_tiles, hipStream_t s);
 void launch_chol_panel(const DevProblem& P, int k, hipStream_t s);
 void launch_chol_update(const DevProblem& P, int k, hipStream_t s);
+void launch_potrf(const DevProblem& P, int k, hipStream_t s);
+void launch_panel(const DevProblem& P, int k, hipStream_t s);
 void launch_trsv(const DevProblem& P, hipStream_t s);
 
 // trust-region control (kernels_control.hip)

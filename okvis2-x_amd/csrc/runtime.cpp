@@ -1167,6 +1167,138 @@ int okvisgpu_profile_iteration(okvisgpu_ctx* c, double* ms) {
   });
 }
 
+// ---- per-kernel timing with algorithmic work models (bench.py's roofline) ------------------
+namespace {
+enum KernelId {
+  K_ASSEMBLE_PP, K_ASSEMBLE_SB, K_CHOL_UPDATE, K_POTRF_INV, K_PANEL, K_VISIT_LIN, K_VISIT_PREP,
+  K_EVAL_IMU, K_EVAL_OBS, K_JV, K_TRSV, K_FGRAD, K_COUNT
+};
+const char* kKernelNames[K_COUNT] = {"k_assemble_pp", "k_assemble_sb", "k_chol_update", "k_potrf_inv",
+                                     "k_panel",       "k_visit_lin",   "k_visit_prep",  "k_eval_imu",
+                                     "k_eval_obs",    "k_jv",          "k_trsv",        "k_fgrad"};
+// bound: 0 = HBM bytes, 1 = FP64 matrix-core FLOPs
+const int kKernelBound[K_COUNT] = {0, 0, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0};
+
+// Algorithmic work of one iteration's launches of kernel k over the whole batch: compulsory HBM
+// bytes (every operand read once, every result written once) or FP64 FLOPs.
+double kernelWork(const HostBatch& B, const DevProblem& P, int k) {
+  const double d8 = 8.0;
+  const double nObs = P.n_obs, nVis = P.n_visit, nLm = P.n_lm, nImu = P.n_imu;
+  const double tile3 = 64.0 * 64.0 * 64.0;
+  switch (k) {
+    case K_ASSEMBLE_PP: {
+      double desc = 0, pairs = 0;
+      for (int it : B.asm_pp_items)
+        if (it >= 0) { desc += B.pair_cbegin[it + 1] - B.pair_cbegin[it]; pairs += 1; }
+      return desc * 16 + nVis * (kVisitUY + 21) * d8 + pairs * (36 + 12) * d8;
+    }
+    case K_ASSEMBLE_SB: {
+      double desc = 0, entries = 0;
+      for (int it : B.asm_sb_items) {
+        desc += B.pair_cbegin[it + 1] - B.pair_cbegin[it];
+        const int ni = B.fb_kind[B.pair_fi[it]] == 0 ? 6 : 9, nj = B.fb_kind[B.pair_fj[it]] == 0 ? 6 : 9;
+        entries += ni * nj;
+      }
+      return desc * 16 + nImu * kImuLin * d8 + entries * d8;
+    }
+    case K_CHOL_UPDATE: return (double)(B.chol_upd_items.size() / 3) * 2.0 * tile3;
+    case K_POTRF_INV: {
+      double t = 0;
+      for (int w = 0; w < P.n_win; ++w) t += B.tileT[w];
+      return t * (2.0 * tile3 / 3.0 + 2.0 * 64 * 64);  // LLT + triangular inverse + y_k
+    }
+    case K_PANEL: return (double)(B.chol_panel_items.size() / 2) * (2.0 * tile3 + 2.0 * 64 * 64);
+    case K_VISIT_LIN: return nObs * (20 * d8 + 1) + nVis * (kVisitLin * d8 + 16);
+    case K_VISIT_PREP: return nVis * (18 * d8 + kVisitUY * d8 + 12) + nLm * 15 * d8;
+    case K_EVAL_IMU: return nImu * (2.0 * kImuState + kImuLin + 2 * 16) * d8 + (double)B.imu_ts.size() * 7 * d8;
+    case K_EVAL_OBS: return nObs * (16 + 32 + 13 + 20 * d8 + 8) + nLm * 4 * d8 + (double)B.pose_f.size() * 7 * d8;
+    case K_JV: return nObs * (20 * d8 + 2 * 2 * d8) + nImu * kImuLin * d8 + nLm * 3 * d8 * 2;
+    case K_TRSV: {
+      double t = 0;
+      for (int w = 0; w < P.n_win; ++w) t += B.tileT[w];
+      return (double)(B.tile_items.size() / 3) * 64 * 64 * d8 + t * 64 * 64 * d8;
+    }
+    case K_FGRAD: return nVis * 12 * d8 + nImu * kImuLin * d8 + (double)B.fb_contrib.size() * 16;
+  }
+  return 0.0;
+}
+}  // namespace
+
+int okvisgpu_kernel_count(void) { return K_COUNT; }
+const char* okvisgpu_kernel_name(int32_t k) { return (k >= 0 && k < K_COUNT) ? kKernelNames[k] : ""; }
+
+int okvisgpu_time_kernel(okvisgpu_ctx* c, int32_t kernel, int32_t reps, double* avg_ms, double* work,
+                         int32_t* bound) {
+  if (!c || kernel < 0 || kernel >= K_COUNT || reps < 1) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
+  if (c->inSolve) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "time_kernel: call after solve_end");
+  return guarded(c, [&]() {
+    HIPCHK(hipSetDevice(c->device));
+    const DevProblem& P = c->P;
+    hipStream_t s = c->stream;
+    // re-arm every window (the linearisation of the finished solve stays resident); the solve
+    // state is scratch afterwards and is rebuilt by the next solve_begin
+    std::vector<WinState> st = c->readStates();
+    for (WinState& w : st) {
+      w.done = 0; w.need_gn = 1; w.gn_failed = 0; w.eval_cand = 1; w.accepted = 1; w.step_valid = 1;
+    }
+    HIPCHK(hipMemcpyAsync(P.st, st.data(), sizeof(WinState) * st.size(), hipMemcpyHostToDevice, s));
+    std::vector<hipEvent_t> ev;
+    size_t used = 0;
+    auto event = [&]() {
+      if (used == ev.size()) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        ev.push_back(e);
+      }
+      HIPCHK(hipEventRecord(ev[used], s));
+      return used++;
+    };
+    std::vector<std::pair<size_t, size_t>> spans;
+    auto timed = [&](auto&& launch) {
+      const size_t a = event();
+      launch();
+      const size_t b = event();
+      spans.emplace_back(a, b);
+    };
+    for (int r = 0; r < reps; ++r) {
+      switch (kernel) {
+        case K_ASSEMBLE_PP: timed([&] { launch_assemble_pp(P, s); }); break;
+        case K_ASSEMBLE_SB: timed([&] { launch_assemble_sb(P, s); }); break;
+        case K_VISIT_LIN: timed([&] { launch_visit_lin(P, 1, s); }); break;
+        case K_VISIT_PREP: timed([&] { launch_visit_prep(P, s); }); break;
+        case K_EVAL_IMU: timed([&] { launch_eval_imu(P, 1, s); }); break;
+        case K_EVAL_OBS: timed([&] { launch_eval_obs(P, 1, s); }); break;
+        case K_JV: timed([&] { launch_jv(P, R_JV_STEP, s); }); break;
+        case K_FGRAD: timed([&] { launch_fgrad(P, 1, s); }); break;
+        default: {  // the factorisation kernels need a fresh S each repetition
+          launch_zero_S(P, s);
+          launch_assemble(P, s);
+          for (int k = 0; k < P.max_tiles; ++k) {
+            if (kernel == K_POTRF_INV) timed([&] { launch_potrf(P, k, s); }); else launch_potrf(P, k, s);
+            if (kernel == K_PANEL) timed([&] { launch_panel(P, k, s); }); else launch_panel(P, k, s);
+            if (kernel == K_CHOL_UPDATE) timed([&] { launch_chol_update(P, k, s); }); else launch_chol_update(P, k, s);
+          }
+          if (kernel == K_TRSV) timed([&] { launch_trsv(P, s); });
+        }
+      }
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    double tot = 0.0;
+    for (auto& sp : spans) {
+      float t = 0.f;
+      HIPCHK(hipEventElapsedTime(&t, ev[sp.first], ev[sp.second]));
+      tot += t;
+    }
+    for (auto e : ev) (void)hipEventDestroy(e);
+    if (avg_ms) *avg_ms = tot / reps;
+    if (work) *work = kernelWork(c->B, P, kernel);
+    if (bound) *bound = kKernelBound[kernel];
+    return (int)OKVISGPU_OK;
+  });
+}
+
 int okvisgpu_evaluate(okvisgpu_ctx* c, int32_t window, double* cost) {
   if (!c) return OKVISGPU_ERR_INVALID_ARGUMENT;
   if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");

@@ -101,7 +101,8 @@ EXPORTED_SYMBOLS = [
     "okvisgpu_synth_default_config", "okvisgpu_synth_create", "okvisgpu_synth_problem",
     "okvisgpu_synth_ground_truth", "okvisgpu_synth_reset", "okvisgpu_synth_destroy",
     "okvisgpu_solve_begin", "okvisgpu_solve_iterate", "okvisgpu_solve_end", "okvisgpu_synchronize",
-    "okvisgpu_profile_iteration", "okvisgpu_phase_name",
+    "okvisgpu_profile_iteration", "okvisgpu_phase_name", "okvisgpu_kernel_count", "okvisgpu_kernel_name",
+    "okvisgpu_time_kernel",
 ]
 N_PHASES = 19
 
@@ -145,6 +146,10 @@ def lib():
         L.okvisgpu_profile_iteration.argtypes = [C.c_void_p, _dp]
         L.okvisgpu_phase_name.argtypes = [C.c_int32]
         L.okvisgpu_phase_name.restype = C.c_char_p
+        L.okvisgpu_kernel_count.restype = C.c_int
+        L.okvisgpu_kernel_name.argtypes = [C.c_int32]
+        L.okvisgpu_kernel_name.restype = C.c_char_p
+        L.okvisgpu_time_kernel.argtypes = [C.c_void_p, C.c_int32, C.c_int32, _dp, _dp, C.POINTER(C.c_int32)]
         _lib = L
     return _lib
 
@@ -279,6 +284,15 @@ class Context:
         self._check(lib().okvisgpu_profile_iteration(self.h, dptr(ms)), "okvisgpu_profile_iteration")
         return {lib().okvisgpu_phase_name(i).decode(): float(ms[i]) for i in range(N_PHASES)}
 
+    def time_kernel(self, name, reps=5):
+        """(avg_ms, work, bound) of one iteration's launches of kernel `name` (see include/okvisgpu.h)."""
+        names = kernel_names()
+        k = names.index(name)
+        ms, work, bound = C.c_double(), C.c_double(), C.c_int32()
+        self._check(lib().okvisgpu_time_kernel(self.h, k, reps, C.byref(ms), C.byref(work), C.byref(bound)),
+                    "okvisgpu_time_kernel")
+        return ms.value, work.value, ("hbm", "mfma")[bound.value]
+
     def get_params(self):
         self._check(lib().okvisgpu_get_params(self.h), "okvisgpu_get_params")
 
@@ -323,6 +337,10 @@ class Context:
             self.close()
         except Exception:
             pass
+
+
+def kernel_names():
+    return [lib().okvisgpu_kernel_name(i).decode() for i in range(lib().okvisgpu_kernel_count())]
 
 
 def device_count() -> int:

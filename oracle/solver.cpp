@@ -878,7 +878,8 @@ struct Minimizer {
           consecutive_invalid = 0;
         }
       }
-      if (!valid) {  // HandleInvalidStep
+      if (!valid) {  // HandleInvalidStep (the iteration counts as an unsuccessful one)
+        ++num_unsucc;
         if (++consecutive_invalid >= o.max_num_consecutive_invalid_steps) {
           termination = OKVISGPU_FAILURE;
           break;
@@ -894,10 +895,11 @@ struct Minimizer {
       double sn = 0;
       for (int i = 0; i < P.nx; ++i) sn += (x[i] - cand[i]) * (x[i] - cand[i]);
       sn = std::sqrt(sn);
-      if (sn <= o.parameter_tolerance * (x_norm + o.parameter_tolerance)) { termination = OKVISGPU_CONVERGENCE; break; }
+      // (Ceres returns before the iteration's summary is recorded: it is not counted)
+      if (sn <= o.parameter_tolerance * (x_norm + o.parameter_tolerance)) { termination = OKVISGPU_CONVERGENCE; --iteration; break; }
       // FunctionToleranceReached
       const double cost_change = x_cost - cand_cost;
-      if (std::fabs(cost_change) <= o.function_tolerance * x_cost) { termination = OKVISGPU_CONVERGENCE; break; }
+      if (std::fabs(cost_change) <= o.function_tolerance * x_cost) { termination = OKVISGPU_CONVERGENCE; --iteration; break; }
       // IsStepSuccessful
       const double rel = (cand_cost >= std::numeric_limits<double>::max())
                              ? std::numeric_limits<double>::lowest()

@@ -1,0 +1,76 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports exactly the entry points
+include/okvisgpu.h declares, reports errors instead of crashing without a device, and its
+default options are Ceres' Solver::Options defaults plus the okvis settings."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from _paths import REPO
+
+HEADER = os.path.join(REPO, "include", "okvisgpu.h")
+
+
+def _declared():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    txt = re.sub(r"//[^\n]*", "", txt)
+    return sorted(set(re.findall(r"\b(okvisgpu_\w+)\s*\(", txt)))
+
+
+def test_header_declares_the_python_symbol_list(og):
+    assert _declared() == sorted(og.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol(og):
+    lib = og.lib()
+    for name in _declared():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", og.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (okvisgpu_\w+)", out))
+    assert exported == set(_declared())
+
+
+def test_library_is_gfx950_code(og):
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", og.LIB_PATH],
+                         capture_output=True, text=True, cwd="/tmp")
+    if out.returncode != 0:
+        pytest.skip("llvm-objdump --offloading unavailable")
+    assert "gfx950" in out.stdout + out.stderr
+
+
+def test_abi_version_and_phase_names(og):
+    lib = og.lib()
+    assert lib.okvisgpu_abi_version() >= 1
+    names = [lib.okvisgpu_phase_name(i) for i in range(og.N_PHASES)]
+    assert all(n for n in names) and len(set(names)) == og.N_PHASES
+    assert lib.okvisgpu_phase_name(og.N_PHASES) in (None, b"")
+
+
+def test_default_options_are_ceres_defaults(og):
+    o = og.default_options()
+    # ceres::Solver::Options defaults (types.h / solver.h of Ceres >= 2.1) as used by okvis, which
+    # sets only DOGLEG, DENSE_SCHUR, max_num_iterations and num_threads (ViGraph.cpp:248-249,1854)
+    assert o.trust_region_strategy == 0 and o.linear_solver == 0  # OKVISGPU_DOGLEG, OKVISGPU_DENSE_SCHUR
+    assert o.function_tolerance == 1e-6 and o.gradient_tolerance == 1e-10 and o.parameter_tolerance == 1e-8
+    assert o.initial_trust_region_radius == 1e4 and o.max_trust_region_radius == 1e16
+    assert o.min_trust_region_radius == 1e-32 and o.min_relative_decrease == 1e-3
+    assert o.min_lm_diagonal == 1e-6 and o.max_lm_diagonal == 1e32
+    assert o.max_num_consecutive_invalid_steps == 5 and o.jacobi_scaling == 1
+
+
+def test_no_device_is_an_error_not_a_crash(og):
+    if og.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    h = C.c_void_p()
+    rc = og.lib().okvisgpu_ctx_create(0, C.byref(h))
+    assert rc != 0 and not h.value
+
+
+def test_null_arguments_are_rejected(og):
+    lib = og.lib()
+    assert lib.okvisgpu_solve(None, None, None) != 0
+    assert lib.okvisgpu_set_problems(None, None, 0) != 0
+    assert lib.okvisgpu_synth_create(None, None) != 0

@@ -140,3 +140,130 @@ def test_solve_is_deterministic(og, gpu_ctx):
     b = gpu_ctx.solve(opts, 1)[0]
     assert a["final_cost"] == b["final_cost"]
     assert np.array_equal(Pa, w.poses())
+
+
+def _close(sg, so, rel=1e-7):
+    assert sg["num_iterations"] == so["num_iterations"], (sg, so)
+    assert sg["termination"] == so["termination"], (sg, so)
+    assert abs(sg["final_cost"] - so["final_cost"]) <= rel * so["final_cost"], (sg, so)
+
+
+def test_solve_default_tolerances(og, oracle, gpu_ctx):
+    """Ceres default tolerances (function_tolerance 1e-6 etc.): same termination and count."""
+    w = _window(og)
+    opts = og.default_options(max_num_iterations=50)
+    gpu_ctx.set_problems([w.problem])
+    sg = gpu_ctx.solve(opts, 1)[0]
+    w.reset()
+    so = oracle.solve(w.problem_ptr(), opts)
+    _close(sg, so)
+
+
+def test_ragged_batch(og, oracle, gpu_ctx):
+    """Windows of different sizes in one batch, each against its own oracle solve."""
+    ws = [og.SynthWindow(6, 150, 1000, seed=11), og.SynthWindow(10, 500, 4000, seed=12),
+          og.SynthWindow(3, 40, 200, seed=13), og.SynthWindow(20, 800, 6000, seed=14)]
+    opts = og.default_options(max_num_iterations=4, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    gpu_ctx.set_problems([w.problem for w in ws])
+    sgs = gpu_ctx.solve(opts, len(ws))
+    for w, sg in zip(ws, sgs):
+        P = w.poses().copy()
+        w.reset()
+        so = oracle.solve(w.problem_ptr(), opts)
+        # the 3-keyframe window is far from converged after 4 steps: positions agree to ~1e-8 m but
+        # the cost gradient there (~1e6) turns that into ~1e-6 relative cost differences
+        _close(sg, so, rel=2e-6)
+        assert np.abs(P[:, :3] - w.poses()[:, :3]).max() <= 1e-6
+
+
+def test_constant_blocks(og, oracle, gpu_ctx):
+    """Frozen pose / speed-bias / landmark blocks (SetParameterBlockConstant, ViGraph.cpp:597-637)."""
+    w = _window(og, seed=21)
+    p = w.problem
+    p.pose_constant[0] = 1
+    p.speed_bias_constant[0] = 1
+    p.pose_constant[3] = 1
+    for l in range(0, p.n_landmarks, 7):
+        p.landmark_constant[l] = 1
+    opts = og.default_options(max_num_iterations=5, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    gpu_ctx.set_problems([p])
+    sg = gpu_ctx.solve(opts, 1)[0]
+    P = w.poses().copy()
+    w.reset()
+    so = oracle.solve(w.problem_ptr(), opts)
+    _close(sg, so)
+    assert np.array_equal(P[0], w.poses()[0]) and np.array_equal(P[3], w.poses()[3])
+    assert np.abs(P[:, :3] - w.poses()[:, :3]).max() <= 1e-6
+
+
+def test_set_block_constant_between_solves(og, oracle, gpu_ctx):
+    """Freeze a state after set_problems (the realtime graph's freeze/unfreeze pattern)."""
+    w = _window(og, seed=22)
+    opts = og.default_options(max_num_iterations=4, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    gpu_ctx.set_problems([w.problem])
+    gpu_ctx.set_block_constant(0, 0, 2, True)
+    gpu_ctx.set_block_constant(0, 1, 2, True)
+    sg = gpu_ctx.solve(opts, 1)[0]
+    w.reset()
+    w.problem.pose_constant[2] = 1
+    w.problem.speed_bias_constant[2] = 1
+    so = oracle.solve(w.problem_ptr(), opts)
+    _close(sg, so)
+
+
+def test_s50_window_parity(og, oracle, gpu_ctx):
+    """The north-star window after the bench's 10 iterations: SURVEY.md §8c contract (poses within
+    1e-6 m, landmarks within 1e-5 m of the oracle)."""
+    w = og.SynthWindow(50, 2000, 16000, seed=20251015)
+    opts = og.default_options(max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    gpu_ctx.set_problems([w.problem])
+    sg = gpu_ctx.solve(opts, 1)[0]
+    P, L = w.poses().copy(), w.landmarks().copy()
+    w.reset()
+    so = oracle.solve(w.problem_ptr(), opts)
+    _close(sg, so)
+    assert np.abs(P[:, :3] - w.poses()[:, :3]).max() <= 1e-6
+    # Landmarks: a few synthetic points have (numerically) unobservable depth (smallest eigenvalue
+    # of their robustified J_l^T J_l ~1e-16) and drift to tens of km in both solvers; compare all
+    # landmarks in the information metric and the observable ones in metres.
+    p = w.problem
+    L0 = w.landmarks()
+    r, _, Jl = oracle.eval_reprojection(w.problem_ptr(), p.n_observations)
+    obs_lm = np.ctypeslib.as_array(p.obs_landmark, (p.n_observations,))
+    wgt = 1.0 / (1.0 + (r * r).sum(1))  # Cauchy corrector weight rho'
+    V = np.zeros((p.n_landmarks, 3, 3))
+    np.add.at(V, obs_lm, wgt[:, None, None] * np.einsum("oki,okj->oij", Jl, Jl))
+    d = L[:, :3] - L0[:, :3]
+    maha = np.sqrt(np.einsum("li,lij,lj->l", d, V, d))
+    assert maha.max() <= 1e-4, maha.max()
+    observable = np.linalg.eigvalsh(V)[:, 0] > 1e-3  # depth sigma below ~30 px-equivalents
+    assert observable.mean() > 0.9
+    assert np.abs(d[observable]).max() <= 1e-5
+
+
+def test_pseudo_inverse_solve(og, oracle, gpu_ctx):
+    """A full solve whose IMU square roots all take the clamped-eigenvalue branch."""
+    w = _window(og, seed=23)
+    w.problem.imu_params.sigma_gw_c = 0.0
+    w.problem.imu_params.sigma_aw_c = 0.0
+    opts = og.default_options(max_num_iterations=3, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    gpu_ctx.set_problems([w.problem])
+    sg = gpu_ctx.solve(opts, 1)[0]
+    w.reset()
+    so = oracle.solve(w.problem_ptr(), opts)
+    assert sg["num_iterations"] == so["num_iterations"]
+    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-6 * so["final_cost"], (sg, so)
+
+
+def test_kernel_timing_hook(og, gpu_ctx):
+    w = _window(og, seed=24)
+    gpu_ctx.set_problems([w.problem])
+    gpu_ctx.solve(og.default_options(max_num_iterations=2), 1)
+    for name in og.kernel_names():
+        ms, work, bound = gpu_ctx.time_kernel(name, 2)
+        assert ms > 0 and work > 0 and bound in ("hbm", "mfma"), name
