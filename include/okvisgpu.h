@@ -228,7 +228,8 @@ const char* okvisgpu_phase_name(int32_t phase);
 
 /* Measurement hooks (not part of the reference interface; used by bench.py's roofline).
  * okvisgpu_time_kernel re-arms every window of the last finished solve (call after
- * okvisgpu_solve_end / okvisgpu_solve; the solve state is scratch afterwards) and launches one
+ * okvisgpu_solve_end / okvisgpu_solve; the device-side solve and IMU state are scratch afterwards:
+ * call okvisgpu_update_params before the next solve) and launches one
  * iteration's worth of kernel `kernel` `reps` times on the context's stream between HIP events.
  * avg_ms = device time per repetition; work = algorithmic work of one repetition over the whole
  * batch (compulsory HBM bytes if *bound == 0, FP64 FLOPs if *bound == 1). */

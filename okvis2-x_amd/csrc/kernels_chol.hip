@@ -79,12 +79,47 @@ __device__ __forceinline__ void storeTile(double* A, int64_t ld, int r0g, int c0
       }
 }
 
-// Factor + invert the diagonal tile k with register-owned elements: thread (tr, tc) owns rows
-// tr + 16a and columns tc + 16b (a, b < 4) of both A (being factored) and X = L^-1. One barrier
-// per column c: owners publish column c of A (right-looking with deferred scaling,
-// A_ij -= A_ic A_jc / A_cc) and, lagging one column, the finalised row c-1 of X (right-looking
-// inverse: X_c /= L_cc; X_i -= L_ic X_c); multi-buffered LDS rows avoid write-after-read hazards.
-// The forward substitution of the Schur rhs is fused: y_k = L_kk^-1 rhs_k.
+__device__ __forceinline__ double readlaneD(double v, int lane) {  // v of `lane`, wave-uniform
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// 16x16 block product on one wavefront: acc += sign * A(16 x 16K) B(16K x 16) with
+// A[m][k] = a[m * lda + k], B[k][n] = b[k * ldbk + n * ldbn] (LDS), result in the MFMA C layout.
+template <int KB>
+__device__ __forceinline__ void mfma16(const double* a, int lda, const double* b, int ldbk, int ldbn, double sign,
+                                       dbl4& acc, int lane) {
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < 4 * KB; ++q) {
+    const double av = sign * a[lr * lda + 4 * q + lk];
+    const double bv = b[(4 * q + lk) * ldbk + lr * ldbn];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+  }
+}
+__device__ __forceinline__ dbl4 loadC16(const double* c, int ldc, int lane) {
+  dbl4 v;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = c[((lane >> 4) + 4 * r) * ldc + (lane & 15)];
+  return v;
+}
+__device__ __forceinline__ void storeC16(double* c, int ldc, const dbl4& v, int lane) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) c[((lane >> 4) + 4 * r) * ldc + (lane & 15)] = v[r];
+}
+
+// Diagonal tile k of every active window: L_kk (into S), X = L_kk^-1 (into Linv) and the forward
+// substitution y_k = X work_k. One workgroup (4 wavefronts) per window, tile staged in LDS.
+// Blocked right-looking LLT with 16-column panels (Eigen::LLT semantics: fail at the first
+// non-positive pivot):
+//   panel p   wavefront 0, lane = row i >= 16p holding its 16 panel entries in registers; the 16
+//             column steps broadcast pivots and column entries with v_readlane (no barriers)
+//   update p  A22 -= L21 L21^T on the matrix cores (v_mfma_f64_16x16x4_f64), 16x16 output blocks
+//             spread over the 4 wavefronts
+// then X = L^-1 blockwise: the 4 diagonal 16x16 inverses in parallel (one per wavefront), and
+// X_ij = -X_ii (sum_{m=j}^{i-1} L_im X_mj) by sub-diagonal on the matrix cores.
 __global__ __launch_bounds__(256) void k_potrf_inv(const DevProblem* __restrict__ Pp, int k) {
   const DevProblem& P = *Pp;
   const int w = blockIdx.x;
@@ -92,121 +127,112 @@ __global__ __launch_bounds__(256) void k_potrf_inv(const DevProblem* __restrict_
   const int ld = P.win_fpad[w];
   const int T = ld / kTile;
   if (k >= T) return;
-  double* Sg = P.S + P.win_soff[w];
+  double* Sg = P.S + P.win_soff[w] + (int64_t)k * kTile * ld + k * kTile;  // tile origin
   double* work = P.fwdF + P.win_fwdoff[w];
-  // colbuf[s][i]: column c of A for rows i > c, ZERO for i <= c (so the updates need no masks);
-  // triple-buffered because the lagging inverse still reads column c-1 during step c.
-  __shared__ double colbuf[3][kTile];
-  __shared__ double rowbuf[2][kTile];
-  __shared__ double dgs[3];
-  __shared__ double rsq[kTile];  // 1 / sqrt(pivot)
+  __shared__ double sA[kTile * kLd];
+  __shared__ double sX[kTile * kLd];
   __shared__ double sy[kTile];
-  const int t = threadIdx.x;
-  const int tr = t >> 4, tc = t & 15;
+  __shared__ int sFail;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   if (k == 0)  // start of the factorisation: work = rhs (zero-padded)
     for (int e = t; e < ld; e += 256) work[e] = (e < P.win_fdim[w]) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
-  double A[4][4], X[4][4];
+  for (int e = t; e < kTile * kTile; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    sA[r * kLd + c] = Sg[(int64_t)r * ld + c];
+    sX[r * kLd + c] = 0.0;
+  }
+  if (t == 0) sFail = 0;
+  __syncthreads();
+  if (t < kTile) sy[t] = work[k * kTile + t];
+  for (int p = 0; p < 4; ++p) {
+    // ---- panel p: columns [16p, 16p + 16), rows >= 16p, wavefront 0
+    if (wave == 0) {
+      const int i = lane;
+      double a[16];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+      for (int c = 0; c < 16; ++c) a[c] = sA[i * kLd + 16 * p + c];
+      bool bad = false;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int i = tr + 16 * a, j = tc + 16 * b;
-      A[a][b] = Sg[(int64_t)(k * kTile + i) * ld + k * kTile + j];
-      X[a][b] = (i == j) ? 1.0 : 0.0;
-    }
-  bool failed = false;
-  double rl_prev = 0.0;  // 1/sqrt(pivot c-1)
-  for (int c = 0; c <= kTile; ++c) {
-    const int cb = c % 3, pb = (c + 2) % 3, rb = (c - 1) & 1;
-    // ---- publish: column c of A (owners tc == c%16, block column c/16) and row c-1 of X
-    if (c < kTile && tc == (c & 15)) {
-      const int bc = c >> 4;
+      for (int c = 0; c < 16; ++c) {
+        const int col = 16 * p + c;
+        const double dcc = readlaneD(a[c], col);
+        if (!(dcc > 0.0)) bad = true;  // wave-uniform
+        const double rl = 1.0 / sqrt(dcc);
+        const double l = (i == col) ? dcc * rl : a[c] * rl;
+        a[c] = l;
 #pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        double v = 0.0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) v = (b == bc) ? A[a][b] : v;
-        const int i = tr + 16 * a;
-        colbuf[cb][i] = (i > c) ? v : 0.0;
-        if (i == c) dgs[cb] = v;
+        for (int j = c + 1; j < 16; ++j) a[j] -= l * readlaneD(l, 16 * p + j);
       }
-    }
-    if (c >= 1 && tr == ((c - 1) & 15)) {
-      const int ac = (c - 1) >> 4;
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
-        if (a == ac)
-#pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            X[a][b] *= rl_prev;
-            rowbuf[rb][tc + 16 * b] = X[a][b];
-          }
+      for (int c = 0; c < 16; ++c)
+        if (i >= 16 * p + c) sA[i * kLd + 16 * p + c] = a[c];
+      if (bad && lane == 0) sFail = 1;
     }
     __syncthreads();
-    // ---- X update with column c-1 of L and row c-1 of X (rows <= c-1 see zeros)
-    if (c >= 1) {
-      double li[4], xr[4];
-#pragma unroll
-      for (int a = 0; a < 4; ++a) li[a] = colbuf[pb][tr + 16 * a] * rl_prev;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) xr[b] = rowbuf[rb][tc + 16 * b];
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) X[a][b] -= li[a] * xr[b];
+    if (sFail) break;
+    // ---- trailing update of the blocks (rb, cb), p < cb <= rb < 4
+    {
+      int idx = 0;
+      for (int rb = p + 1; rb < 4; ++rb)
+        for (int cb = p + 1; cb <= rb; ++cb, ++idx) {
+          if ((idx & 3) != wave) continue;
+          double* C = sA + 16 * rb * kLd + 16 * cb;
+          dbl4 acc = loadC16(C, kLd, lane);
+          // acc -= L[rb, p] L[cb, p]^T : B[k][n] = L[16cb + n][16p + k]
+          mfma16<1>(sA + 16 * rb * kLd + 16 * p, kLd, sA + 16 * cb * kLd + 16 * p, 1, kLd, -1.0, acc, lane);
+          storeC16(C, kLd, acc, lane);
+        }
     }
-    if (c == kTile) break;
-    // ---- A update with column c: A_ij -= A_ic A_jc / A_cc (zeros outside the trailing block)
-    const double dcc = dgs[cb];
-    if (!(dcc > 0.0)) { failed = true; break; }  // uniform across the workgroup
-    const double rinv = 1.0 / dcc;
-    rl_prev = 1.0 / sqrt(dcc);
-    if (t == 0) rsq[c] = rl_prev;
-    double ci[4], cj[4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) ci[a] = colbuf[cb][tr + 16 * a] * rinv;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) cj[b] = colbuf[cb][tc + 16 * b];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) A[a][b] -= ci[a] * cj[b];
+    __syncthreads();
   }
-  if (failed) {
+  if (sFail) {
     if (t == 0) P.st[w].gn_failed = 1;
     return;
   }
-  __syncthreads();
-  // ---- L_kk back into S, X into the inverse store, forward substitution y_k
-  double* Li = P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile;
+  // ---- X = L^-1: diagonal 16x16 blocks, one per wavefront (lanes 0..15 = columns)
+  {
+    const int q = wave, j = lane;
+    if (j < 16) {
+      double x[16];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+      for (int i = 0; i < 16; ++i) {
+        double v = (i == j) ? 1.0 : 0.0;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int i = tr + 16 * a, j = tc + 16 * b;
-      if (j <= i) {
-        const double rj = rsq[j];
-        Sg[(int64_t)(k * kTile + i) * ld + k * kTile + j] = (i == j) ? 1.0 / rj : A[a][b] * rj;
+        for (int m = 0; m < i; ++m) v -= sA[(16 * q + i) * kLd + 16 * q + m] * x[m];
+        x[i] = (i >= j) ? v / sA[(16 * q + i) * kLd + 16 * q + i] : 0.0;
       }
-      Li[i * kTile + j] = (j <= i) ? X[a][b] : 0.0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sX[(16 * q + i) * kLd + 16 * q + j] = x[i];
     }
-  if (t < kTile) sy[t] = work[k * kTile + t];
-  __syncthreads();
-  double part[4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    part[a] = 0.0;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const int i = tr + 16 * a, j = tc + 16 * b;
-      part[a] += (j <= i) ? X[a][b] * sy[j] : 0.0;
-    }
-#pragma unroll
-    for (int sh = 8; sh > 0; sh >>= 1) part[a] += __shfl_xor(part[a], sh, 16);
   }
-  if (tc == 0)
-#pragma unroll
-    for (int a = 0; a < 4; ++a) work[k * kTile + tr + 16 * a] = part[a];
+  __syncthreads();
+  // ---- off-diagonal blocks by sub-diagonal d: X_ij = -X_ii (sum_{m=j}^{i-1} L_im X_mj), i = j + d
+  for (int d = 1; d < 4; ++d) {
+    const int j = wave, i = wave + d;
+    if (i < 4) {
+      dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+      for (int m = j; m < i; ++m)  // T = sum L_im X_mj   (B[k][n] = X[16m + k][16j + n])
+        mfma16<1>(sA + 16 * i * kLd + 16 * m, kLd, sX + 16 * m * kLd + 16 * j, kLd, 1, 1.0, acc, lane);
+      double* Xij = sX + 16 * i * kLd + 16 * j;
+      storeC16(Xij, kLd, acc, lane);  // T staged in the (i, j) block (this wavefront only)
+      dbl4 x = dbl4{0.0, 0.0, 0.0, 0.0};
+      mfma16<1>(sX + 16 * i * kLd + 16 * i, kLd, Xij, kLd, 1, -1.0, x, lane);
+      storeC16(Xij, kLd, x, lane);
+    }
+    __syncthreads();
+  }
+  // ---- L_kk back into S (lower), X into the inverse store, forward substitution y_k = X work_k
+  double* Li = P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile;
+  for (int e = t; e < kTile * kTile; e += 256) {
+    const int r = e >> 6, c = e & 63;
+    if (c <= r) Sg[(int64_t)r * ld + c] = sA[r * kLd + c];
+    Li[e] = (c <= r) ? sX[r * kLd + c] : 0.0;
+  }
+  if (t < kTile) {
+    double y = 0.0;
+    for (int j = 0; j <= t; ++j) y += sX[t * kLd + j] * sy[j];
+    work[k * kTile + t] = y;
+  }
 }
 
 // L_ik = A_ik (L_kk^-1)^T on the matrix cores, then the fused forward-substitution update

@@ -1240,7 +1240,7 @@ int okvisgpu_time_kernel(okvisgpu_ctx* c, int32_t kernel, int32_t reps, double* 
     // state is scratch afterwards and is rebuilt by the next solve_begin
     std::vector<WinState> st = c->readStates();
     for (WinState& w : st) {
-      w.done = 0; w.need_gn = 1; w.gn_failed = 0; w.eval_cand = 1; w.accepted = 1; w.step_valid = 1;
+      w.done = 0; w.need_gn = 1; w.gn_failed = 0; w.eval_cand = 1; w.accepted = 1; w.step_valid = 2;
     }
     HIPCHK(hipMemcpyAsync(P.st, st.data(), sizeof(WinState) * st.size(), hipMemcpyHostToDevice, s));
     std::vector<hipEvent_t> ev;
@@ -1267,7 +1267,13 @@ int okvisgpu_time_kernel(okvisgpu_ctx* c, int32_t kernel, int32_t reps, double* 
         case K_ASSEMBLE_SB: timed([&] { launch_assemble_sb(P, s); }); break;
         case K_VISIT_LIN: timed([&] { launch_visit_lin(P, 1, s); }); break;
         case K_VISIT_PREP: timed([&] { launch_visit_prep(P, s); }); break;
-        case K_EVAL_IMU: timed([&] { launch_eval_imu(P, 1, s); }); break;
+        case K_EVAL_IMU:
+          // redo counter := 0 forces the re-preintegration the candidate evaluations of a solve
+          // mostly perform (the device-side IMU state is scratch afterwards)
+          if (P.n_imu > 0)
+            HIPCHK(hipMemset2DAsync(P.imu_state, sizeof(double) * kImuState, 0, sizeof(double), P.n_imu, s));
+          timed([&] { launch_eval_imu(P, 1, s); });
+          break;
         case K_EVAL_OBS: timed([&] { launch_eval_obs(P, 1, s); }); break;
         case K_JV: timed([&] { launch_jv(P, R_JV_STEP, s); }); break;
         case K_FGRAD: timed([&] { launch_fgrad(P, 1, s); }); break;

@@ -1,0 +1,28 @@
+"""Turn rocprofv3 --pmc passes (scripts/gpu_pmc.sh) into profiles/pmc_traffic.json: HBM bytes per
+dispatch of each kernel. FETCH_SIZE / WRITE_SIZE are in KiB; FETCH_SIZE is doubled per the gfx950
+calibration of MI355X_MICROARCH.md (HBM section: it reports half the bytes of 16-byte-per-lane
+reads); other access widths are uncalibrated there, so the figure is an estimate."""
+import collections
+import csv
+import json
+import sys
+
+out = sys.argv[1]
+vals = collections.defaultdict(lambda: collections.defaultdict(list))
+for path in sys.argv[2:]:
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"].split("(")[0].replace("okg::", "")
+        vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+kern = {}
+for k, d in vals.items():
+    if "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
+        continue
+    f = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"]) * 1024 * 2
+    w = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"]) * 1024
+    kern[k] = {"fetch_bytes_per_dispatch": f, "write_bytes_per_dispatch": w, "bytes_per_dispatch": f + w}
+    if k in ("k_assemble_pp", "k_assemble_sb", "k_visit_lin", "k_visit_prep", "k_eval_imu", "k_eval_obs", "k_fgrad",
+             "k_trsv", "k_lm_prep", "k_lm_backsub", "k_zero_S"):
+        kern[k]["bytes_per_iteration"] = f + w  # one dispatch per iteration
+json.dump({"source": sys.argv[2:], "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane calibration), KiB -> bytes",
+           "kernels": kern}, open(out, "w"), indent=1, sort_keys=True)
+print(json.dumps({k: round(v["bytes_per_dispatch"] / 1e9, 3) for k, v in kern.items()}, indent=0))
