@@ -64,8 +64,8 @@ def ate(P, gt):
 
 
 # kernels timed for the roofline table (include/okvisgpu.h okvisgpu_time_kernel)
-ROOFLINE_KERNELS = ["k_assemble_pp", "k_assemble_sb", "k_chol_update", "k_potrf_inv", "k_panel", "k_visit_lin",
-                    "k_visit_prep", "k_eval_imu", "k_eval_obs", "k_jv", "k_trsv", "k_fgrad"]
+ROOFLINE_KERNELS = ["k_assemble_pp", "k_assemble_sb", "k_cholesky", "k_visit_lin", "k_visit_prep", "k_eval_imu",
+                    "k_eval_obs", "k_jv", "k_fgrad"]
 PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
 

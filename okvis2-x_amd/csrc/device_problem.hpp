@@ -185,14 +185,10 @@ struct DevProblem {
   // tile-level symbolic factorisation (host analysis): the reduced camera matrix of a sliding
   // window is block-banded and LLT creates no fill outside its envelope, so only structurally
   // non-zero 64x64 tiles are zeroed, factored and updated (bitwise identical to the dense LLT).
-  const int32_t* chol_panel_items;   // (w, i) pairs; panel k items in [chol_panel_begin[k], ...[k+1])
-  const int32_t* chol_panel_begin;   // [max_tiles + 1]
-  const int32_t* chol_upd_items;     // (w, i, j) triples for the trailing update of panel k
-  const int32_t* chol_upd_begin;     // [max_tiles + 1]
   const int32_t* tile_items;         // (w, i, j) every structurally non-zero tile (i >= j)
+  const uint8_t* tile_nz;            // per window T x T (row-major) structural non-zero flags of L
+  const int64_t* win_tnzoff;         // [n_win] offset of the window's flags in tile_nz
   int32_t n_tiles;
-  const int32_t* h_panel_begin;      // host copies of the begin arrays (launch sizes)
-  const int32_t* h_upd_begin;
   double* fwdF;                    // per window fpad: forward-substitution work vector
   const int64_t* win_fwdoff;       // [n_win] offset into fwdF
   double* sF;   double* sL;        // Jacobi scaling (fixed at iteration 0)

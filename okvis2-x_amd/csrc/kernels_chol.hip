@@ -1,18 +1,17 @@
 // kernels_chol.hip — dense LLT of the reduced camera matrix S (Eigen::LLT semantics: fail at the
-// first non-positive pivot) and the two triangular solves, batched over windows (blockIdx.y).
+// first non-positive pivot) and the two triangular solves, one persistent workgroup per window.
 //
-// Right-looking blocked Cholesky with 64x64 FP64 tiles. Per panel k:
-//   k_potrf_inv(k)   one workgroup per window: factor the diagonal tile with register-owned
-//                    elements and one barrier per column, fused with the inverse of the factor
-//                    and with the forward substitution y_k = L_kk^-1 rhs_k.
-//   (only structurally non-zero tiles: the work lists come from the host's tile-level symbolic
-//    factorisation, DevProblem::chol_*_items)
-//   k_panel(k)       one workgroup per tile row i > k: L_ik = A_ik (L_kk^-1)^T — a 64x64x64 GEMM on
-//                    the FP64 matrix cores — and rhs_i -= L_ik y_k.
-//   k_chol_update(k) one workgroup per trailing tile (i, j), k < j <= i: A_ij -= L_ik L_jk^T — the
-//                    dense reduced-camera block multiply (v_mfma_f64_16x16x4_f64).
-//   k_trsv           one workgroup per window: block backward substitution, every diagonal solve a
-//                    mat-vec with the stored L_kk^-1 (no serial inner loop).
+// k_cholesky: right-looking blocked Cholesky over 64x64 FP64 tiles, only structurally non-zero
+// tiles (the host's tile-level symbolic factorisation, DevProblem::tile_nz: the reduced camera
+// matrix of a sliding window is block-banded and LLT creates no fill outside its envelope, so
+// skipping zero tiles is exact). Per step k, inside one workgroup:
+//   diagonal  L_kk and X = L_kk^-1 (16-column register panels with v_readlane broadcasts, MFMA
+//             trailing updates, blockwise inverse), fused forward substitution y_k = X rhs_k
+//   panel     L_ik = A_ik X^T for every non-zero tile below (64x64x64 on the FP64 matrix cores)
+//             and rhs_i -= L_ik y_k
+//   update    A_ij -= L_ik L_jk^T for the non-zero tiles of the trailing band (matrix cores;
+//             operands staged in LDS, freshly written tiles come back from L2)
+// then the backward substitution x = L^-T y with the stored diagonal inverses.
 //
 // MFMA tile: each of the 4 wavefronts owns a 32x32 quarter of the 64x64 output (2x2 16x16 MFMA
 // tiles), K = 64 in steps of 4. v_mfma_f64_16x16x4_f64 operand map: lane l supplies A[l&15][l>>4]
@@ -31,10 +30,20 @@ __device__ __forceinline__ bool cholSelect(const DevProblem& P, int w) {
   return !s.done && s.need_gn && !s.gn_failed;
 }
 
+// 64x64 global tile (row stride ld) -> LDS [64][kLd]: all 8 16-byte loads of a thread are issued
+// before the LDS stores.
 __device__ __forceinline__ void loadTile(const double* A, int64_t ld, int r0, int c0, double* s, int t) {
-  for (int e = t; e < kTile * kTile; e += 256) {
-    const int r = e >> 6, c = e & 63;
-    s[r * kLd + c] = A[(int64_t)(r0 + r) * ld + c0 + c];
+  double2 v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = t + 256 * u, r = e >> 5, c = 2 * (e & 31);
+    v[u] = *reinterpret_cast<const double2*>(A + (int64_t)(r0 + r) * ld + c0 + c);
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = t + 256 * u, r = e >> 5, c = 2 * (e & 31);
+    s[r * kLd + c] = v[u].x;
+    s[r * kLd + c + 1] = v[u].y;
   }
 }
 
@@ -110,42 +119,27 @@ __device__ __forceinline__ void storeC16(double* c, int ldc, const dbl4& v, int 
   for (int r = 0; r < 4; ++r) c[((lane >> 4) + 4 * r) * ldc + (lane & 15)] = v[r];
 }
 
-// Diagonal tile k of every active window: L_kk (into S), X = L_kk^-1 (into Linv) and the forward
-// substitution y_k = X work_k. One workgroup (4 wavefronts) per window, tile staged in LDS.
-// Blocked right-looking LLT with 16-column panels (Eigen::LLT semantics: fail at the first
-// non-positive pivot):
+// Diagonal tile: L_kk (into S, lower), X = L_kk^-1 (into sX and the Linv store) and y_k = X rhs_k
+// (sy holds rhs_k on entry, y_k on exit; also written to work). Blocked right-looking LLT with
+// 16-column panels:
 //   panel p   wavefront 0, lane = row i >= 16p holding its 16 panel entries in registers; the 16
 //             column steps broadcast pivots and column entries with v_readlane (no barriers)
-//   update p  A22 -= L21 L21^T on the matrix cores (v_mfma_f64_16x16x4_f64), 16x16 output blocks
-//             spread over the 4 wavefronts
-// then X = L^-1 blockwise: the 4 diagonal 16x16 inverses in parallel (one per wavefront), and
+//   update p  A22 -= L21 L21^T on the matrix cores, 16x16 output blocks over the 4 wavefronts
+// then X blockwise: the 4 diagonal 16x16 inverses in parallel (one per wavefront), and
 // X_ij = -X_ii (sum_{m=j}^{i-1} L_im X_mj) by sub-diagonal on the matrix cores.
-__global__ __launch_bounds__(256) void k_potrf_inv(const DevProblem* __restrict__ Pp, int k) {
-  const DevProblem& P = *Pp;
-  const int w = blockIdx.x;
-  if (!cholSelect(P, w)) return;
-  const int ld = P.win_fpad[w];
-  const int T = ld / kTile;
-  if (k >= T) return;
-  double* Sg = P.S + P.win_soff[w] + (int64_t)k * kTile * ld + k * kTile;  // tile origin
-  double* work = P.fwdF + P.win_fwdoff[w];
-  __shared__ double sA[kTile * kLd];
-  __shared__ double sX[kTile * kLd];
-  __shared__ double sy[kTile];
-  __shared__ int sFail;
-  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  if (k == 0)  // start of the factorisation: work = rhs (zero-padded)
-    for (int e = t; e < ld; e += 256) work[e] = (e < P.win_fdim[w]) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
-  for (int e = t; e < kTile * kTile; e += 256) {
-    const int r = e >> 6, c = e & 63;
-    sA[r * kLd + c] = Sg[(int64_t)r * ld + c];
-    sX[r * kLd + c] = 0.0;
+// Returns false (uniformly) at a non-positive pivot.
+__device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX, double* sy,
+                          int* sFail, int t) {
+  const int wave = t >> 6, lane = t & 63;
+  loadTile(Sg, ld, 0, 0, sA, t);
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = t + 256 * u;
+    sX[(e >> 6) * kLd + (e & 63)] = 0.0;
   }
-  if (t == 0) sFail = 0;
+  if (t == 0) *sFail = 0;
   __syncthreads();
-  if (t < kTile) sy[t] = work[k * kTile + t];
   for (int p = 0; p < 4; ++p) {
-    // ---- panel p: columns [16p, 16p + 16), rows >= 16p, wavefront 0
     if (wave == 0) {
       const int i = lane;
       double a[16];
@@ -166,48 +160,37 @@ __global__ __launch_bounds__(256) void k_potrf_inv(const DevProblem* __restrict_
 #pragma unroll
       for (int c = 0; c < 16; ++c)
         if (i >= 16 * p + c) sA[i * kLd + 16 * p + c] = a[c];
-      if (bad && lane == 0) sFail = 1;
+      if (bad && lane == 0) *sFail = 1;
     }
     __syncthreads();
-    if (sFail) break;
-    // ---- trailing update of the blocks (rb, cb), p < cb <= rb < 4
-    {
-      int idx = 0;
-      for (int rb = p + 1; rb < 4; ++rb)
-        for (int cb = p + 1; cb <= rb; ++cb, ++idx) {
-          if ((idx & 3) != wave) continue;
-          double* C = sA + 16 * rb * kLd + 16 * cb;
-          dbl4 acc = loadC16(C, kLd, lane);
-          // acc -= L[rb, p] L[cb, p]^T : B[k][n] = L[16cb + n][16p + k]
-          mfma16<1>(sA + 16 * rb * kLd + 16 * p, kLd, sA + 16 * cb * kLd + 16 * p, 1, kLd, -1.0, acc, lane);
-          storeC16(C, kLd, acc, lane);
-        }
-    }
-    __syncthreads();
-  }
-  if (sFail) {
-    if (t == 0) P.st[w].gn_failed = 1;
-    return;
-  }
-  // ---- X = L^-1: diagonal 16x16 blocks, one per wavefront (lanes 0..15 = columns)
-  {
-    const int q = wave, j = lane;
-    if (j < 16) {
-      double x[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        double v = (i == j) ? 1.0 : 0.0;
-#pragma unroll
-        for (int m = 0; m < i; ++m) v -= sA[(16 * q + i) * kLd + 16 * q + m] * x[m];
-        x[i] = (i >= j) ? v / sA[(16 * q + i) * kLd + 16 * q + i] : 0.0;
+    if (*sFail) return false;
+    int idx = 0;
+    for (int rb = p + 1; rb < 4; ++rb)
+      for (int cb = p + 1; cb <= rb; ++cb, ++idx) {
+        if ((idx & 3) != wave) continue;
+        double* C = sA + 16 * rb * kLd + 16 * cb;
+        dbl4 acc = loadC16(C, kLd, lane);
+        // acc -= L[rb, p] L[cb, p]^T : B[k][n] = L[16cb + n][16p + k]
+        mfma16<1>(sA + 16 * rb * kLd + 16 * p, kLd, sA + 16 * cb * kLd + 16 * p, 1, kLd, -1.0, acc, lane);
+        storeC16(C, kLd, acc, lane);
       }
+    __syncthreads();
+  }
+  if (lane < 16) {  // diagonal 16x16 inverses, wavefront q, lane = column
+    const int q = wave, j = lane;
+    double x[16];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) sX[(16 * q + i) * kLd + 16 * q + j] = x[i];
+    for (int i = 0; i < 16; ++i) {
+      double v = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+      for (int m = 0; m < i; ++m) v -= sA[(16 * q + i) * kLd + 16 * q + m] * x[m];
+      x[i] = (i >= j) ? v / sA[(16 * q + i) * kLd + 16 * q + i] : 0.0;
     }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sX[(16 * q + i) * kLd + 16 * q + j] = x[i];
   }
   __syncthreads();
-  // ---- off-diagonal blocks by sub-diagonal d: X_ij = -X_ii (sum_{m=j}^{i-1} L_im X_mj), i = j + d
-  for (int d = 1; d < 4; ++d) {
+  for (int d = 1; d < 4; ++d) {  // sub-diagonal d: X_ij, i = j + d, wavefront j
     const int j = wave, i = wave + d;
     if (i < 4) {
       dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
@@ -221,144 +204,116 @@ __global__ __launch_bounds__(256) void k_potrf_inv(const DevProblem* __restrict_
     }
     __syncthreads();
   }
-  // ---- L_kk back into S (lower), X into the inverse store, forward substitution y_k = X work_k
-  double* Li = P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile;
-  for (int e = t; e < kTile * kTile; e += 256) {
-    const int r = e >> 6, c = e & 63;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = t + 256 * u, r = e >> 5, c = 2 * (e & 31);
     if (c <= r) Sg[(int64_t)r * ld + c] = sA[r * kLd + c];
-    Li[e] = (c <= r) ? sX[r * kLd + c] : 0.0;
+    if (c + 1 <= r) Sg[(int64_t)r * ld + c + 1] = sA[r * kLd + c + 1];
+    *reinterpret_cast<double2*>(Li + r * kTile + c) =
+        double2{(c <= r) ? sX[r * kLd + c] : 0.0, (c + 1 <= r) ? sX[r * kLd + c + 1] : 0.0};
   }
-  if (t < kTile) {
-    double y = 0.0;
+  double y = 0.0;
+  if (t < kTile)
     for (int j = 0; j <= t; ++j) y += sX[t * kLd + j] * sy[j];
-    work[k * kTile + t] = y;
-  }
-}
-
-// L_ik = A_ik (L_kk^-1)^T on the matrix cores, then the fused forward-substitution update
-// rhs_i -= L_ik y_k.
-__global__ __launch_bounds__(256) void k_panel(const DevProblem* __restrict__ Pp, int k) {
-  const DevProblem& P = *Pp;
-  const int item = P.chol_panel_begin[k] + blockIdx.x;
-  const int w = P.chol_panel_items[2 * item], i = P.chol_panel_items[2 * item + 1];
-  if (!cholSelect(P, w)) return;
-  const int ld = P.win_fpad[w];
-  double* A = P.S + P.win_soff[w];
-  double* work = P.fwdF + P.win_fwdoff[w];
-  __shared__ double sA[kTile * kLd];
-  __shared__ double sB[kTile * kLd];
-  __shared__ double sy[kTile];
-  const int t = threadIdx.x;
-  loadTile(A, ld, i * kTile, k * kTile, sA, t);
-  const double* Li = P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile;
-  for (int e = t; e < kTile * kTile; e += 256) sB[(e >> 6) * kLd + (e & 63)] = Li[e];
-  if (t < kTile) sy[t] = work[k * kTile + t];
   __syncthreads();
-  dbl4 acc[2][2];
-  mfmaTileNT(sA, sB, acc, t);  // A_ik (L_kk^-1)^T
-  storeTile<false>(A, ld, i * kTile, k * kTile, acc, t);
-  __syncthreads();
-  // stage L_ik into LDS (reuse sA) for the rhs update
-  {
-    const int wave = t >> 6, lane = t & 63;
-    const int r0 = 32 * (wave >> 1), c0 = 32 * (wave & 1);
-    for (int a = 0; a < 2; ++a)
-      for (int b = 0; b < 2; ++b)
-        for (int reg = 0; reg < 4; ++reg)
-          sA[(r0 + 16 * a + (lane >> 4) + 4 * reg) * kLd + c0 + 16 * b + (lane & 15)] = acc[a][b][reg];
+  if (t < kTile) {
+    sy[t] = y;
+    workk[t] = y;
   }
   __syncthreads();
-  const int row = t >> 2, q = t & 3;
-  double s = 0.0;
-  for (int c = q; c < kTile; c += 4) s += sA[row * kLd + c] * sy[c];
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
-  if (q == 0) work[i * kTile + row] -= s;
+  return true;
 }
 
-__global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restrict__ Pp, int k) {
-  const DevProblem& P = *Pp;
-  const int item = P.chol_upd_begin[k] + blockIdx.x;
-  const int w = P.chol_upd_items[3 * item], i = P.chol_upd_items[3 * item + 1], j = P.chol_upd_items[3 * item + 2];
-  if (!cholSelect(P, w)) return;
-  const int ld = P.win_fpad[w];
-  double* A = P.S + P.win_soff[w];
-  __shared__ double sA[kTile * kLd];
-  __shared__ double sB[kTile * kLd];
-  const int t = threadIdx.x;
-  loadTile(A, ld, i * kTile, k * kTile, sA, t);
-  loadTile(A, ld, j * kTile, k * kTile, sB, t);
-  __syncthreads();
-  dbl4 acc[2][2];
-  mfmaTileNT(sA, sB, acc, t);
-  storeTile<true>(A, ld, i * kTile, j * kTile, acc, t);
-}
-
-// Backward substitution L^T y = u (u = the forward-substituted rhs left by k_potrf_inv / k_panel),
-// y in LDS (dynamic shared memory: fpad doubles); diagonal blocks through the stored inverses.
-__global__ __launch_bounds__(256) void k_trsv(const DevProblem* __restrict__ Pp) {
+__global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int w = blockIdx.x;
   if (!cholSelect(P, w)) return;
-  extern __shared__ double y[];
-  __shared__ double part[4 * kTile];
-  __shared__ double v[kTile];
-  const int ld = P.win_fpad[w], fdim = P.win_fdim[w], foff = P.win_foff[w];
-  const int T = ld / kTile;
-  const double* A = P.S + P.win_soff[w];
-  const double* Linv = P.Linv + P.win_linvoff[w];
-  const double* work = P.fwdF + P.win_fwdoff[w];
+  const int64_t ld = P.win_fpad[w];
+  const int T = (int)(ld / kTile);
+  double* S = P.S + P.win_soff[w];
+  double* work = P.fwdF + P.win_fwdoff[w];
+  double* Linv = P.Linv + P.win_linvoff[w];
+  const uint8_t* nz = P.tile_nz + P.win_tnzoff[w];
+  __shared__ double sA[kTile * kLd];
+  __shared__ double sX[kTile * kLd];
+  __shared__ double sy[kTile];
+  __shared__ int sFail;
   const int t = threadIdx.x;
-  for (int e = t; e < ld; e += 256) y[e] = work[e];
+  const int fdim = P.win_fdim[w];
+  for (int e = t; e < ld; e += 256) work[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
   __syncthreads();
+  for (int k = 0; k < T; ++k) {
+    if (t < kTile) sy[t] = work[k * kTile + t];
+    __syncthreads();
+    if (!potrfTile(S + k * kTile * ld + k * kTile, ld, Linv + (int64_t)k * kTile * kTile, work + k * kTile, sA, sX,
+                   sy, &sFail, t)) {
+      if (t == 0) P.st[w].gn_failed = 1;
+      return;
+    }
+    // ---- panel: L_ik = A_ik X^T, rhs_i -= L_ik y_k
+    for (int i = k + 1; i < T; ++i) {
+      if (!nz[i * T + k]) continue;
+      double* Aik = S + i * kTile * ld + k * kTile;
+      loadTile(Aik, ld, 0, 0, sA, t);
+      __syncthreads();
+      dbl4 acc[2][2];
+      mfmaTileNT(sA, sX, acc, t);
+      __syncthreads();
+      storeTile<false>(Aik, ld, 0, 0, acc, t);
+      storeTile<false>(sA, kLd, 0, 0, acc, t);  // L_ik staged for the rhs update
+      __syncthreads();
+      if (t < kTile) {
+        double a = 0.0;
+        for (int c = 0; c < kTile; ++c) a += sA[t * kLd + c] * sy[c];
+        work[i * kTile + t] -= a;
+      }
+      __syncthreads();
+    }
+    // ---- trailing band update: A_ij -= L_ik L_jk^T, k < j <= i, both tiles non-zero
+    for (int i = k + 1; i < T; ++i) {
+      if (!nz[i * T + k]) continue;
+      loadTile(S + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
+      for (int j = k + 1; j <= i; ++j) {
+        if (!nz[j * T + k]) continue;
+        if (j != i) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sX, t);
+        __syncthreads();
+        dbl4 acc[2][2];
+        mfmaTileNT(sA, j == i ? sA : sX, acc, t);
+        storeTile<true>(S + i * kTile * ld + j * kTile, ld, 0, 0, acc, t);
+        __syncthreads();
+      }
+    }
+  }
+  // ---- backward substitution x = L^-T y (work holds y; x overwrites it from the back)
   for (int I = T - 1; I >= 0; --I) {
-    {
-      const int col = t & 63, q = t >> 6;
-      double acc = 0.0;
-      for (int r = (I + 1) * kTile + q; r < ld; r += 4) acc += A[(int64_t)r * ld + I * kTile + col] * y[r];
-      part[q * kTile + col] = acc;
+    const int col = t & 63, q = t >> 6;
+    double acc = 0.0;
+    for (int i = I + 1; i < T; ++i) {
+      if (!nz[i * T + I]) continue;
+      const double* Lt = S + i * kTile * ld + I * kTile;
+#pragma unroll
+      for (int r = q; r < kTile; r += 4) acc += Lt[(int64_t)r * ld + col] * work[i * kTile + r];
     }
+    sX[q * kTile + col] = acc;
     __syncthreads();
-    if (t < kTile) v[t] = y[I * kTile + t] - (part[t] + part[kTile + t] + part[2 * kTile + t] + part[3 * kTile + t]);
+    if (t < kTile) sy[t] = work[I * kTile + t] - (sX[t] + sX[kTile + t] + sX[2 * kTile + t] + sX[3 * kTile + t]);
     __syncthreads();
     {
-      const int col = t & 63, q = t >> 6;
       const double* Li = Linv + (int64_t)I * kTile * kTile;
-      double acc = 0.0;
-      for (int r = col + q; r < kTile; r += 4) acc += Li[r * kTile + col] * v[r];
-      part[q * kTile + col] = acc;
+      double a = 0.0;
+#pragma unroll
+      for (int r = q; r < kTile; r += 4) a += (r >= col) ? Li[r * kTile + col] * sy[r] : 0.0;
+      sA[q * kTile + col] = a;
     }
     __syncthreads();
-    if (t < kTile) y[I * kTile + t] = part[t] + part[kTile + t] + part[2 * kTile + t] + part[3 * kTile + t];
+    if (t < kTile) work[I * kTile + t] = sA[t] + sA[kTile + t] + sA[2 * kTile + t] + sA[3 * kTile + t];
     __syncthreads();
   }
-  for (int e = t; e < fdim; e += 256) P.yF[(size_t)foff + e] = y[e];
+  for (int e = t; e < fdim; e += 256) P.yF[(size_t)P.win_foff[w] + e] = work[e];
 }
 
-void launch_potrf(const DevProblem& P, int k, hipStream_t s) {
-  hipLaunchKernelGGL(k_potrf_inv, dim3(P.n_win), dim3(256), 0, s, P.self, k);
-}
-void launch_panel(const DevProblem& P, int k, hipStream_t s) {
-  const int n = P.h_panel_begin[k + 1] - P.h_panel_begin[k];
-  if (n > 0) hipLaunchKernelGGL(k_panel, dim3(n), dim3(256), 0, s, P.self, k);
-}
-void launch_chol_panel(const DevProblem& P, int k, hipStream_t s) {
-  launch_potrf(P, k, s);
-  launch_panel(P, k, s);
-}
-void launch_chol_update(const DevProblem& P, int k, hipStream_t s) {
-  const int n = P.h_upd_begin[k + 1] - P.h_upd_begin[k];
-  if (n > 0) hipLaunchKernelGGL(k_chol_update, dim3(n), dim3(256), 0, s, P.self, k);
-}
-void launch_cholesky(const DevProblem& P, int max_tiles, hipStream_t s) {
-  for (int k = 0; k < max_tiles; ++k) {
-    launch_chol_panel(P, k, s);
-    launch_chol_update(P, k, s);
-  }
-}
-
-void launch_trsv(const DevProblem& P, hipStream_t s) {
-  if (P.max_fpad > 0) hipLaunchKernelGGL(k_trsv, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
+void launch_cholesky(const DevProblem& P, hipStream_t s) {
+  if (P.n_win > 0) hipLaunchKernelGGL(k_cholesky, dim3(P.n_win), dim3(256), 0, s, P.self);
 }
 
 }  // namespace okg

@@ -30,13 +30,9 @@ void launch_visit_lin(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_visit_prep(const DevProblem& P, hipStream_t s);
 void launch_gn_finalize(const DevProblem& P, hipStream_t s);
 
-// dense factorisation (kernels_chol.hip)
-void launch_cholesky(const DevProblem& P, int max_tiles, hipStream_t s);
-void launch_chol_panel(const DevProblem& P, int k, hipStream_t s);
-void launch_chol_update(const DevProblem& P, int k, hipStream_t s);
-void launch_potrf(const DevProblem& P, int k, hipStream_t s);
-void launch_panel(const DevProblem& P, int k, hipStream_t s);
-void launch_trsv(const DevProblem& P, hipStream_t s);
+// dense factorisation + both triangular solves, one persistent workgroup per window
+// (kernels_chol.hip)
+void launch_cholesky(const DevProblem& P, hipStream_t s);
 
 // trust-region control (kernels_control.hip)
 enum ReduceMode { R_COST_INIT = 0, R_COST_CAND = 1, R_JV_CAUCHY = 2, R_JV_STEP = 3 };

@@ -87,6 +87,8 @@ struct HostBatch {
   std::vector<Contrib> pair_contrib;
   int64_t s_total = 0, linv_total = 0, fwd_total = 0;
   std::vector<std::vector<uint8_t>> tileNz;
+  std::vector<uint8_t> tile_nz;
+  std::vector<int64_t> win_tnzoff;
   std::vector<int> tileT;
   int f_total = 0;
   int max_fpad = 0;
@@ -485,6 +487,10 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     while (!B.asm_pp_items.empty() && B.asm_pp_items.back() < 0) B.asm_pp_items.pop_back();
   }
   for (int w = 0; w < B.n_win; ++w) {
+    B.win_tnzoff.push_back((int64_t)B.tile_nz.size());
+    B.tile_nz.insert(B.tile_nz.end(), B.tileNz[w].begin(), B.tileNz[w].end());
+  }
+  for (int w = 0; w < B.n_win; ++w) {
     const int T = B.tileT[w];
     for (int i = 0; i < T; ++i)
       for (int j = 0; j <= i; ++j)
@@ -646,9 +652,9 @@ struct okvisgpu_ctx {
     const size_t o_pw = upl(B.pair_win), o_pfi = upl(B.pair_fi), o_pfj = upl(B.pair_fj), o_pcb = upl(B.pair_cbegin),
                  o_pc = upl(B.pair_contrib);
     const size_t o_pruns = upl(B.pair_runs);
+    const size_t o_tnz = upl(B.tile_nz), o_tnzoff = upl(B.win_tnzoff);
     const size_t o_app = upl(B.asm_pp_items), o_asb = upl(B.asm_sb_items);
-    const size_t o_cpi = upl(B.chol_panel_items), o_cpb = upl(B.chol_panel_begin), o_cui = upl(B.chol_upd_items),
-                 o_cub = upl(B.chol_upd_begin), o_ti = upl(B.tile_items);
+    const size_t o_ti = upl(B.tile_items);
     const size_t nf = std::max(1, B.f_total), nl3 = std::max<size_t>(1, (size_t)3 * D.n_lm);
     const size_t o_S = scratch(sizeof(double) * std::max<int64_t>(1, B.s_total));
     const size_t o_Linv = scratch(sizeof(double) * std::max<int64_t>(1, B.linv_total));
@@ -701,14 +707,12 @@ struct okvisgpu_ctx {
     D.pair_win = ip(o_pw); D.pair_fi = ip(o_pfi); D.pair_fj = ip(o_pfj); D.pair_cbegin = ip(o_pcb);
     D.pair_contrib = reinterpret_cast<const Contrib*>(base + o_pc);
     D.pair_runs = ip(o_pruns);
+    D.tile_nz = reinterpret_cast<const uint8_t*>(base + o_tnz);
+    D.win_tnzoff = reinterpret_cast<const int64_t*>(base + o_tnzoff);
     D.asm_pp_items = ip(o_app); D.asm_sb_items = ip(o_asb);
     D.n_asm_pp = (int)B.asm_pp_items.size(); D.n_asm_sb = (int)B.asm_sb_items.size();
-    D.chol_panel_items = ip(o_cpi); D.chol_panel_begin = ip(o_cpb);
-    D.chol_upd_items = ip(o_cui); D.chol_upd_begin = ip(o_cub);
     D.tile_items = ip(o_ti);
     D.n_tiles = (int)(B.tile_items.size() / 3);
-    D.h_panel_begin = B.chol_panel_begin.data();
-    D.h_upd_begin = B.chol_upd_begin.data();
     D.S = dp(o_S);
     D.Linv = dp(o_Linv);
     D.win_linvoff = lp(o_wlinv);
@@ -827,8 +831,7 @@ struct okvisgpu_ctx {
 
   void launchIteration() {
     launch_gn_reduce(P, stream);
-    launch_cholesky(P, P.max_tiles, stream);
-    launch_trsv(P, stream);
+    launch_cholesky(P, stream);
     launch_gn_backsub(P, stream);
     launch_jv(P, R_JV_CAUCHY, stream);
     launch_reduce(P, R_JV_CAUCHY, stream);
@@ -1110,9 +1113,9 @@ int okvisgpu_solve(okvisgpu_ctx* c, const okvisgpu_options* o, okvisgpu_summary*
 }
 
 static const char* kPhaseNames[OKVISGPU_N_PHASES] = {
-    "lm_prep", "zero_S", "assemble", "chol_panel", "chol_update", "trsv", "lm_backsub", "gn_finalize",
-    "jv_cauchy", "reduce_cauchy", "dogleg", "jv_step", "reduce_step", "eval_obs", "eval_imu",
-    "eval_priors", "reduce_cand", "lin_blocks", "gradnorm"};
+    "lm_prep",     "zero_S",   "assemble",   "cholesky",  "lm_backsub", "gn_finalize",
+    "jv_cauchy",   "reduce_cauchy", "dogleg", "jv_step",  "reduce_step", "eval_obs",
+    "eval_imu",    "eval_priors", "reduce_cand", "lin_blocks", "gradnorm"};
 
 const char* okvisgpu_phase_name(int32_t i) { return (i >= 0 && i < OKVISGPU_N_PHASES) ? kPhaseNames[i] : ""; }
 
@@ -1135,24 +1138,20 @@ int okvisgpu_profile_iteration(okvisgpu_ctx* c, double* ms) {
     launch_lm_prep(P, s); mark(0);
     launch_zero_S(P, s); mark(1);
     launch_assemble(P, s); mark(2);
-    for (int k = 0; k < P.max_tiles; ++k) {
-      launch_chol_panel(P, k, s); mark(3);
-      launch_chol_update(P, k, s); mark(4);
-    }
-    launch_trsv(P, s); mark(5);
-    launch_lm_backsub(P, s); mark(6);
-    launch_gn_finalize(P, s); mark(7);
-    launch_jv(P, R_JV_CAUCHY, s); mark(8);
-    launch_reduce(P, R_JV_CAUCHY, s); mark(9);
-    launch_dogleg(P, s); mark(10);
-    launch_jv(P, R_JV_STEP, s); mark(11);
-    launch_reduce(P, R_JV_STEP, s); mark(12);
-    launch_eval_obs(P, 1, s); mark(13);
-    launch_eval_imu(P, 1, s); mark(14);
-    launch_eval_priors(P, 1, s); mark(15);
-    launch_reduce(P, R_COST_CAND, s); mark(16);
-    launch_linearization_blocks(P, 1, s); mark(17);
-    launch_gradnorm(P, 1, s); mark(18);
+    launch_cholesky(P, s); mark(3);
+    launch_lm_backsub(P, s); mark(4);
+    launch_gn_finalize(P, s); mark(5);
+    launch_jv(P, R_JV_CAUCHY, s); mark(6);
+    launch_reduce(P, R_JV_CAUCHY, s); mark(7);
+    launch_dogleg(P, s); mark(8);
+    launch_jv(P, R_JV_STEP, s); mark(9);
+    launch_reduce(P, R_JV_STEP, s); mark(10);
+    launch_eval_obs(P, 1, s); mark(11);
+    launch_eval_imu(P, 1, s); mark(12);
+    launch_eval_priors(P, 1, s); mark(13);
+    launch_reduce(P, R_COST_CAND, s); mark(14);
+    launch_linearization_blocks(P, 1, s); mark(15);
+    launch_gradnorm(P, 1, s); mark(16);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));
     for (int i = 0; i < OKVISGPU_N_PHASES; ++i) ms[i] = 0.0;
@@ -1170,14 +1169,13 @@ int okvisgpu_profile_iteration(okvisgpu_ctx* c, double* ms) {
 // ---- per-kernel timing with algorithmic work models (bench.py's roofline) ------------------
 namespace {
 enum KernelId {
-  K_ASSEMBLE_PP, K_ASSEMBLE_SB, K_CHOL_UPDATE, K_POTRF_INV, K_PANEL, K_VISIT_LIN, K_VISIT_PREP,
-  K_EVAL_IMU, K_EVAL_OBS, K_JV, K_TRSV, K_FGRAD, K_COUNT
+  K_ASSEMBLE_PP, K_ASSEMBLE_SB, K_CHOLESKY, K_VISIT_LIN, K_VISIT_PREP, K_EVAL_IMU, K_EVAL_OBS, K_JV,
+  K_FGRAD, K_COUNT
 };
-const char* kKernelNames[K_COUNT] = {"k_assemble_pp", "k_assemble_sb", "k_chol_update", "k_potrf_inv",
-                                     "k_panel",       "k_visit_lin",   "k_visit_prep",  "k_eval_imu",
-                                     "k_eval_obs",    "k_jv",          "k_trsv",        "k_fgrad"};
+const char* kKernelNames[K_COUNT] = {"k_assemble_pp", "k_assemble_sb", "k_cholesky", "k_visit_lin", "k_visit_prep",
+                                     "k_eval_imu",    "k_eval_obs",    "k_jv",       "k_fgrad"};
 // bound: 0 = HBM bytes, 1 = FP64 matrix-core FLOPs
-const int kKernelBound[K_COUNT] = {0, 0, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0};
+const int kKernelBound[K_COUNT] = {0, 0, 1, 0, 0, 0, 0, 0, 0};
 
 // Algorithmic work of one iteration's launches of kernel k over the whole batch: compulsory HBM
 // bytes (every operand read once, every result written once) or FP64 FLOPs.
@@ -1201,23 +1199,17 @@ double kernelWork(const HostBatch& B, const DevProblem& P, int k) {
       }
       return desc * 16 + nImu * kImuLin * d8 + entries * d8;
     }
-    case K_CHOL_UPDATE: return (double)(B.chol_upd_items.size() / 3) * 2.0 * tile3;
-    case K_POTRF_INV: {
-      double t = 0;
-      for (int w = 0; w < P.n_win; ++w) t += B.tileT[w];
-      return t * (2.0 * tile3 / 3.0 + 2.0 * 64 * 64);  // LLT + triangular inverse + y_k
+    case K_CHOLESKY: {  // diagonal LLT + inverse + y_k, panels, band updates, backward solve
+      double diag = 0;
+      for (int w = 0; w < P.n_win; ++w) diag += B.tileT[w];
+      const double panels = (double)(B.chol_panel_items.size() / 2), upd = (double)(B.chol_upd_items.size() / 3);
+      return diag * (2.0 * tile3 / 3.0 + 4.0 * 64 * 64) + panels * (2.0 * tile3 + 4.0 * 64 * 64) + upd * 2.0 * tile3;
     }
-    case K_PANEL: return (double)(B.chol_panel_items.size() / 2) * (2.0 * tile3 + 2.0 * 64 * 64);
     case K_VISIT_LIN: return nObs * (20 * d8 + 1) + nVis * (kVisitLin * d8 + 16);
     case K_VISIT_PREP: return nVis * (18 * d8 + kVisitUY * d8 + 12) + nLm * 15 * d8;
     case K_EVAL_IMU: return nImu * (2.0 * kImuState + kImuLin + 2 * 16) * d8 + (double)B.imu_ts.size() * 7 * d8;
     case K_EVAL_OBS: return nObs * (16 + 32 + 13 + 20 * d8 + 8) + nLm * 4 * d8 + (double)B.pose_f.size() * 7 * d8;
     case K_JV: return nObs * (20 * d8 + 2 * 2 * d8) + nImu * kImuLin * d8 + nLm * 3 * d8 * 2;
-    case K_TRSV: {
-      double t = 0;
-      for (int w = 0; w < P.n_win; ++w) t += B.tileT[w];
-      return (double)(B.tile_items.size() / 3) * 64 * 64 * d8 + t * 64 * 64 * d8;
-    }
     case K_FGRAD: return nVis * 12 * d8 + nImu * kImuLin * d8 + (double)B.fb_contrib.size() * 16;
   }
   return 0.0;
@@ -1277,16 +1269,11 @@ int okvisgpu_time_kernel(okvisgpu_ctx* c, int32_t kernel, int32_t reps, double* 
         case K_EVAL_OBS: timed([&] { launch_eval_obs(P, 1, s); }); break;
         case K_JV: timed([&] { launch_jv(P, R_JV_STEP, s); }); break;
         case K_FGRAD: timed([&] { launch_fgrad(P, 1, s); }); break;
-        default: {  // the factorisation kernels need a fresh S each repetition
+        case K_CHOLESKY:  // needs a freshly assembled S each repetition
           launch_zero_S(P, s);
           launch_assemble(P, s);
-          for (int k = 0; k < P.max_tiles; ++k) {
-            if (kernel == K_POTRF_INV) timed([&] { launch_potrf(P, k, s); }); else launch_potrf(P, k, s);
-            if (kernel == K_PANEL) timed([&] { launch_panel(P, k, s); }); else launch_panel(P, k, s);
-            if (kernel == K_CHOL_UPDATE) timed([&] { launch_chol_update(P, k, s); }); else launch_chol_update(P, k, s);
-          }
-          if (kernel == K_TRSV) timed([&] { launch_trsv(P, s); });
-        }
+          timed([&] { launch_cholesky(P, s); });
+          break;
       }
     }
     HIPCHK(hipGetLastError());
