@@ -1,0 +1,15 @@
+"""rocprofv3 kernel_trace.csv -> per (kernel, grid size) launch count and mean duration, so the
+batched launches can be compared with bench.py's event-timed roofline entry."""
+import collections
+import csv
+import sys
+
+g = collections.defaultdict(list)
+for r in csv.DictReader(open(sys.argv[1])):
+    name = r["Kernel_Name"].split("(")[0].replace("okg::", "")
+    grid = int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)
+    g[(name, grid)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+rows = sorted(g.items(), key=lambda kv: -sum(kv[1]))
+print(f"{'kernel':24s} {'grid':>9s} {'calls':>6s} {'avg_us':>10s} {'total_ms':>9s}")
+for (name, grid), d in rows[: int(sys.argv[2]) if len(sys.argv) > 2 else 40]:
+    print(f"{name:24s} {grid:9d} {len(d):6d} {sum(d) / len(d):10.1f} {sum(d) / 1e3:9.2f}")
