@@ -23,7 +23,7 @@ constexpr int kImuState = 292;        // == OKVISGPU_IMU_STATE_DOUBLES
 
 // Linearisation record per observation (structure of arrays, plane-major):
 //   plane 0-1: r (Cauchy-corrected)   plane 2-13: J_pose 2x6   plane 14-19: J_lm 2x3
-constexpr int kObsLin = 20;
+constexpr int kObsLin = 8;   // r (2) | A = L Jh C_CW (2x3), Cauchy-scaled
 constexpr int kVisitLin = 54;
 constexpr int kVisitUY = 42;
 
@@ -102,9 +102,9 @@ struct DevProblem {
   const uint8_t* obs_flags;        // bit0 cauchy, bit1 fixed (all blocks constant)
   const double* obs_kp;            // [n_obs][2]
   const double* obs_L;             // [n_obs][4]
-  double* obs_lin[2];              // [kObsLin][obs_stride]
+  double* obs_lin[2];              // [kObsLin][obs_stride]; lin[lcur] belongs to params X[xcur]
   double* obs_cost[2];             // [n_obs]
-  double* obs_jv;                  // [2][n_obs]: (Jv)^2, (Jv).r
+  double* obs_jv;                  // [n_visit]: |J_s v|^2 of the visit's residuals
 
   // --- landmarks / visits
   const int32_t* lm_visit_begin;   // [n_lm+1] visits of landmark l
@@ -132,7 +132,7 @@ struct DevProblem {
   double* imu_state;               // [n_imu][kImuState]
   double* imu_lin[2];              // [n_imu][kImuLin]
   double* imu_cost[2];             // [n_imu]
-  double* imu_jv;                  // [2][n_imu]
+  double* imu_jv;                  // [n_imu] |J_s v|^2
 
   // --- priors
   const int32_t* pp_block;         // [n_pprior] global pose

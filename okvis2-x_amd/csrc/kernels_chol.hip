@@ -291,7 +291,7 @@ __global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__
     for (int i = I + 1; i < T; ++i) {
       if (!nz[i * T + I]) continue;
       const double* Lt = S + i * kTile * ld + I * kTile;
-#pragma unroll
+#pragma unroll 4
       for (int r = q; r < kTile; r += 4) acc += Lt[(int64_t)r * ld + col] * work[i * kTile + r];
     }
     sX[q * kTile + col] = acc;
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__
     {
       const double* Li = Linv + (int64_t)I * kTile * kTile;
       double a = 0.0;
-#pragma unroll
+#pragma unroll 4
       for (int r = q; r < kTile; r += 4) a += (r >= col) ? Li[r * kTile + col] * sy[r] : 0.0;
       sA[q * kTile + col] = a;
     }

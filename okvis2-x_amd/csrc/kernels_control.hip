@@ -54,47 +54,65 @@ __device__ __forceinline__ bool jvSelect(const DevProblem& P, int w, int mode) {
   return s.step_valid == 2;
 }
 
+// |J_s v|^2 per residual block, J_s = J diag(s) (the Jacobi-scaled Jacobian the dogleg works in),
+// v = Cauchy direction or the step. Reprojections: one thread per (landmark, pose) visit (its 1-2
+// residuals share the pose/landmark vectors); IMU factors and priors: one thread each. The
+// companion (J_s v).r of the step is v.(s g) with the gradient g = J^T r already at hand, so it is
+// formed in k_reduce without touching J (DoglegStrategy / TrustRegionMinimizer model cost).
 __global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp, int mode) {
   const DevProblem& P = *Pp;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const double* vF = (mode == R_JV_CAUCHY) ? P.vF : P.stepF;
   const double* vL = (mode == R_JV_CAUCHY) ? P.vL : P.stepL;
-  if (t < P.n_obs) {
-    const int o = t;
-    const int w = P.obs_win[o];
+  if (t < P.n_visit) {
+    const int v = t;
+    const int l = P.visit_lm[v];
+    const int w = P.lm_win[l];
     if (!jvSelect(P, w, mode)) return;
-    double a = 0.0, b = 0.0;
-    if (!(P.obs_flags[o] & 2)) {
-      const int lb = P.st[w].lcur;
-      const double* lin = P.obs_lin[lb];
-      const int64_t S = P.obs_stride;
-      const int pf = P.pose_f[P.obs_pose[o]];
-      const int l = P.obs_lm[o];
-      double vp[6] = {0, 0, 0, 0, 0, 0}, vl[3] = {0, 0, 0};
-      if (pf >= 0) {
-        const size_t base = (size_t)P.win_foff[w] + pf;
-        for (int c = 0; c < 6; ++c) vp[c] = P.sF[base + c] * vF[base + c];
-      }
-      if (P.lm_free[l])
-        for (int c = 0; c < 3; ++c) vl[c] = P.sL[3 * (size_t)l + c] * vL[3 * (size_t)l + c];
+    const WinState& st = P.st[w];
+    const int ps = P.visit_pose[v];
+    const int pf = P.pose_f[ps];
+    double vp[6] = {0, 0, 0, 0, 0, 0}, vl[3] = {0, 0, 0};
+    if (pf >= 0) {
+      const size_t base = (size_t)P.win_foff[w] + pf;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) vp[c] = P.sF[base + c] * vF[base + c];
+    }
+    if (P.lm_free[l])
+#pragma unroll
+      for (int c = 0; c < 3; ++c) vl[c] = P.sL[3 * (size_t)l + c] * vL[3 * (size_t)l + c];
+    const auto lin = gmem(P.obs_lin[st.lcur]);
+    const int64_t S = P.obs_stride;
+    const double* hp = P.lm[st.xcur] + 4 * (size_t)l;
+    const double* tw = P.pose[st.xcur] + 7 * (size_t)ps;
+    const double w4 = hp[3];
+    const double p3[3] = {hp[0] - tw[0] * w4, hp[1] - tw[1] * w4, hp[2] - tw[2] * w4};
+    double a = 0.0;
+    for (int o = P.visit_obs_begin[v]; o < P.visit_obs_begin[v + 1]; ++o) {
+      if (P.obs_flags[o] & 2) continue;
+      double A[6], Jp[12], Jl[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) A[k] = lin[(2 + k) * S + o];
+      obsJacobians(A, p3, w4, Jp, Jl);
+#pragma unroll
       for (int r = 0; r < 2; ++r) {
         double jv = 0.0;
-        for (int c = 0; c < 6; ++c) jv += lin[(2 + r * 6 + c) * S + o] * vp[c];
-        for (int c = 0; c < 3; ++c) jv += lin[(14 + r * 3 + c) * S + o] * vl[c];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) jv += Jp[r * 6 + c] * vp[c];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) jv += Jl[r * 3 + c] * vl[c];
         a += jv * jv;
-        b += jv * lin[r * S + o];
       }
     }
-    P.obs_jv[o] = a;
-    P.obs_jv[(size_t)P.n_obs + o] = b;
+    P.obs_jv[v] = a;
     return;
   }
-  int u = t - P.n_obs;
+  int u = t - P.n_visit;
   if (u < P.n_imu) {
     const int f = u;
     const int w = P.imu_win[f];
     if (!jvSelect(P, w, mode)) return;
-    double a = 0.0, b = 0.0;
+    double a = 0.0;
     if (!(P.imu_flags[f] & 2)) {
       const int lb = P.st[w].lcur;
       const double* L = P.imu_lin[lb] + (size_t)f * kImuLin;
@@ -110,11 +128,9 @@ __global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp, i
         double jv = 0.0;
         for (int c = 0; c < 30; ++c) jv += L[15 + r * 30 + c] * v[c];
         a += jv * jv;
-        b += jv * L[r];
       }
     }
     P.imu_jv[f] = a;
-    P.imu_jv[(size_t)P.n_imu + f] = b;
     return;
   }
   u -= P.n_imu;
@@ -122,7 +138,7 @@ __global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp, i
     const int i = u;
     const int w = P.pp_win[i];
     if (!jvSelect(P, w, mode)) return;
-    double a = 0.0, b = 0.0;
+    double a = 0.0;
     const int pf = P.pose_f[P.pp_block[i]];
     if (pf >= 0) {
       const double* L = P.pp_lin[P.st[w].lcur] + 42 * (size_t)i;
@@ -131,11 +147,9 @@ __global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp, i
         double jv = 0.0;
         for (int c = 0; c < 6; ++c) jv += L[6 + r * 6 + c] * P.sF[base + c] * vF[base + c];
         a += jv * jv;
-        b += jv * L[r];
       }
     }
     P.pp_jv[i] = a;
-    P.pp_jv[(size_t)P.n_pprior + i] = b;
     return;
   }
   u -= P.n_pprior;
@@ -143,7 +157,7 @@ __global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp, i
     const int i = u;
     const int w = P.sbp_win[i];
     if (!jvSelect(P, w, mode)) return;
-    double a = 0.0, b = 0.0;
+    double a = 0.0;
     const int sf = P.sb_f[P.sbp_block[i]];
     if (sf >= 0) {
       const double* L = P.sbp_lin[P.st[w].lcur] + 90 * (size_t)i;
@@ -152,11 +166,9 @@ __global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp, i
         double jv = 0.0;
         for (int c = 0; c < 9; ++c) jv += L[9 + r * 9 + c] * P.sF[base + c] * vF[base + c];
         a += jv * jv;
-        b += jv * L[r];
       }
     }
     P.sbp_jv[i] = a;
-    P.sbp_jv[(size_t)P.n_sbprior + i] = b;
   }
 }
 
@@ -266,12 +278,25 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
   if (mode == R_JV_CAUCHY && !(s.need_gn && !s.gn_failed)) return;
   if (mode == R_JV_STEP && s.step_valid != 2) return;
   double a = 0.0, b = 0.0;
-  for (int o = ob + t; o < oe; o += kRB) { a += P.obs_jv[o]; b += P.obs_jv[(size_t)P.n_obs + o]; }
-  for (int f = ib + t; f < ie; f += kRB) { a += P.imu_jv[f]; b += P.imu_jv[(size_t)P.n_imu + f]; }
-  for (int i = pb + t; i < pe; i += kRB) { a += P.pp_jv[i]; b += P.pp_jv[(size_t)P.n_pprior + i]; }
-  for (int i = sbb + t; i < sbe; i += kRB) { a += P.sbp_jv[i]; b += P.sbp_jv[(size_t)P.n_sbprior + i]; }
+  const int lmb = P.win_lm_range[2 * w], lme = P.win_lm_range[2 * w + 1];
+  const int vb = P.lm_visit_begin[lmb], ve = P.lm_visit_begin[lme];
+  for (int v = vb + t; v < ve; v += kRB) a += P.obs_jv[v];
+  for (int f = ib + t; f < ie; f += kRB) a += P.imu_jv[f];
+  for (int i = pb + t; i < pe; i += kRB) a += P.pp_jv[i];
+  for (int i = sbb + t; i < sbe; i += kRB) a += P.sbp_jv[i];
   a = blockSum(a, sh);
-  b = blockSum(b, sh);
+  if (mode == R_JV_STEP) {
+    // (J_s step).r = step.(s g): f-blocks and free landmarks of the window
+    const int fo = P.win_foff[w], fd = P.win_fdim[w];
+    for (int e = t; e < fd; e += kRB) b += P.stepF[fo + e] * P.sF[fo + e] * P.gF[fo + e];
+    for (int l = lmb + t; l < lme; l += kRB)
+      if (P.lm_free[l])
+        for (int c = 0; c < 3; ++c) {
+          const size_t i = 3 * (size_t)l + c;
+          b += P.stepL[i] * P.sL[i] * P.gL[i];
+        }
+    b = blockSum(b, sh);
+  }
   if (mode == R_JV_CAUCHY) {
     // |gradient_|^2 over the window (f-vector + free landmarks)
     double g2 = 0.0;
@@ -542,7 +567,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
 }
 
 void launch_jv(const DevProblem& P, int mode, hipStream_t s) {
-  const int n = P.n_obs + P.n_imu + P.n_pprior + P.n_sbprior;
+  const int n = P.n_visit + P.n_imu + P.n_pprior + P.n_sbprior;
   if (n > 0) hipLaunchKernelGGL(k_jv, dim3((n + 255) / 256), dim3(256), 0, s, P.self, mode);
 }
 void launch_reduce(const DevProblem& P, int mode, hipStream_t s) {

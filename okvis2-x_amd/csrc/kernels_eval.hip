@@ -1,8 +1,8 @@
 // kernels_eval.hip — batched cost-functor evaluation for gfx950 (FP64).
 //
-//  k_eval_obs    one thread per ReprojectionError residual block: residual + minimal Jacobians
-//                (pose 2x6, landmark 2x3) with the Cauchy(1) corrector applied, written as
-//                structure-of-arrays planes (coalesced 8-byte-per-lane stores).
+//  k_eval_obs    one thread per ReprojectionError residual block: residual and the 2x3 factor A
+//                of both minimal Jacobians (pose 2x6, landmark 2x3), Cauchy(1) corrector applied,
+//                written as structure-of-arrays planes (coalesced 8-byte-per-lane stores).
 //                Restates implementation/ReprojectionError.hpp:71-220 fused: with
 //                A = L * Jh * C_CW,  J_pose = [w A, -A [p]x],  J_lm = -A  (the reference's
 //                J0_minimal = Jh_w T_CS J and J1 = -Jh_w T_CW, first three columns).
@@ -108,27 +108,14 @@ __global__ __launch_bounds__(256) void k_eval_obs(const DevProblem* __restrict__
   } else {
     cost = 0.5 * sq;
   }
+  // stored: r and A (both Cauchy-scaled); the pose/landmark Jacobians follow from A and the
+  // linearisation point (obsJacobians)
   double* lin = P.obs_lin[lb];
   const int64_t S = P.obs_stride;
   lin[0 * S + o] = r0 * sc;
   lin[1 * S + o] = r1 * sc;
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const double a0 = A[r * 3 + 0], a1 = A[r * 3 + 1], a2 = A[r * 3 + 2];
-    // -A [p]x : row a^T [p]x = (a1 p2 - a2 p1, a2 p0 - a0 p2, a0 p1 - a1 p0) ... times -1
-    const double c0 = -(a1 * p[2] - a2 * p[1]);
-    const double c1 = -(a2 * p[0] - a0 * p[2]);
-    const double c2 = -(a0 * p[1] - a1 * p[0]);
-    lin[(2 + r * 6 + 0) * S + o] = w4 * a0 * sc;
-    lin[(2 + r * 6 + 1) * S + o] = w4 * a1 * sc;
-    lin[(2 + r * 6 + 2) * S + o] = w4 * a2 * sc;
-    lin[(2 + r * 6 + 3) * S + o] = c0 * sc;
-    lin[(2 + r * 6 + 4) * S + o] = c1 * sc;
-    lin[(2 + r * 6 + 5) * S + o] = c2 * sc;
-    lin[(14 + r * 3 + 0) * S + o] = -a0 * sc;
-    lin[(14 + r * 3 + 1) * S + o] = -a1 * sc;
-    lin[(14 + r * 3 + 2) * S + o] = -a2 * sc;
-  }
+  for (int k = 0; k < 6; ++k) lin[(2 + k) * S + o] = A[k] * sc;
   P.obs_cost[lb][o] = cost;
 }
 

@@ -58,17 +58,22 @@ __global__ __launch_bounds__(256) void k_visit_lin(const DevProblem* __restrict_
   for (int i = 0; i < kVisitLin; ++i) o[i] = 0.0;
   const bool lfree = P.lm_free[l] != 0;
   const bool pf = P.pose_f[P.visit_pose[v]] >= 0;
-  const auto lin = gmem(P.obs_lin[P.st[w].lcur]);
+  const WinState& st = P.st[w];
+  const auto lin = gmem(P.obs_lin[st.lcur]);
   const int64_t S = P.obs_stride;
+  // linearisation point of lin[lcur]: params X[xcur]
+  const double* hp = P.lm[st.xcur] + 4 * (size_t)l;
+  const double* tw = P.pose[st.xcur] + 7 * (size_t)P.visit_pose[v];
+  const double w4 = hp[3];
+  const double p3[3] = {hp[0] - tw[0] * w4, hp[1] - tw[1] * w4, hp[2] - tw[2] * w4};
   for (int ob = P.visit_obs_begin[v]; ob < P.visit_obs_begin[v + 1]; ++ob) {
     if (P.obs_flags[ob] & 2) continue;
-    double r[2], Jp[12], Jl[6];
+    double r[2], A[6], Jp[12], Jl[6];
     r[0] = lin[0 * S + ob];
     r[1] = lin[1 * S + ob];
 #pragma unroll
-    for (int k = 0; k < 12; ++k) Jp[k] = lin[(2 + k) * S + ob];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) Jl[k] = lin[(14 + k) * S + ob];
+    for (int k = 0; k < 6; ++k) A[k] = lin[(2 + k) * S + ob];
+    obsJacobians(A, p3, w4, Jp, Jl);
     if (lfree) {
 #pragma unroll
       for (int a2 = 0; a2 < 3; ++a2) {

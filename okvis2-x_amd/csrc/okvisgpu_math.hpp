@@ -211,4 +211,23 @@ OKG_HD void projectHomogeneous(const Cam& c, double x, double y, double z, doubl
   kp[1] = c.fv * d1 + c.cv;
 }
 
+// Minimal reprojection Jacobians from the stored linearisation (ReprojectionError.hpp:71-220 in the
+// fused form): with A = L Jh C_CW (2x3, Cauchy-scaled) and p = hp_W.xyz - t_WS w at the
+// linearisation point, J_pose = [w A, -A [p]x] (2x6) and J_landmark = -A (2x3).
+OKG_HD void obsJacobians(const double A[6], const double p[3], double w, double Jp[12], double Jl[6]) {
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const double a0 = A[r * 3 + 0], a1 = A[r * 3 + 1], a2 = A[r * 3 + 2];
+    Jp[r * 6 + 0] = w * a0;
+    Jp[r * 6 + 1] = w * a1;
+    Jp[r * 6 + 2] = w * a2;
+    Jp[r * 6 + 3] = -(a1 * p[2] - a2 * p[1]);
+    Jp[r * 6 + 4] = -(a2 * p[0] - a0 * p[2]);
+    Jp[r * 6 + 5] = -(a0 * p[1] - a1 * p[0]);
+    Jl[r * 3 + 0] = -a0;
+    Jl[r * 3 + 1] = -a1;
+    Jl[r * 3 + 2] = -a2;
+  }
+}
+
 }  // namespace okg

@@ -24,6 +24,7 @@
 #include "../../include/okvisgpu.h"
 #include "device_problem.hpp"
 #include "launch.hpp"
+#include "okvisgpu_math.hpp"
 
 using namespace okg;
 
@@ -1205,11 +1206,11 @@ double kernelWork(const HostBatch& B, const DevProblem& P, int k) {
       const double panels = (double)(B.chol_panel_items.size() / 2), upd = (double)(B.chol_upd_items.size() / 3);
       return diag * (2.0 * tile3 / 3.0 + 4.0 * 64 * 64) + panels * (2.0 * tile3 + 4.0 * 64 * 64) + upd * 2.0 * tile3;
     }
-    case K_VISIT_LIN: return nObs * (20 * d8 + 1) + nVis * (kVisitLin * d8 + 16);
+    case K_VISIT_LIN: return nObs * (kObsLin * d8 + 1) + nVis * (kVisitLin * d8 + 7 * d8 + 16);
     case K_VISIT_PREP: return nVis * (18 * d8 + kVisitUY * d8 + 12) + nLm * 15 * d8;
     case K_EVAL_IMU: return nImu * (2.0 * kImuState + kImuLin + 2 * 16) * d8 + (double)B.imu_ts.size() * 7 * d8;
-    case K_EVAL_OBS: return nObs * (16 + 32 + 13 + 20 * d8 + 8) + nLm * 4 * d8 + (double)B.pose_f.size() * 7 * d8;
-    case K_JV: return nObs * (20 * d8 + 2 * 2 * d8) + nImu * kImuLin * d8 + nLm * 3 * d8 * 2;
+    case K_EVAL_OBS: return nObs * (16 + 32 + 13 + kObsLin * d8 + 8) + nLm * 4 * d8 + (double)B.pose_f.size() * 7 * d8;
+    case K_JV: return nObs * (kObsLin * d8 + 1) + nVis * (7 + 9 + 1) * d8 + nImu * kImuLin * d8;
     case K_FGRAD: return nVis * 12 * d8 + nImu * kImuLin * d8 + (double)B.fb_contrib.size() * 16;
   }
   return 0.0;
@@ -1359,12 +1360,19 @@ int okvisgpu_eval_reprojection(okvisgpu_ctx* c, int32_t window, double* r, doubl
     std::vector<double> lin((size_t)kObsLin * S);
     HIPCHK(hipMemcpyAsync(lin.data(), c->P.obs_lin[0], lin.size() * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    const int ob = c->B.obs_base[window], n = c->probs[window]->n_observations;
+    const okvisgpu_problem* pr = c->probs[window];
+    const int ob = c->B.obs_base[window], n = pr->n_observations;
     for (int k = 0; k < n; ++k) {
       const int g = ob + k, o = c->B.obs_orig[g];
       if (r) for (int i = 0; i < 2; ++i) r[2 * o + i] = lin[(size_t)i * S + g];
-      if (Jp) for (int i = 0; i < 12; ++i) Jp[12 * o + i] = lin[(size_t)(2 + i) * S + g];
-      if (Jl) for (int i = 0; i < 6; ++i) Jl[6 * o + i] = lin[(size_t)(14 + i) * S + g];
+      double A[6], Jpo[12], Jlo[6];
+      for (int i = 0; i < 6; ++i) A[i] = lin[(size_t)(2 + i) * S + g];
+      const double* hp = &pr->landmarks[4 * pr->obs_landmark[o]];
+      const double* tw = &pr->poses[7 * pr->obs_pose[o]];
+      const double p3[3] = {hp[0] - tw[0] * hp[3], hp[1] - tw[1] * hp[3], hp[2] - tw[2] * hp[3]};
+      obsJacobians(A, p3, hp[3], Jpo, Jlo);
+      if (Jp) for (int i = 0; i < 12; ++i) Jp[12 * o + i] = Jpo[i];
+      if (Jl) for (int i = 0; i < 6; ++i) Jl[6 * o + i] = Jlo[i];
     }
     return (int)OKVISGPU_OK;
   });
