@@ -25,7 +25,7 @@ constexpr int kImuState = 292;        // == OKVISGPU_IMU_STATE_DOUBLES
 //   plane 0-1: r (Cauchy-corrected)   plane 2-13: J_pose 2x6   plane 14-19: J_lm 2x3
 constexpr int kObsLin = 8;   // r (2) | A = L Jh C_CW (2x3), Cauchy-scaled
 constexpr int kVisitLin = 54;
-constexpr int kVisitUY = 42;
+constexpr int kVisitUY = 24;  // Z = U L^-T (6x3) | U z (6)
 
 // contribution record types for the reduced-system assembly
 enum ContribType : int32_t {
@@ -113,11 +113,11 @@ struct DevProblem {
   const int32_t* visit_lm;         // [n_visit]
   double* lm_V;                    // [n_lm][6]  sum J_l^T J_l (unscaled, sym packed 00 01 02 11 12 22)
   double* lm_g;                    // [n_lm][3]  J_l^T r
-  double* lm_Vinv;                 // [n_lm][9]  (s V s + D^2)^-1
-  double* lm_z;                    // [n_lm][3]  Vinv (s g)
+  double* lm_Linv;                 // [n_lm][9]  L^-1, L L^T = s V s + D^2 (lower triangular)
+  double* lm_zz;                   // [n_lm][3]  L^-1 (s g)
   double* visit_lin;               // [n_visit][kVisitLin] W = J_p^T J_l (18) | H = J_p^T J_p (21, sym packed)
                                    //   | g = J_p^T r (6) | V part J_l^T J_l (6) | J_l^T r (3)   (unscaled)
-  double* visit_UY;                // [n_visit][kVisitUY] U = s_p W s_l (6x3) | Y = U Vinv (6x3) | U z (6)
+  double* visit_UY;                // [n_visit][kVisitUY] Z = s_p W s_l L^-T (6x3) | U z (6)   (per GN solve)
 
   // --- IMU factors
   const int32_t* imu_blocks;       // [n_imu][4] global pose0 sb0 pose1 sb1

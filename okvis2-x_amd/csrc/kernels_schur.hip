@@ -8,8 +8,8 @@
 //   k_lm_lin      one thread per landmark: V, g_l over its visits; iteration 0: Jacobi scaling.
 //   k_fgrad       one wavefront per f-block (pose / speed-bias): unscaled gradient and
 //                 diag(H_ff), and at iteration 0 the Jacobi scaling 1/(1+sqrt(diag)).
-//   k_lm_prep     one thread per landmark: (s V s + D^2)^-1 via 3x3 LLT (InvertPSDMatrix), z.
-//   k_visit_prep  one thread per visit: U = s_p W s_l, Y = U V^-1, U z.
+//   k_lm_prep     one thread per landmark: 3x3 LLT of s V s + D^2 (InvertPSDMatrix), L^-1, L^-1 s g.
+//   k_visit_prep  one thread per visit: Z = s_p W s_l L^-T and U z (Y_a U_b^T = Z_a Z_b^T).
 //   k_zero_S      clears the structurally non-zero tiles of S (padded diagonal = 1).
 //   k_assemble_pp one wavefront per pose-pose block pair (i >= j): 8 groups of 6 lanes (one per
 //                 row) sum fixed, interleaved subsets of the pair's contributions — visits,
@@ -247,34 +247,27 @@ __global__ __launch_bounds__(256) void k_lm_prep(const DevProblem* __restrict__ 
     P.st[w].gn_failed = 1;
     return;
   }
-  double inv[9];
+  // L^-1 (lower triangular) and zz = L^-1 (s g): V'^-1 = L^-T L^-1, so the Schur terms factor as
+  // Y_a U_b^T = U_a V'^-1 U_b^T = Z_a Z_b^T with Z = U L^-T (k_visit_prep)
+  double Li[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   for (int c = 0; c < 3; ++c) {
-    double e[3] = {0, 0, 0};
-    e[c] = 1.0;
-    for (int i = 0; i < 3; ++i) {
-      double t = e[i];
-      for (int j = 0; j < i; ++j) t -= L[i * 3 + j] * e[j];
-      e[i] = t / L[i * 3 + i];
+    Li[c * 3 + c] = 1.0 / L[c * 3 + c];
+    for (int i = c + 1; i < 3; ++i) {
+      double t = 0.0;
+      for (int j = c; j < i; ++j) t -= L[i * 3 + j] * Li[j * 3 + c];
+      Li[i * 3 + c] = t / L[i * 3 + i];
     }
-    for (int i = 2; i >= 0; --i) {
-      double t = e[i];
-      for (int j = i + 1; j < 3; ++j) t -= L[j * 3 + i] * e[j];
-      e[i] = t / L[i * 3 + i];
-    }
-    for (int r = 0; r < 3; ++r) inv[r * 3 + c] = e[r];
   }
-  double sg[3] = {s[0] * g[0], s[1] * g[1], s[2] * g[2]};
-  double* Vi = P.lm_Vinv + 9 * (size_t)l;
-  for (int i = 0; i < 9; ++i) Vi[i] = inv[i];
-  double z[3];
-  for (int a = 0; a < 3; ++a) {
-    z[a] = inv[a * 3 + 0] * sg[0] + inv[a * 3 + 1] * sg[1] + inv[a * 3 + 2] * sg[2];
-    P.lm_z[3 * (size_t)l + a] = z[a];
-  }
+  const double sg[3] = {s[0] * g[0], s[1] * g[1], s[2] * g[2]};
+  double* Lo = P.lm_Linv + 9 * (size_t)l;
+  for (int i = 0; i < 9; ++i) Lo[i] = Li[i];
+  for (int a = 0; a < 3; ++a)
+    P.lm_zz[3 * (size_t)l + a] = Li[a * 3 + 0] * sg[0] + Li[a * 3 + 1] * sg[1] + Li[a * 3 + 2] * sg[2];
 }
 
-// One thread per visit with a free pose and landmark: U = s_p W s_l, Y = U Vinv, U z — the
-// operands of the Schur terms (42-double AoS records; 16-byte stores, merged in L2).
+// One thread per visit with a free pose and landmark: Z = U L^-T with U = s_p W s_l, and U z = Z zz
+// — the operands of the Schur terms Y_a U_b^T = Z_a Z_b^T (24-double AoS records; 16-byte stores,
+// merged in L2).
 __global__ __launch_bounds__(256) void k_visit_prep(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int v = blockIdx.x * blockDim.x + threadIdx.x;
@@ -291,27 +284,28 @@ __global__ __launch_bounds__(256) void k_visit_prep(const DevProblem* __restrict
   }
   const auto W = gmem(P.visit_lin + (size_t)v * kVisitLin);
   const auto sl = gmem(P.sL + 3 * (size_t)l);
-  const auto inv = gmem(P.lm_Vinv + 9 * (size_t)l);
-  const auto z = gmem(P.lm_z + 3 * (size_t)l);
+  const auto Lig = gmem(P.lm_Linv + 9 * (size_t)l);
+  const auto zg = gmem(P.lm_zz + 3 * (size_t)l);
   const auto sp = gmem(P.sF + (size_t)P.win_foff[w] + pf);
-  double w18[18], iv[9], zz[3], s3[3], spr[6];
+  double w18[18], Li[9], zz[3], s3[3], spr[6];
 #pragma unroll
   for (int i = 0; i < 18; ++i) w18[i] = W[i];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) iv[i] = inv[i];
+  for (int i = 0; i < 9; ++i) Li[i] = Lig[i];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) { zz[i] = z[i]; s3[i] = sl[i]; }
+  for (int i = 0; i < 3; ++i) { zz[i] = zg[i]; s3[i] = sl[i]; }
 #pragma unroll
   for (int i = 0; i < 6; ++i) spr[i] = sp[i];
-  double o[kVisitUY];
+  double o[kVisitUY];  // Z = s_p W s_l L^-T (6x3) | U z = Z zz (6)
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     const double u0 = spr[r] * w18[r * 3 + 0] * s3[0], u1 = spr[r] * w18[r * 3 + 1] * s3[1],
                  u2 = spr[r] * w18[r * 3 + 2] * s3[2];
-    o[r * 3 + 0] = u0; o[r * 3 + 1] = u1; o[r * 3 + 2] = u2;
-#pragma unroll
-    for (int b2 = 0; b2 < 3; ++b2) o[18 + r * 3 + b2] = u0 * iv[0 * 3 + b2] + u1 * iv[1 * 3 + b2] + u2 * iv[2 * 3 + b2];
-    o[36 + r] = u0 * zz[0] + u1 * zz[1] + u2 * zz[2];
+    const double z0 = u0 * Li[0];
+    const double z1 = u0 * Li[3] + u1 * Li[4];
+    const double z2 = u0 * Li[6] + u1 * Li[7] + u2 * Li[8];
+    o[r * 3 + 0] = z0; o[r * 3 + 1] = z1; o[r * 3 + 2] = z2;
+    o[18 + r] = z0 * zz[0] + z1 * zz[1] + z2 * zz[2];
   }
 #pragma unroll
   for (int i = 0; i < kVisitUY / 2; ++i) out[i] = double2{o[2 * i], o[2 * i + 1]};
@@ -371,17 +365,17 @@ __global__ __launch_bounds__(256) void k_assemble_pp(const DevProblem* __restric
     double h0[6], h1[6];
 #pragma unroll
     for (int q = 0; q < 6; ++q) { h0[q] = H0[sym6(r, q)]; h1[q] = H1[sym6(r, q)]; }
-    const double z0 = vuy[(size_t)C0.a * kVisitUY + 36 + r], z1 = vuy[(size_t)C1.a * kVisitUY + 36 + r];
+    const double z0 = vuy[(size_t)C0.a * kVisitUY + 18 + r], z1 = vuy[(size_t)C1.a * kVisitUY + 18 + r];
 #pragma unroll
     for (int q = 0; q < 6; ++q) H[q] += h0[q] + (v1 ? h1[q] : 0.0);
     uz += (C0.b ? z0 : 0.0) + ((v1 && C1.b) ? z1 : 0.0);
   }
-  // landmark pairs: row r of Y_a U_b^T
+  // landmark pairs: row r of Z_a Z_b^T (= Y_a U_b^T)
   for (int c0 = pb + g0; c0 < ob; c0 += 2 * kGroups) {
     const int c1 = c0 + kGroups;
     const bool v1 = c1 < ob;
     const Contrib C0 = pc[c0], C1 = pc[v1 ? c1 : c0];
-    const auto Y0 = vuy + (size_t)C0.a * kVisitUY + 18 + 3 * r, Y1 = vuy + (size_t)C1.a * kVisitUY + 18 + 3 * r;
+    const auto Y0 = vuy + (size_t)C0.a * kVisitUY + 3 * r, Y1 = vuy + (size_t)C1.a * kVisitUY + 3 * r;
     const auto U0 = vuy + (size_t)C0.b * kVisitUY, U1 = vuy + (size_t)C1.b * kVisitUY;
     double y0[3], y1[3], u0[18], u1[18];
 #pragma unroll
@@ -514,21 +508,24 @@ __global__ __launch_bounds__(256) void k_lm_backsub(const DevProblem* __restrict
   const int w = P.lm_win[l];
   if (!gnSelect(P, w)) return;
   const int foff = P.win_foff[w];
-  const double* s = P.sL + 3 * (size_t)l;
-  const double* g = P.lm_g + 3 * (size_t)l;
-  double rhs[3] = {s[0] * g[0], s[1] * g[1], s[2] * g[2]};
+  // y_l = V'^-1 (s g - sum_v U_v^T y_p) = L^-T (zz - sum_v Z_v^T y_p)
+  const double* zz = P.lm_zz + 3 * (size_t)l;
+  double t3[3] = {zz[0], zz[1], zz[2]};
   for (int v = P.lm_visit_begin[l]; v < P.lm_visit_begin[l + 1]; ++v) {
     const int pf = P.pose_f[P.visit_pose[v]];
     if (pf < 0) continue;
-    const double* U = P.visit_UY + (size_t)v * kVisitUY;  // U = s_p W s_l
+    const double* Z = P.visit_UY + (size_t)v * kVisitUY;
     for (int rr = 0; rr < 6; ++rr) {
       const double y = P.yF[(size_t)foff + pf + rr];
-      for (int a = 0; a < 3; ++a) rhs[a] -= U[rr * 3 + a] * y;
+      for (int a = 0; a < 3; ++a) t3[a] -= Z[rr * 3 + a] * y;
     }
   }
-  const double* Vi = P.lm_Vinv + 9 * (size_t)l;
-  for (int a = 0; a < 3; ++a)
-    P.yL[3 * (size_t)l + a] = Vi[a * 3 + 0] * rhs[0] + Vi[a * 3 + 1] * rhs[1] + Vi[a * 3 + 2] * rhs[2];
+  const double* Li = P.lm_Linv + 9 * (size_t)l;
+  for (int a = 0; a < 3; ++a) {
+    double y = 0.0;
+    for (int c = a; c < 3; ++c) y += Li[c * 3 + a] * t3[c];
+    P.yL[3 * (size_t)l + a] = y;
+  }
 }
 
 // gauss_newton_step_ = -diagonal_ .* y ; gradient_ = s .* g / diagonal_ ; v = gradient_ / diagonal_

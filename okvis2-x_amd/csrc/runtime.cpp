@@ -686,7 +686,7 @@ struct okvisgpu_ctx {
     D.obs_lin[0] = dp(o_obs_lin0); D.obs_lin[1] = dp(o_obs_lin1);
     D.obs_cost[0] = dp(o_obs_cost0); D.obs_cost[1] = dp(o_obs_cost1); D.obs_jv = dp(o_obs_jv);
     D.lm_visit_begin = ip(o_lmvb); D.visit_pose = ip(o_vpose); D.visit_obs_begin = ip(o_vob); D.visit_lm = ip(o_vlm);
-    D.lm_V = dp(o_lmV); D.lm_g = dp(o_lmg); D.lm_Vinv = dp(o_lmVi); D.lm_z = dp(o_lmz);
+    D.lm_V = dp(o_lmV); D.lm_g = dp(o_lmg); D.lm_Linv = dp(o_lmVi); D.lm_zz = dp(o_lmz);
     D.visit_lin = dp(o_vlin); D.visit_UY = dp(o_vUY);
     D.imu_blocks = ip(o_imu_blocks); D.imu_win = ip(o_imu_win); D.imu_flags = up(o_imu_flags);
     D.imu_t0 = lp(o_imu_t0); D.imu_t1 = lp(o_imu_t1); D.imu_sbegin = ip(o_imu_sb); D.imu_ts = lp(o_imu_ts);
