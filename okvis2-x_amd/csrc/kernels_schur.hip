@@ -355,38 +355,52 @@ __global__ __launch_bounds__(256) void k_assemble_pp(const DevProblem* __restric
   double H[6], Sc[6], uz = 0.0;
 #pragma unroll
   for (int q = 0; q < 6; ++q) { H[q] = 0.0; Sc[q] = 0.0; }
-  const int g0 = inGroup ? g : 1 << 29;  // lanes 48..63 idle
+  const int g0 = inGroup ? g : 1 << 29;  // lanes 48..63 idle (factor-block loop)
+  // Descriptors: one coalesced load of 64 per round (lane L holds c = base + L), handed to the
+  // groups with __shfl, so each step waits on a single round of operand loads.
   // visits (diagonal pairs): row r of H_v, and (U_v z_l)_r
-  for (int c0 = cb + g0; c0 < pb; c0 += 2 * kGroups) {
-    const int c1 = c0 + kGroups;
-    const bool v1 = c1 < pb;
-    const Contrib C0 = pc[c0], C1 = pc[v1 ? c1 : c0];
-    const auto H0 = vlin + (size_t)C0.a * kVisitLin + 18, H1 = vlin + (size_t)C1.a * kVisitLin + 18;
-    double h0[6], h1[6];
+  for (int base = cb; base < pb; base += 64) {
+    const int myc = min(base + lane, pb - 1);
+    const int da = pc[myc].a, db = pc[myc].b;
+    const int nstep = min(64, pb - base);
+    for (int st = 0; st < nstep; st += 2 * kGroups) {
+      const int k0 = st + g, k1 = st + kGroups + g;
+      const int a0 = __shfl(da, k0 & 63, 64), a1 = __shfl(da, k1 & 63, 64);
+      const int b0 = __shfl(db, k0 & 63, 64), b1 = __shfl(db, k1 & 63, 64);
+      const bool v0 = inGroup && k0 < nstep, v1 = inGroup && k1 < nstep;
+      const auto H0 = vlin + (size_t)a0 * kVisitLin + 18, H1 = vlin + (size_t)a1 * kVisitLin + 18;
+      double h0[6], h1[6];
 #pragma unroll
-    for (int q = 0; q < 6; ++q) { h0[q] = H0[sym6(r, q)]; h1[q] = H1[sym6(r, q)]; }
-    const double z0 = vuy[(size_t)C0.a * kVisitUY + 18 + r], z1 = vuy[(size_t)C1.a * kVisitUY + 18 + r];
+      for (int q = 0; q < 6; ++q) { h0[q] = H0[sym6(r, q)]; h1[q] = H1[sym6(r, q)]; }
+      const double z0 = vuy[(size_t)a0 * kVisitUY + 18 + r], z1 = vuy[(size_t)a1 * kVisitUY + 18 + r];
 #pragma unroll
-    for (int q = 0; q < 6; ++q) H[q] += h0[q] + (v1 ? h1[q] : 0.0);
-    uz += (C0.b ? z0 : 0.0) + ((v1 && C1.b) ? z1 : 0.0);
+      for (int q = 0; q < 6; ++q) H[q] += (v0 ? h0[q] : 0.0) + (v1 ? h1[q] : 0.0);
+      uz += ((v0 && b0) ? z0 : 0.0) + ((v1 && b1) ? z1 : 0.0);
+    }
   }
   // landmark pairs: row r of Z_a Z_b^T (= Y_a U_b^T)
-  for (int c0 = pb + g0; c0 < ob; c0 += 2 * kGroups) {
-    const int c1 = c0 + kGroups;
-    const bool v1 = c1 < ob;
-    const Contrib C0 = pc[c0], C1 = pc[v1 ? c1 : c0];
-    const auto Y0 = vuy + (size_t)C0.a * kVisitUY + 3 * r, Y1 = vuy + (size_t)C1.a * kVisitUY + 3 * r;
-    const auto U0 = vuy + (size_t)C0.b * kVisitUY, U1 = vuy + (size_t)C1.b * kVisitUY;
-    double y0[3], y1[3], u0[18], u1[18];
+  for (int base = pb; base < ob; base += 64) {
+    const int myc = min(base + lane, ob - 1);
+    const int da = pc[myc].a, db = pc[myc].b;
+    const int nstep = min(64, ob - base);
+    for (int st = 0; st < nstep; st += 2 * kGroups) {
+      const int k0 = st + g, k1 = st + kGroups + g;
+      const int a0 = __shfl(da, k0 & 63, 64), a1 = __shfl(da, k1 & 63, 64);
+      const int b0 = __shfl(db, k0 & 63, 64), b1 = __shfl(db, k1 & 63, 64);
+      const bool v0 = inGroup && k0 < nstep, v1 = inGroup && k1 < nstep;
+      const auto Y0 = vuy + (size_t)a0 * kVisitUY + 3 * r, Y1 = vuy + (size_t)a1 * kVisitUY + 3 * r;
+      const auto U0 = vuy + (size_t)b0 * kVisitUY, U1 = vuy + (size_t)b1 * kVisitUY;
+      double y0[3], y1[3], u0[18], u1[18];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) { y0[i] = Y0[i]; y1[i] = Y1[i]; }
+      for (int i = 0; i < 3; ++i) { y0[i] = Y0[i]; y1[i] = Y1[i]; }
 #pragma unroll
-    for (int i = 0; i < 18; ++i) { u0[i] = U0[i]; u1[i] = U1[i]; }
+      for (int i = 0; i < 18; ++i) { u0[i] = U0[i]; u1[i] = U1[i]; }
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const double t0 = y0[0] * u0[3 * q] + y0[1] * u0[3 * q + 1] + y0[2] * u0[3 * q + 2];
-      const double t1 = y1[0] * u1[3 * q] + y1[1] * u1[3 * q + 1] + y1[2] * u1[3 * q + 2];
-      Sc[q] += t0 + (v1 ? t1 : 0.0);
+      for (int q = 0; q < 6; ++q) {
+        const double t0 = y0[0] * u0[3 * q] + y0[1] * u0[3 * q + 1] + y0[2] * u0[3 * q + 2];
+        const double t1 = y1[0] * u1[3 * q] + y1[1] * u1[3 * q + 1] + y1[2] * u1[3 * q + 2];
+        Sc[q] += (v0 ? t0 : 0.0) + (v1 ? t1 : 0.0);
+      }
     }
   }
   // factor blocks (IMU, pose prior): row r of J_i^T J_j
