@@ -25,6 +25,7 @@ constexpr int kImuState = 292;        // == OKVISGPU_IMU_STATE_DOUBLES
 //   plane 0-1: r (Cauchy-corrected)   plane 2-13: J_pose 2x6   plane 14-19: J_lm 2x3
 constexpr int kObsLin = 8;   // r (2) | A = L Jh C_CW (2x3), Cauchy-scaled
 constexpr int kVisitLin = 54;
+constexpr int kImuHess = 465 + 30;  // packed upper J^T J (30x30) | J^T r
 constexpr int kVisitUY = 24;  // Z = U L^-T (6x3) | U z (6)
 
 // contribution record types for the reduced-system assembly
@@ -132,6 +133,7 @@ struct DevProblem {
   double* imu_state;               // [n_imu][kImuState]
   double* imu_lin[2];              // [n_imu][kImuLin]
   double* imu_cost[2];             // [n_imu]
+  double* imu_H;                   // [n_imu][kImuHess] of the linearisation lin[lcur] (k_imu_hess)
   double* imu_jv;                  // [n_imu] |J_s v|^2
 
   // --- priors

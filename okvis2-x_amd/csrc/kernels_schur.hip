@@ -6,6 +6,7 @@
 //                 g_p = J_p^T r and the visit's share of V = J_l^T J_l, g_l = J_l^T r from the
 //                 stored linearisation (unscaled; the Jacobi scaling is applied by consumers).
 //   k_lm_lin      one thread per landmark: V, g_l over its visits; iteration 0: Jacobi scaling.
+//   k_imu_hess    one wavefront per IMU factor: J^T J (packed) and J^T r of its 15x30 Jacobian.
 //   k_fgrad       one wavefront per f-block (pose / speed-bias): unscaled gradient and
 //                 diag(H_ff), and at iteration 0 the Jacobi scaling 1/(1+sqrt(diag)).
 //   k_lm_prep     one thread per landmark: 3x3 LLT of s V s + D^2 (InvertPSDMatrix), L^-1, L^-1 s g.
@@ -127,6 +128,43 @@ __device__ __forceinline__ const double* imuLin(const DevProblem& P, int lb, int
   return P.imu_lin[lb] + (size_t)f * kImuLin;
 }
 
+__device__ __forceinline__ int sym30(int a, int b) {  // packed upper triangle of a 30x30
+  if (a > b) { const int t = a; a = b; b = t; }
+  return a * 30 - (a * (a - 1)) / 2 + (b - a);
+}
+
+// J^T J (30x30, packed) and J^T r of every IMU factor of the windows being linearised, one
+// wavefront per factor with J staged in LDS; consumed by k_fgrad and both assembly kernels.
+__global__ __launch_bounds__(256) void k_imu_hess(const DevProblem* __restrict__ Pp, int lin_mode) {
+  const DevProblem& P = *Pp;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int f = blockIdx.x * 4 + wv;
+  __shared__ double sJ[4][kImuLin];
+  if (f >= P.n_imu) return;
+  const int w = P.imu_win[f];
+  if (!linSelect(P, w, lin_mode) || (P.imu_flags[f] & 2)) return;
+  const auto L = gmem(P.imu_lin[P.st[w].lcur] + (size_t)f * kImuLin);
+  double* J = sJ[wv];
+  for (int e = lane; e < kImuLin; e += 64) J[e] = L[e];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double* H = P.imu_H + (size_t)f * kImuHess;
+  for (int e = lane; e < kImuHess; e += 64) {
+    double acc = 0.0;
+    if (e < 465) {
+      int a = 0, rem = e;
+      while (rem >= 30 - a) { rem -= 30 - a; ++a; }
+      const int b = a + rem;
+      for (int k = 0; k < 15; ++k) acc += J[15 + k * 30 + a] * J[15 + k * 30 + b];
+    } else {
+      const int a = e - 465;
+      for (int k = 0; k < 15; ++k) acc += J[15 + k * 30 + a] * J[k];
+    }
+    H[e] = acc;
+  }
+}
+
 // One wavefront per f-block: lanes stride over the contribution list, then a fixed xor-tree
 // reduction (deterministic).
 __global__ __launch_bounds__(64) void k_fgrad(const DevProblem* __restrict__ Pp, int lin_mode) {
@@ -149,16 +187,10 @@ __global__ __launch_bounds__(64) void k_fgrad(const DevProblem* __restrict__ Pp,
 #pragma unroll
       for (int c = 0; c < 6; ++c) { g[c] += gp[c]; hd[c] += H[sym6(c, c)]; }
     } else if (cb.type == C_IMU) {
-      const double* L = imuLin(P, lb, cb.a);
+      const double* Hf = P.imu_H + (size_t)cb.a * kImuHess;
       for (int c = 0; c < n; ++c) {
-        double sg = 0, sh = 0;
-        for (int k2 = 0; k2 < 15; ++k2) {
-          const double j = L[15 + k2 * 30 + cb.b + c];
-          sg += j * L[k2];
-          sh += j * j;
-        }
-        g[c] += sg;
-        hd[c] += sh;
+        g[c] += Hf[465 + cb.b + c];
+        hd[c] += Hf[sym30(cb.b + c, cb.b + c)];
       }
     } else if (cb.type == C_PPRIOR) {
       const double* L = P.pp_lin[lb] + 42 * (size_t)cb.a;
@@ -337,7 +369,7 @@ __global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ P
 // its own Y row, and two steps of descriptors/operands are in flight per lane.
 constexpr int kGroups = 8;
 
-__global__ __launch_bounds__(256) void k_assemble_pp(const DevProblem* __restrict__ Pp) {
+__global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -363,43 +395,41 @@ __global__ __launch_bounds__(256) void k_assemble_pp(const DevProblem* __restric
     const int myc = min(base + lane, pb - 1);
     const int da = pc[myc].a, db = pc[myc].b;
     const int nstep = min(64, pb - base);
-    for (int st = 0; st < nstep; st += 2 * kGroups) {
-      const int k0 = st + g, k1 = st + kGroups + g;
-      const int a0 = __shfl(da, k0 & 63, 64), a1 = __shfl(da, k1 & 63, 64);
-      const int b0 = __shfl(db, k0 & 63, 64), b1 = __shfl(db, k1 & 63, 64);
-      const bool v0 = inGroup && k0 < nstep, v1 = inGroup && k1 < nstep;
-      const auto H0 = vlin + (size_t)a0 * kVisitLin + 18, H1 = vlin + (size_t)a1 * kVisitLin + 18;
-      double h0[6], h1[6];
+    for (int st = 0; st < nstep; st += kGroups) {
+      const int k0 = st + g;
+      const int a0 = __shfl(da, k0 & 63, 64), b0 = __shfl(db, k0 & 63, 64);
+      const bool v0 = inGroup && k0 < nstep;
+      const auto H0 = vlin + (size_t)a0 * kVisitLin + 18;
+      double h0[6];
 #pragma unroll
-      for (int q = 0; q < 6; ++q) { h0[q] = H0[sym6(r, q)]; h1[q] = H1[sym6(r, q)]; }
-      const double z0 = vuy[(size_t)a0 * kVisitUY + 18 + r], z1 = vuy[(size_t)a1 * kVisitUY + 18 + r];
+      for (int q = 0; q < 6; ++q) h0[q] = H0[sym6(r, q)];
+      const double z0 = vuy[(size_t)a0 * kVisitUY + 18 + r];
 #pragma unroll
-      for (int q = 0; q < 6; ++q) H[q] += (v0 ? h0[q] : 0.0) + (v1 ? h1[q] : 0.0);
-      uz += ((v0 && b0) ? z0 : 0.0) + ((v1 && b1) ? z1 : 0.0);
+      for (int q = 0; q < 6; ++q) H[q] += v0 ? h0[q] : 0.0;
+      uz += (v0 && b0) ? z0 : 0.0;
     }
   }
-  // landmark pairs: row r of Z_a Z_b^T (= Y_a U_b^T)
+  // landmark pairs: row r of Z_a Z_b^T (= Y_a U_b^T); one contribution per group and step keeps
+  // the operand registers low enough for 6 wavefronts per SIMD
   for (int base = pb; base < ob; base += 64) {
     const int myc = min(base + lane, ob - 1);
     const int da = pc[myc].a, db = pc[myc].b;
     const int nstep = min(64, ob - base);
-    for (int st = 0; st < nstep; st += 2 * kGroups) {
-      const int k0 = st + g, k1 = st + kGroups + g;
-      const int a0 = __shfl(da, k0 & 63, 64), a1 = __shfl(da, k1 & 63, 64);
-      const int b0 = __shfl(db, k0 & 63, 64), b1 = __shfl(db, k1 & 63, 64);
-      const bool v0 = inGroup && k0 < nstep, v1 = inGroup && k1 < nstep;
-      const auto Y0 = vuy + (size_t)a0 * kVisitUY + 3 * r, Y1 = vuy + (size_t)a1 * kVisitUY + 3 * r;
-      const auto U0 = vuy + (size_t)b0 * kVisitUY, U1 = vuy + (size_t)b1 * kVisitUY;
-      double y0[3], y1[3], u0[18], u1[18];
+    for (int st = 0; st < nstep; st += kGroups) {
+      const int k0 = st + g;
+      const int a0 = __shfl(da, k0 & 63, 64), b0 = __shfl(db, k0 & 63, 64);
+      const bool v0 = inGroup && k0 < nstep;
+      const auto Y0 = vuy + (size_t)a0 * kVisitUY + 3 * r;
+      const auto U0 = vuy + (size_t)b0 * kVisitUY;
+      double y0[3], u0[18];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) { y0[i] = Y0[i]; y1[i] = Y1[i]; }
+      for (int i = 0; i < 3; ++i) y0[i] = Y0[i];
 #pragma unroll
-      for (int i = 0; i < 18; ++i) { u0[i] = U0[i]; u1[i] = U1[i]; }
+      for (int i = 0; i < 18; ++i) u0[i] = U0[i];
 #pragma unroll
       for (int q = 0; q < 6; ++q) {
         const double t0 = y0[0] * u0[3 * q] + y0[1] * u0[3 * q + 1] + y0[2] * u0[3 * q + 2];
-        const double t1 = y1[0] * u1[3 * q] + y1[1] * u1[3 * q + 1] + y1[2] * u1[3 * q + 2];
-        Sc[q] += (v0 ? t0 : 0.0) + (v1 ? t1 : 0.0);
+        Sc[q] += v0 ? t0 : 0.0;
       }
     }
   }
@@ -407,14 +437,17 @@ __global__ __launch_bounds__(256) void k_assemble_pp(const DevProblem* __restric
   const int lb = P.st[w].lcur;
   for (int c = ob + g0; c < ce; c += kGroups) {
     const Contrib C = pc[c];
-    const double* L;
-    int rows, ld, ci, cj;
-    if (C.type == C_IMU) { L = imuLin(P, lb, C.a) + 15; rows = 15; ld = 30; ci = C.b; cj = C.c; }
-    else { L = P.pp_lin[lb] + 42 * (size_t)C.a + 6; rows = 6; ld = 6; ci = 0; cj = 0; }
-    for (int k2 = 0; k2 < rows; ++k2) {
-      const double jr = L[k2 * ld + ci + r];
+    if (C.type == C_IMU) {
+      const auto Hf = gmem(P.imu_H + (size_t)C.a * kImuHess);
 #pragma unroll
-      for (int q = 0; q < 6; ++q) H[q] += jr * L[k2 * ld + cj + q];
+      for (int q = 0; q < 6; ++q) H[q] += Hf[sym30(C.b + r, C.c + q)];
+    } else {
+      const double* L = P.pp_lin[lb] + 42 * (size_t)C.a + 6;
+      for (int k2 = 0; k2 < 6; ++k2) {
+        const double jr = L[k2 * 6 + r];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) H[q] += jr * L[k2 * 6 + q];
+      }
     }
   }
   // fixed tree over the groups: g += g + 4, g += g + 2, g += g + 1
@@ -481,10 +514,7 @@ __global__ __launch_bounds__(256) void k_assemble_sb(const DevProblem* __restric
     for (int c = cb; c < ce; ++c) {
       const Contrib C = P.pair_contrib[c];
       if (C.type == C_IMU) {
-        const double* L = imuLin(P, lb, C.a) + 15;
-        double s2 = 0;
-        for (int k2 = 0; k2 < 15; ++k2) s2 += L[k2 * 30 + C.b + r] * L[k2 * 30 + C.c + q];
-        H += s2;
+        H += P.imu_H[(size_t)C.a * kImuHess + sym30(C.b + r, C.c + q)];
       } else if (C.type == C_SBPRIOR) {
         const double* L = P.sbp_lin[lb] + 90 * (size_t)C.a + 9;
         double s2 = 0;
@@ -597,8 +627,12 @@ void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
 void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s) {
   if (P.n_fblock > 0) hipLaunchKernelGGL(k_fgrad, dim3(P.n_fblock), dim3(64), 0, s, P.self, lin_mode);
 }
+void launch_imu_hess(const DevProblem& P, int lin_mode, hipStream_t s) {
+  if (P.n_imu > 0) hipLaunchKernelGGL(k_imu_hess, dim3((P.n_imu + 3) / 4), dim3(256), 0, s, P.self, lin_mode);
+}
 void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
   launch_lm_blocks(P, lin_mode, s);
+  launch_imu_hess(P, lin_mode, s);
   launch_fgrad(P, lin_mode, s);
 }
 void launch_lm_prep(const DevProblem& P, hipStream_t s) {

@@ -632,7 +632,8 @@ struct okvisgpu_ctx {
     const size_t o_imu_lin0 = scratch(sizeof(double) * kImuLin * D.n_imu),
                  o_imu_lin1 = scratch(sizeof(double) * kImuLin * D.n_imu);
     const size_t o_imu_cost0 = scratch(sizeof(double) * D.n_imu), o_imu_cost1 = scratch(sizeof(double) * D.n_imu),
-                 o_imu_jv = scratch(sizeof(double) * 2 * D.n_imu);
+                 o_imu_jv = scratch(sizeof(double) * 2 * D.n_imu),
+                 o_imu_H = scratch(sizeof(double) * kImuHess * D.n_imu);
     const size_t o_pp_block = upl(B.pp_block), o_pp_win = upl(B.pp_win), o_pp_meas = upl(B.pp_meas),
                  o_pp_L = upl(B.pp_L);
     const size_t o_pp_lin0 = scratch(sizeof(double) * 42 * D.n_pprior), o_pp_lin1 = scratch(sizeof(double) * 42 * D.n_pprior),
@@ -693,6 +694,7 @@ struct okvisgpu_ctx {
     D.imu_ga = dp(o_imu_ga); D.imu_par = dp(o_imu_par); D.imu_state = dp(o_imu_state);
     D.imu_lin[0] = dp(o_imu_lin0); D.imu_lin[1] = dp(o_imu_lin1);
     D.imu_cost[0] = dp(o_imu_cost0); D.imu_cost[1] = dp(o_imu_cost1); D.imu_jv = dp(o_imu_jv);
+    D.imu_H = dp(o_imu_H);
     D.pp_block = ip(o_pp_block); D.pp_win = ip(o_pp_win); D.pp_meas = dp(o_pp_meas); D.pp_L = dp(o_pp_L);
     D.pp_lin[0] = dp(o_pp_lin0); D.pp_lin[1] = dp(o_pp_lin1); D.pp_cost[0] = dp(o_pp_cost0);
     D.pp_cost[1] = dp(o_pp_cost1); D.pp_jv = dp(o_pp_jv);
