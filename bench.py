@@ -145,6 +145,7 @@ def main():
     ap.add_argument("--cpu-reps", type=int, default=3, help="median of this many timed passes after 1 warm-up")
     ap.add_argument("--cpu-windows", type=int, default=8, help="windows in the CPU baseline sample")
     ap.add_argument("--kernel-reps", type=int, default=5, help="repetitions per kernel in the roofline table")
+    ap.add_argument("--cholesky-schedule", type=int, default=0, help="0 auto, 1 persistent per window, 2 tile-parallel")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
@@ -169,6 +170,7 @@ def main():
     ctx.set_problems([w.problem for w in windows])
     total_iters = args.warmup + args.steps
     opts = bench_options(total_iters)
+    opts.cholesky_schedule = args.cholesky_schedule
 
     ctx.solve_begin(opts)
     ctx.solve_iterate(args.warmup)

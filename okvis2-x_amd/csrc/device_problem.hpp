@@ -188,6 +188,15 @@ struct DevProblem {
   // window is block-banded and LLT creates no fill outside its envelope, so only structurally
   // non-zero 64x64 tiles are zeroed, factored and updated (bitwise identical to the dense LLT).
   const int32_t* tile_items;         // (w, i, j) every structurally non-zero tile (i >= j)
+  // tile-parallel schedule (few windows): per step k, the panel tiles (w, i) and the band updates
+  // (w, i, j) of all windows; begin offsets per k, host copies for the launch sizes
+  const int32_t* chol_panel_items;
+  const int32_t* chol_panel_begin;
+  const int32_t* chol_upd_items;
+  const int32_t* chol_upd_begin;
+  const int32_t* h_panel_begin;
+  const int32_t* h_upd_begin;
+  int32_t chol_schedule;             // 1 persistent per window, 2 tile-parallel (host-resolved)
   const uint8_t* tile_nz;            // per window T x T (row-major) structural non-zero flags of L
   const int64_t* win_tnzoff;         // [n_win] offset of the window's flags in tile_nz
   int32_t n_tiles;

@@ -1,5 +1,8 @@
 // kernels_chol.hip — dense LLT of the reduced camera matrix S (Eigen::LLT semantics: fail at the
-// first non-positive pivot) and the two triangular solves, one persistent workgroup per window.
+// first non-positive pivot) and the two triangular solves. Two schedules of the same tile
+// routines: one persistent workgroup per window (large batches: fills the chip with whole
+// windows) or per-step launches over all windows' panel / band-update tiles (few windows:
+// spreads each window over many CUs); launch_cholesky picks the host-resolved one.
 //
 // k_cholesky: right-looking blocked Cholesky over 64x64 FP64 tiles, only structurally non-zero
 // tiles (the host's tile-level symbolic factorisation, DevProblem::tile_nz: the reduced camera
@@ -95,6 +98,16 @@ __device__ __forceinline__ double readlaneD(double v, int lane) {  // v of `lane
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// 1/sqrt(d) to ~1 ulp: v_rsq_f64 (~5e-8 relative) refined by two Newton steps (measured on
+// gfx950: 2.3e-16 max relative error over d in [e^-40, e^40]).
+__device__ __forceinline__ double rsqrtRefined(double d) {
+  double r = __builtin_amdgcn_rsq(d);
+  const double h = 0.5 * d;
+  r = r * (1.5 - h * r * r);
+  r = r * (1.5 - h * r * r);
+  return r;
+}
+
 // 16x16 block product on one wavefront: acc += sign * A(16 x 16K) B(16K x 16) with
 // A[m][k] = a[m * lda + k], B[k][n] = b[k * ldbk + n * ldbn] (LDS), result in the MFMA C layout.
 template <int KB>
@@ -128,8 +141,11 @@ __device__ __forceinline__ void storeC16(double* c, int ldc, const dbl4& v, int 
 // then X blockwise: the 4 diagonal 16x16 inverses in parallel (one per wavefront), and
 // X_ij = -X_ii (sum_{m=j}^{i-1} L_im X_mj) by sub-diagonal on the matrix cores.
 // Returns false (uniformly) at a non-positive pivot.
+// (one non-inlined instantiation per calling kernel: a shared callee gets a generic register
+// budget that halves the persistent kernel's occupancy)
+template <int kCaller>
 __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX, double* sy,
-                          int* sFail, int t) {
+                                      double* sRl, int* sFail, int t) {
   const int wave = t >> 6, lane = t & 63;
   loadTile(Sg, ld, 0, 0, sA, t);
 #pragma unroll
@@ -151,7 +167,8 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
         const int col = 16 * p + c;
         const double dcc = readlaneD(a[c], col);
         if (!(dcc > 0.0)) bad = true;  // wave-uniform
-        const double rl = 1.0 / sqrt(dcc);
+        const double rl = rsqrtRefined(dcc);
+        if (lane == 0) sRl[col] = rl;  // 1 / L_cc for the inverse
         const double l = (i == col) ? dcc * rl : a[c] * rl;
         a[c] = l;
 #pragma unroll
@@ -184,7 +201,7 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
       double v = (i == j) ? 1.0 : 0.0;
 #pragma unroll
       for (int m = 0; m < i; ++m) v -= sA[(16 * q + i) * kLd + 16 * q + m] * x[m];
-      x[i] = (i >= j) ? v / sA[(16 * q + i) * kLd + 16 * q + i] : 0.0;
+      x[i] = (i >= j) ? v * sRl[16 * q + i] : 0.0;
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) sX[(16 * q + i) * kLd + 16 * q + j] = x[i];
@@ -212,11 +229,17 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
     *reinterpret_cast<double2*>(Li + r * kTile + c) =
         double2{(c <= r) ? sX[r * kLd + c] : 0.0, (c + 1 <= r) ? sX[r * kLd + c + 1] : 0.0};
   }
-  double y = 0.0;
-  if (t < kTile)
-    for (int j = 0; j <= t; ++j) y += sX[t * kLd + j] * sy[j];
+  __syncthreads();
+  {  // y_k = X rhs_k: row t & 63, quarter t >> 6 of the columns, partials through LDS
+    const int row = t & 63, qq = t >> 6;
+    double y = 0.0;
+#pragma unroll
+    for (int j = 16 * qq; j < 16 * qq + 16; ++j) y += (j <= row) ? sX[row * kLd + j] * sy[j] : 0.0;
+    sA[qq * kTile + row] = y;  // sA is free once L_kk has been stored
+  }
   __syncthreads();
   if (t < kTile) {
+    const double y = (sA[t] + sA[kTile + t]) + (sA[2 * kTile + t] + sA[3 * kTile + t]);
     sy[t] = y;
     workk[t] = y;
   }
@@ -224,67 +247,28 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__ Pp) {
-  const DevProblem& P = *Pp;
-  const int w = blockIdx.x;
-  if (!cholSelect(P, w)) return;
-  const int64_t ld = P.win_fpad[w];
-  const int T = (int)(ld / kTile);
-  double* S = P.S + P.win_soff[w];
-  double* work = P.fwdF + P.win_fwdoff[w];
-  double* Linv = P.Linv + P.win_linvoff[w];
-  const uint8_t* nz = P.tile_nz + P.win_tnzoff[w];
-  __shared__ double sA[kTile * kLd];
-  __shared__ double sX[kTile * kLd];
-  __shared__ double sy[kTile];
-  __shared__ int sFail;
-  const int t = threadIdx.x;
-  const int fdim = P.win_fdim[w];
-  for (int e = t; e < ld; e += 256) work[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
+// L_ik = A_ik X^T (X = L_kk^-1 in sX, y_k in sy) stored over A_ik, and rhs_i -= L_ik y_k.
+__device__ void panelTile(double* Aik, int64_t ld, double* worki, double* sA, const double* sX, const double* sy,
+                          int t) {
+  loadTile(Aik, ld, 0, 0, sA, t);
   __syncthreads();
-  for (int k = 0; k < T; ++k) {
-    if (t < kTile) sy[t] = work[k * kTile + t];
-    __syncthreads();
-    if (!potrfTile(S + k * kTile * ld + k * kTile, ld, Linv + (int64_t)k * kTile * kTile, work + k * kTile, sA, sX,
-                   sy, &sFail, t)) {
-      if (t == 0) P.st[w].gn_failed = 1;
-      return;
-    }
-    // ---- panel: L_ik = A_ik X^T, rhs_i -= L_ik y_k
-    for (int i = k + 1; i < T; ++i) {
-      if (!nz[i * T + k]) continue;
-      double* Aik = S + i * kTile * ld + k * kTile;
-      loadTile(Aik, ld, 0, 0, sA, t);
-      __syncthreads();
-      dbl4 acc[2][2];
-      mfmaTileNT(sA, sX, acc, t);
-      __syncthreads();
-      storeTile<false>(Aik, ld, 0, 0, acc, t);
-      storeTile<false>(sA, kLd, 0, 0, acc, t);  // L_ik staged for the rhs update
-      __syncthreads();
-      if (t < kTile) {
-        double a = 0.0;
-        for (int c = 0; c < kTile; ++c) a += sA[t * kLd + c] * sy[c];
-        work[i * kTile + t] -= a;
-      }
-      __syncthreads();
-    }
-    // ---- trailing band update: A_ij -= L_ik L_jk^T, k < j <= i, both tiles non-zero
-    for (int i = k + 1; i < T; ++i) {
-      if (!nz[i * T + k]) continue;
-      loadTile(S + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
-      for (int j = k + 1; j <= i; ++j) {
-        if (!nz[j * T + k]) continue;
-        if (j != i) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sX, t);
-        __syncthreads();
-        dbl4 acc[2][2];
-        mfmaTileNT(sA, j == i ? sA : sX, acc, t);
-        storeTile<true>(S + i * kTile * ld + j * kTile, ld, 0, 0, acc, t);
-        __syncthreads();
-      }
-    }
+  dbl4 acc[2][2];
+  mfmaTileNT(sA, sX, acc, t);
+  __syncthreads();
+  storeTile<false>(Aik, ld, 0, 0, acc, t);
+  storeTile<false>(sA, kLd, 0, 0, acc, t);  // L_ik staged for the rhs update
+  __syncthreads();
+  if (t < kTile) {
+    double a = 0.0;
+    for (int c = 0; c < kTile; ++c) a += sA[t * kLd + c] * sy[c];
+    worki[t] -= a;
   }
-  // ---- backward substitution x = L^-T y (work holds y; x overwrites it from the back)
+  __syncthreads();
+}
+
+// Backward substitution x = L^-T y (work holds y; x overwrites it from the back), then y_F := x.
+__device__ void backSubstitute(const DevProblem& P, int w, const double* S, int64_t ld, int T, double* work,
+                               const double* Linv, const uint8_t* nz, double* sA, double* sX, double* sy, int t) {
   for (int I = T - 1; I >= 0; --I) {
     const int col = t & 63, q = t >> 6;
     double acc = 0.0;
@@ -309,11 +293,148 @@ __global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__
     if (t < kTile) work[I * kTile + t] = sA[t] + sA[kTile + t] + sA[2 * kTile + t] + sA[3 * kTile + t];
     __syncthreads();
   }
+  const int fdim = P.win_fdim[w];
   for (int e = t; e < fdim; e += 256) P.yF[(size_t)P.win_foff[w] + e] = work[e];
 }
 
+__global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
+  const int w = blockIdx.x;
+  if (!cholSelect(P, w)) return;
+  const int64_t ld = P.win_fpad[w];
+  const int T = (int)(ld / kTile);
+  double* S = P.S + P.win_soff[w];
+  double* work = P.fwdF + P.win_fwdoff[w];
+  double* Linv = P.Linv + P.win_linvoff[w];
+  const uint8_t* nz = P.tile_nz + P.win_tnzoff[w];
+  __shared__ double sA[kTile * kLd];
+  __shared__ double sX[kTile * kLd];
+  __shared__ double sy[2 * kTile];  // y_k | panel column scratch
+  __shared__ double sRl[kTile];
+  __shared__ int sFail;
+  const int t = threadIdx.x;
+  const int fdim = P.win_fdim[w];
+  for (int e = t; e < ld; e += 256) work[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
+  __syncthreads();
+  for (int k = 0; k < T; ++k) {
+    if (t < kTile) sy[t] = work[k * kTile + t];
+    __syncthreads();
+    if (!potrfTile<0>(S + k * kTile * ld + k * kTile, ld, Linv + (int64_t)k * kTile * kTile, work + k * kTile, sA, sX,
+                   sy, sRl, &sFail, t)) {
+      if (t == 0) P.st[w].gn_failed = 1;
+      return;
+    }
+    // ---- panel: L_ik = A_ik X^T, rhs_i -= L_ik y_k
+    for (int i = k + 1; i < T; ++i)
+      if (nz[i * T + k]) panelTile(S + i * kTile * ld + k * kTile, ld, work + i * kTile, sA, sX, sy, t);
+    // ---- trailing band update: A_ij -= L_ik L_jk^T, k < j <= i, both tiles non-zero
+    for (int i = k + 1; i < T; ++i) {
+      if (!nz[i * T + k]) continue;
+      loadTile(S + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
+      for (int j = k + 1; j <= i; ++j) {
+        if (!nz[j * T + k]) continue;
+        if (j != i) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sX, t);
+        __syncthreads();
+        dbl4 acc[2][2];
+        mfmaTileNT(sA, j == i ? sA : sX, acc, t);
+        storeTile<true>(S + i * kTile * ld + j * kTile, ld, 0, 0, acc, t);
+        __syncthreads();
+      }
+    }
+  }
+  backSubstitute(P, w, S, ld, T, work, Linv, nz, sA, sX, sy, t);
+}
+
+// ---- tile-parallel schedule: per step k one launch each for the diagonal tiles, the panel tiles
+// and the band updates of all windows (many workgroups per window), then the backward solves.
+__global__ __launch_bounds__(256) void k_chol_diag(const DevProblem* __restrict__ Pp, int k) {
+  const DevProblem& P = *Pp;
+  const int w = blockIdx.x;
+  if (!cholSelect(P, w)) return;
+  const int64_t ld = P.win_fpad[w];
+  const int T = (int)(ld / kTile);
+  if (k >= T) return;
+  double* S = P.S + P.win_soff[w];
+  double* work = P.fwdF + P.win_fwdoff[w];
+  __shared__ double sA[kTile * kLd];
+  __shared__ double sX[kTile * kLd];
+  __shared__ double sy[2 * kTile];
+  __shared__ double sRl[kTile];
+  __shared__ int sFail;
+  const int t = threadIdx.x;
+  if (k == 0) {
+    const int fdim = P.win_fdim[w];
+    for (int e = t; e < ld; e += 256) work[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
+    __syncthreads();
+  }
+  if (t < kTile) sy[t] = work[k * kTile + t];
+  __syncthreads();
+  if (!potrfTile<1>(S + k * kTile * ld + k * kTile, ld, P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile,
+                 work + k * kTile, sA, sX, sy, sRl, &sFail, t))
+    if (t == 0) P.st[w].gn_failed = 1;
+}
+
+__global__ __launch_bounds__(256) void k_chol_panel(const DevProblem* __restrict__ Pp, int k) {
+  const DevProblem& P = *Pp;
+  const int item = P.chol_panel_begin[k] + blockIdx.x;
+  const int w = P.chol_panel_items[2 * item], i = P.chol_panel_items[2 * item + 1];
+  if (!cholSelect(P, w)) return;
+  const int64_t ld = P.win_fpad[w];
+  double* work = P.fwdF + P.win_fwdoff[w];
+  __shared__ double sA[kTile * kLd];
+  __shared__ double sX[kTile * kLd];
+  __shared__ double sy[kTile];
+  const int t = threadIdx.x;
+  const double* X = P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile;
+  loadTile(X, kTile, 0, 0, sX, t);
+  if (t < kTile) sy[t] = work[k * kTile + t];
+  panelTile(P.S + P.win_soff[w] + i * kTile * ld + k * kTile, ld, work + i * kTile, sA, sX, sy, t);
+}
+
+__global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restrict__ Pp, int k) {
+  const DevProblem& P = *Pp;
+  const int item = P.chol_upd_begin[k] + blockIdx.x;
+  const int w = P.chol_upd_items[3 * item], i = P.chol_upd_items[3 * item + 1], j = P.chol_upd_items[3 * item + 2];
+  if (!cholSelect(P, w)) return;
+  const int64_t ld = P.win_fpad[w];
+  double* S = P.S + P.win_soff[w];
+  __shared__ double sA[kTile * kLd];
+  __shared__ double sX[kTile * kLd];
+  const int t = threadIdx.x;
+  loadTile(S + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
+  if (j != i) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sX, t);
+  __syncthreads();
+  dbl4 acc[2][2];
+  mfmaTileNT(sA, j == i ? sA : sX, acc, t);
+  storeTile<true>(S + i * kTile * ld + j * kTile, ld, 0, 0, acc, t);
+}
+
+__global__ __launch_bounds__(256) void k_chol_bsub(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
+  const int w = blockIdx.x;
+  if (!cholSelect(P, w)) return;
+  const int64_t ld = P.win_fpad[w];
+  __shared__ double sA[4 * kTile];
+  __shared__ double sX[4 * kTile];
+  __shared__ double sy[kTile];
+  backSubstitute(P, w, P.S + P.win_soff[w], ld, (int)(ld / kTile), P.fwdF + P.win_fwdoff[w],
+                 P.Linv + P.win_linvoff[w], P.tile_nz + P.win_tnzoff[w], sA, sX, sy, threadIdx.x);
+}
+
 void launch_cholesky(const DevProblem& P, hipStream_t s) {
-  if (P.n_win > 0) hipLaunchKernelGGL(k_cholesky, dim3(P.n_win), dim3(256), 0, s, P.self);
+  if (P.n_win == 0) return;
+  if (P.chol_schedule == 1) {
+    hipLaunchKernelGGL(k_cholesky, dim3(P.n_win), dim3(256), 0, s, P.self);
+    return;
+  }
+  for (int k = 0; k < P.max_tiles; ++k) {
+    hipLaunchKernelGGL(k_chol_diag, dim3(P.n_win), dim3(256), 0, s, P.self, k);
+    const int np = P.h_panel_begin[k + 1] - P.h_panel_begin[k];
+    if (np > 0) hipLaunchKernelGGL(k_chol_panel, dim3(np), dim3(256), 0, s, P.self, k);
+    const int nu = P.h_upd_begin[k + 1] - P.h_upd_begin[k];
+    if (nu > 0) hipLaunchKernelGGL(k_chol_update, dim3(nu), dim3(256), 0, s, P.self, k);
+  }
+  hipLaunchKernelGGL(k_chol_bsub, dim3(P.n_win), dim3(256), 0, s, P.self);
 }
 
 }  // namespace okg

@@ -532,6 +532,8 @@ struct okvisgpu_ctx {
   void* arena = nullptr;
   size_t arenaBytes = 0;
   hipGraphExec_t iterGraph = nullptr;
+  int cuCount = 256;
+  static constexpr int kPersistentWindowsPerCU = 1;
   bool haveProblem = false;
   // split-solve state
   bool inSolve = false;
@@ -657,6 +659,8 @@ struct okvisgpu_ctx {
     const size_t o_tnz = upl(B.tile_nz), o_tnzoff = upl(B.win_tnzoff);
     const size_t o_app = upl(B.asm_pp_items), o_asb = upl(B.asm_sb_items);
     const size_t o_ti = upl(B.tile_items);
+    const size_t o_cpi = upl(B.chol_panel_items), o_cpb = upl(B.chol_panel_begin), o_cui = upl(B.chol_upd_items),
+                 o_cub = upl(B.chol_upd_begin);
     const size_t nf = std::max(1, B.f_total), nl3 = std::max<size_t>(1, (size_t)3 * D.n_lm);
     const size_t o_S = scratch(sizeof(double) * std::max<int64_t>(1, B.s_total));
     const size_t o_Linv = scratch(sizeof(double) * std::max<int64_t>(1, B.linv_total));
@@ -712,6 +716,11 @@ struct okvisgpu_ctx {
     D.pair_runs = ip(o_pruns);
     D.tile_nz = reinterpret_cast<const uint8_t*>(base + o_tnz);
     D.win_tnzoff = reinterpret_cast<const int64_t*>(base + o_tnzoff);
+    D.chol_panel_items = ip(o_cpi); D.chol_panel_begin = ip(o_cpb);
+    D.chol_upd_items = ip(o_cui); D.chol_upd_begin = ip(o_cub);
+    D.h_panel_begin = B.chol_panel_begin.data();
+    D.h_upd_begin = B.chol_upd_begin.data();
+    D.chol_schedule = 1;
     D.asm_pp_items = ip(o_app); D.asm_sb_items = ip(o_asb);
     D.n_asm_pp = (int)B.asm_pp_items.size(); D.n_asm_sb = (int)B.asm_sb_items.size();
     D.tile_items = ip(o_ti);
@@ -756,6 +765,16 @@ struct okvisgpu_ctx {
     d.min_relative_decrease = o.min_relative_decrease;
     d.min_lm_diagonal = o.min_lm_diagonal;
     d.max_lm_diagonal = o.max_lm_diagonal;
+    // Cholesky schedule: one persistent workgroup per window needs about one window per CU to fill
+    // the chip; below that the tile-parallel launches spread each window over many CUs
+    const int sched = o.cholesky_schedule == 1 || o.cholesky_schedule == 2
+                          ? o.cholesky_schedule
+                          : (P.n_win >= kPersistentWindowsPerCU * cuCount ? 1 : 2);
+    if (sched != P.chol_schedule && iterGraph) {
+      (void)hipGraphExecDestroy(iterGraph);
+      iterGraph = nullptr;
+    }
+    P.chol_schedule = sched;
     uploadDescriptor();
   }
 
@@ -911,6 +930,7 @@ void okvisgpu_default_options(okvisgpu_options* o) {
   o->redo_propagation_always = 0;
   o->num_threads = 1;
   o->verbose = 0;
+  o->cholesky_schedule = 0;
 }
 
 int okvisgpu_device_count(int32_t* count) {
@@ -936,6 +956,7 @@ int okvisgpu_ctx_create(int32_t device, okvisgpu_ctx** out) {
     if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
       throw HipError{std::string("okvisgpu is built for gfx950 only; device is ") + prop.gcnArchName,
                      OKVISGPU_ERR_DEVICE};
+    c->cuCount = prop.multiProcessorCount;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     return (int)OKVISGPU_OK;
   });

@@ -70,6 +70,7 @@ class Options(C.Structure):
         ("max_lm_diagonal", C.c_double), ("max_num_consecutive_invalid_steps", C.c_int32),
         ("time_limit_s", C.c_double), ("min_iterations", C.c_int32),
         ("redo_propagation_always", C.c_int32), ("num_threads", C.c_int32), ("verbose", C.c_int32),
+        ("cholesky_schedule", C.c_int32),
     ]
 
 
