@@ -266,35 +266,44 @@ __device__ void panelTile(double* Aik, int64_t ld, double* worki, double* sA, co
   __syncthreads();
 }
 
-// Backward substitution x = L^-T y (work holds y; x overwrites it from the back), then y_F := x.
-__device__ void backSubstitute(const DevProblem& P, int w, const double* S, int64_t ld, int T, double* work,
-                               const double* Linv, const uint8_t* nz, double* sA, double* sX, double* sy, int t) {
+// Backward substitution x = L^-T y (work holds y), x := y_F. x lives in LDS (sx, ld doubles);
+// per block row I the 16 row loads of every non-zero tile below are issued together, then
+// x_I = X_II^T (y_I - sum_i L_iI^T x_i) with the stored diagonal inverse.
+__device__ void backSubstitute(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* work,
+                               const double* Linv, const uint8_t* nz, double* sx, double* sA, double* sy, int t) {
+  for (int e = t; e < ld; e += 256) sx[e] = work[e];
+  __syncthreads();
+  const int col = t & 63, q = t >> 6;
   for (int I = T - 1; I >= 0; --I) {
-    const int col = t & 63, q = t >> 6;
     double acc = 0.0;
     for (int i = I + 1; i < T; ++i) {
       if (!nz[i * T + I]) continue;
-      const double* Lt = S + i * kTile * ld + I * kTile;
-#pragma unroll 4
-      for (int r = q; r < kTile; r += 4) acc += Lt[(int64_t)r * ld + col] * work[i * kTile + r];
+      const double* Lt = S + i * kTile * ld + I * kTile + col;
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = Lt[(int64_t)(q + 4 * u) * ld];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += v[u] * sx[i * kTile + q + 4 * u];
     }
-    sX[q * kTile + col] = acc;
+    const double* Li = Linv + (int64_t)I * kTile * kTile + col;
+    double li[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) li[u] = Li[(q + 4 * u) * kTile];
+    sA[q * kTile + col] = acc;
     __syncthreads();
-    if (t < kTile) sy[t] = work[I * kTile + t] - (sX[t] + sX[kTile + t] + sX[2 * kTile + t] + sX[3 * kTile + t]);
+    if (t < kTile) sy[t] = sx[I * kTile + t] - ((sA[t] + sA[kTile + t]) + (sA[2 * kTile + t] + sA[3 * kTile + t]));
     __syncthreads();
-    {
-      const double* Li = Linv + (int64_t)I * kTile * kTile;
-      double a = 0.0;
-#pragma unroll 4
-      for (int r = q; r < kTile; r += 4) a += (r >= col) ? Li[r * kTile + col] * sy[r] : 0.0;
-      sA[q * kTile + col] = a;
-    }
+    double a = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) a += (q + 4 * u >= col) ? li[u] * sy[q + 4 * u] : 0.0;
+    sA[256 + q * kTile + col] = a;
     __syncthreads();
-    if (t < kTile) work[I * kTile + t] = sA[t] + sA[kTile + t] + sA[2 * kTile + t] + sA[3 * kTile + t];
+    if (t < kTile)
+      sx[I * kTile + t] = (sA[256 + t] + sA[256 + kTile + t]) + (sA[256 + 2 * kTile + t] + sA[256 + 3 * kTile + t]);
     __syncthreads();
   }
   const int fdim = P.win_fdim[w];
-  for (int e = t; e < fdim; e += 256) P.yF[(size_t)P.win_foff[w] + e] = work[e];
+  for (int e = t; e < fdim; e += 256) P.yF[(size_t)P.win_foff[w] + e] = sx[e];
 }
 
 __global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__ Pp) {
@@ -342,7 +351,8 @@ __global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__
       }
     }
   }
-  backSubstitute(P, w, S, ld, T, work, Linv, nz, sA, sX, sy, t);
+  extern __shared__ double sxDyn[];
+  backSubstitute(P, w, S, ld, T, work, Linv, nz, sxDyn, sA, sy, t);
 }
 
 // ---- tile-parallel schedule: per step k one launch each for the diagonal tiles, the panel tiles
@@ -414,17 +424,17 @@ __global__ __launch_bounds__(256) void k_chol_bsub(const DevProblem* __restrict_
   const int w = blockIdx.x;
   if (!cholSelect(P, w)) return;
   const int64_t ld = P.win_fpad[w];
-  __shared__ double sA[4 * kTile];
-  __shared__ double sX[4 * kTile];
+  __shared__ double sA[8 * kTile];
   __shared__ double sy[kTile];
+  extern __shared__ double sxDyn[];
   backSubstitute(P, w, P.S + P.win_soff[w], ld, (int)(ld / kTile), P.fwdF + P.win_fwdoff[w],
-                 P.Linv + P.win_linvoff[w], P.tile_nz + P.win_tnzoff[w], sA, sX, sy, threadIdx.x);
+                 P.Linv + P.win_linvoff[w], P.tile_nz + P.win_tnzoff[w], sxDyn, sA, sy, threadIdx.x);
 }
 
 void launch_cholesky(const DevProblem& P, hipStream_t s) {
   if (P.n_win == 0) return;
   if (P.chol_schedule == 1) {
-    hipLaunchKernelGGL(k_cholesky, dim3(P.n_win), dim3(256), 0, s, P.self);
+    hipLaunchKernelGGL(k_cholesky, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
     return;
   }
   for (int k = 0; k < P.max_tiles; ++k) {
@@ -434,7 +444,7 @@ void launch_cholesky(const DevProblem& P, hipStream_t s) {
     const int nu = P.h_upd_begin[k + 1] - P.h_upd_begin[k];
     if (nu > 0) hipLaunchKernelGGL(k_chol_update, dim3(nu), dim3(256), 0, s, P.self, k);
   }
-  hipLaunchKernelGGL(k_chol_bsub, dim3(P.n_win), dim3(256), 0, s, P.self);
+  hipLaunchKernelGGL(k_chol_bsub, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
 }
 
 }  // namespace okg
