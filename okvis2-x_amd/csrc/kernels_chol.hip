@@ -401,22 +401,39 @@ __global__ __launch_bounds__(256) void k_chol_panel(const DevProblem* __restrict
   panelTile(P.S + P.win_soff[w] + i * kTile * ld + k * kTile, ld, work + i * kTile, sA, sX, sy, t);
 }
 
+// band updates of step k; the workgroup owning tile (k+1,k+1) factors it right after its update
+// (mode bit 1), so the next diagonal overlaps the remaining updates of this step
 __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restrict__ Pp, int k) {
   const DevProblem& P = *Pp;
   const int item = P.chol_upd_begin[k] + blockIdx.x;
-  const int w = P.chol_upd_items[3 * item], i = P.chol_upd_items[3 * item + 1], j = P.chol_upd_items[3 * item + 2];
+  const int4 it = reinterpret_cast<const int4*>(P.chol_upd_items)[item];
+  const int w = it.x, i = it.y, j = it.z, mode = it.w;
   if (!cholSelect(P, w)) return;
   const int64_t ld = P.win_fpad[w];
   double* S = P.S + P.win_soff[w];
   __shared__ double sA[kTile * kLd];
   __shared__ double sX[kTile * kLd];
+  __shared__ double sy[2 * kTile];
+  __shared__ double sRl[kTile];
+  __shared__ int sFail;
   const int t = threadIdx.x;
-  loadTile(S + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
-  if (j != i) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sX, t);
+  if (mode & 1) {
+    loadTile(S + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
+    if (j != i) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sX, t);
+    __syncthreads();
+    dbl4 acc[2][2];
+    mfmaTileNT(sA, j == i ? sA : sX, acc, t);
+    storeTile<true>(S + i * kTile * ld + j * kTile, ld, 0, 0, acc, t);
+  }
+  if (!(mode & 2)) return;
+  double* work = P.fwdF + P.win_fwdoff[w];
+  const int d = k + 1;
   __syncthreads();
-  dbl4 acc[2][2];
-  mfmaTileNT(sA, j == i ? sA : sX, acc, t);
-  storeTile<true>(S + i * kTile * ld + j * kTile, ld, 0, 0, acc, t);
+  if (t < kTile) sy[t] = work[d * kTile + t];
+  __syncthreads();
+  if (!potrfTile<2>(S + d * kTile * ld + d * kTile, ld, P.Linv + P.win_linvoff[w] + (int64_t)d * kTile * kTile,
+                    work + d * kTile, sA, sX, sy, sRl, &sFail, t))
+    if (t == 0) P.st[w].gn_failed = 1;
 }
 
 __global__ __launch_bounds__(256) void k_chol_bsub(const DevProblem* __restrict__ Pp) {
@@ -437,8 +454,8 @@ void launch_cholesky(const DevProblem& P, hipStream_t s) {
     hipLaunchKernelGGL(k_cholesky, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
     return;
   }
+  hipLaunchKernelGGL(k_chol_diag, dim3(P.n_win), dim3(256), 0, s, P.self, 0);
   for (int k = 0; k < P.max_tiles; ++k) {
-    hipLaunchKernelGGL(k_chol_diag, dim3(P.n_win), dim3(256), 0, s, P.self, k);
     const int np = P.h_panel_begin[k + 1] - P.h_panel_begin[k];
     if (np > 0) hipLaunchKernelGGL(k_chol_panel, dim3(np), dim3(256), 0, s, P.self, k);
     const int nu = P.h_upd_begin[k + 1] - P.h_upd_begin[k];

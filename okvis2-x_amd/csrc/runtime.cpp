@@ -85,6 +85,7 @@ struct HostBatch {
   std::vector<int32_t> pair_win, pair_fi, pair_fj, pair_cbegin, pair_runs;
   std::vector<int32_t> asm_pp_items, asm_sb_items;
   std::vector<int32_t> chol_panel_items, chol_panel_begin, chol_upd_items, chol_upd_begin, tile_items;
+  int64_t n_band_updates = 0;
   std::vector<Contrib> pair_contrib;
   int64_t s_total = 0, linv_total = 0, fwd_total = 0;
   std::vector<std::vector<uint8_t>> tileNz;
@@ -447,18 +448,26 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
   const int maxT = B.max_fpad / kTile;
   for (int k = 0; k <= maxT; ++k) {
     B.chol_panel_begin.push_back((int)B.chol_panel_items.size() / 2);
-    B.chol_upd_begin.push_back((int)B.chol_upd_items.size() / 3);
+    B.chol_upd_begin.push_back((int)B.chol_upd_items.size() / 4);
     if (k == maxT) break;
     for (int w = 0; w < B.n_win; ++w) {
       const int T = B.tileT[w];
       const auto& nz = B.tileNz[w];
       for (int i = k + 1; i < T; ++i)
         if (nz[(size_t)i * T + k]) { B.chol_panel_items.push_back(w); B.chol_panel_items.push_back(i); }
+      // band updates of step k; the workgroup updating tile (k+1,k+1) then factors it (mode bit 1),
+      // or a factor-only item is added when step k does not touch that tile
+      auto push = [&](int i, int j, int mode) {
+        B.chol_upd_items.push_back(w); B.chol_upd_items.push_back(i);
+        B.chol_upd_items.push_back(j); B.chol_upd_items.push_back(mode);
+      };
+      if (k + 1 < T && !nz[(size_t)(k + 1) * T + k]) push(k + 1, k + 1, 2);
       for (int i = k + 1; i < T; ++i)
         if (nz[(size_t)i * T + k])
           for (int j = k + 1; j <= i; ++j)
             if (nz[(size_t)j * T + k]) {
-              B.chol_upd_items.push_back(w); B.chol_upd_items.push_back(i); B.chol_upd_items.push_back(j);
+              push(i, j, (i == k + 1 && j == k + 1) ? 3 : 1);
+              ++B.n_band_updates;
             }
     }
   }
@@ -1226,7 +1235,7 @@ double kernelWork(const HostBatch& B, const DevProblem& P, int k) {
     case K_CHOLESKY: {  // diagonal LLT + inverse + y_k, panels, band updates, backward solve
       double diag = 0;
       for (int w = 0; w < P.n_win; ++w) diag += B.tileT[w];
-      const double panels = (double)(B.chol_panel_items.size() / 2), upd = (double)(B.chol_upd_items.size() / 3);
+      const double panels = (double)(B.chol_panel_items.size() / 2), upd = (double)B.n_band_updates;
       return diag * (2.0 * tile3 / 3.0 + 4.0 * 64 * 64) + panels * (2.0 * tile3 + 4.0 * 64 * 64) + upd * 2.0 * tile3;
     }
     case K_VISIT_LIN: return nObs * (kObsLin * d8 + 1) + nVis * (kVisitLin * d8 + 7 * d8 + 16);
