@@ -224,7 +224,7 @@ int okvisgpu_synchronize(okvisgpu_ctx* ctx);
  * the context's stream, bracketed by HIP events; must follow okvisgpu_solve_begin (it advances the
  * solve by one iteration). phase_ms[OKVISGPU_N_PHASES] (ms, summed over the launches of that
  * kernel in the iteration); phase i is named by okvisgpu_phase_name(i). */
-#define OKVISGPU_N_PHASES 17
+#define OKVISGPU_N_PHASES 15
 int okvisgpu_profile_iteration(okvisgpu_ctx* ctx, double* phase_ms);
 const char* okvisgpu_phase_name(int32_t phase);
 

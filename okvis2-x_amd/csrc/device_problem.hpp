@@ -48,7 +48,7 @@ struct WinState {
   double x_norm, step_norm;
   double alpha, dogleg_step_norm, model_cost_change;
   double grad_max_norm, grad_norm;
-  double jv2, jvr;                 // reductions of the last J*v pass
+  double jcc, jgg, jcg;            // |J_s v_c|^2, |J_s v_g|^2, (J_s v_c).(J_s v_g) of the current GN / Cauchy pair
   int32_t xcur, lcur;              // current parameter set / linearisation buffer (0/1)
   int32_t need_gn;                 // !DoglegStrategy::reuse_
   int32_t done, termination;
@@ -105,7 +105,7 @@ struct DevProblem {
   const double* obs_L;             // [n_obs][4]
   double* obs_lin[2];              // [kObsLin][obs_stride]; lin[lcur] belongs to params X[xcur]
   double* obs_cost[2];             // [n_obs]
-  double* obs_jv;                  // [n_visit]: |J_s v|^2 of the visit's residuals
+  double* obs_jv;                  // [3][n_visit]: the visit's share of jcc | jgg | jcg
 
   // --- landmarks / visits
   const int32_t* lm_visit_begin;   // [n_lm+1] visits of landmark l
@@ -134,7 +134,7 @@ struct DevProblem {
   double* imu_lin[2];              // [n_imu][kImuLin]
   double* imu_cost[2];             // [n_imu]
   double* imu_H;                   // [n_imu][kImuHess] of the linearisation lin[lcur] (k_imu_hess)
-  double* imu_jv;                  // [n_imu] |J_s v|^2
+  double* imu_jv;                  // [3][n_imu]
 
   // --- priors
   const int32_t* pp_block;         // [n_pprior] global pose
@@ -143,7 +143,7 @@ struct DevProblem {
   const double* pp_L;              // [n][36]
   double* pp_lin[2];               // [n][6 + 36]
   double* pp_cost[2];
-  double* pp_jv;                   // [2][n]
+  double* pp_jv;                   // [3][n]
   const int32_t* sbp_block;
   const int32_t* sbp_win;
   const double* sbp_meas;          // [n][9]

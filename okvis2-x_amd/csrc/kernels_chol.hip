@@ -26,6 +26,22 @@ namespace okg {
 
 constexpr int kLd = kTile + 1;  // padded LDS row (65 doubles)
 
+// Development-only phase clock (make OPT="-O3 -DOKG_CHOL_CLOCK"): workgroup 0 of k_cholesky
+// accumulates s_memrealtime ticks (100 MHz) per phase and prints them.
+#ifdef OKG_CHOL_CLOCK
+__device__ unsigned long long g_cholClk[16];
+#define CLK_INIT unsigned long long clkLast = __builtin_amdgcn_s_memrealtime();
+#define CLK(i)                                                                  \
+  if (blockIdx.x == 0 && threadIdx.x == 0) {                                    \
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();            \
+    g_cholClk[i] += now - clkLast;                                              \
+    clkLast = now;                                                              \
+  }
+#else
+#define CLK_INIT
+#define CLK(i)
+#endif
+
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ bool cholSelect(const DevProblem& P, int w) {
@@ -147,6 +163,7 @@ template <int kCaller>
 __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX, double* sy,
                                       double* sRl, int* sFail, int t) {
   const int wave = t >> 6, lane = t & 63;
+  CLK_INIT
   loadTile(Sg, ld, 0, 0, sA, t);
 #pragma unroll
   for (int u = 0; u < 16; ++u) {
@@ -155,6 +172,7 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
   }
   if (t == 0) *sFail = 0;
   __syncthreads();
+  CLK(4)
   for (int p = 0; p < 4; ++p) {
     if (wave == 0) {
       const int i = lane;
@@ -180,6 +198,7 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
       if (bad && lane == 0) *sFail = 1;
     }
     __syncthreads();
+    CLK(5)
     if (*sFail) return false;
     int idx = 0;
     for (int rb = p + 1; rb < 4; ++rb)
@@ -192,6 +211,7 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
         storeC16(C, kLd, acc, lane);
       }
     __syncthreads();
+    CLK(6)
   }
   if (lane < 16) {  // diagonal 16x16 inverses, wavefront q, lane = column
     const int q = wave, j = lane;
@@ -207,6 +227,7 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
     for (int i = 0; i < 16; ++i) sX[(16 * q + i) * kLd + 16 * q + j] = x[i];
   }
   __syncthreads();
+  CLK(7)
   for (int d = 1; d < 4; ++d) {  // sub-diagonal d: X_ij, i = j + d, wavefront j
     const int j = wave, i = wave + d;
     if (i < 4) {
@@ -221,6 +242,7 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
     }
     __syncthreads();
   }
+  CLK(8)
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int e = t + 256 * u, r = e >> 5, c = 2 * (e & 31);
@@ -230,6 +252,7 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
         double2{(c <= r) ? sX[r * kLd + c] : 0.0, (c + 1 <= r) ? sX[r * kLd + c + 1] : 0.0};
   }
   __syncthreads();
+  CLK(9)
   {  // y_k = X rhs_k: row t & 63, quarter t >> 6 of the columns, partials through LDS
     const int row = t & 63, qq = t >> 6;
     double y = 0.0;
@@ -244,6 +267,7 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
     workk[t] = y;
   }
   __syncthreads();
+  CLK(10)
   return true;
 }
 
@@ -323,9 +347,11 @@ __global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__
   __shared__ int sFail;
   const int t = threadIdx.x;
   const int fdim = P.win_fdim[w];
+  CLK_INIT
   for (int e = t; e < ld; e += 256) work[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
   __syncthreads();
   for (int k = 0; k < T; ++k) {
+    CLK(11)
     if (t < kTile) sy[t] = work[k * kTile + t];
     __syncthreads();
     if (!potrfTile<0>(S + k * kTile * ld + k * kTile, ld, Linv + (int64_t)k * kTile * kTile, work + k * kTile, sA, sX,
@@ -333,9 +359,11 @@ __global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__
       if (t == 0) P.st[w].gn_failed = 1;
       return;
     }
+    CLK(0)
     // ---- panel: L_ik = A_ik X^T, rhs_i -= L_ik y_k
     for (int i = k + 1; i < T; ++i)
       if (nz[i * T + k]) panelTile(S + i * kTile * ld + k * kTile, ld, work + i * kTile, sA, sX, sy, t);
+    CLK(1)
     // ---- trailing band update: A_ij -= L_ik L_jk^T, k < j <= i, both tiles non-zero
     for (int i = k + 1; i < T; ++i) {
       if (!nz[i * T + k]) continue;
@@ -351,8 +379,16 @@ __global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__
       }
     }
   }
+  CLK(2)
   extern __shared__ double sxDyn[];
   backSubstitute(P, w, S, ld, T, work, Linv, nz, sxDyn, sA, sy, t);
+  CLK(3)
+#ifdef OKG_CHOL_CLOCK
+  if (blockIdx.x == 0 && t == 0)
+    printf("CHOLCLK T=%d potrf %llu panel %llu update %llu bsub %llu | load %llu pfac %llu ptrail %llu dinv %llu subd %llu store %llu y %llu (x10ns)\n",
+           T, g_cholClk[0], g_cholClk[1], g_cholClk[2] + g_cholClk[11], g_cholClk[3], g_cholClk[4], g_cholClk[5], g_cholClk[6],
+           g_cholClk[7], g_cholClk[8], g_cholClk[9], g_cholClk[10]);
+#endif
 }
 
 // ---- tile-parallel schedule: per step k one launch each for the diagonal tiles, the panel tiles

@@ -2,16 +2,17 @@
 //
 // Restates ceres::internal::TrustRegionMinimizer + DoglegStrategy (TRADITIONAL_DOGLEG) as used by
 // okvis (ViGraph.cpp:249, ViSlamBackend.cpp:877) [ext-Ceres, un-vendored; see DESIGN.md]:
-//   k_jv        per residual block: J*v with the Jacobi scaling applied on the fly; emits
-//               (Jv)^2 and (Jv).r for the Cauchy point (|J g|^2) and the model cost change.
+//   k_jv        per residual block, once per GN step: J_s v for the Cauchy and GN directions
+//               (Jacobi scaling applied on the fly) -> the three quadratic forms every dogleg
+//               step of that linearisation needs for its model cost change.
 //   k_reduce    one workgroup per window, fixed-order tree reductions (bitwise reproducible):
-//               costs, Cauchy alpha, model_cost_change (+ the step-validity bookkeeping), and the
+//               costs, the J*v forms and the Cauchy alpha, and the
 //               candidate acceptance test (parameter / function tolerance, relative decrease,
 //               radius and mu updates).
 //   k_gradnorm  |x - Plus(x, -g)|_inf / _2 and |x| after every accepted step.
 //   k_dogleg    one workgroup per window: LM-failure retries of the GN step, the traditional
-//               dogleg interpolation, delta = step .* jacobi_scaling and the manifold Plus into
-//               the candidate parameter set.
+//               dogleg interpolation, delta = step .* jacobi_scaling, the manifold Plus into
+//               the candidate parameter set, model_cost_change and the step-validity bookkeeping.
 #include <cfloat>
 
 #include "device_problem.hpp"
@@ -47,47 +48,63 @@ __device__ __forceinline__ double blockMax(double v, double* sh) {
   return r;
 }
 
-__device__ __forceinline__ bool jvSelect(const DevProblem& P, int w, int mode) {
+__device__ __forceinline__ bool jvSelect(const DevProblem& P, int w) {
   const WinState& s = P.st[w];
-  if (s.done) return false;
-  if (mode == R_JV_CAUCHY) return s.need_gn && !s.gn_failed;
-  return s.step_valid == 2;
+  return !s.done && s.need_gn && !s.gn_failed;
 }
 
-// |J_s v|^2 per residual block, J_s = J diag(s) (the Jacobi-scaled Jacobian the dogleg works in),
-// v = Cauchy direction or the step. Reprojections: one thread per (landmark, pose) visit (its 1-2
-// residuals share the pose/landmark vectors); IMU factors and priors: one thread each. The
-// companion (J_s v).r of the step is v.(s g) with the gradient g = J^T r already at hand, so it is
-// formed in k_reduce without touching J (DoglegStrategy / TrustRegionMinimizer model cost).
-__global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp, int mode) {
+// Accumulates one residual row's J_s v_c and J_s v_g into (jcc, jgg, jcg).
+__device__ __forceinline__ void jvAcc(double jc, double jg, double (&a)[3]) {
+  a[0] += jc * jc;
+  a[1] += jg * jg;
+  a[2] += jc * jg;
+}
+
+// Once per Gauss-Newton step, per residual block: J_s v_c and J_s v_g with J_s = J diag(s) (the
+// Jacobi-scaled Jacobian the dogleg works in), v_c = gradient_ / diagonal_ (Cauchy direction) and
+// v_g = gauss_newton_step_ / diagonal_ = -y. Every dogleg step of this linearisation is
+// step = ca v_c + cb v_g, so |J_s step|^2 = ca^2 jcc + 2 ca cb jcg + cb^2 jgg is formed in k_dogleg,
+// also for the steps re-tried at a smaller radius without a new GN step (DoglegStrategy reuse_).
+// The companion (J_s step).r = step.(s g) uses the gradient g = J^T r already at hand.
+// Reprojections: one thread per (landmark, pose) visit (its 1-2 residuals share the pose/landmark
+// vectors); IMU factors and priors: one thread each.
+__global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const double* vF = (mode == R_JV_CAUCHY) ? P.vF : P.stepF;
-  const double* vL = (mode == R_JV_CAUCHY) ? P.vL : P.stepL;
+  const double* __restrict__ cF = P.vF;
+  const double* __restrict__ yF = P.yF;
   if (t < P.n_visit) {
     const int v = t;
     const int l = P.visit_lm[v];
     const int w = P.lm_win[l];
-    if (!jvSelect(P, w, mode)) return;
+    if (!jvSelect(P, w)) return;
     const WinState& st = P.st[w];
     const int ps = P.visit_pose[v];
     const int pf = P.pose_f[ps];
-    double vp[6] = {0, 0, 0, 0, 0, 0}, vl[3] = {0, 0, 0};
+    double cp[6] = {0, 0, 0, 0, 0, 0}, gp[6] = {0, 0, 0, 0, 0, 0}, cl[3] = {0, 0, 0}, gl[3] = {0, 0, 0};
     if (pf >= 0) {
       const size_t base = (size_t)P.win_foff[w] + pf;
 #pragma unroll
-      for (int c = 0; c < 6; ++c) vp[c] = P.sF[base + c] * vF[base + c];
+      for (int c = 0; c < 6; ++c) {
+        const double sc = P.sF[base + c];
+        cp[c] = sc * cF[base + c];
+        gp[c] = -sc * yF[base + c];
+      }
     }
     if (P.lm_free[l])
 #pragma unroll
-      for (int c = 0; c < 3; ++c) vl[c] = P.sL[3 * (size_t)l + c] * vL[3 * (size_t)l + c];
+      for (int c = 0; c < 3; ++c) {
+        const size_t i = 3 * (size_t)l + c;
+        cl[c] = P.sL[i] * P.vL[i];
+        gl[c] = -P.sL[i] * P.yL[i];
+      }
     const auto lin = gmem(P.obs_lin[st.lcur]);
     const int64_t S = P.obs_stride;
     const double* hp = P.lm[st.xcur] + 4 * (size_t)l;
     const double* tw = P.pose[st.xcur] + 7 * (size_t)ps;
     const double w4 = hp[3];
     const double p3[3] = {hp[0] - tw[0] * w4, hp[1] - tw[1] * w4, hp[2] - tw[2] * w4};
-    double a = 0.0;
+    double a[3] = {0.0, 0.0, 0.0};
     for (int o = P.visit_obs_begin[v]; o < P.visit_obs_begin[v + 1]; ++o) {
       if (P.obs_flags[o] & 2) continue;
       double A[6], Jp[12], Jl[6];
@@ -96,79 +113,98 @@ __global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp, i
       obsJacobians(A, p3, w4, Jp, Jl);
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
-        double jv = 0.0;
+        double jc = 0.0, jg = 0.0;
 #pragma unroll
-        for (int c = 0; c < 6; ++c) jv += Jp[r * 6 + c] * vp[c];
+        for (int c = 0; c < 6; ++c) {
+          jc += Jp[r * 6 + c] * cp[c];
+          jg += Jp[r * 6 + c] * gp[c];
+        }
 #pragma unroll
-        for (int c = 0; c < 3; ++c) jv += Jl[r * 3 + c] * vl[c];
-        a += jv * jv;
+        for (int c = 0; c < 3; ++c) {
+          jc += Jl[r * 3 + c] * cl[c];
+          jg += Jl[r * 3 + c] * gl[c];
+        }
+        jvAcc(jc, jg, a);
       }
     }
-    P.obs_jv[v] = a;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) P.obs_jv[(size_t)k * P.n_visit + v] = a[k];
     return;
   }
   int u = t - P.n_visit;
   if (u < P.n_imu) {
     const int f = u;
     const int w = P.imu_win[f];
-    if (!jvSelect(P, w, mode)) return;
-    double a = 0.0;
+    if (!jvSelect(P, w)) return;
+    double a[3] = {0.0, 0.0, 0.0};
     if (!(P.imu_flags[f] & 2)) {
       const int lb = P.st[w].lcur;
       const double* L = P.imu_lin[lb] + (size_t)f * kImuLin;
       const int* blk = P.imu_blocks + 4 * f;
-      double v[30];
+      double vc[30], vg[30];
       const size_t foff = P.win_foff[w];
       const int offs[4] = {P.pose_f[blk[0]], P.sb_f[blk[1]], P.pose_f[blk[2]], P.sb_f[blk[3]]};
       const int cols[4] = {0, 6, 15, 21}, ns[4] = {6, 9, 6, 9};
       for (int q = 0; q < 4; ++q)
-        for (int c = 0; c < ns[q]; ++c)
-          v[cols[q] + c] = offs[q] >= 0 ? P.sF[foff + offs[q] + c] * vF[foff + offs[q] + c] : 0.0;
+        for (int c = 0; c < ns[q]; ++c) {
+          const size_t i = foff + offs[q] + c;
+          vc[cols[q] + c] = offs[q] >= 0 ? P.sF[i] * cF[i] : 0.0;
+          vg[cols[q] + c] = offs[q] >= 0 ? -P.sF[i] * yF[i] : 0.0;
+        }
       for (int r = 0; r < 15; ++r) {
-        double jv = 0.0;
-        for (int c = 0; c < 30; ++c) jv += L[15 + r * 30 + c] * v[c];
-        a += jv * jv;
+        double jc = 0.0, jg = 0.0;
+        for (int c = 0; c < 30; ++c) {
+          jc += L[15 + r * 30 + c] * vc[c];
+          jg += L[15 + r * 30 + c] * vg[c];
+        }
+        jvAcc(jc, jg, a);
       }
     }
-    P.imu_jv[f] = a;
+    for (int k = 0; k < 3; ++k) P.imu_jv[(size_t)k * P.n_imu + f] = a[k];
     return;
   }
   u -= P.n_imu;
   if (u < P.n_pprior) {
     const int i = u;
     const int w = P.pp_win[i];
-    if (!jvSelect(P, w, mode)) return;
-    double a = 0.0;
+    if (!jvSelect(P, w)) return;
+    double a[3] = {0.0, 0.0, 0.0};
     const int pf = P.pose_f[P.pp_block[i]];
     if (pf >= 0) {
       const double* L = P.pp_lin[P.st[w].lcur] + 42 * (size_t)i;
       const size_t base = (size_t)P.win_foff[w] + pf;
       for (int r = 0; r < 6; ++r) {
-        double jv = 0.0;
-        for (int c = 0; c < 6; ++c) jv += L[6 + r * 6 + c] * P.sF[base + c] * vF[base + c];
-        a += jv * jv;
+        double jc = 0.0, jg = 0.0;
+        for (int c = 0; c < 6; ++c) {
+          jc += L[6 + r * 6 + c] * P.sF[base + c] * cF[base + c];
+          jg += L[6 + r * 6 + c] * (-P.sF[base + c] * yF[base + c]);
+        }
+        jvAcc(jc, jg, a);
       }
     }
-    P.pp_jv[i] = a;
+    for (int k = 0; k < 3; ++k) P.pp_jv[(size_t)k * P.n_pprior + i] = a[k];
     return;
   }
   u -= P.n_pprior;
   if (u < P.n_sbprior) {
     const int i = u;
     const int w = P.sbp_win[i];
-    if (!jvSelect(P, w, mode)) return;
-    double a = 0.0;
+    if (!jvSelect(P, w)) return;
+    double a[3] = {0.0, 0.0, 0.0};
     const int sf = P.sb_f[P.sbp_block[i]];
     if (sf >= 0) {
       const double* L = P.sbp_lin[P.st[w].lcur] + 90 * (size_t)i;
       const size_t base = (size_t)P.win_foff[w] + sf;
       for (int r = 0; r < 9; ++r) {
-        double jv = 0.0;
-        for (int c = 0; c < 9; ++c) jv += L[9 + r * 9 + c] * P.sF[base + c] * vF[base + c];
-        a += jv * jv;
+        double jc = 0.0, jg = 0.0;
+        for (int c = 0; c < 9; ++c) {
+          jc += L[9 + r * 9 + c] * P.sF[base + c] * cF[base + c];
+          jg += L[9 + r * 9 + c] * (-P.sF[base + c] * yF[base + c]);
+        }
+        jvAcc(jc, jg, a);
       }
     }
-    P.sbp_jv[i] = a;
+    for (int k = 0; k < 3; ++k) P.sbp_jv[(size_t)k * P.n_sbprior + i] = a[k];
   }
 }
 
@@ -274,67 +310,33 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
     return;
   }
 
-  // J*v reductions
-  if (mode == R_JV_CAUCHY && !(s.need_gn && !s.gn_failed)) return;
-  if (mode == R_JV_STEP && s.step_valid != 2) return;
-  double a = 0.0, b = 0.0;
+  // J*v reductions (once per GN step): jcc, jgg, jcg and the Cauchy alpha = |gradient_|^2 / jcc
+  if (!(s.need_gn && !s.gn_failed)) return;
   const int lmb = P.win_lm_range[2 * w], lme = P.win_lm_range[2 * w + 1];
   const int vb = P.lm_visit_begin[lmb], ve = P.lm_visit_begin[lme];
-  for (int v = vb + t; v < ve; v += kRB) a += P.obs_jv[v];
-  for (int f = ib + t; f < ie; f += kRB) a += P.imu_jv[f];
-  for (int i = pb + t; i < pe; i += kRB) a += P.pp_jv[i];
-  for (int i = sbb + t; i < sbe; i += kRB) a += P.sbp_jv[i];
-  a = blockSum(a, sh);
-  if (mode == R_JV_STEP) {
-    // (J_s step).r = step.(s g): f-blocks and free landmarks of the window
-    const int fo = P.win_foff[w], fd = P.win_fdim[w];
-    for (int e = t; e < fd; e += kRB) b += P.stepF[fo + e] * P.sF[fo + e] * P.gF[fo + e];
-    for (int l = lmb + t; l < lme; l += kRB)
-      if (P.lm_free[l])
-        for (int c = 0; c < 3; ++c) {
-          const size_t i = 3 * (size_t)l + c;
-          b += P.stepL[i] * P.sL[i] * P.gL[i];
-        }
-    b = blockSum(b, sh);
+  double a[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    double acc = 0.0;
+    for (int v = vb + t; v < ve; v += kRB) acc += P.obs_jv[(size_t)k * P.n_visit + v];
+    for (int f = ib + t; f < ie; f += kRB) acc += P.imu_jv[(size_t)k * P.n_imu + f];
+    for (int i = pb + t; i < pe; i += kRB) acc += P.pp_jv[(size_t)k * P.n_pprior + i];
+    for (int i = sbb + t; i < sbe; i += kRB) acc += P.sbp_jv[(size_t)k * P.n_sbprior + i];
+    a[k] = blockSum(acc, sh);
   }
-  if (mode == R_JV_CAUCHY) {
-    // |gradient_|^2 over the window (f-vector + free landmarks)
-    double g2 = 0.0;
-    const int fo = P.win_foff[w], fd = P.win_fdim[w];
-    for (int e = t; e < fd; e += kRB) g2 += P.dgF[fo + e] * P.dgF[fo + e];
-    const int lbg = P.win_lm_range[2 * w], lnd = P.win_lm_range[2 * w + 1];
-    for (int l = lbg + t; l < lnd; l += kRB)
-      if (P.lm_free[l])
-        for (int c = 0; c < 3; ++c) g2 += P.dgL[3 * (size_t)l + c] * P.dgL[3 * (size_t)l + c];
-    g2 = blockSum(g2, sh);
-    if (t == 0) {
-      s.jv2 = a;
-      s.alpha = g2 / a;
-    }
-    return;
-  }
-  if (t != 0) return;
-  // model_cost_change = -(J step).(r + J step / 2)
-  s.jv2 = a;
-  s.jvr = b;
-  s.model_cost_change = -(b + 0.5 * a);
-  if (s.model_cost_change > 0.0) {
-    s.step_valid = 1;
-    s.consecutive_invalid = 0;
-    s.eval_cand = 1;
-  } else {
-    // HandleInvalidStep + DoglegStrategy::StepIsInvalid
-    s.step_valid = 0;
-    s.eval_cand = 0;
-    s.num_unsucc += 1;
-    if (++s.consecutive_invalid >= P.opt.max_num_consecutive_invalid_steps) {
-      s.done = 1;
-      s.termination = 2;  // FAILURE
-      return;
-    }
-    s.mu *= 10.0;
-    s.need_gn = 1;
-    finalizeIteration(P, s);
+  // |gradient_|^2 over the window (f-vector + free landmarks)
+  double g2 = 0.0;
+  const int fo = P.win_foff[w], fd = P.win_fdim[w];
+  for (int e = t; e < fd; e += kRB) g2 += P.dgF[fo + e] * P.dgF[fo + e];
+  for (int l = lmb + t; l < lme; l += kRB)
+    if (P.lm_free[l])
+      for (int c = 0; c < 3; ++c) g2 += P.dgL[3 * (size_t)l + c] * P.dgL[3 * (size_t)l + c];
+  g2 = blockSum(g2, sh);
+  if (t == 0) {
+    s.jcc = a[0];
+    s.jgg = a[1];
+    s.jcg = a[2];
+    s.alpha = g2 / a[0];
   }
 }
 
@@ -500,7 +502,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
   }
   // pass 2: step, delta, Plus, |x - x_cand|
   const int xs = s.xcur, xd = 1 - s.xcur;
-  double sn2 = 0.0, dn2 = 0.0;
+  double sn2 = 0.0, dn2 = 0.0, jr = 0.0;
   const int p0 = P.win_pose_range[2 * w], p1 = P.win_pose_range[2 * w + 1];
   for (int p = p0 + t; p < p1; p += kRB) {
     const int pf = P.pose_f[p];
@@ -513,6 +515,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
       const double st = v / P.diagF[i];
       P.stepF[i] = st;
       delta[c] = st * P.sF[i];
+      jr += delta[c] * P.gF[i];
     }
     const double* x = P.pose[xs] + 7 * (size_t)p;
     double* y = P.pose[xd] + 7 * (size_t)p;
@@ -536,6 +539,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
       dn2 += v * v;
       const double st = v / P.diagF[i];
       P.stepF[i] = st;
+      jr += (st * P.sF[i]) * P.gF[i];
       const double yv = x[c] + st * P.sF[i];
       y[c] = yv;
       sn2 += (x[c] - yv) * (x[c] - yv);
@@ -551,6 +555,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
       dn2 += v * v;
       const double st = v / P.diagL[i];
       P.stepL[i] = st;
+      jr += (st * P.sL[i]) * P.gL[i];
       const double yv = x[c] + st * P.sL[i];
       y[c] = yv;
       sn2 += (x[c] - yv) * (x[c] - yv);
@@ -559,16 +564,36 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
   }
   sn2 = blockSum(sn2, sh);
   dn2 = blockSum(dn2, sh);
-  if (t == 0) {
-    s.dogleg_step_norm = (dcase == 1) ? gauss_newton_norm : (dcase == 2) ? radius : sqrt(dn2);
-    s.step_norm = sqrt(sn2);
-    s.step_valid = 2;  // pending the model-cost test
+  jr = blockSum(jr, sh);
+  if (t != 0) return;
+  s.dogleg_step_norm = (dcase == 1) ? gauss_newton_norm : (dcase == 2) ? radius : sqrt(dn2);
+  s.step_norm = sqrt(sn2);
+  // model_cost_change = -(J step).(r + J step / 2), step = ca v_c + cb v_g
+  const double jj = (ca * ca) * s.jcc + 2.0 * (ca * cb) * s.jcg + (cb * cb) * s.jgg;
+  s.model_cost_change = -(jr + 0.5 * jj);
+  if (s.model_cost_change > 0.0) {
+    s.step_valid = 1;
+    s.consecutive_invalid = 0;
+    s.eval_cand = 1;
+  } else {
+    // HandleInvalidStep + DoglegStrategy::StepIsInvalid
+    s.step_valid = 0;
+    s.eval_cand = 0;
+    s.num_unsucc += 1;
+    if (++s.consecutive_invalid >= P.opt.max_num_consecutive_invalid_steps) {
+      s.done = 1;
+      s.termination = 2;  // FAILURE
+      return;
+    }
+    s.mu *= 10.0;
+    s.need_gn = 1;
+    finalizeIteration(P, s);
   }
 }
 
-void launch_jv(const DevProblem& P, int mode, hipStream_t s) {
+void launch_jv(const DevProblem& P, hipStream_t s) {
   const int n = P.n_visit + P.n_imu + P.n_pprior + P.n_sbprior;
-  if (n > 0) hipLaunchKernelGGL(k_jv, dim3((n + 255) / 256), dim3(256), 0, s, P.self, mode);
+  if (n > 0) hipLaunchKernelGGL(k_jv, dim3((n + 255) / 256), dim3(256), 0, s, P.self);
 }
 void launch_reduce(const DevProblem& P, int mode, hipStream_t s) {
   hipLaunchKernelGGL(k_reduce, dim3(P.n_win), dim3(kRB), 0, s, P.self, mode);

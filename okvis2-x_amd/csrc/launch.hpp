@@ -35,9 +35,9 @@ void launch_gn_finalize(const DevProblem& P, hipStream_t s);
 void launch_cholesky(const DevProblem& P, hipStream_t s);
 
 // trust-region control (kernels_control.hip)
-enum ReduceMode { R_COST_INIT = 0, R_COST_CAND = 1, R_JV_CAUCHY = 2, R_JV_STEP = 3 };
+enum ReduceMode { R_COST_INIT = 0, R_COST_CAND = 1, R_JV = 2 };
 void launch_reduce(const DevProblem& P, int mode, hipStream_t s);
-void launch_jv(const DevProblem& P, int mode, hipStream_t s);     // mode: R_JV_CAUCHY / R_JV_STEP
+void launch_jv(const DevProblem& P, hipStream_t s);
 void launch_gradnorm(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_dogleg(const DevProblem& P, hipStream_t s);
 

@@ -629,7 +629,7 @@ struct okvisgpu_ctx {
     const size_t o_obs_lin0 = scratch(sizeof(double) * kObsLin * D.obs_stride);
     const size_t o_obs_lin1 = scratch(sizeof(double) * kObsLin * D.obs_stride);
     const size_t o_obs_cost0 = scratch(sizeof(double) * D.n_obs), o_obs_cost1 = scratch(sizeof(double) * D.n_obs);
-    const size_t o_obs_jv = scratch(sizeof(double) * 2 * D.n_obs);
+    const size_t o_obs_jv = scratch(sizeof(double) * 3 * D.n_obs);
     const size_t o_lmvb = upl(B.lm_visit_begin), o_vpose = upl(B.visit_pose), o_vob = upl(B.visit_obs_begin),
                  o_vlm = upl(B.visit_lm);
     const size_t o_lmV = scratch(sizeof(double) * 6 * D.n_lm), o_lmg = scratch(sizeof(double) * 3 * D.n_lm),
@@ -643,19 +643,19 @@ struct okvisgpu_ctx {
     const size_t o_imu_lin0 = scratch(sizeof(double) * kImuLin * D.n_imu),
                  o_imu_lin1 = scratch(sizeof(double) * kImuLin * D.n_imu);
     const size_t o_imu_cost0 = scratch(sizeof(double) * D.n_imu), o_imu_cost1 = scratch(sizeof(double) * D.n_imu),
-                 o_imu_jv = scratch(sizeof(double) * 2 * D.n_imu),
+                 o_imu_jv = scratch(sizeof(double) * 3 * D.n_imu),
                  o_imu_H = scratch(sizeof(double) * kImuHess * D.n_imu);
     const size_t o_pp_block = upl(B.pp_block), o_pp_win = upl(B.pp_win), o_pp_meas = upl(B.pp_meas),
                  o_pp_L = upl(B.pp_L);
     const size_t o_pp_lin0 = scratch(sizeof(double) * 42 * D.n_pprior), o_pp_lin1 = scratch(sizeof(double) * 42 * D.n_pprior),
                  o_pp_cost0 = scratch(sizeof(double) * D.n_pprior), o_pp_cost1 = scratch(sizeof(double) * D.n_pprior),
-                 o_pp_jv = scratch(sizeof(double) * 2 * D.n_pprior);
+                 o_pp_jv = scratch(sizeof(double) * 3 * D.n_pprior);
     const size_t o_sbp_block = upl(B.sbp_block), o_sbp_win = upl(B.sbp_win), o_sbp_meas = upl(B.sbp_meas),
                  o_sbp_L = upl(B.sbp_L);
     const size_t o_sbp_lin0 = scratch(sizeof(double) * 90 * D.n_sbprior),
                  o_sbp_lin1 = scratch(sizeof(double) * 90 * D.n_sbprior),
                  o_sbp_cost0 = scratch(sizeof(double) * D.n_sbprior), o_sbp_cost1 = scratch(sizeof(double) * D.n_sbprior),
-                 o_sbp_jv = scratch(sizeof(double) * 2 * D.n_sbprior);
+                 o_sbp_jv = scratch(sizeof(double) * 3 * D.n_sbprior);
     const size_t o_wfoff = upl(B.win_foff), o_wfdim = upl(B.win_fdim), o_wfpad = upl(B.win_fpad),
                  o_wsoff = upl(B.win_soff), o_wlinv = upl(B.win_linvoff), o_wfwd = upl(B.win_fwdoff), o_wpr = upl(B.win_pose_range), o_wsr = upl(B.win_sb_range),
                  o_wlr = upl(B.win_lm_range), o_wor = upl(B.win_obs_range), o_wir = upl(B.win_imu_range),
@@ -864,11 +864,9 @@ struct okvisgpu_ctx {
     launch_gn_reduce(P, stream);
     launch_cholesky(P, stream);
     launch_gn_backsub(P, stream);
-    launch_jv(P, R_JV_CAUCHY, stream);
-    launch_reduce(P, R_JV_CAUCHY, stream);
+    launch_jv(P, stream);
+    launch_reduce(P, R_JV, stream);
     launch_dogleg(P, stream);
-    launch_jv(P, R_JV_STEP, stream);
-    launch_reduce(P, R_JV_STEP, stream);
     launch_eval(P, 1, stream);
     launch_reduce(P, R_COST_CAND, stream);
     launch_linearization_blocks(P, 1, stream);
@@ -1147,7 +1145,7 @@ int okvisgpu_solve(okvisgpu_ctx* c, const okvisgpu_options* o, okvisgpu_summary*
 
 static const char* kPhaseNames[OKVISGPU_N_PHASES] = {
     "lm_prep",     "zero_S",   "assemble",   "cholesky",  "lm_backsub", "gn_finalize",
-    "jv_cauchy",   "reduce_cauchy", "dogleg", "jv_step",  "reduce_step", "eval_obs",
+    "jv",          "reduce_jv", "dogleg",   "eval_obs",
     "eval_imu",    "eval_priors", "reduce_cand", "lin_blocks", "gradnorm"};
 
 const char* okvisgpu_phase_name(int32_t i) { return (i >= 0 && i < OKVISGPU_N_PHASES) ? kPhaseNames[i] : ""; }
@@ -1174,17 +1172,15 @@ int okvisgpu_profile_iteration(okvisgpu_ctx* c, double* ms) {
     launch_cholesky(P, s); mark(3);
     launch_lm_backsub(P, s); mark(4);
     launch_gn_finalize(P, s); mark(5);
-    launch_jv(P, R_JV_CAUCHY, s); mark(6);
-    launch_reduce(P, R_JV_CAUCHY, s); mark(7);
+    launch_jv(P, s); mark(6);
+    launch_reduce(P, R_JV, s); mark(7);
     launch_dogleg(P, s); mark(8);
-    launch_jv(P, R_JV_STEP, s); mark(9);
-    launch_reduce(P, R_JV_STEP, s); mark(10);
-    launch_eval_obs(P, 1, s); mark(11);
-    launch_eval_imu(P, 1, s); mark(12);
-    launch_eval_priors(P, 1, s); mark(13);
-    launch_reduce(P, R_COST_CAND, s); mark(14);
-    launch_linearization_blocks(P, 1, s); mark(15);
-    launch_gradnorm(P, 1, s); mark(16);
+    launch_eval_obs(P, 1, s); mark(9);
+    launch_eval_imu(P, 1, s); mark(10);
+    launch_eval_priors(P, 1, s); mark(11);
+    launch_reduce(P, R_COST_CAND, s); mark(12);
+    launch_linearization_blocks(P, 1, s); mark(13);
+    launch_gradnorm(P, 1, s); mark(14);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(s));
     for (int i = 0; i < OKVISGPU_N_PHASES; ++i) ms[i] = 0.0;
@@ -1242,7 +1238,7 @@ double kernelWork(const HostBatch& B, const DevProblem& P, int k) {
     case K_VISIT_PREP: return nVis * (18 * d8 + kVisitUY * d8 + 12) + nLm * 15 * d8;
     case K_EVAL_IMU: return nImu * (2.0 * kImuState + kImuLin + 2 * 16) * d8 + (double)B.imu_ts.size() * 7 * d8;
     case K_EVAL_OBS: return nObs * (16 + 32 + 13 + kObsLin * d8 + 8) + nLm * 4 * d8 + (double)B.pose_f.size() * 7 * d8;
-    case K_JV: return nObs * (kObsLin * d8 + 1) + nVis * (7 + 9 + 1) * d8 + nImu * kImuLin * d8;
+    case K_JV: return nObs * (kObsLin * d8 + 1) + nVis * (7 + 4 + 3 * 9 + 3) * d8 + nImu * (kImuLin + 3) * d8;
     case K_FGRAD: return nVis * 12 * d8 + nImu * kImuLin * d8 + (double)B.fb_contrib.size() * 16;
   }
   return 0.0;
@@ -1300,7 +1296,7 @@ int okvisgpu_time_kernel(okvisgpu_ctx* c, int32_t kernel, int32_t reps, double* 
           timed([&] { launch_eval_imu(P, 1, s); });
           break;
         case K_EVAL_OBS: timed([&] { launch_eval_obs(P, 1, s); }); break;
-        case K_JV: timed([&] { launch_jv(P, R_JV_STEP, s); }); break;
+        case K_JV: timed([&] { launch_jv(P, s); }); break;
         case K_FGRAD: timed([&] { launch_fgrad(P, 1, s); }); break;
         case K_CHOLESKY:  // needs a freshly assembled S each repetition
           launch_zero_S(P, s);

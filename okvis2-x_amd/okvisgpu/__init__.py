@@ -105,7 +105,7 @@ EXPORTED_SYMBOLS = [
     "okvisgpu_profile_iteration", "okvisgpu_phase_name", "okvisgpu_kernel_count", "okvisgpu_kernel_name",
     "okvisgpu_time_kernel",
 ]
-N_PHASES = 17
+N_PHASES = 15
 
 _lib = None
 
