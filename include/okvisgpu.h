@@ -161,8 +161,9 @@ typedef struct okvisgpu_options {   /* ::ceres::Solver::Options fields okvis set
   int32_t redo_propagation_always;  /* ImuError::redoPropagationAlways (ViSlamBackend.cpp:2036)  */
   int32_t num_threads;              /* host threads (reference path / host evaluation)          */
   int32_t verbose;
-  int32_t cholesky_schedule;        /* 0 auto, 1 one persistent workgroup per window (large       */
-                                    /* batches), 2 tile-parallel launches per step (few windows)  */
+  int32_t cholesky_schedule;        /* 0 auto, 1 one persistent workgroup per window (more        */
+                                    /* windows than CUs), 2 tile-parallel launches per step (few  */
+                                    /* windows), 3 wave-specialised workgroup per window          */
 } okvisgpu_options;
 
 typedef struct okvisgpu_summary {   /* ::ceres::Solver::Summary subset */

@@ -29,7 +29,7 @@ constexpr int kLd = kTile + 1;  // padded LDS row (65 doubles)
 // Development-only phase clock (make OPT="-O3 -DOKG_CHOL_CLOCK"): workgroup 0 of k_cholesky
 // accumulates s_memrealtime ticks (100 MHz) per phase and prints them.
 #ifdef OKG_CHOL_CLOCK
-__device__ unsigned long long g_cholClk[16];
+__device__ unsigned long long g_cholClk[32];
 #define CLK_INIT unsigned long long clkLast = __builtin_amdgcn_s_memrealtime();
 #define CLK(i)                                                                  \
   if (blockIdx.x == 0 && threadIdx.x == 0) {                                    \
@@ -37,9 +37,16 @@ __device__ unsigned long long g_cholClk[16];
     g_cholClk[i] += now - clkLast;                                              \
     clkLast = now;                                                              \
   }
+#define CLKW(i, cond)                                                           \
+  if (blockIdx.x == 0 && (cond)) {                                              \
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();            \
+    g_cholClk[i] += now - clkLast;                                              \
+    clkLast = now;                                                              \
+  }
 #else
 #define CLK_INIT
 #define CLK(i)
+#define CLKW(i, cond)
 #endif
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
@@ -290,44 +297,56 @@ __device__ void panelTile(double* Aik, int64_t ld, double* worki, double* sA, co
   __syncthreads();
 }
 
-// Backward substitution x = L^-T y (work holds y), x := y_F. x lives in LDS (sx, ld doubles);
-// per block row I the 16 row loads of every non-zero tile below are issued together, then
-// x_I = X_II^T (y_I - sum_i L_iI^T x_i) with the stored diagonal inverse.
-__device__ void backSubstitute(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* work,
-                               const double* Linv, const uint8_t* nz, double* sx, double* sA, double* sy, int t) {
-  for (int e = t; e < ld; e += 256) sx[e] = work[e];
-  __syncthreads();
-  const int col = t & 63, q = t >> 6;
+// Backward substitution x = L^-T y, x := y_F. sx (LDS, ld doubles) holds y on entry and x on
+// exit; per block row I the 16 row loads of every non-zero tile below are issued together, then
+// x_I = X_II^T (y_I - sum_i L_iI^T x_i) with the stored diagonal inverse. Threads 0..255 work;
+// any further threads of the workgroup only take part in the barriers.
+__device__ void backSubstituteY(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* Linv,
+                                const uint8_t* nz, double* sx, double* sA, double* sy, int t) {
+  const bool act = t < 256;
+  const int col = t & 63, q = (t >> 6) & 3;
   for (int I = T - 1; I >= 0; --I) {
     double acc = 0.0;
-    for (int i = I + 1; i < T; ++i) {
-      if (!nz[i * T + I]) continue;
-      const double* Lt = S + i * kTile * ld + I * kTile + col;
-      double v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = Lt[(int64_t)(q + 4 * u) * ld];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) acc += v[u] * sx[i * kTile + q + 4 * u];
-    }
-    const double* Li = Linv + (int64_t)I * kTile * kTile + col;
     double li[16];
+    if (act) {
+      for (int i = I + 1; i < T; ++i) {
+        if (!nz[i * T + I]) continue;
+        const double* Lt = S + i * kTile * ld + I * kTile + col;
+        double v[16];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) li[u] = Li[(q + 4 * u) * kTile];
-    sA[q * kTile + col] = acc;
+        for (int u = 0; u < 16; ++u) v[u] = Lt[(int64_t)(q + 4 * u) * ld];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc += v[u] * sx[i * kTile + q + 4 * u];
+      }
+      const double* Li = Linv + (int64_t)I * kTile * kTile + col;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) li[u] = Li[(q + 4 * u) * kTile];
+      sA[q * kTile + col] = acc;
+    }
     __syncthreads();
     if (t < kTile) sy[t] = sx[I * kTile + t] - ((sA[t] + sA[kTile + t]) + (sA[2 * kTile + t] + sA[3 * kTile + t]));
     __syncthreads();
-    double a = 0.0;
+    if (act) {
+      double a = 0.0;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) a += (q + 4 * u >= col) ? li[u] * sy[q + 4 * u] : 0.0;
-    sA[256 + q * kTile + col] = a;
+      for (int u = 0; u < 16; ++u) a += (q + 4 * u >= col) ? li[u] * sy[q + 4 * u] : 0.0;
+      sA[256 + q * kTile + col] = a;
+    }
     __syncthreads();
     if (t < kTile)
       sx[I * kTile + t] = (sA[256 + t] + sA[256 + kTile + t]) + (sA[256 + 2 * kTile + t] + sA[256 + 3 * kTile + t]);
     __syncthreads();
   }
   const int fdim = P.win_fdim[w];
-  for (int e = t; e < fdim; e += 256) P.yF[(size_t)P.win_foff[w] + e] = sx[e];
+  for (int e = t; e < fdim; e += blockDim.x) P.yF[(size_t)P.win_foff[w] + e] = sx[e];
+}
+
+// As backSubstituteY with y taken from work (global).
+__device__ void backSubstitute(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* work,
+                               const double* Linv, const uint8_t* nz, double* sx, double* sA, double* sy, int t) {
+  for (int e = t; e < ld; e += blockDim.x) sx[e] = work[e];
+  __syncthreads();
+  backSubstituteY(P, w, S, ld, T, Linv, nz, sx, sA, sy, t);
 }
 
 __global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__ Pp) {
@@ -484,10 +503,524 @@ __global__ __launch_bounds__(256) void k_chol_bsub(const DevProblem* __restrict_
                  P.Linv + P.win_linvoff[w], P.tile_nz + P.win_tnzoff[w], sxDyn, sA, sy, threadIdx.x);
 }
 
+// ---- wave-specialised persistent schedule. A workgroup of 8 wavefronts holds two window slots
+// when there are more windows than CUs (pairs mode), else one window. The factor wavefront of a
+// window (diagonal LLT, X = L^-1, y_k, all in LDS) is wavefront 4s of its slot; the MFMA
+// wavefronts (panels, band updates, forward-substitution updates) are 4s+1..4s+3 in pairs mode
+// and 1,2,3,5,6,7 with one window. Wavefronts are placed on the SIMDs round-robin (w and w+4
+// share one), so factor wavefronts never share a SIMD with MFMA wavefronts: a stream of FP64
+// MFMAs starves a readlane/VALU chain on the same SIMD ~40x. The LDS request keeps this to one
+// workgroup per CU. Within a window the wavefronts hand over through LDS flags, so the
+// factorisation of tile k+1 runs while the MFMA wavefronts finish the rest of step k:
+//   factor  k: wait diagReady > k (S_kk in sF, rhs_k final in work) -> LLT in sF
+//              -> wait xFree >= k -> X_k into sX, y_k, z_k = X_k^T y_k -> xReady = k+1
+//   MFMA    k: wait xReady > k -> panel (k+1,k) -> update (k+1,k+1) into sF -> diagReady = k+2
+//              -> X_k to global, other panels of step k -> xFree = k+1 -> other band updates
+// Panels: L_ik = A_ik X_k^T, and the forward substitution rhs_i -= L_ik y_k is formed as
+// A_ik z_k from the A_ik fragments already in registers. The 16x16 output blocks of a tile (only
+// the 10 lower ones of a diagonal tile: its upper triangle is never read) are dealt round-robin
+// to the MFMA wavefronts, two per round; operands come straight from global memory (or LDS) in
+// the 16x16x4 layout with the inner index permuted per lane (lane group lk owns k = 16 lk ..
+// 16 lk + 15): each lane reads 128 contiguous bytes; the sum is unchanged.
+constexpr int kSlotThreads = 256;
+constexpr int kWsThreads = 2 * kSlotThreads;
+constexpr int kMaxBlocksPerWave = 6;     // 16 blocks over >= 3 MFMA wavefronts
+
+struct WsFlags {
+  int xReady, diagReady, xFree, fail, gbar, sbar;
+};
+
+__device__ __forceinline__ int ldsAcquire(int* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void ldsRelease(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Wave-uniform wait for *p >= v; false once the factor wavefront reported a failed pivot.
+__device__ __forceinline__ bool waitFlag(int* p, int v, int* fail) {
+  for (;;) {
+    if (ldsAcquire(p) >= v) return true;
+    if (ldsAcquire(fail)) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+// Barrier of n wavefronts on a monotonic arrival counter (gen counts this wavefront's barriers).
+__device__ __forceinline__ void waveBarrier(int* ctr, int& gen, int n, int lane) {
+  ++gen;
+  if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (ldsAcquire(ctr) < gen * n) __builtin_amdgcn_s_sleep(1);
+}
+
+// The n-th output block of MFMA wavefront g (of ng) in a full (16 blocks) or lower (10 blocks)
+// tile; -1 past the end. Block bi is (bi >> 2, bi & 3).
+__device__ __forceinline__ int blockOf(bool lower, int g, int ng, int n) {
+  const int idx = g + ng * n;
+  if (!lower) return idx < 16 ? idx : -1;
+  // lower blocks (a >= b) in order: 0 4 5 8 9 10 12 13 14 15
+  if (idx >= 10) return -1;
+  const int a = idx < 1 ? 0 : idx < 3 ? 1 : idx < 6 ? 2 : 3;
+  const int b = idx - a * (a + 1) / 2;
+  return 4 * a + b;
+}
+
+// Two 16x16 output blocks bi0, bi1 (bi1 < 0: one block) of a 64x64 tile product:
+// acc[m] = A[16a..][0..63] B[16b..][0..63]^T. Rows come from global memory (row stride ld) or LDS
+// (row stride kLd), inner index permuted per lane group; both blocks' operands are loaded before
+// the MFMAs. With sz != nullptr also pz[m] = A[16a + (lane & 15)][.] . sz for blocks of column 0
+// (complete in lanes 0..15).
+template <bool ALDS, bool BLDS>
+__device__ __forceinline__ void gemmPair(const double* A, int lda, const double* B, int ldb, int bi0, int bi1,
+                                         dbl4 acc[2], const double* sz, double pz[2], int lane) {
+  const int lr = lane & 15, lk = lane >> 4;
+  const int bis[2] = {bi0, bi1};
+  double fa[2][16], fb[2][16];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int bi = bis[m];
+    if (bi < 0) break;
+    const double* pa = A + (16 * (bi >> 2) + lr) * (ALDS ? kLd : lda) + 16 * lk;
+    const double* pb = B + (16 * (bi & 3) + lr) * (BLDS ? kLd : ldb) + 16 * lk;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (ALDS) {
+        fa[m][2 * u] = pa[2 * u];
+        fa[m][2 * u + 1] = pa[2 * u + 1];
+      } else {
+        const double2 v = *reinterpret_cast<const double2*>(pa + 2 * u);
+        fa[m][2 * u] = v.x;
+        fa[m][2 * u + 1] = v.y;
+      }
+      if (BLDS) {
+        fb[m][2 * u] = pb[2 * u];
+        fb[m][2 * u + 1] = pb[2 * u + 1];
+      } else {
+        const double2 v = *reinterpret_cast<const double2*>(pb + 2 * u);
+        fb[m][2 * u] = v.x;
+        fb[m][2 * u + 1] = v.y;
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int bi = bis[m];
+    if (bi < 0) break;
+    acc[m] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[m][q], fb[m][q], acc[m], 0, 0, 0);
+    if (sz && (bi & 3) == 0) {
+      double d0 = 0.0, d1 = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; q += 2) {
+        d0 += fa[m][q] * sz[16 * lk + q];
+        d1 += fa[m][q + 1] * sz[16 * lk + q + 1];
+      }
+      double d = d0 + d1;
+      d += __shfl_xor(d, 16);
+      d += __shfl_xor(d, 32);
+      pz[m] = d;
+    }
+  }
+}
+__device__ __forceinline__ void storeBlock(double* C, int ld, int bi, const dbl4& acc, int lane) {
+  double* dst = C + (16 * (bi >> 2) + (lane >> 4)) * ld + 16 * (bi & 3) + (lane & 15);
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) dst[4 * reg * ld] = acc[reg];
+}
+__device__ __forceinline__ dbl4 subFromBlock(const double* C, int ld, int bi, const dbl4& acc, int lane) {
+  const double* src = C + (16 * (bi >> 2) + (lane >> 4)) * ld + 16 * (bi & 3) + (lane & 15);
+  dbl4 r;
+#pragma unroll
+  for (int reg = 0; reg < 4; ++reg) r[reg] = src[4 * reg * ld] - acc[reg];
+  return r;
+}
+
+// Panel tile, compute part: acc[n] = (A_ik X^T) blocks of wavefront g and the rhs correction
+// rhs_i -= A_ik z (blocks (a, 0) carry the row products). L_ik overwrites A_ik only after every
+// wavefront has read A_ik (blocksStore after a barrier).
+__device__ __forceinline__ void panelCompute(const double* Aik, int ld, const double* sX, const double* sZ,
+                                             double* worki, dbl4 acc[kMaxBlocksPerWave], int g, int ng, int lane) {
+#pragma unroll
+  for (int n0 = 0; n0 < kMaxBlocksPerWave; n0 += 2) {
+    const int bi0 = blockOf(false, g, ng, n0), bi1 = blockOf(false, g, ng, n0 + 1);
+    if (bi0 < 0) break;
+    double pz[2];
+    gemmPair<false, true>(Aik, ld, sX, 0, bi0, bi1, acc + n0, sZ, pz, lane);
+    if ((bi0 & 3) == 0 && lane < 16) worki[16 * (bi0 >> 2) + lane] -= pz[0];
+    if (bi1 >= 0 && (bi1 & 3) == 0 && lane < 16) worki[16 * (bi1 >> 2) + lane] -= pz[1];
+  }
+}
+__device__ __forceinline__ void blocksStore(double* C, int ld, const dbl4 acc[kMaxBlocksPerWave], bool lower, int g,
+                                            int ng, int lane) {
+#pragma unroll
+  for (int n = 0; n < kMaxBlocksPerWave; ++n) {
+    const int bi = blockOf(lower, g, ng, n);
+    if (bi < 0) break;
+    storeBlock(C, ld, bi, acc[n], lane);
+  }
+}
+// Band update tile C -= Li Lj^T (all global; lower blocks only for a diagonal tile).
+__device__ __forceinline__ void updateBlocks(double* C, const double* Li, const double* Lj, int ld, bool lower, int g,
+                                             int ng, int lane) {
+#pragma unroll 1
+  for (int n0 = 0; n0 < kMaxBlocksPerWave; n0 += 2) {
+    const int bi0 = blockOf(lower, g, ng, n0), bi1 = blockOf(lower, g, ng, n0 + 1);
+    if (bi0 < 0) break;
+    dbl4 acc[2];
+    double pz[2];
+    gemmPair<false, false>(Li, ld, Lj, ld, bi0, bi1, acc, nullptr, pz, lane);
+    storeBlock(C, ld, bi0, subFromBlock(C, ld, bi0, acc[0], lane), lane);
+    if (bi1 >= 0) storeBlock(C, ld, bi1, subFromBlock(C, ld, bi1, acc[1], lane), lane);
+  }
+}
+
+// Band update tile C -= A B^T with both operands in LDS (row stride kLd).
+__device__ __forceinline__ void updateBlocksLds(double* C, int ld, const double* sA, const double* sB, bool lower, int g,
+                                                int ng, int lane) {
+#pragma unroll 1
+  for (int n0 = 0; n0 < kMaxBlocksPerWave; n0 += 2) {
+    const int bi0 = blockOf(lower, g, ng, n0), bi1 = blockOf(lower, g, ng, n0 + 1);
+    if (bi0 < 0) break;
+    dbl4 acc[2];
+    double pz[2];
+    gemmPair<true, true>(sA, 0, sB, 0, bi0, bi1, acc, nullptr, pz, lane);
+    storeBlock(C, ld, bi0, subFromBlock(C, ld, bi0, acc[0], lane), lane);
+    if (bi1 >= 0) storeBlock(C, ld, bi1, subFromBlock(C, ld, bi1, acc[1], lane), lane);
+  }
+}
+// 64x64 global tile -> LDS (row stride kLd) by the nthr threads gt = 0.. of the MFMA wavefronts.
+__device__ __forceinline__ void stageTile(double* dst, const double* src, int ld, int gt, int nthr) {
+  for (int e = gt; e < kTile * kTile / 2; e += nthr) {
+    const int r = e >> 5, c = 2 * (e & 31);
+    const double2 v = *reinterpret_cast<const double2*>(src + r * ld + c);
+    dst[r * kLd + c] = v.x;
+    dst[r * kLd + c + 1] = v.y;
+  }
+}
+
+// Diagonal tile on the factor wavefront, all in LDS: sF holds S_kk on entry and L_kk on exit;
+// X = L_kk^-1 -> sX (after xFree >= xFreeNeed); y = X r (r: this lane's rhs row) -> sYk;
+// z = X^T y -> sZ. Blocked LLT with 16-column readlane panels and MFMA trailing updates;
+// blockwise inverse as in potrfTile. Returns false (uniformly) at a non-positive pivot.
+__device__ __forceinline__ bool potrfWave(double* sF, double* sX, double* sRl, double* sYk, double* sZ, double r,
+                                       int* xFree, int xFreeNeed, int* fail, int lane) {
+  CLK_INIT
+  const bool clk = lane == 0;
+#pragma unroll 1
+  for (int p = 0; p < 4; ++p) {
+    const int i = lane;
+    double a[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) a[c] = sF[i * kLd + 16 * p + c];
+    bool bad = false;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int col = 16 * p + c;
+      const double dcc = readlaneD(a[c], col);
+      if (!(dcc > 0.0)) bad = true;  // wave-uniform
+      const double rl = rsqrtRefined(dcc);
+      if (lane == 0) sRl[col] = rl;
+      const double l = (i == col) ? dcc * rl : a[c] * rl;
+      a[c] = l;
+#pragma unroll
+      for (int j = c + 1; j < 16; ++j) a[j] -= l * readlaneD(l, 16 * p + j);
+    }
+    if (bad) return false;
+#pragma unroll
+    for (int c = 0; c < 16; ++c)
+      if (i >= 16 * p + c) sF[i * kLd + 16 * p + c] = a[c];
+    __builtin_amdgcn_wave_barrier();
+    CLKW(4, clk)
+    for (int rb = p + 1; rb < 4; ++rb)
+      for (int cb = p + 1; cb <= rb; ++cb) {
+        double* C = sF + 16 * rb * kLd + 16 * cb;
+        dbl4 acc = loadC16(C, kLd, lane);
+        mfma16<1>(sF + 16 * rb * kLd + 16 * p, kLd, sF + 16 * cb * kLd + 16 * p, 1, kLd, -1.0, acc, lane);
+        storeC16(C, kLd, acc, lane);
+      }
+    __builtin_amdgcn_wave_barrier();
+    CLKW(5, clk)
+  }
+  if (!waitFlag(xFree, xFreeNeed, fail)) return false;  // X_{k-1}, z_{k-1} no longer read
+  CLKW(6, clk)
+#pragma unroll 8
+  for (int u = 0; u < 64; ++u) {
+    const int e = lane + 64 * u;
+    sX[(e >> 6) * kLd + (e & 63)] = 0.0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  CLKW(7, clk)
+  {  // the 4 diagonal 16x16 inverses, lane group q, lane = column j
+    const int q = lane >> 4, j = lane & 15;
+    double x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      double v = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+      for (int m = 0; m < i; ++m) v -= sF[(16 * q + i) * kLd + 16 * q + m] * x[m];
+      x[i] = (i >= j) ? v * sRl[16 * q + i] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sX[(16 * q + i) * kLd + 16 * q + j] = x[i];
+  }
+  __builtin_amdgcn_wave_barrier();
+  CLKW(8, clk)
+  for (int d = 1; d < 4; ++d)
+    for (int j = 0; j + d < 4; ++j) {
+      const int i = j + d;
+      dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+      for (int m = j; m < i; ++m)
+        mfma16<1>(sF + 16 * i * kLd + 16 * m, kLd, sX + 16 * m * kLd + 16 * j, kLd, 1, 1.0, acc, lane);
+      double* Xij = sX + 16 * i * kLd + 16 * j;
+      storeC16(Xij, kLd, acc, lane);
+      __builtin_amdgcn_wave_barrier();
+      dbl4 x = dbl4{0.0, 0.0, 0.0, 0.0};
+      mfma16<1>(sX + 16 * i * kLd + 16 * i, kLd, Xij, kLd, 1, -1.0, x, lane);
+      __builtin_amdgcn_wave_barrier();
+      storeC16(Xij, kLd, x, lane);
+      __builtin_amdgcn_wave_barrier();
+    }
+  CLKW(9, clk)
+  // y = X r, z = X^T y (X is stored with its zero upper triangle: full-length unpredicated sums,
+  // so the LDS reads pipeline)
+  sYk[lane] = r;
+  __builtin_amdgcn_wave_barrier();
+  double y4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 16
+  for (int j = 0; j < kTile; ++j) y4[j & 3] += sX[lane * kLd + j] * sYk[j];
+  const double y = (y4[0] + y4[1]) + (y4[2] + y4[3]);
+  __builtin_amdgcn_wave_barrier();
+  sYk[lane] = y;
+  __builtin_amdgcn_wave_barrier();
+  double z4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 16
+  for (int i = 0; i < kTile; ++i) z4[i & 3] += sX[i * kLd + lane] * sYk[i];
+  const double z = (z4[0] + z4[1]) + (z4[2] + z4[3]);
+  sZ[lane] = z;
+  __builtin_amdgcn_wave_barrier();
+  CLKW(10, clk)
+  return true;
+}
+
+// Backward substitution on one slot (4 wavefronts, slot-local barriers): x = L^-T y with y in sx
+// (LDS) on entry and x there on exit; then x -> yF.
+__device__ void backSubstituteSlot(const DevProblem& P, int w, const double* S, int ld, int T, const double* Linv,
+                                   const uint8_t* nz, double* sx, double* sA, double* sy, int* bar, int& gen, int t) {
+  const int col = t & 63, q = t >> 6;
+  for (int I = T - 1; I >= 0; --I) {
+    double acc = 0.0;
+    for (int i = I + 1; i < T; ++i) {
+      if (!nz[i * T + I]) continue;
+      const double* Lt = S + i * kTile * ld + I * kTile + col;
+      double v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = Lt[(q + 4 * u) * ld];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) acc += v[u] * sx[i * kTile + q + 4 * u];
+    }
+    const double* Li = Linv + I * kTile * kTile + col;
+    double li[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) li[u] = Li[(q + 4 * u) * kTile];
+    sA[q * kTile + col] = acc;
+    waveBarrier(bar, gen, 4, t & 63);
+    if (t < kTile) sy[t] = sx[I * kTile + t] - ((sA[t] + sA[kTile + t]) + (sA[2 * kTile + t] + sA[3 * kTile + t]));
+    waveBarrier(bar, gen, 4, t & 63);
+    double a = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) a += (q + 4 * u >= col) ? li[u] * sy[q + 4 * u] : 0.0;
+    sA[256 + q * kTile + col] = a;
+    waveBarrier(bar, gen, 4, t & 63);
+    if (t < kTile)
+      sx[I * kTile + t] = (sA[256 + t] + sA[256 + kTile + t]) + (sA[256 + 2 * kTile + t] + sA[256 + 3 * kTile + t]);
+    waveBarrier(bar, gen, 4, t & 63);
+  }
+  const int fdim = P.win_fdim[w];
+  for (int e = t; e < fdim; e += kSlotThreads) P.yF[(size_t)P.win_foff[w] + e] = sx[e];
+}
+
+__global__ __launch_bounds__(kWsThreads, 2) void k_cholesky_ws(const DevProblem* __restrict__ Pp, int pairs) {
+  const DevProblem& P = *Pp;
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  // roles: slot, factor wavefront or MFMA wavefront g of ng
+  const int slot = pairs ? wid >> 2 : 0;
+  const bool isF = pairs ? (wid & 3) == 0 : wid == 0;
+  const int ng = pairs ? 3 : 6;
+  const int g = pairs ? (wid & 3) - 1 : (wid < 4 ? wid - 1 : wid - 2);
+  const int t = tid - slot * kSlotThreads;  // thread index within the slot (bsub: waves 0..3)
+  __shared__ double sFs[2][kTile * kLd];
+  __shared__ double sXs[2][kTile * kLd];
+  __shared__ double sRls[2][kTile];
+  __shared__ double sZs[2][kTile];
+  __shared__ WsFlags fls[2];
+  extern __shared__ double sxDyn[];  // per slot: y, then x (max_fpad doubles)
+  if (tid < 2) fls[tid] = WsFlags{0, 0, 0, 0, 0, 0};
+  __syncthreads();  // the only workgroup-wide barrier: from here on a slot never waits on the other
+  const int w = pairs ? 2 * blockIdx.x + slot : blockIdx.x;
+  if ((!pairs && wid == 4) || w >= P.n_win || !cholSelect(P, w)) return;
+  double* sF = sFs[slot];
+  double* sX = sXs[slot];
+  double* sRl = sRls[slot];
+  double* sZ = sZs[slot];
+  WsFlags& fl = fls[slot];
+  double* sy = sxDyn + slot * P.max_fpad;
+  const int ld = (int)P.win_fpad[w];
+  const int T = ld / kTile;
+  double* S = P.S + P.win_soff[w];
+  double* Linv = P.Linv + P.win_linvoff[w];
+  double* work = P.fwdF + P.win_fwdoff[w];
+  const uint8_t* nz = P.tile_nz + P.win_tnzoff[w];
+  int sgen = 0;
+  CLK_INIT
+  const bool fClk = blockIdx.x == 0 && slot == 0 && isF && lane == 0, gClk = slot == 0 && g == 0 && lane == 0;
+  if (isF) {
+    // ------------------------------------------------------------------ factor wavefront
+    for (int k = 0; k < T; ++k) {
+      CLKW(18, fClk)
+      if (!waitFlag(&fl.diagReady, k + 1, &fl.fail)) break;
+      CLKW(19, fClk)
+      const double r = work[k * kTile + lane];  // rhs_k, corrected by the MFMA wavefronts
+      if (!potrfWave(sF, sX, sRl, sy + k * kTile, sZ, r, &fl.xFree, k, &fl.fail, lane)) {
+        if (lane == 0) {
+          ldsRelease(&fl.fail, 1);
+          P.st[w].gn_failed = 1;
+        }
+        break;
+      }
+      CLKW(20, fClk)
+      if (lane == 0) ldsRelease(&fl.xReady, k + 1);
+    }
+  } else {
+    // ------------------------------------------------------------------ MFMA wavefronts
+    const int gt = 64 * g + lane;
+    int gen = 0;
+    {
+      const int fdim = P.win_fdim[w];
+      const double* rhs0 = P.rhsF + P.win_foff[w];
+      for (int e = gt; e < ld; e += 64 * ng) work[e] = e < fdim ? rhs0[e] : 0.0;
+    }
+    for (int e = gt; e < kTile * kTile; e += 64 * ng) sF[(e >> 6) * kLd + (e & 63)] = S[(e >> 6) * ld + (e & 63)];
+    waveBarrier(&fl.gbar, gen, ng, lane);
+    if (gt == 0) ldsRelease(&fl.diagReady, 1);
+    for (int k = 0; k < T; ++k) {
+      CLKW(21, gClk)
+      if (!waitFlag(&fl.xReady, k + 1, &fl.fail)) break;
+      CLKW(22, gClk)
+      const bool more = k + 1 < T;
+      const bool has1 = more && nz[(k + 1) * T + k];
+      double* Sd = S + (k + 1) * kTile * ld + (k + 1) * kTile;  // S_{k+1,k+1}
+      dbl4 acc[kMaxBlocksPerWave];
+      if (has1) {  // L_{k+1,k}: staged in sF now, over A_{k+1,k} once every wavefront has read it
+        panelCompute(S + (k + 1) * kTile * ld + k * kTile, ld, sX, sZ, work + (k + 1) * kTile, acc, g, ng, lane);
+        blocksStore(sF, kLd, acc, false, g, ng, lane);
+      }
+      CLKW(23, gClk)
+      waveBarrier(&fl.gbar, gen, ng, lane);
+      CLKW(24, gClk)
+      if (has1) {  // S_{k+1,k+1} - L L^T (lower blocks) -> sF (L staged in sF)
+        blocksStore(S + (k + 1) * kTile * ld + k * kTile, ld, acc, false, g, ng, lane);
+#pragma unroll
+        for (int n0 = 0; n0 < 4; n0 += 2) {  // <= 4 of the 10 lower blocks per wavefront
+          const int bi0 = blockOf(true, g, ng, n0), bi1 = blockOf(true, g, ng, n0 + 1);
+          if (bi0 < 0) break;
+          double pzd[2];
+          gemmPair<true, true>(sF, 0, sF, 0, bi0, bi1, acc + n0, nullptr, pzd, lane);
+          acc[n0] = subFromBlock(Sd, ld, bi0, acc[n0], lane);
+          if (bi1 >= 0) acc[n0 + 1] = subFromBlock(Sd, ld, bi1, acc[n0 + 1], lane);
+        }
+        waveBarrier(&fl.gbar, gen, ng, lane);  // every block has read L from sF
+        blocksStore(sF, kLd, acc, true, g, ng, lane);
+      } else if (more) {
+        for (int e = gt; e < kTile * kTile; e += 64 * ng) sF[(e >> 6) * kLd + (e & 63)] = Sd[(e >> 6) * ld + (e & 63)];
+      }
+      CLKW(25, gClk)
+      waveBarrier(&fl.gbar, gen, ng, lane);
+      CLKW(24, gClk)
+      if (gt == 0) ldsRelease(&fl.diagReady, k + 2);
+      // X_k -> global (backward substitution)
+      for (int e = gt; e < kTile * kTile / 2; e += 64 * ng) {
+        const int row = e >> 5, c = 2 * (e & 31);
+        *reinterpret_cast<double2*>(Linv + k * kTile * kTile + row * kTile + c) =
+            double2{sX[row * kLd + c], sX[row * kLd + c + 1]};
+      }
+      for (int i = k + 2; i < T; ++i) {
+        if (!nz[i * T + k]) continue;
+        panelCompute(S + i * kTile * ld + k * kTile, ld, sX, sZ, work + i * kTile, acc, g, ng, lane);
+        waveBarrier(&fl.gbar, gen, ng, lane);  // A_ik fully read
+        blocksStore(S + i * kTile * ld + k * kTile, ld, acc, false, g, ng, lane);
+      }
+      CLKW(26, gClk)
+      waveBarrier(&fl.gbar, gen, ng, lane);
+      CLKW(24, gClk)
+      if (gt == 0) ldsRelease(&fl.xFree, k + 1);
+      if (pairs) {
+        for (int i = k + 1; i < T; ++i) {
+          if (!nz[i * T + k]) continue;
+          for (int j = k + 1; j <= i; ++j) {
+            if (!nz[j * T + k] || (i == k + 1 && j == k + 1)) continue;
+            updateBlocks(S + i * kTile * ld + j * kTile, S + i * kTile * ld + k * kTile, S + j * kTile * ld + k * kTile,
+                         ld, i == j, g, ng, lane);
+          }
+        }
+      } else {
+        // one window per workgroup: the idle slot's LDS stages the operands (L_ik once per row)
+        double* stA = sFs[1];
+        double* stB = sXs[1];
+        for (int i = k + 1; i < T; ++i) {
+          if (!nz[i * T + k]) continue;
+          bool staged = false;
+          for (int j = k + 1; j <= i; ++j) {
+            if (!nz[j * T + k] || (i == k + 1 && j == k + 1)) continue;
+            if (!staged) {
+              stageTile(stA, S + i * kTile * ld + k * kTile, ld, gt, 64 * ng);
+              staged = true;
+            }
+            if (j != i) stageTile(stB, S + j * kTile * ld + k * kTile, ld, gt, 64 * ng);
+            waveBarrier(&fl.gbar, gen, ng, lane);
+            updateBlocksLds(S + i * kTile * ld + j * kTile, ld, stA, j == i ? stA : stB, i == j, g, ng, lane);
+            waveBarrier(&fl.gbar, gen, ng, lane);  // stB (and stA after the row) free again
+          }
+        }
+      }
+      CLKW(27, gClk)
+      waveBarrier(&fl.gbar, gen, ng, lane);
+      CLKW(24, gClk)
+    }
+  }
+  if (!pairs && wid > 4) return;  // MFMA wavefronts 5..7: done (the backward substitution uses 0..3)
+  CLKW(28, fClk || gClk)
+  waveBarrier(&fl.sbar, sgen, 4, lane);
+  CLKW(29, gClk)
+  if (ldsAcquire(&fl.fail)) return;
+  backSubstituteSlot(P, w, S, ld, T, Linv, nz, sy, sF, sX, &fl.sbar, sgen, t);  // sF / sX reused as scratch
+  CLKW(30, gClk)
+#ifdef OKG_CHOL_CLOCK
+  if (blockIdx.x == 0 && slot == 0 && t == 0)
+    printf("WSPOTRF pfac %llu ptrail %llu waitXFree %llu zeroX %llu dinv %llu subd %llu yz %llu\n", g_cholClk[4],
+           g_cholClk[5], g_cholClk[6], g_cholClk[7], g_cholClk[8], g_cholClk[9], g_cholClk[10]);
+  if (blockIdx.x == 0 && slot == 0 && t == 64)
+    printf("WSCLK T=%d F: waitDiag %llu potrf %llu | G: waitX %llu p1 %llu bar %llu upd1 %llu panels %llu upds %llu bsub %llu (x10ns)\n",
+           T, g_cholClk[19], g_cholClk[20], g_cholClk[22], g_cholClk[23], g_cholClk[24], g_cholClk[25], g_cholClk[26],
+           g_cholClk[27], g_cholClk[30]);
+#endif
+}
+
+bool cholesky_ws_fits(int max_fpad, size_t lds_per_block) {
+  hipFuncAttributes attr;
+  if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky_ws)) != hipSuccess) return false;
+  return attr.sharedSizeBytes + 2 * sizeof(double) * (size_t)max_fpad <= lds_per_block;
+}
+
 void launch_cholesky(const DevProblem& P, hipStream_t s) {
   if (P.n_win == 0) return;
   if (P.chol_schedule == 1) {
     hipLaunchKernelGGL(k_cholesky, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
+    return;
+  }
+  if (P.chol_schedule == 3) {
+    // two windows per workgroup once there are more windows than CUs (set by the runtime)
+    const int pairs = P.chol_pairs;
+    const int nb = pairs ? (P.n_win + 1) / 2 : P.n_win;
+    hipLaunchKernelGGL(k_cholesky_ws, dim3(nb), dim3(kWsThreads), 2 * sizeof(double) * P.max_fpad, s, P.self, pairs);
     return;
   }
   hipLaunchKernelGGL(k_chol_diag, dim3(P.n_win), dim3(256), 0, s, P.self, 0);

@@ -32,6 +32,8 @@ void launch_gn_finalize(const DevProblem& P, hipStream_t s);
 
 // dense factorisation + both triangular solves, one persistent workgroup per window
 // (kernels_chol.hip)
+// wave-specialised Cholesky: does its LDS (static + 2 windows' solve vectors) fit a workgroup?
+bool cholesky_ws_fits(int max_fpad, size_t lds_per_block);
 void launch_cholesky(const DevProblem& P, hipStream_t s);
 
 // trust-region control (kernels_control.hip)

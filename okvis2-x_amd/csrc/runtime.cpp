@@ -542,7 +542,8 @@ struct okvisgpu_ctx {
   size_t arenaBytes = 0;
   hipGraphExec_t iterGraph = nullptr;
   int cuCount = 256;
-  static constexpr int kPersistentWindowsPerCU = 1;
+  size_t ldsPerBlock = 65536;
+  bool wsFits() const { return cholesky_ws_fits(P.max_fpad, ldsPerBlock); }
   bool haveProblem = false;
   // split-solve state
   bool inSolve = false;
@@ -730,6 +731,7 @@ struct okvisgpu_ctx {
     D.h_panel_begin = B.chol_panel_begin.data();
     D.h_upd_begin = B.chol_upd_begin.data();
     D.chol_schedule = 1;
+    D.chol_pairs = 0;
     D.asm_pp_items = ip(o_app); D.asm_sb_items = ip(o_asb);
     D.n_asm_pp = (int)B.asm_pp_items.size(); D.n_asm_sb = (int)B.asm_sb_items.size();
     D.tile_items = ip(o_ti);
@@ -774,16 +776,19 @@ struct okvisgpu_ctx {
     d.min_relative_decrease = o.min_relative_decrease;
     d.min_lm_diagonal = o.min_lm_diagonal;
     d.max_lm_diagonal = o.max_lm_diagonal;
-    // Cholesky schedule: one persistent workgroup per window needs about one window per CU to fill
-    // the chip; below that the tile-parallel launches spread each window over many CUs
-    const int sched = o.cholesky_schedule == 1 || o.cholesky_schedule == 2
-                          ? o.cholesky_schedule
-                          : (P.n_win >= kPersistentWindowsPerCU * cuCount ? 1 : 2);
+    // Cholesky schedule (measured on MI355X, S50 windows): below half a window per CU the
+    // tile-parallel launches spread each window over many CUs; up to one window per CU the
+    // wave-specialised kernel (one workgroup per window, factorisation overlapped with the MFMA
+    // tiles); beyond that the plain persistent kernel (two windows per CU)
+    int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 3 ? o.cholesky_schedule : 0;
+    if (sched == 0) sched = P.n_win > cuCount ? 1 : (2 * P.n_win >= cuCount && wsFits() ? 3 : 2);
+    if (sched == 3 && !wsFits()) sched = 2;
     if (sched != P.chol_schedule && iterGraph) {
       (void)hipGraphExecDestroy(iterGraph);
       iterGraph = nullptr;
     }
     P.chol_schedule = sched;
+    P.chol_pairs = P.n_win > cuCount ? 1 : 0;
     uploadDescriptor();
   }
 
@@ -964,6 +969,7 @@ int okvisgpu_ctx_create(int32_t device, okvisgpu_ctx** out) {
       throw HipError{std::string("okvisgpu is built for gfx950 only; device is ") + prop.gcnArchName,
                      OKVISGPU_ERR_DEVICE};
     c->cuCount = prop.multiProcessorCount;
+    c->ldsPerBlock = prop.sharedMemPerBlock;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     return (int)OKVISGPU_OK;
   });

@@ -274,7 +274,7 @@ def test_cholesky_schedules_agree(og, oracle, gpu_ctx):
     operations in the same order: bitwise-equal solves, both matching the oracle."""
     ws = [og.SynthWindow(10, 500, 4000, seed=s) for s in (31, 32)]
     res = []
-    for sched in (1, 2):
+    for sched in (1, 2, 3):
         for w in ws:
             w.reset()
         opts = og.default_options(max_num_iterations=5, function_tolerance=0.0, gradient_tolerance=0.0,
@@ -289,3 +289,8 @@ def test_cholesky_schedules_agree(og, oracle, gpu_ctx):
     so = oracle.solve(ws[0].problem_ptr(), og.default_options(max_num_iterations=5, function_tolerance=0.0,
                                                               gradient_tolerance=0.0, parameter_tolerance=0.0))
     _close(res[1][0][0], so)
+    # wave-specialised schedule: same factorisation, different summation order inside the tiles
+    for k in range(len(ws)):
+        assert res[2][0][k]["final_cost"] == pytest.approx(res[0][0][k]["final_cost"], rel=1e-9)
+        np.testing.assert_allclose(res[2][1][k], res[0][1][k], rtol=0, atol=1e-7)
+    _close(res[2][0][0], so)
