@@ -24,7 +24,9 @@ constexpr int kImuState = 292;        // == OKVISGPU_IMU_STATE_DOUBLES
 // Linearisation record per observation (structure of arrays, plane-major):
 //   plane 0-1: r (Cauchy-corrected)   plane 2-13: J_pose 2x6   plane 14-19: J_lm 2x3
 constexpr int kObsLin = 8;   // r (2) | A = L Jh C_CW (2x3), Cauchy-scaled
-constexpr int kVisitLin = 54;
+constexpr int kVisitHG = 28;   // per visit: H = J_p^T J_p (21, sym packed) | g = J_p^T r (6) | pad
+constexpr int kLmGroupVisits = 256;  // k_lm_visit: visits of one landmark group (one workgroup)
+constexpr int kLmGroupMax = 64;      // landmarks per group
 constexpr int kImuHess = 465 + 30;  // packed upper J^T J (30x30) | J^T r
 constexpr int kVisitUY = 24;  // Z = U L^-T (6x3) | U z (6)
 
@@ -48,6 +50,7 @@ struct WinState {
   double x_norm, step_norm;
   double alpha, dogleg_step_norm, model_cost_change;
   double grad_max_norm, grad_norm;
+  double z_mu;                     // mu the stored Z operands were formed with (-1: none)
   double jcc, jgg, jcg;            // |J_s v_c|^2, |J_s v_g|^2, (J_s v_c).(J_s v_g) of the current GN / Cauchy pair
   int32_t xcur, lcur;              // current parameter set / linearisation buffer (0/1)
   int32_t need_gn;                 // !DoglegStrategy::reuse_
@@ -116,8 +119,9 @@ struct DevProblem {
   double* lm_g;                    // [n_lm][3]  J_l^T r
   double* lm_Linv;                 // [n_lm][9]  L^-1, L L^T = s V s + D^2 (lower triangular)
   double* lm_zz;                   // [n_lm][3]  L^-1 (s g)
-  double* visit_lin;               // [n_visit][kVisitLin] W = J_p^T J_l (18) | H = J_p^T J_p (21, sym packed)
-                                   //   | g = J_p^T r (6) | V part J_l^T J_l (6) | J_l^T r (3)   (unscaled)
+  double* visit_hg;                // [n_visit][kVisitHG] H = J_p^T J_p (21, sym packed) | g = J_p^T r (6) (unscaled)
+  const int32_t* lmg_begin;        // [n_lmg+1] landmark groups of k_lm_visit (<= kLmGroupVisits visits each)
+  int32_t n_lmg;
   double* visit_UY;                // [n_visit][kVisitUY] Z = s_p W s_l L^-T (6x3) | U z (6)   (per GN solve)
 
   // --- IMU factors

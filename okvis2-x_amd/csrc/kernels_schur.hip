@@ -2,15 +2,15 @@
 //
 // The reduced ("camera") system of a window is formed exactly as Ceres' SchurEliminator does for
 // e-blocks = landmarks, but organised for the GPU:
-//   k_visit_lin   one thread per (landmark, pose) visit: W = J_p^T J_l, H_pp = J_p^T J_p,
-//                 g_p = J_p^T r and the visit's share of V = J_l^T J_l, g_l = J_l^T r from the
-//                 stored linearisation (unscaled; the Jacobi scaling is applied by consumers).
-//   k_lm_lin      one thread per landmark: V, g_l over its visits; iteration 0: Jacobi scaling.
+//   k_lm_visit    one workgroup per landmark group, one thread per (landmark, pose) visit:
+//                 J from the stored linearisation, H_pp = J_p^T J_p and g_p = J_p^T r per visit
+//                 (unscaled), V = J_l^T J_l and g_l per landmark (iteration 0: Jacobi scaling),
+//                 the landmark's 3x3 LLT of s V s + mu D^2 (InvertPSDMatrix) -> L^-1, L^-1 s g,
+//                 and per visit Z = s_p W s_l L^-T and U z (Y_a U_b^T = Z_a Z_b^T) — the
+//                 per-e-block SchurEliminator work in one pass; W never leaves the registers.
 //   k_imu_hess    one wavefront per IMU factor: J^T J (packed) and J^T r of its 15x30 Jacobian.
 //   k_fgrad       one wavefront per f-block (pose / speed-bias): unscaled gradient and
 //                 diag(H_ff), and at iteration 0 the Jacobi scaling 1/(1+sqrt(diag)).
-//   k_lm_prep     one thread per landmark: 3x3 LLT of s V s + D^2 (InvertPSDMatrix), L^-1, L^-1 s g.
-//   k_visit_prep  one thread per visit: Z = s_p W s_l L^-T and U z (Y_a U_b^T = Z_a Z_b^T).
 //   k_zero_S      clears the structurally non-zero tiles of S (padded diagonal = 1).
 //   k_assemble_pp one wavefront per pose-pose block pair (i >= j): 8 groups of 6 lanes (one per
 //                 row) sum fixed, interleaved subsets of the pair's contributions — visits,
@@ -44,83 +44,225 @@ __device__ __forceinline__ bool linSelect(const DevProblem& P, int w, int lin_mo
   return true;
 }
 
-// One thread per (landmark, pose) visit: the 1-2 reprojection residuals of the visit give the
-// pose-landmark blocks W = J_p^T J_l, H = J_p^T J_p, g = J_p^T r and the visit's share of the
-// landmark block (V, J_l^T r): one 54-double AoS record per visit (16-byte stores, merged in L2).
-__global__ __launch_bounds__(256) void k_visit_lin(const DevProblem* __restrict__ Pp, int lin_mode) {
-  const DevProblem& P = *Pp;
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= P.n_visit) return;
-  const int l = P.visit_lm[v];
-  const int w = P.lm_win[l];
-  if (!linSelect(P, w, lin_mode)) return;
-  double o[kVisitLin];  // W 0..17 | H 18..38 | g 39..44 | V 45..50 | g_l 51..53
-#pragma unroll
-  for (int i = 0; i < kVisitLin; ++i) o[i] = 0.0;
-  const bool lfree = P.lm_free[l] != 0;
-  const bool pf = P.pose_f[P.visit_pose[v]] >= 0;
-  const WinState& st = P.st[w];
-  const auto lin = gmem(P.obs_lin[st.lcur]);
-  const int64_t S = P.obs_stride;
-  // linearisation point of lin[lcur]: params X[xcur]
-  const double* hp = P.lm[st.xcur] + 4 * (size_t)l;
-  const double* tw = P.pose[st.xcur] + 7 * (size_t)P.visit_pose[v];
-  const double w4 = hp[3];
-  const double p3[3] = {hp[0] - tw[0] * w4, hp[1] - tw[1] * w4, hp[2] - tw[2] * w4};
-  for (int ob = P.visit_obs_begin[v]; ob < P.visit_obs_begin[v + 1]; ++ob) {
-    if (P.obs_flags[ob] & 2) continue;
-    double r[2], A[6], Jp[12], Jl[6];
-    r[0] = lin[0 * S + ob];
-    r[1] = lin[1 * S + ob];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) A[k] = lin[(2 + k) * S + ob];
-    obsJacobians(A, p3, w4, Jp, Jl);
-    if (lfree) {
-#pragma unroll
-      for (int a2 = 0; a2 < 3; ++a2) {
-        o[51 + a2] += Jl[a2] * r[0] + Jl[3 + a2] * r[1];
-#pragma unroll
-        for (int b2 = a2; b2 < 3; ++b2) o[45 + sym3(a2, b2)] += Jl[a2] * Jl[b2] + Jl[3 + a2] * Jl[3 + b2];
-      }
-    }
-    if (pf) {
-#pragma unroll
-      for (int a2 = 0; a2 < 6; ++a2) {
-        o[39 + a2] += Jp[a2] * r[0] + Jp[6 + a2] * r[1];
-#pragma unroll
-        for (int b2 = a2; b2 < 6; ++b2) o[18 + sym6(a2, b2)] += Jp[a2] * Jp[b2] + Jp[6 + a2] * Jp[6 + b2];
-        if (lfree)
-#pragma unroll
-          for (int b2 = 0; b2 < 3; ++b2) o[a2 * 3 + b2] += Jp[a2] * Jl[b2] + Jp[6 + a2] * Jl[3 + b2];
-      }
-    }
-  }
-  double2* out = reinterpret_cast<double2*>(P.visit_lin + (size_t)v * kVisitLin);
-#pragma unroll
-  for (int i = 0; i < kVisitLin / 2; ++i) out[i] = double2{o[2 * i], o[2 * i + 1]};
+// Landmark-major linearisation + landmark elimination prep, one workgroup per landmark group
+// (whole landmarks, <= kLmGroupVisits visits; visits of a landmark are contiguous), one thread
+// per (landmark, pose) visit. Restates SchurEliminator's per-e-block work:
+//   visit    J_p, J_l of its 1-2 residuals from the stored linearisation (r | A) -> W = J_p^T J_l,
+//            H = J_p^T J_p and g = J_p^T r (stored for k_fgrad / k_assemble_pp), and its share
+//            of V = J_l^T J_l, g_l = J_l^T r (LDS)
+//   landmark (one thread each) V, g_l summed over its visits in visit order; iteration 0: the
+//            Jacobi scaling 1 / (1 + sqrt(diag V)); then the 3x3 LLT of s V s + mu D^2
+//            (InvertPSDMatrix) -> L^-1, zz = L^-1 (s g), the dogleg diagonal D
+//   visit    Z = s_p W s_l L^-T and U z = Z zz, the operands of the Schur terms
+//            Y_a U_b^T = Z_a Z_b^T (k_assemble_pp) and of the back substitution (k_lm_backsub)
+// mode 0: linearisation at iteration 0 (no Z: the pose scaling comes from k_fgrad afterwards);
+// mode 1: linearisation after an accepted step, Z for the new mu (WinState::z_mu);
+// mode 2: GN prep of windows whose Z is stale (mu raised by a retry or an invalid step): W is
+//         recomputed from the stored linearisation, V / g_l reused.
+__device__ __forceinline__ bool lmVisitSelect(const DevProblem& P, int w, int mode) {
+  const WinState& s = P.st[w];
+  if (s.done) return false;
+  if (mode == 0) return true;
+  if (mode == 1) return s.accepted;
+  return s.need_gn && !s.gn_failed && s.z_mu != s.mu;
 }
 
-// One thread per landmark: V = sum over visits, J_l^T r, and (iteration 0) the landmark's Jacobi
-// scaling 1 / (1 + sqrt(diag(V)))  (TrustRegionMinimizer / ScaledJacobian).
-__global__ __launch_bounds__(256) void k_lm_lin(const DevProblem* __restrict__ Pp, int lin_mode) {
+__global__ __launch_bounds__(kLmGroupVisits) void k_lm_visit(const DevProblem* __restrict__ Pp, int mode) {
   const DevProblem& P = *Pp;
-  const int l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= P.n_lm || !P.lm_free[l]) return;
+  const int t = threadIdx.x;
+  const int l0 = P.lmg_begin[blockIdx.x], l1 = P.lmg_begin[blockIdx.x + 1];
+  const int v0 = P.lm_visit_begin[l0], v1 = P.lm_visit_begin[l1];
+  __shared__ double sVg[9][kLmGroupVisits];  // visit shares of V (6) | g_l (3)
+  __shared__ double sLz[15][kLmGroupMax];    // per landmark: L^-1 (9) | zz (3) | s_l (3)
+  const int v = v0 + t;
+  const bool hasV = v < v1;
+  const int l = hasV ? P.visit_lm[v] : l0;
   const int w = P.lm_win[l];
-  if (!linSelect(P, w, lin_mode)) return;
-  double V[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
-  for (int v = P.lm_visit_begin[l]; v < P.lm_visit_begin[l + 1]; ++v) {
-    const double* src = P.visit_lin + (size_t)v * kVisitLin + 45;
+  const bool sel = hasV && lmVisitSelect(P, w, mode);
+  const bool lfree = P.lm_free[l] != 0;
+  const int pose = hasV ? P.visit_pose[v] : 0;
+  const int pf = P.pose_f[pose];
+  double W[18], H[21], gp[6], Vv[6], gl[3];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) V[i] += src[i];
+  for (int i = 0; i < 18; ++i) W[i] = 0.0;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) g[i] += src[6 + i];
+  for (int i = 0; i < 21; ++i) H[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) { gp[i] = 0.0; Vv[i] = 0.0; }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) gl[i] = 0.0;
+  if (sel) {
+    const WinState& st = P.st[w];
+    const auto lin = gmem(P.obs_lin[st.lcur]);
+    const int64_t S = P.obs_stride;
+    // linearisation point of lin[lcur]: params X[xcur]
+    const double* hp = P.lm[st.xcur] + 4 * (size_t)l;
+    const double* tw = P.pose[st.xcur] + 7 * (size_t)pose;
+    const double w4 = hp[3];
+    const double p3[3] = {hp[0] - tw[0] * w4, hp[1] - tw[1] * w4, hp[2] - tw[2] * w4};
+    for (int ob = P.visit_obs_begin[v]; ob < P.visit_obs_begin[v + 1]; ++ob) {
+      if (P.obs_flags[ob] & 2) continue;
+      double r[2], A[6], Jp[12], Jl[6];
+      r[0] = lin[0 * S + ob];
+      r[1] = lin[1 * S + ob];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) A[k] = lin[(2 + k) * S + ob];
+      obsJacobians(A, p3, w4, Jp, Jl);
+      if (lfree) {
+#pragma unroll
+        for (int a2 = 0; a2 < 3; ++a2) {
+          gl[a2] += Jl[a2] * r[0] + Jl[3 + a2] * r[1];
+#pragma unroll
+          for (int b2 = a2; b2 < 3; ++b2) Vv[sym3(a2, b2)] += Jl[a2] * Jl[b2] + Jl[3 + a2] * Jl[3 + b2];
+        }
+      }
+      if (pf >= 0) {
+#pragma unroll
+        for (int a2 = 0; a2 < 6; ++a2) {
+          gp[a2] += Jp[a2] * r[0] + Jp[6 + a2] * r[1];
+#pragma unroll
+          for (int b2 = a2; b2 < 6; ++b2) H[sym6(a2, b2)] += Jp[a2] * Jp[b2] + Jp[6 + a2] * Jp[6 + b2];
+          if (lfree)
+#pragma unroll
+            for (int b2 = 0; b2 < 3; ++b2) W[a2 * 3 + b2] += Jp[a2] * Jl[b2] + Jp[6 + a2] * Jl[3 + b2];
+        }
+      }
+    }
+    if (mode != 2) {
+      double2* out = reinterpret_cast<double2*>(P.visit_hg + (size_t)v * kVisitHG);
+#pragma unroll
+      for (int i = 0; i < 10; ++i) out[i] = double2{H[2 * i], H[2 * i + 1]};
+      out[10] = double2{H[20], gp[0]};
+#pragma unroll
+      for (int i = 0; i < 2; ++i) out[11 + i] = double2{gp[1 + 2 * i], gp[2 + 2 * i]};
+      out[13] = double2{gp[5], 0.0};
+    }
   }
-  for (int i = 0; i < 6; ++i) P.lm_V[6 * (size_t)l + i] = V[i];
-  for (int i = 0; i < 3; ++i) P.lm_g[3 * (size_t)l + i] = g[i];
-  if (lin_mode == 0)  // Jacobi scaling fixed at iteration 0 (TrustRegionMinimizer)
-    for (int a = 0; a < 3; ++a)
-      P.sL[3 * (size_t)l + a] = P.opt.jacobi_scaling ? 1.0 / (1.0 + sqrt(V[sym3(a, a)])) : 1.0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) sVg[i][t] = Vv[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) sVg[6 + i][t] = gl[i];
+  __syncthreads();
+  // ---- one thread per landmark of the group
+  if (t < l1 - l0) {
+    const int L = l0 + t;
+    const int wL = P.lm_win[L];
+    WinState& st = P.st[wL];
+    if (lmVisitSelect(P, wL, mode)) {
+      if (mode == 1 && L == P.win_lm_range[2 * wL]) st.z_mu = st.mu;  // one writer per window
+      if (P.lm_free[L]) {
+        double V[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
+        if (mode == 2) {
+#pragma unroll
+          for (int i = 0; i < 6; ++i) V[i] = P.lm_V[6 * (size_t)L + i];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) g[i] = P.lm_g[3 * (size_t)L + i];
+        } else {
+          for (int u = P.lm_visit_begin[L] - v0; u < P.lm_visit_begin[L + 1] - v0; ++u) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) V[i] += sVg[i][u];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) g[i] += sVg[6 + i][u];
+          }
+#pragma unroll
+          for (int i = 0; i < 6; ++i) P.lm_V[6 * (size_t)L + i] = V[i];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) P.lm_g[3 * (size_t)L + i] = g[i];
+          if (mode == 0)  // Jacobi scaling fixed at iteration 0 (TrustRegionMinimizer)
+            for (int a = 0; a < 3; ++a)
+              P.sL[3 * (size_t)L + a] = P.opt.jacobi_scaling ? 1.0 / (1.0 + sqrt(V[sym3(a, a)])) : 1.0;
+        }
+        if (mode != 0) {
+          const double* s = P.sL + 3 * (size_t)L;
+          const double mu = st.mu;
+          double A[9];
+          for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) A[a * 3 + b] = s[a] * s[b] * V[sym3(a, b)];
+          const double smu = sqrt(mu);
+          for (int a = 0; a < 3; ++a) {
+            const double dg = sqrt(fmin(fmax(A[a * 3 + a], P.opt.min_lm_diagonal), P.opt.max_lm_diagonal));
+            P.diagL[3 * (size_t)L + a] = dg;
+            const double d = dg * smu;
+            A[a * 3 + a] += d * d;
+          }
+          // LLT and inverse (InvertPSDMatrix, full rank)
+          double Lc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+          bool ok = true;
+          for (int k = 0; k < 3 && ok; ++k) {
+            double d = A[k * 3 + k];
+            for (int j = 0; j < k; ++j) d -= Lc[k * 3 + j] * Lc[k * 3 + j];
+            if (!(d > 0.0)) { ok = false; break; }
+            d = sqrt(d);
+            Lc[k * 3 + k] = d;
+            for (int i = k + 1; i < 3; ++i) {
+              double tt = A[i * 3 + k];
+              for (int j = 0; j < k; ++j) tt -= Lc[i * 3 + j] * Lc[k * 3 + j];
+              Lc[i * 3 + k] = tt / d;
+            }
+          }
+          double Li[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, zz[3] = {0, 0, 0};
+          if (!ok) {
+            st.gn_failed = 1;
+          } else {
+            // L^-1 (lower) and zz = L^-1 (s g): V'^-1 = L^-T L^-1, so Y_a U_b^T = Z_a Z_b^T, Z = U L^-T
+            for (int c = 0; c < 3; ++c) {
+              Li[c * 3 + c] = 1.0 / Lc[c * 3 + c];
+              for (int i = c + 1; i < 3; ++i) {
+                double tt = 0.0;
+                for (int j = c; j < i; ++j) tt -= Lc[i * 3 + j] * Li[j * 3 + c];
+                Li[i * 3 + c] = tt / Lc[i * 3 + i];
+              }
+            }
+            const double sg[3] = {s[0] * g[0], s[1] * g[1], s[2] * g[2]};
+            for (int a = 0; a < 3; ++a) zz[a] = Li[a * 3 + 0] * sg[0] + Li[a * 3 + 1] * sg[1] + Li[a * 3 + 2] * sg[2];
+          }
+          double* Lo = P.lm_Linv + 9 * (size_t)L;
+          for (int i = 0; i < 9; ++i) Lo[i] = Li[i];
+          for (int a = 0; a < 3; ++a) P.lm_zz[3 * (size_t)L + a] = zz[a];
+#pragma unroll
+          for (int i = 0; i < 9; ++i) sLz[i][t] = Li[i];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            sLz[9 + i][t] = zz[i];
+            sLz[12 + i][t] = s[i];
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---- visit: Z = s_p W s_l L^-T (6x3) | U z = Z zz (6)
+  if (!sel || mode == 0) return;
+  double o[kVisitUY];
+#pragma unroll
+  for (int i = 0; i < kVisitUY; ++i) o[i] = 0.0;
+  if (pf >= 0 && lfree) {
+    const int u = l - l0;
+    double Li[9], zz[3], s3[3], spr[6];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Li[i] = sLz[i][u];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      zz[i] = sLz[9 + i][u];
+      s3[i] = sLz[12 + i][u];
+    }
+    const auto sp = gmem(P.sF + (size_t)P.win_foff[w] + pf);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) spr[i] = sp[i];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const double u0 = spr[r] * W[r * 3 + 0] * s3[0], u1 = spr[r] * W[r * 3 + 1] * s3[1],
+                   u2 = spr[r] * W[r * 3 + 2] * s3[2];
+      const double z0 = u0 * Li[0];
+      const double z1 = u0 * Li[3] + u1 * Li[4];
+      const double z2 = u0 * Li[6] + u1 * Li[7] + u2 * Li[8];
+      o[r * 3 + 0] = z0; o[r * 3 + 1] = z1; o[r * 3 + 2] = z2;
+      o[18 + r] = z0 * zz[0] + z1 * zz[1] + z2 * zz[2];
+    }
+  }
+  double2* out = reinterpret_cast<double2*>(P.visit_UY + (size_t)v * kVisitUY);
+#pragma unroll
+  for (int i = 0; i < kVisitUY / 2; ++i) out[i] = double2{o[2 * i], o[2 * i + 1]};
 }
 
 // contribution helpers -------------------------------------------------------------------------
@@ -182,7 +324,7 @@ __global__ __launch_bounds__(64) void k_fgrad(const DevProblem* __restrict__ Pp,
   for (int k = P.fb_cbegin[fb] + lane; k < P.fb_cbegin[fb + 1]; k += 64) {
     const Contrib cb = P.fb_contrib[k];
     if (cb.type == C_VISIT) {
-      const double* H = P.visit_lin + (size_t)cb.a * kVisitLin + 18;
+      const double* H = P.visit_hg + (size_t)cb.a * kVisitHG;
       const double* gp = H + 21;
 #pragma unroll
       for (int c = 0; c < 6; ++c) { g[c] += gp[c]; hd[c] += H[sym6(c, c)]; }
@@ -239,110 +381,6 @@ __device__ __forceinline__ bool gnSelect(const DevProblem& P, int w) {
   return !s.done && s.need_gn && !s.gn_failed;
 }
 
-__global__ __launch_bounds__(256) void k_lm_prep(const DevProblem* __restrict__ Pp) {
-  const DevProblem& P = *Pp;
-  const int l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= P.n_lm) return;
-  if (!P.lm_free[l]) return;
-  const int w = P.lm_win[l];
-  if (!gnSelect(P, w)) return;
-  const double mu = P.st[w].mu;
-  const double* V = P.lm_V + 6 * (size_t)l;
-  const double* s = P.sL + 3 * (size_t)l;
-  const double* g = P.lm_g + 3 * (size_t)l;
-  double A[9];
-  for (int a = 0; a < 3; ++a)
-    for (int b = 0; b < 3; ++b) A[a * 3 + b] = s[a] * s[b] * V[sym3(a, b)];
-  const double smu = sqrt(mu);
-  for (int a = 0; a < 3; ++a) {
-    const double dg = sqrt(fmin(fmax(A[a * 3 + a], P.opt.min_lm_diagonal), P.opt.max_lm_diagonal));
-    P.diagL[3 * (size_t)l + a] = dg;
-    const double d = dg * smu;
-    A[a * 3 + a] += d * d;
-  }
-  // LLT and inverse (InvertPSDMatrix, full rank)
-  double L[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  bool ok = true;
-  for (int k = 0; k < 3 && ok; ++k) {
-    double d = A[k * 3 + k];
-    for (int j = 0; j < k; ++j) d -= L[k * 3 + j] * L[k * 3 + j];
-    if (!(d > 0.0)) { ok = false; break; }
-    d = sqrt(d);
-    L[k * 3 + k] = d;
-    for (int i = k + 1; i < 3; ++i) {
-      double t = A[i * 3 + k];
-      for (int j = 0; j < k; ++j) t -= L[i * 3 + j] * L[k * 3 + j];
-      L[i * 3 + k] = t / d;
-    }
-  }
-  if (!ok) {
-    P.st[w].gn_failed = 1;
-    return;
-  }
-  // L^-1 (lower triangular) and zz = L^-1 (s g): V'^-1 = L^-T L^-1, so the Schur terms factor as
-  // Y_a U_b^T = U_a V'^-1 U_b^T = Z_a Z_b^T with Z = U L^-T (k_visit_prep)
-  double Li[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (int c = 0; c < 3; ++c) {
-    Li[c * 3 + c] = 1.0 / L[c * 3 + c];
-    for (int i = c + 1; i < 3; ++i) {
-      double t = 0.0;
-      for (int j = c; j < i; ++j) t -= L[i * 3 + j] * Li[j * 3 + c];
-      Li[i * 3 + c] = t / L[i * 3 + i];
-    }
-  }
-  const double sg[3] = {s[0] * g[0], s[1] * g[1], s[2] * g[2]};
-  double* Lo = P.lm_Linv + 9 * (size_t)l;
-  for (int i = 0; i < 9; ++i) Lo[i] = Li[i];
-  for (int a = 0; a < 3; ++a)
-    P.lm_zz[3 * (size_t)l + a] = Li[a * 3 + 0] * sg[0] + Li[a * 3 + 1] * sg[1] + Li[a * 3 + 2] * sg[2];
-}
-
-// One thread per visit with a free pose and landmark: Z = U L^-T with U = s_p W s_l, and U z = Z zz
-// — the operands of the Schur terms Y_a U_b^T = Z_a Z_b^T (24-double AoS records; 16-byte stores,
-// merged in L2).
-__global__ __launch_bounds__(256) void k_visit_prep(const DevProblem* __restrict__ Pp) {
-  const DevProblem& P = *Pp;
-  const int v = blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= P.n_visit) return;
-  const int l = P.visit_lm[v];
-  const int w = P.lm_win[l];
-  if (!gnSelect(P, w)) return;
-  const int pf = P.pose_f[P.visit_pose[v]];
-  double2* out = reinterpret_cast<double2*>(P.visit_UY + (size_t)v * kVisitUY);
-  if (pf < 0 || !P.lm_free[l]) {
-#pragma unroll
-    for (int i = 0; i < kVisitUY / 2; ++i) out[i] = double2{0.0, 0.0};
-    return;
-  }
-  const auto W = gmem(P.visit_lin + (size_t)v * kVisitLin);
-  const auto sl = gmem(P.sL + 3 * (size_t)l);
-  const auto Lig = gmem(P.lm_Linv + 9 * (size_t)l);
-  const auto zg = gmem(P.lm_zz + 3 * (size_t)l);
-  const auto sp = gmem(P.sF + (size_t)P.win_foff[w] + pf);
-  double w18[18], Li[9], zz[3], s3[3], spr[6];
-#pragma unroll
-  for (int i = 0; i < 18; ++i) w18[i] = W[i];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) Li[i] = Lig[i];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) { zz[i] = zg[i]; s3[i] = sl[i]; }
-#pragma unroll
-  for (int i = 0; i < 6; ++i) spr[i] = sp[i];
-  double o[kVisitUY];  // Z = s_p W s_l L^-T (6x3) | U z = Z zz (6)
-#pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    const double u0 = spr[r] * w18[r * 3 + 0] * s3[0], u1 = spr[r] * w18[r * 3 + 1] * s3[1],
-                 u2 = spr[r] * w18[r * 3 + 2] * s3[2];
-    const double z0 = u0 * Li[0];
-    const double z1 = u0 * Li[3] + u1 * Li[4];
-    const double z2 = u0 * Li[6] + u1 * Li[7] + u2 * Li[8];
-    o[r * 3 + 0] = z0; o[r * 3 + 1] = z1; o[r * 3 + 2] = z2;
-    o[18 + r] = z0 * zz[0] + z1 * zz[1] + z2 * zz[2];
-  }
-#pragma unroll
-  for (int i = 0; i < kVisitUY / 2; ++i) out[i] = double2{o[2 * i], o[2 * i + 1]};
-}
-
 // Clears the structurally non-zero tiles of S (one workgroup per tile; padded diagonal = 1). Zero
 // tiles are never written by the factorisation and stay zero from the initial arena clear.
 __global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ Pp) {
@@ -382,7 +420,7 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
   const bool inGroup = g < kGroups;
   const int cb = P.pair_cbegin[k], pb = P.pair_runs[2 * k], ob = P.pair_runs[2 * k + 1], ce = P.pair_cbegin[k + 1];
   const auto pc = gmem(P.pair_contrib);
-  const auto vlin = gmem(P.visit_lin);
+  const auto vhg = gmem(P.visit_hg);
   const auto vuy = gmem(P.visit_UY);
   double H[6], Sc[6], uz = 0.0;
 #pragma unroll
@@ -399,7 +437,7 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
       const int k0 = st + g;
       const int a0 = __shfl(da, k0 & 63, 64), b0 = __shfl(db, k0 & 63, 64);
       const bool v0 = inGroup && k0 < nstep;
-      const auto H0 = vlin + (size_t)a0 * kVisitLin + 18;
+      const auto H0 = vhg + (size_t)a0 * kVisitHG;
       double h0[6];
 #pragma unroll
       for (int q = 0; q < 6; ++q) h0[q] = H0[sym6(r, q)];
@@ -607,12 +645,8 @@ __global__ __launch_bounds__(256) void k_gn_finalize(const DevProblem* __restric
 }
 
 // ------------------------------------------------------------------------------------ launchers
-void launch_visit_lin(const DevProblem& P, int lin_mode, hipStream_t s) {
-  if (P.n_visit > 0)
-    hipLaunchKernelGGL(k_visit_lin, dim3((P.n_visit + 255) / 256), dim3(256), 0, s, P.self, lin_mode);
-}
-void launch_visit_prep(const DevProblem& P, hipStream_t s) {
-  if (P.n_visit > 0) hipLaunchKernelGGL(k_visit_prep, dim3((P.n_visit + 255) / 256), dim3(256), 0, s, P.self);
+void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s) {
+  if (P.n_lmg > 0) hipLaunchKernelGGL(k_lm_visit, dim3(P.n_lmg), dim3(kLmGroupVisits), 0, s, P.self, mode);
 }
 void launch_assemble_pp(const DevProblem& P, hipStream_t s) {
   if (P.n_asm_pp > 0) hipLaunchKernelGGL(k_assemble_pp, dim3((P.n_asm_pp + 3) / 4), dim3(256), 0, s, P.self);
@@ -620,10 +654,7 @@ void launch_assemble_pp(const DevProblem& P, hipStream_t s) {
 void launch_assemble_sb(const DevProblem& P, hipStream_t s) {
   if (P.n_asm_sb > 0) hipLaunchKernelGGL(k_assemble_sb, dim3((P.n_asm_sb + 3) / 4), dim3(256), 0, s, P.self);
 }
-void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
-  launch_visit_lin(P, lin_mode, s);
-  if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_lin, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P.self, lin_mode);
-}
+void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s) { launch_lm_visit(P, lin_mode, s); }
 void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s) {
   if (P.n_fblock > 0) hipLaunchKernelGGL(k_fgrad, dim3(P.n_fblock), dim3(64), 0, s, P.self, lin_mode);
 }
@@ -635,10 +666,7 @@ void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t 
   launch_imu_hess(P, lin_mode, s);
   launch_fgrad(P, lin_mode, s);
 }
-void launch_lm_prep(const DevProblem& P, hipStream_t s) {
-  if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_prep, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P.self);
-  launch_visit_prep(P, s);
-}
+void launch_lm_prep(const DevProblem& P, hipStream_t s) { launch_lm_visit(P, 2, s); }
 void launch_zero_S(const DevProblem& P, hipStream_t s) {
   if (P.n_tiles > 0) hipLaunchKernelGGL(k_zero_S, dim3(P.n_tiles), dim3(256), 0, s, P.self);
 }

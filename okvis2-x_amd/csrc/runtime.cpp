@@ -66,7 +66,7 @@ struct HostBatch {
   std::vector<uint8_t> obs_flags;
   std::vector<double> obs_kp, obs_L;
   // visits
-  std::vector<int32_t> lm_visit_begin, visit_pose, visit_obs_begin, visit_lm;
+  std::vector<int32_t> lm_visit_begin, visit_pose, visit_obs_begin, visit_lm, lmg_begin;
   // imu
   std::vector<int32_t> imu_blocks, imu_win, imu_sbegin;
   std::vector<uint8_t> imu_flags;
@@ -507,6 +507,25 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
         if (B.tileNz[w][(size_t)i * T + j]) { B.tile_items.push_back(w); B.tile_items.push_back(i); B.tile_items.push_back(j); }
   }
   B.lm_visit_begin.push_back((int)B.visit_pose.size());
+  // landmark groups of k_lm_visit: consecutive whole landmarks, <= kLmGroupVisits visits and
+  // <= kLmGroupMax landmarks per group (one workgroup, one thread per visit)
+  {
+    const int nl = (int)B.lm_visit_begin.size() - 1;
+    int gl = 0;
+    B.lmg_begin.push_back(0);
+    for (int l = 0; l < nl; ++l) {
+      const int nv = B.lm_visit_begin[l + 1] - B.lm_visit_begin[l];
+      if (nv > kLmGroupVisits)
+        throw std::invalid_argument("landmark with more than " + std::to_string(kLmGroupVisits) + " observing poses");
+      const int gv = B.lm_visit_begin[l] - B.lm_visit_begin[B.lmg_begin.back()];
+      if (l > B.lmg_begin.back() && (gv + nv > kLmGroupVisits || gl == kLmGroupMax)) {
+        B.lmg_begin.push_back(l);
+        gl = 0;
+      }
+      ++gl;
+    }
+    if (nl > 0) B.lmg_begin.push_back(nl);
+  }
   B.visit_obs_begin.push_back((int)B.obs_win.size());
   B.imu_sbegin.push_back((int)B.imu_ts.size());
   B.fb_cbegin.push_back((int)B.fb_contrib.size());
@@ -632,10 +651,10 @@ struct okvisgpu_ctx {
     const size_t o_obs_cost0 = scratch(sizeof(double) * D.n_obs), o_obs_cost1 = scratch(sizeof(double) * D.n_obs);
     const size_t o_obs_jv = scratch(sizeof(double) * 3 * D.n_obs);
     const size_t o_lmvb = upl(B.lm_visit_begin), o_vpose = upl(B.visit_pose), o_vob = upl(B.visit_obs_begin),
-                 o_vlm = upl(B.visit_lm);
+                 o_vlm = upl(B.visit_lm), o_lmg_b = upl(B.lmg_begin);
     const size_t o_lmV = scratch(sizeof(double) * 6 * D.n_lm), o_lmg = scratch(sizeof(double) * 3 * D.n_lm),
                  o_lmVi = scratch(sizeof(double) * 9 * D.n_lm), o_lmz = scratch(sizeof(double) * 3 * D.n_lm);
-    const size_t o_vlin = scratch(sizeof(double) * kVisitLin * D.n_visit),
+    const size_t o_vhg = scratch(sizeof(double) * kVisitHG * D.n_visit),
                  o_vUY = scratch(sizeof(double) * kVisitUY * D.n_visit);
     const size_t o_imu_blocks = upl(B.imu_blocks), o_imu_win = upl(B.imu_win), o_imu_flags = upl(B.imu_flags),
                  o_imu_t0 = upl(B.imu_t0), o_imu_t1 = upl(B.imu_t1), o_imu_sb = upl(B.imu_sbegin),
@@ -702,7 +721,8 @@ struct okvisgpu_ctx {
     D.obs_cost[0] = dp(o_obs_cost0); D.obs_cost[1] = dp(o_obs_cost1); D.obs_jv = dp(o_obs_jv);
     D.lm_visit_begin = ip(o_lmvb); D.visit_pose = ip(o_vpose); D.visit_obs_begin = ip(o_vob); D.visit_lm = ip(o_vlm);
     D.lm_V = dp(o_lmV); D.lm_g = dp(o_lmg); D.lm_Linv = dp(o_lmVi); D.lm_zz = dp(o_lmz);
-    D.visit_lin = dp(o_vlin); D.visit_UY = dp(o_vUY);
+    D.visit_hg = dp(o_vhg); D.visit_UY = dp(o_vUY);
+    D.lmg_begin = ip(o_lmg_b); D.n_lmg = B.lmg_begin.empty() ? 0 : (int)B.lmg_begin.size() - 1;
     D.imu_blocks = ip(o_imu_blocks); D.imu_win = ip(o_imu_win); D.imu_flags = up(o_imu_flags);
     D.imu_t0 = lp(o_imu_t0); D.imu_t1 = lp(o_imu_t1); D.imu_sbegin = ip(o_imu_sb); D.imu_ts = lp(o_imu_ts);
     D.imu_ga = dp(o_imu_ga); D.imu_par = dp(o_imu_par); D.imu_state = dp(o_imu_state);
@@ -799,6 +819,7 @@ struct okvisgpu_ctx {
       x.radius = P.opt.initial_radius;
       x.mu = mu;
       x.need_gn = 1;
+      x.z_mu = -1.0;
       x.termination = OKVISGPU_NO_CONVERGENCE;
     }
     HIPCHK(hipMemcpyAsync(P.st, s.data(), sizeof(WinState) * s.size(), hipMemcpyHostToDevice, stream));
@@ -1204,10 +1225,10 @@ int okvisgpu_profile_iteration(okvisgpu_ctx* c, double* ms) {
 // ---- per-kernel timing with algorithmic work models (bench.py's roofline) ------------------
 namespace {
 enum KernelId {
-  K_ASSEMBLE_PP, K_ASSEMBLE_SB, K_CHOLESKY, K_VISIT_LIN, K_VISIT_PREP, K_EVAL_IMU, K_EVAL_OBS, K_JV,
+  K_ASSEMBLE_PP, K_ASSEMBLE_SB, K_CHOLESKY, K_LM_VISIT, K_LM_VISIT_PREP, K_EVAL_IMU, K_EVAL_OBS, K_JV,
   K_FGRAD, K_COUNT
 };
-const char* kKernelNames[K_COUNT] = {"k_assemble_pp", "k_assemble_sb", "k_cholesky", "k_visit_lin", "k_visit_prep",
+const char* kKernelNames[K_COUNT] = {"k_assemble_pp", "k_assemble_sb", "k_cholesky", "k_lm_visit", "k_lm_visit_prep",
                                      "k_eval_imu",    "k_eval_obs",    "k_jv",       "k_fgrad"};
 // bound: 0 = HBM bytes, 1 = FP64 matrix-core FLOPs
 const int kKernelBound[K_COUNT] = {0, 0, 1, 0, 0, 0, 0, 0, 0};
@@ -1240,8 +1261,10 @@ double kernelWork(const HostBatch& B, const DevProblem& P, int k) {
       const double panels = (double)(B.chol_panel_items.size() / 2), upd = (double)B.n_band_updates;
       return diag * (2.0 * tile3 / 3.0 + 4.0 * 64 * 64) + panels * (2.0 * tile3 + 4.0 * 64 * 64) + upd * 2.0 * tile3;
     }
-    case K_VISIT_LIN: return nObs * (kObsLin * d8 + 1) + nVis * (kVisitLin * d8 + 7 * d8 + 16);
-    case K_VISIT_PREP: return nVis * (18 * d8 + kVisitUY * d8 + 12) + nLm * 15 * d8;
+    case K_LM_VISIT:  // obs linearisation + params in; H|g and Z|Uz per visit, landmark blocks out
+      return nObs * (kObsLin * d8 + 1) + nVis * (kVisitHG * d8 + kVisitUY * d8 + 7 * d8 + 16) + nLm * 40 * d8;
+    case K_LM_VISIT_PREP:  // W recomputed from the obs linearisation; Z|Uz out
+      return nObs * (kObsLin * d8 + 1) + nVis * (kVisitUY * d8 + 7 * d8 + 16) + nLm * 34 * d8;
     case K_EVAL_IMU: return nImu * (2.0 * kImuState + kImuLin + 2 * 16) * d8 + (double)B.imu_ts.size() * 7 * d8;
     case K_EVAL_OBS: return nObs * (16 + 32 + 13 + kObsLin * d8 + 8) + nLm * 4 * d8 + (double)B.pose_f.size() * 7 * d8;
     case K_JV: return nObs * (kObsLin * d8 + 1) + nVis * (7 + 4 + 3 * 9 + 3) * d8 + nImu * (kImuLin + 3) * d8;
@@ -1268,6 +1291,7 @@ int okvisgpu_time_kernel(okvisgpu_ctx* c, int32_t kernel, int32_t reps, double* 
     std::vector<WinState> st = c->readStates();
     for (WinState& w : st) {
       w.done = 0; w.need_gn = 1; w.gn_failed = 0; w.eval_cand = 1; w.accepted = 1; w.step_valid = 2;
+      w.z_mu = -1.0;  // stale: the prep mode recomputes Z
     }
     HIPCHK(hipMemcpyAsync(P.st, st.data(), sizeof(WinState) * st.size(), hipMemcpyHostToDevice, s));
     std::vector<hipEvent_t> ev;
@@ -1292,8 +1316,8 @@ int okvisgpu_time_kernel(okvisgpu_ctx* c, int32_t kernel, int32_t reps, double* 
       switch (kernel) {
         case K_ASSEMBLE_PP: timed([&] { launch_assemble_pp(P, s); }); break;
         case K_ASSEMBLE_SB: timed([&] { launch_assemble_sb(P, s); }); break;
-        case K_VISIT_LIN: timed([&] { launch_visit_lin(P, 1, s); }); break;
-        case K_VISIT_PREP: timed([&] { launch_visit_prep(P, s); }); break;
+        case K_LM_VISIT: timed([&] { launch_lm_visit(P, 1, s); }); break;
+        case K_LM_VISIT_PREP: timed([&] { launch_lm_visit(P, 2, s); }); break;
         case K_EVAL_IMU:
           // redo counter := 0 forces the re-preintegration the candidate evaluations of a solve
           // mostly perform (the device-side IMU state is scratch afterwards)
