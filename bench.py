@@ -63,9 +63,6 @@ def ate(P, gt):
     return float(np.sqrt(np.mean(np.sum((aligned - b) ** 2, axis=1))))
 
 
-# kernels timed for the roofline table (include/okvisgpu.h okvisgpu_time_kernel)
-ROOFLINE_KERNELS = ["k_assemble_pp", "k_assemble_sb", "k_cholesky", "k_visit_lin", "k_visit_prep", "k_eval_imu",
-                    "k_eval_obs", "k_jv", "k_fgrad"]
 PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
 
@@ -92,7 +89,7 @@ def roofline_table(ctx, reps):
     """Per-kernel device time (HIP events on the context's stream, `reps` back-to-back launches of
     one iteration's worth on the resident data) and achieved rate of its algorithmic work."""
     table = {}
-    for name in ROOFLINE_KERNELS:
+    for name in og.kernel_names():  # every kernel okvisgpu_time_kernel exposes
         ms, work, bound = ctx.time_kernel(name, reps)
         rate = work / (ms * 1e-3) / (1e9 if bound == "hbm" else 1e12) if ms > 0 else 0.0
         peak = HBM_PEAK_GBS if bound == "hbm" else FP64_MFMA_PEAK_TFLOPS

@@ -20,8 +20,8 @@ for k, d in vals.items():
     f = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"]) * 1024 * 2
     w = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"]) * 1024
     kern[k] = {"fetch_bytes_per_dispatch": f, "write_bytes_per_dispatch": w, "bytes_per_dispatch": f + w}
-    if k in ("k_assemble_pp", "k_assemble_sb", "k_visit_lin", "k_visit_prep", "k_eval_imu", "k_eval_obs", "k_fgrad",
-             "k_cholesky", "k_lm_prep", "k_lm_backsub", "k_zero_S"):
+    if k in ("k_assemble_pp", "k_assemble_sb", "k_eval_imu", "k_eval_obs", "k_fgrad", "k_cholesky", "k_lm_backsub",
+             "k_zero_S"):
         kern[k]["bytes_per_iteration"] = f + w  # one dispatch per iteration
 json.dump({"source": sys.argv[2:], "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane calibration), KiB -> bytes",
            "kernels": kern}, open(out, "w"), indent=1, sort_keys=True)
