@@ -47,7 +47,14 @@ def bench_options(max_iter):
 
 
 def make_windows(cfg, indices):
-    return [og.SynthWindow(cfg["n_kf"], cfg["n_lm"], cfg["n_obs"], seed=SEED0 + i) for i in indices]
+    """Synthetic windows, generated on host threads (the C generator runs outside the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+    indices = list(indices)
+    mk = lambda i: og.SynthWindow(cfg["n_kf"], cfg["n_lm"], cfg["n_obs"], seed=SEED0 + i)  # noqa: E731
+    if len(indices) < 16:
+        return [mk(i) for i in indices]
+    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4)) as ex:
+        return list(ex.map(mk, indices))
 
 
 def ate(P, gt):
@@ -135,7 +142,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--windows", type=int, default=512, help="total windows in the job (strong scaling)")
+    ap.add_argument("--windows", type=int, default=2048, help="total windows in the job (strong scaling)")
     ap.add_argument("--config", default="s50", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-threads", type=int, default=3, help="realtime_num_threads (okvis2.yaml:93)")
     ap.add_argument("--cpu-iters", type=int, default=None, help="default: warmup + steps")
