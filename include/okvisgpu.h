@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OKVISGPU_ABI_VERSION 1
+#define OKVISGPU_ABI_VERSION 2
 
 /* ---------------------------------------------------------------- status codes */
 typedef enum okvisgpu_status {
@@ -138,6 +138,17 @@ typedef struct okvisgpu_problem {
   const int32_t* sb_prior_block;
   const double* sb_prior_meas;      /* [n][9]                                                   */
   const double* sb_prior_sqrt_info; /* [n][81] row-major                                        */
+
+  /* --- TwoPoseStandardGraphError / TwoPoseStandardGraphErrorConst residual blocks: relative-pose
+   * (pose-graph) edges that marginalisation leaves between two keyframes of the window
+   * (TwoPoseGraphError.cpp:467-606 and :631-767; added without a loss function at
+   * ViGraphEstimator.cpp:770). Parameter order (reference pose, other pose). The edge is the output
+   * of TwoPoseStandardGraphError::compute (okvisgpu_twopose_compute below). */
+  int32_t n_relpose;
+  const int32_t* relpose_blocks;    /* [n][2] reference pose, other pose                        */
+  const double* relpose_delta_x;    /* [n][6] DeltaX_                                           */
+  const double* relpose_sqrt_info;  /* [n][36] J_ row-major (information = J_^T J_)             */
+  const double* relpose_lin_point;  /* [n][7] linearisationPoint_T_S0S1_                        */
 } okvisgpu_problem;
 
 /* ---------------------------------------------------------------- solver options / summary */
@@ -241,6 +252,39 @@ const char* okvisgpu_kernel_name(int32_t kernel);
 int okvisgpu_time_kernel(okvisgpu_ctx* ctx, int32_t kernel, int32_t reps, double* avg_ms, double* work,
                          int32_t* bound);
 
+/* ---------------------------------------------------------------- pose-graph edges
+ * TwoPoseStandardGraphError::compute (TwoPoseGraphError.cpp:162-397) for a batch of edges on the
+ * GPU: the reprojection observations of the landmarks shared by a reference keyframe S0 and another
+ * keyframe S1 are linearised in S0 coordinates (Cauchy-corrected, |r| > 3 outliers dropped), every
+ * landmark is marginalised with the pseudo-inverse square root of its 3x3 block (dropped when
+ * rank < 3 and its depth in S0 < 2.99), and the 6x6 relative system H00_, b0_ is decomposed into
+ * J_ = D^(1/2) E^T and DeltaX_ = -H^+ b0_ (eigenvalues <= 1e-8*6*max treated as zero, ascending
+ * order as Eigen::SelfAdjointEigenSolver). Inputs are the values TwoPoseGraphError::addObservation
+ * recorded: landmarks and the other pose as added, the reference pose as its current estimate.
+ * The edges of one call share the camera rig (stayConst_ = true, do_extrinsics: false). */
+typedef struct okvisgpu_twopose_edges {
+  int32_t n_edges;
+  const double* ref_pose;           /* [n_edges][7] T_WS0                                        */
+  const double* other_pose;         /* [n_edges][7] T_WS1                                        */
+  int32_t n_cameras;
+  const okvisgpu_camera* cameras;   /* [n_cameras]                                               */
+  const double* extrinsics;         /* [n_cameras][7] T_SC                                       */
+  const int32_t* landmark_begin;    /* [n_edges+1] CSR: landmarks of edge e (observations_ map order) */
+  const double* landmarks;          /* [n_landmarks][4] hp_W                                     */
+  const int32_t* obs_begin;         /* [n_landmarks+1] CSR: observations of landmark l           */
+  const uint8_t* obs_other;         /* [n_obs] 0 = seen from the reference pose, 1 = from the other */
+  const int32_t* obs_camera;        /* [n_obs]                                                   */
+  const double* obs_keypoint;       /* [n_obs][2]                                                */
+  const double* obs_sqrt_info;      /* [n_obs][4] (ReprojectionError::setInformation; weight applied) */
+  const uint8_t* obs_cauchy;        /* [n_obs] 1 = CauchyLoss(1) (may be NULL = all)             */
+} okvisgpu_twopose_edges;
+
+/* Outputs per edge (host, caller-owned): delta_x [6], sqrt_info (J_) [36], lin_point [7];
+ * H00 [36] and b0 [6] (the marginalised relative system, may be NULL). Uses the context's device and
+ * stream; independent of the problem set with okvisgpu_set_problems. */
+int okvisgpu_twopose_compute(okvisgpu_ctx* ctx, const okvisgpu_twopose_edges* edges, double* delta_x,
+                             double* sqrt_info, double* lin_point, double* H00, double* b0);
+
 /* Copy device parameter values back into the caller's host arrays without solving. */
 int okvisgpu_get_params(okvisgpu_ctx* ctx);
 
@@ -269,6 +313,8 @@ int okvisgpu_linearize_reduce(okvisgpu_ctx* ctx, int32_t window, int32_t jacobi_
 int okvisgpu_eval_reprojection(okvisgpu_ctx* ctx, int32_t window, double* r, double* J_pose,
                                double* J_landmark);
 int okvisgpu_eval_imu(okvisgpu_ctx* ctx, int32_t window, int32_t redo_always, double* r, double* J);
+/*   relative pose: r [n_relpose][6], J [n_relpose][6][12] minimal (reference pose 6, other pose 6) */
+int okvisgpu_eval_relpose(okvisgpu_ctx* ctx, int32_t window, double* r, double* J);
 
 /* ---------------------------------------------------------------- synthetic windows
  * Host-side generator of the synthetic sliding windows the benchmark is quoted on:
@@ -287,6 +333,12 @@ typedef struct okvisgpu_synth_config {
   double pixel_noise;               /* 1.0 */
   double init_sigma_pos, init_sigma_rot, init_sigma_lm, init_sigma_vel; /* 0.05 0.01 0.05 0.02 */
   uint64_t seed;
+  /* pose-graph edges (TwoPoseStandardGraphErrorConst) from keyframe i to i + relpose_stride,
+   * i = 0, 1, ...: information from sigmas 0.02 m / 0.005 rad (random rotation of the frame),
+   * linearisation point = the ground-truth relative pose perturbed at that noise, DeltaX_ small.
+   * 0 (default) = none, as in the benchmark windows. */
+  int32_t n_relpose;
+  int32_t relpose_stride;
 } okvisgpu_synth_config;
 
 typedef struct okvisgpu_synth_window okvisgpu_synth_window;  /* owns all arrays of one problem */

@@ -36,8 +36,10 @@ enum ContribType : int32_t {
   C_PAIR = 1,       // a = visit i, b = visit j (same landmark): - W_i V^-1 W_j^T
   C_IMU = 2,        // a = factor, b = column offset of row block, c = column offset of col block
   C_PPRIOR = 3,     // a = pose prior
-  C_SBPRIOR = 4     // a = sb prior
+  C_SBPRIOR = 4,    // a = sb prior
+  C_RELPOSE = 5     // a = relative-pose edge, b / c = column offset (0 reference, 6 other) of row / col block
 };
+constexpr int kRelPoseLin = 6 + 6 * 12;  // per relative-pose edge: r[6] | J minimal 6x12 (reference 6 | other 6)
 
 struct Contrib {
   int32_t type, a, b, c;
@@ -156,6 +158,18 @@ struct DevProblem {
   double* sbp_cost[2];
   double* sbp_jv;
 
+  // --- relative-pose (pose-graph) edges, TwoPoseStandardGraphError(Const)
+  int32_t n_relpose;
+  const int32_t* rp_blocks;        // [n][2] global reference pose, other pose
+  const int32_t* rp_win;
+  const uint8_t* rp_flags;         // bit1 fixed (both poses constant)
+  const double* rp_dx;             // [n][6]  DeltaX_
+  const double* rp_J;              // [n][36] J_
+  const double* rp_lp;             // [n][7]  linearisationPoint_T_S0S1_
+  double* rp_lin[2];               // [n][kRelPoseLin]
+  double* rp_cost[2];
+  double* rp_jv;                   // [3][n]
+
   // --- reduced system structure
   const int32_t* win_foff;         // [n_win]
   const int32_t* win_fdim;
@@ -168,6 +182,7 @@ struct DevProblem {
   const int32_t* win_imu_range;
   const int32_t* win_pp_range;
   const int32_t* win_sbp_range;
+  const int32_t* win_rp_range;
   const int32_t* fb_win;           // [n_fblock] window
   const int32_t* fb_kind;          // 0 pose / 1 sb
   const int32_t* fb_index;         // global pose / sb index
@@ -220,6 +235,26 @@ struct DevProblem {
 
   WinState* st;                    // [n_win]
   DevOptions opt;
+};
+
+// Batch of TwoPoseStandardGraphError::compute inputs (okvisgpu_twopose_edges on device) and the
+// per-edge output record: DeltaX_ [6] | J_ [36] | linearisation point [7] | H00_ [36] | b0_ [6].
+constexpr int kTwoPoseOut = 6 + 36 + 7 + 36 + 6;
+struct TwoPoseDev {
+  int32_t n_edges, n_cam;
+  const double* ref_pose;     // [n_edges][7]
+  const double* other_pose;   // [n_edges][7]
+  const double* cam;          // [n_cam][9] as DevProblem::cam
+  const double* extr;         // [n_cam][7]
+  const int32_t* lm_begin;    // [n_edges+1]
+  const double* lm;           // [n_lm][4]
+  const int32_t* obs_begin;   // [n_lm+1]
+  const uint8_t* obs_other;   // [n_obs]
+  const int32_t* obs_cam;
+  const double* obs_kp;       // [n_obs][2]
+  const double* obs_L;        // [n_obs][4]
+  const uint8_t* obs_cauchy;  // [n_obs]
+  double* out;                // [n_edges][kTwoPoseOut]
 };
 
 }  // namespace okg

@@ -205,6 +205,35 @@ __global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp) {
       }
     }
     for (int k = 0; k < 3; ++k) P.sbp_jv[(size_t)k * P.n_sbprior + i] = a[k];
+    return;
+  }
+  u -= P.n_sbprior;
+  if (u < P.n_relpose) {
+    const int i = u;
+    const int w = P.rp_win[i];
+    if (!jvSelect(P, w)) return;
+    double a[3] = {0.0, 0.0, 0.0};
+    if (!(P.rp_flags[i] & 2)) {
+      const double* L = P.rp_lin[P.st[w].lcur] + kRelPoseLin * (size_t)i;
+      const size_t foff = P.win_foff[w];
+      const int offs[2] = {P.pose_f[P.rp_blocks[2 * i]], P.pose_f[P.rp_blocks[2 * i + 1]]};
+      double vc[12], vg[12];
+      for (int q = 0; q < 2; ++q)
+        for (int c = 0; c < 6; ++c) {
+          const size_t j = foff + offs[q] + c;
+          vc[6 * q + c] = offs[q] >= 0 ? P.sF[j] * cF[j] : 0.0;
+          vg[6 * q + c] = offs[q] >= 0 ? -P.sF[j] * yF[j] : 0.0;
+        }
+      for (int r = 0; r < 6; ++r) {
+        double jc = 0.0, jg = 0.0;
+        for (int c = 0; c < 12; ++c) {
+          jc += L[6 + r * 12 + c] * vc[c];
+          jg += L[6 + r * 12 + c] * vg[c];
+        }
+        jvAcc(jc, jg, a);
+      }
+    }
+    for (int k = 0; k < 3; ++k) P.rp_jv[(size_t)k * P.n_relpose + i] = a[k];
   }
 }
 
@@ -235,6 +264,7 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
   const int ib = P.win_imu_range[2 * w], ie = P.win_imu_range[2 * w + 1];
   const int pb = P.win_pp_range[2 * w], pe = P.win_pp_range[2 * w + 1];
   const int sbb = P.win_sbp_range[2 * w], sbe = P.win_sbp_range[2 * w + 1];
+  const int rpb = P.win_rp_range[2 * w], rpe = P.win_rp_range[2 * w + 1];
 
   if (mode == R_COST_INIT || mode == R_COST_CAND) {
     if (mode == R_COST_CAND && !s.eval_cand) return;
@@ -255,6 +285,10 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
     for (int i = sbb + t; i < sbe; i += kRB) {
       if (P.sb_f[P.sbp_block[i]] < 0) cf += P.sbp_cost[lb][i];
       else c += P.sbp_cost[lb][i];
+    }
+    for (int i = rpb + t; i < rpe; i += kRB) {
+      if (P.rp_flags[i] & 2) cf += P.rp_cost[lb][i];
+      else c += P.rp_cost[lb][i];
     }
     c = blockSum(c, sh);
     cf = blockSum(cf, sh);
@@ -322,6 +356,7 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
     for (int f = ib + t; f < ie; f += kRB) acc += P.imu_jv[(size_t)k * P.n_imu + f];
     for (int i = pb + t; i < pe; i += kRB) acc += P.pp_jv[(size_t)k * P.n_pprior + i];
     for (int i = sbb + t; i < sbe; i += kRB) acc += P.sbp_jv[(size_t)k * P.n_sbprior + i];
+    for (int i = rpb + t; i < rpe; i += kRB) acc += P.rp_jv[(size_t)k * P.n_relpose + i];
     a[k] = blockSum(acc, sh);
   }
   // |gradient_|^2 over the window (f-vector + free landmarks)
@@ -592,7 +627,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
 }
 
 void launch_jv(const DevProblem& P, hipStream_t s) {
-  const int n = P.n_visit + P.n_imu + P.n_pprior + P.n_sbprior;
+  const int n = P.n_visit + P.n_imu + P.n_pprior + P.n_sbprior + P.n_relpose;
   if (n > 0) hipLaunchKernelGGL(k_jv, dim3((n + 255) / 256), dim3(256), 0, s, P.self);
 }
 void launch_reduce(const DevProblem& P, int mode, hipStream_t s) {

@@ -783,26 +783,87 @@ __global__ __launch_bounds__(64) void k_eval_priors(const DevProblem* __restrict
     return;
   }
   const int i = t - P.n_pprior;
-  if (i >= P.n_sbprior) return;
-  const int w = P.sbp_win[i];
+  if (i < P.n_sbprior) {
+    const int w = P.sbp_win[i];
+    int xs, lb;
+    if (!evalSelect(P, w, mode, xs, lb)) return;
+    if (P.sb_f[P.sbp_block[i]] < 0 && mode != 2) return;
+    const double* sbv = P.sb[xs] + 9 * (size_t)P.sbp_block[i];
+    const double* m = P.sbp_meas + 9 * (size_t)i;
+    const double* L = P.sbp_L + 81 * (size_t)i;
+    double* lin = P.sbp_lin[lb] + 90 * (size_t)i;
+    double e[9];
+    for (int k = 0; k < 9; ++k) e[k] = m[k] - sbv[k];
+    double c = 0;
+    for (int r = 0; r < 9; ++r) {
+      double s = 0;
+      for (int k = 0; k < 9; ++k) s += L[r * 9 + k] * e[k];
+      lin[r] = s;
+      c += s * s;
+      for (int k = 0; k < 9; ++k) lin[9 + r * 9 + k] = -L[r * 9 + k];
+    }
+    P.sbp_cost[lb][i] = 0.5 * c;
+    return;
+  }
+  // ---- relative-pose edge, TwoPoseStandardGraphError(Const)::EvaluateWithMinimalJacobians
+  // (TwoPoseGraphError.cpp:467-606 / :631-767), no loss function (ViGraphEstimator.cpp:770)
+  const int k = i - P.n_sbprior;
+  if (k >= P.n_relpose) return;
+  const int w = P.rp_win[k];
   int xs, lb;
   if (!evalSelect(P, w, mode, xs, lb)) return;
-  if (P.sb_f[P.sbp_block[i]] < 0 && mode != 2) return;
-  const double* sbv = P.sb[xs] + 9 * (size_t)P.sbp_block[i];
-  const double* m = P.sbp_meas + 9 * (size_t)i;
-  const double* L = P.sbp_L + 81 * (size_t)i;
-  double* lin = P.sbp_lin[lb] + 90 * (size_t)i;
-  double e[9];
-  for (int k = 0; k < 9; ++k) e[k] = m[k] - sbv[k];
-  double c = 0;
-  for (int r = 0; r < 9; ++r) {
-    double s = 0;
-    for (int k = 0; k < 9; ++k) s += L[r * 9 + k] * e[k];
+  if ((P.rp_flags[k] & 2) && mode < 2) return;  // both poses constant: fixed_cost only
+  const double* p0 = P.pose[xs] + 7 * (size_t)P.rp_blocks[2 * k];
+  const double* p1 = P.pose[xs] + 7 * (size_t)P.rp_blocks[2 * k + 1];
+  const double* dx = P.rp_dx + 6 * (size_t)k;
+  const double* Jq = P.rp_J + 36 * (size_t)k;
+  const double* lp = P.rp_lp + 7 * (size_t)k;
+  const Q q0 = qnormalize(Q{p0[3], p0[4], p0[5], p0[6]}), q1 = qnormalize(Q{p1[3], p1[4], p1[5], p1[6]});
+  const Q qlinv = qinv(qnormalize(Q{lp[3], lp[4], lp[5], lp[6]}));
+  double C0[9];
+  qrot(q0, C0);  // C_WS0; C_S0W = C0^T
+  const double d01[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
+  double rS[3];
+  mtv3(C0, d01, rS);  // T_S0Si.r
+  const Q q0inv = qinv(q0);
+  const Q dq = qmul(qnormalize(qmul(q0inv, q1)), qlinv);  // T_S0Si.q * q_lin^-1
+  const double err[6] = {dx[0] + rS[0] - lp[0], dx[1] + rS[1] - lp[1], dx[2] + rS[2] - lp[2],
+                         dx[3] + 2.0 * dq.x, dx[4] + 2.0 * dq.y, dx[5] + 2.0 * dq.z};
+  double* lin = P.rp_lin[lb] + kRelPoseLin * (size_t)k;
+  double c = 0.0;
+  for (int r = 0; r < 6; ++r) {
+    double s = 0.0;
+    for (int q = 0; q < 6; ++q) s += Jq[r * 6 + q] * err[q];
     lin[r] = s;
     c += s * s;
-    for (int k = 0; k < 9; ++k) lin[9 + r * 9 + k] = -L[r * 9 + k];
   }
-  P.sbp_cost[lb][i] = 0.5 * c;
+  // Jerr = [C_S0W 0; 0 B], B = (plus(q_WS0^-1) oplus(q_WS q_lin^-1))_3x3;
+  // JerrRef = [-C_S0W, C_S0W [r_WS - r_WS0]x; 0, -B]
+  double Pm[16], Om[16], B[9];
+  qplusM(q0inv, Pm);
+  qoplusM(qmul(q1, qlinv), Om);
+  for (int r = 0; r < 3; ++r)
+    for (int q = 0; q < 3; ++q)
+      B[r * 3 + q] = Pm[r * 4 + 0] * Om[0 * 4 + q] + Pm[r * 4 + 1] * Om[1 * 4 + q] + Pm[r * 4 + 2] * Om[2 * 4 + q] +
+                     Pm[r * 4 + 3] * Om[3 * 4 + q];
+  double X[9], CX[9];
+  crossMx(d01, X);
+  for (int r = 0; r < 3; ++r)  // C_S0W X = C0^T X
+    for (int q = 0; q < 3; ++q) CX[r * 3 + q] = C0[0 * 3 + r] * X[0 * 3 + q] + C0[1 * 3 + r] * X[1 * 3 + q] + C0[2 * 3 + r] * X[2 * 3 + q];
+  for (int r = 0; r < 6; ++r) {
+    const double* Jr = Jq + r * 6;
+    double* Lr = lin + 6 + r * 12;
+    for (int q = 0; q < 3; ++q) {
+      const double jt = Jr[0] * C0[q * 3 + 0] + Jr[1] * C0[q * 3 + 1] + Jr[2] * C0[q * 3 + 2];  // (J C0^T)_q
+      const double jb = Jr[3] * B[0 * 3 + q] + Jr[4] * B[1 * 3 + q] + Jr[5] * B[2 * 3 + q];
+      const double jx = Jr[0] * CX[0 * 3 + q] + Jr[1] * CX[1 * 3 + q] + Jr[2] * CX[2 * 3 + q];
+      Lr[q] = -jt;          // reference pose, translation
+      Lr[3 + q] = jx - jb;  // reference pose, rotation
+      Lr[6 + q] = jt;       // other pose, translation
+      Lr[9 + q] = jb;       // other pose, rotation
+    }
+  }
+  P.rp_cost[lb][k] = 0.5 * c;
 }
 
 // ------------------------------------------------------------------------------------ launchers
@@ -813,7 +874,7 @@ void launch_eval_imu(const DevProblem& P, int mode, hipStream_t s) {
   if (P.n_imu > 0) hipLaunchKernelGGL(k_eval_imu, dim3((P.n_imu + kImuPerWG - 1) / kImuPerWG), dim3(64), 0, s, P.self, mode);
 }
 void launch_eval_priors(const DevProblem& P, int mode, hipStream_t s) {
-  const int np = P.n_pprior + P.n_sbprior;
+  const int np = P.n_pprior + P.n_sbprior + P.n_relpose;
   if (np > 0) hipLaunchKernelGGL(k_eval_priors, dim3((np + 63) / 64), dim3(64), 0, s, P.self, mode);
 }
 void launch_eval(const DevProblem& P, int mode, hipStream_t s) {

@@ -346,6 +346,18 @@ __global__ __launch_bounds__(64) void k_fgrad(const DevProblem* __restrict__ Pp,
         g[c] += sg;
         hd[c] += sh;
       }
+    } else if (cb.type == C_RELPOSE) {
+      const double* L = P.rp_lin[lb] + kRelPoseLin * (size_t)cb.a;
+      for (int c = 0; c < 6; ++c) {
+        double sg = 0, sh = 0;
+        for (int k2 = 0; k2 < 6; ++k2) {
+          const double j = L[6 + k2 * 12 + cb.b + c];
+          sg += j * L[k2];
+          sh += j * j;
+        }
+        g[c] += sg;
+        hd[c] += sh;
+      }
     } else if (cb.type == C_SBPRIOR) {
       const double* L = P.sbp_lin[lb] + 90 * (size_t)cb.a;
       for (int c = 0; c < 9; ++c) {
@@ -471,7 +483,7 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
       }
     }
   }
-  // factor blocks (IMU, pose prior): row r of J_i^T J_j
+  // factor blocks (IMU, relative pose, pose prior): row r of J_i^T J_j
   const int lb = P.st[w].lcur;
   for (int c = ob + g0; c < ce; c += kGroups) {
     const Contrib C = pc[c];
@@ -479,7 +491,14 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
       const auto Hf = gmem(P.imu_H + (size_t)C.a * kImuHess);
 #pragma unroll
       for (int q = 0; q < 6; ++q) H[q] += Hf[sym30(C.b + r, C.c + q)];
-    } else {
+    } else if (C.type == C_RELPOSE) {
+      const double* L = P.rp_lin[lb] + kRelPoseLin * (size_t)C.a + 6;
+      for (int k2 = 0; k2 < 6; ++k2) {
+        const double jr = L[k2 * 12 + C.b + r];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) H[q] += jr * L[k2 * 12 + C.c + q];
+      }
+    } else {  // C_PPRIOR
       const double* L = P.pp_lin[lb] + 42 * (size_t)C.a + 6;
       for (int k2 = 0; k2 < 6; ++k2) {
         const double jr = L[k2 * 6 + r];

@@ -42,4 +42,7 @@ void launch_jv(const DevProblem& P, hipStream_t s);
 void launch_gradnorm(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_dogleg(const DevProblem& P, hipStream_t s);
 
+// pose-graph edges (kernels_twopose.hip): TwoPoseStandardGraphError::compute, one wavefront per edge
+void launch_twopose_compute(const TwoPoseDev& T, hipStream_t s);
+
 }  // namespace okg

@@ -230,4 +230,88 @@ OKG_HD void obsJacobians(const double A[6], const double p[3], double w, double 
   }
 }
 
+// ReprojectionError<G>::EvaluateWithMinimalJacobians in the factored form
+// (implementation/ReprojectionError.hpp:71-220): weighted residual r = L (meas - kp) (no loss) and
+// A = L Jh C_CS C_SW (2x3), so that J_pose = [w A, -A [p]x] and J_landmark = -A (obsJacobians)
+// with p = hp.xyz - t_WS w returned in p.
+OKG_HD void reprojectA(const Cam& cam, const double* pose, const double* hp, const double* ex, const double* L,
+                       const double* meas, double r[2], double A[6], double p[3]) {
+  double C_WS[9], C_SC[9];
+  qrot(qnormalize(Q{pose[3], pose[4], pose[5], pose[6]}), C_WS);
+  qrot(qnormalize(Q{ex[3], ex[4], ex[5], ex[6]}), C_SC);
+  const double w4 = hp[3];
+  p[0] = hp[0] - pose[0] * w4;
+  p[1] = hp[1] - pose[1] * w4;
+  p[2] = hp[2] - pose[2] * w4;
+  double hS[3];
+  mtv3(C_WS, p, hS);
+  const double q3[3] = {hS[0] - ex[0] * w4, hS[1] - ex[1] * w4, hS[2] - ex[2] * w4};
+  double hC[3];
+  mtv3(C_SC, q3, hC);
+  double kp[2], Jh[6];
+  projectHomogeneous(cam, hC[0], hC[1], hC[2], w4, kp, Jh, true);
+  const double e0 = meas[0] - kp[0], e1 = meas[1] - kp[1];
+  r[0] = L[0] * e0 + L[1] * e1;
+  r[1] = L[2] * e0 + L[3] * e1;
+  double Jw[6], B[6];
+  for (int c = 0; c < 3; ++c) {
+    Jw[c] = L[0] * Jh[c] + L[1] * Jh[3 + c];
+    Jw[3 + c] = L[2] * Jh[c] + L[3] * Jh[3 + c];
+  }
+  for (int rr = 0; rr < 2; ++rr)
+    for (int k = 0; k < 3; ++k)
+      B[rr * 3 + k] = Jw[rr * 3 + 0] * C_SC[k * 3 + 0] + Jw[rr * 3 + 1] * C_SC[k * 3 + 1] + Jw[rr * 3 + 2] * C_SC[k * 3 + 2];
+  for (int rr = 0; rr < 2; ++rr)
+    for (int c = 0; c < 3; ++c)
+      A[rr * 3 + c] = B[rr * 3 + 0] * C_WS[c * 3 + 0] + B[rr * 3 + 1] * C_WS[c * 3 + 1] + B[rr * 3 + 2] * C_WS[c * 3 + 2];
+}
+
+// Symmetric eigen-decomposition A = V diag(lam) V^T by cyclic Jacobi (Eigen's
+// SelfAdjointEigenSolver restated; eigenvalues ascending, eigenvector signs arbitrary). A is
+// destroyed. N <= 6, one thread.
+template <int N>
+OKG_HD void jacobiEigenSym(double* A, double lam[N], double V[N * N]) {
+  for (int i = 0; i < N * N; ++i) V[i] = (i % (N + 1)) == 0 ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 32; ++sweep) {
+    double off = 0.0, dg = 0.0;
+    for (int i = 0; i < N; ++i) {
+      dg += A[i * N + i] * A[i * N + i];
+      for (int j = i + 1; j < N; ++j) off += A[i * N + j] * A[i * N + j];
+    }
+    if (off <= 1e-36 * dg || off == 0.0) break;
+    for (int p = 0; p < N - 1; ++p)
+      for (int q = p + 1; q < N; ++q) {
+        const double apq = A[p * N + q];
+        if (apq == 0.0) continue;
+        const double theta = (A[q * N + q] - A[p * N + p]) / (2.0 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+        const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+        for (int k = 0; k < N; ++k) {
+          const double akp = A[k * N + p], akq = A[k * N + q];
+          A[k * N + p] = c * akp - s * akq;
+          A[k * N + q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < N; ++k) {
+          const double apk = A[p * N + k], aqk = A[q * N + k];
+          A[p * N + k] = c * apk - s * aqk;
+          A[q * N + k] = s * apk + c * aqk;
+        }
+        A[p * N + q] = A[q * N + p] = 0.0;
+        for (int k = 0; k < N; ++k) {
+          const double vkp = V[k * N + p], vkq = V[k * N + q];
+          V[k * N + p] = c * vkp - s * vkq;
+          V[k * N + q] = s * vkp + c * vkq;
+        }
+      }
+  }
+  for (int i = 0; i < N; ++i) lam[i] = A[i * N + i];
+  for (int i = 1; i < N; ++i)  // insertion sort, ascending, columns of V follow
+    for (int j = i; j > 0 && lam[j] < lam[j - 1]; --j) {
+      const double t = lam[j]; lam[j] = lam[j - 1]; lam[j - 1] = t;
+      for (int k = 0; k < N; ++k) {
+        const double v = V[k * N + j]; V[k * N + j] = V[k * N + j - 1]; V[k * N + j - 1] = v;
+      }
+    }
+}
+
 }  // namespace okg

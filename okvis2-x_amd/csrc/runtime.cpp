@@ -56,7 +56,7 @@ struct HostBatch {
   int n_win = 0;
   std::vector<const okvisgpu_problem*> probs;
   // bases per window
-  std::vector<int> pose_base, sb_base, lm_base, cam_base, obs_base, imu_base, pp_base, sbp_base, sample_base;
+  std::vector<int> pose_base, sb_base, lm_base, cam_base, obs_base, imu_base, pp_base, sbp_base, rp_base, sample_base;
   // parameters (initial copies)
   std::vector<double> pose, sb, lm, extr, cam;
   std::vector<int32_t> pose_win, sb_win, lm_win, pose_f, sb_f;
@@ -75,11 +75,15 @@ struct HostBatch {
   // priors
   std::vector<int32_t> pp_block, pp_win, sbp_block, sbp_win;
   std::vector<double> pp_meas, pp_L, sbp_meas, sbp_L;
+  // relative-pose edges
+  std::vector<int32_t> rp_blocks, rp_win;
+  std::vector<uint8_t> rp_flags;
+  std::vector<double> rp_dx, rp_J, rp_lp;
   // reduced structure
   std::vector<int32_t> win_foff, win_fdim, win_fpad;
   std::vector<int64_t> win_soff, win_linvoff, win_fwdoff;
   std::vector<int32_t> win_pose_range, win_sb_range, win_lm_range, win_obs_range, win_imu_range, win_pp_range,
-      win_sbp_range;
+      win_sbp_range, win_rp_range;
   std::vector<int32_t> fb_win, fb_kind, fb_index, fb_off, fb_cbegin;
   std::vector<Contrib> fb_contrib;
   std::vector<int32_t> pair_win, pair_fi, pair_fj, pair_cbegin, pair_runs;
@@ -104,7 +108,7 @@ void appendN(std::vector<T>& v, const T* src, size_t n) {
 void validate(const okvisgpu_problem* p, int w) {
   auto bad = [&](const std::string& m) { throw ArgError{"window " + std::to_string(w) + ": " + m}; };
   if (p->n_poses < 0 || p->n_speed_biases < 0 || p->n_landmarks < 0 || p->n_observations < 0 || p->n_imu < 0 ||
-      p->n_pose_priors < 0 || p->n_sb_priors < 0 || p->n_cameras < 0)
+      p->n_pose_priors < 0 || p->n_sb_priors < 0 || p->n_cameras < 0 || p->n_relpose < 0)
     bad("negative count");
   if (p->n_poses && !p->poses) bad("poses == NULL");
   if (p->n_speed_biases && !p->speed_biases) bad("speed_biases == NULL");
@@ -137,6 +141,15 @@ void validate(const okvisgpu_problem* p, int w) {
     if (p->pose_prior_block[i] < 0 || p->pose_prior_block[i] >= p->n_poses) bad("pose prior block out of range");
   for (int i = 0; i < p->n_sb_priors; ++i)
     if (p->sb_prior_block[i] < 0 || p->sb_prior_block[i] >= p->n_speed_biases) bad("sb prior block out of range");
+  if (p->n_relpose) {
+    if (!p->relpose_blocks || !p->relpose_delta_x || !p->relpose_sqrt_info || !p->relpose_lin_point)
+      bad("relative-pose arrays missing");
+    for (int i = 0; i < p->n_relpose; ++i) {
+      const int a = p->relpose_blocks[2 * i], b = p->relpose_blocks[2 * i + 1];
+      if (a < 0 || a >= p->n_poses || b < 0 || b >= p->n_poses) bad("relative-pose block out of range");
+      if (a == b) bad("relative-pose edge connects a pose to itself");
+    }
+  }
 }
 
 // Build the batch. `constOverride` carries okvisgpu_set_block_constant() edits.
@@ -150,9 +163,10 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     validate(p, w);
     const int pb = (int)B.pose_win.size(), sbb = (int)B.sb_win.size(), lb = (int)B.lm_win.size();
     const int cb = (int)(B.cam.size() / 9), ob = (int)B.obs_win.size(), ib = (int)B.imu_win.size();
-    const int ppb = (int)B.pp_win.size(), sbpb = (int)B.sbp_win.size();
+    const int ppb = (int)B.pp_win.size(), sbpb = (int)B.sbp_win.size(), rpb = (int)B.rp_win.size();
     B.pose_base.push_back(pb); B.sb_base.push_back(sbb); B.lm_base.push_back(lb); B.cam_base.push_back(cb);
     B.obs_base.push_back(ob); B.imu_base.push_back(ib); B.pp_base.push_back(ppb); B.sbp_base.push_back(sbpb);
+    B.rp_base.push_back(rpb);
     auto isConst = [&](int kind, int idx, const uint8_t* flags) {
       auto it = constOverride.find(std::make_tuple(w, kind, idx));
       if (it != constOverride.end()) return it->second != 0;
@@ -196,6 +210,13 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       if (!pc[p->pose_prior_block[i]]) pa[p->pose_prior_block[i]] = 1;
     for (int i = 0; i < p->n_sb_priors; ++i)
       if (!sc[p->sb_prior_block[i]]) sa[p->sb_prior_block[i]] = 1;
+    std::vector<uint8_t> rfix(p->n_relpose);
+    for (int i = 0; i < p->n_relpose; ++i) {
+      const int a = p->relpose_blocks[2 * i], b = p->relpose_blocks[2 * i + 1];
+      rfix[i] = pc[a] && pc[b];
+      if (!pc[a]) pa[a] = 1;
+      if (!pc[b]) pa[b] = 1;
+    }
     // f-blocks in the reduced ordering: pose i, then speed/bias i
     std::vector<int> posef(p->n_poses, -1), sbf(p->n_speed_biases, -1), poseFb(p->n_poses, -1),
         sbFb(p->n_speed_biases, -1);
@@ -318,14 +339,24 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       appendN(B.sbp_meas, &p->sb_prior_meas[9 * i], 9);
       appendN(B.sbp_L, &p->sb_prior_sqrt_info[81 * i], 81);
     }
+    for (int i = 0; i < p->n_relpose; ++i) {
+      B.rp_blocks.push_back(pb + p->relpose_blocks[2 * i]);
+      B.rp_blocks.push_back(pb + p->relpose_blocks[2 * i + 1]);
+      B.rp_win.push_back(w);
+      B.rp_flags.push_back(rfix[i] ? 2 : 0);
+      appendN(B.rp_dx, &p->relpose_delta_x[6 * i], 6);
+      appendN(B.rp_J, &p->relpose_sqrt_info[36 * i], 36);
+      appendN(B.rp_lp, &p->relpose_lin_point[7 * i], 7);
+    }
     // ranges
     const int r_pose[2] = {pb, pb + p->n_poses}, r_sb[2] = {sbb, sbb + p->n_speed_biases},
               r_lm[2] = {lb, lb + p->n_landmarks}, r_obs[2] = {ob, ob + p->n_observations},
               r_imu[2] = {ib, ib + p->n_imu}, r_pp[2] = {ppb, ppb + p->n_pose_priors},
-              r_sbp[2] = {sbpb, sbpb + p->n_sb_priors};
+              r_sbp[2] = {sbpb, sbpb + p->n_sb_priors}, r_rp[2] = {rpb, rpb + p->n_relpose};
     appendN(B.win_pose_range, r_pose, 2); appendN(B.win_sb_range, r_sb, 2); appendN(B.win_lm_range, r_lm, 2);
     appendN(B.win_obs_range, r_obs, 2); appendN(B.win_imu_range, r_imu, 2); appendN(B.win_pp_range, r_pp, 2);
     appendN(B.win_sbp_range, r_sbp, 2);
+    appendN(B.win_rp_range, r_rp, 2);
 
     // ---- f-block gradient / diagonal contribution lists
     const int nFb = (int)B.fb_win.size() - fbBase;
@@ -349,6 +380,13 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     for (int i = 0; i < p->n_sb_priors; ++i) {
       const int fb = sbFb[p->sb_prior_block[i]];
       if (fb >= 0) fbc[fb - fbBase].push_back(Contrib{C_SBPRIOR, sbpb + i, 0, 0});
+    }
+    for (int i = 0; i < p->n_relpose; ++i) {
+      if (rfix[i]) continue;
+      for (int q = 0; q < 2; ++q) {
+        const int fb = poseFb[p->relpose_blocks[2 * i + q]];
+        if (fb >= 0) fbc[fb - fbBase].push_back(Contrib{C_RELPOSE, rpb + i, 6 * q, 6 * q});
+      }
     }
     for (int k = 0; k < nFb; ++k) {
       B.fb_cbegin.push_back((int)B.fb_contrib.size());
@@ -399,6 +437,16 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     for (int i = 0; i < p->n_sb_priors; ++i) {
       const int fb = sbFb[p->sb_prior_block[i]];
       if (fb >= 0) pairs[std::make_pair(fb, fb)].push_back(Contrib{C_SBPRIOR, sbpb + i, 0, 0});
+    }
+    for (int i = 0; i < p->n_relpose; ++i) {
+      if (rfix[i]) continue;
+      const int fbs[2] = {poseFb[p->relpose_blocks[2 * i]], poseFb[p->relpose_blocks[2 * i + 1]]};
+      for (int u = 0; u < 2; ++u)
+        for (int v = 0; v < 2; ++v) {
+          if (fbs[u] < 0 || fbs[v] < 0) continue;
+          if (B.fb_off[fbs[u]] < B.fb_off[fbs[v]]) continue;
+          pairs[key(fbs[u], fbs[v])].push_back(Contrib{C_RELPOSE, rpb + i, 6 * u, 6 * v});
+        }
     }
     // diagonal pairs must exist for every f-block (they carry the damping, diag and rhs)
     for (int k = fbBase; k < (int)B.fb_win.size(); ++k) pairs[std::make_pair(k, k)];
@@ -621,6 +669,7 @@ struct okvisgpu_ctx {
     D.n_imu = (int)B.imu_win.size();
     D.n_pprior = (int)B.pp_win.size();
     D.n_sbprior = (int)B.sbp_win.size();
+    D.n_relpose = (int)B.rp_win.size();
     D.n_cam = (int)(B.cam.size() / 9);
     D.n_fblock = (int)B.fb_win.size();
     D.n_pair = (int)B.pair_win.size();
@@ -676,6 +725,12 @@ struct okvisgpu_ctx {
                  o_sbp_lin1 = scratch(sizeof(double) * 90 * D.n_sbprior),
                  o_sbp_cost0 = scratch(sizeof(double) * D.n_sbprior), o_sbp_cost1 = scratch(sizeof(double) * D.n_sbprior),
                  o_sbp_jv = scratch(sizeof(double) * 3 * D.n_sbprior);
+    const size_t o_rp_blocks = upl(B.rp_blocks), o_rp_win = upl(B.rp_win), o_rp_flags = upl(B.rp_flags),
+                 o_rp_dx = upl(B.rp_dx), o_rp_J = upl(B.rp_J), o_rp_lp = upl(B.rp_lp);
+    const size_t o_rp_lin0 = scratch(sizeof(double) * kRelPoseLin * D.n_relpose),
+                 o_rp_lin1 = scratch(sizeof(double) * kRelPoseLin * D.n_relpose),
+                 o_rp_cost0 = scratch(sizeof(double) * D.n_relpose), o_rp_cost1 = scratch(sizeof(double) * D.n_relpose),
+                 o_rp_jv = scratch(sizeof(double) * 3 * D.n_relpose), o_wrpr = upl(B.win_rp_range);
     const size_t o_wfoff = upl(B.win_foff), o_wfdim = upl(B.win_fdim), o_wfpad = upl(B.win_fpad),
                  o_wsoff = upl(B.win_soff), o_wlinv = upl(B.win_linvoff), o_wfwd = upl(B.win_fwdoff), o_wpr = upl(B.win_pose_range), o_wsr = upl(B.win_sb_range),
                  o_wlr = upl(B.win_lm_range), o_wor = upl(B.win_obs_range), o_wir = upl(B.win_imu_range),
@@ -739,6 +794,11 @@ struct okvisgpu_ctx {
     D.win_pose_range = ip(o_wpr); D.win_sb_range = ip(o_wsr); D.win_lm_range = ip(o_wlr);
     D.win_obs_range = ip(o_wor); D.win_imu_range = ip(o_wir); D.win_pp_range = ip(o_wppr);
     D.win_sbp_range = ip(o_wsbpr);
+    D.win_rp_range = ip(o_wrpr);
+    D.rp_blocks = ip(o_rp_blocks); D.rp_win = ip(o_rp_win); D.rp_flags = up(o_rp_flags);
+    D.rp_dx = dp(o_rp_dx); D.rp_J = dp(o_rp_J); D.rp_lp = dp(o_rp_lp);
+    D.rp_lin[0] = dp(o_rp_lin0); D.rp_lin[1] = dp(o_rp_lin1);
+    D.rp_cost[0] = dp(o_rp_cost0); D.rp_cost[1] = dp(o_rp_cost1); D.rp_jv = dp(o_rp_jv);
     D.fb_win = ip(o_fbw); D.fb_kind = ip(o_fbk); D.fb_index = ip(o_fbi); D.fb_off = ip(o_fbo);
     D.fb_cbegin = ip(o_fbcb); D.fb_contrib = reinterpret_cast<const Contrib*>(base + o_fbc);
     D.pair_win = ip(o_pw); D.pair_fi = ip(o_pfi); D.pair_fj = ip(o_pfj); D.pair_cbegin = ip(o_pcb);
@@ -1460,6 +1520,124 @@ int okvisgpu_eval_imu(okvisgpu_ctx* c, int32_t window, int32_t redo_always, doub
     }
     // keep the caller's ImuError state in sync (the evaluation may have re-integrated)
     c->downloadParams(c->readStates());
+    return (int)OKVISGPU_OK;
+  });
+}
+
+int okvisgpu_eval_relpose(okvisgpu_ctx* c, int32_t window, double* r, double* J) {
+  if (!c) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
+  if (window < 0 || window >= c->P.n_win) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "bad window");
+  return guarded(c, [&]() {
+    HIPCHK(hipSetDevice(c->device));
+    c->resetStates(1e-8);
+    launch_eval(c->P, 3, c->stream);
+    HIPCHK(hipGetLastError());
+    const int n = c->probs[window]->n_relpose, rb = c->B.rp_base[window];
+    std::vector<double> lin((size_t)kRelPoseLin * std::max(1, n));
+    if (n) HIPCHK(hipMemcpyAsync(lin.data(), c->P.rp_lin[0] + (size_t)rb * kRelPoseLin, (size_t)kRelPoseLin * n * 8,
+                                 hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < n; ++i) {
+      if (r) for (int k = 0; k < 6; ++k) r[6 * i + k] = lin[(size_t)i * kRelPoseLin + k];
+      if (J) for (int k = 0; k < 72; ++k) J[72 * (size_t)i + k] = lin[(size_t)i * kRelPoseLin + 6 + k];
+    }
+    return (int)OKVISGPU_OK;
+  });
+}
+
+int okvisgpu_twopose_compute(okvisgpu_ctx* c, const okvisgpu_twopose_edges* E, double* delta_x, double* sqrt_info,
+                             double* lin_point, double* H00, double* b0) {
+  if (!c || !E || E->n_edges < 0) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "twopose_compute: bad arguments");
+  if (E->n_edges == 0) return OKVISGPU_OK;
+  if (!E->ref_pose || !E->other_pose || !E->landmark_begin || !E->obs_begin || !delta_x || !sqrt_info || !lin_point)
+    return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "twopose_compute: missing arrays");
+  return guarded(c, [&]() {
+    HIPCHK(hipSetDevice(c->device));
+    const int ne = E->n_edges;
+    const int nl = E->landmark_begin[ne] - E->landmark_begin[0];
+    if (E->landmark_begin[0] != 0 || nl < 0) throw ArgError{"twopose_compute: landmark_begin must start at 0"};
+    for (int e = 0; e < ne; ++e)
+      if (E->landmark_begin[e + 1] < E->landmark_begin[e]) throw ArgError{"twopose_compute: landmark_begin not monotone"};
+    const int no = nl ? E->obs_begin[nl] - E->obs_begin[0] : 0;
+    if (nl && (E->obs_begin[0] != 0 || no < 0)) throw ArgError{"twopose_compute: obs_begin must start at 0"};
+    for (int l = 0; l < nl; ++l)
+      if (E->obs_begin[l + 1] < E->obs_begin[l]) throw ArgError{"twopose_compute: obs_begin not monotone"};
+    if (no && (!E->landmarks || !E->obs_other || !E->obs_camera || !E->obs_keypoint || !E->obs_sqrt_info ||
+               !E->cameras || !E->extrinsics))
+      throw ArgError{"twopose_compute: observation arrays missing"};
+    for (int o = 0; o < no; ++o)
+      if (E->obs_camera[o] < 0 || E->obs_camera[o] >= E->n_cameras) throw ArgError{"twopose_compute: obs_camera out of range"};
+    std::vector<double> cam((size_t)9 * std::max(1, E->n_cameras));
+    for (int k = 0; k < E->n_cameras; ++k) {
+      const okvisgpu_camera& q = E->cameras[k];
+      if (q.distortion < 0 || q.distortion > 2) throw ArgError{"twopose_compute: unknown distortion model"};
+      const double cv[9] = {(double)q.distortion, q.fu, q.fv, q.cu, q.cv, q.dist[0], q.dist[1], q.dist[2], q.dist[3]};
+      std::memcpy(&cam[9 * (size_t)k], cv, sizeof(cv));
+    }
+    std::vector<uint8_t> cauchy(std::max(1, no), 1);
+    if (E->obs_cauchy) for (int o = 0; o < no; ++o) cauchy[o] = E->obs_cauchy[o] ? 1 : 0;
+    // one scratch allocation for inputs and outputs
+    Arena A;
+    auto put = [&](size_t bytes) { return A.reserve(bytes); };
+    const size_t o_ref = put(56 * (size_t)ne), o_oth = put(56 * (size_t)ne), o_cam = put(cam.size() * 8),
+                 o_ex = put(56 * (size_t)std::max(1, E->n_cameras)), o_lb = put(4 * (size_t)(ne + 1)),
+                 o_lm = put(32 * (size_t)std::max(1, nl)), o_ob = put(4 * (size_t)(nl + 1)),
+                 o_oo = put((size_t)std::max(1, no)), o_oc = put(4 * (size_t)std::max(1, no)),
+                 o_kp = put(16 * (size_t)std::max(1, no)), o_L = put(32 * (size_t)std::max(1, no)),
+                 o_ca = put((size_t)std::max(1, no)), o_out = put(8 * (size_t)kTwoPoseOut * ne);
+    char* base = nullptr;
+    HIPCHK(hipMalloc(&base, A.size));
+    std::unique_ptr<char, void (*)(char*)> guard(base, [](char* p) { (void)hipFree(p); });
+    auto up = [&](size_t off, const void* src, size_t bytes) {
+      if (bytes && src) HIPCHK(hipMemcpyAsync(base + off, src, bytes, hipMemcpyHostToDevice, c->stream));
+    };
+    up(o_ref, E->ref_pose, 56 * (size_t)ne);
+    up(o_oth, E->other_pose, 56 * (size_t)ne);
+    up(o_cam, cam.data(), cam.size() * 8);
+    up(o_ex, E->extrinsics, 56 * (size_t)E->n_cameras);
+    up(o_lb, E->landmark_begin, 4 * (size_t)(ne + 1));
+    if (nl) {
+      up(o_lm, E->landmarks, 32 * (size_t)nl);
+      up(o_ob, E->obs_begin, 4 * (size_t)(nl + 1));
+    }
+    if (no) {
+      up(o_oo, E->obs_other, (size_t)no);
+      up(o_oc, E->obs_camera, 4 * (size_t)no);
+      up(o_kp, E->obs_keypoint, 16 * (size_t)no);
+      up(o_L, E->obs_sqrt_info, 32 * (size_t)no);
+      up(o_ca, cauchy.data(), (size_t)no);
+    }
+    TwoPoseDev T{};
+    T.n_edges = ne;
+    T.n_cam = E->n_cameras;
+    T.ref_pose = reinterpret_cast<const double*>(base + o_ref);
+    T.other_pose = reinterpret_cast<const double*>(base + o_oth);
+    T.cam = reinterpret_cast<const double*>(base + o_cam);
+    T.extr = reinterpret_cast<const double*>(base + o_ex);
+    T.lm_begin = reinterpret_cast<const int32_t*>(base + o_lb);
+    T.lm = reinterpret_cast<const double*>(base + o_lm);
+    T.obs_begin = reinterpret_cast<const int32_t*>(base + o_ob);
+    T.obs_other = reinterpret_cast<const uint8_t*>(base + o_oo);
+    T.obs_cam = reinterpret_cast<const int32_t*>(base + o_oc);
+    T.obs_kp = reinterpret_cast<const double*>(base + o_kp);
+    T.obs_L = reinterpret_cast<const double*>(base + o_L);
+    T.obs_cauchy = reinterpret_cast<const uint8_t*>(base + o_ca);
+    T.out = reinterpret_cast<double*>(base + o_out);
+    if (!nl) HIPCHK(hipMemsetAsync(base + o_ob, 0, 4, c->stream));
+    launch_twopose_compute(T, c->stream);
+    HIPCHK(hipGetLastError());
+    std::vector<double> out((size_t)kTwoPoseOut * ne);
+    HIPCHK(hipMemcpyAsync(out.data(), T.out, out.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int e = 0; e < ne; ++e) {
+      const double* r = &out[(size_t)kTwoPoseOut * e];
+      std::memcpy(&delta_x[6 * (size_t)e], r, 6 * 8);
+      std::memcpy(&sqrt_info[36 * (size_t)e], r + 6, 36 * 8);
+      std::memcpy(&lin_point[7 * (size_t)e], r + 42, 7 * 8);
+      if (H00) std::memcpy(&H00[36 * (size_t)e], r + 49, 36 * 8);
+      if (b0) std::memcpy(&b0[6 * (size_t)e], r + 85, 6 * 8);
+    }
     return (int)OKVISGPU_OK;
   });
 }

@@ -31,6 +31,8 @@ struct okvisgpu_synth_window {
   std::vector<double> imu_ga, imu_state;
   std::vector<int32_t> pp_block, sbp_block;
   std::vector<double> pp_meas, pp_L, sbp_meas, sbp_L;
+  std::vector<int32_t> rp_blocks;
+  std::vector<double> rp_dx, rp_J, rp_lin;
 };
 
 namespace {
@@ -86,6 +88,8 @@ void okvisgpu_synth_default_config(okvisgpu_synth_config* c, int32_t n_kf, int32
   c->init_sigma_lm = 0.05;
   c->init_sigma_vel = 0.02;
   c->seed = seed;
+  c->n_relpose = 0;
+  c->relpose_stride = 5;
 }
 
 int okvisgpu_synth_create(const okvisgpu_synth_config* cfg, okvisgpu_synth_window** out) {
@@ -414,6 +418,43 @@ int okvisgpu_synth_create(const okvisgpu_synth_config* cfg, okvisgpu_synth_windo
   }
   W->imu_state.assign((size_t)(nkf - 1) * OKVISGPU_IMU_STATE_DOUBLES, 0.0);
 
+  // ---------------- pose-graph edges (TwoPoseStandardGraphErrorConst), own random stream so the
+  // windows without edges are unchanged
+  if (cfg->n_relpose > 0) {
+    if (cfg->relpose_stride < 1 || cfg->relpose_stride >= nkf) {
+      delete W;
+      return OKVISGPU_ERR_INVALID_ARGUMENT;
+    }
+    std::mt19937_64 rng2(cfg->seed ^ 0x9E3779B97F4A7C15ull);
+    std::normal_distribution<double> G(0.0, 1.0);
+    const double sp = 0.02, sr = 0.005;
+    for (int e = 0; e < cfg->n_relpose; ++e) {
+      const int a = e % (nkf - cfg->relpose_stride), b = a + cfg->relpose_stride;
+      W->rp_blocks.push_back(a);
+      W->rp_blocks.push_back(b);
+      // linearisation point: ground-truth T_S0S1 perturbed at the edge's noise level
+      const double* p0 = &W->gt_poses[7 * a];
+      const double* p1 = &W->gt_poses[7 * b];
+      const Q q0 = okg::qnormalize(Q{p0[3], p0[4], p0[5], p0[6]}), q1 = okg::qnormalize(Q{p1[3], p1[4], p1[5], p1[6]});
+      double C0[9];
+      okg::qrot(q0, C0);
+      const double d[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
+      double r[3];
+      okg::mtv3(C0, d, r);
+      const Q dq = okg::deltaQ(sr * G(rng2), sr * G(rng2), sr * G(rng2));
+      const Q ql = okg::qnormalize(okg::qmul(dq, okg::qmul(okg::qinv(q0), q1)));
+      const double lin[7] = {r[0] + sp * G(rng2), r[1] + sp * G(rng2), r[2] + sp * G(rng2), ql.x, ql.y, ql.z, ql.w};
+      W->rp_lin.insert(W->rp_lin.end(), lin, lin + 7);
+      for (int i = 0; i < 6; ++i) W->rp_dx.push_back(0.5 * (i < 3 ? sp : sr) * G(rng2));
+      // J_: upper triangular square-root information, diagonal 1/sigma, 10 % couplings
+      for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) {
+          const double s = 1.0 / (i < 3 ? sp : sr);
+          W->rp_J.push_back(j < i ? 0.0 : (j == i ? s : 0.1 * s * G(rng2)));
+        }
+    }
+  }
+
   // ---------------- problem view
   okvisgpu_problem& P = W->prob;
   std::memset(&P, 0, sizeof(P));
@@ -453,6 +494,11 @@ int okvisgpu_synth_create(const okvisgpu_synth_config* cfg, okvisgpu_synth_windo
   P.sb_prior_block = W->sbp_block.data();
   P.sb_prior_meas = W->sbp_meas.data();
   P.sb_prior_sqrt_info = W->sbp_L.data();
+  P.n_relpose = (int32_t)W->rp_blocks.size() / 2;
+  P.relpose_blocks = W->rp_blocks.data();
+  P.relpose_delta_x = W->rp_dx.data();
+  P.relpose_sqrt_info = W->rp_J.data();
+  P.relpose_lin_point = W->rp_lin.data();
   *out = W;
   return OKVISGPU_OK;
 }

@@ -56,6 +56,8 @@ class Problem(C.Structure):
         ("pose_prior_sqrt_info", _dp),
         ("n_sb_priors", C.c_int32), ("sb_prior_block", _ip), ("sb_prior_meas", _dp),
         ("sb_prior_sqrt_info", _dp),
+        ("n_relpose", C.c_int32), ("relpose_blocks", _ip), ("relpose_delta_x", _dp),
+        ("relpose_sqrt_info", _dp), ("relpose_lin_point", _dp),
     ]
 
 
@@ -90,7 +92,15 @@ class SynthConfig(C.Structure):
     _fields_ = [("n_keyframes", C.c_int32), ("n_landmarks", C.c_int32), ("n_observations", C.c_int32),
                 ("max_obs_per_landmark", C.c_int32), ("kf_dt_s", C.c_double), ("imu_rate_hz", C.c_double),
                 ("pixel_noise", C.c_double), ("init_sigma_pos", C.c_double), ("init_sigma_rot", C.c_double),
-                ("init_sigma_lm", C.c_double), ("init_sigma_vel", C.c_double), ("seed", C.c_uint64)]
+                ("init_sigma_lm", C.c_double), ("init_sigma_vel", C.c_double), ("seed", C.c_uint64),
+                ("n_relpose", C.c_int32), ("relpose_stride", C.c_int32)]
+
+
+class TwoPoseEdges(C.Structure):
+    _fields_ = [("n_edges", C.c_int32), ("ref_pose", _dp), ("other_pose", _dp),
+                ("n_cameras", C.c_int32), ("cameras", C.POINTER(Camera)), ("extrinsics", _dp),
+                ("landmark_begin", _ip), ("landmarks", _dp), ("obs_begin", _ip), ("obs_other", _up),
+                ("obs_camera", _ip), ("obs_keypoint", _dp), ("obs_sqrt_info", _dp), ("obs_cauchy", _up)]
 
 
 # Exported symbols of include/okvisgpu.h (checked by tests/test_abi.py).
@@ -103,7 +113,7 @@ EXPORTED_SYMBOLS = [
     "okvisgpu_synth_ground_truth", "okvisgpu_synth_reset", "okvisgpu_synth_destroy",
     "okvisgpu_solve_begin", "okvisgpu_solve_iterate", "okvisgpu_solve_end", "okvisgpu_synchronize",
     "okvisgpu_profile_iteration", "okvisgpu_phase_name", "okvisgpu_kernel_count", "okvisgpu_kernel_name",
-    "okvisgpu_time_kernel",
+    "okvisgpu_time_kernel", "okvisgpu_eval_relpose", "okvisgpu_twopose_compute",
 ]
 N_PHASES = 15
 
@@ -151,6 +161,8 @@ def lib():
         L.okvisgpu_kernel_name.argtypes = [C.c_int32]
         L.okvisgpu_kernel_name.restype = C.c_char_p
         L.okvisgpu_time_kernel.argtypes = [C.c_void_p, C.c_int32, C.c_int32, _dp, _dp, C.POINTER(C.c_int32)]
+        L.okvisgpu_eval_relpose.argtypes = [C.c_void_p, C.c_int32, _dp, _dp]
+        L.okvisgpu_twopose_compute.argtypes = [C.c_void_p, C.POINTER(TwoPoseEdges), _dp, _dp, _dp, _dp, _dp]
         _lib = L
     return _lib
 
@@ -229,6 +241,55 @@ class SynthWindow:
                 self.handle = None
         except Exception:
             pass
+
+
+class TwoPoseBatch:
+    """Owns the arrays of an okvisgpu_twopose_edges batch (TwoPoseStandardGraphError::compute inputs).
+
+    edges: list of dicts with keys ref_pose [7], other_pose [7], landmarks [n_l,4] and
+    observations: list (one per landmark) of lists of (other: bool, camera: int, keypoint [2],
+    sqrt_info [4], cauchy: bool). cameras: list of Camera; extrinsics [n_cam,7]."""
+
+    def __init__(self, edges, cameras, extrinsics):
+        self.ref = np.ascontiguousarray([e["ref_pose"] for e in edges], dtype=np.float64).reshape(-1, 7)
+        self.other = np.ascontiguousarray([e["other_pose"] for e in edges], dtype=np.float64).reshape(-1, 7)
+        lb, lms, ob, oo, oc, kp, L, ca = [0], [], [0], [], [], [], [], []
+        for e in edges:
+            for l, obs in zip(e["landmarks"], e["observations"]):
+                lms.append(l)
+                for (other, cam, k, s, cauchy) in obs:
+                    oo.append(1 if other else 0)
+                    oc.append(cam)
+                    kp.append(k)
+                    L.append(s)
+                    ca.append(1 if cauchy else 0)
+                ob.append(len(oo))
+            lb.append(len(lms))
+        self.lb = np.asarray(lb, dtype=np.int32)
+        self.lms = np.ascontiguousarray(np.asarray(lms, dtype=np.float64).reshape(-1, 4))
+        self.ob = np.asarray(ob, dtype=np.int32)
+        self.oo = np.asarray(oo, dtype=np.uint8)
+        self.oc = np.asarray(oc, dtype=np.int32)
+        self.kp = np.ascontiguousarray(np.asarray(kp, dtype=np.float64).reshape(-1, 2))
+        self.L = np.ascontiguousarray(np.asarray(L, dtype=np.float64).reshape(-1, 4))
+        self.ca = np.asarray(ca, dtype=np.uint8)
+        self.cams = (Camera * len(cameras))(*cameras)
+        self.ex = np.ascontiguousarray(extrinsics, dtype=np.float64).reshape(-1, 7)
+        s = TwoPoseEdges()
+        s.n_edges = len(edges)
+        s.ref_pose, s.other_pose = dptr(self.ref), dptr(self.other)
+        s.n_cameras = len(cameras)
+        s.cameras = self.cams
+        s.extrinsics = dptr(self.ex)
+        s.landmark_begin = self.lb.ctypes.data_as(_ip)
+        s.landmarks = dptr(self.lms)
+        s.obs_begin = self.ob.ctypes.data_as(_ip)
+        s.obs_other = self.oo.ctypes.data_as(_up)
+        s.obs_camera = self.oc.ctypes.data_as(_ip)
+        s.obs_keypoint = dptr(self.kp)
+        s.obs_sqrt_info = dptr(self.L)
+        s.obs_cauchy = self.ca.ctypes.data_as(_up)
+        self.struct = s
 
 
 class Context:
@@ -327,6 +388,23 @@ class Context:
         J = np.zeros((n_imu, 15, 30))
         self._check(lib().okvisgpu_eval_imu(self.h, window, int(redo_always), dptr(r), dptr(J)), "eval_imu")
         return r, J
+
+    def eval_relpose(self, n_relpose, window=0):
+        r = np.zeros((n_relpose, 6))
+        J = np.zeros((n_relpose, 6, 12))
+        self._check(lib().okvisgpu_eval_relpose(self.h, window, dptr(r), dptr(J)), "eval_relpose")
+        return r, J
+
+    def twopose_compute(self, edges: "TwoPoseBatch"):
+        """TwoPoseStandardGraphError::compute for every edge of the batch: dict of DeltaX_ [n,6],
+        J_ [n,6,6], linearisation point [n,7], H00_ [n,6,6], b0_ [n,6]."""
+        n = edges.struct.n_edges
+        out = {"delta_x": np.zeros((n, 6)), "sqrt_info": np.zeros((n, 6, 6)), "lin_point": np.zeros((n, 7)),
+               "H00": np.zeros((n, 6, 6)), "b0": np.zeros((n, 6))}
+        self._check(lib().okvisgpu_twopose_compute(self.h, C.byref(edges.struct), dptr(out["delta_x"]),
+                                                   dptr(out["sqrt_info"]), dptr(out["lin_point"]), dptr(out["H00"]),
+                                                   dptr(out["b0"])), "okvisgpu_twopose_compute")
+        return out
 
     def close(self):
         if getattr(self, "h", None):

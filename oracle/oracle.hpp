@@ -89,6 +89,15 @@ void poseErrorEvaluate(const double* meas, const double* sqrtInfo /*6x6*/, const
 void sbErrorEvaluate(const double* meas, const double* sqrtInfo /*9x9*/, const double* sb,
                      double* r, double* J /*9x9*/);
 
+// TwoPoseStandardGraphError(Const)::EvaluateWithMinimalJacobians (TwoPoseGraphError.cpp:467-606,
+// :631-767): dx = DeltaX_ [6], Jsq = J_ [36], lin = linearisationPoint_T_S0S1_ [7]. Jmin0/Jmin1 6x6
+// (reference / other pose), J0/J1 ambient 6x7. Any output Jacobian may be null.
+void relPoseEvaluate(const double* dx, const double* Jsq, const double* lin, const double* pose0,
+                     const double* pose1, double* r, double* Jmin0, double* Jmin1, double* J0, double* J1);
+// TwoPoseStandardGraphError::compute (TwoPoseGraphError.cpp:162-397) of edge e (twopose.cpp).
+void twoPoseCompute(const okvisgpu_twopose_edges* E, int e, double* deltaX, double* Jsq, double* linPoint,
+                    double* H00, double* b0);
+
 }  // namespace oracle
 
 // ------------------------------------------------------------------ C API (ctypes)
@@ -100,10 +109,13 @@ int oracle_linearize_reduce(const okvisgpu_problem* p, int32_t jacobi_scaling, d
 int oracle_eval_reprojection(const okvisgpu_problem* p, double* r, double* Jp, double* Jl);
 int oracle_eval_imu(const okvisgpu_problem* p, int32_t redo_always, double* r, double* J);
 /* numeric-vs-analytic Jacobian check with jacobiansCorrect semantics (ErrorInterface.cpp:44-163):
- * kind 0 = reprojection obs, 1 = imu factor, 2 = pose prior, 3 = sb prior. Returns the max over
+ * kind 0 = reprojection obs, 1 = imu factor, 2 = pose prior, 3 = sb prior, 4 = relative pose. Returns the max over
  * parameter blocks of ||Ja - Jn||_F / min(||Ja||_F, ||Jn||_F) in max_rel. */
 int oracle_check_jacobians(const okvisgpu_problem* p, int32_t kind, int32_t index, double delta,
                            double* max_rel);
+int oracle_eval_relpose(const okvisgpu_problem* p, double* r, double* J /*[n][6][12] minimal*/);
+int oracle_twopose_compute(const okvisgpu_twopose_edges* E, double* delta_x, double* sqrt_info, double* lin_point,
+                           double* H00, double* b0);
 int oracle_project(const okvisgpu_camera* cam, const double* hp4, double* kp2, double* J24);
 void oracle_pose_plus(const double* x, const double* delta, double* out);
 void oracle_pose_plus_jacobian(const double* x, double* J76);

@@ -24,7 +24,7 @@ namespace oracle {
 namespace {
 
 enum Kind { kPose = 0, kSb = 1, kLm = 2 };
-enum RKind { rReproj = 0, rImu = 1, rPosePrior = 2, rSbPrior = 3 };
+enum RKind { rReproj = 0, rImu = 1, rPosePrior = 2, rSbPrior = 3, rRelPose = 4 };
 
 struct PBlock {
   int kind, index;
@@ -116,6 +116,8 @@ void buildProgram(const okvisgpu_problem* p, Program& P, bool loadImuState) {
   }
   for (int i = 0; i < p->n_pose_priors; ++i) addR(rPosePrior, i, 6, {P.poseBase + p->pose_prior_block[i]});
   for (int i = 0; i < p->n_sb_priors; ++i) addR(rSbPrior, i, 9, {P.sbBase + p->sb_prior_block[i]});
+  for (int i = 0; i < p->n_relpose; ++i)
+    addR(rRelPose, i, 6, {P.poseBase + p->relpose_blocks[2 * i], P.poseBase + p->relpose_blocks[2 * i + 1]});
 
   // Active blocks (Ceres Program::RemoveFixedBlocks: unused or constant blocks removed).
   for (RBlock& r : P.rbs) {
@@ -277,6 +279,10 @@ double evalResidual(Program& P, const std::vector<double>& x, int ri, double* re
       break;
     case rSbPrior:
       sbErrorEvaluate(&p->sb_prior_meas[9 * r.index], &p->sb_prior_sqrt_info[81 * r.index], prm[0], rr, ja[0]);
+      break;
+    case rRelPose:  // no loss function (ViGraphEstimator.cpp:770)
+      relPoseEvaluate(&p->relpose_delta_x[6 * r.index], &p->relpose_sqrt_info[36 * r.index],
+                      &p->relpose_lin_point[7 * r.index], prm[0], prm[1], rr, nullptr, nullptr, ja[0], ja[1]);
       break;
   }
   double sq = 0;
@@ -1064,10 +1070,16 @@ int oracle_check_jacobians(const okvisgpu_problem* p, int32_t kind, int32_t inde
     blocks.push_back(std::vector<double>(&p->poses[7 * p->pose_prior_block[index]], &p->poses[7 * p->pose_prior_block[index]] + 7));
     kinds = {kPose};
     nres = 6;
-  } else {
+  } else if (kind == 3) {
     blocks.push_back(std::vector<double>(&p->speed_biases[9 * p->sb_prior_block[index]], &p->speed_biases[9 * p->sb_prior_block[index]] + 9));
     kinds = {kSb};
     nres = 9;
+  } else {
+    const int* b = &p->relpose_blocks[2 * index];
+    blocks.push_back(std::vector<double>(&p->poses[7 * b[0]], &p->poses[7 * b[0]] + 7));
+    blocks.push_back(std::vector<double>(&p->poses[7 * b[1]], &p->poses[7 * b[1]] + 7));
+    kinds = {kPose, kPose};
+    nres = 6;
   }
   const int nb = (int)blocks.size();
   auto eval = [&](const std::vector<std::vector<double>>& bl, double* r, double** jmin) {
@@ -1081,9 +1093,13 @@ int oracle_check_jacobians(const okvisgpu_problem* p, int32_t kind, int32_t inde
     } else if (kind == 2) {
       poseErrorEvaluate(&p->pose_prior_meas[7 * index], &p->pose_prior_sqrt_info[36 * index], prm[0], r, nullptr,
                         jmin ? jmin[0] : nullptr);
-    } else {
+    } else if (kind == 3) {
       sbErrorEvaluate(&p->sb_prior_meas[9 * index], &p->sb_prior_sqrt_info[81 * index], prm[0], r,
                       jmin ? jmin[0] : nullptr);
+    } else {
+      relPoseEvaluate(&p->relpose_delta_x[6 * index], &p->relpose_sqrt_info[36 * index],
+                      &p->relpose_lin_point[7 * index], prm[0], prm[1], r, jmin ? jmin[0] : nullptr,
+                      jmin ? jmin[1] : nullptr, nullptr, nullptr);
     }
   };
   std::vector<std::vector<double>> Ja(nb);
@@ -1129,6 +1145,23 @@ int oracle_check_jacobians(const okvisgpu_problem* p, int32_t kind, int32_t inde
     worst = std::max(worst, rel);
   }
   if (max_rel) *max_rel = worst;
+  return OKVISGPU_OK;
+}
+
+int oracle_eval_relpose(const okvisgpu_problem* p, double* r, double* J) {
+  for (int i = 0; i < p->n_relpose; ++i) {
+    const int* b = &p->relpose_blocks[2 * i];
+    double J0[36], J1[36], rr6[6];
+    relPoseEvaluate(&p->relpose_delta_x[6 * i], &p->relpose_sqrt_info[36 * i], &p->relpose_lin_point[7 * i],
+                    &p->poses[7 * b[0]], &p->poses[7 * b[1]], rr6, J0, J1, nullptr, nullptr);
+    if (r) for (int k = 0; k < 6; ++k) r[6 * i + k] = rr6[k];
+    if (J)
+      for (int rr = 0; rr < 6; ++rr)
+        for (int c = 0; c < 6; ++c) {
+          J[72 * i + rr * 12 + c] = J0[rr * 6 + c];
+          J[72 * i + rr * 12 + 6 + c] = J1[rr * 6 + c];
+        }
+  }
   return OKVISGPU_OK;
 }
 

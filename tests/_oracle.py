@@ -35,6 +35,8 @@ def lib():
         L.oracle_pose_plus_jacobian.argtypes = [_dp, _dp]
         L.oracle_pose_minus_jacobian.argtypes = [_dp, _dp]
         L.oracle_dense_cholesky.argtypes = [C.c_int32, _dp, C.c_int32]
+        L.oracle_eval_relpose.argtypes = [P, _dp, _dp]
+        L.oracle_twopose_compute.argtypes = [C.POINTER(og.TwoPoseEdges), _dp, _dp, _dp, _dp, _dp]
         _lib = L
     return _lib
 
@@ -83,3 +85,20 @@ def check_jacobians(problem_ptr, kind, index, delta=1e-7):
     m = C.c_double()
     lib().oracle_check_jacobians(problem_ptr, kind, index, delta, C.byref(m))
     return m.value
+
+
+def eval_relpose(problem_ptr, n):
+    r = np.zeros((n, 6))
+    J = np.zeros((n, 6, 12))
+    lib().oracle_eval_relpose(problem_ptr, og.dptr(r), og.dptr(J))
+    return r, J
+
+
+def twopose_compute(batch):
+    n = batch.struct.n_edges
+    out = {"delta_x": np.zeros((n, 6)), "sqrt_info": np.zeros((n, 6, 6)), "lin_point": np.zeros((n, 7)),
+           "H00": np.zeros((n, 6, 6)), "b0": np.zeros((n, 6))}
+    rc = lib().oracle_twopose_compute(C.byref(batch.struct), og.dptr(out["delta_x"]), og.dptr(out["sqrt_info"]),
+                                      og.dptr(out["lin_point"]), og.dptr(out["H00"]), og.dptr(out["b0"]))
+    assert rc == 0
+    return out
