@@ -104,14 +104,15 @@ def roofline_table(ctx, reps):
     return table
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per iteration of `kernel` from the committed rocprofv3 --pmc summary
-    (scripts/pmc_traffic.py: FETCH_SIZE x 2 per the gfx950 calibration + WRITE_SIZE), or None."""
+def pmc_traffic(kernel, windows):
+    """HBM bytes per iteration of `kernel` over `windows` windows from the committed rocprofv3 --pmc
+    summary (scripts/pmc_traffic.py: FETCH_SIZE x 2 per the gfx950 calibration + WRITE_SIZE, measured
+    per window-iteration on the default workload), or None."""
     try:
         with open(PMC_TRAFFIC) as f:
             d = json.load(f)
-        return d["kernels"][kernel]["bytes_per_iteration"]
-    except (OSError, KeyError, ValueError):
+        return d["kernels"][kernel]["bytes_per_window_iteration"] * windows
+    except (OSError, KeyError, ValueError, TypeError):
         return None
 
 
@@ -266,7 +267,7 @@ def main():
             table = roofline_table(ctx, args.kernel_reps)
             dominant = max(table, key=lambda k: table[k]["ms"])
             d = table[dominant]
-            traffic = pmc_traffic(dominant)
+            traffic = pmc_traffic(dominant, len(mine))
             result["roofline"] = {
                 "kernel": dominant, "bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"],
                 "unit": "GB/s" if d["bound"] == "hbm" else "TFLOP/s", "frac": d["frac"],
@@ -277,7 +278,8 @@ def main():
                           "rocprofv3 --pmc HBM bytes per iteration from profiles/pmc_traffic.json",
             }
             result["kernels"] = {k: {"ms": round(v["ms"], 4), "bound": v["bound"], "achieved": round(v["achieved"], 2),
-                                     "frac": round(v["frac"], 4)} for k, v in table.items()}
+                                     "frac": round(v["frac"], 4), "work": v["work"],
+                                     "traffic": pmc_traffic(k, len(mine))} for k, v in table.items()}
         # ---- CPU baseline (oracle restatement timed on this host) + accuracy vs CPU
         if not args.no_cpu:
             wc, sc, dt = run_cpu_baseline(cfg, args.cpu_iters, args.cpu_threads, args.cpu_windows, args.cpu_reps)

@@ -24,15 +24,16 @@ constexpr int kImuState = 292;        // == OKVISGPU_IMU_STATE_DOUBLES
 // Linearisation record per observation (structure of arrays, plane-major):
 //   plane 0-1: r (Cauchy-corrected)   plane 2-13: J_pose 2x6   plane 14-19: J_lm 2x3
 constexpr int kObsLin = 8;   // r (2) | A = L Jh C_CW (2x3), Cauchy-scaled
-constexpr int kVisitHG = 28;   // per visit: H = J_p^T J_p (21, sym packed) | g = J_p^T r (6) | pad
+constexpr int kSegHG = 28;   // per visit segment: H = sum J_p^T J_p (21, sym packed) | g = sum J_p^T r (6) | pad
+constexpr int kSegUz = 8;    // per visit segment: sum U z (6) | pad
 constexpr int kLmGroupVisits = 256;  // k_lm_visit: visits of one landmark group (one workgroup)
 constexpr int kLmGroupMax = 64;      // landmarks per group
 constexpr int kImuHess = 465 + 30;  // packed upper J^T J (30x30) | J^T r
-constexpr int kVisitUY = 24;  // Z = U L^-T (6x3) | U z (6)
+constexpr int kVisitZ = 18;   // per visit: Z = s_p W s_l L^-T (6x3)
 
 // contribution record types for the reduced-system assembly
 enum ContribType : int32_t {
-  C_VISIT = 0,      // a = visit: Hpp / gp of the visit (pose diagonal block)
+  C_VISIT = 0,      // a = visit segment: summed Hpp / gp / U z of one pose's visits in a landmark group
   C_PAIR = 1,       // a = visit i, b = visit j (same landmark): - W_i V^-1 W_j^T
   C_IMU = 2,        // a = factor, b = column offset of row block, c = column offset of col block
   C_PPRIOR = 3,     // a = pose prior
@@ -121,10 +122,17 @@ struct DevProblem {
   double* lm_g;                    // [n_lm][3]  J_l^T r
   double* lm_Linv;                 // [n_lm][9]  L^-1, L L^T = s V s + D^2 (lower triangular)
   double* lm_zz;                   // [n_lm][3]  L^-1 (s g)
-  double* visit_hg;                // [n_visit][kVisitHG] H = J_p^T J_p (21, sym packed) | g = J_p^T r (6) (unscaled)
   const int32_t* lmg_begin;        // [n_lmg+1] landmark groups of k_lm_visit (<= kLmGroupVisits visits each)
   int32_t n_lmg;
-  double* visit_UY;                // [n_visit][kVisitUY] Z = s_p W s_l L^-T (6x3) | U z (6)   (per GN solve)
+  double* visit_Z;                 // [n_visit][kVisitZ] Z = s_p W s_l L^-T (6x3)   (per GN solve)
+  // visit segments: the visits of one free pose inside one landmark group, pre-summed in k_lm_visit
+  int32_t n_seg;
+  const int32_t* seg_gbegin;       // [n_lmg+1] segments of group g
+  const int32_t* seg_pose;         // [n_seg] global pose
+  const int32_t* seg_range;        // [n_seg][2] slot range of the segment's visits within its group
+  const int32_t* visit_slot;       // [n_visit] slot in the group's (pose, visit) order, -1: pose not free
+  double* seg_hg;                  // [n_seg][kSegHG] H (21, sym packed) | g (6), unscaled
+  double* seg_uz;                  // [n_seg][kSegUz] U z (6)
 
   // --- IMU factors
   const int32_t* imu_blocks;       // [n_imu][4] global pose0 sb0 pose1 sb1

@@ -74,11 +74,13 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_visit(const DevProblem* _
   const int v0 = P.lm_visit_begin[l0], v1 = P.lm_visit_begin[l1];
   __shared__ double sVg[9][kLmGroupVisits];  // visit shares of V (6) | g_l (3)
   __shared__ double sLz[15][kLmGroupMax];    // per landmark: L^-1 (9) | zz (3) | s_l (3)
+  __shared__ double sR[14][kLmGroupVisits];  // visit values being summed into segments
+  const int w = P.lm_win[l0];                // a group never spans windows
+  if (!lmVisitSelect(P, w, mode)) return;    // uniform
   const int v = v0 + t;
   const bool hasV = v < v1;
   const int l = hasV ? P.visit_lm[v] : l0;
-  const int w = P.lm_win[l];
-  const bool sel = hasV && lmVisitSelect(P, w, mode);
+  const bool sel = hasV;
   const bool lfree = P.lm_free[l] != 0;
   const int pose = hasV ? P.visit_pose[v] : 0;
   const int pf = P.pose_f[pose];
@@ -127,15 +129,6 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_visit(const DevProblem* _
             for (int b2 = 0; b2 < 3; ++b2) W[a2 * 3 + b2] += Jp[a2] * Jl[b2] + Jp[6 + a2] * Jl[3 + b2];
         }
       }
-    }
-    if (mode != 2) {
-      double2* out = reinterpret_cast<double2*>(P.visit_hg + (size_t)v * kVisitHG);
-#pragma unroll
-      for (int i = 0; i < 10; ++i) out[i] = double2{H[2 * i], H[2 * i + 1]};
-      out[10] = double2{H[20], gp[0]};
-#pragma unroll
-      for (int i = 0; i < 2; ++i) out[11 + i] = double2{gp[1 + 2 * i], gp[2 + 2 * i]};
-      out[13] = double2{gp[5], 0.0};
     }
   }
 #pragma unroll
@@ -231,11 +224,36 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_visit(const DevProblem* _
     }
   }
   __syncthreads();
-  // ---- visit: Z = s_p W s_l L^-T (6x3) | U z = Z zz (6)
-  if (!sel || mode == 0) return;
-  double o[kVisitUY];
+  // ---- segments: H | g of each (group, free pose) summed over its visits in visit order
+  // (visits are scattered to their slots so that every segment is a contiguous LDS range)
+  const int sg0 = P.seg_gbegin[blockIdx.x], nseg = P.seg_gbegin[blockIdx.x + 1] - sg0;
+  const int slot = hasV ? P.visit_slot[v] : -1;
+  if (mode != 2) {
 #pragma unroll
-  for (int i = 0; i < kVisitUY; ++i) o[i] = 0.0;
+    for (int chunk = 0; chunk < 2; ++chunk) {
+      const int nval = chunk == 0 ? 14 : 13;
+      if (slot >= 0)
+#pragma unroll
+        for (int i = 0; i < 14; ++i) {
+          const int e = 14 * chunk + i;
+          if (i < nval) sR[i][slot] = e < 21 ? H[e] : gp[e - 21];
+        }
+      __syncthreads();
+      for (int e = t; e < nseg * nval; e += kLmGroupVisits) {
+        const int sgi = e / nval, i = e - sgi * nval;
+        const int m0 = P.seg_range[2 * (sg0 + sgi)], m1 = P.seg_range[2 * (sg0 + sgi) + 1];
+        double a = 0.0;
+        for (int m = m0; m < m1; ++m) a += sR[i][m];
+        P.seg_hg[(size_t)(sg0 + sgi) * kSegHG + 14 * chunk + i] = a;
+      }
+      __syncthreads();
+    }
+  }
+  if (mode == 0) return;
+  // ---- visit: Z = s_p W s_l L^-T (6x3) | U z = Z zz (6, summed into the segments)
+  double o[kVisitZ + 6];
+#pragma unroll
+  for (int i = 0; i < kVisitZ + 6; ++i) o[i] = 0.0;
   if (pf >= 0 && lfree) {
     const int u = l - l0;
     double Li[9], zz[3], s3[3], spr[6];
@@ -260,9 +278,22 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_visit(const DevProblem* _
       o[18 + r] = z0 * zz[0] + z1 * zz[1] + z2 * zz[2];
     }
   }
-  double2* out = reinterpret_cast<double2*>(P.visit_UY + (size_t)v * kVisitUY);
+  if (hasV) {
+    double2* out = reinterpret_cast<double2*>(P.visit_Z + (size_t)v * kVisitZ);
 #pragma unroll
-  for (int i = 0; i < kVisitUY / 2; ++i) out[i] = double2{o[2 * i], o[2 * i + 1]};
+    for (int i = 0; i < kVisitZ / 2; ++i) out[i] = double2{o[2 * i], o[2 * i + 1]};
+  }
+  if (slot >= 0)
+#pragma unroll
+    for (int i = 0; i < 6; ++i) sR[i][slot] = o[kVisitZ + i];
+  __syncthreads();
+  for (int e = t; e < nseg * 6; e += kLmGroupVisits) {
+    const int sgi = e / 6, i = e - sgi * 6;
+    const int m0 = P.seg_range[2 * (sg0 + sgi)], m1 = P.seg_range[2 * (sg0 + sgi) + 1];
+    double a = 0.0;
+    for (int m = m0; m < m1; ++m) a += sR[i][m];
+    P.seg_uz[(size_t)(sg0 + sgi) * kSegUz + i] = a;
+  }
 }
 
 // contribution helpers -------------------------------------------------------------------------
@@ -324,7 +355,7 @@ __global__ __launch_bounds__(64) void k_fgrad(const DevProblem* __restrict__ Pp,
   for (int k = P.fb_cbegin[fb] + lane; k < P.fb_cbegin[fb + 1]; k += 64) {
     const Contrib cb = P.fb_contrib[k];
     if (cb.type == C_VISIT) {
-      const double* H = P.visit_hg + (size_t)cb.a * kVisitHG;
+      const double* H = P.seg_hg + (size_t)cb.a * kSegHG;
       const double* gp = H + 21;
 #pragma unroll
       for (int c = 0; c < 6; ++c) { g[c] += gp[c]; hd[c] += H[sym6(c, c)]; }
@@ -432,8 +463,9 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
   const bool inGroup = g < kGroups;
   const int cb = P.pair_cbegin[k], pb = P.pair_runs[2 * k], ob = P.pair_runs[2 * k + 1], ce = P.pair_cbegin[k + 1];
   const auto pc = gmem(P.pair_contrib);
-  const auto vhg = gmem(P.visit_hg);
-  const auto vuy = gmem(P.visit_UY);
+  const auto vhg = gmem(P.seg_hg);
+  const auto suz = gmem(P.seg_uz);
+  const auto vuy = gmem(P.visit_Z);
   double H[6], Sc[6], uz = 0.0;
 #pragma unroll
   for (int q = 0; q < 6; ++q) { H[q] = 0.0; Sc[q] = 0.0; }
@@ -449,14 +481,14 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
       const int k0 = st + g;
       const int a0 = __shfl(da, k0 & 63, 64), b0 = __shfl(db, k0 & 63, 64);
       const bool v0 = inGroup && k0 < nstep;
-      const auto H0 = vhg + (size_t)a0 * kVisitHG;
+      const auto H0 = vhg + (size_t)a0 * kSegHG;
       double h0[6];
 #pragma unroll
       for (int q = 0; q < 6; ++q) h0[q] = H0[sym6(r, q)];
-      const double z0 = vuy[(size_t)a0 * kVisitUY + 18 + r];
+      const double z0 = suz[(size_t)a0 * kSegUz + r];
 #pragma unroll
       for (int q = 0; q < 6; ++q) H[q] += v0 ? h0[q] : 0.0;
-      uz += (v0 && b0) ? z0 : 0.0;
+      uz += v0 ? z0 : 0.0;
     }
   }
   // landmark pairs: row r of Z_a Z_b^T (= Y_a U_b^T); one contribution per group and step keeps
@@ -469,8 +501,8 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
       const int k0 = st + g;
       const int a0 = __shfl(da, k0 & 63, 64), b0 = __shfl(db, k0 & 63, 64);
       const bool v0 = inGroup && k0 < nstep;
-      const auto Y0 = vuy + (size_t)a0 * kVisitUY + 3 * r;
-      const auto U0 = vuy + (size_t)b0 * kVisitUY;
+      const auto Y0 = vuy + (size_t)a0 * kVisitZ + 3 * r;
+      const auto U0 = vuy + (size_t)b0 * kVisitZ;
       double y0[3], u0[18];
 #pragma unroll
       for (int i = 0; i < 3; ++i) y0[i] = Y0[i];
@@ -615,7 +647,7 @@ __global__ __launch_bounds__(256) void k_lm_backsub(const DevProblem* __restrict
   for (int v = P.lm_visit_begin[l]; v < P.lm_visit_begin[l + 1]; ++v) {
     const int pf = P.pose_f[P.visit_pose[v]];
     if (pf < 0) continue;
-    const double* Z = P.visit_UY + (size_t)v * kVisitUY;
+    const double* Z = P.visit_Z + (size_t)v * kVisitZ;
     for (int rr = 0; rr < 6; ++rr) {
       const double y = P.yF[(size_t)foff + pf + rr];
       for (int a = 0; a < 3; ++a) t3[a] -= Z[rr * 3 + a] * y;

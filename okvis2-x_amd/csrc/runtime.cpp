@@ -13,6 +13,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -59,6 +60,7 @@ struct HostBatch {
   std::vector<int> pose_base, sb_base, lm_base, cam_base, obs_base, imu_base, pp_base, sbp_base, rp_base, sample_base;
   // parameters (initial copies)
   std::vector<double> pose, sb, lm, extr, cam;
+  std::vector<int32_t> lm_perm;  // internal landmark k of window w is the caller's landmark lm_perm[lm_base[w] + k]
   std::vector<int32_t> pose_win, sb_win, lm_win, pose_f, sb_f;
   std::vector<uint8_t> lm_free, pose_active, sb_active;
   // obs (sorted) + permutation to the caller's order (within the window)
@@ -67,6 +69,8 @@ struct HostBatch {
   std::vector<double> obs_kp, obs_L;
   // visits
   std::vector<int32_t> lm_visit_begin, visit_pose, visit_obs_begin, visit_lm, lmg_begin;
+  // visit segments: per landmark group, the visits of one free pose (k_lm_visit pre-sums them)
+  std::vector<int32_t> seg_gbegin, seg_pose, seg_range, visit_slot;
   // imu
   std::vector<int32_t> imu_blocks, imu_win, imu_sbegin;
   std::vector<uint8_t> imu_flags;
@@ -156,6 +160,7 @@ void validate(const okvisgpu_problem* p, int w) {
 void analyse(const std::vector<const okvisgpu_problem*>& probs,
              const std::map<std::tuple<int, int, int>, int>& constOverride, HostBatch& B) {
   B = HostBatch();
+  B.seg_gbegin.push_back(0);
   B.n_win = (int)probs.size();
   B.probs = probs;
   for (int w = 0; w < B.n_win; ++w) {
@@ -179,7 +184,22 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     // parameters
     appendN(B.pose, p->poses, (size_t)7 * p->n_poses);
     appendN(B.sb, p->speed_biases, (size_t)9 * p->n_speed_biases);
-    appendN(B.lm, p->landmarks, (size_t)4 * p->n_landmarks);
+    // internal landmark order: by first observing pose (then caller order), so that the visits of
+    // neighbouring keyframes are close in memory whatever order the caller numbers landmarks in
+    // (okvis numbers them by creation, which is nearly this order already)
+    std::vector<int> perm(p->n_landmarks), inv(p->n_landmarks);
+    {
+      std::vector<int> firstPose(p->n_landmarks, p->n_poses);
+      for (int o = 0; o < p->n_observations; ++o)
+        firstPose[p->obs_landmark[o]] = std::min(firstPose[p->obs_landmark[o]], p->obs_pose[o]);
+      std::iota(perm.begin(), perm.end(), 0);
+      std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) { return firstPose[a] < firstPose[b]; });
+      for (int k = 0; k < p->n_landmarks; ++k) inv[perm[k]] = k;
+    }
+    for (int k = 0; k < p->n_landmarks; ++k) {
+      appendN(B.lm, &p->landmarks[4 * (size_t)perm[k]], 4);
+      B.lm_perm.push_back(perm[k]);
+    }
     for (int c = 0; c < p->n_cameras; ++c) {
       const okvisgpu_camera& k = p->cameras[c];
       const double cv[9] = {(double)k.distortion, k.fu, k.fv, k.cu, k.cv, k.dist[0], k.dist[1], k.dist[2], k.dist[3]};
@@ -239,7 +259,9 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     }
     for (int i = 0; i < p->n_poses; ++i) { B.pose_f.push_back(posef[i]); B.pose_active.push_back(pa[i]); }
     for (int i = 0; i < p->n_speed_biases; ++i) { B.sb_f.push_back(sbf[i]); B.sb_active.push_back(sa[i]); }
-    for (int i = 0; i < p->n_landmarks; ++i) B.lm_free.push_back(la[i]);
+    std::vector<uint8_t> laNew(p->n_landmarks);
+    for (int k = 0; k < p->n_landmarks; ++k) laNew[k] = la[perm[k]];
+    for (int k = 0; k < p->n_landmarks; ++k) B.lm_free.push_back(laNew[k]);
     const int fpad = ((fo + kTile - 1) / kTile) * kTile;
     B.win_foff.push_back(B.f_total);
     B.win_fdim.push_back(fo);
@@ -253,11 +275,11 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     B.linv_total += (int64_t)(fpad / kTile) * kTile * kTile;
     B.max_fpad = std::max(B.max_fpad, fpad);
 
-    // observations sorted by (landmark, pose, camera, original index)
+    // observations sorted by (internal landmark, pose, camera, original index)
     std::vector<int> order(p->n_observations);
     std::iota(order.begin(), order.end(), 0);
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
-      if (p->obs_landmark[a] != p->obs_landmark[b]) return p->obs_landmark[a] < p->obs_landmark[b];
+      if (p->obs_landmark[a] != p->obs_landmark[b]) return inv[p->obs_landmark[a]] < inv[p->obs_landmark[b]];
       if (p->obs_pose[a] != p->obs_pose[b]) return p->obs_pose[a] < p->obs_pose[b];
       return p->obs_camera[a] < p->obs_camera[b];
     });
@@ -270,7 +292,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       std::vector<int> vcount(p->n_landmarks, 0);
       for (int k = 0; k < p->n_observations; ++k) {
         const int o = order[k];
-        const int l = p->obs_landmark[o], ps = p->obs_pose[o];
+        const int l = inv[p->obs_landmark[o]], ps = p->obs_pose[o];
         B.obs_pose.push_back(pb + ps);
         B.obs_lm.push_back(lb + l);
         B.obs_cam.push_back(cb + p->obs_camera[o]);
@@ -299,6 +321,49 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       }
       lmVisitBegin[p->n_landmarks] = acc;
       for (int l = 0; l < p->n_landmarks; ++l) B.lm_visit_begin.push_back(lmVisitBegin[l]);
+    }
+    // landmark groups of k_lm_visit (consecutive whole landmarks of this window, <= kLmGroupVisits
+    // visits and <= kLmGroupMax landmarks; one workgroup, one thread per visit) and their visit
+    // segments: the visits of a group that belong to one free pose, pre-summed by k_lm_visit into
+    // one H | g and one U z record (ascending pose; members in visit order)
+    std::vector<std::vector<int>> segsAtPose(p->n_poses);
+    {
+      // each visit of a free pose gets the slot of its position in the group's (pose, visit)
+      // order, so a segment is a contiguous slot range [seg_range.x, seg_range.y)
+      auto closeGroup = [&](int gl0, int gl1) {
+        const int gv0 = lmVisitBegin[gl0], gv1 = lmVisitBegin[gl1];
+        std::map<int, std::vector<int>> mem;
+        for (int v = gv0; v < gv1; ++v) {
+          const int ps = B.visit_pose[v] - pb;
+          if (posef[ps] >= 0) mem[ps].push_back(v);
+          else B.visit_slot[v] = -1;
+        }
+        int slot = 0;
+        for (auto& kv : mem) {
+          segsAtPose[kv.first].push_back((int)B.seg_pose.size());
+          B.seg_pose.push_back(pb + kv.first);
+          B.seg_range.push_back(slot);
+          for (int v : kv.second) B.visit_slot[v] = slot++;
+          B.seg_range.push_back(slot);
+        }
+        B.lmg_begin.push_back(lb + gl0);
+        B.seg_gbegin.push_back((int)B.seg_pose.size());
+      };
+      B.visit_slot.resize(B.visit_pose.size(), -1);
+      int g0 = 0, gl = 0;
+      for (int l = 0; l < p->n_landmarks; ++l) {
+        const int nv = lmVisitBegin[l + 1] - lmVisitBegin[l];
+        if (nv > kLmGroupVisits)
+          throw ArgError{"landmark with more than " + std::to_string(kLmGroupVisits) + " observing poses"};
+        const int gv = lmVisitBegin[l] - lmVisitBegin[g0];
+        if (l > g0 && (gv + nv > kLmGroupVisits || gl == kLmGroupMax)) {
+          closeGroup(g0, l);
+          g0 = l;
+          gl = 0;
+        }
+        ++gl;
+      }
+      if (p->n_landmarks > 0) closeGroup(g0, p->n_landmarks);
     }
     // imu
     const int sBase = (int)B.imu_ts.size();
@@ -363,7 +428,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     std::vector<std::vector<Contrib>> fbc(nFb);
     for (int i = 0; i < p->n_poses; ++i) {
       if (poseFb[i] < 0) continue;
-      for (int v : visitsAtPose[i]) fbc[poseFb[i] - fbBase].push_back(Contrib{C_VISIT, v, la[B.visit_lm[v] - lb], 0});
+      for (int sg : segsAtPose[i]) fbc[poseFb[i] - fbBase].push_back(Contrib{C_VISIT, sg, 0, 0});
     }
     const int imuCol[4] = {0, 6, 15, 21};
     for (int f = 0; f < p->n_imu; ++f) {
@@ -400,13 +465,10 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     for (int i = 0; i < p->n_poses; ++i) {
       if (poseFb[i] < 0) continue;
       auto& lst = pairs[std::make_pair(poseFb[i], poseFb[i])];
-      for (int v : visitsAtPose[i]) {
-        const int l = B.visit_lm[v] - lb;
-        lst.push_back(Contrib{C_VISIT, v, la[l], 0});
-      }
+      for (int sg : segsAtPose[i]) lst.push_back(Contrib{C_VISIT, sg, 0, 0});
     }
     for (int l = 0; l < p->n_landmarks; ++l) {
-      if (!la[l]) continue;
+      if (!laNew[l]) continue;
       const int v0 = lmVisitBegin[l], v1 = lmVisitBegin[l + 1];
       for (int va = v0; va < v1; ++va) {
         const int fa = poseFb[B.visit_pose[va] - pb];
@@ -555,25 +617,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
         if (B.tileNz[w][(size_t)i * T + j]) { B.tile_items.push_back(w); B.tile_items.push_back(i); B.tile_items.push_back(j); }
   }
   B.lm_visit_begin.push_back((int)B.visit_pose.size());
-  // landmark groups of k_lm_visit: consecutive whole landmarks, <= kLmGroupVisits visits and
-  // <= kLmGroupMax landmarks per group (one workgroup, one thread per visit)
-  {
-    const int nl = (int)B.lm_visit_begin.size() - 1;
-    int gl = 0;
-    B.lmg_begin.push_back(0);
-    for (int l = 0; l < nl; ++l) {
-      const int nv = B.lm_visit_begin[l + 1] - B.lm_visit_begin[l];
-      if (nv > kLmGroupVisits)
-        throw std::invalid_argument("landmark with more than " + std::to_string(kLmGroupVisits) + " observing poses");
-      const int gv = B.lm_visit_begin[l] - B.lm_visit_begin[B.lmg_begin.back()];
-      if (l > B.lmg_begin.back() && (gv + nv > kLmGroupVisits || gl == kLmGroupMax)) {
-        B.lmg_begin.push_back(l);
-        gl = 0;
-      }
-      ++gl;
-    }
-    if (nl > 0) B.lmg_begin.push_back(nl);
-  }
+  B.lmg_begin.push_back((int)B.lm_win.size());  // groups: begin of each, then the end
   B.visit_obs_begin.push_back((int)B.obs_win.size());
   B.imu_sbegin.push_back((int)B.imu_ts.size());
   B.fb_cbegin.push_back((int)B.fb_contrib.size());
@@ -703,8 +747,11 @@ struct okvisgpu_ctx {
                  o_vlm = upl(B.visit_lm), o_lmg_b = upl(B.lmg_begin);
     const size_t o_lmV = scratch(sizeof(double) * 6 * D.n_lm), o_lmg = scratch(sizeof(double) * 3 * D.n_lm),
                  o_lmVi = scratch(sizeof(double) * 9 * D.n_lm), o_lmz = scratch(sizeof(double) * 3 * D.n_lm);
-    const size_t o_vhg = scratch(sizeof(double) * kVisitHG * D.n_visit),
-                 o_vUY = scratch(sizeof(double) * kVisitUY * D.n_visit);
+    D.n_seg = (int)B.seg_pose.size();
+    const size_t o_seg_gb = upl(B.seg_gbegin), o_seg_pose = upl(B.seg_pose), o_seg_rg = upl(B.seg_range),
+                 o_vslot = upl(B.visit_slot);
+    const size_t o_shg = scratch(sizeof(double) * kSegHG * D.n_seg), o_suz = scratch(sizeof(double) * kSegUz * D.n_seg),
+                 o_vZ = scratch(sizeof(double) * kVisitZ * D.n_visit);
     const size_t o_imu_blocks = upl(B.imu_blocks), o_imu_win = upl(B.imu_win), o_imu_flags = upl(B.imu_flags),
                  o_imu_t0 = upl(B.imu_t0), o_imu_t1 = upl(B.imu_t1), o_imu_sb = upl(B.imu_sbegin),
                  o_imu_ts = upl(B.imu_ts), o_imu_ga = upl(B.imu_ga), o_imu_par = upl(B.imu_par),
@@ -776,7 +823,8 @@ struct okvisgpu_ctx {
     D.obs_cost[0] = dp(o_obs_cost0); D.obs_cost[1] = dp(o_obs_cost1); D.obs_jv = dp(o_obs_jv);
     D.lm_visit_begin = ip(o_lmvb); D.visit_pose = ip(o_vpose); D.visit_obs_begin = ip(o_vob); D.visit_lm = ip(o_vlm);
     D.lm_V = dp(o_lmV); D.lm_g = dp(o_lmg); D.lm_Linv = dp(o_lmVi); D.lm_zz = dp(o_lmz);
-    D.visit_hg = dp(o_vhg); D.visit_UY = dp(o_vUY);
+    D.seg_hg = dp(o_shg); D.seg_uz = dp(o_suz); D.visit_Z = dp(o_vZ);
+    D.seg_gbegin = ip(o_seg_gb); D.seg_pose = ip(o_seg_pose); D.seg_range = ip(o_seg_rg); D.visit_slot = ip(o_vslot);
     D.lmg_begin = ip(o_lmg_b); D.n_lmg = B.lmg_begin.empty() ? 0 : (int)B.lmg_begin.size() - 1;
     D.imu_blocks = ip(o_imu_blocks); D.imu_win = ip(o_imu_win); D.imu_flags = up(o_imu_flags);
     D.imu_t0 = lp(o_imu_t0); D.imu_t1 = lp(o_imu_t1); D.imu_sbegin = ip(o_imu_sb); D.imu_ts = lp(o_imu_ts);
@@ -892,7 +940,8 @@ struct okvisgpu_ctx {
       const okvisgpu_problem* p = probs[w];
       appendN(pose, p->poses, (size_t)7 * p->n_poses);
       appendN(sb, p->speed_biases, (size_t)9 * p->n_speed_biases);
-      appendN(lm, p->landmarks, (size_t)4 * p->n_landmarks);
+      for (int k = 0; k < p->n_landmarks; ++k)
+        appendN(lm, &p->landmarks[4 * (size_t)B.lm_perm[B.lm_base[w] + k]], 4);
       for (int f = 0; f < p->n_imu; ++f) {
         if (p->imu_state) appendN(imu, &p->imu_state[(size_t)f * OKVISGPU_IMU_STATE_DOUBLES], OKVISGPU_IMU_STATE_DOUBLES);
         else imu.insert(imu.end(), OKVISGPU_IMU_STATE_DOUBLES, 0.0);
@@ -924,7 +973,9 @@ struct okvisgpu_ctx {
       const int x = st.empty() ? 0 : st[w].xcur;
       std::memcpy(p->poses, &pose[x][7 * (size_t)B.pose_base[w]], sizeof(double) * 7 * p->n_poses);
       std::memcpy(p->speed_biases, &sb[x][9 * (size_t)B.sb_base[w]], sizeof(double) * 9 * p->n_speed_biases);
-      std::memcpy(p->landmarks, &lm[x][4 * (size_t)B.lm_base[w]], sizeof(double) * 4 * p->n_landmarks);
+      for (int k = 0; k < p->n_landmarks; ++k)
+        std::memcpy(&p->landmarks[4 * (size_t)B.lm_perm[B.lm_base[w] + k]], &lm[x][4 * ((size_t)B.lm_base[w] + k)],
+                    sizeof(double) * 4);
       if (p->imu_state && p->n_imu)
         std::memcpy(p->imu_state, &imu[(size_t)B.imu_base[w] * kImuState],
                     sizeof(double) * kImuState * p->n_imu);
@@ -1304,7 +1355,7 @@ double kernelWork(const HostBatch& B, const DevProblem& P, int k) {
       double desc = 0, pairs = 0;
       for (int it : B.asm_pp_items)
         if (it >= 0) { desc += B.pair_cbegin[it + 1] - B.pair_cbegin[it]; pairs += 1; }
-      return desc * 16 + nVis * (kVisitUY + 21) * d8 + pairs * (36 + 12) * d8;
+      return desc * 16 + nVis * kVisitZ * d8 + (double)P.n_seg * (21 + 6) * d8 + pairs * (36 + 12) * d8;
     }
     case K_ASSEMBLE_SB: {
       double desc = 0, entries = 0;
@@ -1322,13 +1373,14 @@ double kernelWork(const HostBatch& B, const DevProblem& P, int k) {
       return diag * (2.0 * tile3 / 3.0 + 4.0 * 64 * 64) + panels * (2.0 * tile3 + 4.0 * 64 * 64) + upd * 2.0 * tile3;
     }
     case K_LM_VISIT:  // obs linearisation + params in; H|g and Z|Uz per visit, landmark blocks out
-      return nObs * (kObsLin * d8 + 1) + nVis * (kVisitHG * d8 + kVisitUY * d8 + 7 * d8 + 16) + nLm * 40 * d8;
+      return nObs * (kObsLin * d8 + 1) + nVis * (kVisitZ * d8 + 7 * d8 + 16) + (double)P.n_seg * (27 + 6) * d8 +
+             nLm * 40 * d8;
     case K_LM_VISIT_PREP:  // W recomputed from the obs linearisation; Z|Uz out
-      return nObs * (kObsLin * d8 + 1) + nVis * (kVisitUY * d8 + 7 * d8 + 16) + nLm * 34 * d8;
+      return nObs * (kObsLin * d8 + 1) + nVis * (kVisitZ * d8 + 7 * d8 + 16) + (double)P.n_seg * 6 * d8 + nLm * 34 * d8;
     case K_EVAL_IMU: return nImu * (2.0 * kImuState + kImuLin + 2 * 16) * d8 + (double)B.imu_ts.size() * 7 * d8;
     case K_EVAL_OBS: return nObs * (16 + 32 + 13 + kObsLin * d8 + 8) + nLm * 4 * d8 + (double)B.pose_f.size() * 7 * d8;
     case K_JV: return nObs * (kObsLin * d8 + 1) + nVis * (7 + 4 + 3 * 9 + 3) * d8 + nImu * (kImuLin + 3) * d8;
-    case K_FGRAD: return nVis * 12 * d8 + nImu * kImuLin * d8 + (double)B.fb_contrib.size() * 16;
+    case K_FGRAD: return (double)P.n_seg * 27 * d8 + nImu * kImuLin * d8 + (double)B.fb_contrib.size() * 16;
   }
   return 0.0;
 }

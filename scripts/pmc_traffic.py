@@ -1,15 +1,19 @@
 """Turn rocprofv3 --pmc passes (scripts/gpu_pmc.sh) into profiles/pmc_traffic.json: HBM bytes per
 dispatch of each kernel. FETCH_SIZE / WRITE_SIZE are in KiB; FETCH_SIZE is doubled per the gfx950
 calibration of MI355X_MICROARCH.md (HBM section: it reports half the bytes of 16-byte-per-lane
-reads); other access widths are uncalibrated there, so the figure is an estimate."""
+reads); other access widths are uncalibrated there, so the figure is an estimate.
+
+Usage: pmc_traffic.py OUT.json WINDOWS pass1.csv pass2.csv ... (WINDOWS = windows in the profiled
+batch; bench.py scales bytes_per_window_iteration by its own windows per GPU)."""
 import collections
 import csv
 import json
 import sys
 
 out = sys.argv[1]
+windows = int(sys.argv[2])
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
-for path in sys.argv[2:]:
+for path in sys.argv[3:]:
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"].split("(")[0].replace("okg::", "")
         vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -23,6 +27,8 @@ for k, d in vals.items():
     if k in ("k_assemble_pp", "k_assemble_sb", "k_eval_imu", "k_eval_obs", "k_fgrad", "k_cholesky", "k_lm_backsub",
              "k_zero_S"):
         kern[k]["bytes_per_iteration"] = f + w  # one dispatch per iteration
-json.dump({"source": sys.argv[2:], "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane calibration), KiB -> bytes",
+        kern[k]["bytes_per_window_iteration"] = (f + w) / windows
+json.dump({"source": sys.argv[3:], "windows": windows,
+           "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane calibration), KiB -> bytes",
            "kernels": kern}, open(out, "w"), indent=1, sort_keys=True)
 print(json.dumps({k: round(v["bytes_per_dispatch"] / 1e9, 3) for k, v in kern.items()}, indent=0))
