@@ -28,13 +28,14 @@ constexpr int kSegHG = 28;   // per visit segment: H = sum J_p^T J_p (21, sym pa
 constexpr int kSegUz = 8;    // per visit segment: sum U z (6) | pad
 constexpr int kLmGroupVisits = 256;  // k_lm_visit: visits of one landmark group (one workgroup)
 constexpr int kLmGroupMax = 64;      // landmarks per group
+constexpr int kLmPartStage = 2048;   // landmark-pair products per group (staged in LDS)
 constexpr int kImuHess = 465 + 30;  // packed upper J^T J (30x30) | J^T r
 constexpr int kVisitZ = 18;   // per visit: Z = s_p W s_l L^-T (6x3)
 
 // contribution record types for the reduced-system assembly
 enum ContribType : int32_t {
   C_VISIT = 0,      // a = visit segment: summed Hpp / gp / U z of one pose's visits in a landmark group
-  C_PAIR = 1,       // a = visit i, b = visit j (same landmark): - W_i V^-1 W_j^T
+  C_PAIR = 1,       // a = partial Schur block: sum over a landmark group of Z_a Z_b^T (= W_a V^-1 W_b^T)
   C_IMU = 2,        // a = factor, b = column offset of row block, c = column offset of col block
   C_PPRIOR = 3,     // a = pose prior
   C_SBPRIOR = 4,    // a = sb prior
@@ -133,6 +134,12 @@ struct DevProblem {
   const int32_t* visit_slot;       // [n_visit] slot in the group's (pose, visit) order, -1: pose not free
   double* seg_hg;                  // [n_seg][kSegHG] H (21, sym packed) | g (6), unscaled
   double* seg_uz;                  // [n_seg][kSegUz] U z (6)
+  // partial Schur blocks: per landmark group and pose pair, P = sum Z_a Z_b^T (6x6, row-major)
+  int32_t n_part;
+  const int32_t* part_gbegin;      // [n_lmg+1] partial blocks of group g
+  const int32_t* part_cbegin;      // [n_part+1] CSR into part_contrib
+  const int32_t* part_contrib;     // (a | b << 16): visit offsets within the group
+  double* part_S;                  // [n_part][36]
 
   // --- IMU factors
   const int32_t* imu_blocks;       // [n_imu][4] global pose0 sb0 pose1 sb1

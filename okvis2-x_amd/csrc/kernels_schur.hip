@@ -72,9 +72,13 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_visit(const DevProblem* _
   const int t = threadIdx.x;
   const int l0 = P.lmg_begin[blockIdx.x], l1 = P.lmg_begin[blockIdx.x + 1];
   const int v0 = P.lm_visit_begin[l0], v1 = P.lm_visit_begin[l1];
-  __shared__ double sVg[9][kLmGroupVisits];  // visit shares of V (6) | g_l (3)
+  // sBuf rows 0..8: visit shares of V (6) | g_l (3); rows 9..22: visit values being summed into
+  // segments; finally rows 0..17: the visits' Z for the partial Schur blocks
+  __shared__ double sBuf[23][kLmGroupVisits];
   __shared__ double sLz[15][kLmGroupMax];    // per landmark: L^-1 (9) | zz (3) | s_l (3)
-  __shared__ double sR[14][kLmGroupVisits];  // visit values being summed into segments
+  __shared__ int sPC[kLmPartStage];          // the group's landmark-pair products (a | b << 16)
+  double (*sVg)[kLmGroupVisits] = sBuf;
+  double (*sR)[kLmGroupVisits] = sBuf + 9;
   const int w = P.lm_win[l0];                // a group never spans windows
   if (!lmVisitSelect(P, w, mode)) return;    // uniform
   const int v = v0 + t;
@@ -294,6 +298,45 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_visit(const DevProblem* _
     for (int m = m0; m < m1; ++m) a += sR[i][m];
     P.seg_uz[(size_t)(sg0 + sgi) * kSegUz + i] = a;
   }
+  // ---- partial Schur blocks: for each pose pair of the group, rows 2h, 2h+1 of sum Z_a Z_b^T over
+  // the group's landmark-pair products (fixed order), from Z staged visit-major in LDS (144-byte
+  // records read with 16-byte LDS loads)
+  const int pg0 = P.part_gbegin[blockIdx.x], npart = P.part_gbegin[blockIdx.x + 1] - pg0;
+  const int pc0 = P.part_cbegin[pg0], npc = P.part_cbegin[pg0 + npart] - pc0;
+  double* sZ = &sBuf[0][0];
+  __syncthreads();  // sR reads above are done
+  {
+    double2* zo = reinterpret_cast<double2*>(sZ + kVisitZ * t);
+#pragma unroll
+    for (int i = 0; i < kVisitZ / 2; ++i) zo[i] = double2{o[2 * i], o[2 * i + 1]};
+  }
+  for (int c = t; c < npc; c += kLmGroupVisits) sPC[c] = P.part_contrib[pc0 + c];
+  __syncthreads();
+  for (int e = t; e < npart * 3; e += kLmGroupVisits) {
+    const int pi = e / 3, h = e - pi * 3;
+    const int c0 = P.part_cbegin[pg0 + pi] - pc0, c1 = P.part_cbegin[pg0 + pi + 1] - pc0;
+    double acc[12];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) acc[i] = 0.0;
+    for (int c = c0; c < c1; ++c) {
+      const int ab = sPC[c], a = ab & 0xffff, b = ab >> 16;
+      const double2* za2 = reinterpret_cast<const double2*>(sZ + kVisitZ * a + 6 * h);
+      const double2* zb2 = reinterpret_cast<const double2*>(sZ + kVisitZ * b);
+      double za[6], zb[18];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) { const double2 v = za2[i]; za[2 * i] = v.x; za[2 * i + 1] = v.y; }
+#pragma unroll
+      for (int i = 0; i < 9; ++i) { const double2 v = zb2[i]; zb[2 * i] = v.x; zb[2 * i + 1] = v.y; }
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+          acc[rr * 6 + q] += za[3 * rr] * zb[3 * q] + za[3 * rr + 1] * zb[3 * q + 1] + za[3 * rr + 2] * zb[3 * q + 2];
+    }
+    double2* out = reinterpret_cast<double2*>(P.part_S + (size_t)(pg0 + pi) * 36 + 12 * h);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) out[q] = double2{acc[2 * q], acc[2 * q + 1]};
+  }
 }
 
 // contribution helpers -------------------------------------------------------------------------
@@ -491,28 +534,15 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
       uz += v0 ? z0 : 0.0;
     }
   }
-  // landmark pairs: row r of Z_a Z_b^T (= Y_a U_b^T); one contribution per group and step keeps
-  // the operand registers low enough for 6 wavefronts per SIMD
-  for (int base = pb; base < ob; base += 64) {
-    const int myc = min(base + lane, ob - 1);
-    const int da = pc[myc].a, db = pc[myc].b;
-    const int nstep = min(64, ob - base);
-    for (int st = 0; st < nstep; st += kGroups) {
-      const int k0 = st + g;
-      const int a0 = __shfl(da, k0 & 63, 64), b0 = __shfl(db, k0 & 63, 64);
-      const bool v0 = inGroup && k0 < nstep;
-      const auto Y0 = vuy + (size_t)a0 * kVisitZ + 3 * r;
-      const auto U0 = vuy + (size_t)b0 * kVisitZ;
-      double y0[3], u0[18];
+  // partial Schur blocks of the landmark groups: row r of sum Z_a Z_b^T (= Y_a U_b^T)
+  const auto ps = gmem(P.part_S);
+  for (int c = pb + g0; c < ob; c += kGroups) {
+    const auto R2 = reinterpret_cast<gptr<double2>>(ps + (size_t)pc[c].a * 36 + 6 * r);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) y0[i] = Y0[i];
-#pragma unroll
-      for (int i = 0; i < 18; ++i) u0[i] = U0[i];
-#pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const double t0 = y0[0] * u0[3 * q] + y0[1] * u0[3 * q + 1] + y0[2] * u0[3 * q + 2];
-        Sc[q] += v0 ? t0 : 0.0;
-      }
+    for (int q = 0; q < 3; ++q) {
+      const double2 v = R2[q];
+      Sc[2 * q] += v.x;
+      Sc[2 * q + 1] += v.y;
     }
   }
   // factor blocks (IMU, relative pose, pose prior): row r of J_i^T J_j

@@ -71,6 +71,8 @@ struct HostBatch {
   std::vector<int32_t> lm_visit_begin, visit_pose, visit_obs_begin, visit_lm, lmg_begin;
   // visit segments: per landmark group, the visits of one free pose (k_lm_visit pre-sums them)
   std::vector<int32_t> seg_gbegin, seg_pose, seg_range, visit_slot;
+  // partial Schur blocks: per landmark group and pose pair, sum of Z_a Z_b^T over the group's landmarks
+  std::vector<int32_t> part_gbegin, part_cbegin, part_contrib;
   // imu
   std::vector<int32_t> imu_blocks, imu_win, imu_sbegin;
   std::vector<uint8_t> imu_flags;
@@ -161,6 +163,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
              const std::map<std::tuple<int, int, int>, int>& constOverride, HostBatch& B) {
   B = HostBatch();
   B.seg_gbegin.push_back(0);
+  B.part_gbegin.push_back(0);
   B.n_win = (int)probs.size();
   B.probs = probs;
   for (int w = 0; w < B.n_win; ++w) {
@@ -327,6 +330,8 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     // segments: the visits of a group that belong to one free pose, pre-summed by k_lm_visit into
     // one H | g and one U z record (ascending pose; members in visit order)
     std::vector<std::vector<int>> segsAtPose(p->n_poses);
+    std::vector<std::pair<int, int>> partKeys;  // f-block pair of each partial block of this window
+    const int partBase = (int)B.part_cbegin.size();
     {
       // each visit of a free pose gets the slot of its position in the group's (pose, visit)
       // order, so a segment is a contiguous slot range [seg_range.x, seg_range.y)
@@ -346,9 +351,43 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
           for (int v : kv.second) B.visit_slot[v] = slot++;
           B.seg_range.push_back(slot);
         }
+        // partial Schur blocks (k_lm_visit): per pose pair (row >= col by f offset) the products
+        // Z_a Z_b^T of the group's free landmarks; contributions packed as (a | b << 16), visit
+        // offsets within the group
+        std::map<std::pair<int, int>, std::vector<int32_t>> gparts;
+        for (int l = gl0; l < gl1; ++l) {
+          if (!laNew[l]) continue;
+          for (int va = lmVisitBegin[l]; va < lmVisitBegin[l + 1]; ++va) {
+            const int fa = poseFb[B.visit_pose[va] - pb];
+            if (fa < 0) continue;
+            for (int vb = lmVisitBegin[l]; vb < lmVisitBegin[l + 1]; ++vb) {
+              const int fb2 = poseFb[B.visit_pose[vb] - pb];
+              if (fb2 < 0 || B.fb_off[fa] < B.fb_off[fb2]) continue;
+              gparts[std::make_pair(fa, fb2)].push_back((va - gv0) | ((vb - gv0) << 16));
+            }
+          }
+        }
+        // long blocks are split into chunks of <= kPartChunk products (separate records, summed
+        // in order by k_assemble_pp) so that no k_lm_visit thread serialises a whole block
+        constexpr size_t kPartChunk = 24;  // measured: 6 / 12 / 24 / unsplit on 2048 S50 windows
+        for (auto& kv : gparts)
+          for (size_t c0 = 0; c0 < kv.second.size(); c0 += kPartChunk) {
+            const size_t c1 = std::min(kv.second.size(), c0 + kPartChunk);
+            partKeys.push_back(kv.first);
+            B.part_cbegin.push_back((int)B.part_contrib.size());
+            B.part_contrib.insert(B.part_contrib.end(), kv.second.begin() + c0, kv.second.begin() + c1);
+          }
         B.lmg_begin.push_back(lb + gl0);
         B.seg_gbegin.push_back((int)B.seg_pose.size());
+        B.part_gbegin.push_back((int)B.part_cbegin.size());
       };
+      // landmark-pair products a group stages in LDS (kLmPartStage) bound the group as well
+      auto pairCount = [&](int l) {
+        if (!laNew[l]) return 0;
+        const int nv = lmVisitBegin[l + 1] - lmVisitBegin[l];
+        return nv * (nv + 1) / 2;
+      };
+      int gpc = 0;
       B.visit_slot.resize(B.visit_pose.size(), -1);
       int g0 = 0, gl = 0;
       for (int l = 0; l < p->n_landmarks; ++l) {
@@ -356,12 +395,17 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
         if (nv > kLmGroupVisits)
           throw ArgError{"landmark with more than " + std::to_string(kLmGroupVisits) + " observing poses"};
         const int gv = lmVisitBegin[l] - lmVisitBegin[g0];
-        if (l > g0 && (gv + nv > kLmGroupVisits || gl == kLmGroupMax)) {
+        const int pcl = pairCount(l);
+        if (pcl > kLmPartStage)
+          throw ArgError{"landmark with more than " + std::to_string(kLmPartStage) + " visit pairs"};
+        if (l > g0 && (gv + nv > kLmGroupVisits || gl == kLmGroupMax || gpc + pcl > kLmPartStage)) {
           closeGroup(g0, l);
           g0 = l;
           gl = 0;
+          gpc = 0;
         }
         ++gl;
+        gpc += pcl;
       }
       if (p->n_landmarks > 0) closeGroup(g0, p->n_landmarks);
     }
@@ -467,20 +511,8 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       auto& lst = pairs[std::make_pair(poseFb[i], poseFb[i])];
       for (int sg : segsAtPose[i]) lst.push_back(Contrib{C_VISIT, sg, 0, 0});
     }
-    for (int l = 0; l < p->n_landmarks; ++l) {
-      if (!laNew[l]) continue;
-      const int v0 = lmVisitBegin[l], v1 = lmVisitBegin[l + 1];
-      for (int va = v0; va < v1; ++va) {
-        const int fa = poseFb[B.visit_pose[va] - pb];
-        if (fa < 0) continue;
-        for (int vb = v0; vb < v1; ++vb) {
-          const int fb2 = poseFb[B.visit_pose[vb] - pb];
-          if (fb2 < 0) continue;
-          if (B.fb_off[fa] < B.fb_off[fb2]) continue;  // each unordered pair once, row >= col
-          pairs[std::make_pair(fa, fb2)].push_back(Contrib{C_PAIR, va, vb, 0});
-        }
-      }
-    }
+    for (size_t k = 0; k < partKeys.size(); ++k)  // partial Schur blocks, group order
+      pairs[partKeys[k]].push_back(Contrib{C_PAIR, partBase + (int)k, 0, 0});
     for (int f = 0; f < p->n_imu; ++f) {
       if (ifix[f]) continue;
       const int* b = &p->imu_blocks[4 * f];
@@ -618,6 +650,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
   }
   B.lm_visit_begin.push_back((int)B.visit_pose.size());
   B.lmg_begin.push_back((int)B.lm_win.size());  // groups: begin of each, then the end
+  B.part_cbegin.push_back((int)B.part_contrib.size());
   B.visit_obs_begin.push_back((int)B.obs_win.size());
   B.imu_sbegin.push_back((int)B.imu_ts.size());
   B.fb_cbegin.push_back((int)B.fb_contrib.size());
@@ -750,6 +783,9 @@ struct okvisgpu_ctx {
     D.n_seg = (int)B.seg_pose.size();
     const size_t o_seg_gb = upl(B.seg_gbegin), o_seg_pose = upl(B.seg_pose), o_seg_rg = upl(B.seg_range),
                  o_vslot = upl(B.visit_slot);
+    D.n_part = (int)B.part_cbegin.size() - 1;
+    const size_t o_pgb = upl(B.part_gbegin), o_pcb2 = upl(B.part_cbegin), o_pcon = upl(B.part_contrib),
+                 o_partS = scratch(sizeof(double) * 36 * std::max(1, D.n_part));
     const size_t o_shg = scratch(sizeof(double) * kSegHG * D.n_seg), o_suz = scratch(sizeof(double) * kSegUz * D.n_seg),
                  o_vZ = scratch(sizeof(double) * kVisitZ * D.n_visit);
     const size_t o_imu_blocks = upl(B.imu_blocks), o_imu_win = upl(B.imu_win), o_imu_flags = upl(B.imu_flags),
@@ -823,6 +859,7 @@ struct okvisgpu_ctx {
     D.obs_cost[0] = dp(o_obs_cost0); D.obs_cost[1] = dp(o_obs_cost1); D.obs_jv = dp(o_obs_jv);
     D.lm_visit_begin = ip(o_lmvb); D.visit_pose = ip(o_vpose); D.visit_obs_begin = ip(o_vob); D.visit_lm = ip(o_vlm);
     D.lm_V = dp(o_lmV); D.lm_g = dp(o_lmg); D.lm_Linv = dp(o_lmVi); D.lm_zz = dp(o_lmz);
+    D.part_gbegin = ip(o_pgb); D.part_cbegin = ip(o_pcb2); D.part_contrib = ip(o_pcon); D.part_S = dp(o_partS);
     D.seg_hg = dp(o_shg); D.seg_uz = dp(o_suz); D.visit_Z = dp(o_vZ);
     D.seg_gbegin = ip(o_seg_gb); D.seg_pose = ip(o_seg_pose); D.seg_range = ip(o_seg_rg); D.visit_slot = ip(o_vslot);
     D.lmg_begin = ip(o_lmg_b); D.n_lmg = B.lmg_begin.empty() ? 0 : (int)B.lmg_begin.size() - 1;
@@ -1355,7 +1392,7 @@ double kernelWork(const HostBatch& B, const DevProblem& P, int k) {
       double desc = 0, pairs = 0;
       for (int it : B.asm_pp_items)
         if (it >= 0) { desc += B.pair_cbegin[it + 1] - B.pair_cbegin[it]; pairs += 1; }
-      return desc * 16 + nVis * kVisitZ * d8 + (double)P.n_seg * (21 + 6) * d8 + pairs * (36 + 12) * d8;
+      return desc * 16 + (double)P.n_part * 36 * d8 + (double)P.n_seg * (21 + 6) * d8 + pairs * (36 + 12) * d8;
     }
     case K_ASSEMBLE_SB: {
       double desc = 0, entries = 0;
@@ -1374,9 +1411,10 @@ double kernelWork(const HostBatch& B, const DevProblem& P, int k) {
     }
     case K_LM_VISIT:  // obs linearisation + params in; H|g and Z|Uz per visit, landmark blocks out
       return nObs * (kObsLin * d8 + 1) + nVis * (kVisitZ * d8 + 7 * d8 + 16) + (double)P.n_seg * (27 + 6) * d8 +
-             nLm * 40 * d8;
+             (double)B.part_contrib.size() * 4 + (double)P.n_part * 36 * d8 + nLm * 40 * d8;
     case K_LM_VISIT_PREP:  // W recomputed from the obs linearisation; Z|Uz out
-      return nObs * (kObsLin * d8 + 1) + nVis * (kVisitZ * d8 + 7 * d8 + 16) + (double)P.n_seg * 6 * d8 + nLm * 34 * d8;
+      return nObs * (kObsLin * d8 + 1) + nVis * (kVisitZ * d8 + 7 * d8 + 16) + (double)P.n_seg * 6 * d8 +
+             (double)B.part_contrib.size() * 4 + (double)P.n_part * 36 * d8 + nLm * 34 * d8;
     case K_EVAL_IMU: return nImu * (2.0 * kImuState + kImuLin + 2 * 16) * d8 + (double)B.imu_ts.size() * 7 * d8;
     case K_EVAL_OBS: return nObs * (16 + 32 + 13 + kObsLin * d8 + 8) + nLm * 4 * d8 + (double)B.pose_f.size() * 7 * d8;
     case K_JV: return nObs * (kObsLin * d8 + 1) + nVis * (7 + 4 + 3 * 9 + 3) * d8 + nImu * (kImuLin + 3) * d8;
