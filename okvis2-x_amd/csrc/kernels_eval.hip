@@ -278,7 +278,10 @@ __device__ void groupJacobi(double* A, double* V, double* rot, int l, bool need)
 
 }  // namespace
 
-__global__ __launch_bounds__(64) void k_eval_imu(const DevProblem* __restrict__ Pp, int mode) {
+#ifndef OKG_IMU_OCC
+#define OKG_IMU_OCC 1
+#endif
+__global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* __restrict__ Pp, int mode) {
   const DevProblem& P = *Pp;
   const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
   const int f = blockIdx.x * kImuPerWG + g;

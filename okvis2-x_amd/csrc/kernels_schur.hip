@@ -67,14 +67,17 @@ __device__ __forceinline__ bool lmVisitSelect(const DevProblem& P, int w, int mo
   return s.need_gn && !s.gn_failed && s.z_mu != s.mu;
 }
 
-__global__ __launch_bounds__(kLmGroupVisits) void k_lm_visit(const DevProblem* __restrict__ Pp, int mode) {
+#ifndef OKG_LMV_OCC
+#define OKG_LMV_OCC 3
+#endif
+__global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const DevProblem* __restrict__ Pp, int mode) {
   const DevProblem& P = *Pp;
   const int t = threadIdx.x;
   const int l0 = P.lmg_begin[blockIdx.x], l1 = P.lmg_begin[blockIdx.x + 1];
   const int v0 = P.lm_visit_begin[l0], v1 = P.lm_visit_begin[l1];
-  // sBuf rows 0..8: visit shares of V (6) | g_l (3); rows 9..22: visit values being summed into
+  // sBuf rows 0..8: visit shares of V (6) | g_l (3); rows 9..17: visit values being summed into
   // segments; finally rows 0..17: the visits' Z for the partial Schur blocks
-  __shared__ double sBuf[23][kLmGroupVisits];
+  __shared__ double sBuf[18][kLmGroupVisits];
   __shared__ double sLz[15][kLmGroupMax];    // per landmark: L^-1 (9) | zz (3) | s_l (3)
   __shared__ int sPC[kLmPartStage];          // the group's landmark-pair products (a | b << 16)
   double (*sVg)[kLmGroupVisits] = sBuf;
@@ -234,13 +237,13 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_visit(const DevProblem* _
   const int slot = hasV ? P.visit_slot[v] : -1;
   if (mode != 2) {
 #pragma unroll
-    for (int chunk = 0; chunk < 2; ++chunk) {
-      const int nval = chunk == 0 ? 14 : 13;
+    for (int chunk = 0; chunk < 3; ++chunk) {
+      const int nval = 9;
       if (slot >= 0)
 #pragma unroll
-        for (int i = 0; i < 14; ++i) {
-          const int e = 14 * chunk + i;
-          if (i < nval) sR[i][slot] = e < 21 ? H[e] : gp[e - 21];
+        for (int i = 0; i < 9; ++i) {
+          const int e = 9 * chunk + i;
+          sR[i][slot] = e < 21 ? H[e] : gp[e - 21];
         }
       __syncthreads();
       for (int e = t; e < nseg * nval; e += kLmGroupVisits) {
@@ -248,7 +251,7 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_visit(const DevProblem* _
         const int m0 = P.seg_range[2 * (sg0 + sgi)], m1 = P.seg_range[2 * (sg0 + sgi) + 1];
         double a = 0.0;
         for (int m = m0; m < m1; ++m) a += sR[i][m];
-        P.seg_hg[(size_t)(sg0 + sgi) * kSegHG + 14 * chunk + i] = a;
+        P.seg_hg[(size_t)(sg0 + sgi) * kSegHG + 9 * chunk + i] = a;
       }
       __syncthreads();
     }

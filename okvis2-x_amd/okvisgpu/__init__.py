@@ -16,7 +16,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
 REPO_ROOT = os.path.dirname(PKG_ROOT)
-LIB_PATH = os.path.join(PKG_ROOT, "libokvisgpu.so")
+LIB_PATH = os.environ.get("OKVISGPU_LIB") or os.path.join(PKG_ROOT, "libokvisgpu.so")  # env: A/B builds
 
 IMU_STATE_DOUBLES = 292
 

@@ -4,7 +4,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 make -s -C okvis2-x_amd clean && make -s -C okvis2-x_amd -j16 OPT="-O3 -DOKG_CHOL_CLOCK" || exit 1
 for n in ${CLKWINDOWS:-1 64 512}; do
-timeout -k 10 300 python - $n 3 <<'PY' || exit 1
+timeout -k 10 300 python - $n ${SCHED:-3} <<'PY' || exit 1
 import sys; sys.path.insert(0, 'okvis2-x_amd')
 import okvisgpu as og
 n = int(sys.argv[1])
