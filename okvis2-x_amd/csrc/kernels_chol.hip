@@ -114,6 +114,30 @@ __device__ __forceinline__ void storeTile(double* A, int64_t ld, int r0g, int c0
       }
 }
 
+// The C-layout values of a 64x64 global tile (as storeTile writes them), and C - acc stored back.
+__device__ __forceinline__ void loadC(const double* A, int64_t ld, dbl4 c[2][2], int t) {
+  const int wave = t >> 6, lane = t & 63;
+  const int r0 = 32 * (wave >> 1), c0 = 32 * (wave & 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg)
+        c[a][b][reg] = A[(int64_t)(r0 + 16 * a + (lane >> 4) + 4 * reg) * ld + c0 + 16 * b + (lane & 15)];
+}
+__device__ __forceinline__ void storeTileSub(double* A, int64_t ld, const dbl4 c[2][2], const dbl4 acc[2][2], int t) {
+  const int wave = t >> 6, lane = t & 63;
+  const int r0 = 32 * (wave >> 1), c0 = 32 * (wave & 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg)
+        A[(int64_t)(r0 + 16 * a + (lane >> 4) + 4 * reg) * ld + c0 + 16 * b + (lane & 15)] = c[a][b][reg] - acc[a][b][reg];
+}
+
 __device__ __forceinline__ double readlaneD(double v, int lane) {  // v of `lane`, wave-uniform
   const long long b = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)b, lane);
@@ -383,7 +407,8 @@ __global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__
     for (int i = k + 1; i < T; ++i)
       if (nz[i * T + k]) panelTile(S + i * kTile * ld + k * kTile, ld, work + i * kTile, sA, sX, sy, t);
     CLK(1)
-    // ---- trailing band update: A_ij -= L_ik L_jk^T, k < j <= i, both tiles non-zero
+    // ---- trailing band update: A_ij -= L_ik L_jk^T, k < j <= i, both tiles non-zero. The A_ij
+    // read of the read-modify-write is issued before the MFMAs, so its latency overlaps them.
     for (int i = k + 1; i < T; ++i) {
       if (!nz[i * T + k]) continue;
       loadTile(S + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
@@ -391,9 +416,11 @@ __global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__
         if (!nz[j * T + k]) continue;
         if (j != i) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sX, t);
         __syncthreads();
-        dbl4 acc[2][2];
+        double* Cij = S + i * kTile * ld + j * kTile;
+        dbl4 c[2][2], acc[2][2];
+        loadC(Cij, ld, c, t);
         mfmaTileNT(sA, j == i ? sA : sX, acc, t);
-        storeTile<true>(S + i * kTile * ld + j * kTile, ld, 0, 0, acc, t);
+        storeTileSub(Cij, ld, c, acc, t);
         __syncthreads();
       }
     }
