@@ -302,23 +302,38 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
   return true;
 }
 
-// L_ik = A_ik X^T (X = L_kk^-1 in sX, y_k in sy) stored over A_ik, and rhs_i -= L_ik y_k.
-__device__ void panelTile(double* Aik, int64_t ld, double* worki, double* sA, const double* sX, const double* sy,
+// z = X^T y_k (X = L_kk^-1 lower in sX, y_k in sy), so that the forward substitution update of
+// every panel is rhs_i -= L_ik y_k = A_ik z. Partials of four row quarters via sP (4 x 64).
+__device__ void panelRhsVector(const double* sX, const double* sy, double* sz, double* sP, int t) {
+  const int c = t & 63, q = t >> 6;
+  double a = 0.0;
+#pragma unroll
+  for (int r = 16 * q; r < 16 * q + 16; ++r) a += (r >= c) ? sX[r * kLd + c] * sy[r] : 0.0;
+  sP[q * kTile + c] = a;
+  __syncthreads();
+  if (t < kTile) sz[t] = (sP[t] + sP[kTile + t]) + (sP[2 * kTile + t] + sP[3 * kTile + t]);
+  __syncthreads();
+}
+
+// L_ik = A_ik X^T (X = L_kk^-1 in sX) stored over A_ik, and rhs_i -= A_ik z (z = X^T y_k in sz),
+// the row products formed from the A_ik tile in LDS while the MFMAs run.
+__device__ void panelTile(double* Aik, int64_t ld, double* worki, double* sA, const double* sX, const double* sz,
                           int t) {
   loadTile(Aik, ld, 0, 0, sA, t);
   __syncthreads();
   dbl4 acc[2][2];
   mfmaTileNT(sA, sX, acc, t);
-  __syncthreads();
-  storeTile<false>(Aik, ld, 0, 0, acc, t);
-  storeTile<false>(sA, kLd, 0, 0, acc, t);  // L_ik staged for the rhs update
-  __syncthreads();
-  if (t < kTile) {
+  {
+    const int row = t >> 2, q = t & 3;
     double a = 0.0;
-    for (int c = 0; c < kTile; ++c) a += sA[t * kLd + c] * sy[c];
-    worki[t] -= a;
+#pragma unroll
+    for (int c = 16 * q; c < 16 * q + 16; ++c) a += sA[row * kLd + c] * sz[c];
+    a += __shfl_xor(a, 1, 64);
+    a += __shfl_xor(a, 2, 64);
+    if (q == 0) worki[row] -= a;
   }
-  __syncthreads();
+  __syncthreads();  // sA is free for the next panel
+  storeTile<false>(Aik, ld, 0, 0, acc, t);
 }
 
 // Backward substitution x = L^-T y, x := y_F. sx (LDS, ld doubles) holds y on entry and x on
@@ -403,9 +418,10 @@ __global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__
       return;
     }
     CLK(0)
-    // ---- panel: L_ik = A_ik X^T, rhs_i -= L_ik y_k
+    // ---- panel: L_ik = A_ik X^T, rhs_i -= L_ik y_k = A_ik X^T y_k
+    panelRhsVector(sX, sy, sy + kTile, sA, t);
     for (int i = k + 1; i < T; ++i)
-      if (nz[i * T + k]) panelTile(S + i * kTile * ld + k * kTile, ld, work + i * kTile, sA, sX, sy, t);
+      if (nz[i * T + k]) panelTile(S + i * kTile * ld + k * kTile, ld, work + i * kTile, sA, sX, sy + kTile, t);
     CLK(1)
     // ---- trailing band update: A_ij -= L_ik L_jk^T, k < j <= i, both tiles non-zero. The A_ij
     // read of the read-modify-write is issued before the MFMAs, so its latency overlaps them.
@@ -475,12 +491,14 @@ __global__ __launch_bounds__(256) void k_chol_panel(const DevProblem* __restrict
   double* work = P.fwdF + P.win_fwdoff[w];
   __shared__ double sA[kTile * kLd];
   __shared__ double sX[kTile * kLd];
-  __shared__ double sy[kTile];
+  __shared__ double sy[2 * kTile];
   const int t = threadIdx.x;
   const double* X = P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile;
   loadTile(X, kTile, 0, 0, sX, t);
   if (t < kTile) sy[t] = work[k * kTile + t];
-  panelTile(P.S + P.win_soff[w] + i * kTile * ld + k * kTile, ld, work + i * kTile, sA, sX, sy, t);
+  __syncthreads();
+  panelRhsVector(sX, sy, sy + kTile, sA, t);
+  panelTile(P.S + P.win_soff[w] + i * kTile * ld + k * kTile, ld, work + i * kTile, sA, sX, sy + kTile, t);
 }
 
 // band updates of step k; the workgroup owning tile (k+1,k+1) factors it right after its update
@@ -503,9 +521,11 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
     loadTile(S + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
     if (j != i) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sX, t);
     __syncthreads();
-    dbl4 acc[2][2];
+    double* Cij = S + i * kTile * ld + j * kTile;
+    dbl4 c[2][2], acc[2][2];
+    loadC(Cij, ld, c, t);  // read of the read-modify-write overlaps the MFMAs
     mfmaTileNT(sA, j == i ? sA : sX, acc, t);
-    storeTile<true>(S + i * kTile * ld + j * kTile, ld, 0, 0, acc, t);
+    storeTileSub(Cij, ld, c, acc, t);
   }
   if (!(mode & 2)) return;
   double* work = P.fwdF + P.win_fwdoff[w];
