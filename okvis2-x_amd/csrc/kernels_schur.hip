@@ -70,7 +70,10 @@ __device__ __forceinline__ bool lmVisitSelect(const DevProblem& P, int w, int mo
 #ifndef OKG_LMV_OCC
 #define OKG_LMV_OCC 3
 #endif
-__global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const DevProblem* __restrict__ Pp, int mode) {
+// (mode is a template parameter: each mode is its own specialised kernel, and rocprof reports them
+// apart — k_lm_visit<1> is the per-iteration linearisation, k_lm_visit<2> the GN prep)
+template <int mode>
+__global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int t = threadIdx.x;
   const int l0 = P.lmg_begin[blockIdx.x], l1 = P.lmg_begin[blockIdx.x + 1];
@@ -187,15 +190,19 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
           }
           // LLT and inverse (InvertPSDMatrix, full rank)
           double Lc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-          bool ok = true;
-          for (int k = 0; k < 3 && ok; ++k) {
+          bool ok = true;  // (fully unrolled: no dynamically indexed private arrays)
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
             double d = A[k * 3 + k];
+#pragma unroll
             for (int j = 0; j < k; ++j) d -= Lc[k * 3 + j] * Lc[k * 3 + j];
-            if (!(d > 0.0)) { ok = false; break; }
-            d = sqrt(d);
+            ok = ok && (d > 0.0);
+            d = ok ? sqrt(d) : 1.0;
             Lc[k * 3 + k] = d;
+#pragma unroll
             for (int i = k + 1; i < 3; ++i) {
               double tt = A[i * 3 + k];
+#pragma unroll
               for (int j = 0; j < k; ++j) tt -= Lc[i * 3 + j] * Lc[k * 3 + j];
               Lc[i * 3 + k] = tt / d;
             }
@@ -205,10 +212,13 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
             st.gn_failed = 1;
           } else {
             // L^-1 (lower) and zz = L^-1 (s g): V'^-1 = L^-T L^-1, so Y_a U_b^T = Z_a Z_b^T, Z = U L^-T
+#pragma unroll
             for (int c = 0; c < 3; ++c) {
               Li[c * 3 + c] = 1.0 / Lc[c * 3 + c];
+#pragma unroll
               for (int i = c + 1; i < 3; ++i) {
                 double tt = 0.0;
+#pragma unroll
                 for (int j = c; j < i; ++j) tt -= Lc[i * 3 + j] * Li[j * 3 + c];
                 Li[i * 3 + c] = tt / Lc[i * 3 + i];
               }
@@ -730,7 +740,10 @@ __global__ __launch_bounds__(256) void k_gn_finalize(const DevProblem* __restric
 
 // ------------------------------------------------------------------------------------ launchers
 void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s) {
-  if (P.n_lmg > 0) hipLaunchKernelGGL(k_lm_visit, dim3(P.n_lmg), dim3(kLmGroupVisits), 0, s, P.self, mode);
+  if (P.n_lmg <= 0) return;
+  if (mode == 0) hipLaunchKernelGGL(k_lm_visit<0>, dim3(P.n_lmg), dim3(kLmGroupVisits), 0, s, P.self);
+  else if (mode == 1) hipLaunchKernelGGL(k_lm_visit<1>, dim3(P.n_lmg), dim3(kLmGroupVisits), 0, s, P.self);
+  else hipLaunchKernelGGL(k_lm_visit<2>, dim3(P.n_lmg), dim3(kLmGroupVisits), 0, s, P.self);
 }
 void launch_assemble_pp(const DevProblem& P, hipStream_t s) {
   if (P.n_asm_pp > 0) hipLaunchKernelGGL(k_assemble_pp, dim3((P.n_asm_pp + 3) / 4), dim3(256), 0, s, P.self);

@@ -1417,7 +1417,9 @@ double kernelWork(const HostBatch& B, const DevProblem& P, int k) {
              (double)B.part_contrib.size() * 4 + (double)P.n_part * 36 * d8 + nLm * 34 * d8;
     case K_EVAL_IMU: return nImu * (2.0 * kImuState + kImuLin + 2 * 16) * d8 + (double)B.imu_ts.size() * 7 * d8;
     case K_EVAL_OBS: return nObs * (16 + 32 + 13 + kObsLin * d8 + 8) + nLm * 4 * d8 + (double)B.pose_f.size() * 7 * d8;
-    case K_JV: return nObs * (kObsLin * d8 + 1) + nVis * (7 + 4 + 3 * 9 + 3) * d8 + nImu * (kImuLin + 3) * d8;
+    case K_JV:  // obs linearisation once; pose / landmark parameters and both operand vectors once per block
+      return nObs * (kObsLin * d8 + 1) + nVis * (3 * d8 + 8) + (double)P.n_pose * (7 + 12) * d8 +
+             nLm * (4 + 6) * d8 + nImu * (kImuLin + 3) * d8;
     case K_FGRAD: return (double)P.n_seg * 27 * d8 + nImu * kImuLin * d8 + (double)B.fb_contrib.size() * 16;
   }
   return 0.0;

@@ -25,9 +25,14 @@ for k, d in vals.items():
     w = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"]) * 1024
     kern[k] = {"fetch_bytes_per_dispatch": f, "write_bytes_per_dispatch": w, "bytes_per_dispatch": f + w}
     if k in ("k_assemble_pp", "k_assemble_sb", "k_eval_imu", "k_eval_obs", "k_fgrad", "k_cholesky", "k_lm_backsub",
-             "k_zero_S"):
+             "k_zero_S", "k_jv", "k_gn_finalize", "k_dogleg"):
         kern[k]["bytes_per_iteration"] = f + w  # one dispatch per iteration
-        kern[k]["bytes_per_window_iteration"] = (f + w) / windows
+    elif k == "k_lm_visit":
+        # two dispatches per iteration: the GN prep (mode 2, a no-op for windows whose Z is current)
+        # and the linearisation of the accepted step (mode 1): the heaviest dispatch is the latter
+        kern[k]["bytes_per_iteration"] = max(a * 2 + b for a, b in zip(d["FETCH_SIZE"], d["WRITE_SIZE"])) * 1024
+    if "bytes_per_iteration" in kern[k]:
+        kern[k]["bytes_per_window_iteration"] = kern[k]["bytes_per_iteration"] / windows
 json.dump({"source": sys.argv[3:], "windows": windows,
            "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane calibration), KiB -> bytes",
            "kernels": kern}, open(out, "w"), indent=1, sort_keys=True)
