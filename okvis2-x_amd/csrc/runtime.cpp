@@ -946,7 +946,7 @@ struct okvisgpu_ctx {
     // wave-specialised kernel (one workgroup per window, factorisation overlapped with the MFMA
     // tiles); beyond that the plain persistent kernel (two windows per CU)
     int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 3 ? o.cholesky_schedule : 0;
-    if (sched == 0) sched = P.n_win > cuCount ? 1 : (2 * P.n_win >= cuCount && wsFits() ? 3 : 2);
+    if (sched == 0) sched = P.n_win >= cuCount ? 1 : (2 * P.n_win >= cuCount && wsFits() ? 3 : 2);
     if (sched == 3 && !wsFits()) sched = 2;
     if (sched != P.chol_schedule && iterGraph) {
       (void)hipGraphExecDestroy(iterGraph);

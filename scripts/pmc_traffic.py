@@ -16,6 +16,9 @@ vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for path in sys.argv[3:]:
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"].split("(")[0].replace("okg::", "")
+        # the specialised k_lm_visit<mode> kernels under bench.py's table names
+        name = {"k_lm_visit<1>": "k_lm_visit", "k_lm_visit<2>": "k_lm_visit_prep", "k_lm_visit<0>": "k_lm_visit_init"}.get(
+            name, name)
         vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 kern = {}
 for k, d in vals.items():
@@ -27,9 +30,10 @@ for k, d in vals.items():
     if k in ("k_assemble_pp", "k_assemble_sb", "k_eval_imu", "k_eval_obs", "k_fgrad", "k_cholesky", "k_lm_backsub",
              "k_zero_S", "k_jv", "k_gn_finalize", "k_dogleg"):
         kern[k]["bytes_per_iteration"] = f + w  # one dispatch per iteration
-    elif k == "k_lm_visit":
-        # two dispatches per iteration: the GN prep (mode 2, a no-op for windows whose Z is current)
-        # and the linearisation of the accepted step (mode 1): the heaviest dispatch is the latter
+    elif k in ("k_lm_visit", "k_lm_visit_prep"):
+        # one dispatch each per iteration; the solve's dispatches only touch the windows that need
+        # them (accepted steps / stale Z), the roofline table's dispatches every window: the
+        # heaviest dispatch is the full-batch figure bench.py compares with
         kern[k]["bytes_per_iteration"] = max(a * 2 + b for a, b in zip(d["FETCH_SIZE"], d["WRITE_SIZE"])) * 1024
     if "bytes_per_iteration" in kern[k]:
         kern[k]["bytes_per_window_iteration"] = kern[k]["bytes_per_iteration"] / windows
