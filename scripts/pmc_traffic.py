@@ -15,7 +15,7 @@ windows = int(sys.argv[2])
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for path in sys.argv[3:]:
     for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].split("(")[0].replace("okg::", "")
+        name = r["Kernel_Name"].split("(")[0].replace("okg::", "").replace("void ", "")
         # the specialised k_lm_visit<mode> kernels under bench.py's table names
         name = {"k_lm_visit<1>": "k_lm_visit", "k_lm_visit<2>": "k_lm_visit_prep", "k_lm_visit<0>": "k_lm_visit_init"}.get(
             name, name)
