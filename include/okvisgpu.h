@@ -149,6 +149,13 @@ typedef struct okvisgpu_problem {
   const double* relpose_delta_x;    /* [n][6] DeltaX_                                           */
   const double* relpose_sqrt_info;  /* [n][36] J_ row-major (information = J_^T J_)             */
   const double* relpose_lin_point;  /* [n][7] linearisationPoint_T_S0S1_                        */
+  /* [n] residual kind (may be NULL = all 0):
+   *   0 TwoPoseStandardGraphError(Const): r = J_ (DeltaX_ + [r_S0S1 - r_lin; 2 vec(q_S0S1 q_lin^-1)])
+   *   1 RelativePoseError (RelativePoseError.cpp:59-140, added by ViGraph::addRelativePoseConstraint,
+   *     ViGraph.cpp:786-808, no loss): relpose_lin_point = the measured T_AB, relpose_sqrt_info =
+   *     LLT(information).L^T, relpose_delta_x unused;
+   *     r = L [r_AB_meas - r_AB; 2 vec(q_AB_meas q_AB^-1)], T_AB = T_WA^-1 T_WB                 */
+  const uint8_t* relpose_kind;
 } okvisgpu_problem;
 
 /* ---------------------------------------------------------------- solver options / summary */
@@ -339,6 +346,7 @@ typedef struct okvisgpu_synth_config {
    * 0 (default) = none, as in the benchmark windows. */
   int32_t n_relpose;
   int32_t relpose_stride;
+  int32_t relpose_kind;             /* 0 pose-graph edges, 1 RelativePoseError, 2 alternating */
 } okvisgpu_synth_config;
 
 typedef struct okvisgpu_synth_window okvisgpu_synth_window;  /* owns all arrays of one problem */

@@ -178,6 +178,7 @@ struct DevProblem {
   const int32_t* rp_blocks;        // [n][2] global reference pose, other pose
   const int32_t* rp_win;
   const uint8_t* rp_flags;         // bit1 fixed (both poses constant)
+  const uint8_t* rp_kind;          // 0 TwoPoseStandardGraphError(Const), 1 RelativePoseError
   const double* rp_dx;             // [n][6]  DeltaX_
   const double* rp_J;              // [n][36] J_
   const double* rp_lp;             // [n][7]  linearisationPoint_T_S0S1_

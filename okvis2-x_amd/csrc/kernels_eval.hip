@@ -808,8 +808,11 @@ __global__ __launch_bounds__(64) void k_eval_priors(const DevProblem* __restrict
     P.sbp_cost[lb][i] = 0.5 * c;
     return;
   }
-  // ---- relative-pose edge, TwoPoseStandardGraphError(Const)::EvaluateWithMinimalJacobians
-  // (TwoPoseGraphError.cpp:467-606 / :631-767), no loss function (ViGraphEstimator.cpp:770)
+  // ---- relative-pose residual blocks, no loss function:
+  //   kind 0 TwoPoseStandardGraphError(Const)::EvaluateWithMinimalJacobians (TwoPoseGraphError.cpp:
+  //          467-606 / :631-767; ViGraphEstimator.cpp:770)
+  //   kind 1 RelativePoseError::EvaluateWithMinimalJacobians (RelativePoseError.cpp:59-140;
+  //          ViGraph.cpp:786-808): T_AB measured in rp_lp, LLT(information).L^T in rp_J
   const int k = i - P.n_sbprior;
   if (k >= P.n_relpose) return;
   const int w = P.rp_win[k];
@@ -821,17 +824,27 @@ __global__ __launch_bounds__(64) void k_eval_priors(const DevProblem* __restrict
   const double* dx = P.rp_dx + 6 * (size_t)k;
   const double* Jq = P.rp_J + 36 * (size_t)k;
   const double* lp = P.rp_lp + 7 * (size_t)k;
+  const bool relErr = P.rp_kind[k] == 1;
   const Q q0 = qnormalize(Q{p0[3], p0[4], p0[5], p0[6]}), q1 = qnormalize(Q{p1[3], p1[4], p1[5], p1[6]});
-  const Q qlinv = qinv(qnormalize(Q{lp[3], lp[4], lp[5], lp[6]}));
+  const Q ql = qnormalize(Q{lp[3], lp[4], lp[5], lp[6]});
+  const Q qlinv = qinv(ql);
   double C0[9];
-  qrot(q0, C0);  // C_WS0; C_S0W = C0^T
+  qrot(q0, C0);  // C_WS0 (C_WA); C_S0W = C0^T
   const double d01[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
   double rS[3];
-  mtv3(C0, d01, rS);  // T_S0Si.r
+  mtv3(C0, d01, rS);  // T_S0Si.r (T_AB.r)
   const Q q0inv = qinv(q0);
-  const Q dq = qmul(qnormalize(qmul(q0inv, q1)), qlinv);  // T_S0Si.q * q_lin^-1
-  const double err[6] = {dx[0] + rS[0] - lp[0], dx[1] + rS[1] - lp[1], dx[2] + rS[2] - lp[2],
-                         dx[3] + 2.0 * dq.x, dx[4] + 2.0 * dq.y, dx[5] + 2.0 * dq.z};
+  const Q qrel = qnormalize(qmul(q0inv, q1));  // T_S0Si.q (T_AB.q)
+  double err[6];
+  if (relErr) {  // [r_AB_meas - r_AB; 2 vec(q_AB_meas q_AB^-1)]
+    const Q dq = qmul(ql, qinv(qrel));
+    err[0] = lp[0] - rS[0]; err[1] = lp[1] - rS[1]; err[2] = lp[2] - rS[2];
+    err[3] = 2.0 * dq.x; err[4] = 2.0 * dq.y; err[5] = 2.0 * dq.z;
+  } else {  // DeltaX_ + [r_S0Si - r_lin; 2 vec(q_S0Si q_lin^-1)]
+    const Q dq = qmul(qrel, qlinv);
+    err[0] = dx[0] + rS[0] - lp[0]; err[1] = dx[1] + rS[1] - lp[1]; err[2] = dx[2] + rS[2] - lp[2];
+    err[3] = dx[3] + 2.0 * dq.x; err[4] = dx[4] + 2.0 * dq.y; err[5] = dx[5] + 2.0 * dq.z;
+  }
   double* lin = P.rp_lin[lb] + kRelPoseLin * (size_t)k;
   double c = 0.0;
   for (int r = 0; r < 6; ++r) {
@@ -840,11 +853,18 @@ __global__ __launch_bounds__(64) void k_eval_priors(const DevProblem* __restrict
     lin[r] = s;
     c += s * s;
   }
-  // Jerr = [C_S0W 0; 0 B], B = (plus(q_WS0^-1) oplus(q_WS q_lin^-1))_3x3;
-  // JerrRef = [-C_S0W, C_S0W [r_WS - r_WS0]x; 0, -B]
+  // kind 0: Jerr = [C_S0W 0; 0 B], B = (plus(q_WS0^-1) oplus(q_WS q_lin^-1))_3x3,
+  //         JerrRef = [-C_S0W, C_S0W [r_WS - r_WS0]x; 0, -B]
+  // kind 1: J0 = [C_AW, -C_AW [r_WB - r_WA]x; 0, B], J1 = [-C_AW, 0; 0, -B],
+  //         B = (plus(q_AB_meas q_BW) oplus(q_WA))_3x3   (signs folded into sg below)
   double Pm[16], Om[16], B[9];
-  qplusM(q0inv, Pm);
-  qoplusM(qmul(q1, qlinv), Om);
+  if (relErr) {
+    qplusM(qmul(ql, qinv(q1)), Pm);
+    qoplusM(q0, Om);
+  } else {
+    qplusM(q0inv, Pm);
+    qoplusM(qmul(q1, qlinv), Om);
+  }
   for (int r = 0; r < 3; ++r)
     for (int q = 0; q < 3; ++q)
       B[r * 3 + q] = Pm[r * 4 + 0] * Om[0 * 4 + q] + Pm[r * 4 + 1] * Om[1 * 4 + q] + Pm[r * 4 + 2] * Om[2 * 4 + q] +
@@ -860,10 +880,11 @@ __global__ __launch_bounds__(64) void k_eval_priors(const DevProblem* __restrict
       const double jt = Jr[0] * C0[q * 3 + 0] + Jr[1] * C0[q * 3 + 1] + Jr[2] * C0[q * 3 + 2];  // (J C0^T)_q
       const double jb = Jr[3] * B[0 * 3 + q] + Jr[4] * B[1 * 3 + q] + Jr[5] * B[2 * 3 + q];
       const double jx = Jr[0] * CX[0 * 3 + q] + Jr[1] * CX[1 * 3 + q] + Jr[2] * CX[2 * 3 + q];
-      Lr[q] = -jt;          // reference pose, translation
-      Lr[3 + q] = jx - jb;  // reference pose, rotation
-      Lr[6 + q] = jt;       // other pose, translation
-      Lr[9 + q] = jb;       // other pose, rotation
+      const double sg = relErr ? -1.0 : 1.0;
+      Lr[q] = -sg * jt;          // reference pose, translation
+      Lr[3 + q] = sg * (jx - jb);  // reference pose, rotation
+      Lr[6 + q] = sg * jt;       // other pose, translation
+      Lr[9 + q] = sg * jb;       // other pose, rotation
     }
   }
   P.rp_cost[lb][k] = 0.5 * c;

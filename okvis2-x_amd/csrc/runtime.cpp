@@ -83,7 +83,7 @@ struct HostBatch {
   std::vector<double> pp_meas, pp_L, sbp_meas, sbp_L;
   // relative-pose edges
   std::vector<int32_t> rp_blocks, rp_win;
-  std::vector<uint8_t> rp_flags;
+  std::vector<uint8_t> rp_flags, rp_kind;
   std::vector<double> rp_dx, rp_J, rp_lp;
   // reduced structure
   std::vector<int32_t> win_foff, win_fdim, win_fpad;
@@ -154,6 +154,7 @@ void validate(const okvisgpu_problem* p, int w) {
       const int a = p->relpose_blocks[2 * i], b = p->relpose_blocks[2 * i + 1];
       if (a < 0 || a >= p->n_poses || b < 0 || b >= p->n_poses) bad("relative-pose block out of range");
       if (a == b) bad("relative-pose edge connects a pose to itself");
+      if (p->relpose_kind && p->relpose_kind[i] > 1) bad("unknown relative-pose kind");
     }
   }
 }
@@ -453,6 +454,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       B.rp_blocks.push_back(pb + p->relpose_blocks[2 * i + 1]);
       B.rp_win.push_back(w);
       B.rp_flags.push_back(rfix[i] ? 2 : 0);
+      B.rp_kind.push_back(p->relpose_kind ? p->relpose_kind[i] : 0);
       appendN(B.rp_dx, &p->relpose_delta_x[6 * i], 6);
       appendN(B.rp_J, &p->relpose_sqrt_info[36 * i], 36);
       appendN(B.rp_lp, &p->relpose_lin_point[7 * i], 7);
@@ -809,6 +811,7 @@ struct okvisgpu_ctx {
                  o_sbp_cost0 = scratch(sizeof(double) * D.n_sbprior), o_sbp_cost1 = scratch(sizeof(double) * D.n_sbprior),
                  o_sbp_jv = scratch(sizeof(double) * 3 * D.n_sbprior);
     const size_t o_rp_blocks = upl(B.rp_blocks), o_rp_win = upl(B.rp_win), o_rp_flags = upl(B.rp_flags),
+                 o_rp_kind = upl(B.rp_kind),
                  o_rp_dx = upl(B.rp_dx), o_rp_J = upl(B.rp_J), o_rp_lp = upl(B.rp_lp);
     const size_t o_rp_lin0 = scratch(sizeof(double) * kRelPoseLin * D.n_relpose),
                  o_rp_lin1 = scratch(sizeof(double) * kRelPoseLin * D.n_relpose),
@@ -880,7 +883,7 @@ struct okvisgpu_ctx {
     D.win_obs_range = ip(o_wor); D.win_imu_range = ip(o_wir); D.win_pp_range = ip(o_wppr);
     D.win_sbp_range = ip(o_wsbpr);
     D.win_rp_range = ip(o_wrpr);
-    D.rp_blocks = ip(o_rp_blocks); D.rp_win = ip(o_rp_win); D.rp_flags = up(o_rp_flags);
+    D.rp_blocks = ip(o_rp_blocks); D.rp_win = ip(o_rp_win); D.rp_flags = up(o_rp_flags); D.rp_kind = up(o_rp_kind);
     D.rp_dx = dp(o_rp_dx); D.rp_J = dp(o_rp_J); D.rp_lp = dp(o_rp_lp);
     D.rp_lin[0] = dp(o_rp_lin0); D.rp_lin[1] = dp(o_rp_lin1);
     D.rp_cost[0] = dp(o_rp_cost0); D.rp_cost[1] = dp(o_rp_cost1); D.rp_jv = dp(o_rp_jv);

@@ -33,6 +33,7 @@ struct okvisgpu_synth_window {
   std::vector<double> pp_meas, pp_L, sbp_meas, sbp_L;
   std::vector<int32_t> rp_blocks;
   std::vector<double> rp_dx, rp_J, rp_lin;
+  std::vector<uint8_t> rp_kind;
 };
 
 namespace {
@@ -90,6 +91,7 @@ void okvisgpu_synth_default_config(okvisgpu_synth_config* c, int32_t n_kf, int32
   c->seed = seed;
   c->n_relpose = 0;
   c->relpose_stride = 5;
+  c->relpose_kind = 0;
 }
 
 int okvisgpu_synth_create(const okvisgpu_synth_config* cfg, okvisgpu_synth_window** out) {
@@ -432,6 +434,9 @@ int okvisgpu_synth_create(const okvisgpu_synth_config* cfg, okvisgpu_synth_windo
       const int a = e % (nkf - cfg->relpose_stride), b = a + cfg->relpose_stride;
       W->rp_blocks.push_back(a);
       W->rp_blocks.push_back(b);
+      // kind 1 (RelativePoseError): the perturbed relative pose below is the measurement T_AB and
+      // the upper-triangular J_ is LLT(information).L^T of information = J_^T J_
+      W->rp_kind.push_back(cfg->relpose_kind == 2 ? (uint8_t)(e & 1) : (uint8_t)(cfg->relpose_kind == 1));
       // linearisation point: ground-truth T_S0S1 perturbed at the edge's noise level
       const double* p0 = &W->gt_poses[7 * a];
       const double* p1 = &W->gt_poses[7 * b];
@@ -499,6 +504,7 @@ int okvisgpu_synth_create(const okvisgpu_synth_config* cfg, okvisgpu_synth_windo
   P.relpose_delta_x = W->rp_dx.data();
   P.relpose_sqrt_info = W->rp_J.data();
   P.relpose_lin_point = W->rp_lin.data();
+  P.relpose_kind = W->rp_kind.data();
   *out = W;
   return OKVISGPU_OK;
 }

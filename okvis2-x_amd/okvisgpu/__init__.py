@@ -57,7 +57,7 @@ class Problem(C.Structure):
         ("n_sb_priors", C.c_int32), ("sb_prior_block", _ip), ("sb_prior_meas", _dp),
         ("sb_prior_sqrt_info", _dp),
         ("n_relpose", C.c_int32), ("relpose_blocks", _ip), ("relpose_delta_x", _dp),
-        ("relpose_sqrt_info", _dp), ("relpose_lin_point", _dp),
+        ("relpose_sqrt_info", _dp), ("relpose_lin_point", _dp), ("relpose_kind", _up),
     ]
 
 
@@ -93,7 +93,7 @@ class SynthConfig(C.Structure):
                 ("max_obs_per_landmark", C.c_int32), ("kf_dt_s", C.c_double), ("imu_rate_hz", C.c_double),
                 ("pixel_noise", C.c_double), ("init_sigma_pos", C.c_double), ("init_sigma_rot", C.c_double),
                 ("init_sigma_lm", C.c_double), ("init_sigma_vel", C.c_double), ("seed", C.c_uint64),
-                ("n_relpose", C.c_int32), ("relpose_stride", C.c_int32)]
+                ("n_relpose", C.c_int32), ("relpose_stride", C.c_int32), ("relpose_kind", C.c_int32)]
 
 
 class TwoPoseEdges(C.Structure):

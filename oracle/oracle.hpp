@@ -94,6 +94,12 @@ void sbErrorEvaluate(const double* meas, const double* sqrtInfo /*9x9*/, const d
 // (reference / other pose), J0/J1 ambient 6x7. Any output Jacobian may be null.
 void relPoseEvaluate(const double* dx, const double* Jsq, const double* lin, const double* pose0,
                      const double* pose1, double* r, double* Jmin0, double* Jmin1, double* J0, double* J1);
+// RelativePoseError::EvaluateWithMinimalJacobians (RelativePoseError.cpp:59-140), twopose.cpp.
+void relativePoseErrorEvaluate(const double* Tab, const double* Lsq, const double* pose0, const double* pose1,
+                               double* r, double* Jmin0, double* Jmin1, double* J0, double* J1);
+// The relative-pose residual block i of a problem: kind 0 graph edge, 1 RelativePoseError.
+void relPoseBlockEvaluate(const okvisgpu_problem* p, int i, const double* pose0, const double* pose1, double* r,
+                          double* Jmin0, double* Jmin1, double* J0, double* J1);
 // TwoPoseStandardGraphError::compute (TwoPoseGraphError.cpp:162-397) of edge e (twopose.cpp).
 void twoPoseCompute(const okvisgpu_twopose_edges* E, int e, double* deltaX, double* Jsq, double* linPoint,
                     double* H00, double* b0);

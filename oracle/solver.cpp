@@ -280,9 +280,8 @@ double evalResidual(Program& P, const std::vector<double>& x, int ri, double* re
     case rSbPrior:
       sbErrorEvaluate(&p->sb_prior_meas[9 * r.index], &p->sb_prior_sqrt_info[81 * r.index], prm[0], rr, ja[0]);
       break;
-    case rRelPose:  // no loss function (ViGraphEstimator.cpp:770)
-      relPoseEvaluate(&p->relpose_delta_x[6 * r.index], &p->relpose_sqrt_info[36 * r.index],
-                      &p->relpose_lin_point[7 * r.index], prm[0], prm[1], rr, nullptr, nullptr, ja[0], ja[1]);
+    case rRelPose:  // no loss function (ViGraphEstimator.cpp:770, ViGraph.cpp:801)
+      relPoseBlockEvaluate(p, r.index, prm[0], prm[1], rr, nullptr, nullptr, ja[0], ja[1]);
       break;
   }
   double sq = 0;
@@ -1097,9 +1096,8 @@ int oracle_check_jacobians(const okvisgpu_problem* p, int32_t kind, int32_t inde
       sbErrorEvaluate(&p->sb_prior_meas[9 * index], &p->sb_prior_sqrt_info[81 * index], prm[0], r,
                       jmin ? jmin[0] : nullptr);
     } else {
-      relPoseEvaluate(&p->relpose_delta_x[6 * index], &p->relpose_sqrt_info[36 * index],
-                      &p->relpose_lin_point[7 * index], prm[0], prm[1], r, jmin ? jmin[0] : nullptr,
-                      jmin ? jmin[1] : nullptr, nullptr, nullptr);
+      relPoseBlockEvaluate(p, index, prm[0], prm[1], r, jmin ? jmin[0] : nullptr, jmin ? jmin[1] : nullptr, nullptr,
+                           nullptr);
     }
   };
   std::vector<std::vector<double>> Ja(nb);
@@ -1152,8 +1150,7 @@ int oracle_eval_relpose(const okvisgpu_problem* p, double* r, double* J) {
   for (int i = 0; i < p->n_relpose; ++i) {
     const int* b = &p->relpose_blocks[2 * i];
     double J0[36], J1[36], rr6[6];
-    relPoseEvaluate(&p->relpose_delta_x[6 * i], &p->relpose_sqrt_info[36 * i], &p->relpose_lin_point[7 * i],
-                    &p->poses[7 * b[0]], &p->poses[7 * b[1]], rr6, J0, J1, nullptr, nullptr);
+    relPoseBlockEvaluate(p, i, &p->poses[7 * b[0]], &p->poses[7 * b[1]], rr6, J0, J1, nullptr, nullptr);
     if (r) for (int k = 0; k < 6; ++k) r[6 * i + k] = rr6[k];
     if (J)
       for (int rr = 0; rr < 6; ++rr)

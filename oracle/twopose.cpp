@@ -4,6 +4,7 @@
 //   TwoPoseStandardGraphError(Const)::Evaluate... okvis_ceres/src/TwoPoseGraphError.cpp:467-606,
 //                                                 :631-767 (both classes evaluate identically)
 //   PseudoInverse::symmSqrt                       okvis_ceres/include/okvis/PseudoInverse.hpp:101-129
+//   RelativePoseError::EvaluateWithMinimalJacobians okvis_ceres/src/RelativePoseError.cpp:59-140
 // Eigen's SelfAdjointEigenSolver is restated as a cyclic Jacobi eigen-solve with eigenvalues sorted
 // ascending; eigenvector signs are arbitrary in both, and everything the solver consumes (J_^T J_,
 // DeltaX_, the marginalised H00_ / b0_) is sign-invariant.
@@ -124,6 +125,48 @@ void relPoseEvaluate(const double* dx, const double* Jsq, const double* lin, con
   }
 }
 
+// RelativePoseError::EvaluateWithMinimalJacobians (RelativePoseError.cpp:59-140): T_AB measured,
+// L = LLT(information).L^T; parameters T_WA (pose0), T_WB (pose1).
+void relativePoseErrorEvaluate(const double* Tab, const double* Lsq, const double* pose0, const double* pose1,
+                               double* r, double* Jmin0, double* Jmin1, double* J0, double* J1) {
+  const Pose T_WA = poseOf(pose0), T_WB = poseOf(pose1), T_ABm = poseOf(Tab);
+  const Pose T_AW = inverse(T_WA), T_BW = inverse(T_WB);
+  const Pose T_AB = compose(T_AW, T_WB);
+  const V3 dr = T_ABm.r - T_AB.r;
+  const Quat dq = qmul(T_ABm.q, qinverse(T_AB.q));
+  const double e[6] = {dr.a[0], dr.a[1], dr.a[2], 2.0 * dq.x, 2.0 * dq.y, 2.0 * dq.z};
+  Mat<6, 6> L;
+  for (int i = 0; i < 36; ++i) L.a[i] = Lsq[i];
+  for (int i = 0; i < 6; ++i) {
+    double s = 0;
+    for (int k = 0; k < 6; ++k) s += L(i, k) * e[k];
+    r[i] = s;
+  }
+  if (!Jmin0 && !Jmin1 && !J0 && !J1) return;
+  const M3 C_AW = qrot(T_AW.q);
+  const M4 Pm = qplusMat(qmul(T_ABm.q, T_BW.q)) * qoplusMat(T_WA.q);
+  const M3 B = Pm.block<3, 3>(0, 0);
+  Mat<6, 6> A0 = Mat<6, 6>::Identity(), A1 = Mat<6, 6>::Identity();
+  A0.setBlock(0, 0, C_AW);
+  A0.setBlock(0, 3, -(C_AW * crossMx(T_WB.r - T_WA.r)));
+  A0.setBlock(3, 3, B);
+  A1.setBlock(0, 0, -C_AW);
+  A1.setBlock(3, 3, -B);
+  const Mat<6, 6> Jm0 = L * A0, Jm1 = L * A1;
+  if (Jmin0) for (int i = 0; i < 36; ++i) Jmin0[i] = Jm0.a[i];
+  if (Jmin1) for (int i = 0; i < 36; ++i) Jmin1[i] = Jm1.a[i];
+  if (J0) {
+    Mat<6, 7> Jl; poseMinusJacobian(pose0, Jl.a);
+    const Mat<6, 7> Ja = Jm0 * Jl;
+    for (int i = 0; i < 42; ++i) J0[i] = Ja.a[i];
+  }
+  if (J1) {
+    Mat<6, 7> Jl; poseMinusJacobian(pose1, Jl.a);
+    const Mat<6, 7> Ja = Jm1 * Jl;
+    for (int i = 0; i < 42; ++i) J1[i] = Ja.a[i];
+  }
+}
+
 // TwoPoseStandardGraphError::compute (TwoPoseGraphError.cpp:162-397) for edge e of the batch.
 void twoPoseCompute(const okvisgpu_twopose_edges* E, int e, double* deltaX, double* Jsq, double* linPoint,
                     double* H00out, double* b0out) {
@@ -225,6 +268,16 @@ void twoPoseCompute(const okvisgpu_twopose_edges* E, int e, double* deltaX, doub
   }
   if (H00out) for (int i = 0; i < 36; ++i) H00out[i] = H00_.a[i];
   if (b0out) for (int i = 0; i < 6; ++i) b0out[i] = b0_.a[i];
+}
+
+void relPoseBlockEvaluate(const okvisgpu_problem* p, int i, const double* pose0, const double* pose1, double* r,
+                          double* Jmin0, double* Jmin1, double* J0, double* J1) {
+  if (p->relpose_kind && p->relpose_kind[i] == 1)
+    relativePoseErrorEvaluate(&p->relpose_lin_point[7 * i], &p->relpose_sqrt_info[36 * i], pose0, pose1, r, Jmin0,
+                              Jmin1, J0, J1);
+  else
+    relPoseEvaluate(&p->relpose_delta_x[6 * i], &p->relpose_sqrt_info[36 * i], &p->relpose_lin_point[7 * i], pose0,
+                    pose1, r, Jmin0, Jmin1, J0, J1);
 }
 
 }  // namespace oracle

@@ -1,5 +1,7 @@
-"""GPU parity of the pose-graph edge (TwoPoseStandardGraphError, TwoPoseGraphError.cpp:162-767)
-through the C ABI against the CPU oracle (tests/test_oracle_twopose.py pins the oracle).
+"""GPU parity of the two-pose residual blocks through the C ABI against the CPU oracle
+(tests/test_oracle_twopose.py pins the oracle): the pose-graph edge (TwoPoseStandardGraphError,
+TwoPoseGraphError.cpp:162-767) and RelativePoseError (RelativePoseError.cpp:59-140); the synthetic
+windows mix both kinds unless a test says otherwise.
 
 Tolerances (FP64 both sides, different operation orders):
   * edge residuals / minimal Jacobians: 1e-12 relative to the block norm;
@@ -16,8 +18,9 @@ import _twopose as tp
 pytestmark = pytest.mark.gpu
 
 
-def _relpose_window(og, kf=10, lm=500, obs=4000, n_relpose=6, stride=3, seed=20251015):
-    return og.SynthWindow(kf, lm, obs, seed=seed, n_relpose=n_relpose, relpose_stride=stride)
+def _relpose_window(og, kf=10, lm=500, obs=4000, n_relpose=6, stride=3, seed=20251015, kind=2):
+    """kind 0 pose-graph edges, 1 RelativePoseError, 2 alternating."""
+    return og.SynthWindow(kf, lm, obs, seed=seed, n_relpose=n_relpose, relpose_stride=stride, relpose_kind=kind)
 
 
 def _opts(og, iters, **kw):
@@ -25,8 +28,9 @@ def _opts(og, iters, **kw):
                               parameter_tolerance=0.0, **kw)
 
 
-def test_relpose_functor_parity(og, oracle, gpu_ctx):
-    w = _relpose_window(og)
+@pytest.mark.parametrize("kind", [0, 1])
+def test_relpose_functor_parity(og, oracle, gpu_ctx, kind):
+    w = _relpose_window(og, kind=kind)
     P = w.poses()
     rng = np.random.default_rng(5)
     P[:, :3] += rng.normal(0, 0.05, P[:, :3].shape)  # away from the linearisation points

@@ -18,14 +18,37 @@ import okvisgpu as og
 import _twopose as tp
 
 
-def _relpose_window(n_relpose=6, stride=3, seed=20251015):
-    return og.SynthWindow(8, 200, 1600, seed=seed, n_relpose=n_relpose, relpose_stride=stride)
+def _relpose_window(n_relpose=6, stride=3, seed=20251015, kind=0):
+    return og.SynthWindow(8, 200, 1600, seed=seed, n_relpose=n_relpose, relpose_stride=stride, relpose_kind=kind)
 
 
-def test_relpose_jacobians(oracle):
-    w = _relpose_window()
+@pytest.mark.parametrize("kind", [0, 1])
+def test_relpose_jacobians(oracle, kind):
+    """kind 0: TwoPoseStandardGraphError(Const); kind 1: RelativePoseError (RelativePoseError.cpp)."""
+    w = _relpose_window(kind=kind)
     for i in range(w.problem.n_relpose):
         assert oracle.check_jacobians(w.problem_ptr(), 4, i) < 1e-6
+
+
+def test_relative_pose_error_at_measurement(oracle):
+    """RelativePoseError is zero with the measured T_AB, and its residual is L times the
+    [translation; 2 vec(dq)] error (RelativePoseError.cpp:70-86)."""
+    w = _relpose_window(kind=1, n_relpose=4)
+    p = w.problem
+    P = w.poses()
+    blocks = np.ctypeslib.as_array(p.relpose_blocks, (p.n_relpose, 2))
+    lin = np.ctypeslib.as_array(p.relpose_lin_point, (p.n_relpose, 7))
+    for i in range(p.n_relpose):
+        a, b = blocks[i]
+        # place pose b exactly at T_WA * T_AB_meas
+        Ra = tp.rot(P[a, 3:])
+        P[b, :3] = P[a, :3] + Ra @ lin[i, :3]
+        x0, y0, z0, w0 = P[a, 3:] / np.linalg.norm(P[a, 3:])
+        x1, y1, z1, w1 = lin[i, 3:]
+        P[b, 3:] = [w0 * x1 + x0 * w1 + y0 * z1 - z0 * y1, w0 * y1 + y0 * w1 + z0 * x1 - x0 * z1,
+                    w0 * z1 + z0 * w1 + x0 * y1 - y0 * x1, w0 * w1 - x0 * x1 - y0 * y1 - z0 * z1]
+        r, _ = oracle.eval_relpose(w.problem_ptr(), p.n_relpose)
+        assert np.abs(r[i]).max() < 1e-9
 
 
 def test_relpose_jacobians_rotated_reference(oracle):
@@ -120,8 +143,9 @@ def test_compute_without_other_observations(oracle):
     assert np.array_equal(out["lin_point"][0], [0, 0, 0, 0, 0, 0, 1])
 
 
-def test_oracle_solve_with_relpose_edges(oracle):
-    w = _relpose_window(n_relpose=5, stride=4)
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_oracle_solve_with_relpose_edges(oracle, kind):
+    w = _relpose_window(n_relpose=5, stride=4, kind=kind)
     opts = og.default_options(max_num_iterations=10)
     c0 = oracle.evaluate(w.problem_ptr())
     s = oracle.solve(w.problem_ptr(), opts)
