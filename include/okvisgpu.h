@@ -292,6 +292,25 @@ typedef struct okvisgpu_twopose_edges {
 int okvisgpu_twopose_compute(okvisgpu_ctx* ctx, const okvisgpu_twopose_edges* edges, double* delta_x,
                              double* sqrt_info, double* lin_point, double* H00, double* b0);
 
+/* ---------------------------------------------------------------- okvis Component graphs
+ * Component::load (okvis_ceres/src/Component.cpp:50-383) as an okvisgpu_problem: states (pose and
+ * speed/bias blocks, ordered by state id), landmarks (ordered by id), one extrinsics block per camera,
+ * EDGE_IMU factors with their measurements, EDGE_OBS reprojections with the measurement and the
+ * information 64/size^2 of the frame's FRAME:KEYPOINT (float, as cv::KeyPoint) and Cauchy(1). The
+ * camera intrinsics and IMU parameters are configuration (not in the file) and are passed in. No
+ * priors and no constant blocks are added: the caller freezes what its solve needs. Host only. */
+typedef struct okvisgpu_graph okvisgpu_graph;
+int okvisgpu_graph_load(const char* path, const okvisgpu_camera* cameras, int32_t n_cameras,
+                        const okvisgpu_imu_params* imu, okvisgpu_graph** out);
+/* The problem view into the graph's arrays (valid until destroy; solves write into them). */
+const okvisgpu_problem* okvisgpu_graph_problem(okvisgpu_graph* g);
+/* File ids of the states / landmarks in problem order and the state time stamps (may be NULL). */
+int okvisgpu_graph_ids(const okvisgpu_graph* g, uint64_t* state_ids, int64_t* state_t_ns, uint64_t* landmark_ids);
+void okvisgpu_graph_destroy(okvisgpu_graph* g);
+/* Component::save (Component.cpp:385-506) of a problem (one speed/bias block per state, isotropic
+ * reprojection information): ids = problem indices, time stamps from state_t_ns or the IMU factors. */
+int okvisgpu_graph_save(const okvisgpu_problem* p, const int64_t* state_t_ns, const char* path);
+
 /* Copy device parameter values back into the caller's host arrays without solving. */
 int okvisgpu_get_params(okvisgpu_ctx* ctx);
 

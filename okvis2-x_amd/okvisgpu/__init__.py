@@ -114,6 +114,8 @@ EXPORTED_SYMBOLS = [
     "okvisgpu_solve_begin", "okvisgpu_solve_iterate", "okvisgpu_solve_end", "okvisgpu_synchronize",
     "okvisgpu_profile_iteration", "okvisgpu_phase_name", "okvisgpu_kernel_count", "okvisgpu_kernel_name",
     "okvisgpu_time_kernel", "okvisgpu_eval_relpose", "okvisgpu_twopose_compute",
+    "okvisgpu_graph_load", "okvisgpu_graph_problem", "okvisgpu_graph_ids", "okvisgpu_graph_destroy",
+    "okvisgpu_graph_save",
 ]
 N_PHASES = 15
 
@@ -162,6 +164,13 @@ def lib():
         L.okvisgpu_kernel_name.restype = C.c_char_p
         L.okvisgpu_time_kernel.argtypes = [C.c_void_p, C.c_int32, C.c_int32, _dp, _dp, C.POINTER(C.c_int32)]
         L.okvisgpu_eval_relpose.argtypes = [C.c_void_p, C.c_int32, _dp, _dp]
+        L.okvisgpu_graph_load.argtypes = [C.c_char_p, C.POINTER(Camera), C.c_int32, C.POINTER(ImuParams),
+                                          C.POINTER(C.c_void_p)]
+        L.okvisgpu_graph_problem.argtypes = [C.c_void_p]
+        L.okvisgpu_graph_problem.restype = C.POINTER(Problem)
+        L.okvisgpu_graph_ids.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), _lp, C.POINTER(C.c_uint64)]
+        L.okvisgpu_graph_destroy.argtypes = [C.c_void_p]
+        L.okvisgpu_graph_save.argtypes = [C.POINTER(Problem), _lp, C.c_char_p]
         L.okvisgpu_twopose_compute.argtypes = [C.c_void_p, C.POINTER(TwoPoseEdges), _dp, _dp, _dp, _dp, _dp]
         _lib = L
     return _lib
@@ -290,6 +299,57 @@ class TwoPoseBatch:
         s.obs_sqrt_info = dptr(self.L)
         s.obs_cauchy = self.ca.ctypes.data_as(_up)
         self.struct = s
+
+
+class Graph:
+    """An okvis Component text graph loaded into an okvisgpu problem (okvisgpu_graph_load)."""
+
+    def __init__(self, path, cameras, imu_params):
+        cams = (Camera * len(cameras))(*cameras)
+        h = C.c_void_p()
+        rc = lib().okvisgpu_graph_load(str(path).encode(), cams, len(cameras), C.byref(imu_params), C.byref(h))
+        if rc != 0:
+            raise OkvisGpuError(f"okvisgpu_graph_load({path}) failed ({rc})")
+        self.handle = h
+
+    @property
+    def problem(self) -> Problem:
+        return lib().okvisgpu_graph_problem(self.handle).contents
+
+    def problem_ptr(self):
+        return lib().okvisgpu_graph_problem(self.handle)
+
+    def ids(self):
+        p = self.problem
+        sid = (C.c_uint64 * p.n_poses)()
+        lid = (C.c_uint64 * max(1, p.n_landmarks))()
+        t = np.zeros(p.n_poses, dtype=np.int64)
+        lib().okvisgpu_graph_ids(self.handle, sid, t.ctypes.data_as(_lp), lid)
+        return np.array(sid[:], dtype=np.uint64), t, np.array(lid[:p.n_landmarks], dtype=np.uint64)
+
+    def poses(self):
+        p = self.problem
+        return np.ctypeslib.as_array(p.poses, shape=(p.n_poses, 7))
+
+    def landmarks(self):
+        p = self.problem
+        return np.ctypeslib.as_array(p.landmarks, shape=(p.n_landmarks, 4))
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                lib().okvisgpu_graph_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+def save_graph(problem_ptr, path, state_t_ns=None):
+    """okvisgpu_graph_save: write a problem as an okvis Component text graph."""
+    t = None if state_t_ns is None else np.ascontiguousarray(state_t_ns, dtype=np.int64).ctypes.data_as(_lp)
+    rc = lib().okvisgpu_graph_save(problem_ptr, t, str(path).encode())
+    if rc != 0:
+        raise OkvisGpuError(f"okvisgpu_graph_save({path}) failed ({rc})")
 
 
 class Context:

@@ -294,3 +294,43 @@ def test_cholesky_schedules_agree(og, oracle, gpu_ctx):
         assert res[2][0][k]["final_cost"] == pytest.approx(res[0][0][k]["final_cost"], rel=1e-9)
         np.testing.assert_allclose(res[2][1][k], res[0][1][k], rtol=0, atol=1e-7)
     _close(res[2][0][0], so)
+
+
+def test_graph_file_solve_parity(og, oracle, gpu_ctx, tmp_path):
+    """A window written as an okvis Component graph and loaded back (okvisgpu_graph_save / _load)
+    solves on the GPU like the oracle on the same loaded arrays."""
+    import ctypes as C
+    w = _window(og, seed=25)
+    path = tmp_path / "w.graph"
+    og.save_graph(w.problem_ptr(), path)
+    p = w.problem
+    cams = [og.Camera() for _ in range(p.n_cameras)]
+    for i in range(p.n_cameras):
+        C.pointer(cams[i])[0] = p.cameras[i]
+    opts = og.default_options(max_num_iterations=5, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    g = og.Graph(path, cams, p.imu_params)
+    g.problem.pose_constant[0] = 1  # gauge: the loaded full graph carries no priors
+    gpu_ctx.set_problems([g.problem])
+    sg = gpu_ctx.solve(opts, 1)[0]
+    P = g.poses().copy()
+    g2 = og.Graph(path, cams, p.imu_params)
+    g2.problem.pose_constant[0] = 1
+    so = oracle.solve(g2.problem_ptr(), opts)
+    _close(sg, so)
+    assert np.abs(P[:, :3] - g2.poses()[:, :3]).max() <= 1e-6
+
+
+def test_large_window_parity(og, oracle, gpu_ctx):
+    """A 200-keyframe window (reduced dimension 3,000, 47 tiles: the full-graph / final-BA size
+    class) against the oracle: two iterations."""
+    w = og.SynthWindow(200, 8000, 64000, seed=26)
+    opts = og.default_options(max_num_iterations=2, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0, num_threads=8)
+    gpu_ctx.set_problems([w.problem])
+    sg = gpu_ctx.solve(opts, 1)[0]
+    P = w.poses().copy()
+    w.reset()
+    so = oracle.solve(w.problem_ptr(), opts)
+    _close(sg, so, rel=1e-6)
+    assert np.abs(P[:, :3] - w.poses()[:, :3]).max() <= 1e-6
