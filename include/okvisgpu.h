@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OKVISGPU_ABI_VERSION 2
+#define OKVISGPU_ABI_VERSION 3
 
 /* ---------------------------------------------------------------- status codes */
 typedef enum okvisgpu_status {
@@ -48,7 +48,8 @@ typedef enum okvisgpu_status {
 typedef enum okvisgpu_distortion {
   OKVISGPU_DIST_NONE = 0,           /* okvis_cv/.../NoDistortion.hpp */
   OKVISGPU_DIST_RADTAN = 1,         /* okvis_cv/.../implementation/RadialTangentialDistortion.hpp:70-137 */
-  OKVISGPU_DIST_EQUIDISTANT = 2     /* okvis_cv/.../implementation/EquidistantDistortion.hpp:67-188 */
+  OKVISGPU_DIST_EQUIDISTANT = 2,    /* okvis_cv/.../implementation/EquidistantDistortion.hpp:67-188 */
+  OKVISGPU_DIST_RADTAN8 = 3         /* okvis_cv/.../implementation/RadialTangentialDistortion8.hpp:88-170 */
 } okvisgpu_distortion;
 
 typedef enum okvisgpu_linear_solver {
@@ -71,7 +72,8 @@ typedef struct okvisgpu_camera {
   int32_t distortion;               /* okvisgpu_distortion */
   int32_t width, height;
   double fu, fv, cu, cv;            /* PinholeCamera intrinsics (PinholeCamera.hpp:288-366) */
-  double dist[4];                   /* radtan: k1 k2 p1 p2 ; equidistant: k1 k2 k3 k4 */
+  double dist[8];                   /* radtan: k1 k2 p1 p2 ; equidistant: k1 k2 k3 k4 ;
+                                       radtan8: k1 k2 p1 p2 k3 k4 k5 k6 (unused entries 0) */
 } okvisgpu_camera;
 
 typedef struct okvisgpu_imu_params { /* okvis::ImuParameters subset, okvis_common/.../Parameters.hpp:89-105 */

@@ -17,6 +17,7 @@
 
 namespace okg {
 
+constexpr int kCamDoubles = 13;       // per camera on the device: dist, fu, fv, cu, cv, 8 distortion parameters
 constexpr int kTile = 64;             // Cholesky tile (one 64x64 FP64 tile = 32 KiB of LDS)
 constexpr int kImuLin = 15 + 15 * 30; // per-IMU-factor linearisation record: r[15], J[15][30]
 constexpr int kImuState = 292;        // == OKVISGPU_IMU_STATE_DOUBLES
@@ -90,7 +91,7 @@ struct DevProblem {
   double* sb[2];                   // [n_sb][9]
   double* lm[2];                   // [n_lm][4]
   const double* extr;              // [n_cam][7]
-  const double* cam;               // [n_cam][9]: dist, fu, fv, cu, cv, d0..d3 (dist as double)
+  const double* cam;               // [n_cam][kCamDoubles]: dist, fu, fv, cu, cv, d0..d7 (dist as double)
 
   // --- per-block window id and reduced-system offsets (-1: not a free f-block / e-block)
   const int32_t* pose_win;         // [n_pose]
@@ -260,7 +261,7 @@ struct TwoPoseDev {
   int32_t n_edges, n_cam;
   const double* ref_pose;     // [n_edges][7]
   const double* other_pose;   // [n_edges][7]
-  const double* cam;          // [n_cam][9] as DevProblem::cam
+  const double* cam;          // [n_cam][kCamDoubles] as DevProblem::cam
   const double* extr;         // [n_cam][7]
   const int32_t* lm_begin;    // [n_edges+1]
   const double* lm;           // [n_lm][4]

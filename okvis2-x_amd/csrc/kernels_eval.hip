@@ -56,8 +56,7 @@ __global__ __launch_bounds__(256) void k_eval_obs(const DevProblem* __restrict__
   const double* hp = P.lm[xs] + 4 * (size_t)P.obs_lm[o];
   const int ci = P.obs_cam[o];
   const double* ex = P.extr + 7 * ci;
-  const double* cp = P.cam + 9 * ci;
-  const Cam cam{(int)cp[0], cp[1], cp[2], cp[3], cp[4], cp[5], cp[6], cp[7], cp[8]};
+  const Cam cam = loadCam(P.cam + kCamDoubles * ci);
 
   double C_WS[9], C_SC[9];
   qrot(qnormalize(Q{pose[3], pose[4], pose[5], pose[6]}), C_WS);

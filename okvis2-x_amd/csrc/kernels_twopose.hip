@@ -72,8 +72,7 @@ __global__ __launch_bounds__(64) void k_twopose_compute(TwoPoseDev T) {
       const bool other = T.obs_other[o] != 0;
       sawOther = sawOther || other;
       const int ci = T.obs_cam[o];
-      const double* cp = T.cam + 9 * ci;
-      const Cam cam{(int)cp[0], cp[1], cp[2], cp[3], cp[4], cp[5], cp[6], cp[7], cp[8]};
+      const Cam cam = loadCam(T.cam + kCamDoubles * ci);
       double r[2], A[6], p[3];
       reprojectA(cam, other ? rel : ident, hp, T.extr + 7 * ci, T.obs_L + 4 * (size_t)o, T.obs_kp + 2 * (size_t)o, r,
                  A, p);

@@ -133,8 +133,12 @@ OKG_HD double durToSec(int64_t dns) {
 struct Cam {
   int dist;
   double fu, fv, cu, cv;
-  double d0, d1, d2, d3;
+  double d0, d1, d2, d3, d4, d5, d6, d7;
 };
+// [dist, fu, fv, cu, cv, d0..d7] (DevProblem::cam)
+OKG_HD Cam loadCam(const double* c) {
+  return Cam{(int)c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9], c[10], c[11], c[12]};
+}
 
 // distortion_.distort (RadialTangentialDistortion.hpp:89-137, EquidistantDistortion.hpp:87-188)
 OKG_HD void distort(const Cam& c, double u0, double u1, double& o0, double& o1, double Jd[4], bool wantJ) {
@@ -150,6 +154,27 @@ OKG_HD void distort(const Cam& c, double u0, double u1, double& o0, double& o1, 
       Jd[2] = k1 * 2.0 * u0 * u1 + k2 * 4 * rho_u * u0 * u1 + p1 * 2.0 * u0 + 2.0 * p2 * u1;
       Jd[1] = Jd[2];
       Jd[3] = 1 + rad + k1 * 2.0 * my_u + k2 * rho_u * 4 * my_u + 6 * p1 * u1 + 2.0 * p2 * u0;
+    }
+  } else if (c.dist == 3) {
+    // RadialTangentialDistortion8 (k1 k2 p1 p2 k3 k4 k5 k6): rational radial model. The reference
+    // returns false for rho > 9 and then reads uninitialised outputs; the model is evaluated there.
+    const double k1 = c.d0, k2 = c.d1, p1 = c.d2, p2 = c.d3, k3 = c.d4, k4 = c.d5, k5 = c.d6, k6 = c.d7;
+    const double mx_u = u0 * u0, my_u = u1 * u1, mxy_u = u0 * u1;
+    const double rho_u = mx_u + my_u;
+    const double num = 1.0 + ((k3 * rho_u + k2) * rho_u + k1) * rho_u;
+    const double den = 1.0 + ((k6 * rho_u + k5) * rho_u + k4) * rho_u;
+    const double rad = num / den;
+    o0 = u0 * rad + 2.0 * p1 * mxy_u + p2 * (rho_u + 2.0 * mx_u);
+    o1 = u1 * rad + 2.0 * p2 * mxy_u + p1 * (rho_u + 2.0 * my_u);
+    if (wantJ) {
+      // d rad / d rho = (num' den - num den') / den^2, d rho / du = 2u
+      const double dnum = k1 + rho_u * (2.0 * k2 + 3.0 * k3 * rho_u);
+      const double dden = k4 + rho_u * (2.0 * k5 + 3.0 * k6 * rho_u);
+      const double drad = (dnum * den - num * dden) / (den * den);
+      Jd[0] = rad + 2.0 * mx_u * drad + 2.0 * p1 * u1 + 6.0 * p2 * u0;
+      Jd[1] = 2.0 * mxy_u * drad + 2.0 * p1 * u0 + 2.0 * p2 * u1;
+      Jd[2] = Jd[1];
+      Jd[3] = rad + 2.0 * my_u * drad + 6.0 * p1 * u1 + 2.0 * p2 * u0;
     }
   } else if (c.dist == 2) {
     const double k1 = c.d0, k2 = c.d1, k3 = c.d2, k4 = c.d3;

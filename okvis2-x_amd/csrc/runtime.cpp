@@ -130,7 +130,7 @@ void validate(const okvisgpu_problem* p, int w) {
     }
   }
   for (int c = 0; c < p->n_cameras; ++c)
-    if (p->cameras[c].distortion < 0 || p->cameras[c].distortion > 2) bad("unknown distortion model");
+    if (p->cameras[c].distortion < 0 || p->cameras[c].distortion > 3) bad("unknown distortion model");
   if (p->n_imu) {
     if (!p->imu_blocks || !p->imu_t0_ns || !p->imu_t1_ns || !p->imu_sample_begin || !p->imu_sample_t_ns ||
         !p->imu_sample_gyr_acc)
@@ -171,7 +171,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     const okvisgpu_problem* p = probs[w];
     validate(p, w);
     const int pb = (int)B.pose_win.size(), sbb = (int)B.sb_win.size(), lb = (int)B.lm_win.size();
-    const int cb = (int)(B.cam.size() / 9), ob = (int)B.obs_win.size(), ib = (int)B.imu_win.size();
+    const int cb = (int)(B.cam.size() / kCamDoubles), ob = (int)B.obs_win.size(), ib = (int)B.imu_win.size();
     const int ppb = (int)B.pp_win.size(), sbpb = (int)B.sbp_win.size(), rpb = (int)B.rp_win.size();
     B.pose_base.push_back(pb); B.sb_base.push_back(sbb); B.lm_base.push_back(lb); B.cam_base.push_back(cb);
     B.obs_base.push_back(ob); B.imu_base.push_back(ib); B.pp_base.push_back(ppb); B.sbp_base.push_back(sbpb);
@@ -206,8 +206,9 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     }
     for (int c = 0; c < p->n_cameras; ++c) {
       const okvisgpu_camera& k = p->cameras[c];
-      const double cv[9] = {(double)k.distortion, k.fu, k.fv, k.cu, k.cv, k.dist[0], k.dist[1], k.dist[2], k.dist[3]};
-      appendN(B.cam, cv, 9);
+      const double cv[kCamDoubles] = {(double)k.distortion, k.fu, k.fv, k.cu, k.cv, k.dist[0], k.dist[1],
+                                      k.dist[2], k.dist[3], k.dist[4], k.dist[5], k.dist[6], k.dist[7]};
+      appendN(B.cam, cv, kCamDoubles);
       appendN(B.extr, &p->extrinsics[7 * c], 7);
     }
     for (int i = 0; i < p->n_poses; ++i) B.pose_win.push_back(w);
@@ -749,7 +750,7 @@ struct okvisgpu_ctx {
     D.n_pprior = (int)B.pp_win.size();
     D.n_sbprior = (int)B.sbp_win.size();
     D.n_relpose = (int)B.rp_win.size();
-    D.n_cam = (int)(B.cam.size() / 9);
+    D.n_cam = (int)(B.cam.size() / kCamDoubles);
     D.n_fblock = (int)B.fb_win.size();
     D.n_pair = (int)B.pair_win.size();
     D.max_fpad = B.max_fpad;
@@ -1663,12 +1664,13 @@ int okvisgpu_twopose_compute(okvisgpu_ctx* c, const okvisgpu_twopose_edges* E, d
       throw ArgError{"twopose_compute: observation arrays missing"};
     for (int o = 0; o < no; ++o)
       if (E->obs_camera[o] < 0 || E->obs_camera[o] >= E->n_cameras) throw ArgError{"twopose_compute: obs_camera out of range"};
-    std::vector<double> cam((size_t)9 * std::max(1, E->n_cameras));
+    std::vector<double> cam((size_t)kCamDoubles * std::max(1, E->n_cameras));
     for (int k = 0; k < E->n_cameras; ++k) {
       const okvisgpu_camera& q = E->cameras[k];
-      if (q.distortion < 0 || q.distortion > 2) throw ArgError{"twopose_compute: unknown distortion model"};
-      const double cv[9] = {(double)q.distortion, q.fu, q.fv, q.cu, q.cv, q.dist[0], q.dist[1], q.dist[2], q.dist[3]};
-      std::memcpy(&cam[9 * (size_t)k], cv, sizeof(cv));
+      if (q.distortion < 0 || q.distortion > 3) throw ArgError{"twopose_compute: unknown distortion model"};
+      const double cv[kCamDoubles] = {(double)q.distortion, q.fu, q.fv, q.cu, q.cv, q.dist[0], q.dist[1],
+                                      q.dist[2], q.dist[3], q.dist[4], q.dist[5], q.dist[6], q.dist[7]};
+      std::memcpy(&cam[kCamDoubles * (size_t)k], cv, sizeof(cv));
     }
     std::vector<uint8_t> cauchy(std::max(1, no), 1);
     if (E->obs_cauchy) for (int o = 0; o < no; ++o) cauchy[o] = E->obs_cauchy[o] ? 1 : 0;

@@ -135,7 +135,8 @@ int okvisgpu_synth_create(const okvisgpu_synth_config* cfg, okvisgpu_synth_windo
   }
   okg::Cam gcam[2];
   for (int c = 0; c < 2; ++c)
-    gcam[c] = okg::Cam{1, foc[c][0], foc[c][1], pp[c][0], pp[c][1], dist[c][0], dist[c][1], dist[c][2], dist[c][3]};
+    gcam[c] = okg::Cam{1, foc[c][0], foc[c][1], pp[c][0], pp[c][1], dist[c][0], dist[c][1], dist[c][2], dist[c][3],
+                       0.0, 0.0, 0.0, 0.0};
 
   // ---------------- IMU parameters: config/euroc/okvis2.yaml:49-61
   okvisgpu_imu_params ip;

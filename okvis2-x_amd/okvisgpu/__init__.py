@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("OKVISGPU_LIB") or os.path.join(PKG_ROOT, "libokvisgpu
 
 IMU_STATE_DOUBLES = 292
 
-DIST_NONE, DIST_RADTAN, DIST_EQUIDISTANT = 0, 1, 2
+DIST_NONE, DIST_RADTAN, DIST_EQUIDISTANT, DIST_RADTAN8 = 0, 1, 2, 3
 TERMINATION = {0: "CONVERGENCE", 1: "NO_CONVERGENCE", 2: "FAILURE", 3: "USER_SUCCESS"}
 
 _dp = C.POINTER(C.c_double)
@@ -32,7 +32,7 @@ _up = C.POINTER(C.c_uint8)
 class Camera(C.Structure):
     _fields_ = [("distortion", C.c_int32), ("width", C.c_int32), ("height", C.c_int32),
                 ("fu", C.c_double), ("fv", C.c_double), ("cu", C.c_double), ("cv", C.c_double),
-                ("dist", C.c_double * 4)]
+                ("dist", C.c_double * 8)]
 
 
 class ImuParams(C.Structure):

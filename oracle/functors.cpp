@@ -61,6 +61,36 @@ static void distort(const Camera& cam, double u0, double u1, double out[2], doub
         Jd[0] = 1; Jd[1] = 0; Jd[2] = 0; Jd[3] = 1;
       }
     }
+  } else if (cam.dist == OKVISGPU_DIST_RADTAN8) {
+    // RadialTangentialDistortion8::distort (RadialTangentialDistortion8.hpp:88-170). The reference
+    // returns false for rho > 9 and PinholeCamera::project (PinholeCamera.hpp:311-354) still writes
+    // the keypoint from the (then uninitialised) outputs while ReprojectionError ignores the status;
+    // here the model is evaluated there too.
+    const double k1 = cam.d[0], k2 = cam.d[1], p1 = cam.d[2], p2 = cam.d[3];
+    const double k3 = cam.d[4], k4 = cam.d[5], k5 = cam.d[6], k6 = cam.d[7];
+    const double mx_u = u0 * u0, my_u = u1 * u1, mxy_u = u0 * u1;
+    const double rho_u = mx_u + my_u;
+    const double num = rho_u * (k1 + rho_u * (k2 + k3 * rho_u)) + 1.0;
+    const double den = rho_u * (k4 + rho_u * (k5 + k6 * rho_u)) + 1.0;
+    const double rad = num / den;
+    out[0] = u0 * rad + 2.0 * p1 * mxy_u + p2 * (rho_u + 2.0 * mx_u);
+    out[1] = u1 * rad + 2.0 * p2 * mxy_u + p1 * (rho_u + 2.0 * my_u);
+    if (Jd) {
+      // d num / d u_j and d den / d u_j, expanded as in the reference's J(i, j) expressions
+      const double dn[2] = {rho_u * (u0 * (k2 + k3 * rho_u) * 2.0 + k3 * u0 * rho_u * 2.0) +
+                                u0 * (k1 + rho_u * (k2 + k3 * rho_u)) * 2.0,
+                            rho_u * (u1 * (k2 + k3 * rho_u) * 2.0 + k3 * u1 * rho_u * 2.0) +
+                                u1 * (k1 + rho_u * (k2 + k3 * rho_u)) * 2.0};
+      const double dd[2] = {rho_u * (u0 * (k5 + k6 * rho_u) * 2.0 + k6 * u0 * rho_u * 2.0) +
+                                u0 * (k4 + rho_u * (k5 + k6 * rho_u)) * 2.0,
+                            rho_u * (u1 * (k5 + k6 * rho_u) * 2.0 + k6 * u1 * rho_u * 2.0) +
+                                u1 * (k4 + rho_u * (k5 + k6 * rho_u)) * 2.0};
+      const double c2 = den * den;
+      Jd[0] = p1 * u1 * 2.0 + p2 * u0 * 6.0 + rad + u0 * dn[0] / den - u0 * dd[0] * num / c2;
+      Jd[1] = p1 * u0 * 2.0 + p2 * u1 * 2.0 + u0 * dn[1] / den - u0 * dd[1] * num / c2;
+      Jd[2] = p1 * u0 * 2.0 + p2 * u1 * 2.0 + u1 * dn[0] / den - u1 * dd[0] * num / c2;
+      Jd[3] = p1 * u1 * 6.0 + p2 * u0 * 2.0 + rad + u1 * dn[1] / den - u1 * dd[1] * num / c2;
+    }
   } else {
     out[0] = u0;
     out[1] = u1;

@@ -22,8 +22,12 @@ namespace oracle {
 struct Camera {
   int dist;
   double fu, fv, cu, cv;
-  double d[4];
+  double d[8];
 };
+inline Camera cameraOf(const okvisgpu_camera& k) {
+  return Camera{k.distortion, k.fu, k.fv, k.cu, k.cv,
+                {k.dist[0], k.dist[1], k.dist[2], k.dist[3], k.dist[4], k.dist[5], k.dist[6], k.dist[7]}};
+}
 // PinholeCamera<D>::project with point Jacobian (PinholeCamera.hpp:288-366). Returns false when
 // |z| < 1e-12 (ProjectionStatus::Invalid before any output is written).
 bool cameraProject(const Camera& cam, const V3& p, double kp[2], double J[6] /*2x3 or null*/);

@@ -85,7 +85,7 @@ void buildProgram(const okvisgpu_problem* p, Program& P, bool loadImuState) {
     P.pbs.push_back(PBlock{kLm, i, 4, 3, p->landmark_constant ? p->landmark_constant[i] != 0 : false});
   for (int c = 0; c < p->n_cameras; ++c) {
     const okvisgpu_camera& k = p->cameras[c];
-    P.cams.push_back(Camera{k.distortion, k.fu, k.fv, k.cu, k.cv, {k.dist[0], k.dist[1], k.dist[2], k.dist[3]}});
+    P.cams.push_back(cameraOf(k));
   }
   auto addR = [&](int kind, int index, int nres, std::initializer_list<int> ids) {
     RBlock r;
@@ -1001,7 +1001,7 @@ int oracle_eval_reprojection(const okvisgpu_problem* p, double* r, double* Jp, d
   std::vector<Camera> cams;
   for (int c = 0; c < p->n_cameras; ++c) {
     const okvisgpu_camera& k = p->cameras[c];
-    cams.push_back(Camera{k.distortion, k.fu, k.fv, k.cu, k.cv, {k.dist[0], k.dist[1], k.dist[2], k.dist[3]}});
+    cams.push_back(cameraOf(k));
   }
   for (int o = 0; o < p->n_observations; ++o) {
     const int cam = p->obs_camera[o];
@@ -1163,7 +1163,7 @@ int oracle_eval_relpose(const okvisgpu_problem* p, double* r, double* J) {
 }
 
 int oracle_project(const okvisgpu_camera* k, const double* hp4, double* kp2, double* J24) {
-  Camera cam{k->distortion, k->fu, k->fv, k->cu, k->cv, {k->dist[0], k->dist[1], k->dist[2], k->dist[3]}};
+  Camera cam = cameraOf(*k);
   V4 hp;
   for (int i = 0; i < 4; ++i) hp.a[i] = hp4[i];
   return cameraProjectHomogeneous(cam, hp, kp2, J24) ? 0 : 1;

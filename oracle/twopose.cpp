@@ -176,7 +176,7 @@ void twoPoseCompute(const okvisgpu_twopose_edges* E, int e, double* deltaX, doub
   std::vector<Camera> cams;
   for (int c = 0; c < E->n_cameras; ++c) {
     const okvisgpu_camera& k = E->cameras[c];
-    cams.push_back(Camera{k.distortion, k.fu, k.fv, k.cu, k.cv, {k.dist[0], k.dist[1], k.dist[2], k.dist[3]}});
+    cams.push_back(cameraOf(k));
   }
   bool relPoseSet = false;
   Mat<6, 6> H00_ = Mat<6, 6>::Zero(), mH = Mat<6, 6>::Zero();

@@ -34,6 +34,58 @@ def test_reprojection_functor_parity(og, oracle, gpu_ctx):
         assert np.all(err <= 1e-9 * ref + 1e-12), f"max rel {np.max(err / ref)}"
 
 
+EQUIDISTANT_TEST = (-0.0041, 0.0063, -0.0067, 0.0023)
+# RadialTangentialDistortion8::testObject (RadialTangentialDistortion8.hpp:94-95): k1 k2 p1 p2 k3 k4 k5 k6
+RADTAN8_TEST = (0.6261, 0.001, -0.0002, 0.0001, 0.0001, 0.9541, 0.1151, -0.0075)
+CAMERA_MODELS = {"none": (0, ()), "equidistant": (2, EQUIDISTANT_TEST), "radtan8": (3, RADTAN8_TEST)}
+
+
+def _switch_camera_model(oracle, w, kind, params):
+    """Gives every camera of a synthetic (radtan) window another distortion model and moves each
+    measured keypoint so that its weighted residual at the initial estimate is unchanged: the same
+    noise and initial error, now consistent with the new model."""
+    p = w.problem
+    n = p.n_observations
+    r_old, _, _ = oracle.eval_reprojection(w.problem_ptr(), n)
+    for c in range(p.n_cameras):
+        cam = p.cameras[c]
+        cam.distortion = kind
+        for i in range(8):
+            cam.dist[i] = params[i] if i < len(params) else 0.0
+    r_new, _, _ = oracle.eval_reprojection(w.problem_ptr(), n)
+    kp = np.ctypeslib.as_array(p.obs_keypoint, shape=(n, 2))
+    L = np.ctypeslib.as_array(p.obs_sqrt_info, shape=(n, 2, 2))
+    kp -= np.linalg.solve(L, (r_new - r_old)[..., None])[..., 0]
+
+
+@pytest.mark.parametrize("distortion", sorted(CAMERA_MODELS))
+def test_distortion_models_parity(og, oracle, gpu_ctx, distortion):
+    """The other camera models of PinholeCamera<D> (NoDistortion, EquidistantDistortion.hpp:87-188,
+    RadialTangentialDistortion8.hpp:88-170): functor outputs and a short full solve against the
+    oracle."""
+    w = _window(og, seed=27)
+    assert og.DIST_EQUIDISTANT == 2 and og.DIST_RADTAN8 == 3
+    _switch_camera_model(oracle, w, *CAMERA_MODELS[distortion])
+    p = w.problem
+    n = p.n_observations
+    gpu_ctx.set_problems([p])
+    r, Jp, Jl = gpu_ctx.eval_reprojection(n)
+    r0, Jp0, Jl0 = oracle.eval_reprojection(w.problem_ptr(), n)
+    assert np.abs(r - r0).max() <= 1e-9 * np.abs(r0).max()
+    for a, b in ((Jp, Jp0), (Jl, Jl0)):
+        err = np.linalg.norm((a - b).reshape(n, -1), axis=1)
+        assert np.all(err <= 1e-9 * np.linalg.norm(b.reshape(n, -1), axis=1) + 1e-12)
+    opts = og.default_options(max_num_iterations=4, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    sg = gpu_ctx.solve(opts, 1)[0]
+    P = w.poses().copy()
+    w.reset()
+    so = oracle.solve(w.problem_ptr(), opts)
+    assert sg["num_iterations"] == so["num_iterations"]
+    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-6 * so["final_cost"], (sg, so)
+    assert np.abs(P[:, :3] - w.poses()[:, :3]).max() <= 1e-6
+
+
 def test_imu_functor_invariants(og, oracle, gpu_ctx):
     w = _window(og)
     p = w.problem

@@ -16,18 +16,22 @@ def _window(kf=6, lm=120, obs=900, seed=20251015):
 
 
 EQUIDISTANT_TEST = (-0.0041, 0.0063, -0.0067, 0.0023)
+# RadialTangentialDistortion8::testObject (RadialTangentialDistortion8.hpp:94-95): k1 k2 p1 p2 k3 k4 k5 k6
+RADTAN8_TEST = (0.6261, 0.001, -0.0002, 0.0001, 0.0001, 0.9541, 0.1151, -0.0075)
+DISTORTIONS = [og.DIST_NONE, og.DIST_RADTAN, og.DIST_EQUIDISTANT, og.DIST_RADTAN8]
 
 
-@pytest.mark.parametrize("distortion", [og.DIST_NONE, og.DIST_RADTAN, og.DIST_EQUIDISTANT])
+@pytest.mark.parametrize("distortion", DISTORTIONS)
 def test_reprojection_jacobians(oracle, distortion):
     w = _window()
     p = w.problem
     for c in range(p.n_cameras):
         cam = p.cameras[c]
         cam.distortion = distortion
-        if distortion == og.DIST_EQUIDISTANT:
-            for i, v in enumerate(EQUIDISTANT_TEST):
-                cam.dist[i] = v
+        params = {og.DIST_EQUIDISTANT: EQUIDISTANT_TEST, og.DIST_RADTAN8: RADTAN8_TEST}.get(distortion)
+        if params is not None:
+            for i in range(8):
+                cam.dist[i] = params[i] if i < len(params) else 0.0
     rng = np.random.default_rng(0)
     for o in rng.choice(p.n_observations, 40, replace=False):
         assert oracle.check_jacobians(w.problem_ptr(), 0, int(o)) < 1e-6
@@ -95,13 +99,13 @@ def _camera(distortion):
     cam.distortion, cam.width, cam.height = distortion, 752, 480
     cam.fu, cam.fv, cam.cu, cam.cv = 350.0, 360.0, 378.0, 238.0  # PinholeCamera::testObject
     d = {og.DIST_NONE: (0, 0, 0, 0), og.DIST_RADTAN: (-0.16, 0.15, 3e-4, 2e-4),
-         og.DIST_EQUIDISTANT: EQUIDISTANT_TEST}[distortion]
+         og.DIST_EQUIDISTANT: EQUIDISTANT_TEST, og.DIST_RADTAN8: RADTAN8_TEST}[distortion]
     for i, v in enumerate(d):
         cam.dist[i] = v
     return cam
 
 
-@pytest.mark.parametrize("distortion", [og.DIST_NONE, og.DIST_RADTAN, og.DIST_EQUIDISTANT])
+@pytest.mark.parametrize("distortion", DISTORTIONS)
 def test_camera_point_jacobian(oracle, distortion):
     cam = _camera(distortion)
     rng = np.random.default_rng(3)
