@@ -31,7 +31,7 @@ constexpr int kLmGroupVisits = 256;  // k_lm_visit: visits of one landmark group
 constexpr int kLmGroupMax = 64;      // landmarks per group
 constexpr int kLmPartStage = 2048;   // landmark-pair products per group (staged in LDS)
 constexpr int kImuHess = 465 + 30;  // packed upper J^T J (30x30) | J^T r
-constexpr int kVisitZ = 18;   // per visit: Z = s_p W s_l L^-T (6x3)
+constexpr int kVisitZ = 18;   // per visit: Z = s_p W s_l L^-T (6x3), k_lm_visit LDS only
 
 // contribution record types for the reduced-system assembly
 enum ContribType : int32_t {
@@ -126,7 +126,6 @@ struct DevProblem {
   double* lm_zz;                   // [n_lm][3]  L^-1 (s g)
   const int32_t* lmg_begin;        // [n_lmg+1] landmark groups of k_lm_visit (<= kLmGroupVisits visits each)
   int32_t n_lmg;
-  double* visit_Z;                 // [n_visit][kVisitZ] Z = s_p W s_l L^-T (6x3)   (per GN solve)
   // visit segments: the visits of one free pose inside one landmark group, pre-summed in k_lm_visit
   int32_t n_seg;
   const int32_t* seg_gbegin;       // [n_lmg+1] segments of group g

@@ -1,0 +1,171 @@
+// kernels_backsub.hip — landmark back substitution, the landmarks' dogleg vectors and the J*v forms
+// of the reprojection residuals, in one pass over the landmark groups of k_lm_visit.
+//
+// After the reduced system is solved (y_f, Jacobi-scaled), DoglegStrategy needs per landmark
+//   y_l = V'^-1 (s g_l - s W^T s_p y_p) = L^-T (zz - L^-1 s_l sum_v W_v^T s_p y_p)
+//   gauss_newton_step_ = -D y_l,  gradient_ = s g_l / D,  v_c = gradient_ / D
+// (SchurEliminator back substitution; DoglegStrategy::ComputeGradient / ComputeGaussNewtonStep)
+// and per reprojection residual the rows of J_s v_c and J_s v_g (v_g = -y) whose squares and cross
+// product give the model cost of every dogleg step of this linearisation (k_reduce, k_dogleg).
+// W_v^T s_p y_p is formed from the stored linearisation (r | A) that the J*v part reads anyway, so
+// the per-visit Schur operands Z of k_lm_visit never leave its LDS.
+// One workgroup per landmark group (whole landmarks, <= kLmGroupVisits visits), one thread per
+// (landmark, pose) visit, three phases separated by barriers:
+//   visit    q_v = W_v^T s_p y_p = -sum_obs J_l^T (J_p g_p), g_p = -s_p y_p
+//   landmark y_l from the q_v of its visits (visit order), its dogleg vectors, and s v_c, -s y_l
+//            to LDS for the visits
+//   visit    J_s v_c and J_s v_g of its 1-2 residuals (A re-read from L1/L2)
+// The f-block half of k_gn_finalize runs before (v_c of the poses); the IMU factors', priors' and
+// edges' J*v stay in k_jv.
+#include "device_problem.hpp"
+#include "launch.hpp"
+#include "okvisgpu_math.hpp"
+
+namespace okg {
+
+__global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
+  const int t = threadIdx.x;
+  const int l0 = P.lmg_begin[blockIdx.x], l1 = P.lmg_begin[blockIdx.x + 1];
+  const int w = P.lm_win[l0];  // a group never spans windows
+  const WinState& st = P.st[w];
+  if (st.done || !st.need_gn || st.gn_failed) return;  // uniform
+  __shared__ double sQ[3][kLmGroupVisits];
+  __shared__ double sC[6][kLmGroupMax];  // per landmark: s v_c (3) | -s y_l (3)
+  const int v0 = P.lm_visit_begin[l0], v1 = P.lm_visit_begin[l1];
+  const int v = v0 + t;
+  const bool hasV = v < v1;
+  const int l = hasV ? P.visit_lm[v] : l0;
+  const int pose = hasV ? P.visit_pose[v] : 0;
+  const int pf = hasV ? P.pose_f[pose] : -1;
+  const bool lfree = P.lm_free[l] != 0;
+  double cp[6], gp[6];
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    cp[c] = 0.0;
+    gp[c] = 0.0;
+  }
+  if (pf >= 0) {
+    const size_t b = (size_t)P.win_foff[w] + pf;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const double sc = P.sF[b + c];
+      cp[c] = sc * P.vF[b + c];
+      gp[c] = -sc * P.yF[b + c];
+    }
+  }
+  const auto lin = gmem(P.obs_lin[st.lcur]);
+  const int64_t S = P.obs_stride;
+  const double* hp = P.lm[st.xcur] + 4 * (size_t)l;
+  const double* tw = P.pose[st.xcur] + 7 * (size_t)pose;
+  const double w4 = hp[3];
+  const double p3[3] = {hp[0] - tw[0] * w4, hp[1] - tw[1] * w4, hp[2] - tw[2] * w4};
+  const int ob0 = hasV ? P.visit_obs_begin[v] : 0, ob1 = hasV ? P.visit_obs_begin[v + 1] : 0;
+
+  // ---- visit: q_v = W_v^T s_p y_p
+  double q[3] = {0.0, 0.0, 0.0};
+  if (pf >= 0 && lfree)
+    for (int o = ob0; o < ob1; ++o) {
+      if (P.obs_flags[o] & 2) continue;
+      double A[6], Jp[12], Jl[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) A[k] = lin[(2 + k) * S + o];
+      obsJacobians(A, p3, w4, Jp, Jl);
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        double jg = 0.0;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) jg += Jp[r * 6 + c] * gp[c];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) q[a] -= Jl[r * 3 + a] * jg;
+      }
+    }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) sQ[a][t] = q[a];
+  __syncthreads();
+
+  // ---- landmark: y_l = L^-T (zz - L^-1 s_l sum_v q_v), the dogleg vectors
+  if (t < l1 - l0) {
+    const int L = l0 + t;
+    double c6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (P.lm_free[L]) {
+      double qs[3] = {0.0, 0.0, 0.0};
+      for (int m = P.lm_visit_begin[L] - v0; m < P.lm_visit_begin[L + 1] - v0; ++m)
+#pragma unroll
+        for (int a = 0; a < 3; ++a) qs[a] += sQ[a][m];
+      double li[9], s3[3], u[3];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) li[i] = P.lm_Linv[9 * (size_t)L + i];  // lower triangular
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        s3[a] = P.sL[3 * (size_t)L + a];
+        qs[a] *= s3[a];
+      }
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+        u[a] = P.lm_zz[3 * (size_t)L + a] - (li[a * 3] * qs[0] + li[a * 3 + 1] * qs[1] + li[a * 3 + 2] * qs[2]);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        double y = 0.0;
+#pragma unroll
+        for (int c = a; c < 3; ++c) y += li[c * 3 + a] * u[c];
+        const size_t i = 3 * (size_t)L + a;
+        const double dg = P.diagL[i];
+        P.yL[i] = y;
+        P.gnL[i] = -dg * y;
+        const double gr = s3[a] * P.lm_g[i] / dg;
+        const double vc = gr / dg;
+        P.dgL[i] = gr;
+        P.vL[i] = vc;
+        c6[a] = s3[a] * vc;
+        c6[3 + a] = -s3[a] * y;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) sC[i][t] = c6[i];
+  }
+  __syncthreads();
+  if (!hasV) return;
+
+  // ---- visit: J_s v_c and J_s v_g of its residuals (fixed residuals excluded)
+  const int u = l - l0;
+  double cl[3], gl[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    cl[c] = sC[c][u];
+    gl[c] = sC[3 + c][u];
+  }
+  double acc[3] = {0.0, 0.0, 0.0};
+  for (int o = ob0; o < ob1; ++o) {
+    if (P.obs_flags[o] & 2) continue;
+    double A[6], Jp[12], Jl[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) A[k] = lin[(2 + k) * S + o];
+    obsJacobians(A, p3, w4, Jp, Jl);
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      double jc = 0.0, jg = 0.0;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        jc += Jp[r * 6 + c] * cp[c];
+        jg += Jp[r * 6 + c] * gp[c];
+      }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        jc += Jl[r * 3 + c] * cl[c];
+        jg += Jl[r * 3 + c] * gl[c];
+      }
+      acc[0] += jc * jc;
+      acc[1] += jg * jg;
+      acc[2] += jc * jg;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) P.obs_jv[(size_t)k * P.n_visit + v] = acc[k];
+}
+
+void launch_lm_backsub(const DevProblem& P, hipStream_t s) {
+  if (P.n_lmg > 0) hipLaunchKernelGGL(k_lm_backsub_jv, dim3(P.n_lmg), dim3(kLmGroupVisits), 0, s, P.self);
+}
+
+}  // namespace okg

@@ -66,72 +66,14 @@ __device__ __forceinline__ void jvAcc(double jc, double jg, double (&a)[3]) {
 // step = ca v_c + cb v_g, so |J_s step|^2 = ca^2 jcc + 2 ca cb jcg + cb^2 jgg is formed in k_dogleg,
 // also for the steps re-tried at a smaller radius without a new GN step (DoglegStrategy reuse_).
 // The companion (J_s step).r = step.(s g) uses the gradient g = J^T r already at hand.
-// Reprojections: one thread per (landmark, pose) visit (its 1-2 residuals share the pose/landmark
-// vectors); IMU factors and priors: one thread each.
+// Here the IMU factors, priors and relative-pose edges, one thread each; the reprojection residuals'
+// share is formed with the landmark back substitution (k_lm_backsub_jv, kernels_backsub.hip).
 __global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const double* __restrict__ cF = P.vF;
   const double* __restrict__ yF = P.yF;
-  if (t < P.n_visit) {
-    const int v = t;
-    const int l = P.visit_lm[v];
-    const int w = P.lm_win[l];
-    if (!jvSelect(P, w)) return;
-    const WinState& st = P.st[w];
-    const int ps = P.visit_pose[v];
-    const int pf = P.pose_f[ps];
-    double cp[6] = {0, 0, 0, 0, 0, 0}, gp[6] = {0, 0, 0, 0, 0, 0}, cl[3] = {0, 0, 0}, gl[3] = {0, 0, 0};
-    if (pf >= 0) {
-      const size_t base = (size_t)P.win_foff[w] + pf;
-#pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        const double sc = P.sF[base + c];
-        cp[c] = sc * cF[base + c];
-        gp[c] = -sc * yF[base + c];
-      }
-    }
-    if (P.lm_free[l])
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const size_t i = 3 * (size_t)l + c;
-        cl[c] = P.sL[i] * P.vL[i];
-        gl[c] = -P.sL[i] * P.yL[i];
-      }
-    const auto lin = gmem(P.obs_lin[st.lcur]);
-    const int64_t S = P.obs_stride;
-    const double* hp = P.lm[st.xcur] + 4 * (size_t)l;
-    const double* tw = P.pose[st.xcur] + 7 * (size_t)ps;
-    const double w4 = hp[3];
-    const double p3[3] = {hp[0] - tw[0] * w4, hp[1] - tw[1] * w4, hp[2] - tw[2] * w4};
-    double a[3] = {0.0, 0.0, 0.0};
-    for (int o = P.visit_obs_begin[v]; o < P.visit_obs_begin[v + 1]; ++o) {
-      if (P.obs_flags[o] & 2) continue;
-      double A[6], Jp[12], Jl[6];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) A[k] = lin[(2 + k) * S + o];
-      obsJacobians(A, p3, w4, Jp, Jl);
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        double jc = 0.0, jg = 0.0;
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-          jc += Jp[r * 6 + c] * cp[c];
-          jg += Jp[r * 6 + c] * gp[c];
-        }
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          jc += Jl[r * 3 + c] * cl[c];
-          jg += Jl[r * 3 + c] * gl[c];
-        }
-        jvAcc(jc, jg, a);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) P.obs_jv[(size_t)k * P.n_visit + v] = a[k];
-    return;
-  }
-  int u = t - P.n_visit;
+  int u = t;
   if (u < P.n_imu) {
     const int f = u;
     const int w = P.imu_win[f];
@@ -627,7 +569,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
 }
 
 void launch_jv(const DevProblem& P, hipStream_t s) {
-  const int n = P.n_visit + P.n_imu + P.n_pprior + P.n_sbprior + P.n_relpose;
+  const int n = P.n_imu + P.n_pprior + P.n_sbprior + P.n_relpose;
   if (n > 0) hipLaunchKernelGGL(k_jv, dim3((n + 255) / 256), dim3(256), 0, s, P.self);
 }
 void launch_reduce(const DevProblem& P, int mode, hipStream_t s) {

@@ -18,8 +18,8 @@
 //                 a fixed tree combines the groups, so the sum is deterministic without atomics;
 //                 diagonal pairs also emit the Schur rhs and the dogleg diagonal.
 //   k_assemble_sb one wavefront per block pair involving a speed/bias block (one entry per lane).
-//   k_lm_backsub  one thread per landmark: y_l = V^-1 (g_l - W^T y_f).
-//   k_gn_finalize Gauss-Newton step / dogleg gradient in the dogleg-scaled space.
+//   k_gn_finalize Gauss-Newton step / dogleg gradient of the f-blocks in the dogleg-scaled space
+//                 (the landmarks' back substitution and vectors: k_lm_backsub_jv, kernels_backsub.hip).
 #include <cfloat>
 
 #include "device_problem.hpp"
@@ -54,7 +54,7 @@ __device__ __forceinline__ bool linSelect(const DevProblem& P, int w, int lin_mo
 //            Jacobi scaling 1 / (1 + sqrt(diag V)); then the 3x3 LLT of s V s + mu D^2
 //            (InvertPSDMatrix) -> L^-1, zz = L^-1 (s g), the dogleg diagonal D
 //   visit    Z = s_p W s_l L^-T and U z = Z zz, the operands of the Schur terms
-//            Y_a U_b^T = Z_a Z_b^T (k_assemble_pp) and of the back substitution (k_lm_backsub)
+//            Y_a U_b^T = Z_a Z_b^T (the partial blocks below; Z never leaves the workgroup)
 // mode 0: linearisation at iteration 0 (no Z: the pose scaling comes from k_fgrad afterwards);
 // mode 1: linearisation after an accepted step, Z for the new mu (WinState::z_mu);
 // mode 2: GN prep of windows whose Z is stale (mu raised by a retry or an invalid step): W is
@@ -295,11 +295,6 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
       o[18 + r] = z0 * zz[0] + z1 * zz[1] + z2 * zz[2];
     }
   }
-  if (hasV) {
-    double2* out = reinterpret_cast<double2*>(P.visit_Z + (size_t)v * kVisitZ);
-#pragma unroll
-    for (int i = 0; i < kVisitZ / 2; ++i) out[i] = double2{o[2 * i], o[2 * i + 1]};
-  }
   if (slot >= 0)
 #pragma unroll
     for (int i = 0; i < 6; ++i) sR[i][slot] = o[kVisitZ + i];
@@ -521,7 +516,6 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
   const auto pc = gmem(P.pair_contrib);
   const auto vhg = gmem(P.seg_hg);
   const auto suz = gmem(P.seg_uz);
-  const auto vuy = gmem(P.visit_Z);
   double H[6], Sc[6], uz = 0.0;
 #pragma unroll
   for (int q = 0; q < 6; ++q) { H[q] = 0.0; Sc[q] = 0.0; }
@@ -676,65 +670,24 @@ __global__ __launch_bounds__(256) void k_assemble_sb(const DevProblem* __restric
   }
 }
 
-__global__ __launch_bounds__(256) void k_lm_backsub(const DevProblem* __restrict__ Pp) {
-  const DevProblem& P = *Pp;
-  const int l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= P.n_lm) return;
-  if (!P.lm_free[l]) return;
-  const int w = P.lm_win[l];
-  if (!gnSelect(P, w)) return;
-  const int foff = P.win_foff[w];
-  // y_l = V'^-1 (s g - sum_v U_v^T y_p) = L^-T (zz - sum_v Z_v^T y_p)
-  const double* zz = P.lm_zz + 3 * (size_t)l;
-  double t3[3] = {zz[0], zz[1], zz[2]};
-  for (int v = P.lm_visit_begin[l]; v < P.lm_visit_begin[l + 1]; ++v) {
-    const int pf = P.pose_f[P.visit_pose[v]];
-    if (pf < 0) continue;
-    const double* Z = P.visit_Z + (size_t)v * kVisitZ;
-    for (int rr = 0; rr < 6; ++rr) {
-      const double y = P.yF[(size_t)foff + pf + rr];
-      for (int a = 0; a < 3; ++a) t3[a] -= Z[rr * 3 + a] * y;
-    }
-  }
-  const double* Li = P.lm_Linv + 9 * (size_t)l;
-  for (int a = 0; a < 3; ++a) {
-    double y = 0.0;
-    for (int c = a; c < 3; ++c) y += Li[c * 3 + a] * t3[c];
-    P.yL[3 * (size_t)l + a] = y;
-  }
-}
-
 // gauss_newton_step_ = -diagonal_ .* y ; gradient_ = s .* g / diagonal_ ; v = gradient_ / diagonal_
-// (DoglegStrategy::ComputeGradient / ComputeCauchyPoint / ComputeGaussNewtonStep)
+// (DoglegStrategy::ComputeGradient / ComputeCauchyPoint / ComputeGaussNewtonStep) of the f-blocks;
+// the landmarks' share is formed with their back substitution (k_lm_backsub_jv).
 __global__ __launch_bounds__(256) void k_gn_finalize(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < P.n_fblock) {
-    const int w = P.fb_win[t];
-    if (!gnSelect(P, w)) return;
-    const int n = P.fb_kind[t] == 0 ? 6 : 9;
-    const size_t base = (size_t)P.win_foff[w] + P.fb_off[t];
-    for (int c = 0; c < n; ++c) {
-      const size_t i = base + c;
-      const double dg = P.diagF[i];
-      P.gnF[i] = -dg * P.yF[i];
-      const double gr = P.sF[i] * P.gF[i] / dg;
-      P.dgF[i] = gr;
-      P.vF[i] = gr / dg;
-    }
-    return;
-  }
-  const int l = t - P.n_fblock;
-  if (l >= P.n_lm || !P.lm_free[l]) return;
-  const int w = P.lm_win[l];
+  if (t >= P.n_fblock) return;
+  const int w = P.fb_win[t];
   if (!gnSelect(P, w)) return;
-  for (int a = 0; a < 3; ++a) {
-    const size_t i = 3 * (size_t)l + a;
-    const double dg = P.diagL[i];
-    P.gnL[i] = -dg * P.yL[i];
-    const double gr = P.sL[i] * P.lm_g[i] / dg;
-    P.dgL[i] = gr;
-    P.vL[i] = gr / dg;
+  const int n = P.fb_kind[t] == 0 ? 6 : 9;
+  const size_t base = (size_t)P.win_foff[w] + P.fb_off[t];
+  for (int c = 0; c < n; ++c) {
+    const size_t i = base + c;
+    const double dg = P.diagF[i];
+    P.gnF[i] = -dg * P.yF[i];
+    const double gr = P.sF[i] * P.gF[i] / dg;
+    P.dgF[i] = gr;
+    P.vF[i] = gr / dg;
   }
 }
 
@@ -776,16 +729,12 @@ void launch_gn_reduce(const DevProblem& P, hipStream_t s) {
   launch_zero_S(P, s);
   launch_assemble(P, s);
 }
-void launch_lm_backsub(const DevProblem& P, hipStream_t s) {
-  if (P.n_lm > 0) hipLaunchKernelGGL(k_lm_backsub, dim3((P.n_lm + 255) / 256), dim3(256), 0, s, P.self);
-}
 void launch_gn_finalize(const DevProblem& P, hipStream_t s) {
-  const int n = P.n_fblock + P.n_lm;
-  if (n > 0) hipLaunchKernelGGL(k_gn_finalize, dim3((n + 255) / 256), dim3(256), 0, s, P.self);
+  if (P.n_fblock > 0) hipLaunchKernelGGL(k_gn_finalize, dim3((P.n_fblock + 255) / 256), dim3(256), 0, s, P.self);
 }
 void launch_gn_backsub(const DevProblem& P, hipStream_t s) {
+  launch_gn_finalize(P, s);  // v_c of the f-blocks: read by the landmark pass
   launch_lm_backsub(P, s);
-  launch_gn_finalize(P, s);
 }
 
 }  // namespace okg

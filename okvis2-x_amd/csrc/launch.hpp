@@ -23,7 +23,7 @@ void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_lm_prep(const DevProblem& P, hipStream_t s);
 void launch_zero_S(const DevProblem& P, hipStream_t s);
 void launch_assemble(const DevProblem& P, hipStream_t s);
-void launch_lm_backsub(const DevProblem& P, hipStream_t s);
+void launch_lm_backsub(const DevProblem& P, hipStream_t s);  // kernels_backsub.hip: + landmark dogleg vectors, J*v
 void launch_assemble_pp(const DevProblem& P, hipStream_t s);
 void launch_assemble_sb(const DevProblem& P, hipStream_t s);
 void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s);  // 0/1: linearisation, 2: GN prep

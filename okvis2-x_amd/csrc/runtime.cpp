@@ -789,8 +789,7 @@ struct okvisgpu_ctx {
     D.n_part = (int)B.part_cbegin.size() - 1;
     const size_t o_pgb = upl(B.part_gbegin), o_pcb2 = upl(B.part_cbegin), o_pcon = upl(B.part_contrib),
                  o_partS = scratch(sizeof(double) * 36 * std::max(1, D.n_part));
-    const size_t o_shg = scratch(sizeof(double) * kSegHG * D.n_seg), o_suz = scratch(sizeof(double) * kSegUz * D.n_seg),
-                 o_vZ = scratch(sizeof(double) * kVisitZ * D.n_visit);
+    const size_t o_shg = scratch(sizeof(double) * kSegHG * D.n_seg), o_suz = scratch(sizeof(double) * kSegUz * D.n_seg);
     const size_t o_imu_blocks = upl(B.imu_blocks), o_imu_win = upl(B.imu_win), o_imu_flags = upl(B.imu_flags),
                  o_imu_t0 = upl(B.imu_t0), o_imu_t1 = upl(B.imu_t1), o_imu_sb = upl(B.imu_sbegin),
                  o_imu_ts = upl(B.imu_ts), o_imu_ga = upl(B.imu_ga), o_imu_par = upl(B.imu_par),
@@ -864,7 +863,7 @@ struct okvisgpu_ctx {
     D.lm_visit_begin = ip(o_lmvb); D.visit_pose = ip(o_vpose); D.visit_obs_begin = ip(o_vob); D.visit_lm = ip(o_vlm);
     D.lm_V = dp(o_lmV); D.lm_g = dp(o_lmg); D.lm_Linv = dp(o_lmVi); D.lm_zz = dp(o_lmz);
     D.part_gbegin = ip(o_pgb); D.part_cbegin = ip(o_pcb2); D.part_contrib = ip(o_pcon); D.part_S = dp(o_partS);
-    D.seg_hg = dp(o_shg); D.seg_uz = dp(o_suz); D.visit_Z = dp(o_vZ);
+    D.seg_hg = dp(o_shg); D.seg_uz = dp(o_suz);
     D.seg_gbegin = ip(o_seg_gb); D.seg_pose = ip(o_seg_pose); D.seg_range = ip(o_seg_rg); D.visit_slot = ip(o_vslot);
     D.lmg_begin = ip(o_lmg_b); D.n_lmg = B.lmg_begin.empty() ? 0 : (int)B.lmg_begin.size() - 1;
     D.imu_blocks = ip(o_imu_blocks); D.imu_win = ip(o_imu_win); D.imu_flags = up(o_imu_flags);
@@ -1349,8 +1348,8 @@ int okvisgpu_profile_iteration(okvisgpu_ctx* c, double* ms) {
     launch_zero_S(P, s); mark(1);
     launch_assemble(P, s); mark(2);
     launch_cholesky(P, s); mark(3);
-    launch_lm_backsub(P, s); mark(4);
     launch_gn_finalize(P, s); mark(5);
+    launch_lm_backsub(P, s); mark(4);
     launch_jv(P, s); mark(6);
     launch_reduce(P, R_JV, s); mark(7);
     launch_dogleg(P, s); mark(8);
@@ -1378,12 +1377,13 @@ int okvisgpu_profile_iteration(okvisgpu_ctx* c, double* ms) {
 namespace {
 enum KernelId {
   K_ASSEMBLE_PP, K_ASSEMBLE_SB, K_CHOLESKY, K_LM_VISIT, K_LM_VISIT_PREP, K_EVAL_IMU, K_EVAL_OBS, K_JV,
-  K_FGRAD, K_COUNT
+  K_FGRAD, K_LM_BACKSUB, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {"k_assemble_pp", "k_assemble_sb", "k_cholesky", "k_lm_visit", "k_lm_visit_prep",
-                                     "k_eval_imu",    "k_eval_obs",    "k_jv",       "k_fgrad"};
+                                     "k_eval_imu",    "k_eval_obs",    "k_jv",       "k_fgrad",
+                                     "k_lm_backsub_jv"};
 // bound: 0 = HBM bytes, 1 = FP64 matrix-core FLOPs
-const int kKernelBound[K_COUNT] = {0, 0, 1, 0, 0, 0, 0, 0, 0};
+const int kKernelBound[K_COUNT] = {0, 0, 1, 0, 0, 0, 0, 0, 0, 0};
 
 // Algorithmic work of one iteration's launches of kernel k over the whole batch: compulsory HBM
 // bytes (every operand read once, every result written once) or FP64 FLOPs.
@@ -1413,17 +1413,21 @@ double kernelWork(const HostBatch& B, const DevProblem& P, int k) {
       const double panels = (double)(B.chol_panel_items.size() / 2), upd = (double)B.n_band_updates;
       return diag * (2.0 * tile3 / 3.0 + 4.0 * 64 * 64) + panels * (2.0 * tile3 + 4.0 * 64 * 64) + upd * 2.0 * tile3;
     }
-    case K_LM_VISIT:  // obs linearisation + params in; H|g and Z|Uz per visit, landmark blocks out
-      return nObs * (kObsLin * d8 + 1) + nVis * (kVisitZ * d8 + 7 * d8 + 16) + (double)P.n_seg * (27 + 6) * d8 +
+    case K_LM_VISIT:  // obs linearisation + params in; segments, partial blocks, landmark blocks out
+      return nObs * (kObsLin * d8 + 1) + nVis * (7 * d8 + 16) + (double)P.n_seg * (27 + 6) * d8 +
              (double)B.part_contrib.size() * 4 + (double)P.n_part * 36 * d8 + nLm * 40 * d8;
-    case K_LM_VISIT_PREP:  // W recomputed from the obs linearisation; Z|Uz out
-      return nObs * (kObsLin * d8 + 1) + nVis * (kVisitZ * d8 + 7 * d8 + 16) + (double)P.n_seg * 6 * d8 +
+    case K_LM_VISIT_PREP:  // W recomputed from the obs linearisation; U z, partial blocks, L^-1 out
+      return nObs * (kObsLin * d8 + 1) + nVis * (7 * d8 + 16) + (double)P.n_seg * 6 * d8 +
              (double)B.part_contrib.size() * 4 + (double)P.n_part * 36 * d8 + nLm * 34 * d8;
     case K_EVAL_IMU: return nImu * (2.0 * kImuState + kImuLin + 2 * 16) * d8 + (double)B.imu_ts.size() * 7 * d8;
     case K_EVAL_OBS: return nObs * (16 + 32 + 13 + kObsLin * d8 + 8) + nLm * 4 * d8 + (double)B.pose_f.size() * 7 * d8;
-    case K_JV:  // obs linearisation once; pose / landmark parameters and both operand vectors once per block
-      return nObs * (kObsLin * d8 + 1) + nVis * (3 * d8 + 8) + (double)P.n_pose * (7 + 12) * d8 +
-             nLm * (4 + 6) * d8 + nImu * (kImuLin + 3) * d8;
+    case K_JV:  // factors: IMU linearisation, prior / edge Jacobians in, their J*v forms out
+      return nImu * (kImuLin + 3) * d8 + (double)P.n_pprior * (42 + 3) * d8 + (double)P.n_sbprior * (90 + 3) * d8 +
+             (double)P.n_relpose * (kRelPoseLin + 3) * d8;
+    case K_LM_BACKSUB:  // obs linearisation (A, flags) once; pose / landmark parameters and vectors once per
+                        // block; landmark step + dogleg vectors and the visits' J*v forms out
+      return nObs * (6 * d8 + 1) + nVis * (3 * d8 + 16) + (double)P.n_pose * (7 + 18) * d8 +
+             nLm * (4 + 9 + 3 + 3 + 3 + 3 + 12) * d8;
     case K_FGRAD: return (double)P.n_seg * 27 * d8 + nImu * kImuLin * d8 + (double)B.fb_contrib.size() * 16;
   }
   return 0.0;
@@ -1483,6 +1487,7 @@ int okvisgpu_time_kernel(okvisgpu_ctx* c, int32_t kernel, int32_t reps, double* 
           break;
         case K_EVAL_OBS: timed([&] { launch_eval_obs(P, 1, s); }); break;
         case K_JV: timed([&] { launch_jv(P, s); }); break;
+        case K_LM_BACKSUB: timed([&] { launch_lm_backsub(P, s); }); break;
         case K_FGRAD: timed([&] { launch_fgrad(P, 1, s); }); break;
         case K_CHOLESKY:  // needs a freshly assembled S each repetition
           launch_zero_S(P, s);

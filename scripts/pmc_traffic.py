@@ -27,7 +27,7 @@ for k, d in vals.items():
     f = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"]) * 1024 * 2
     w = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"]) * 1024
     kern[k] = {"fetch_bytes_per_dispatch": f, "write_bytes_per_dispatch": w, "bytes_per_dispatch": f + w}
-    if k in ("k_assemble_pp", "k_assemble_sb", "k_eval_imu", "k_eval_obs", "k_fgrad", "k_cholesky", "k_lm_backsub",
+    if k in ("k_assemble_pp", "k_assemble_sb", "k_eval_imu", "k_eval_obs", "k_fgrad", "k_cholesky", "k_lm_backsub", "k_lm_backsub_jv",
              "k_zero_S", "k_jv", "k_gn_finalize", "k_dogleg"):
         kern[k]["bytes_per_iteration"] = f + w  # one dispatch per iteration
     elif k in ("k_lm_visit", "k_lm_visit_prep"):
