@@ -160,6 +160,7 @@ __device__ void loadPre(const double* s, ImuPre& p) {
 // reference's clamp exactly.
 constexpr int kImuGroup = 16;
 constexpr int kImuPerWG = 4;
+constexpr int kStepRec = 32;  // dt | dq (4) | a_true (3) | Jr (9) | R(dq)^T (9) | noise (5) | pad
 
 // F_delta (ImuError.cpp:395-410) of one step in LDS: non-identity 3x3 blocks
 constexpr int kF03 = 0, kF09 = 9, kF012 = 18, kF39 = 27, kF63 = 36, kF69 = 45, kF612 = 54, kFdt = 63;
@@ -292,6 +293,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   double* sB = sAll[g] + 256;
   double* sR = sAll[g] + 512;
   double* sF = sAll[g] + 544;
+  __shared__ double sStep[kImuPerWG][kImuGroup * kStepRec];  // per-step records of a chunk
 
   int w = 0, xs = 0, lb = 0;
   bool live = f < P.n_imu;
@@ -341,67 +343,109 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   for (int i = 0; i < 15; ++i) Pc[i] = 0.0;
   int steps = 0;
 
-  // ---- redoPreintegration (ImuError.cpp:258-466), uniform trip count over the wavefront
+  // ---- redoPreintegration (ImuError.cpp:258-466), uniform trip count over the wavefront.
+  // What a step needs that does not depend on the integration chain (its length, the interpolated
+  // samples, dq = exp(w dt), the right Jacobian of w dt, R(dq)^T, the noise terms) is formed for 16
+  // steps at a time, one step per lane, and staged in LDS; the sequential chain only does products.
+  // The integration time before step `it` is t0 for the first sample and max(t0, min(ts[it], t1))
+  // after it: where the previous step ended, or unchanged when that step was skipped for dt <= 0
+  // (ImuError.cpp:339). Steps after the one that reaches t1 then have dt = 0 as well.
   {
     const double bg[3] = {sb0[3], sb0[4], sb0[5]}, ba[3] = {sb0[6], sb0[7], sb0[8]};
-    int64_t time = t0;
-    bool hasStarted = false, running = integrate;
     const int N = integrate ? send - sbeg : 0;
     int Nmax = N;
     Nmax = max(Nmax, __shfl_xor(Nmax, 16, 64));
     Nmax = max(Nmax, __shfl_xor(Nmax, 32, 64));
-    for (int it = 0; it < Nmax; ++it) {
-      bool doStep = false;
-      double qa0 = 0, qg = 0, qa = 0, qbg = 0, qba = 0;
-      if (running && it < N) {
-        const int s0 = sbeg + it;
-        const int s1 = (it + 1 < N) ? s0 + 1 : s0;
-        double om0[3], ac0[3], om1[3], ac1[3];
-        for (int k = 0; k < 3; ++k) {
-          om0[k] = P.imu_ga[6 * (size_t)s0 + k];
-          ac0[k] = P.imu_ga[6 * (size_t)s0 + 3 + k];
-          om1[k] = P.imu_ga[6 * (size_t)s1 + k];
-          ac1[k] = P.imu_ga[6 * (size_t)s1 + 3 + k];
-        }
-        int64_t nexttime = (it + 1 == N) ? t1 : P.imu_ts[s0 + 1];
-        double dt = durToSec(nexttime - time);
-        if (t1 < nexttime) {
-          const double interval = durToSec(nexttime - P.imu_ts[s0]);
-          nexttime = t1;
-          dt = durToSec(nexttime - time);
-          const double r = dt / interval;
+    bool started = false;                       // hasStarted: an earlier step was integrated
+    double C[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};  // R(cdq), carried from step to step
+    double* rec = sStep[g];
+    for (int c0 = 0; c0 < Nmax; c0 += kImuGroup) {
+      {
+        const int it = c0 + l;
+        bool ok = false;
+        double dt = 0.0, om0[3] = {0, 0, 0}, ac0[3] = {0, 0, 0}, om1[3] = {0, 0, 0}, ac1[3] = {0, 0, 0};
+        int64_t nexttime = 0;
+        int s0 = sbeg;
+        if (it < N) {
+          s0 = sbeg + it;
+          const int s1 = (it + 1 < N) ? s0 + 1 : s0;
           for (int k = 0; k < 3; ++k) {
-            om1[k] = (1.0 - r) * om0[k] + r * om1[k];
-            ac1[k] = (1.0 - r) * ac0[k] + r * ac1[k];
+            om0[k] = P.imu_ga[6 * (size_t)s0 + k];
+            ac0[k] = P.imu_ga[6 * (size_t)s0 + 3 + k];
+            om1[k] = P.imu_ga[6 * (size_t)s1 + k];
+            ac1[k] = P.imu_ga[6 * (size_t)s1 + 3 + k];
           }
-        }
-        if (dt > 0.0) {  // dt <= 0: the sample is skipped (ImuError.cpp:339)
-          doStep = true;
-          if (!hasStarted) {
-            hasStarted = true;
-            const double r = dt / durToSec(nexttime - P.imu_ts[s0]);
+          nexttime = (it + 1 == N) ? t1 : P.imu_ts[s0 + 1];
+          const int64_t tb = (it == 0) ? t0 : max(t0, min(P.imu_ts[s0], t1));
+          dt = durToSec(nexttime - tb);
+          if (t1 < nexttime) {
+            const double interval = durToSec(nexttime - P.imu_ts[s0]);
+            nexttime = t1;
+            dt = durToSec(nexttime - tb);
+            const double r = dt / interval;
             for (int k = 0; k < 3; ++k) {
-              om0[k] = r * om0[k] + (1.0 - r) * om1[k];
-              ac0[k] = r * ac0[k] + (1.0 - r) * ac1[k];
+              om1[k] = (1.0 - r) * om0[k] + r * om1[k];
+              ac1[k] = (1.0 - r) * ac0[k] + r * ac1[k];
             }
           }
+          ok = dt > 0.0;  // dt <= 0: the sample is skipped (ImuError.cpp:339)
+        }
+        const unsigned gm = (unsigned)((__ballot(ok) >> (16 * g)) & 0xFFFFull);
+        if (ok && !started && l == __ffs(gm) - 1) {  // the first integrated step starts at t0
+          const double r = dt / durToSec(nexttime - P.imu_ts[s0]);
+          for (int k = 0; k < 3; ++k) {
+            om0[k] = r * om0[k] + (1.0 - r) * om1[k];
+            ac0[k] = r * ac0[k] + (1.0 - r) * ac1[k];
+          }
+        }
+        started = started || gm != 0;
+        steps += __popc(gm);
+        double* R = rec + l * kStepRec;
+        R[0] = ok ? dt : 0.0;
+        if (ok) {
           double gyr_sat = 1.0, acc_sat = 1.0;
           for (int k = 0; k < 3; ++k) {
             if (fabs(om0[k]) > g_max || fabs(om1[k]) > g_max) gyr_sat = 100.0;
             if (fabs(ac0[k]) > a_max || fabs(ac1[k]) > a_max) acc_sat = 100.0;
           }
-          double w_true[3], a_true[3];
+          double w_true[3];
           for (int k = 0; k < 3; ++k) {
             w_true[k] = 0.5 * (om0[k] + om1[k]) - bg[k];
-            a_true[k] = 0.5 * (ac0[k] + ac1[k]) - ba[k];
+            R[5 + k] = 0.5 * (ac0[k] + ac1[k]) - ba[k];  // a_true
           }
           const double theta_half =
               sqrt(w_true[0] * w_true[0] + w_true[1] * w_true[1] + w_true[2] * w_true[2]) * 0.5 * dt;
           const double sth = sinc(theta_half) * 0.5 * dt;
           const Q dq{sth * w_true[0], sth * w_true[1], sth * w_true[2], cos(theta_half)};
+          R[1] = dq.x; R[2] = dq.y; R[3] = dq.z; R[4] = dq.w;
+          const double wdt[3] = {w_true[0] * dt, w_true[1] * dt, w_true[2] * dt};
+          double Jr[9], Rdqi[9];
+          rightJacobian(wdt, Jr);  // Jacobian parts (ImuError.cpp:385-392)
+          qrot(qinv(dq), Rdqi);
+          for (int i = 0; i < 9; ++i) {
+            R[8 + i] = Jr[i];
+            R[17 + i] = Rdqi[i];
+          }
+          // discrete noise of this step on the diagonal (ImuError.cpp:412-426, summed over sigma)
+          R[26] = sa_c * sa_c * (0.5 * dt * dt * dt * acc_sat * acc_sat * acc_sat);
+          R[27] = sg_c * sg_c * (gyr_sat * dt);
+          R[28] = sa_c * sa_c * (acc_sat * dt);
+          R[29] = sgw_c * sgw_c * dt;
+          R[30] = saw_c * saw_c * dt;
+        }
+      }
+      __syncthreads();
+      const int nk = min(kImuGroup, Nmax - c0);
+      for (int k = 0; k < nk; ++k) {
+        const double* R = rec + k * kStepRec;
+        const double dt = R[0];
+        const bool doStep = dt > 0.0;  // uniform over the group
+        double qa0 = 0, qg = 0, qa = 0, qbg = 0, qba = 0;
+        if (doStep) {
+          const Q dq{R[1], R[2], R[3], R[4]};
+          const double a_true[3] = {R[5], R[6], R[7]};
           const Q dq1 = qmul(cdq, dq);
-          double C[9], C1[9], CC1[9];
-          qrot(cdq, C);
+          double C1[9], CC1[9];
           qrot(dq1, C1);
           for (int i = 0; i < 9; ++i) CC1[i] = C[i] + C1[i];
           double CCa[3];
@@ -429,14 +473,14 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
           aadi += (l == 0) ? tmp[0] : ((l == 1) ? tmp[1] : tmp[2]);
           for (int i = 0; i < 9; ++i) cCi[i] += 0.5 * dt * CC1[i];
           for (int i = 0; i < 3; ++i) cai[i] += 0.5 * dt * CCa[i];
-          // Jacobian parts (ImuError.cpp:385-392)
-          const double wdt[3] = {w_true[0] * dt, w_true[1] * dt, w_true[2] * dt};
-          double Jr[9];
-          rightJacobian(wdt, Jr);
+          double Jr[9], Rdqi[9];
+          for (int i = 0; i < 9; ++i) {
+            Jr[i] = R[8 + i];
+            Rdqi[i] = R[17 + i];
+          }
           mm3(C1, Jr, tmp);
           adadbg += pick9(tmp, l) * dt;
-          double Rdqi[9], cross1[9];
-          qrot(qinv(dq), Rdqi);
+          double cross1[9];
           mm3(Rdqi, cross, tmp);
           for (int i = 0; i < 9; ++i) cross1[i] = tmp[i] + Jr[i] * dt;
           double ax[9], t1m[9], X[9];
@@ -456,37 +500,30 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
           for (int i = 0; i < 9; ++i) {
             cdvdbg[i] += 0.5 * dt * X[i];
             cross[i] = cross1[i];
+            C[i] = C1[i];
           }
           cdq = dq1;
-          // discrete noise of this step on the diagonal (ImuError.cpp:412-426, summed over sigma)
-          qa0 = sa_c * sa_c * (0.5 * dt * dt * dt * acc_sat * acc_sat * acc_sat);
-          qg = sg_c * sg_c * (gyr_sat * dt);
-          qa = sa_c * sa_c * (acc_sat * dt);
-          qbg = sgw_c * sgw_c * dt;
-          qba = saw_c * saw_c * dt;
-          time = nexttime;
-          ++steps;
-          if (nexttime == t1) running = false;
+          qa0 = R[26]; qg = R[27]; qa = R[28]; qbg = R[29]; qba = R[30];
         }
-      }
-      __syncthreads();
-      // P <- F P F^T + Q : M = F P (column l), exchange rows, P' = F M^T (column l)
-      if (doStep && l < 15) {
-        double Mc[15];
-        applyF(sF, Pc, Mc);
-        for (int i = 0; i < 15; ++i) sB[l * 16 + i] = Mc[i];  // column l of M
-      }
-      __syncthreads();
-      if (doStep && l < 15) {
-        double Mr[15];
-        for (int j = 0; j < 15; ++j) Mr[j] = sB[j * 16 + l];  // row l of M
-        applyF(sF, Mr, Pc);
-        for (int i = 0; i < 15; ++i) {
-          const double q = i < 3 ? qa0 : (i < 6 ? qg : (i < 9 ? qa : (i < 12 ? qbg : qba)));
-          Pc[i] += (i == l) ? q : 0.0;
+        __syncthreads();
+        // P <- F P F^T + Q : M = F P (column l), exchange rows, P' = F M^T (column l)
+        if (doStep && l < 15) {
+          double Mc[15];
+          applyF(sF, Pc, Mc);
+          for (int i = 0; i < 15; ++i) sB[l * 16 + i] = Mc[i];  // column l of M
         }
+        __syncthreads();
+        if (doStep && l < 15) {
+          double Mr[15];
+          for (int j = 0; j < 15; ++j) Mr[j] = sB[j * 16 + l];  // row l of M
+          applyF(sF, Mr, Pc);
+          for (int i = 0; i < 15; ++i) {
+            const double q = i < 3 ? qa0 : (i < 6 ? qg : (i < 9 ? qa : (i < 12 ? qbg : qba)));
+            Pc[i] += (i == l) ? q : 0.0;
+          }
+        }
+        __syncthreads();
       }
-      __syncthreads();
     }
   }
   // new preintegration state (ImuError.hpp:273-304 members) straight from the chain registers;
