@@ -21,7 +21,10 @@
 
 namespace okg {
 
-constexpr int kRB = 256;  // reduction workgroup size
+#ifndef OKG_RB
+#define OKG_RB 256
+#endif
+constexpr int kRB = OKG_RB;  // per-window workgroup size (k_reduce, k_gradnorm, k_dogleg)
 
 __device__ __forceinline__ double blockSum(double v, double* sh) {
   const int t = threadIdx.x;
