@@ -7,20 +7,29 @@ candidate evaluation + accept/reject) of EVERY window in the job's batch of inde
 S50 windows (50 keyframes, 2,000 landmarks, 16,000 reprojections, 49 IMU factors).
 value = (windows x timed iterations) / wall time of the timed region, max over ranks
 (window-iterations per second, whole job). Strong scaling: the total window count is fixed and
-split across ranks (one process per GPU, no data-path collective).
+split across ranks (one process per GPU, no data-path collective). At the end of the
+run the per-window summaries and final poses are all-gathered to rank 0 over RCCL (§8e), outside
+the timed region, and rank 0 checks that every window of the job ran every iteration.
+
+`--gpus N` without a launcher starts N ranks itself: a `torch.distributed.run` child process
+(this process never touches the GPU), one rank per GPU, 127.0.0.1 rendezvous.
 
 All tolerances are set to 0 so every timed iteration does real work (the K-iteration protocol of
 BASELINE.md); inputs are resident in HBM before the timed region.
 
-Also reported: the single-window latency mode (1 window on 1 GPU), per-kernel device time of one
-iteration (HIP events on the context's stream), the roofline of the dominant kernel, accuracy (ATE
-of window 0 vs ground truth for GPU and CPU oracle, max pose deviation GPU vs CPU), and the CPU
-baseline = the repo's CPU restatement (oracle/liboracle.so, "port") timed on this host.
+Also reported (rank 0): the single-window latency mode (the reference's own use: one window per
+::ceres::Solve) — resident iters/s and the end-to-end set_problems + solve wall time; per-kernel
+device time of one iteration (HIP events on the context's stream); the roofline of the dominant
+kernel against both the builder's byte model and SURVEY.md §8(d)'s compulsory bytes, plus the
+whole-iteration §8(d) HBM fraction; accuracy (ATE of window 0 vs ground truth for GPU and CPU
+oracle, max pose deviation); the CPU baseline = the repo's CPU restatement (oracle/liboracle.so,
+"port") at realtime_num_threads = 3 and at all host cores given to the job, median of 5.
 """
 import argparse
-import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,33 +37,66 @@ import numpy as np
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "okvis2-x_amd"))
-import okvisgpu as og  # noqa: E402
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (spec; SURVEY.md §8d, not in the gfx950 guide)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 SEED0 = 20251015
+METRIC = "Gauss-Newton iters/sec on 50-KF/2000-landmark window; ATE vs CPU ref"
 
 CONFIGS = {
     "s50": dict(n_kf=50, n_lm=2000, n_obs=16000),
     "s10": dict(n_kf=10, n_lm=500, n_obs=4000),
 }
 
+# summary columns gathered to rank 0 (cost, iterations, status per window)
+SUMMARY_COLS = ("window", "initial_cost", "final_cost", "num_iterations", "num_successful_steps",
+                "termination_type")
+
+
+def og_module():
+    import okvisgpu
+    return okvisgpu
+
 
 def bench_options(max_iter):
     # all tolerances 0: every iteration is performed (BASELINE.md timing protocol)
-    return og.default_options(max_num_iterations=max_iter, function_tolerance=0.0, gradient_tolerance=0.0,
-                              parameter_tolerance=0.0)
+    return og_module().default_options(max_num_iterations=max_iter, function_tolerance=0.0,
+                                       gradient_tolerance=0.0, parameter_tolerance=0.0)
 
 
 def make_windows(cfg, indices):
     """Synthetic windows, generated on host threads (the C generator runs outside the GIL)."""
     from concurrent.futures import ThreadPoolExecutor
+    og = og_module()
     indices = list(indices)
     mk = lambda i: og.SynthWindow(cfg["n_kf"], cfg["n_lm"], cfg["n_obs"], seed=SEED0 + i)  # noqa: E731
     if len(indices) < 16:
         return [mk(i) for i in indices]
-    with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4)) as ex:
+    with ThreadPoolExecutor(max_workers=min(16, host_threads())) as ex:
         return list(ex.map(mk, indices))
+
+
+def host_threads():
+    """Host cores given to this job: OMP_NUM_THREADS when the launcher sets it (16 per GPU on the
+    MI355X box), else the CPU affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def ate(P, gt):
@@ -81,7 +123,7 @@ def rank_windows(total, world, rank):
 
 
 def aggregate(dist, elapsed, early, device):
-    """Max of the timed region over ranks, sum of early-terminated windows (the only exchange)."""
+    """Max of the timed region over ranks, sum of early-terminated windows."""
     if dist is None:
         return elapsed, early
     import torch
@@ -92,9 +134,36 @@ def aggregate(dist, elapsed, early, device):
     return float(tmax[0].item()), int(tsum[1].item())
 
 
+def gather_rows(dist, rows, total, device):
+    """SURVEY.md §8e end-of-run gather: every rank holds the rows of its windows (rank_windows
+    order, float64 [n_mine, k]); returns the [total, k] array of the whole job on every rank (one
+    all_gather over RCCL/xGMI on the GPU box, gloo in the CPU tests). Ranks may hold different
+    counts (total % world != 0): rows are padded to the largest share and trimmed after."""
+    rows = np.ascontiguousarray(rows, dtype=np.float64)
+    if dist is None:
+        return rows
+    import torch
+    world = dist.get_world_size()
+    counts = [len(rank_windows(total, world, r)) for r in range(world)]
+    per = max(counts)
+    k = rows.shape[1]
+    buf = torch.zeros((per, k), dtype=torch.float64, device=device)
+    if len(rows):
+        buf[: len(rows)] = torch.from_numpy(rows).to(device)
+    parts = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf)
+    return np.concatenate([p[:c].cpu().numpy() for p, c in zip(parts, counts)], axis=0)
+
+
+def summary_rows(mine, sums):
+    return np.array([[i, s["initial_cost"], s["final_cost"], s["num_iterations"], s["num_successful_steps"],
+                      s["termination_type"]] for i, s in zip(mine, sums)], dtype=np.float64).reshape(-1, len(SUMMARY_COLS))
+
+
 def roofline_table(ctx, reps):
     """Per-kernel device time (HIP events on the context's stream, `reps` back-to-back launches of
     one iteration's worth on the resident data) and achieved rate of its algorithmic work."""
+    og = og_module()
     table = {}
     for name in og.kernel_names():  # every kernel okvisgpu_time_kernel exposes
         ms, work, bound = ctx.time_kernel(name, reps)
@@ -102,6 +171,27 @@ def roofline_table(ctx, reps):
         peak = HBM_PEAK_GBS if bound == "hbm" else FP64_MFMA_PEAK_TFLOPS
         table[name] = {"ms": ms, "bound": bound, "work": work, "achieved": rate, "peak": peak, "frac": rate / peak}
     return table
+
+
+def survey_bytes(st):
+    """SURVEY.md §8(d) compulsory HBM bytes of one iteration of the whole batch, with S counted
+    tile-sparse (the 64x64 tiles the LLT touches instead of d(d+1)/2), and its split onto the
+    kernels that own each term (VERDICT r01 decomposition). Returns (whole_iteration, per_kernel)."""
+    obs = 48.0 * st["n_observations"]                       # meas 16 + sqrtInfo 24 + idx 8
+    lm_rw = 2 * 4 * 8.0 * st["n_landmarks_free"]            # landmark read + write
+    params = 2 * 8.0 * (7 * st["n_poses"] + 9 * st["n_speed_biases"]) + lm_rw
+    imu = 2336.0 * st["n_imu"]                              # ImuError state 292 doubles
+    s_tiles = 64 * 64 * 8.0 * st["s_tiles_nonzero"]
+    vinv = 2 * 9 * 8.0 * st["n_landmarks_free"]            # per-landmark V^-1 / rhs
+    whole = obs + params + imu + 4 * s_tiles + vinv
+    per = {
+        "k_lm_visit": obs + lm_rw + vinv,                   # linearisation + landmark elimination
+        "k_cholesky": 3 * s_tiles,                          # read S, write L, read L for the solves
+        "k_assemble_pp": s_tiles,                           # write S (pose-pose and speed/bias blocks
+        "k_eval_obs": obs + params,                         #  counted on the larger kernel)
+        "k_eval_imu": imu,
+    }
+    return whole, per
 
 
 def pmc_traffic(kernel, windows):
@@ -138,7 +228,25 @@ def run_cpu_baseline(cfg, iters, threads, n_windows, reps):
     return ws[0], s0, float(np.median(times))
 
 
-def main():
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(argv, n):
+    """One process per GPU without an external launcher: run `torch.distributed.run` as a CHILD
+    process (this parent never touches the GPU and does not exec) and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -147,25 +255,105 @@ def main():
     ap.add_argument("--config", default="s50", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-threads", type=int, default=3, help="realtime_num_threads (okvis2.yaml:93)")
     ap.add_argument("--cpu-iters", type=int, default=None, help="default: warmup + steps")
-    ap.add_argument("--cpu-reps", type=int, default=3, help="median of this many timed passes after 1 warm-up")
-    ap.add_argument("--cpu-windows", type=int, default=24, help="windows in the CPU baseline sample")
+    ap.add_argument("--cpu-reps", type=int, default=5, help="median of this many timed passes after 1 warm-up")
+    ap.add_argument("--cpu-windows", type=int, default=6, help="windows in the CPU baseline sample")
     ap.add_argument("--kernel-reps", type=int, default=5, help="repetitions per kernel in the roofline table")
+    ap.add_argument("--e2e-reps", type=int, default=5, help="single-window set_problems + solve repetitions")
     ap.add_argument("--cholesky-schedule", type=int, default=0, help="0 auto, 1 persistent per window, 2 tile-parallel, 3 wave-specialised")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+
+def single_window(og, cfg, opts, args, device):
+    """The reference's own use: ONE window per ::ceres::Solve. Resident iters/s (K iterations timed
+    between two synchronisations) and the end-to-end wall time a ViGraph caller sees for a fresh
+    window: okvisgpu_set_problems (host structure analysis + upload) + okvisgpu_solve (K iterations +
+    write-back), median over repetitions."""
+    w1 = make_windows(cfg, [0])
+    c1 = og.Context(device)
+    c1.set_problems([w1[0].problem])
+    c1.solve_begin(opts)
+    c1.solve_iterate(args.warmup)
+    c1.synchronize()
+    a = time.perf_counter()
+    c1.solve_iterate(args.steps)
+    c1.synchronize()
+    b = time.perf_counter()
+    s1 = c1.solve_end()[0]
+    out = {"iters_per_s": args.steps / (b - a), "ms_per_iter": (b - a) / args.steps * 1e3,
+           "final_cost": s1["final_cost"]}
+    gpu_pose = w1[0].poses().copy()
+    gt_p, _, _ = w1[0].ground_truth()
+    e2e = []
+    total_iters = args.warmup + args.steps
+    for _ in range(args.e2e_reps + 1):
+        w1[0].reset()
+        t0 = time.perf_counter()
+        c1.set_problems([w1[0].problem])
+        c1.solve(opts)
+        e2e.append(time.perf_counter() - t0)
+    e2e = float(np.median(e2e[1:]))
+    out["e2e_set_problems_plus_solve_ms"] = e2e * 1e3
+    out["e2e_iterations"] = total_iters
+    out["e2e_iters_per_s"] = total_iters / e2e
+    if not args.no_profile:
+        w1[0].reset()
+        c1.update_params()
+        c1.solve_begin(opts)
+        c1.solve_iterate(args.warmup)
+        ph1 = c1.profile_iteration()
+        c1.solve_end()
+        out["kernel_ms_per_iteration"] = {k: round(v, 4) for k, v in ph1.items()}
+    c1.close()
+    return out, gpu_pose, gt_p
+
+
+def dry_run(args, world, rank):
+    """Launcher / gather plumbing without a GPU (tests/test_multirank.py): every rank takes its share,
+    the window summaries go through the same gather over gloo, rank 0 prints what it received."""
+    dist = None
+    if world > 1:
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo")
+        dist = tdist
+    mine = rank_windows(args.windows, world, rank)
+    rows = np.array([[i, 0.0, float(i), args.warmup + args.steps, 1, 0] for i in mine]).reshape(-1, len(SUMMARY_COLS))
+    got = gather_rows(dist, rows, args.windows, "cpu")
+    if rank == 0:
+        print(json.dumps({"world": world, "gpus": args.gpus, "windows": int(len(got)),
+                          "in_order": bool(np.array_equal(got[:, 0], np.arange(args.windows))),
+                          "master_addr": os.environ.get("MASTER_ADDR")}), flush=True)
+    if dist:
+        dist.destroy_process_group()
+    return 0
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None:
+        return launch_ranks(argv, args.gpus)
+    world = int(world_env or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("OKVISGPU_BENCH_DRYRUN") == "1":
+        return dry_run(args, world, rank)
     import torch
+    og = og_module()
     dist = None
+    device = f"cuda:{local_rank}"
     if world > 1:
         import torch.distributed as tdist
         torch.cuda.set_device(local_rank)
         tdist.init_process_group("nccl")
         dist = tdist
+        assert dist.get_world_size() == args.gpus
     cfg = CONFIGS[args.config]
 
     # ---- this rank's share of the fixed total (strong scaling)
@@ -173,6 +361,7 @@ def main():
     windows = make_windows(cfg, mine)
     ctx = og.Context(local_rank)
     ctx.set_problems([w.problem for w in windows])
+    stats = ctx.stats()
     total_iters = args.warmup + args.steps
     opts = bench_options(total_iters)
     opts.cholesky_schedule = args.cholesky_schedule
@@ -190,11 +379,17 @@ def main():
     t1 = time.perf_counter()
     if dist:
         dist.barrier()
-    sums = ctx.solve_end(len(windows))
+    sums = ctx.solve_end()
     elapsed = t1 - t0
     early = sum(1 for s in sums if s["num_iterations"] < total_iters)
     gn_frac = float(np.mean([(s["num_successful_steps"] - 1) / max(1, s["num_iterations"]) for s in sums]))
-    elapsed, early = aggregate(dist, elapsed, early, f"cuda:{local_rank}")
+    elapsed, early = aggregate(dist, elapsed, early, device)
+
+    # ---- §8e end-of-run gather (outside the timed region): summaries + final poses to every rank
+    g0 = time.perf_counter()
+    all_sums = gather_rows(dist, summary_rows(mine, sums), args.windows, device)
+    all_poses = gather_rows(dist, np.stack([w.poses().reshape(-1) for w in windows]), args.windows, device)
+    gather_s = time.perf_counter() - g0
 
     # per-solve rate including the PCIe upload of the parameters and the write-back (not `value`)
     for w in windows:
@@ -202,12 +397,12 @@ def main():
     ctx.synchronize()
     a = time.perf_counter()
     ctx.update_params()
-    ctx.solve(opts, len(windows))
+    ctx.solve(opts)
     pcie_s = time.perf_counter() - a
 
     value = args.windows * args.steps / elapsed
     result = {
-        "metric": "Gauss-Newton iters/sec on 50-KF/2000-landmark window; ATE vs CPU ref",
+        "metric": METRIC,
         "value": value,
         "unit": "window-iterations/s",
         "n_gpus": world,
@@ -232,66 +427,79 @@ def main():
     if args.cpu_iters is None:
         args.cpu_iters = total_iters
     if rank == 0:
+        ran_k = bool(np.all(all_sums[:, 3] == total_iters)) and len(all_sums) == args.windows
+        result["gather"] = {
+            "windows": int(len(all_sums)), "all_windows_ran_k_iterations": ran_k,
+            "windows_in_order": bool(np.array_equal(all_sums[:, 0], np.arange(args.windows))),
+            "final_cost_sum": float(all_sums[:, 2].sum()), "pose_bytes": int(all_poses.nbytes),
+            "ms": gather_s * 1e3,
+            "collective": "all_gather (RCCL over xGMI)" if dist else "none (1 rank)",
+        }
         result["early_terminated_windows"] = early
         result["per_solve_incl_pcie"] = {"wall_s": pcie_s, "iterations": total_iters,
                                          "window_iterations_per_s": len(windows) * total_iters / pcie_s}
         result["frac_iterations_with_gn_solve"] = gn_frac
-        # ---- single-window latency mode (1 window, this GPU)
+        result["problem_stats_per_gpu"] = stats
+        # ---- single-window latency mode (1 window, this GPU): the reference's own use
         if not args.no_latency:
-            w1 = make_windows(cfg, [0])
-            c1 = og.Context(local_rank)
-            c1.set_problems([w1[0].problem])
-            c1.solve_begin(opts)
-            c1.solve_iterate(args.warmup)
-            c1.synchronize()
-            a = time.perf_counter()
-            c1.solve_iterate(args.steps)
-            c1.synchronize()
-            b = time.perf_counter()
-            s1 = c1.solve_end(1)[0]
-            result["single_window"] = {"iters_per_s": args.steps / (b - a), "ms_per_iter": (b - a) / args.steps * 1e3,
-                                       "final_cost": s1["final_cost"]}
-            gpu_pose_w0 = w1[0].poses().copy()
-            gt_p, _, _ = w1[0].ground_truth()
-            if not args.no_profile:
-                w1[0].reset()
-                c1.update_params()
-                c1.solve_begin(opts)
-                c1.solve_iterate(args.warmup)
-                ph1 = c1.profile_iteration()
-                c1.solve_end(1)
-                result["single_window"]["kernel_ms_per_iteration"] = {k: round(v, 4) for k, v in ph1.items()}
-            c1.close()
+            sw, gpu_pose_w0, gt_p = single_window(og, cfg, opts, args, local_rank)
+            result["single_window"] = sw
+            result["single_window_iters_per_s"] = sw["iters_per_s"]
         # ---- roofline: per-kernel device time on the resident batch, dominant kernel by time
         if not args.no_profile:
             table = roofline_table(ctx, args.kernel_reps)
             dominant = max(table, key=lambda k: table[k]["ms"])
             d = table[dominant]
             traffic = pmc_traffic(dominant, len(mine))
+            whole, per = survey_bytes(stats)
+            ms_it = elapsed / args.steps * 1e3
+            survey = {k: {"bytes": v, "achieved_GBs": v / (table[k]["ms"] * 1e6),
+                          "frac": v / (table[k]["ms"] * 1e6) / HBM_PEAK_GBS} for k, v in per.items() if k in table}
             result["roofline"] = {
                 "kernel": dominant, "bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"],
                 "unit": "GB/s" if d["bound"] == "hbm" else "TFLOP/s", "frac": d["frac"],
                 "traffic": traffic,
                 "work_per_iteration": d["work"], "ms_per_iteration": d["ms"],
+                "frac_survey_8d": survey.get(dominant, {}).get("frac") if d["bound"] == "hbm" else None,
                 "method": f"HIP events on the context stream, {args.kernel_reps} launches of one iteration's "
-                          "worth on the resident batch; work = algorithmic bytes/FLOPs (DESIGN.md §4); traffic = "
+                          "worth on the resident batch; work = algorithmic bytes/FLOPs of the builder's model "
+                          "(DESIGN.md §4; FP64 flops of the tile-sparse LLT for k_cholesky); frac_survey_8d = "
+                          "SURVEY.md §8(d) compulsory bytes (S tile-sparse) / the same time; traffic = "
                           "rocprofv3 --pmc HBM bytes per iteration from profiles/pmc_traffic.json",
+            }
+            result["survey_8d"] = {
+                "whole_iteration_bytes": whole,
+                "whole_iteration_GBs": whole / (ms_it * 1e6),
+                "whole_iteration_frac_hbm": whole / (ms_it * 1e6) / HBM_PEAK_GBS,
+                "kernels": survey,
+                "note": "compulsory bytes of SURVEY.md §8(d) with S counted as its non-zero 64x64 tiles",
             }
             result["kernels"] = {k: {"ms": round(v["ms"], 4), "bound": v["bound"], "achieved": round(v["achieved"], 2),
                                      "frac": round(v["frac"], 4), "work": v["work"],
                                      "traffic": pmc_traffic(k, len(mine))} for k, v in table.items()}
         # ---- CPU baseline (oracle restatement timed on this host) + accuracy vs CPU
         if not args.no_cpu:
-            wc, sc, dt = run_cpu_baseline(cfg, args.cpu_iters, args.cpu_threads, args.cpu_windows, args.cpu_reps)
+            allc = host_threads()
+            variants = {}
+            wc = sc = None
+            for th in sorted({args.cpu_threads, allc}):
+                wct, sct, dt = run_cpu_baseline(cfg, args.cpu_iters, th, args.cpu_windows, args.cpu_reps)
+                variants[f"{th}_threads"] = {"value": args.cpu_windows * args.cpu_iters / dt, "wall_s": dt,
+                                             "single_window_iters_per_s": args.cpu_iters * args.cpu_windows / dt}
+                if th == args.cpu_threads:
+                    wc, sc = wct, sct
+            best = variants[f"{allc}_threads"]
             result["cpu_baseline"] = {
-                "value": args.cpu_windows * args.cpu_iters / dt,
+                "value": best["value"],
                 "unit": "window-iterations/s",
-                "cores": args.cpu_threads,
+                "cores": allc,
                 "kind": "port",
                 "sample": f"{args.cpu_windows} {args.config.upper()} windows x {args.cpu_iters} iterations each, "
-                          f"median of {args.cpu_reps} passes after 1 warm-up (oracle/liboracle.so, "
-                          f"{args.cpu_threads} threads = realtime_num_threads, same options)",
-                "wall_s": dt,
+                          f"median of {args.cpu_reps} passes after 1 warm-up (oracle/liboracle.so, same options); "
+                          f"value at all {allc} host threads given to the job, also at "
+                          f"{args.cpu_threads} = realtime_num_threads",
+                "host": {"cpu_model": cpu_model(), "host_threads": allc, "nproc": os.cpu_count()},
+                "variants": variants,
             }
             if not args.no_latency and args.cpu_iters == total_iters:
                 P0 = wc.poses()
@@ -301,14 +509,16 @@ def main():
                     "final_cost_gpu": result["single_window"]["final_cost"], "final_cost_cpu": sc["final_cost"],
                 }
             if not args.no_latency:
-                cpu_single = args.cpu_iters * args.cpu_windows / dt
-                result["single_window"]["speedup_vs_cpu"] = result["single_window"]["iters_per_s"] / cpu_single
+                sw = result["single_window"]
+                sw["speedup_vs_cpu_3_threads"] = sw["iters_per_s"] / variants[f"{args.cpu_threads}_threads"]["single_window_iters_per_s"]
+                sw["speedup_vs_cpu_all_threads"] = sw["iters_per_s"] / best["single_window_iters_per_s"]
             result["speedup_vs_cpu_baseline"] = value / result["cpu_baseline"]["value"]
         print(json.dumps(result), flush=True)
     ctx.close()
     if dist:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

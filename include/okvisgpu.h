@@ -224,7 +224,8 @@ int okvisgpu_update_params(okvisgpu_ctx* ctx);
 int okvisgpu_set_block_constant(okvisgpu_ctx* ctx, int32_t window, int32_t kind, int32_t index,
                                 int32_t is_constant);
 
-/* ::ceres::Solve equivalent for every window in the batch. summaries: [n_windows] (may be NULL).
+/* ::ceres::Solve equivalent for every window in the batch. summaries: NULL or an array of n_windows
+ * entries (n_windows of the last okvisgpu_set_problems: one summary is written for EVERY window).
  * Results are written back into the caller's parameter arrays (and imu_state when provided). */
 int okvisgpu_solve(okvisgpu_ctx* ctx, const okvisgpu_options* options, okvisgpu_summary* summaries);
 
@@ -312,6 +313,22 @@ void okvisgpu_graph_destroy(okvisgpu_graph* g);
 /* Component::save (Component.cpp:385-506) of a problem (one speed/bias block per state, isotropic
  * reprojection information): ids = problem indices, time stamps from state_t_ns or the IMU factors. */
 int okvisgpu_graph_save(const okvisgpu_problem* p, const int64_t* state_t_ns, const char* path);
+
+/* Problem statistics of the batch held by a context (the ::ceres::Solver::Summary counters
+ * num_parameter_blocks / num_residual_blocks / num_effective_parameters_reduced analogues, plus the
+ * layout figures bench.py's roofline work model needs). Sums over all windows. */
+typedef struct okvisgpu_problem_stats {
+  int32_t n_windows;
+  int32_t reserved_;
+  int64_t n_poses, n_speed_biases, n_landmarks, n_landmarks_free, n_extrinsics_free;
+  int64_t n_observations, n_visits, n_imu, n_imu_samples, n_pose_priors, n_sb_priors, n_relpose;
+  int64_t reduced_dim;              /* sum of the reduced (Schur) dimensions                      */
+  int64_t s_tiles_nonzero;          /* 64x64 tiles of S the tile-sparse LLT touches (incl. fill)  */
+  int64_t s_tiles_dense;            /* lower-triangle tiles of the dense reduced matrices          */
+  int64_t n_block_pairs, n_visit_segments, n_partial_blocks;
+  int64_t arena_bytes;              /* device memory held by the context                           */
+} okvisgpu_problem_stats;
+int okvisgpu_get_stats(okvisgpu_ctx* ctx, okvisgpu_problem_stats* stats);
 
 /* Copy device parameter values back into the caller's host arrays without solving. */
 int okvisgpu_get_params(okvisgpu_ctx* ctx);

@@ -25,6 +25,8 @@ namespace okg {
 #define OKG_RB 256
 #endif
 constexpr int kRB = OKG_RB;  // per-window workgroup size (k_reduce, k_gradnorm, k_dogleg)
+static_assert((kRB & (kRB - 1)) == 0 && kRB >= 64 && kRB <= 1024,
+              "OKG_RB must be a power of two in [64, 1024] (blockSum / blockMax tree reductions)");
 
 __device__ __forceinline__ double blockSum(double v, double* sh) {
   const int t = threadIdx.x;

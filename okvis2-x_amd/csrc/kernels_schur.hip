@@ -318,8 +318,12 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
 #pragma unroll
     for (int i = 0; i < kVisitZ / 2; ++i) zo[i] = double2{o[2 * i], o[2 * i + 1]};
   }
-  for (int c = t; c < npc; c += kLmGroupVisits) sPC[c] = P.part_contrib[pc0 + c];
+  // (a group of one landmark with more products than the stage holds streams them from HBM)
+  const bool staged = npc <= kLmPartStage;
+  if (staged)
+    for (int c = t; c < npc; c += kLmGroupVisits) sPC[c] = P.part_contrib[pc0 + c];
   __syncthreads();
+  const auto gPC = gmem(P.part_contrib + pc0);
   for (int e = t; e < npart * 3; e += kLmGroupVisits) {
     const int pi = e / 3, h = e - pi * 3;
     const int c0 = P.part_cbegin[pg0 + pi] - pc0, c1 = P.part_cbegin[pg0 + pi + 1] - pc0;
@@ -327,7 +331,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
 #pragma unroll
     for (int i = 0; i < 12; ++i) acc[i] = 0.0;
     for (int c = c0; c < c1; ++c) {
-      const int ab = sPC[c], a = ab & 0xffff, b = ab >> 16;
+      const int ab = staged ? sPC[c] : gPC[c], a = ab & 0xffff, b = ab >> 16;
       const double2* za2 = reinterpret_cast<const double2*>(sZ + kVisitZ * a + 6 * h);
       const double2* zb2 = reinterpret_cast<const double2*>(sZ + kVisitZ * b);
       double za[6], zb[18];

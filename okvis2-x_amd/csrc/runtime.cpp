@@ -162,7 +162,6 @@ void validate(const okvisgpu_problem* p, int w) {
 // Build the batch. `constOverride` carries okvisgpu_set_block_constant() edits.
 void analyse(const std::vector<const okvisgpu_problem*>& probs,
              const std::map<std::tuple<int, int, int>, int>& constOverride, HostBatch& B) {
-  B = HostBatch();
   B.seg_gbegin.push_back(0);
   B.part_gbegin.push_back(0);
   B.n_win = (int)probs.size();
@@ -383,11 +382,15 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
         B.seg_gbegin.push_back((int)B.seg_pose.size());
         B.part_gbegin.push_back((int)B.part_cbegin.size());
       };
-      // landmark-pair products a group stages in LDS (kLmPartStage) bound the group as well
+      // landmark-pair products a group stages in LDS (kLmPartStage) bound the group as well; only
+      // visits of free poses form products. A landmark with more products than the stage holds
+      // (>= 64 free observing poses, e.g. a long track in a full graph) gets a group of its own
+      // whose products k_lm_visit streams from HBM instead.
       auto pairCount = [&](int l) {
         if (!laNew[l]) return 0;
-        const int nv = lmVisitBegin[l + 1] - lmVisitBegin[l];
-        return nv * (nv + 1) / 2;
+        int nf = 0;
+        for (int v = lmVisitBegin[l]; v < lmVisitBegin[l + 1]; ++v) nf += posef[B.visit_pose[v] - pb] >= 0;
+        return nf * (nf + 1) / 2;
       };
       int gpc = 0;
       B.visit_slot.resize(B.visit_pose.size(), -1);
@@ -398,8 +401,6 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
           throw ArgError{"landmark with more than " + std::to_string(kLmGroupVisits) + " observing poses"};
         const int gv = lmVisitBegin[l] - lmVisitBegin[g0];
         const int pcl = pairCount(l);
-        if (pcl > kLmPartStage)
-          throw ArgError{"landmark with more than " + std::to_string(kLmPartStage) + " visit pairs"};
         if (l > g0 && (gv + nv > kLmGroupVisits || gl == kLmGroupMax || gpc + pcl > kLmPartStage)) {
           closeGroup(g0, l);
           g0 = l;
@@ -730,9 +731,17 @@ struct okvisgpu_ctx {
     }
   }
 
+  // (Re)build the device problem. Nothing of the previous batch survives a failure: the context
+  // holds no problem until a build completes (entry points then return OKVISGPU_ERR_NO_PROBLEM).
   void build() {
-    analyse(probs, constOverride, B);
+    haveProblem = false;
+    inSolve = false;
     dropGraph();
+    {
+      HostBatch nb;
+      analyse(probs, constOverride, nb);  // may throw: B is untouched until it succeeds
+      B = std::move(nb);
+    }
     if (arena) {
       HIPCHK(hipFree(arena));
       arena = nullptr;
@@ -1299,7 +1308,7 @@ int okvisgpu_solve(okvisgpu_ctx* c, const okvisgpu_options* o, okvisgpu_summary*
       const double iterTime = now - iterStart, cum = now - c->solveT0;
       bool changed = false;
       for (auto& s : st)
-        if (!s.done && c->replays > 0 && s.iteration >= o->min_iterations && cum + iterTime > o->time_limit_s) {
+        if (!s.done && s.iteration >= o->min_iterations && cum + iterTime > o->time_limit_s) {
           s.done = 1;
           s.termination = OKVISGPU_USER_SUCCESS;
           changed = true;
@@ -1510,6 +1519,34 @@ int okvisgpu_time_kernel(okvisgpu_ctx* c, int32_t kernel, int32_t reps, double* 
     if (bound) *bound = kKernelBound[kernel];
     return (int)OKVISGPU_OK;
   });
+}
+
+int okvisgpu_get_stats(okvisgpu_ctx* c, okvisgpu_problem_stats* st) {
+  if (!c || !st) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
+  const HostBatch& B = c->B;
+  const DevProblem& P = c->P;
+  std::memset(st, 0, sizeof(*st));
+  st->n_windows = B.n_win;
+  st->n_poses = P.n_pose;
+  st->n_speed_biases = P.n_sb;
+  st->n_landmarks = P.n_lm;
+  for (uint8_t f : B.lm_free) st->n_landmarks_free += f != 0;
+  st->n_observations = P.n_obs;
+  st->n_visits = P.n_visit;
+  st->n_imu = P.n_imu;
+  st->n_imu_samples = (int64_t)B.imu_ts.size();
+  st->n_pose_priors = P.n_pprior;
+  st->n_sb_priors = P.n_sbprior;
+  st->n_relpose = P.n_relpose;
+  st->reduced_dim = B.f_total;
+  st->s_tiles_nonzero = (int64_t)B.tile_items.size() / 3;
+  for (int T : B.tileT) st->s_tiles_dense += (int64_t)T * (T + 1) / 2;
+  st->n_block_pairs = P.n_pair;
+  st->n_visit_segments = P.n_seg;
+  st->n_partial_blocks = P.n_part;
+  st->arena_bytes = (int64_t)c->arenaBytes;
+  return OKVISGPU_OK;
 }
 
 int okvisgpu_evaluate(okvisgpu_ctx* c, int32_t window, double* cost) {

@@ -96,6 +96,17 @@ class SynthConfig(C.Structure):
                 ("n_relpose", C.c_int32), ("relpose_stride", C.c_int32), ("relpose_kind", C.c_int32)]
 
 
+class ProblemStats(C.Structure):
+    _fields_ = [("n_windows", C.c_int32), ("reserved_", C.c_int32)] + [(k, C.c_int64) for k in (
+        "n_poses", "n_speed_biases", "n_landmarks", "n_landmarks_free", "n_extrinsics_free", "n_observations",
+        "n_visits", "n_imu", "n_imu_samples", "n_pose_priors", "n_sb_priors", "n_relpose", "reduced_dim",
+        "s_tiles_nonzero", "s_tiles_dense", "n_block_pairs", "n_visit_segments", "n_partial_blocks",
+        "arena_bytes")]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved_"}
+
+
 class TwoPoseEdges(C.Structure):
     _fields_ = [("n_edges", C.c_int32), ("ref_pose", _dp), ("other_pose", _dp),
                 ("n_cameras", C.c_int32), ("cameras", C.POINTER(Camera)), ("extrinsics", _dp),
@@ -115,7 +126,7 @@ EXPORTED_SYMBOLS = [
     "okvisgpu_profile_iteration", "okvisgpu_phase_name", "okvisgpu_kernel_count", "okvisgpu_kernel_name",
     "okvisgpu_time_kernel", "okvisgpu_eval_relpose", "okvisgpu_twopose_compute",
     "okvisgpu_graph_load", "okvisgpu_graph_problem", "okvisgpu_graph_ids", "okvisgpu_graph_destroy",
-    "okvisgpu_graph_save",
+    "okvisgpu_graph_save", "okvisgpu_get_stats",
 ]
 N_PHASES = 15
 
@@ -171,6 +182,7 @@ def lib():
         L.okvisgpu_graph_ids.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), _lp, C.POINTER(C.c_uint64)]
         L.okvisgpu_graph_destroy.argtypes = [C.c_void_p]
         L.okvisgpu_graph_save.argtypes = [C.POINTER(Problem), _lp, C.c_char_p]
+        L.okvisgpu_get_stats.argtypes = [C.c_void_p, C.POINTER(ProblemStats)]
         L.okvisgpu_twopose_compute.argtypes = [C.c_void_p, C.POINTER(TwoPoseEdges), _dp, _dp, _dp, _dp, _dp]
         _lib = L
     return _lib
@@ -370,8 +382,9 @@ class Context:
 
     def set_problems(self, problems):
         arr = (Problem * len(problems))(*problems)
-        self._keep = (arr, problems)
+        self._keep = None
         self._check(lib().okvisgpu_set_problems(self.h, arr, len(problems)), "okvisgpu_set_problems")
+        self._keep = (arr, list(problems))
 
     def update_params(self):
         self._check(lib().okvisgpu_update_params(self.h), "okvisgpu_update_params")
@@ -380,9 +393,19 @@ class Context:
         self._check(lib().okvisgpu_set_block_constant(self.h, window, kind, index, int(is_constant)),
                     "okvisgpu_set_block_constant")
 
-    def solve(self, options: Optional[Options] = None, n_windows: int = 1):
+    def _n_windows(self, n_windows):
+        """Summaries are written for every window of the context (okvisgpu_solve / _solve_end fill
+        [n_windows] entries), so the buffer is sized from the problems held, never smaller."""
+        if self._keep is None:
+            raise OkvisGpuError("no problem set")
+        n = len(self._keep[1])
+        if n_windows is not None and n_windows != n:
+            raise ValueError(f"n_windows={n_windows} but the context holds {n} windows")
+        return n
+
+    def solve(self, options: Optional[Options] = None, n_windows: Optional[int] = None):
         o = options or default_options()
-        sums = (Summary * n_windows)()
+        sums = (Summary * self._n_windows(n_windows))()
         self._check(lib().okvisgpu_solve(self.h, C.byref(o), sums), "okvisgpu_solve")
         return [s.as_dict() for s in sums]
 
@@ -396,8 +419,8 @@ class Context:
     def synchronize(self):
         self._check(lib().okvisgpu_synchronize(self.h), "okvisgpu_synchronize")
 
-    def solve_end(self, n_windows: int = 1):
-        sums = (Summary * n_windows)()
+    def solve_end(self, n_windows: Optional[int] = None):
+        sums = (Summary * self._n_windows(n_windows))()
         self._check(lib().okvisgpu_solve_end(self.h, sums), "okvisgpu_solve_end")
         return [s.as_dict() for s in sums]
 
@@ -414,6 +437,11 @@ class Context:
         self._check(lib().okvisgpu_time_kernel(self.h, k, reps, C.byref(ms), C.byref(work), C.byref(bound)),
                     "okvisgpu_time_kernel")
         return ms.value, work.value, ("hbm", "mfma")[bound.value]
+
+    def stats(self):
+        st = ProblemStats()
+        self._check(lib().okvisgpu_get_stats(self.h, C.byref(st)), "okvisgpu_get_stats")
+        return st.as_dict()
 
     def get_params(self):
         self._check(lib().okvisgpu_get_params(self.h), "okvisgpu_get_params")

@@ -11,6 +11,9 @@
 // Ceres is UNPINNED (no Ceres in this container); see DESIGN.md.
 #include <chrono>
 #include <cfloat>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdio>
 #include <cstring>
 #include <limits>
@@ -231,17 +234,85 @@ void plusAll(const Program& P, const std::vector<double>& x, const double* delta
   }
 }
 
+// Persistent worker pool behind parallelFor (Ceres' ThreadPool + ParallelFor: workers are created
+// once, not per call). Work is split into nthreads static contiguous chunks, so every result is
+// independent of scheduling.
+class Pool {
+ public:
+  static Pool& get() {
+    static Pool pool;
+    return pool;
+  }
+  // run job(t) for t in [0, n) on n workers (the caller runs t = 0)
+  void run(int n, const std::function<void(int)>& job) {
+    std::lock_guard<std::mutex> serial(callMutex_);
+    ensure(n - 1);
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      job_ = &job;
+      want_ = n - 1;
+      pending_ = n - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    job(0);
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [&] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+      ++gen_;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+
+ private:
+  void ensure(int workers) {
+    while ((int)th_.size() < workers) {
+      const int id = (int)th_.size() + 1;
+      const uint64_t g = gen_;  // only run() (serialised by callMutex_) advances gen_
+      th_.emplace_back([this, id, g] { loop(id, g); });
+    }
+  }
+  void loop(int id, uint64_t seen) {  // joins from the job after generation `seen` on
+    for (;;) {
+      const std::function<void(int)>* job = nullptr;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        if (id > want_) continue;
+        job = job_;
+      }
+      (*job)(id);
+      std::lock_guard<std::mutex> lk(m_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::mutex callMutex_, m_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> th_;
+  const std::function<void(int)>* job_ = nullptr;
+  uint64_t gen_ = 0;
+  int want_ = 0, pending_ = 0;
+  bool stop_ = false;
+};
+
 template <class F>
 void parallelFor(int n, int nthreads, F f) {
   if (nthreads <= 1 || n < 64) { for (int i = 0; i < n; ++i) f(i); return; }
-  std::vector<std::thread> th;
   const int chunk = (n + nthreads - 1) / nthreads;
-  for (int t = 0; t < nthreads; ++t) {
+  const int nt = (n + chunk - 1) / chunk;
+  const std::function<void(int)> job = [&](int t) {
     const int b = t * chunk, e = std::min(n, b + chunk);
-    if (b >= e) break;
-    th.emplace_back([=]() { for (int i = b; i < e; ++i) f(i); });
-  }
-  for (auto& t : th) t.join();
+    for (int i = b; i < e; ++i) f(i);
+  };
+  Pool::get().run(nt, job);
 }
 
 // Evaluate one residual block: residuals (corrected), local Jacobian (corrected, row-major
@@ -428,46 +499,65 @@ void rightMultiply(const Program& P, const Linearization& L, const double* v, do
 // ------------------------------------------------------------------ dense LLT (Eigen LLT semantics)
 // Blocked right-looking Cholesky of the lower triangle of a row-major n x n matrix, in place.
 // Fails (returns k+1) at the first non-positive pivot like Eigen::LLT (x <= 0).
+// Envelope (profile) aware: with first[i] the column of row i's first non-zero, the factor keeps
+// that envelope (no fill left of it), so only products inside it are formed. The reduced camera
+// matrix of a sliding window is block-banded, so this does O(n b^2) instead of O(n^3 / 3) work;
+// the values are those of the dense algorithm (the skipped terms are exact zeros).
 int denseCholesky(int n, double* A, int nthreads) {
   const int nb = 64;
+  std::vector<int> first(n);
+  for (int i = 0; i < n; ++i) {
+    const double* Ai = &A[(size_t)i * n];
+    int j = 0;
+    while (j < i && Ai[j] == 0.0) ++j;
+    first[i] = j;
+  }
+  std::vector<int> rows;
   for (int k0 = 0; k0 < n; k0 += nb) {
     const int k1 = std::min(n, k0 + nb);
     // unblocked factorisation of the diagonal block
     for (int k = k0; k < k1; ++k) {
+      const int jk = std::max(k0, first[k]);
       double d = A[(size_t)k * n + k];
-      for (int j = k0; j < k; ++j) d -= A[(size_t)k * n + j] * A[(size_t)k * n + j];
+      for (int j = jk; j < k; ++j) d -= A[(size_t)k * n + j] * A[(size_t)k * n + j];
       if (!(d > 0.0)) return k + 1;
       d = std::sqrt(d);
       A[(size_t)k * n + k] = d;
       for (int i = k + 1; i < k1; ++i) {
+        if (first[i] > k) continue;
         double s = A[(size_t)i * n + k];
-        for (int j = k0; j < k; ++j) s -= A[(size_t)i * n + j] * A[(size_t)k * n + j];
+        for (int j = std::max(jk, first[i]); j < k; ++j) s -= A[(size_t)i * n + j] * A[(size_t)k * n + j];
         A[(size_t)i * n + k] = s / d;
       }
     }
     if (k1 >= n) break;
-    // panel: rows i >= k1, columns k0..k1 : L_ik = (A_ik - sum_j<k L_ij L_kj) / L_kk
-    const int rows = n - k1;
-    parallelFor(rows, nthreads, [&](int ii) {
-      const int i = k1 + ii;
+    // rows below the block whose envelope reaches into it
+    rows.clear();
+    for (int i = k1; i < n; ++i)
+      if (first[i] < k1) rows.push_back(i);
+    const int nr = (int)rows.size();
+    // panel: L_ik = (A_ik - sum_j<k L_ij L_kj) / L_kk
+    parallelFor(nr, nthreads, [&](int ii) {
+      const int i = rows[ii];
       double* Ai = &A[(size_t)i * n];
-      for (int k = k0; k < k1; ++k) {
+      for (int k = std::max(k0, first[i]); k < k1; ++k) {
         double s = Ai[k];
         const double* Ak = &A[(size_t)k * n];
-        for (int j = k0; j < k; ++j) s -= Ai[j] * Ak[j];
+        for (int j = std::max(std::max(k0, first[i]), first[k]); j < k; ++j) s -= Ai[j] * Ak[j];
         Ai[k] = s / Ak[k];
       }
     });
-    // trailing update: A_ij -= L_i(k0:k1) . L_j(k0:k1) for k1 <= j <= i
-    parallelFor(rows, nthreads, [&](int ii) {
-      const int i = k1 + ii;
+    // trailing update: A_ij -= L_i(k0:k1) . L_j(k0:k1) for rows i, j of the list, j <= i
+    parallelFor(nr, nthreads, [&](int ii) {
+      const int i = rows[ii];
       double* Ai = &A[(size_t)i * n];
-      const double* Li = &A[(size_t)i * n + k0];
-      const int w = k1 - k0;
-      for (int j = k1; j <= i; ++j) {
-        const double* Lj = &A[(size_t)j * n + k0];
+      for (int jj = 0; jj <= ii; ++jj) {
+        const int j = rows[jj];
+        const int lo = std::max(k0, std::max(first[i], first[j]));
+        const double* Li = Ai;
+        const double* Lj = &A[(size_t)j * n];
         double s = 0;
-        for (int k = 0; k < w; ++k) s += Li[k] * Lj[k];
+        for (int k = lo; k < k1; ++k) s += Li[k] * Lj[k];
         Ai[j] -= s;
       }
     });
@@ -566,16 +656,19 @@ void buildReduced(const Program& P, const Linearization& L, const double* D, Red
       }
     }
   }
-  // Chunks: one per e-block (landmark).
-  std::vector<std::vector<double>> partialLhs(1);
-  (void)nthreads;
-  for (int e = 0; e < P.ne; ++e) {
+  // Chunks: one per e-block (landmark). Phase 1 (parallel over landmarks): per landmark and
+  // f-block the local F^T F, F^T b and W = F^T E, then (E^T E + D^2)^-1 and z. Phase 2 (parallel
+  // over owners of f-block rows): every lhs / rhs row is accumulated by one thread, landmark by
+  // landmark in e order, so the result does not depend on the thread count.
+  struct FAcc { int fid; int foff; int loc; double W[27]; double H[81]; double g[9]; };
+  struct Chunk { std::vector<FAcc> f; double z[3]; };
+  std::vector<Chunk> chunks(P.ne);
+  std::vector<int> failed(P.ne, 0);
+  parallelFor(P.ne, nthreads, [&](int e) {
     const int eid = P.eOrder[e];
     const PBlock& eb = P.pbs[eid];
     double ete[9] = {0}, ge[3] = {0};
-    // per f-block of this chunk: W_f = sum F^T E (loc x 3), diag F^T F, F^T b
-    struct FAcc { int fid; int foff; int loc; double W[27]; };
-    std::vector<FAcc> facc;
+    std::vector<FAcc>& facc = chunks[e].f;
     for (int ri : P.chunkRows[e]) {
       const RBlock& r = P.rbs[ri];
       const double* J = &L.jac[r.jacoff];
@@ -595,10 +688,12 @@ void buildReduced(const Program& P, const Linearization& L, const double* D, Red
       forEachJacBlock(P, ri, [&](const PBlock& pb, int col) {
         if (&pb == &eb) return;
         const int id = (int)(&pb - &P.pbs[0]);
-        const int fo = P.fOffset[id];
         FAcc* a = nullptr;
         for (auto& x : facc) if (x.fid == id) a = &x;
-        if (!a) { facc.push_back(FAcc{id, fo, pb.loc, {0}}); a = &facc.back(); }
+        if (!a) {
+          facc.push_back(FAcc{id, P.fOffset[id], pb.loc, {0}, {0}, {0}});
+          a = &facc.back();
+        }
         for (int u = 0; u < pb.loc; ++u)
           for (int v = 0; v < 3; ++v) {
             double s = 0;
@@ -609,11 +704,11 @@ void buildReduced(const Program& P, const Linearization& L, const double* D, Red
         for (int u = 0; u < pb.loc; ++u) {
           double g = 0;
           for (int i = 0; i < r.nres; ++i) g += J[i * r.jcols + col + u] * b[i];
-          R.rhs[fo + u] += g;
+          a->g[u] += g;
           for (int v = 0; v < pb.loc; ++v) {
             double s = 0;
             for (int i = 0; i < r.nres; ++i) s += J[i * r.jcols + col + u] * J[i * r.jcols + col + v];
-            R.lhs[(size_t)(fo + u) * fd + fo + v] += s;
+            a->H[u * pb.loc + v] += s;
           }
         }
       });
@@ -621,25 +716,48 @@ void buildReduced(const Program& P, const Linearization& L, const double* D, Red
     if (D)
       for (int u = 0; u < 3; ++u) ete[u * 3 + u] += D[eb.toff + u] * D[eb.toff + u];
     double inv[9];
-    if (!invertSpd3(ete, inv)) { R.ok = false; return; }
+    if (!invertSpd3(ete, inv)) { failed[e] = 1; return; }
     for (int k = 0; k < 9; ++k) R.einv[(size_t)e * 9 + k] = inv[k];
-    double z[3];
-    for (int u = 0; u < 3; ++u) z[u] = inv[u * 3 + 0] * ge[0] + inv[u * 3 + 1] * ge[1] + inv[u * 3 + 2] * ge[2];
-    for (const FAcc& a : facc) {
-      // rhs_f -= W_f z
-      for (int u = 0; u < a.loc; ++u)
-        R.rhs[a.foff + u] -= a.W[u * 3 + 0] * z[0] + a.W[u * 3 + 1] * z[1] + a.W[u * 3 + 2] * z[2];
-      // Y = W_f inv  (loc x 3)
-      double Y[27];
-      for (int u = 0; u < a.loc; ++u)
-        for (int v = 0; v < 3; ++v)
-          Y[u * 3 + v] = a.W[u * 3 + 0] * inv[0 * 3 + v] + a.W[u * 3 + 1] * inv[1 * 3 + v] + a.W[u * 3 + 2] * inv[2 * 3 + v];
-      for (const FAcc& c : facc)
+    for (int u = 0; u < 3; ++u)
+      chunks[e].z[u] = inv[u * 3 + 0] * ge[0] + inv[u * 3 + 1] * ge[1] + inv[u * 3 + 2] * ge[2];
+  });
+  for (int e = 0; e < P.ne; ++e)
+    if (failed[e]) { R.ok = false; return; }
+  // phase 2: thread t owns the f-blocks t, t + T, ... (rows of lhs / rhs)
+  const int nf = (int)P.fblocks.size();
+  std::vector<int> ownerOf(P.pbs.size(), -1);
+  const int T = std::max(1, std::min(nthreads, nf));
+  for (int k = 0; k < nf; ++k) ownerOf[P.fblocks[k]] = k % T;
+  auto rowPass = [&](int t) {
+    for (int e = 0; e < P.ne; ++e) {
+      const Chunk& c = chunks[e];
+      const double* inv = &R.einv[(size_t)e * 9];
+      for (const FAcc& a : c.f) {
+        if (ownerOf[a.fid] != t) continue;
+        for (int u = 0; u < a.loc; ++u) {
+          R.rhs[a.foff + u] += a.g[u];
+          for (int v = 0; v < a.loc; ++v) R.lhs[(size_t)(a.foff + u) * fd + a.foff + v] += a.H[u * a.loc + v];
+        }
+        // rhs_f -= W_f z
         for (int u = 0; u < a.loc; ++u)
-          for (int v = 0; v < c.loc; ++v)
-            R.lhs[(size_t)(a.foff + u) * fd + c.foff + v] -=
-                Y[u * 3 + 0] * c.W[v * 3 + 0] + Y[u * 3 + 1] * c.W[v * 3 + 1] + Y[u * 3 + 2] * c.W[v * 3 + 2];
+          R.rhs[a.foff + u] -= a.W[u * 3 + 0] * c.z[0] + a.W[u * 3 + 1] * c.z[1] + a.W[u * 3 + 2] * c.z[2];
+        // Y = W_f inv  (loc x 3); lhs_ac -= Y W_c^T
+        double Y[27];
+        for (int u = 0; u < a.loc; ++u)
+          for (int v = 0; v < 3; ++v)
+            Y[u * 3 + v] = a.W[u * 3 + 0] * inv[0 * 3 + v] + a.W[u * 3 + 1] * inv[1 * 3 + v] + a.W[u * 3 + 2] * inv[2 * 3 + v];
+        for (const FAcc& cc : c.f)
+          for (int u = 0; u < a.loc; ++u)
+            for (int v = 0; v < cc.loc; ++v)
+              R.lhs[(size_t)(a.foff + u) * fd + cc.foff + v] -=
+                  Y[u * 3 + 0] * cc.W[v * 3 + 0] + Y[u * 3 + 1] * cc.W[v * 3 + 1] + Y[u * 3 + 2] * cc.W[v * 3 + 2];
+      }
     }
+  };
+  if (T <= 1) rowPass(0);
+  else {
+    const std::function<void(int)> job = rowPass;
+    Pool::get().run(T, job);
   }
   if (D)
     for (int f : P.fblocks) {

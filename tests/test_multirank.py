@@ -58,3 +58,66 @@ def test_gloo_two_ranks_aggregate():
     expect_early = (256 % 3) + (256 % 3 + 1)
     for _, _, (elapsed, early) in res:
         assert elapsed == 1.5 and early == expect_early
+
+
+def _gather_worker(rank, world, port, total, q):
+    import numpy as np
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = bench.rank_windows(total, world, rank)
+    sums = [{"initial_cost": 10.0 + i, "final_cost": 1.0 + i, "num_iterations": 13, "num_successful_steps": 12,
+             "termination_type": 1} for i in mine]
+    got = bench.gather_rows(dist, bench.summary_rows(mine, sums), total, "cpu")
+    poses = bench.gather_rows(dist, np.full((len(mine), 14), float(rank)), total, "cpu")
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, got.tolist(), poses.tolist()))
+
+
+@pytest.mark.parametrize("total", [8, 7])
+def test_gloo_two_ranks_gather(total):
+    """SURVEY.md §8e end-of-run gather: per-window summaries and final poses of every rank reach
+    every rank in window order, also when the ranks hold different counts (7 = 4 + 3)."""
+    import numpy as np
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 2, port, total, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, got, poses in res:
+        got, poses = np.array(got), np.array(poses)
+        assert got.shape == (total, len(bench.SUMMARY_COLS))
+        assert np.array_equal(got[:, 0], np.arange(total))
+        assert np.array_equal(got[:, 2], 1.0 + np.arange(total))
+        n0 = len(bench.rank_windows(total, 2, 0))
+        assert np.all(poses[:n0] == 0.0) and np.all(poses[n0:] == 1.0)
+
+
+def test_launcher_starts_n_ranks():
+    """`bench.py --gpus 2` without WORLD_SIZE starts two ranks through a torch.distributed.run child
+    process (127.0.0.1 rendezvous); the dry-run mode exercises the rank env and the gather on gloo
+    without touching a GPU."""
+    import json
+    import subprocess
+    env = dict(os.environ, OKVISGPU_BENCH_DRYRUN="1")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--windows", "9"],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    assert d == {"world": 2, "gpus": 2, "windows": 9, "in_order": True, "master_addr": "127.0.0.1"}
+
+
+def test_world_size_mismatch_is_an_error():
+    import subprocess
+    env = dict(os.environ, OKVISGPU_BENCH_DRYRUN="1", WORLD_SIZE="1")
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 2 and "WORLD_SIZE" in out.stderr
