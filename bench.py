@@ -256,7 +256,7 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=3, help="realtime_num_threads (okvis2.yaml:93)")
     ap.add_argument("--cpu-iters", type=int, default=None, help="default: warmup + steps")
     ap.add_argument("--cpu-reps", type=int, default=5, help="median of this many timed passes after 1 warm-up")
-    ap.add_argument("--cpu-windows", type=int, default=6, help="windows in the CPU baseline sample")
+    ap.add_argument("--cpu-windows", type=int, default=24, help="windows in the CPU baseline sample")
     ap.add_argument("--kernel-reps", type=int, default=5, help="repetitions per kernel in the roofline table")
     ap.add_argument("--e2e-reps", type=int, default=5, help="single-window set_problems + solve repetitions")
     ap.add_argument("--cholesky-schedule", type=int, default=0, help="0 auto, 1 persistent per window, 2 tile-parallel, 3 wave-specialised")

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OKVISGPU_ABI_VERSION 3
+#define OKVISGPU_ABI_VERSION 4
 
 /* ---------------------------------------------------------------- status codes */
 typedef enum okvisgpu_status {
@@ -53,7 +53,12 @@ typedef enum okvisgpu_distortion {
 } okvisgpu_distortion;
 
 typedef enum okvisgpu_linear_solver {
-  OKVISGPU_DENSE_SCHUR = 0          /* ViSlamBackend.cpp:877 realtime graph */
+  OKVISGPU_DENSE_SCHUR = 0,         /* ViSlamBackend.cpp:877 realtime graph */
+  OKVISGPU_SPARSE_NORMAL_CHOLESKY = 1 /* ViGraph.cpp:248 (full graph, ViSlamBackend.cpp:1988-1997):
+                                       the Gauss-Newton step solves the same normal equations; it
+                                       is computed through the exact tile-sparse Schur complement
+                                       (landmarks eliminated, band-envelope LLT of the reduced
+                                       matrix), so both options give the same step up to rounding */
 } okvisgpu_linear_solver;
 
 typedef enum okvisgpu_tr_strategy {
@@ -106,7 +111,9 @@ typedef struct okvisgpu_problem {
   const uint8_t* landmark_constant;
   int32_t n_cameras;
   const okvisgpu_camera* cameras;   /* [n_cameras]                                             */
-  const double* extrinsics;         /* [n_cameras][7] T_SC — constant (do_extrinsics: false)    */
+  double* extrinsics;               /* [n_cameras][7] T_SC, one block per camera shared by all
+                                       states (ViGraph::addStatesPropagate re-uses the block,
+                                       ViGraph.cpp:469-473); written back when variable          */
 
   /* --- ReprojectionError<PinholeCamera<D>> residual blocks (ViGraph.hpp:307-352) */
   int32_t n_observations;
@@ -158,6 +165,16 @@ typedef struct okvisgpu_problem {
    *     LLT(information).L^T, relpose_delta_x unused;
    *     r = L [r_AB_meas - r_AB; 2 vec(q_AB_meas q_AB^-1)], T_AB = T_WA^-1 T_WB                 */
   const uint8_t* relpose_kind;
+
+  /* --- ABI 4: variable extrinsics (online calibration, do_extrinsics: true; ViGraph.cpp:330-386)
+   * extrinsics_constant [n_cameras]: 0 = the camera's T_SC block is variable (NULL = all constant,
+   * do_extrinsics: false). Its PoseError prior, PoseError(T_SC, sigma_r^2, sigma_alpha^2)
+   * (ViGraph.cpp:372-382, PoseError.cpp:73-125), comes through the extrinsics_prior_* arrays. */
+  const uint8_t* extrinsics_constant;
+  int32_t n_extrinsics_priors;
+  const int32_t* extrinsics_prior_camera; /* [n] camera index                                   */
+  const double* extrinsics_prior_meas;    /* [n][7]                                             */
+  const double* extrinsics_prior_sqrt_info; /* [n][36] row-major                                */
 } okvisgpu_problem;
 
 /* ---------------------------------------------------------------- solver options / summary */

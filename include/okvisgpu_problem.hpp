@@ -1,0 +1,647 @@
+// okvisgpu_problem.hpp — C++ facade with the subset of the `::ceres::Problem` API that okvis drives,
+// recording the graph and solving it through the okvisgpu C ABI (okvisgpu.h). Header-only, C++17,
+// no Ceres / Eigen / HIP types: it compiles with any host compiler and links against
+// libokvisgpu.so.
+//
+// What it replaces: `ViGraph::problem_` (a `::ceres::Problem`,
+// okvis_ceres/include/okvis/ViGraph.hpp:27-39) and the `::ceres::Solve(options_, problem_.get(),
+// &summary_)` call of `ViGraph::optimise` (ViGraph.cpp:1884). Method names, argument meaning and
+// ownership follow the call sites:
+//   AddParameterBlock(ptr, size[, manifold])          ViGraph.cpp:327-345, ViGraphEstimator.cpp:84-126
+//   AddResidualBlock(cost, loss, ptrs...)             ViGraph.cpp:367-385,433-459; ViGraph.hpp:336-340
+//   RemoveResidualBlock / RemoveParameterBlock        ViGraph.cpp:597,611,626-637,700-702
+//   SetParameterBlockConstant / Variable              ViGraphEstimator.cpp:216-331, ViSlamBackend.cpp:854-863
+//   HasParameterBlock, IsParameterBlockConstant, NumResidualBlocks, NumParameterBlocks,
+//   GetParameterBlocksForResidualBlock, GetResidualBlocksForParameterBlock,
+//   GetCostFunctionForResidualBlock, GetLossFunctionForResidualBlock, GetManifold, SetManifold
+// Cost functions are recognised by their `typeInfo()` string, as okvis' ErrorInterface::typeInfo()
+// (okvis_ceres/include/okvis/ceres/ErrorInterface.hpp:78) names them: "ReprojectionError",
+// "ImuError", "PoseError", "SpeedAndBiasError", "TwoPoseStandardGraphError(Const)",
+// "RelativePoseError". The term classes below carry the constants the adapter reads from the okvis
+// functors' getters. Any other cost function (GPS, SubmapICP, depth, ...) is
+// rejected at AddResidualBlock with an okvisgpu::Unsupported exception (OKVISGPU_ERR_UNSUPPORTED):
+// the caller keeps its Ceres solve for such a graph.
+//
+// Ownership: like `Problem::Options{DO_NOT_TAKE_OWNERSHIP}` (ViGraph.cpp:239-247), the facade never
+// deletes cost functions, losses or manifolds; parameter memory stays the caller's and is read
+// before and written after every Solve (the reference's in-place ParameterBlock semantics).
+// Errors: misuse (unknown block, wrong sizes) throws okvisgpu::Error (a std::runtime_error, as
+// OKVIS_THROW does); Solve returns the okvisgpu_status of the C ABI.
+#pragma once
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "okvisgpu.h"
+
+namespace okvisgpu {
+
+struct Error : std::runtime_error {
+  explicit Error(const std::string& m) : std::runtime_error("okvisgpu: " + m) {}
+};
+struct Unsupported : Error {
+  explicit Unsupported(const std::string& m) : Error(m) {}
+  int status() const { return OKVISGPU_ERR_UNSUPPORTED; }
+};
+
+// ---------------------------------------------------------------- manifolds (ceres::Manifold)
+class Manifold {
+ public:
+  virtual ~Manifold() = default;
+  virtual int AmbientSize() const = 0;
+  virtual int TangentSize() const = 0;
+  virtual const char* name() const = 0;
+};
+// PoseManifold (okvis_ceres/src/PoseLocalParameterization.cpp:29-107): [t, q xyzw], 7 -> 6
+class PoseManifold final : public Manifold {
+ public:
+  int AmbientSize() const override { return 7; }
+  int TangentSize() const override { return 6; }
+  const char* name() const override { return "PoseManifold"; }
+};
+// HomogeneousPointManifold (HomogeneousPointLocalParameterization.cpp:27-90): 4 -> 3
+class HomogeneousPointManifold final : public Manifold {
+ public:
+  int AmbientSize() const override { return 4; }
+  int TangentSize() const override { return 3; }
+  const char* name() const override { return "HomogeneousPointManifold"; }
+};
+
+// ---------------------------------------------------------------- losses (ceres::LossFunction)
+class LossFunction {
+ public:
+  virtual ~LossFunction() = default;
+  virtual const char* name() const = 0;
+};
+// CauchyLoss(1.0) on every reprojection (ViGraph.cpp:235,338); other scales are not on the path
+class CauchyLoss final : public LossFunction {
+ public:
+  explicit CauchyLoss(double a = 1.0) : a_(a) {
+    if (a != 1.0) throw Unsupported("CauchyLoss scale other than 1 (okvis uses CauchyLoss(1.0))");
+  }
+  const char* name() const override { return "CauchyLoss"; }
+
+ private:
+  double a_;
+};
+
+// ---------------------------------------------------------------- cost functions
+// The okvis functors' constants (what the GPU evaluates from); typeInfo() as ErrorInterface.
+class CostFunction {
+ public:
+  virtual ~CostFunction() = default;
+  virtual std::string typeInfo() const = 0;
+  virtual int residualDim() const = 0;
+  virtual std::vector<int> parameterBlockSizes() const = 0;  // ambient sizes, in call order
+};
+
+// ReprojectionError<PinholeCamera<D>> (implementation/ReprojectionError.hpp:49-220): parameters
+// (T_WS pose, hp_W landmark, T_SC extrinsics); camera = the functor's cameraGeometry_.
+class ReprojectionError final : public CostFunction {
+ public:
+  ReprojectionError(const okvisgpu_camera& camera, const double keypoint[2], const double sqrt_info[4])
+      : camera(camera) {
+    std::memcpy(this->keypoint, keypoint, sizeof(this->keypoint));
+    std::memcpy(this->sqrt_info, sqrt_info, sizeof(this->sqrt_info));
+  }
+  std::string typeInfo() const override { return "ReprojectionError"; }
+  int residualDim() const override { return 2; }
+  std::vector<int> parameterBlockSizes() const override { return {7, 4, 7}; }
+  okvisgpu_camera camera;
+  double keypoint[2];   // measurement_
+  double sqrt_info[4];  // squareRootInformation_ (row-major)
+};
+
+// ImuError (ImuError.cpp:63-1003): parameters (pose0, sb0, pose1, sb1). `state` is the functor's
+// mutable preintegration state (OKVISGPU_IMU_STATE_DOUBLES layout), written back after a solve.
+class ImuError final : public CostFunction {
+ public:
+  ImuError(std::vector<int64_t> sample_t_ns, std::vector<double> gyr_acc, const okvisgpu_imu_params& params,
+           int64_t t0_ns, int64_t t1_ns)
+      : sample_t_ns(std::move(sample_t_ns)), gyr_acc(std::move(gyr_acc)), params(params), t0_ns(t0_ns),
+        t1_ns(t1_ns), state(OKVISGPU_IMU_STATE_DOUBLES, 0.0) {
+    if (this->gyr_acc.size() != 6 * this->sample_t_ns.size()) throw Error("ImuError: gyr_acc must hold 6 per sample");
+  }
+  std::string typeInfo() const override { return "ImuError"; }
+  int residualDim() const override { return 15; }
+  std::vector<int> parameterBlockSizes() const override { return {7, 9, 7, 9}; }
+  std::vector<int64_t> sample_t_ns;
+  std::vector<double> gyr_acc;
+  okvisgpu_imu_params params;
+  int64_t t0_ns, t1_ns;
+  std::vector<double> state;
+};
+
+// PoseError (PoseError.cpp:73-125): a prior on a pose or an extrinsics block.
+class PoseError final : public CostFunction {
+ public:
+  PoseError(const double measurement[7], const double sqrt_info[36]) {
+    std::memcpy(meas, measurement, sizeof(meas));
+    std::memcpy(this->sqrt_info, sqrt_info, sizeof(this->sqrt_info));
+  }
+  std::string typeInfo() const override { return "PoseError"; }
+  int residualDim() const override { return 6; }
+  std::vector<int> parameterBlockSizes() const override { return {7}; }
+  double meas[7];
+  double sqrt_info[36];
+};
+
+// SpeedAndBiasError (SpeedAndBiasError.cpp:67-101).
+class SpeedAndBiasError final : public CostFunction {
+ public:
+  SpeedAndBiasError(const double measurement[9], const double sqrt_info[81]) {
+    std::memcpy(meas, measurement, sizeof(meas));
+    std::memcpy(this->sqrt_info, sqrt_info, sizeof(this->sqrt_info));
+  }
+  std::string typeInfo() const override { return "SpeedAndBiasError"; }
+  int residualDim() const override { return 9; }
+  std::vector<int> parameterBlockSizes() const override { return {9}; }
+  double meas[9];
+  double sqrt_info[81];
+};
+
+// TwoPoseStandardGraphError / ...Const (TwoPoseGraphError.cpp:467-606,631-767): parameters
+// (reference pose, other pose); DeltaX_, J_, linearisationPoint_T_S0S1_.
+class TwoPoseGraphError final : public CostFunction {
+ public:
+  TwoPoseGraphError(const double delta_x[6], const double J[36], const double lin_point[7], bool is_const = true)
+      : is_const(is_const) {
+    std::memcpy(this->delta_x, delta_x, sizeof(this->delta_x));
+    std::memcpy(this->J, J, sizeof(this->J));
+    std::memcpy(this->lin_point, lin_point, sizeof(this->lin_point));
+  }
+  std::string typeInfo() const override {
+    return is_const ? "TwoPoseStandardGraphErrorConst" : "TwoPoseStandardGraphError";
+  }
+  int residualDim() const override { return 6; }
+  std::vector<int> parameterBlockSizes() const override { return {7, 7}; }
+  double delta_x[6], J[36], lin_point[7];
+  bool is_const;
+};
+
+// RelativePoseError (RelativePoseError.cpp:59-140, ViGraph::addRelativePoseConstraint): (A, B).
+class RelativePoseError final : public CostFunction {
+ public:
+  RelativePoseError(const double T_AB[7], const double sqrt_info[36]) {
+    std::memcpy(this->T_AB, T_AB, sizeof(this->T_AB));
+    std::memcpy(this->sqrt_info, sqrt_info, sizeof(this->sqrt_info));
+  }
+  std::string typeInfo() const override { return "RelativePoseError"; }
+  int residualDim() const override { return 6; }
+  std::vector<int> parameterBlockSizes() const override { return {7, 7}; }
+  double T_AB[7], sqrt_info[36];
+};
+
+// ---------------------------------------------------------------- Problem
+struct ResidualBlock;
+using ResidualBlockId = ResidualBlock*;
+
+struct ResidualBlock {
+  CostFunction* cost;
+  LossFunction* loss;
+  std::vector<double*> blocks;
+};
+
+class Problem {
+ public:
+  explicit Problem(int device = 0) : device_(device) {}
+  ~Problem() {
+    if (ctx_) okvisgpu_ctx_destroy(ctx_);
+  }
+  Problem(const Problem&) = delete;
+  Problem& operator=(const Problem&) = delete;
+
+  // ---- parameter blocks
+  void AddParameterBlock(double* values, int size, Manifold* manifold = nullptr) {
+    if (!values) throw Error("AddParameterBlock: null pointer");
+    if (size != 4 && size != 7 && size != 9) throw Unsupported("parameter block of size " + std::to_string(size));
+    auto it = params_.find(values);
+    if (it != params_.end()) {  // Ceres: re-adding with the same size is a no-op
+      if (it->second.size != size) throw Error("AddParameterBlock: block re-added with another size");
+      if (manifold) it->second.manifold = manifold;
+      return;
+    }
+    checkManifold(size, manifold);
+    Param p;
+    p.size = size;
+    p.manifold = manifold;
+    p.order = nextOrder_++;
+    params_[values] = p;
+    dirty_ = true;
+  }
+  void SetManifold(double* values, Manifold* manifold) {
+    Param& p = param(values, "SetManifold");
+    checkManifold(p.size, manifold);
+    p.manifold = manifold;
+    dirty_ = true;
+  }
+  const Manifold* GetManifold(const double* values) const { return param(values, "GetManifold").manifold; }
+  bool HasParameterBlock(const double* values) const { return params_.count(const_cast<double*>(values)) != 0; }
+  int NumParameterBlocks() const { return (int)params_.size(); }
+  int ParameterBlockSize(const double* values) const { return param(values, "ParameterBlockSize").size; }
+
+  void SetParameterBlockConstant(const double* values) { setConstant(values, true); }
+  void SetParameterBlockVariable(double* values) { setConstant(values, false); }
+  bool IsParameterBlockConstant(const double* values) const { return param(values, "IsParameterBlockConstant").constant; }
+
+  // Removes the block and every residual block that depends on it (Ceres semantics).
+  void RemoveParameterBlock(const double* values) {
+    Param& p = param(values, "RemoveParameterBlock");
+    std::vector<ResidualBlockId> deps(p.residuals.begin(), p.residuals.end());
+    for (ResidualBlockId r : deps) RemoveResidualBlock(r);
+    params_.erase(const_cast<double*>(values));
+    dirty_ = true;
+  }
+
+  // ---- residual blocks
+  ResidualBlockId AddResidualBlock(CostFunction* cost, LossFunction* loss, const std::vector<double*>& blocks) {
+    if (!cost) throw Error("AddResidualBlock: null cost function");
+    const std::string t = cost->typeInfo();
+    static const std::set<std::string> known = {"ReprojectionError", "ImuError", "PoseError", "SpeedAndBiasError",
+                                                "TwoPoseStandardGraphError", "TwoPoseStandardGraphErrorConst",
+                                                "RelativePoseError"};
+    if (!known.count(t)) throw Unsupported("cost function \"" + t + "\" has no GPU evaluation (keep the Ceres solve)");
+    if (loss && t != "ReprojectionError") throw Unsupported(t + " with a loss function (okvis adds none)");
+    const std::vector<int> sizes = cost->parameterBlockSizes();
+    if (sizes.size() != blocks.size()) throw Error("AddResidualBlock: " + t + " expects " + std::to_string(sizes.size()) + " blocks");
+    for (size_t k = 0; k < blocks.size(); ++k) {
+      auto it = params_.find(blocks[k]);
+      if (it == params_.end()) {
+        AddParameterBlock(blocks[k], sizes[k]);  // Ceres adds unknown blocks implicitly
+        it = params_.find(blocks[k]);
+      }
+      if (it->second.size != sizes[k]) throw Error("AddResidualBlock: block " + std::to_string(k) + " of " + t + " has size " +
+                                                   std::to_string(it->second.size));
+    }
+    auto rb = std::unique_ptr<ResidualBlock>(new ResidualBlock{cost, loss, blocks});
+    ResidualBlockId id = rb.get();
+    for (double* b : blocks) params_[b].residuals.insert(id);
+    residuals_.push_back(std::move(rb));
+    dirty_ = true;
+    return id;
+  }
+  template <class... Ts>
+  ResidualBlockId AddResidualBlock(CostFunction* cost, LossFunction* loss, double* x0, Ts*... xs) {
+    return AddResidualBlock(cost, loss, std::vector<double*>{x0, xs...});
+  }
+  void RemoveResidualBlock(ResidualBlockId id) {
+    auto it = std::find_if(residuals_.begin(), residuals_.end(), [&](const auto& r) { return r.get() == id; });
+    if (it == residuals_.end()) throw Error("RemoveResidualBlock: unknown residual block");
+    for (double* b : id->blocks) {
+      auto p = params_.find(b);
+      if (p != params_.end()) p->second.residuals.erase(id);
+    }
+    residuals_.erase(it);
+    dirty_ = true;
+  }
+  int NumResidualBlocks() const { return (int)residuals_.size(); }
+  void GetParameterBlocksForResidualBlock(const ResidualBlockId id, std::vector<double*>* out) const {
+    *out = find(id)->blocks;
+  }
+  void GetResidualBlocksForParameterBlock(const double* values, std::vector<ResidualBlockId>* out) const {
+    const Param& p = param(values, "GetResidualBlocksForParameterBlock");
+    out->clear();
+    for (const auto& r : residuals_)  // insertion order
+      if (p.residuals.count(r.get())) out->push_back(r.get());
+  }
+  const CostFunction* GetCostFunctionForResidualBlock(const ResidualBlockId id) const { return find(id)->cost; }
+  const LossFunction* GetLossFunctionForResidualBlock(const ResidualBlockId id) const { return find(id)->loss; }
+
+  // ---- solve: ::ceres::Solve(options, &problem, &summary) (ViGraph.cpp:1884)
+  int Solve(const okvisgpu_options& options, okvisgpu_summary* summary) {
+    int rc = ensureContext();
+    if (rc != OKVISGPU_OK) return rc;
+    if (dirty_ || !uploaded_) {
+      build();
+      rc = okvisgpu_set_problems(ctx_, &view_, 1);
+      if (rc != OKVISGPU_OK) return rc;
+      uploaded_ = true;
+      dirty_ = false;
+      constDirty_.clear();
+    } else {
+      gatherValues();
+      for (const auto& kv : constDirty_) {  // freeze / unfreeze without re-uploading the problem
+        rc = okvisgpu_set_block_constant(ctx_, 0, kv.first.first, kv.first.second, kv.second);
+        if (rc != OKVISGPU_OK) return rc;
+      }
+      constDirty_.clear();
+      rc = okvisgpu_update_params(ctx_);
+      if (rc != OKVISGPU_OK) return rc;
+    }
+    okvisgpu_summary s;
+    rc = okvisgpu_solve(ctx_, &options, &s);
+    if (rc != OKVISGPU_OK) return rc;
+    scatterValues();
+    if (summary) *summary = s;
+    return OKVISGPU_OK;
+  }
+
+  // Problem::Evaluate(total cost) at the caller's current parameter values.
+  int EvaluateCost(double* cost) {
+    int rc = ensureContext();
+    if (rc != OKVISGPU_OK) return rc;
+    build();
+    rc = okvisgpu_set_problems(ctx_, &view_, 1);
+    if (rc != OKVISGPU_OK) return rc;
+    uploaded_ = true;
+    dirty_ = false;
+    constDirty_.clear();
+    return okvisgpu_evaluate(ctx_, 0, cost);
+  }
+
+  const char* last_error() const { return ctx_ ? okvisgpu_last_error(ctx_) : okvisgpu_last_error(nullptr); }
+
+  // The C-ABI problem the facade hands to okvisgpu_set_problems (rebuilt from the recorded graph;
+  // pointers valid until the next structural change). Exposed for inspection and tests.
+  const okvisgpu_problem& view() {
+    if (dirty_ || !built_) build();
+    return view_;
+  }
+  // Block indices in the view (-1 if not a block of that kind).
+  int poseIndex(const double* v) const { return indexIn(poseIdx_, v); }
+  int speedBiasIndex(const double* v) const { return indexIn(sbIdx_, v); }
+  int landmarkIndex(const double* v) const { return indexIn(lmIdx_, v); }
+
+ private:
+  struct Param {
+    int size = 0;
+    Manifold* manifold = nullptr;
+    bool constant = false;
+    int64_t order = 0;
+    std::set<ResidualBlockId> residuals;
+  };
+  struct Cam {  // one ABI camera = (extrinsics block, intrinsics)
+    double* extr;
+    okvisgpu_camera cam;
+  };
+
+  static bool sameCamera(const okvisgpu_camera& a, const okvisgpu_camera& b) {
+    return a.distortion == b.distortion && a.width == b.width && a.height == b.height && a.fu == b.fu &&
+           a.fv == b.fv && a.cu == b.cu && a.cv == b.cv && std::memcmp(a.dist, b.dist, sizeof(a.dist)) == 0;
+  }
+  static void checkManifold(int size, const Manifold* m) {
+    if (m && m->AmbientSize() != size) throw Error(std::string(m->name()) + " on a block of size " + std::to_string(size));
+    if (size == 7 && m && std::strcmp(m->name(), "PoseManifold") != 0) throw Unsupported("7-dim block without PoseManifold");
+  }
+  Param& param(const double* v, const char* what) {
+    auto it = params_.find(const_cast<double*>(v));
+    if (it == params_.end()) throw Error(std::string(what) + ": unknown parameter block");
+    return it->second;
+  }
+  const Param& param(const double* v, const char* what) const {
+    auto it = params_.find(const_cast<double*>(v));
+    if (it == params_.end()) throw Error(std::string(what) + ": unknown parameter block");
+    return it->second;
+  }
+  const ResidualBlock* find(ResidualBlockId id) const {
+    for (const auto& r : residuals_)
+      if (r.get() == id) return id;
+    throw Error("unknown residual block");
+  }
+  static int indexIn(const std::map<double*, int>& m, const double* v) {
+    auto it = m.find(const_cast<double*>(v));
+    return it == m.end() ? -1 : it->second;
+  }
+  void setConstant(const double* values, bool c) {
+    Param& p = param(values, c ? "SetParameterBlockConstant" : "SetParameterBlockVariable");
+    if (p.constant == c) return;
+    p.constant = c;
+    double* v = const_cast<double*>(values);
+    int kind = -1, index = -1;
+    if ((index = indexIn(poseIdx_, v)) >= 0) kind = 0;
+    else if ((index = indexIn(sbIdx_, v)) >= 0) kind = 1;
+    else if ((index = indexIn(lmIdx_, v)) >= 0) kind = 2;
+    if (kind < 0 || dirty_ || !uploaded_) dirty_ = true;  // structure rebuilt at the next Solve anyway
+    else constDirty_[{kind, index}] = c ? 1 : 0;
+  }
+  int ensureContext() {
+    if (ctx_) return OKVISGPU_OK;
+    return okvisgpu_ctx_create(device_, &ctx_);
+  }
+
+  // Flatten the recorded graph into the SoA arrays of okvisgpu_problem. Blocks are ordered by
+  // insertion; a 7-dim block is an extrinsics block if it is the third block of a reprojection
+  // error, a pose otherwise.
+  void build() {
+    std::vector<std::pair<int64_t, double*>> order;
+    for (auto& kv : params_) order.push_back({kv.second.order, kv.first});
+    std::sort(order.begin(), order.end());
+    std::set<double*> extrBlocks;
+    for (const auto& r : residuals_)
+      if (r->cost->typeInfo() == "ReprojectionError") extrBlocks.insert(r->blocks[2]);
+    poseIdx_.clear(); sbIdx_.clear(); lmIdx_.clear();
+    posePtr_.clear(); sbPtr_.clear(); lmPtr_.clear();
+    for (auto& o : order) {
+      const Param& p = params_[o.second];
+      if (p.size == 7 && !extrBlocks.count(o.second)) { poseIdx_[o.second] = (int)posePtr_.size(); posePtr_.push_back(o.second); }
+      else if (p.size == 9) { sbIdx_[o.second] = (int)sbPtr_.size(); sbPtr_.push_back(o.second); }
+      else if (p.size == 4) { lmIdx_[o.second] = (int)lmPtr_.size(); lmPtr_.push_back(o.second); }
+    }
+    A_ = Arrays();
+    for (double* b : posePtr_) A_.pose_c.push_back(params_[b].constant);
+    for (double* b : sbPtr_) A_.sb_c.push_back(params_[b].constant);
+    for (double* b : lmPtr_) A_.lm_c.push_back(params_[b].constant);
+    std::vector<Cam> cams;
+    auto camIndex = [&](double* extr, const okvisgpu_camera& c) {
+      for (size_t i = 0; i < cams.size(); ++i)
+        if (cams[i].extr == extr && sameCamera(cams[i].cam, c)) return (int)i;
+      cams.push_back(Cam{extr, c});
+      return (int)cams.size() - 1;
+    };
+    auto pidx = [&](double* b, const char* what) {
+      const int i = indexIn(poseIdx_, b);
+      if (i < 0) throw Error(std::string(what) + ": block is not a pose");
+      return i;
+    };
+    auto sidx = [&](double* b) {
+      const int i = indexIn(sbIdx_, b);
+      if (i < 0) throw Error("ImuError: block is not a speed/bias block");
+      return i;
+    };
+    A_.imu_begin.push_back(0);
+    imuTerms_.clear();
+    for (const auto& r : residuals_) {
+      const std::string t = r->cost->typeInfo();
+      if (t == "ReprojectionError") {
+        const auto* e = static_cast<const ReprojectionError*>(r->cost);
+        A_.obs_pose.push_back(pidx(r->blocks[0], "ReprojectionError"));
+        const int l = indexIn(lmIdx_, r->blocks[1]);
+        if (l < 0) throw Error("ReprojectionError: block 1 is not a landmark");
+        A_.obs_lm.push_back(l);
+        A_.obs_cam.push_back(camIndex(r->blocks[2], e->camera));
+        A_.obs_kp.insert(A_.obs_kp.end(), e->keypoint, e->keypoint + 2);
+        A_.obs_L.insert(A_.obs_L.end(), e->sqrt_info, e->sqrt_info + 4);
+        A_.obs_cauchy.push_back(r->loss != nullptr);
+      } else if (t == "ImuError") {
+        auto* e = static_cast<ImuError*>(r->cost);
+        const int32_t b[4] = {pidx(r->blocks[0], "ImuError"), sidx(r->blocks[1]), pidx(r->blocks[2], "ImuError"),
+                              sidx(r->blocks[3])};
+        A_.imu_blocks.insert(A_.imu_blocks.end(), b, b + 4);
+        A_.imu_t0.push_back(e->t0_ns);
+        A_.imu_t1.push_back(e->t1_ns);
+        A_.imu_ts.insert(A_.imu_ts.end(), e->sample_t_ns.begin(), e->sample_t_ns.end());
+        A_.imu_ga.insert(A_.imu_ga.end(), e->gyr_acc.begin(), e->gyr_acc.end());
+        A_.imu_begin.push_back((int32_t)A_.imu_ts.size());
+        A_.imu_state.insert(A_.imu_state.end(), e->state.begin(), e->state.end());
+        if (imuTerms_.empty()) A_.imu_params = e->params;
+        else if (std::memcmp(&A_.imu_params, &e->params, sizeof(e->params)) != 0)
+          throw Unsupported("ImuError terms with different ImuParameters in one graph");
+        imuTerms_.push_back(e);
+      } else if (t == "PoseError") {
+        const auto* e = static_cast<const PoseError*>(r->cost);
+        if (extrBlocks.count(r->blocks[0])) {
+          A_.ep_cam_ptr.push_back(r->blocks[0]);
+          A_.ep_meas.insert(A_.ep_meas.end(), e->meas, e->meas + 7);
+          A_.ep_L.insert(A_.ep_L.end(), e->sqrt_info, e->sqrt_info + 36);
+        } else {
+          A_.pp_block.push_back(pidx(r->blocks[0], "PoseError"));
+          A_.pp_meas.insert(A_.pp_meas.end(), e->meas, e->meas + 7);
+          A_.pp_L.insert(A_.pp_L.end(), e->sqrt_info, e->sqrt_info + 36);
+        }
+      } else if (t == "SpeedAndBiasError") {
+        const auto* e = static_cast<const SpeedAndBiasError*>(r->cost);
+        A_.sbp_block.push_back(sidx(r->blocks[0]));
+        A_.sbp_meas.insert(A_.sbp_meas.end(), e->meas, e->meas + 9);
+        A_.sbp_L.insert(A_.sbp_L.end(), e->sqrt_info, e->sqrt_info + 81);
+      } else if (t == "TwoPoseStandardGraphError" || t == "TwoPoseStandardGraphErrorConst") {
+        const auto* e = static_cast<const TwoPoseGraphError*>(r->cost);
+        A_.rp_blocks.push_back(pidx(r->blocks[0], t.c_str()));
+        A_.rp_blocks.push_back(pidx(r->blocks[1], t.c_str()));
+        A_.rp_dx.insert(A_.rp_dx.end(), e->delta_x, e->delta_x + 6);
+        A_.rp_J.insert(A_.rp_J.end(), e->J, e->J + 36);
+        A_.rp_lp.insert(A_.rp_lp.end(), e->lin_point, e->lin_point + 7);
+        A_.rp_kind.push_back(0);
+      } else if (t == "RelativePoseError") {
+        const auto* e = static_cast<const RelativePoseError*>(r->cost);
+        A_.rp_blocks.push_back(pidx(r->blocks[0], t.c_str()));
+        A_.rp_blocks.push_back(pidx(r->blocks[1], t.c_str()));
+        A_.rp_dx.insert(A_.rp_dx.end(), 6, 0.0);
+        A_.rp_J.insert(A_.rp_J.end(), e->sqrt_info, e->sqrt_info + 36);
+        A_.rp_lp.insert(A_.rp_lp.end(), e->T_AB, e->T_AB + 7);
+        A_.rp_kind.push_back(1);
+      }
+    }
+    // cameras / extrinsics (one ABI camera per distinct (extrinsics block, intrinsics) pair)
+    extrPtr_.clear();
+    for (const Cam& c : cams) {
+      A_.cams.push_back(c.cam);
+      A_.extr.insert(A_.extr.end(), c.extr, c.extr + 7);
+      A_.extr_c.push_back(params_[c.extr].constant);
+      extrPtr_.push_back(c.extr);
+    }
+    for (double* e : A_.ep_cam_ptr) {
+      int ci = -1;
+      for (size_t i = 0; i < extrPtr_.size(); ++i)
+        if (extrPtr_[i] == e) { ci = (int)i; break; }
+      A_.ep_cam.push_back(ci);
+    }
+    gatherValues();
+    okvisgpu_problem& P = view_;
+    std::memset(&P, 0, sizeof(P));
+    P.n_poses = (int32_t)posePtr_.size();
+    P.poses = A_.pose.data();
+    P.pose_constant = A_.pose_c.data();
+    P.n_speed_biases = (int32_t)sbPtr_.size();
+    P.speed_biases = A_.sb.data();
+    P.speed_bias_constant = A_.sb_c.data();
+    P.n_landmarks = (int32_t)lmPtr_.size();
+    P.landmarks = A_.lm.data();
+    P.landmark_constant = A_.lm_c.data();
+    P.n_cameras = (int32_t)A_.cams.size();
+    P.cameras = A_.cams.data();
+    P.extrinsics = A_.extr.data();
+    P.extrinsics_constant = A_.extr_c.data();
+    P.n_observations = (int32_t)A_.obs_pose.size();
+    P.obs_pose = A_.obs_pose.data();
+    P.obs_landmark = A_.obs_lm.data();
+    P.obs_camera = A_.obs_cam.data();
+    P.obs_keypoint = A_.obs_kp.data();
+    P.obs_sqrt_info = A_.obs_L.data();
+    P.obs_cauchy = A_.obs_cauchy.data();
+    P.n_imu = (int32_t)imuTerms_.size();
+    P.imu_blocks = A_.imu_blocks.data();
+    P.imu_t0_ns = A_.imu_t0.data();
+    P.imu_t1_ns = A_.imu_t1.data();
+    P.imu_sample_begin = A_.imu_begin.data();
+    P.imu_sample_t_ns = A_.imu_ts.data();
+    P.imu_sample_gyr_acc = A_.imu_ga.data();
+    P.imu_params = A_.imu_params;
+    P.imu_state = A_.imu_state.data();
+    P.n_pose_priors = (int32_t)A_.pp_block.size();
+    P.pose_prior_block = A_.pp_block.data();
+    P.pose_prior_meas = A_.pp_meas.data();
+    P.pose_prior_sqrt_info = A_.pp_L.data();
+    P.n_sb_priors = (int32_t)A_.sbp_block.size();
+    P.sb_prior_block = A_.sbp_block.data();
+    P.sb_prior_meas = A_.sbp_meas.data();
+    P.sb_prior_sqrt_info = A_.sbp_L.data();
+    P.n_relpose = (int32_t)A_.rp_kind.size();
+    P.relpose_blocks = A_.rp_blocks.data();
+    P.relpose_delta_x = A_.rp_dx.data();
+    P.relpose_sqrt_info = A_.rp_J.data();
+    P.relpose_lin_point = A_.rp_lp.data();
+    P.relpose_kind = A_.rp_kind.data();
+    P.n_extrinsics_priors = (int32_t)A_.ep_cam.size();
+    P.extrinsics_prior_camera = A_.ep_cam.data();
+    P.extrinsics_prior_meas = A_.ep_meas.data();
+    P.extrinsics_prior_sqrt_info = A_.ep_L.data();
+    built_ = true;
+  }
+  // caller's parameter memory -> SoA (before a solve)
+  void gatherValues() {
+    A_.pose.resize(7 * posePtr_.size());
+    A_.sb.resize(9 * sbPtr_.size());
+    A_.lm.resize(4 * lmPtr_.size());
+    for (size_t i = 0; i < posePtr_.size(); ++i) std::memcpy(&A_.pose[7 * i], posePtr_[i], 7 * sizeof(double));
+    for (size_t i = 0; i < sbPtr_.size(); ++i) std::memcpy(&A_.sb[9 * i], sbPtr_[i], 9 * sizeof(double));
+    for (size_t i = 0; i < lmPtr_.size(); ++i) std::memcpy(&A_.lm[4 * i], lmPtr_[i], 4 * sizeof(double));
+    for (size_t i = 0; i < extrPtr_.size() && 7 * i < A_.extr.size(); ++i)
+      std::memcpy(&A_.extr[7 * i], extrPtr_[i], 7 * sizeof(double));
+    for (size_t f = 0; f < imuTerms_.size(); ++f)
+      std::memcpy(&A_.imu_state[f * OKVISGPU_IMU_STATE_DOUBLES], imuTerms_[f]->state.data(),
+                  OKVISGPU_IMU_STATE_DOUBLES * sizeof(double));
+  }
+  // SoA -> caller's parameter memory (after a solve): the in-place write-back of Ceres
+  void scatterValues() {
+    for (size_t i = 0; i < posePtr_.size(); ++i) std::memcpy(posePtr_[i], &A_.pose[7 * i], 7 * sizeof(double));
+    for (size_t i = 0; i < sbPtr_.size(); ++i) std::memcpy(sbPtr_[i], &A_.sb[9 * i], 9 * sizeof(double));
+    for (size_t i = 0; i < lmPtr_.size(); ++i) std::memcpy(lmPtr_[i], &A_.lm[4 * i], 4 * sizeof(double));
+    for (size_t i = 0; i < extrPtr_.size(); ++i) std::memcpy(extrPtr_[i], &A_.extr[7 * i], 7 * sizeof(double));
+    for (size_t f = 0; f < imuTerms_.size(); ++f)
+      std::memcpy(imuTerms_[f]->state.data(), &A_.imu_state[f * OKVISGPU_IMU_STATE_DOUBLES],
+                  OKVISGPU_IMU_STATE_DOUBLES * sizeof(double));
+  }
+
+  struct Arrays {
+    std::vector<double> pose, sb, lm, extr, obs_kp, obs_L, imu_ga, imu_state, pp_meas, pp_L, sbp_meas, sbp_L, rp_dx,
+        rp_J, rp_lp, ep_meas, ep_L;
+    std::vector<uint8_t> pose_c, sb_c, lm_c, extr_c, obs_cauchy, rp_kind;
+    std::vector<int32_t> obs_pose, obs_lm, obs_cam, imu_blocks, imu_begin, pp_block, sbp_block, rp_blocks, ep_cam;
+    std::vector<int64_t> imu_t0, imu_t1, imu_ts;
+    std::vector<okvisgpu_camera> cams;
+    std::vector<double*> ep_cam_ptr;
+    okvisgpu_imu_params imu_params{};
+  };
+
+  int device_;
+  okvisgpu_ctx* ctx_ = nullptr;
+  std::map<double*, Param> params_;
+  std::vector<std::unique_ptr<ResidualBlock>> residuals_;
+  int64_t nextOrder_ = 0;
+  bool dirty_ = true, uploaded_ = false, built_ = false;
+  std::map<std::pair<int, int>, int> constDirty_;
+  std::map<double*, int> poseIdx_, sbIdx_, lmIdx_;
+  std::vector<double*> posePtr_, sbPtr_, lmPtr_, extrPtr_;
+  std::vector<ImuError*> imuTerms_;
+  Arrays A_;
+  okvisgpu_problem view_{};
+};
+
+}  // namespace okvisgpu

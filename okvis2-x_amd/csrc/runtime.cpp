@@ -47,6 +47,9 @@ struct HipError {
 struct ArgError {
   std::string msg;
 };
+struct UnsupportedError {
+  std::string msg;
+};
 
 double nowS() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -131,6 +134,11 @@ void validate(const okvisgpu_problem* p, int w) {
   }
   for (int c = 0; c < p->n_cameras; ++c)
     if (p->cameras[c].distortion < 0 || p->cameras[c].distortion > 3) bad("unknown distortion model");
+  if (p->extrinsics_constant)
+    for (int c = 0; c < p->n_cameras; ++c)
+      if (!p->extrinsics_constant[c]) throw UnsupportedError{"window " + std::to_string(w) +
+                                                              ": variable extrinsics are not supported yet"};
+  if (p->n_extrinsics_priors < 0) bad("negative count");
   if (p->n_imu) {
     if (!p->imu_blocks || !p->imu_t0_ns || !p->imu_t1_ns || !p->imu_sample_begin || !p->imu_sample_t_ns ||
         !p->imu_sample_gyr_acc)
@@ -1088,6 +1096,8 @@ int guarded(okvisgpu_ctx* c, F f) {
     return fail(c, e.code, e.msg);
   } catch (const ArgError& e) {
     return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, e.msg);
+  } catch (const UnsupportedError& e) {
+    return fail(c, OKVISGPU_ERR_UNSUPPORTED, e.msg);
   } catch (const std::bad_alloc&) {
     return fail(c, OKVISGPU_ERR_OUT_OF_MEMORY, "host allocation failed");
   } catch (const std::exception& e) {
@@ -1219,8 +1229,12 @@ int okvisgpu_get_params(okvisgpu_ctx* c) {
 static int checkSolveOptions(okvisgpu_ctx* c, const okvisgpu_options* o) {
   if (!c || !o) return OKVISGPU_ERR_INVALID_ARGUMENT;
   if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
-  if (o->linear_solver != OKVISGPU_DENSE_SCHUR || o->trust_region_strategy != OKVISGPU_DOGLEG)
-    return fail(c, OKVISGPU_ERR_UNSUPPORTED, "only DENSE_SCHUR + DOGLEG is implemented on the GPU path");
+  // SPARSE_NORMAL_CHOLESKY (the full graph's option, ViGraph.cpp:248) solves the same normal
+  // equations; the step is formed through the exact tile-sparse Schur complement either way
+  if ((o->linear_solver != OKVISGPU_DENSE_SCHUR && o->linear_solver != OKVISGPU_SPARSE_NORMAL_CHOLESKY) ||
+      o->trust_region_strategy != OKVISGPU_DOGLEG)
+    return fail(c, OKVISGPU_ERR_UNSUPPORTED,
+                "linear solver must be DENSE_SCHUR or SPARSE_NORMAL_CHOLESKY and the strategy DOGLEG");
   if (o->max_num_iterations < 0) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "max_num_iterations < 0");
   return OKVISGPU_OK;
 }

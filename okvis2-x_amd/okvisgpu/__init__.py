@@ -21,6 +21,7 @@ LIB_PATH = os.environ.get("OKVISGPU_LIB") or os.path.join(PKG_ROOT, "libokvisgpu
 IMU_STATE_DOUBLES = 292
 
 DIST_NONE, DIST_RADTAN, DIST_EQUIDISTANT, DIST_RADTAN8 = 0, 1, 2, 3
+DENSE_SCHUR, SPARSE_NORMAL_CHOLESKY = 0, 1
 TERMINATION = {0: "CONVERGENCE", 1: "NO_CONVERGENCE", 2: "FAILURE", 3: "USER_SUCCESS"}
 
 _dp = C.POINTER(C.c_double)
@@ -58,6 +59,8 @@ class Problem(C.Structure):
         ("sb_prior_sqrt_info", _dp),
         ("n_relpose", C.c_int32), ("relpose_blocks", _ip), ("relpose_delta_x", _dp),
         ("relpose_sqrt_info", _dp), ("relpose_lin_point", _dp), ("relpose_kind", _up),
+        ("extrinsics_constant", _up), ("n_extrinsics_priors", C.c_int32), ("extrinsics_prior_camera", _ip),
+        ("extrinsics_prior_meas", _dp), ("extrinsics_prior_sqrt_info", _dp),
     ]
 
 

@@ -1,0 +1,330 @@
+// C++ consumer of the okvisgpu::Problem facade (include/okvisgpu_problem.hpp), compiled with g++
+// only. It drives the facade the way okvis drives ::ceres::Problem (ViGraph.cpp:327-385,433-459,
+// 597-637; ViGraphEstimator.cpp:216-331): parameter blocks with manifolds, typeInfo()-recognised
+// residual blocks, freeze / unfreeze, removal, ::ceres::Solve.
+//   facade_test cpu  bookkeeping, graph flattening and error paths (no GPU needed)
+//   facade_test gpu  the TestReprojectionError.cpp:48-164 scene through the facade (its thresholds),
+//                    and an S10 window through the facade vs the same window through the C ABI
+//                    directly (also after a freeze between solves)
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <memory>
+#include <cstdio>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "okvisgpu.h"
+#include "okvisgpu_problem.hpp"
+
+static int g_fail = 0;
+#define CHECK(c)                                                           \
+  do {                                                                     \
+    if (!(c)) {                                                            \
+      std::fprintf(stderr, "%s:%d CHECK failed: %s\n", __FILE__, __LINE__, #c); \
+      ++g_fail;                                                            \
+    }                                                                      \
+  } while (0)
+
+namespace {
+
+struct Quat { double x, y, z, w; };
+Quat qmul(Quat a, Quat b) {
+  return {a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y, a.w * b.y - a.x * b.z + a.y * b.w + a.z * b.x,
+          a.w * b.z + a.x * b.y - a.y * b.x + a.z * b.w, a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z};
+}
+void rot(Quat q, double R[9]) {
+  const double n = std::sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+  const double x = q.x / n, y = q.y / n, z = q.z / n, w = q.w / n;
+  const double r[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w),
+                       2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
+                       2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)};
+  for (int i = 0; i < 9; ++i) R[i] = r[i];
+}
+struct Pose { double t[3]; Quat q; };
+// Transformation::setRandom (Transformation.hpp:199-208), Random() uniform in [-1, 1]
+Pose setRandom(std::mt19937_64& g, double tmax, double rmax) {
+  std::uniform_real_distribution<double> U(-1.0, 1.0);
+  double a[3] = {rmax * U(g), rmax * U(g), rmax * U(g)};
+  Pose p;
+  for (double& v : p.t) v = tmax * U(g);
+  const double ang = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+  const double s = std::sin(ang / 2) / ang;
+  p.q = {a[0] * s, a[1] * s, a[2] * s, std::cos(ang / 2)};
+  return p;
+}
+Pose compose(const Pose& A, const Pose& B) {
+  double R[9];
+  rot(A.q, R);
+  Pose o;
+  for (int i = 0; i < 3; ++i) o.t[i] = A.t[i] + R[3 * i] * B.t[0] + R[3 * i + 1] * B.t[1] + R[3 * i + 2] * B.t[2];
+  o.q = qmul(A.q, B.q);
+  return o;
+}
+void toArray(const Pose& p, double* a) {
+  a[0] = p.t[0]; a[1] = p.t[1]; a[2] = p.t[2]; a[3] = p.q.x; a[4] = p.q.y; a[5] = p.q.z; a[6] = p.q.w;
+}
+double rotErr(Quat a, Quat b) {  // 2 |vec(a b^-1)|
+  const Quat d = qmul(a, Quat{-b.x, -b.y, -b.z, b.w});
+  return 2 * std::sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
+}
+
+okvisgpu_options zeroTol(int iters) {
+  okvisgpu_options o;
+  okvisgpu_default_options(&o);
+  o.max_num_iterations = iters;
+  o.function_tolerance = o.gradient_tolerance = o.parameter_tolerance = 0.0;
+  return o;
+}
+
+// a cost function the GPU path does not know (GPS / SubmapICP stand-in)
+struct OtherError final : okvisgpu::CostFunction {
+  std::string typeInfo() const override { return "GpsErrorSynchronous"; }
+  int residualDim() const override { return 3; }
+  std::vector<int> parameterBlockSizes() const override { return {7}; }
+};
+
+// Records an okvisgpu_problem (e.g. a synthetic window) into a facade, block by block and residual
+// by residual, the way ViGraph adds them; parameter memory = the problem's own arrays.
+struct Recorded {
+  okvisgpu::PoseManifold poseManifold;
+  okvisgpu::HomogeneousPointManifold pointManifold;
+  okvisgpu::CauchyLoss cauchy{1.0};
+  std::vector<std::unique_ptr<okvisgpu::CostFunction>> costs;
+};
+
+void record(okvisgpu::Problem& P, const okvisgpu_problem* p, Recorded& R) {
+  for (int i = 0; i < p->n_poses; ++i) {
+    P.AddParameterBlock(&p->poses[7 * i], 7, &R.poseManifold);
+    if (p->pose_constant && p->pose_constant[i]) P.SetParameterBlockConstant(&p->poses[7 * i]);
+  }
+  for (int i = 0; i < p->n_speed_biases; ++i) {
+    P.AddParameterBlock(&p->speed_biases[9 * i], 9);
+    if (p->speed_bias_constant && p->speed_bias_constant[i]) P.SetParameterBlockConstant(&p->speed_biases[9 * i]);
+  }
+  for (int c = 0; c < p->n_cameras; ++c) {
+    P.AddParameterBlock(&p->extrinsics[7 * c], 7, &R.poseManifold);
+    P.SetParameterBlockConstant(&p->extrinsics[7 * c]);  // do_extrinsics: false (ViGraph.cpp:385)
+  }
+  for (int l = 0; l < p->n_landmarks; ++l) {
+    P.AddParameterBlock(&p->landmarks[4 * l], 4, &R.pointManifold);
+    if (p->landmark_constant && p->landmark_constant[l]) P.SetParameterBlockConstant(&p->landmarks[4 * l]);
+  }
+  for (int o = 0; o < p->n_observations; ++o) {
+    const int c = p->obs_camera[o];
+    R.costs.emplace_back(new okvisgpu::ReprojectionError(p->cameras[c], &p->obs_keypoint[2 * o], &p->obs_sqrt_info[4 * o]));
+    P.AddResidualBlock(R.costs.back().get(), (!p->obs_cauchy || p->obs_cauchy[o]) ? &R.cauchy : nullptr,
+                       &p->poses[7 * p->obs_pose[o]], &p->landmarks[4 * p->obs_landmark[o]], &p->extrinsics[7 * c]);
+  }
+  for (int f = 0; f < p->n_imu; ++f) {
+    const int s0 = p->imu_sample_begin[f], s1 = p->imu_sample_begin[f + 1];
+    std::vector<int64_t> ts(p->imu_sample_t_ns + s0, p->imu_sample_t_ns + s1);
+    std::vector<double> ga(p->imu_sample_gyr_acc + 6 * s0, p->imu_sample_gyr_acc + 6 * s1);
+    auto* e = new okvisgpu::ImuError(ts, ga, p->imu_params, p->imu_t0_ns[f], p->imu_t1_ns[f]);
+    R.costs.emplace_back(e);
+    const int* b = &p->imu_blocks[4 * f];
+    P.AddResidualBlock(e, nullptr, &p->poses[7 * b[0]], &p->speed_biases[9 * b[1]], &p->poses[7 * b[2]],
+                       &p->speed_biases[9 * b[3]]);
+  }
+  for (int i = 0; i < p->n_pose_priors; ++i) {
+    R.costs.emplace_back(new okvisgpu::PoseError(&p->pose_prior_meas[7 * i], &p->pose_prior_sqrt_info[36 * i]));
+    P.AddResidualBlock(R.costs.back().get(), nullptr, &p->poses[7 * p->pose_prior_block[i]]);
+  }
+  for (int i = 0; i < p->n_sb_priors; ++i) {
+    R.costs.emplace_back(new okvisgpu::SpeedAndBiasError(&p->sb_prior_meas[9 * i], &p->sb_prior_sqrt_info[81 * i]));
+    P.AddResidualBlock(R.costs.back().get(), nullptr, &p->speed_biases[9 * p->sb_prior_block[i]]);
+  }
+}
+
+int cpuTests() {
+  okvisgpu::Problem P;
+  okvisgpu::PoseManifold pm;
+  okvisgpu::HomogeneousPointManifold hm;
+  okvisgpu::CauchyLoss cauchy(1.0);
+  double T0[7] = {0, 0, 0, 0, 0, 0, 1}, T1[7] = {1, 0, 0, 0, 0, 0, 1}, Tsc[7] = {0, 0, 0, 0, 0, 0, 1};
+  double sb0[9] = {0}, sb1[9] = {0};
+  double L0[4] = {0, 0, 5, 1}, L1[4] = {1, 1, 6, 1};
+  P.AddParameterBlock(T0, 7, &pm);
+  P.AddParameterBlock(sb0, 9);
+  P.AddParameterBlock(T1, 7, &pm);
+  P.AddParameterBlock(sb1, 9);
+  P.AddParameterBlock(Tsc, 7, &pm);
+  P.SetParameterBlockConstant(Tsc);
+  P.AddParameterBlock(L0, 4, &hm);
+  P.AddParameterBlock(L1, 4, &hm);
+  P.AddParameterBlock(L1, 4);  // re-adding is a no-op (Ceres)
+  CHECK(P.NumParameterBlocks() == 7);
+  CHECK(P.HasParameterBlock(T0) && !P.HasParameterBlock(T0 + 1));
+  CHECK(P.IsParameterBlockConstant(Tsc) && !P.IsParameterBlockConstant(T1));
+  CHECK(P.GetManifold(L0) == &hm && P.GetManifold(sb0) == nullptr);
+  okvisgpu_camera cam{};
+  cam.distortion = OKVISGPU_DIST_NONE;
+  cam.width = 752; cam.height = 480; cam.fu = 350; cam.fv = 360; cam.cu = 378; cam.cv = 238;
+  const double kp[2] = {378, 238}, Li[4] = {1, 0, 0, 1};
+  okvisgpu::ReprojectionError e00(cam, kp, Li), e01(cam, kp, Li), e10(cam, kp, Li);
+  auto r00 = P.AddResidualBlock(&e00, &cauchy, T0, L0, Tsc);
+  auto r01 = P.AddResidualBlock(&e01, &cauchy, T0, L1, Tsc);
+  auto r10 = P.AddResidualBlock(&e10, &cauchy, T1, L0, Tsc);
+  std::vector<int64_t> ts = {0, 5000000, 10000000};
+  std::vector<double> ga(18, 0.0);
+  okvisgpu_imu_params ip{};
+  okvisgpu::ImuError imu(ts, ga, ip, 1000000, 9000000);
+  auto rimu = P.AddResidualBlock(&imu, nullptr, T0, sb0, T1, sb1);
+  const double pm7[7] = {0, 0, 0, 0, 0, 0, 1}, pL[36] = {0};
+  okvisgpu::PoseError prior(pm7, pL), extrPrior(pm7, pL);
+  P.AddResidualBlock(&prior, nullptr, T0);
+  P.AddResidualBlock(&extrPrior, nullptr, Tsc);
+  CHECK(P.NumResidualBlocks() == 6);
+  std::vector<double*> blocks;
+  P.GetParameterBlocksForResidualBlock(rimu, &blocks);
+  CHECK(blocks.size() == 4 && blocks[0] == T0 && blocks[3] == sb1);
+  std::vector<okvisgpu::ResidualBlockId> rs;
+  P.GetResidualBlocksForParameterBlock(L0, &rs);
+  CHECK(rs.size() == 2 && rs[0] == r00 && rs[1] == r10);
+  CHECK(P.GetCostFunctionForResidualBlock(r01) == &e01 && P.GetLossFunctionForResidualBlock(rimu) == nullptr);
+  // the flattened C-ABI problem: Tsc is an extrinsics block (third block of a reprojection), not a pose
+  const okvisgpu_problem& v = P.view();
+  CHECK(v.n_poses == 2 && v.n_speed_biases == 2 && v.n_landmarks == 2 && v.n_cameras == 1);
+  CHECK(v.n_observations == 3 && v.n_imu == 1 && v.n_pose_priors == 1 && v.n_extrinsics_priors == 1);
+  CHECK(v.obs_pose[2] == 1 && v.obs_landmark[1] == 1 && v.obs_cauchy[0] == 1 && v.extrinsics_constant[0] == 1);
+  CHECK(v.imu_blocks[0] == 0 && v.imu_blocks[1] == 0 && v.imu_blocks[2] == 1 && v.imu_blocks[3] == 1);
+  CHECK(v.imu_sample_begin[1] == 3 && v.imu_t1_ns[0] == 9000000);
+  // removal (RemoveParameterBlock drops its residual blocks too)
+  P.RemoveResidualBlock(r01);
+  CHECK(P.NumResidualBlocks() == 5);
+  P.RemoveParameterBlock(L0);
+  CHECK(P.NumResidualBlocks() == 3 && !P.HasParameterBlock(L0));
+  CHECK(P.view().n_observations == 0 && P.view().n_landmarks == 1);
+  // unknown functor -> Unsupported (OKVISGPU_ERR_UNSUPPORTED); wrong block -> Error
+  OtherError gps;
+  bool threw = false;
+  try { P.AddResidualBlock(&gps, nullptr, T0); } catch (const okvisgpu::Unsupported& u) { threw = u.status() == OKVISGPU_ERR_UNSUPPORTED; }
+  CHECK(threw);
+  threw = false;
+  try { P.AddResidualBlock(&prior, nullptr, sb0); } catch (const okvisgpu::Error&) { threw = true; }
+  CHECK(threw);
+  threw = false;
+  try { okvisgpu::CauchyLoss c2(2.0); (void)c2; } catch (const okvisgpu::Unsupported&) { threw = true; }
+  CHECK(threw);
+  // no device in this container: Solve reports the C ABI's status instead of crashing
+  int32_t ndev = 0;
+  okvisgpu_device_count(&ndev);
+  if (ndev == 0) {
+    okvisgpu_summary s;
+    CHECK(P.Solve(zeroTol(2), &s) == OKVISGPU_ERR_DEVICE);
+  }
+  std::printf("facade_test cpu %s\n", g_fail ? "FAILED" : "ok");
+  return g_fail ? 1 : 0;
+}
+
+// TestReprojectionError.cpp:48-164 through the facade
+int reprojectionScene(uint64_t seed) {
+  std::mt19937_64 g(seed);
+  std::uniform_real_distribution<double> U(-1.0, 1.0);
+  const Pose T_WS = setRandom(g, 10.0, M_PI);
+  const Pose T_dist = setRandom(g, 1.0, 0.01);
+  const Pose T_SC = setRandom(g, 0.2, M_PI);
+  double pose[7], extr[7];
+  toArray(compose(T_WS, T_dist), pose);
+  toArray(T_SC, extr);
+  okvisgpu::Problem P;
+  okvisgpu::PoseManifold pm;
+  okvisgpu::HomogeneousPointManifold hm;
+  P.AddParameterBlock(pose, 7, &pm);
+  P.AddParameterBlock(extr, 7, &pm);
+  P.SetParameterBlockVariable(pose);
+  P.SetParameterBlockConstant(extr);
+  okvisgpu_camera cam{};
+  cam.distortion = OKVISGPU_DIST_NONE;
+  cam.width = 752; cam.height = 480; cam.fu = 350; cam.fv = 360; cam.cu = 378; cam.cv = 238;
+  const Pose T_WC = compose(T_WS, T_SC);
+  double R[9];
+  rot(T_WC.q, R);
+  std::vector<std::array<double, 4>> lms(99);
+  std::vector<std::unique_ptr<okvisgpu::ReprojectionError>> errs;
+  const double Li[4] = {1, 0, 0, 1};
+  for (int i = 1; i < 100; ++i) {
+    const double minD = (i % 10) * 3 + 2.0, maxD = 10.0;
+    const double u = (U(g) + 1) * 0.5 * (752 - 0.022) + 0.011, v = (U(g) + 1) * 0.5 * (480 - 0.022) + 0.011;
+    const double d = U(g);
+    double ray[3] = {(u - 378) / 350, (v - 238) / 360, 1.0};
+    const double n = std::sqrt(ray[0] * ray[0] + ray[1] * ray[1] + 1.0), depth = 0.5 * (maxD - minD) * (d + 1) + minD;
+    for (double& x : ray) x *= depth / n;
+    auto& L = lms[i - 1];
+    for (int r = 0; r < 3; ++r) L[r] = T_WC.t[r] + R[3 * r] * ray[0] + R[3 * r + 1] * ray[1] + R[3 * r + 2] * ray[2];
+    L[3] = 1.0;
+    P.AddParameterBlock(L.data(), 4, &hm);
+    P.SetParameterBlockConstant(L.data());
+    const double kp[2] = {350 * ray[0] / ray[2] + 378 + U(g), 360 * ray[1] / ray[2] + 238 + U(g)};
+    errs.emplace_back(new okvisgpu::ReprojectionError(cam, kp, Li));
+    P.AddResidualBlock(errs.back().get(), nullptr, pose, L.data(), extr);
+  }
+  okvisgpu_options o;
+  okvisgpu_default_options(&o);
+  okvisgpu_summary s;
+  const int rc = P.Solve(o, &s);
+  CHECK(rc == OKVISGPU_OK);
+  const double dt = std::sqrt(std::pow(pose[0] - T_WS.t[0], 2) + std::pow(pose[1] - T_WS.t[1], 2) +
+                              std::pow(pose[2] - T_WS.t[2], 2));
+  const double dr = rotErr(T_WS.q, Quat{pose[3], pose[4], pose[5], pose[6]});
+  CHECK(dr < 1e-2);  // TestReprojectionError.cpp:158-160
+  CHECK(dt < 1e-1);  // :161-163
+  std::printf("reprojection scene %llu: rc %d, %d iterations, termination %d, rot %.3g, trans %.3g\n",
+              (unsigned long long)seed, rc, s.num_iterations, s.termination_type, dr, dt);
+  return 0;
+}
+
+int windowVsDirect() {
+  okvisgpu_synth_config cfg;
+  okvisgpu_synth_default_config(&cfg, 10, 500, 4000, 20251015u);
+  okvisgpu_synth_window *wa = nullptr, *wb = nullptr;
+  CHECK(okvisgpu_synth_create(&cfg, &wa) == OKVISGPU_OK && okvisgpu_synth_create(&cfg, &wb) == OKVISGPU_OK);
+  const okvisgpu_problem* pa = okvisgpu_synth_problem(wa);
+  const okvisgpu_problem* pb = okvisgpu_synth_problem(wb);
+  okvisgpu::Problem P;
+  Recorded R;
+  record(P, pa, R);
+  okvisgpu_summary sa, sb;
+  CHECK(P.Solve(zeroTol(5), &sa) == OKVISGPU_OK);
+  okvisgpu_ctx* ctx = nullptr;
+  CHECK(okvisgpu_ctx_create(0, &ctx) == OKVISGPU_OK);
+  CHECK(okvisgpu_set_problems(ctx, pb, 1) == OKVISGPU_OK);
+  const okvisgpu_options o5 = zeroTol(5), o3 = zeroTol(3);
+  CHECK(okvisgpu_solve(ctx, &o5, &sb) == OKVISGPU_OK);
+  double dev = 0;
+  for (int i = 0; i < 7 * pa->n_poses; ++i) dev = std::max(dev, std::fabs(pa->poses[i] - pb->poses[i]));
+  CHECK(sa.num_iterations == sb.num_iterations);
+  CHECK(std::fabs(sa.final_cost - sb.final_cost) <= 1e-9 * sb.final_cost);
+  CHECK(dev <= 1e-9);
+  std::printf("S10 facade vs C ABI: cost %.12g / %.12g, max pose deviation %.3g\n", sa.final_cost, sb.final_cost, dev);
+  // freeze pose 3 between solves (the cheap set_block_constant path) and continue both
+  P.SetParameterBlockConstant(&pa->poses[21]);
+  CHECK(okvisgpu_set_block_constant(ctx, 0, 0, 3, 1) == OKVISGPU_OK);
+  const double p3[7] = {pa->poses[21], pa->poses[22], pa->poses[23], pa->poses[24], pa->poses[25], pa->poses[26], pa->poses[27]};
+  CHECK(P.Solve(zeroTol(3), &sa) == OKVISGPU_OK);
+  CHECK(okvisgpu_update_params(ctx) == OKVISGPU_OK);
+  CHECK(okvisgpu_solve(ctx, &o3, &sb) == OKVISGPU_OK);
+  dev = 0;
+  for (int i = 0; i < 7 * pa->n_poses; ++i) dev = std::max(dev, std::fabs(pa->poses[i] - pb->poses[i]));
+  bool frozen = true;
+  for (int i = 0; i < 7; ++i) frozen = frozen && pa->poses[21 + i] == p3[i];
+  CHECK(frozen);
+  CHECK(std::fabs(sa.final_cost - sb.final_cost) <= 1e-9 * sb.final_cost && dev <= 1e-9);
+  std::printf("after freezing pose 3: cost %.12g / %.12g, max pose deviation %.3g\n", sa.final_cost, sb.final_cost, dev);
+  okvisgpu_ctx_destroy(ctx);
+  okvisgpu_synth_destroy(wa);
+  okvisgpu_synth_destroy(wb);
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const std::string mode = argc > 1 ? argv[1] : "cpu";
+  if (mode == "cpu") return cpuTests();
+  for (uint64_t seed = 1; seed <= 5; ++seed) reprojectionScene(seed);
+  windowVsDirect();
+  std::printf("facade_test gpu %s\n", g_fail ? "FAILED" : "ok");
+  return g_fail ? 1 : 0;
+}
