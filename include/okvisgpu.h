@@ -236,7 +236,9 @@ int okvisgpu_set_problems(okvisgpu_ctx* ctx, const okvisgpu_problem* problems, i
 int okvisgpu_update_params(okvisgpu_ctx* ctx);
 
 /* SetParameterBlockConstant / SetParameterBlockVariable between solves (freeze / unfreeze:
- * ViGraphEstimator.cpp:216-331). kind: 0 pose, 1 speed/bias, 2 landmark. Takes effect at the next
+ * ViGraphEstimator.cpp:216-331; extrinsics: ViGraph::setExtrinsicsVariable, ViGraph.cpp:1733-1739,
+ * and the tracking solve's freeze, ViSlamBackend.cpp:866-872). kind: 0 pose, 1 speed/bias,
+ * 2 landmark, 3 extrinsics (index = camera). Takes effect at the next
  * okvisgpu_solve (the reduced-system structure is rebuilt on the host, values stay on device). */
 int okvisgpu_set_block_constant(okvisgpu_ctx* ctx, int32_t window, int32_t kind, int32_t index,
                                 int32_t is_constant);
@@ -363,7 +365,7 @@ int okvisgpu_evaluate(okvisgpu_ctx* ctx, int32_t window, double* cost);
  * exactly as the solver's first Gauss-Newton solve would form them. Outputs (host, may be NULL):
  *   S   [dim*dim] row-major (full symmetric), rhs [dim], cost [1], dim_out [1].
  * The reduced ordering is: for i = 0 .. max(n_poses, n_speed_biases)-1: pose i (6, if variable)
- * then speed/bias i (9, if variable). */
+ * then speed/bias i (9, if variable); then the variable extrinsics in camera order (6 each). */
 int okvisgpu_linearize_reduce(okvisgpu_ctx* ctx, int32_t window, int32_t jacobi_scaling, double mu,
                               double* S, double* rhs, double* cost, int32_t* dim_out);
 
@@ -402,6 +404,11 @@ typedef struct okvisgpu_synth_config {
   int32_t n_relpose;
   int32_t relpose_stride;
   int32_t relpose_kind;             /* 0 pose-graph edges, 1 RelativePoseError, 2 alternating */
+  /* online extrinsics calibration (ABI 4): both T_SC blocks variable, initialised at the true T_SC
+   * perturbed by N(0, sigma_r^2) / N(0, sigma_alpha^2) and held by a PoseError prior centred on that
+   * initial value (ViGraph.cpp:372-382). 0 (default) = constant extrinsics. */
+  int32_t do_extrinsics;
+  double extrinsics_sigma_r, extrinsics_sigma_alpha;  /* 0.001 m, 0.005 rad (config/hilti22) */
 } okvisgpu_synth_config;
 
 typedef struct okvisgpu_synth_window okvisgpu_synth_window;  /* owns all arrays of one problem */
@@ -411,11 +418,13 @@ void okvisgpu_synth_default_config(okvisgpu_synth_config* cfg, int32_t n_keyfram
 int okvisgpu_synth_create(const okvisgpu_synth_config* cfg, okvisgpu_synth_window** out);
 /* The problem view into the window's arrays (valid until destroy). */
 const okvisgpu_problem* okvisgpu_synth_problem(okvisgpu_synth_window* w);
-/* Ground truth: poses [n_kf][7], landmarks [n_lm][4], speed_biases [n_kf][9] (may be NULL). */
+/* Ground truth: poses [n_kf][7], landmarks [n_lm][4], speed_biases [n_kf][9] (may be NULL); the
+ * true extrinsics are okvisgpu_synth_true_extrinsics [n_cameras][7]. */
 int okvisgpu_synth_ground_truth(const okvisgpu_synth_window* w, double* poses, double* landmarks,
                                 double* speed_biases);
 /* Reset the problem's parameter arrays (and imu_state) to the generated initial estimate. */
 int okvisgpu_synth_reset(okvisgpu_synth_window* w);
+int okvisgpu_synth_true_extrinsics(const okvisgpu_synth_window* w, double* extrinsics);
 void okvisgpu_synth_destroy(okvisgpu_synth_window* w);
 
 #ifdef __cplusplus

@@ -40,7 +40,8 @@ enum ContribType : int32_t {
   C_IMU = 2,        // a = factor, b = column offset of row block, c = column offset of col block
   C_PPRIOR = 3,     // a = pose prior
   C_SBPRIOR = 4,    // a = sb prior
-  C_RELPOSE = 5     // a = relative-pose edge, b / c = column offset (0 reference, 6 other) of row / col block
+  C_RELPOSE = 5,    // a = relative-pose edge, b / c = column offset (0 reference, 6 other) of row / col block
+  C_PEXT = 6        // a = pose-extrinsics record: sum J_e^T J_p (row = extrinsics block, col = state pose)
 };
 constexpr int kRelPoseLin = 6 + 6 * 12;  // per relative-pose edge: r[6] | J minimal 6x12 (reference 6 | other 6)
 
@@ -90,7 +91,8 @@ struct DevProblem {
   double* pose[2];                 // [n_pose][7]
   double* sb[2];                   // [n_sb][9]
   double* lm[2];                   // [n_lm][4]
-  const double* extr;              // [n_cam][7]
+  const double* extr;              // [n_cam][7] initial T_SC (twopose / reference only; solves read pose-kind blocks)
+  const int32_t* cam_pose;         // [n_cam] pose-kind block holding camera c's T_SC (after the window's states)
   const double* cam;               // [n_cam][kCamDoubles]: dist, fu, fv, cu, cv, d0..d7 (dist as double)
 
   // --- per-block window id and reduced-system offsets (-1: not a free f-block / e-block)
@@ -140,6 +142,22 @@ struct DevProblem {
   const int32_t* part_cbegin;      // [n_part+1] CSR into part_contrib
   const int32_t* part_contrib;     // (a | b << 16): visit offsets within the group
   double* part_S;                  // [n_part][36]
+  // extrinsic visits (variable extrinsics only): per (landmark, variable camera) the landmark's
+  // observations through that camera; threads nvg.. of their landmark group (k_lm_visit<.., true>)
+  int32_t n_xvisit;
+  const int32_t* xvisit_pose;      // [n_xvisit] pose-kind block of the extrinsics
+  const int32_t* xvisit_lm;        // [n_xvisit]
+  const int32_t* xvisit_obs_begin; // [n_xvisit+1] CSR into xvisit_obs
+  const int32_t* xvisit_obs;       // global observation indices
+  const int32_t* xvisit_slot;      // [n_xvisit] segment slot within the group
+  const int32_t* lmg_xbegin;       // [n_lmg+1] extrinsic visits of group g
+  // pose-extrinsics cross blocks (k_pose_extr): per (free state pose, variable camera)
+  int32_t n_pe;
+  const int32_t* pe_pose;          // [n_pe] state pose
+  const int32_t* pe_ext;           // [n_pe] pose-kind block of the extrinsics
+  const int32_t* pe_obs_begin;     // [n_pe+1] CSR into pe_obs
+  const int32_t* pe_obs;
+  double* pe_H;                    // [n_pe][36] sum J_e^T J_p (row-major, rows = extrinsics)
 
   // --- IMU factors
   const int32_t* imu_blocks;       // [n_imu][4] global pose0 sb0 pose1 sb1

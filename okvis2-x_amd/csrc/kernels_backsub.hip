@@ -23,6 +23,27 @@
 
 namespace okg {
 
+// EXT (batches with variable extrinsics): an observation through a variable camera also carries
+// J_e (extrJacobian) in q_v and in its J*v rows; its extrinsics' scaled steps are read per observation.
+struct ExtTerm {  // J_e and the extrinsics' s v_c / -s y of one observation
+  double Je[12], ce[6], ge[6];
+};
+__device__ __forceinline__ bool loadExtTerm(const DevProblem& P, int o, int w, int xs, const double C_WS[9],
+                                            const double p3[3], double w4, const double A[6], ExtTerm& X) {
+  if (!(P.obs_flags[o] & 4)) return false;
+  const int e = P.cam_pose[P.obs_cam[o]];
+  const size_t b = (size_t)P.win_foff[w] + P.pose_f[e];
+  extrJacobian(A, C_WS, p3, w4, P.pose[xs] + 7 * (size_t)e, X.Je);
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    const double sc = P.sF[b + c];
+    X.ce[c] = sc * P.vF[b + c];
+    X.ge[c] = -sc * P.yF[b + c];
+  }
+  return true;
+}
+
+template <bool EXT>
 __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int t = threadIdx.x;
@@ -61,21 +82,28 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
   const double w4 = hp[3];
   const double p3[3] = {hp[0] - tw[0] * w4, hp[1] - tw[1] * w4, hp[2] - tw[2] * w4};
   const int ob0 = hasV ? P.visit_obs_begin[v] : 0, ob1 = hasV ? P.visit_obs_begin[v + 1] : 0;
+  double C_WS[9];
+  if (EXT) qrot(qnormalize(Q{tw[3], tw[4], tw[5], tw[6]}), C_WS);
 
   // ---- visit: q_v = W_v^T s_p y_p
   double q[3] = {0.0, 0.0, 0.0};
-  if (pf >= 0 && lfree)
+  if ((pf >= 0 || EXT) && lfree)
     for (int o = ob0; o < ob1; ++o) {
       if (P.obs_flags[o] & 2) continue;
       double A[6], Jp[12], Jl[6];
 #pragma unroll
       for (int k = 0; k < 6; ++k) A[k] = lin[(2 + k) * S + o];
       obsJacobians(A, p3, w4, Jp, Jl);
+      ExtTerm X;
+      const bool hasE = EXT && loadExtTerm(P, o, w, st.xcur, C_WS, p3, w4, A, X);
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
         double jg = 0.0;
 #pragma unroll
         for (int c = 0; c < 6; ++c) jg += Jp[r * 6 + c] * gp[c];
+        if (hasE)
+#pragma unroll
+          for (int c = 0; c < 6; ++c) jg += X.Je[r * 6 + c] * X.ge[c];
 #pragma unroll
         for (int a = 0; a < 3; ++a) q[a] -= Jl[r * 3 + a] * jg;
       }
@@ -142,6 +170,8 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
 #pragma unroll
     for (int k = 0; k < 6; ++k) A[k] = lin[(2 + k) * S + o];
     obsJacobians(A, p3, w4, Jp, Jl);
+    ExtTerm X;
+    const bool hasE = EXT && loadExtTerm(P, o, w, st.xcur, C_WS, p3, w4, A, X);
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       double jc = 0.0, jg = 0.0;
@@ -150,6 +180,12 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
         jc += Jp[r * 6 + c] * cp[c];
         jg += Jp[r * 6 + c] * gp[c];
       }
+      if (hasE)
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          jc += X.Je[r * 6 + c] * X.ce[c];
+          jg += X.Je[r * 6 + c] * X.ge[c];
+        }
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         jc += Jl[r * 3 + c] * cl[c];
@@ -165,7 +201,9 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
 }
 
 void launch_lm_backsub(const DevProblem& P, hipStream_t s) {
-  if (P.n_lmg > 0) hipLaunchKernelGGL(k_lm_backsub_jv, dim3(P.n_lmg), dim3(kLmGroupVisits), 0, s, P.self);
+  if (P.n_lmg <= 0) return;
+  if (P.n_xvisit > 0) hipLaunchKernelGGL(k_lm_backsub_jv<true>, dim3(P.n_lmg), dim3(kLmGroupVisits), 0, s, P.self);
+  else hipLaunchKernelGGL(k_lm_backsub_jv<false>, dim3(P.n_lmg), dim3(kLmGroupVisits), 0, s, P.self);
 }
 
 }  // namespace okg

@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void k_eval_obs(const DevProblem* __restrict__
   const double* pose = P.pose[xs] + 7 * (size_t)P.obs_pose[o];
   const double* hp = P.lm[xs] + 4 * (size_t)P.obs_lm[o];
   const int ci = P.obs_cam[o];
-  const double* ex = P.extr + 7 * ci;
+  const double* ex = P.pose[xs] + 7 * (size_t)P.cam_pose[ci];  // T_SC: a pose-kind block (variable or not)
   const Cam cam = loadCam(P.cam + kCamDoubles * ci);
 
   double C_WS[9], C_SC[9];

@@ -72,7 +72,11 @@ __device__ __forceinline__ bool lmVisitSelect(const DevProblem& P, int w, int mo
 #endif
 // (mode is a template parameter: each mode is its own specialised kernel, and rocprof reports them
 // apart — k_lm_visit<1> is the per-iteration linearisation, k_lm_visit<2> the GN prep)
-template <int mode>
+// EXT (batches with variable extrinsics): threads nvg.. of a group are its extrinsic visits — per
+// (landmark, variable camera) J_e of the landmark's observations through that camera
+// (implementation/ReprojectionError.hpp:186-214, extrJacobian), giving W_e, H_ee, g_e, and so Z_e and
+// the products with the pose visits' Z exactly like a pose visit; V / g_l come from the pose visits.
+template <int mode, bool EXT>
 __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int t = threadIdx.x;
@@ -89,10 +93,13 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   if (!lmVisitSelect(P, w, mode)) return;    // uniform
   const int v = v0 + t;
   const bool hasV = v < v1;
-  const int l = hasV ? P.visit_lm[v] : l0;
+  const int nvg = v1 - v0;
+  const int xv = EXT ? P.lmg_xbegin[blockIdx.x] + t - nvg : 0;
+  const bool hasX = EXT && t >= nvg && xv < P.lmg_xbegin[blockIdx.x + 1];
+  const int l = hasV ? P.visit_lm[v] : (hasX ? P.xvisit_lm[xv] : l0);
   const bool sel = hasV;
   const bool lfree = P.lm_free[l] != 0;
-  const int pose = hasV ? P.visit_pose[v] : 0;
+  const int pose = hasV ? P.visit_pose[v] : (hasX ? P.xvisit_pose[xv] : 0);
   const int pf = P.pose_f[pose];
   double W[18], H[21], gp[6], Vv[6], gl[3];
 #pragma unroll
@@ -138,6 +145,36 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
 #pragma unroll
             for (int b2 = 0; b2 < 3; ++b2) W[a2 * 3 + b2] += Jp[a2] * Jl[b2] + Jp[6 + a2] * Jl[3 + b2];
         }
+      }
+    }
+  }
+  if (EXT && hasX) {  // extrinsic visit: H_ee, g_e, W_e over the landmark's observations via the camera
+    const WinState& st = P.st[w];
+    const auto lin = gmem(P.obs_lin[st.lcur]);
+    const int64_t S = P.obs_stride;
+    const double* hp = P.lm[st.xcur] + 4 * (size_t)l;
+    const double* ex = P.pose[st.xcur] + 7 * (size_t)pose;
+    const double w4 = hp[3];
+    for (int k = P.xvisit_obs_begin[xv]; k < P.xvisit_obs_begin[xv + 1]; ++k) {
+      const int ob = P.xvisit_obs[k];
+      const double* tw = P.pose[st.xcur] + 7 * (size_t)P.obs_pose[ob];
+      const double p3[3] = {hp[0] - tw[0] * w4, hp[1] - tw[1] * w4, hp[2] - tw[2] * w4};
+      double C_WS[9];
+      qrot(qnormalize(Q{tw[3], tw[4], tw[5], tw[6]}), C_WS);
+      double r[2], A[6], Je[12];
+      r[0] = lin[0 * S + ob];
+      r[1] = lin[1 * S + ob];
+#pragma unroll
+      for (int kk = 0; kk < 6; ++kk) A[kk] = lin[(2 + kk) * S + ob];
+      extrJacobian(A, C_WS, p3, w4, ex, Je);
+#pragma unroll
+      for (int a2 = 0; a2 < 6; ++a2) {
+        gp[a2] += Je[a2] * r[0] + Je[6 + a2] * r[1];
+#pragma unroll
+        for (int b2 = a2; b2 < 6; ++b2) H[sym6(a2, b2)] += Je[a2] * Je[b2] + Je[6 + a2] * Je[6 + b2];
+        if (lfree)  // J_l = -A
+#pragma unroll
+          for (int b2 = 0; b2 < 3; ++b2) W[a2 * 3 + b2] -= Je[a2] * A[b2] + Je[6 + a2] * A[3 + b2];
       }
     }
   }
@@ -244,7 +281,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   // ---- segments: H | g of each (group, free pose) summed over its visits in visit order
   // (visits are scattered to their slots so that every segment is a contiguous LDS range)
   const int sg0 = P.seg_gbegin[blockIdx.x], nseg = P.seg_gbegin[blockIdx.x + 1] - sg0;
-  const int slot = hasV ? P.visit_slot[v] : -1;
+  const int slot = hasV ? P.visit_slot[v] : (hasX ? P.xvisit_slot[xv] : -1);
   if (mode != 2) {
 #pragma unroll
     for (int chunk = 0; chunk < 3; ++chunk) {
@@ -349,6 +386,45 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
 #pragma unroll
     for (int q = 0; q < 6; ++q) out[q] = double2{acc[2 * q], acc[2 * q + 1]};
   }
+}
+
+// Pose-extrinsics cross blocks of F^T F (variable extrinsics only): per (free state pose, variable
+// camera) the sum over their observations of J_e^T J_p (6x6, rows = extrinsics), one thread each, in
+// observation order. The landmark terms of the same block come from k_lm_visit's partial blocks.
+__global__ __launch_bounds__(256) void k_pose_extr(const DevProblem* __restrict__ Pp, int lin_mode) {
+  const DevProblem& P = *Pp;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= P.n_pe) return;
+  const int w = P.pose_win[P.pe_pose[k]];
+  if (!linSelect(P, w, lin_mode)) return;
+  const WinState& st = P.st[w];
+  const auto lin = gmem(P.obs_lin[st.lcur]);
+  const int64_t S = P.obs_stride;
+  const double* tw = P.pose[st.xcur] + 7 * (size_t)P.pe_pose[k];
+  const double* ex = P.pose[st.xcur] + 7 * (size_t)P.pe_ext[k];
+  double C_WS[9];
+  qrot(qnormalize(Q{tw[3], tw[4], tw[5], tw[6]}), C_WS);
+  double H[36];
+#pragma unroll
+  for (int i = 0; i < 36; ++i) H[i] = 0.0;
+  for (int j = P.pe_obs_begin[k]; j < P.pe_obs_begin[k + 1]; ++j) {
+    const int ob = P.pe_obs[j];
+    const double* hp = P.lm[st.xcur] + 4 * (size_t)P.obs_lm[ob];
+    const double w4 = hp[3];
+    const double p3[3] = {hp[0] - tw[0] * w4, hp[1] - tw[1] * w4, hp[2] - tw[2] * w4};
+    double A[6], Jp[12], Jl[6], Je[12];
+#pragma unroll
+    for (int kk = 0; kk < 6; ++kk) A[kk] = lin[(2 + kk) * S + ob];
+    obsJacobians(A, p3, w4, Jp, Jl);
+    extrJacobian(A, C_WS, p3, w4, ex, Je);
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int b = 0; b < 6; ++b) H[a * 6 + b] += Je[a] * Jp[b] + Je[6 + a] * Jp[6 + b];
+  }
+  double* out = P.pe_H + 36 * (size_t)k;
+#pragma unroll
+  for (int i = 0; i < 36; ++i) out[i] = H[i];
 }
 
 // contribution helpers -------------------------------------------------------------------------
@@ -571,6 +647,10 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
 #pragma unroll
         for (int q = 0; q < 6; ++q) H[q] += jr * L[k2 * 12 + C.c + q];
       }
+    } else if (C.type == C_PEXT) {  // row r of sum J_e^T J_p (extrinsics row block, pose column block)
+      const auto Hx = gmem(P.pe_H + 36 * (size_t)C.a + 6 * r);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) H[q] += Hx[q];
     } else {  // C_PPRIOR
       const double* L = P.pp_lin[lb] + 42 * (size_t)C.a + 6;
       for (int k2 = 0; k2 < 6; ++k2) {
@@ -698,9 +778,16 @@ __global__ __launch_bounds__(256) void k_gn_finalize(const DevProblem* __restric
 // ------------------------------------------------------------------------------------ launchers
 void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s) {
   if (P.n_lmg <= 0) return;
-  if (mode == 0) hipLaunchKernelGGL(k_lm_visit<0>, dim3(P.n_lmg), dim3(kLmGroupVisits), 0, s, P.self);
-  else if (mode == 1) hipLaunchKernelGGL(k_lm_visit<1>, dim3(P.n_lmg), dim3(kLmGroupVisits), 0, s, P.self);
-  else hipLaunchKernelGGL(k_lm_visit<2>, dim3(P.n_lmg), dim3(kLmGroupVisits), 0, s, P.self);
+  const dim3 g(P.n_lmg), b(kLmGroupVisits);
+  if (P.n_xvisit > 0) {
+    if (mode == 0) hipLaunchKernelGGL((k_lm_visit<0, true>), g, b, 0, s, P.self);
+    else if (mode == 1) hipLaunchKernelGGL((k_lm_visit<1, true>), g, b, 0, s, P.self);
+    else hipLaunchKernelGGL((k_lm_visit<2, true>), g, b, 0, s, P.self);
+  } else {
+    if (mode == 0) hipLaunchKernelGGL((k_lm_visit<0, false>), g, b, 0, s, P.self);
+    else if (mode == 1) hipLaunchKernelGGL((k_lm_visit<1, false>), g, b, 0, s, P.self);
+    else hipLaunchKernelGGL((k_lm_visit<2, false>), g, b, 0, s, P.self);
+  }
 }
 void launch_assemble_pp(const DevProblem& P, hipStream_t s) {
   if (P.n_asm_pp > 0) hipLaunchKernelGGL(k_assemble_pp, dim3((P.n_asm_pp + 3) / 4), dim3(256), 0, s, P.self);
@@ -708,7 +795,10 @@ void launch_assemble_pp(const DevProblem& P, hipStream_t s) {
 void launch_assemble_sb(const DevProblem& P, hipStream_t s) {
   if (P.n_asm_sb > 0) hipLaunchKernelGGL(k_assemble_sb, dim3((P.n_asm_sb + 3) / 4), dim3(256), 0, s, P.self);
 }
-void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s) { launch_lm_visit(P, lin_mode, s); }
+void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
+  launch_lm_visit(P, lin_mode, s);
+  if (P.n_pe > 0) hipLaunchKernelGGL(k_pose_extr, dim3((P.n_pe + 255) / 256), dim3(256), 0, s, P.self, lin_mode);
+}
 void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s) {
   if (P.n_fblock > 0) hipLaunchKernelGGL(k_fgrad, dim3(P.n_fblock), dim3(64), 0, s, P.self, lin_mode);
 }

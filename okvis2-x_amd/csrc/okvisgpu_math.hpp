@@ -255,6 +255,31 @@ OKG_HD void obsJacobians(const double A[6], const double p[3], double w, double 
   }
 }
 
+// Minimal Jacobian of the weighted reprojection residual w.r.t. the extrinsics T_SC
+// (implementation/ReprojectionError.hpp:186-214): J2 = Jh_w [C_CS w, -C_CS [p_S]x] with
+// Jh_w C_CS = A C_WS, p_S = C_SW p - t_SC w (p = hp.xyz - t_WS w); A as stored (Cauchy-scaled).
+OKG_HD void extrJacobian(const double A[6], const double C_WS[9], const double p[3], double w, const double* ex,
+                         double Je[12]) {
+  double pS[3];
+  mtv3(C_WS, p, pS);
+  pS[0] -= ex[0] * w;
+  pS[1] -= ex[1] * w;
+  pS[2] -= ex[2] * w;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    // b = (A C_WS) row r
+    const double b0 = A[r * 3 + 0] * C_WS[0] + A[r * 3 + 1] * C_WS[3] + A[r * 3 + 2] * C_WS[6];
+    const double b1 = A[r * 3 + 0] * C_WS[1] + A[r * 3 + 1] * C_WS[4] + A[r * 3 + 2] * C_WS[7];
+    const double b2 = A[r * 3 + 0] * C_WS[2] + A[r * 3 + 1] * C_WS[5] + A[r * 3 + 2] * C_WS[8];
+    Je[r * 6 + 0] = w * b0;
+    Je[r * 6 + 1] = w * b1;
+    Je[r * 6 + 2] = w * b2;
+    Je[r * 6 + 3] = -(b1 * pS[2] - b2 * pS[1]);
+    Je[r * 6 + 4] = -(b2 * pS[0] - b0 * pS[2]);
+    Je[r * 6 + 5] = -(b0 * pS[1] - b1 * pS[0]);
+  }
+}
+
 // ReprojectionError<G>::EvaluateWithMinimalJacobians in the factored form
 // (implementation/ReprojectionError.hpp:71-220): weighted residual r = L (meas - kp) (no loss) and
 // A = L Jh C_CS C_SW (2x3), so that J_pose = [w A, -A [p]x] and J_landmark = -A (obsJacobians)

@@ -64,6 +64,13 @@ struct HostBatch {
   // parameters (initial copies)
   std::vector<double> pose, sb, lm, extr, cam;
   std::vector<int32_t> lm_perm;  // internal landmark k of window w is the caller's landmark lm_perm[lm_base[w] + k]
+  // extrinsics: camera c of window w is pose-kind block cam_pose[cam_base[w] + c] (after the states)
+  std::vector<int32_t> cam_pose;
+  std::vector<uint8_t> win_ext_free;  // window has a variable extrinsics block (write-back)
+  // extrinsic visits (landmark, variable camera): observation lists (global obs index), the group's
+  // range, segment slots; pose-extrinsics cross blocks (state pose, variable camera) with their obs
+  std::vector<int32_t> xvisit_pose, xvisit_lm, xvisit_obs_begin, xvisit_obs, xvisit_slot, lmg_xbegin;
+  std::vector<int32_t> pe_pose, pe_ext, pe_obs_begin, pe_obs;
   std::vector<int32_t> pose_win, sb_win, lm_win, pose_f, sb_f;
   std::vector<uint8_t> lm_free, pose_active, sb_active;
   // obs (sorted) + permutation to the caller's order (within the window)
@@ -134,11 +141,13 @@ void validate(const okvisgpu_problem* p, int w) {
   }
   for (int c = 0; c < p->n_cameras; ++c)
     if (p->cameras[c].distortion < 0 || p->cameras[c].distortion > 3) bad("unknown distortion model");
-  if (p->extrinsics_constant)
-    for (int c = 0; c < p->n_cameras; ++c)
-      if (!p->extrinsics_constant[c]) throw UnsupportedError{"window " + std::to_string(w) +
-                                                              ": variable extrinsics are not supported yet"};
   if (p->n_extrinsics_priors < 0) bad("negative count");
+  if (p->n_extrinsics_priors && (!p->extrinsics_prior_camera || !p->extrinsics_prior_meas || !p->extrinsics_prior_sqrt_info))
+    bad("extrinsics prior arrays missing");
+  for (int i = 0; i < p->n_extrinsics_priors; ++i)
+    if (p->extrinsics_prior_camera[i] < 0 || p->extrinsics_prior_camera[i] >= p->n_cameras)
+      bad("extrinsics prior camera out of range");
+  if (p->n_cameras && !p->extrinsics) bad("extrinsics == NULL");
   if (p->n_imu) {
     if (!p->imu_blocks || !p->imu_t0_ns || !p->imu_t1_ns || !p->imu_sample_begin || !p->imu_sample_t_ns ||
         !p->imu_sample_gyr_acc)
@@ -188,12 +197,21 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       if (it != constOverride.end()) return it->second != 0;
       return flags ? flags[idx] != 0 : false;
     };
-    std::vector<uint8_t> pc(p->n_poses), sc(p->n_speed_biases), lc(p->n_landmarks);
-    for (int i = 0; i < p->n_poses; ++i) pc[i] = isConst(0, i, p->pose_constant);
+    // pose-kind blocks of the window: the states' poses [0, np), then one extrinsics block per
+    // camera [np, np + ncam) (okvis: PoseParameterBlocks with the PoseManifold, ViGraph.cpp:330-336)
+    const int np = p->n_poses, ncam = p->n_cameras, npx = np + ncam;
+    std::vector<uint8_t> pc(npx), sc(p->n_speed_biases), lc(p->n_landmarks);
+    for (int i = 0; i < np; ++i) pc[i] = isConst(0, i, p->pose_constant);
+    for (int c = 0; c < ncam; ++c) {  // constant unless flagged variable (do_extrinsics: false)
+      auto it = constOverride.find(std::make_tuple(w, 3, c));
+      pc[np + c] = it != constOverride.end() ? it->second != 0
+                                             : (p->extrinsics_constant ? p->extrinsics_constant[c] != 0 : 1);
+    }
     for (int i = 0; i < p->n_speed_biases; ++i) sc[i] = isConst(1, i, p->speed_bias_constant);
     for (int i = 0; i < p->n_landmarks; ++i) lc[i] = isConst(2, i, p->landmark_constant);
     // parameters
     appendN(B.pose, p->poses, (size_t)7 * p->n_poses);
+    appendN(B.pose, p->extrinsics, (size_t)7 * ncam);
     appendN(B.sb, p->speed_biases, (size_t)9 * p->n_speed_biases);
     // internal landmark order: by first observing pose (then caller order), so that the visits of
     // neighbouring keyframes are close in memory whatever order the caller numbers landmarks in
@@ -217,18 +235,20 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
                                       k.dist[2], k.dist[3], k.dist[4], k.dist[5], k.dist[6], k.dist[7]};
       appendN(B.cam, cv, kCamDoubles);
       appendN(B.extr, &p->extrinsics[7 * c], 7);
+      B.cam_pose.push_back(pb + np + c);
     }
-    for (int i = 0; i < p->n_poses; ++i) B.pose_win.push_back(w);
+    for (int i = 0; i < npx; ++i) B.pose_win.push_back(w);
     for (int i = 0; i < p->n_speed_biases; ++i) B.sb_win.push_back(w);
     for (int i = 0; i < p->n_landmarks; ++i) B.lm_win.push_back(w);
     // active blocks: free and used by a residual block that is not entirely constant
-    std::vector<uint8_t> pa(p->n_poses, 0), sa(p->n_speed_biases, 0), la(p->n_landmarks, 0);
+    std::vector<uint8_t> pa(npx, 0), sa(p->n_speed_biases, 0), la(p->n_landmarks, 0);
     std::vector<uint8_t> ofix(p->n_observations), ifix(p->n_imu);
     for (int o = 0; o < p->n_observations; ++o) {
-      const int ps = p->obs_pose[o], l = p->obs_landmark[o];
-      ofix[o] = pc[ps] && lc[l];
+      const int ps = p->obs_pose[o], l = p->obs_landmark[o], xe = np + p->obs_camera[o];
+      ofix[o] = pc[ps] && lc[l] && pc[xe];
       if (!pc[ps]) pa[ps] = 1;
       if (!lc[l]) la[l] = 1;
+      if (!pc[xe]) pa[xe] = 1;
     }
     for (int f = 0; f < p->n_imu; ++f) {
       const int* b = &p->imu_blocks[4 * f];
@@ -238,8 +258,17 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       if (!pc[b[2]]) pa[b[2]] = 1;
       if (!sc[b[3]]) sa[b[3]] = 1;
     }
+    // PoseError priors on pose-kind blocks: the states' (pose_prior_*) then the extrinsics'
+    // (extrinsics_prior_*, ViGraph.cpp:372-382), one prior list on the device
+    struct PPrior { int blk; const double* meas; const double* L; };
+    std::vector<PPrior> pps;
     for (int i = 0; i < p->n_pose_priors; ++i)
-      if (!pc[p->pose_prior_block[i]]) pa[p->pose_prior_block[i]] = 1;
+      pps.push_back(PPrior{p->pose_prior_block[i], &p->pose_prior_meas[7 * i], &p->pose_prior_sqrt_info[36 * i]});
+    for (int i = 0; i < p->n_extrinsics_priors; ++i)
+      pps.push_back(PPrior{np + p->extrinsics_prior_camera[i], &p->extrinsics_prior_meas[7 * i],
+                           &p->extrinsics_prior_sqrt_info[36 * i]});
+    for (const PPrior& q : pps)
+      if (!pc[q.blk]) pa[q.blk] = 1;
     for (int i = 0; i < p->n_sb_priors; ++i)
       if (!sc[p->sb_prior_block[i]]) sa[p->sb_prior_block[i]] = 1;
     std::vector<uint8_t> rfix(p->n_relpose);
@@ -250,8 +279,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       if (!pc[b]) pa[b] = 1;
     }
     // f-blocks in the reduced ordering: pose i, then speed/bias i
-    std::vector<int> posef(p->n_poses, -1), sbf(p->n_speed_biases, -1), poseFb(p->n_poses, -1),
-        sbFb(p->n_speed_biases, -1);
+    std::vector<int> posef(npx, -1), sbf(p->n_speed_biases, -1), poseFb(npx, -1), sbFb(p->n_speed_biases, -1);
     int fo = 0;
     const int nmax = std::max(p->n_poses, p->n_speed_biases);
     const int fbBase = (int)B.fb_win.size();
@@ -269,7 +297,17 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
         fo += 9;
       }
     }
-    for (int i = 0; i < p->n_poses; ++i) { B.pose_f.push_back(posef[i]); B.pose_active.push_back(pa[i]); }
+    // variable extrinsics after all states: S keeps the states' band plus a dense border
+    for (int c = 0; c < ncam; ++c) {
+      const int i = np + c;
+      if (!pa[i]) continue;
+      posef[i] = fo;
+      poseFb[i] = (int)B.fb_win.size();
+      B.fb_win.push_back(w); B.fb_kind.push_back(0); B.fb_index.push_back(pb + i); B.fb_off.push_back(fo);
+      fo += 6;
+    }
+    B.win_ext_free.push_back(fo > 0 && std::any_of(pa.begin() + np, pa.end(), [](uint8_t a) { return a != 0; }));
+    for (int i = 0; i < npx; ++i) { B.pose_f.push_back(posef[i]); B.pose_active.push_back(pa[i]); }
     for (int i = 0; i < p->n_speed_biases; ++i) { B.sb_f.push_back(sbf[i]); B.sb_active.push_back(sa[i]); }
     std::vector<uint8_t> laNew(p->n_landmarks);
     for (int k = 0; k < p->n_landmarks; ++k) laNew[k] = la[perm[k]];
@@ -313,6 +351,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
         uint8_t fl = 0;
         if (p->obs_cauchy ? p->obs_cauchy[o] != 0 : true) fl |= 1;
         if (ofix[o]) fl |= 2;
+        if (posef[np + p->obs_camera[o]] >= 0) fl |= 4;  // variable extrinsics
         B.obs_flags.push_back(fl);
         appendN(B.obs_kp, &p->obs_keypoint[2 * o], 2);
         appendN(B.obs_L, &p->obs_sqrt_info[4 * o], 4);
@@ -334,47 +373,85 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       lmVisitBegin[p->n_landmarks] = acc;
       for (int l = 0; l < p->n_landmarks; ++l) B.lm_visit_begin.push_back(lmVisitBegin[l]);
     }
+    // extrinsic visits: per landmark and variable camera, the landmark's (non-fixed) observations
+    // through that camera (the extrinsics block is the third parameter block of their
+    // ReprojectionErrors); global indices, in landmark order like the visits
+    std::vector<int> lmXBegin(p->n_landmarks + 1, (int)B.xvisit_pose.size());
+    {
+      std::vector<int> freeCams;
+      for (int c = 0; c < ncam; ++c)
+        if (posef[np + c] >= 0) freeCams.push_back(c);
+      int k = 0;
+      for (int l = 0; l < p->n_landmarks; ++l) {
+        lmXBegin[l] = (int)B.xvisit_pose.size();
+        const int k0 = k;
+        while (k < p->n_observations && inv[p->obs_landmark[order[k]]] == l) ++k;
+        for (int c : freeCams) {
+          std::vector<int32_t> obs;
+          for (int j = k0; j < k; ++j)
+            if (p->obs_camera[order[j]] == c && !ofix[order[j]]) obs.push_back(ob + j);
+          if (obs.empty()) continue;
+          B.xvisit_pose.push_back(pb + np + c);
+          B.xvisit_lm.push_back(lb + l);
+          B.xvisit_obs_begin.push_back((int32_t)B.xvisit_obs.size());
+          B.xvisit_obs.insert(B.xvisit_obs.end(), obs.begin(), obs.end());
+          B.xvisit_slot.push_back(-1);
+        }
+      }
+      lmXBegin[p->n_landmarks] = (int)B.xvisit_pose.size();
+    }
     // landmark groups of k_lm_visit (consecutive whole landmarks of this window, <= kLmGroupVisits
     // visits and <= kLmGroupMax landmarks; one workgroup, one thread per visit) and their visit
     // segments: the visits of a group that belong to one free pose, pre-summed by k_lm_visit into
     // one H | g and one U z record (ascending pose; members in visit order)
-    std::vector<std::vector<int>> segsAtPose(p->n_poses);
+    std::vector<std::vector<int>> segsAtPose(npx);
     std::vector<std::pair<int, int>> partKeys;  // f-block pair of each partial block of this window
     const int partBase = (int)B.part_cbegin.size();
     {
       // each visit of a free pose gets the slot of its position in the group's (pose, visit)
       // order, so a segment is a contiguous slot range [seg_range.x, seg_range.y)
+      // A group's threads: its pose visits first (thread t = v - gv0), then its extrinsic visits
+      // (thread t = nvg + xv - gx0).
       auto closeGroup = [&](int gl0, int gl1) {
-        const int gv0 = lmVisitBegin[gl0], gv1 = lmVisitBegin[gl1];
-        std::map<int, std::vector<int>> mem;
+        const int gv0 = lmVisitBegin[gl0], gv1 = lmVisitBegin[gl1], nvg = gv1 - gv0;
+        const int gx0 = lmXBegin[gl0], gx1 = lmXBegin[gl1];
+        std::map<int, std::vector<int>> mem;  // pose-kind block -> members (v >= 0 visit, -1 - xv extrinsic visit)
         for (int v = gv0; v < gv1; ++v) {
           const int ps = B.visit_pose[v] - pb;
           if (posef[ps] >= 0) mem[ps].push_back(v);
           else B.visit_slot[v] = -1;
         }
+        for (int xv = gx0; xv < gx1; ++xv) mem[B.xvisit_pose[xv] - pb].push_back(-1 - xv);
         int slot = 0;
         for (auto& kv : mem) {
           segsAtPose[kv.first].push_back((int)B.seg_pose.size());
           B.seg_pose.push_back(pb + kv.first);
           B.seg_range.push_back(slot);
-          for (int v : kv.second) B.visit_slot[v] = slot++;
+          for (int v : kv.second) {
+            if (v >= 0) B.visit_slot[v] = slot++;
+            else B.xvisit_slot[-1 - v] = slot++;
+          }
           B.seg_range.push_back(slot);
         }
-        // partial Schur blocks (k_lm_visit): per pose pair (row >= col by f offset) the products
-        // Z_a Z_b^T of the group's free landmarks; contributions packed as (a | b << 16), visit
+        // partial Schur blocks (k_lm_visit): per f-block pair (row >= col by f offset) the products
+        // Z_a Z_b^T of the group's free landmarks; contributions packed as (a | b << 16), thread
         // offsets within the group
         std::map<std::pair<int, int>, std::vector<int32_t>> gparts;
+        std::vector<std::pair<int, int>> items;  // (thread, f-block) of one landmark's free visits
         for (int l = gl0; l < gl1; ++l) {
           if (!laNew[l]) continue;
+          items.clear();
           for (int va = lmVisitBegin[l]; va < lmVisitBegin[l + 1]; ++va) {
             const int fa = poseFb[B.visit_pose[va] - pb];
-            if (fa < 0) continue;
-            for (int vb = lmVisitBegin[l]; vb < lmVisitBegin[l + 1]; ++vb) {
-              const int fb2 = poseFb[B.visit_pose[vb] - pb];
-              if (fb2 < 0 || B.fb_off[fa] < B.fb_off[fb2]) continue;
-              gparts[std::make_pair(fa, fb2)].push_back((va - gv0) | ((vb - gv0) << 16));
-            }
+            if (fa >= 0) items.push_back({va - gv0, fa});
           }
+          for (int xv = lmXBegin[l]; xv < lmXBegin[l + 1]; ++xv)
+            items.push_back({nvg + xv - gx0, poseFb[B.xvisit_pose[xv] - pb]});
+          for (const auto& a : items)
+            for (const auto& b : items) {
+              if (B.fb_off[a.second] < B.fb_off[b.second]) continue;
+              gparts[std::make_pair(a.second, b.second)].push_back(a.first | (b.first << 16));
+            }
         }
         // long blocks are split into chunks of <= kPartChunk products (separate records, summed
         // in order by k_assemble_pp) so that no k_lm_visit thread serialises a whole block
@@ -387,6 +464,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
             B.part_contrib.insert(B.part_contrib.end(), kv.second.begin() + c0, kv.second.begin() + c1);
           }
         B.lmg_begin.push_back(lb + gl0);
+        B.lmg_xbegin.push_back(gx0);
         B.seg_gbegin.push_back((int)B.seg_pose.size());
         B.part_gbegin.push_back((int)B.part_cbegin.size());
       };
@@ -396,7 +474,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       // whose products k_lm_visit streams from HBM instead.
       auto pairCount = [&](int l) {
         if (!laNew[l]) return 0;
-        int nf = 0;
+        int nf = lmXBegin[l + 1] - lmXBegin[l];
         for (int v = lmVisitBegin[l]; v < lmVisitBegin[l + 1]; ++v) nf += posef[B.visit_pose[v] - pb] >= 0;
         return nf * (nf + 1) / 2;
       };
@@ -404,10 +482,10 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       B.visit_slot.resize(B.visit_pose.size(), -1);
       int g0 = 0, gl = 0;
       for (int l = 0; l < p->n_landmarks; ++l) {
-        const int nv = lmVisitBegin[l + 1] - lmVisitBegin[l];
+        const int nv = lmVisitBegin[l + 1] - lmVisitBegin[l] + lmXBegin[l + 1] - lmXBegin[l];
         if (nv > kLmGroupVisits)
           throw ArgError{"landmark with more than " + std::to_string(kLmGroupVisits) + " observing poses"};
-        const int gv = lmVisitBegin[l] - lmVisitBegin[g0];
+        const int gv = lmVisitBegin[l] - lmVisitBegin[g0] + lmXBegin[l] - lmXBegin[g0];
         const int pcl = pairCount(l);
         if (l > g0 && (gv + nv > kLmGroupVisits || gl == kLmGroupMax || gpc + pcl > kLmPartStage)) {
           closeGroup(g0, l);
@@ -447,11 +525,11 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       else B.imu_state.insert(B.imu_state.end(), OKVISGPU_IMU_STATE_DOUBLES, 0.0);
     }
     // priors
-    for (int i = 0; i < p->n_pose_priors; ++i) {
-      B.pp_block.push_back(pb + p->pose_prior_block[i]);
+    for (const PPrior& q : pps) {
+      B.pp_block.push_back(pb + q.blk);
       B.pp_win.push_back(w);
-      appendN(B.pp_meas, &p->pose_prior_meas[7 * i], 7);
-      appendN(B.pp_L, &p->pose_prior_sqrt_info[36 * i], 36);
+      appendN(B.pp_meas, q.meas, 7);
+      appendN(B.pp_L, q.L, 36);
     }
     for (int i = 0; i < p->n_sb_priors; ++i) {
       B.sbp_block.push_back(sbb + p->sb_prior_block[i]);
@@ -470,9 +548,9 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       appendN(B.rp_lp, &p->relpose_lin_point[7 * i], 7);
     }
     // ranges
-    const int r_pose[2] = {pb, pb + p->n_poses}, r_sb[2] = {sbb, sbb + p->n_speed_biases},
+    const int r_pose[2] = {pb, pb + npx}, r_sb[2] = {sbb, sbb + p->n_speed_biases},
               r_lm[2] = {lb, lb + p->n_landmarks}, r_obs[2] = {ob, ob + p->n_observations},
-              r_imu[2] = {ib, ib + p->n_imu}, r_pp[2] = {ppb, ppb + p->n_pose_priors},
+              r_imu[2] = {ib, ib + p->n_imu}, r_pp[2] = {ppb, ppb + (int)pps.size()},
               r_sbp[2] = {sbpb, sbpb + p->n_sb_priors}, r_rp[2] = {rpb, rpb + p->n_relpose};
     appendN(B.win_pose_range, r_pose, 2); appendN(B.win_sb_range, r_sb, 2); appendN(B.win_lm_range, r_lm, 2);
     appendN(B.win_obs_range, r_obs, 2); appendN(B.win_imu_range, r_imu, 2); appendN(B.win_pp_range, r_pp, 2);
@@ -482,7 +560,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     // ---- f-block gradient / diagonal contribution lists
     const int nFb = (int)B.fb_win.size() - fbBase;
     std::vector<std::vector<Contrib>> fbc(nFb);
-    for (int i = 0; i < p->n_poses; ++i) {
+    for (int i = 0; i < npx; ++i) {
       if (poseFb[i] < 0) continue;
       for (int sg : segsAtPose[i]) fbc[poseFb[i] - fbBase].push_back(Contrib{C_VISIT, sg, 0, 0});
     }
@@ -494,9 +572,9 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       for (int q = 0; q < 4; ++q)
         if (fbs[q] >= 0) fbc[fbs[q] - fbBase].push_back(Contrib{C_IMU, ib + f, imuCol[q], imuCol[q]});
     }
-    for (int i = 0; i < p->n_pose_priors; ++i) {
-      const int fb = poseFb[p->pose_prior_block[i]];
-      if (fb >= 0) fbc[fb - fbBase].push_back(Contrib{C_PPRIOR, ppb + i, 0, 0});
+    for (size_t i = 0; i < pps.size(); ++i) {
+      const int fb = poseFb[pps[i].blk];
+      if (fb >= 0) fbc[fb - fbBase].push_back(Contrib{C_PPRIOR, ppb + (int)i, 0, 0});
     }
     for (int i = 0; i < p->n_sb_priors; ++i) {
       const int fb = sbFb[p->sb_prior_block[i]];
@@ -518,7 +596,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     auto key = [&](int fa, int fb2) {  // row = larger offset
       return B.fb_off[fa] >= B.fb_off[fb2] ? std::make_pair(fa, fb2) : std::make_pair(fb2, fa);
     };
-    for (int i = 0; i < p->n_poses; ++i) {
+    for (int i = 0; i < npx; ++i) {
       if (poseFb[i] < 0) continue;
       auto& lst = pairs[std::make_pair(poseFb[i], poseFb[i])];
       for (int sg : segsAtPose[i]) lst.push_back(Contrib{C_VISIT, sg, 0, 0});
@@ -536,9 +614,28 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
           pairs[key(fbs[u], fbs[v])].push_back(Contrib{C_IMU, ib + f, imuCol[u], imuCol[v]});
         }
     }
-    for (int i = 0; i < p->n_pose_priors; ++i) {
-      const int fb = poseFb[p->pose_prior_block[i]];
-      if (fb >= 0) pairs[std::make_pair(fb, fb)].push_back(Contrib{C_PPRIOR, ppb + i, 0, 0});
+    for (size_t i = 0; i < pps.size(); ++i) {
+      const int fb = poseFb[pps[i].blk];
+      if (fb >= 0) pairs[std::make_pair(fb, fb)].push_back(Contrib{C_PPRIOR, ppb + (int)i, 0, 0});
+    }
+    // pose-extrinsics cross blocks: sum over the observations of a free state pose through a
+    // variable camera of J_e^T J_p (k_pose_extr); row = the extrinsics block (after all states)
+    for (int ps = 0; ps < np; ++ps) {
+      if (poseFb[ps] < 0) continue;
+      for (int c = 0; c < ncam; ++c) {
+        if (poseFb[np + c] < 0) continue;
+        std::vector<int32_t> obs;
+        for (int k = 0; k < p->n_observations; ++k) {
+          const int o = order[k];
+          if (p->obs_pose[o] == ps && p->obs_camera[o] == c && !ofix[o]) obs.push_back(ob + k);
+        }
+        if (obs.empty()) continue;
+        pairs[key(poseFb[np + c], poseFb[ps])].push_back(Contrib{C_PEXT, (int)B.pe_pose.size(), 0, 0});
+        B.pe_pose.push_back(pb + ps);
+        B.pe_ext.push_back(pb + np + c);
+        B.pe_obs_begin.push_back((int32_t)B.pe_obs.size());
+        B.pe_obs.insert(B.pe_obs.end(), obs.begin(), obs.end());
+      }
     }
     for (int i = 0; i < p->n_sb_priors; ++i) {
       const int fb = sbFb[p->sb_prior_block[i]];
@@ -662,6 +759,9 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
   }
   B.lm_visit_begin.push_back((int)B.visit_pose.size());
   B.lmg_begin.push_back((int)B.lm_win.size());  // groups: begin of each, then the end
+  B.lmg_xbegin.push_back((int)B.xvisit_pose.size());
+  B.xvisit_obs_begin.push_back((int)B.xvisit_obs.size());
+  B.pe_obs_begin.push_back((int)B.pe_obs.size());
   B.part_cbegin.push_back((int)B.part_contrib.size());
   B.visit_obs_begin.push_back((int)B.obs_win.size());
   B.imu_sbegin.push_back((int)B.imu_ts.size());
@@ -807,6 +907,12 @@ struct okvisgpu_ctx {
     const size_t o_pgb = upl(B.part_gbegin), o_pcb2 = upl(B.part_cbegin), o_pcon = upl(B.part_contrib),
                  o_partS = scratch(sizeof(double) * 36 * std::max(1, D.n_part));
     const size_t o_shg = scratch(sizeof(double) * kSegHG * D.n_seg), o_suz = scratch(sizeof(double) * kSegUz * D.n_seg);
+    D.n_xvisit = (int)B.xvisit_pose.size();
+    D.n_pe = (int)B.pe_pose.size();
+    const size_t o_cpose = upl(B.cam_pose), o_xvp = upl(B.xvisit_pose), o_xvl = upl(B.xvisit_lm),
+                 o_xvob = upl(B.xvisit_obs_begin), o_xvo = upl(B.xvisit_obs), o_xvs = upl(B.xvisit_slot),
+                 o_lmgx = upl(B.lmg_xbegin), o_pep = upl(B.pe_pose), o_pee = upl(B.pe_ext), o_peob = upl(B.pe_obs_begin),
+                 o_peo = upl(B.pe_obs), o_peH = scratch(sizeof(double) * 36 * std::max(1, D.n_pe));
     const size_t o_imu_blocks = upl(B.imu_blocks), o_imu_win = upl(B.imu_win), o_imu_flags = upl(B.imu_flags),
                  o_imu_t0 = upl(B.imu_t0), o_imu_t1 = upl(B.imu_t1), o_imu_sb = upl(B.imu_sbegin),
                  o_imu_ts = upl(B.imu_ts), o_imu_ga = upl(B.imu_ga), o_imu_par = upl(B.imu_par),
@@ -882,6 +988,10 @@ struct okvisgpu_ctx {
     D.part_gbegin = ip(o_pgb); D.part_cbegin = ip(o_pcb2); D.part_contrib = ip(o_pcon); D.part_S = dp(o_partS);
     D.seg_hg = dp(o_shg); D.seg_uz = dp(o_suz);
     D.seg_gbegin = ip(o_seg_gb); D.seg_pose = ip(o_seg_pose); D.seg_range = ip(o_seg_rg); D.visit_slot = ip(o_vslot);
+    D.cam_pose = ip(o_cpose);
+    D.xvisit_pose = ip(o_xvp); D.xvisit_lm = ip(o_xvl); D.xvisit_obs_begin = ip(o_xvob); D.xvisit_obs = ip(o_xvo);
+    D.xvisit_slot = ip(o_xvs); D.lmg_xbegin = ip(o_lmgx);
+    D.pe_pose = ip(o_pep); D.pe_ext = ip(o_pee); D.pe_obs_begin = ip(o_peob); D.pe_obs = ip(o_peo); D.pe_H = dp(o_peH);
     D.lmg_begin = ip(o_lmg_b); D.n_lmg = B.lmg_begin.empty() ? 0 : (int)B.lmg_begin.size() - 1;
     D.imu_blocks = ip(o_imu_blocks); D.imu_win = ip(o_imu_win); D.imu_flags = up(o_imu_flags);
     D.imu_t0 = lp(o_imu_t0); D.imu_t1 = lp(o_imu_t1); D.imu_sbegin = ip(o_imu_sb); D.imu_ts = lp(o_imu_ts);
@@ -996,6 +1106,7 @@ struct okvisgpu_ctx {
     for (int w = 0; w < B.n_win; ++w) {
       const okvisgpu_problem* p = probs[w];
       appendN(pose, p->poses, (size_t)7 * p->n_poses);
+      appendN(pose, p->extrinsics, (size_t)7 * p->n_cameras);
       appendN(sb, p->speed_biases, (size_t)9 * p->n_speed_biases);
       for (int k = 0; k < p->n_landmarks; ++k)
         appendN(lm, &p->landmarks[4 * (size_t)B.lm_perm[B.lm_base[w] + k]], 4);
@@ -1029,6 +1140,8 @@ struct okvisgpu_ctx {
       const okvisgpu_problem* p = probs[w];
       const int x = st.empty() ? 0 : st[w].xcur;
       std::memcpy(p->poses, &pose[x][7 * (size_t)B.pose_base[w]], sizeof(double) * 7 * p->n_poses);
+      if (B.win_ext_free[w])  // variable extrinsics are written back like every other block
+        std::memcpy(p->extrinsics, &pose[x][7 * ((size_t)B.pose_base[w] + p->n_poses)], sizeof(double) * 7 * p->n_cameras);
       std::memcpy(p->speed_biases, &sb[x][9 * (size_t)B.sb_base[w]], sizeof(double) * 9 * p->n_speed_biases);
       for (int k = 0; k < p->n_landmarks; ++k)
         std::memcpy(&p->landmarks[4 * (size_t)B.lm_perm[B.lm_base[w] + k]], &lm[x][4 * ((size_t)B.lm_base[w] + k)],
@@ -1206,10 +1319,10 @@ int okvisgpu_update_params(okvisgpu_ctx* c) {
 int okvisgpu_set_block_constant(okvisgpu_ctx* c, int32_t window, int32_t kind, int32_t index, int32_t is_const) {
   if (!c) return OKVISGPU_ERR_INVALID_ARGUMENT;
   if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
-  if (window < 0 || window >= (int)c->probs.size() || kind < 0 || kind > 2)
+  if (window < 0 || window >= (int)c->probs.size() || kind < 0 || kind > 3)
     return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "set_block_constant: bad window/kind");
   const okvisgpu_problem* p = c->probs[window];
-  const int n = kind == 0 ? p->n_poses : kind == 1 ? p->n_speed_biases : p->n_landmarks;
+  const int n = kind == 0 ? p->n_poses : kind == 1 ? p->n_speed_biases : kind == 2 ? p->n_landmarks : p->n_cameras;
   if (index < 0 || index >= n) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "set_block_constant: bad index");
   c->constOverride[std::make_tuple(window, kind, index)] = is_const ? 1 : 0;
   c->structureDirty = true;
@@ -1545,6 +1658,10 @@ int okvisgpu_get_stats(okvisgpu_ctx* c, okvisgpu_problem_stats* st) {
   st->n_poses = P.n_pose;
   st->n_speed_biases = P.n_sb;
   st->n_landmarks = P.n_lm;
+  for (int w = 0; w < B.n_win; ++w) {
+    const okvisgpu_problem* p = B.probs[w];
+    for (int c = 0; c < p->n_cameras; ++c) st->n_extrinsics_free += B.pose_f[B.pose_base[w] + p->n_poses + c] >= 0;
+  }
   for (uint8_t f : B.lm_free) st->n_landmarks_free += f != 0;
   st->n_observations = P.n_obs;
   st->n_visits = P.n_visit;

@@ -34,6 +34,10 @@ struct okvisgpu_synth_window {
   std::vector<int32_t> rp_blocks;
   std::vector<double> rp_dx, rp_J, rp_lin;
   std::vector<uint8_t> rp_kind;
+  std::vector<double> extr0, gt_extr;     // initial / true T_SC (online calibration windows)
+  std::vector<uint8_t> extr_const;
+  std::vector<int32_t> ep_cam;
+  std::vector<double> ep_meas, ep_L;
 };
 
 namespace {
@@ -92,6 +96,9 @@ void okvisgpu_synth_default_config(okvisgpu_synth_config* c, int32_t n_kf, int32
   c->n_relpose = 0;
   c->relpose_stride = 5;
   c->relpose_kind = 0;
+  c->do_extrinsics = 0;
+  c->extrinsics_sigma_r = 0.001;      // config/hilti22/okvis2.yaml:84-85
+  c->extrinsics_sigma_alpha = 0.005;
 }
 
 int okvisgpu_synth_create(const okvisgpu_synth_config* cfg, okvisgpu_synth_window** out) {
@@ -461,6 +468,30 @@ int okvisgpu_synth_create(const okvisgpu_synth_config* cfg, okvisgpu_synth_windo
     }
   }
 
+  // ---------------- online extrinsics calibration (do_extrinsics: true, ViGraph.cpp:372-382): the
+  // calibration the window starts from is the true T_SC perturbed at the prior's sigmas, and the
+  // prior PoseError(T_SC_init, sigma_r^2, sigma_alpha^2) is centred on it. Own random stream, so
+  // windows without online calibration are unchanged.
+  W->gt_extr = W->extr;
+  W->extr_const.assign(2, 1);
+  if (cfg->do_extrinsics) {
+    std::mt19937_64 rng3(cfg->seed ^ 0xC2B2AE3D27D4EB4Full);
+    std::normal_distribution<double> G(0.0, 1.0);
+    const double sr = cfg->extrinsics_sigma_r, sa = cfg->extrinsics_sigma_alpha;
+    for (int c = 0; c < 2; ++c) {
+      double* e = &W->extr[7 * c];
+      for (int i = 0; i < 3; ++i) e[i] += sr * G(rng3);
+      const Q q = okg::qnormalize(okg::qmul(okg::deltaQ(sa * G(rng3), sa * G(rng3), sa * G(rng3)), Q{e[3], e[4], e[5], e[6]}));
+      e[3] = q.x; e[4] = q.y; e[5] = q.z; e[6] = q.w;
+      W->extr_const[c] = 0;
+      W->ep_cam.push_back(c);
+      W->ep_meas.insert(W->ep_meas.end(), e, e + 7);
+      for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) W->ep_L.push_back(i != j ? 0.0 : 1.0 / (i < 3 ? sr : sa));  // PoseError.cpp:41-66
+    }
+  }
+  W->extr0 = W->extr;
+
   // ---------------- problem view
   okvisgpu_problem& P = W->prob;
   std::memset(&P, 0, sizeof(P));
@@ -506,6 +537,11 @@ int okvisgpu_synth_create(const okvisgpu_synth_config* cfg, okvisgpu_synth_windo
   P.relpose_sqrt_info = W->rp_J.data();
   P.relpose_lin_point = W->rp_lin.data();
   P.relpose_kind = W->rp_kind.data();
+  P.extrinsics_constant = W->extr_const.data();
+  P.n_extrinsics_priors = (int32_t)W->ep_cam.size();
+  P.extrinsics_prior_camera = W->ep_cam.data();
+  P.extrinsics_prior_meas = W->ep_meas.data();
+  P.extrinsics_prior_sqrt_info = W->ep_L.data();
   *out = W;
   return OKVISGPU_OK;
 }
@@ -521,11 +557,19 @@ int okvisgpu_synth_ground_truth(const okvisgpu_synth_window* w, double* poses, d
   return OKVISGPU_OK;
 }
 
+int okvisgpu_synth_true_extrinsics(const okvisgpu_synth_window* w, double* extrinsics) {
+  if (!w || !extrinsics) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  std::memcpy(extrinsics, w->gt_extr.data(), sizeof(double) * w->gt_extr.size());
+  return OKVISGPU_OK;
+}
+
 int okvisgpu_synth_reset(okvisgpu_synth_window* w) {
   if (!w) return OKVISGPU_ERR_INVALID_ARGUMENT;
   w->poses = w->poses0;
   w->sbs = w->sbs0;
   w->lms = w->lms0;
+  w->extr = w->extr0;
+  w->prob.extrinsics = w->extr.data();
   std::fill(w->imu_state.begin(), w->imu_state.end(), 0.0);
   w->prob.poses = w->poses.data();
   w->prob.speed_biases = w->sbs.data();

@@ -96,7 +96,8 @@ class SynthConfig(C.Structure):
                 ("max_obs_per_landmark", C.c_int32), ("kf_dt_s", C.c_double), ("imu_rate_hz", C.c_double),
                 ("pixel_noise", C.c_double), ("init_sigma_pos", C.c_double), ("init_sigma_rot", C.c_double),
                 ("init_sigma_lm", C.c_double), ("init_sigma_vel", C.c_double), ("seed", C.c_uint64),
-                ("n_relpose", C.c_int32), ("relpose_stride", C.c_int32), ("relpose_kind", C.c_int32)]
+                ("n_relpose", C.c_int32), ("relpose_stride", C.c_int32), ("relpose_kind", C.c_int32),
+                ("do_extrinsics", C.c_int32), ("extrinsics_sigma_r", C.c_double), ("extrinsics_sigma_alpha", C.c_double)]
 
 
 class ProblemStats(C.Structure):
@@ -129,7 +130,7 @@ EXPORTED_SYMBOLS = [
     "okvisgpu_profile_iteration", "okvisgpu_phase_name", "okvisgpu_kernel_count", "okvisgpu_kernel_name",
     "okvisgpu_time_kernel", "okvisgpu_eval_relpose", "okvisgpu_twopose_compute",
     "okvisgpu_graph_load", "okvisgpu_graph_problem", "okvisgpu_graph_ids", "okvisgpu_graph_destroy",
-    "okvisgpu_graph_save", "okvisgpu_get_stats",
+    "okvisgpu_graph_save", "okvisgpu_get_stats", "okvisgpu_synth_true_extrinsics",
 ]
 N_PHASES = 15
 
@@ -165,6 +166,7 @@ def lib():
         L.okvisgpu_synth_problem.restype = C.POINTER(Problem)
         L.okvisgpu_synth_ground_truth.argtypes = [C.c_void_p, _dp, _dp, _dp]
         L.okvisgpu_synth_reset.argtypes = [C.c_void_p]
+        L.okvisgpu_synth_true_extrinsics.argtypes = [C.c_void_p, _dp]
         L.okvisgpu_synth_destroy.argtypes = [C.c_void_p]
         L.okvisgpu_solve_begin.argtypes = [C.c_void_p, C.POINTER(Options)]
         L.okvisgpu_solve_iterate.argtypes = [C.c_void_p, C.c_int32]
@@ -240,6 +242,15 @@ class SynthWindow:
         sbs = np.zeros((p.n_speed_biases, 9))
         lib().okvisgpu_synth_ground_truth(self.handle, dptr(poses), dptr(lms), dptr(sbs))
         return poses, lms, sbs
+
+    def true_extrinsics(self):
+        e = np.zeros((self.problem.n_cameras, 7))
+        lib().okvisgpu_synth_true_extrinsics(self.handle, dptr(e))
+        return e
+
+    def extrinsics(self):
+        p = self.problem
+        return np.ctypeslib.as_array(p.extrinsics, shape=(p.n_cameras, 7))
 
     # views into the (mutable) parameter arrays
     def poses(self):

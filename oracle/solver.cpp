@@ -26,8 +26,8 @@
 namespace oracle {
 namespace {
 
-enum Kind { kPose = 0, kSb = 1, kLm = 2 };
-enum RKind { rReproj = 0, rImu = 1, rPosePrior = 2, rSbPrior = 3, rRelPose = 4 };
+enum Kind { kPose = 0, kSb = 1, kLm = 2, kExt = 3 };  // kExt: extrinsics T_SC (PoseParameterBlock + PoseManifold)
+enum RKind { rReproj = 0, rImu = 1, rPosePrior = 2, rSbPrior = 3, rRelPose = 4, rExtPrior = 5 };
 
 struct PBlock {
   int kind, index;
@@ -55,7 +55,7 @@ struct Program {
   std::vector<RBlock> rbs;
   std::vector<Camera> cams;
   std::vector<ImuError> imus;
-  int poseBase, sbBase, lmBase;
+  int poseBase, sbBase, lmBase, extBase;
   int nx = 0, nt = 0, nres = 0, njac = 0;
   int ne = 0;                    // number of active e-blocks (landmarks)
   int eTangent = 0;              // tangent size of all e-blocks (they come first)
@@ -86,6 +86,11 @@ void buildProgram(const okvisgpu_problem* p, Program& P, bool loadImuState) {
     P.pbs.push_back(PBlock{kSb, i, 9, 9, p->speed_bias_constant ? p->speed_bias_constant[i] != 0 : false});
   for (int i = 0; i < p->n_landmarks; ++i)
     P.pbs.push_back(PBlock{kLm, i, 4, 3, p->landmark_constant ? p->landmark_constant[i] != 0 : false});
+  // one extrinsics block per camera, shared by all states (ViGraph.cpp:330-336,469-473); constant
+  // unless online calibration (ViGraph.cpp:372-386)
+  P.extBase = (int)P.pbs.size();
+  for (int c = 0; c < p->n_cameras; ++c)
+    P.pbs.push_back(PBlock{kExt, c, 7, 6, p->extrinsics_constant ? p->extrinsics_constant[c] != 0 : true});
   for (int c = 0; c < p->n_cameras; ++c) {
     const okvisgpu_camera& k = p->cameras[c];
     P.cams.push_back(cameraOf(k));
@@ -97,7 +102,7 @@ void buildProgram(const okvisgpu_problem* p, Program& P, bool loadImuState) {
     P.rbs.push_back(r);
   };
   for (int o = 0; o < p->n_observations; ++o)
-    addR(rReproj, o, 2, {P.poseBase + p->obs_pose[o], P.lmBase + p->obs_landmark[o]});
+    addR(rReproj, o, 2, {P.poseBase + p->obs_pose[o], P.lmBase + p->obs_landmark[o], P.extBase + p->obs_camera[o]});
   for (int f = 0; f < p->n_imu; ++f) {
     const int* b = &p->imu_blocks[4 * f];
     addR(rImu, f, 15, {P.poseBase + b[0], P.sbBase + b[1], P.poseBase + b[2], P.sbBase + b[3]});
@@ -121,6 +126,8 @@ void buildProgram(const okvisgpu_problem* p, Program& P, bool loadImuState) {
   for (int i = 0; i < p->n_sb_priors; ++i) addR(rSbPrior, i, 9, {P.sbBase + p->sb_prior_block[i]});
   for (int i = 0; i < p->n_relpose; ++i)
     addR(rRelPose, i, 6, {P.poseBase + p->relpose_blocks[2 * i], P.poseBase + p->relpose_blocks[2 * i + 1]});
+  for (int i = 0; i < p->n_extrinsics_priors; ++i)  // PoseError on T_SC (ViGraph.cpp:372-382)
+    addR(rExtPrior, i, 6, {P.extBase + p->extrinsics_prior_camera[i]});
 
   // Active blocks (Ceres Program::RemoveFixedBlocks: unused or constant blocks removed).
   for (RBlock& r : P.rbs) {
@@ -162,6 +169,17 @@ void buildProgram(const okvisgpu_problem* p, Program& P, bool loadImuState) {
       fo += b.loc;
     }
   }
+  // variable extrinsics after all states (the reduced ordering of the GPU path: band + border)
+  for (int c = 0; c < p->n_cameras; ++c) {
+    const int id = P.extBase + c;
+    PBlock& b = P.pbs[id];
+    if (!b.active) continue;
+    b.xoff = xo; b.toff = to;
+    xo += b.amb; to += b.loc;
+    P.fblocks.push_back(id);
+    P.fOffset[id] = fo;
+    fo += b.loc;
+  }
   P.fdim = fo;
   P.nx = xo;
   P.nt = to;
@@ -173,6 +191,7 @@ void buildProgram(const okvisgpu_problem* p, Program& P, bool loadImuState) {
     P.constOff[id] = (int)P.constVals.size();
     const double* src = b.kind == kPose ? &p->poses[7 * b.index]
                         : b.kind == kSb ? &p->speed_biases[9 * b.index]
+                        : b.kind == kExt ? &p->extrinsics[7 * b.index]
                                         : &p->landmarks[4 * b.index];
     for (int k = 0; k < b.amb; ++k) P.constVals.push_back(src[k]);
   }
@@ -208,6 +227,7 @@ void gatherX(const Program& P, std::vector<double>& x) {
     if (!b.active) continue;
     const double* src = b.kind == kPose ? &p->poses[7 * b.index]
                         : b.kind == kSb ? &p->speed_biases[9 * b.index]
+                        : b.kind == kExt ? &p->extrinsics[7 * b.index]
                                         : &p->landmarks[4 * b.index];
     for (int k = 0; k < b.amb; ++k) x[b.xoff + k] = src[k];
   }
@@ -218,6 +238,7 @@ void scatterX(const Program& P, const std::vector<double>& x) {
     if (!b.active) continue;
     double* dst = b.kind == kPose ? &p->poses[7 * b.index]
                   : b.kind == kSb ? &p->speed_biases[9 * b.index]
+                  : b.kind == kExt ? &p->extrinsics[7 * b.index]
                                   : &p->landmarks[4 * b.index];
     for (int k = 0; k < b.amb; ++k) dst[k] = x[b.xoff + k];
   }
@@ -228,7 +249,7 @@ void plusAll(const Program& P, const std::vector<double>& x, const double* delta
   out.resize(P.nx);
   for (const PBlock& b : P.pbs) {
     if (!b.active) continue;
-    if (b.kind == kPose) posePlus(&x[b.xoff], &delta[b.toff], &out[b.xoff]);
+    if (b.kind == kPose || b.kind == kExt) posePlus(&x[b.xoff], &delta[b.toff], &out[b.xoff]);
     else if (b.kind == kLm) pointPlus(&x[b.xoff], &delta[b.toff], &out[b.xoff]);
     else for (int k = 0; k < 9; ++k) out[b.xoff + k] = x[b.xoff + k] + delta[b.toff + k];
   }
@@ -335,7 +356,7 @@ double evalResidual(Program& P, const std::vector<double>& x, int ri, double* re
       const int o = r.index;
       const int cam = p->obs_camera[o];
       reprojectionEvaluate(P.cams[cam], &p->obs_keypoint[2 * o], &p->obs_sqrt_info[4 * o], prm[0], prm[1],
-                           &p->extrinsics[7 * cam], rr, ja[0], ja[1], nullptr, nullptr, nullptr, nullptr);
+                           prm[2], rr, ja[0], ja[1], ja[2], nullptr, nullptr, nullptr);
       useLoss = p->obs_cauchy ? p->obs_cauchy[o] != 0 : true;
       break;
     }
@@ -350,6 +371,10 @@ double evalResidual(Program& P, const std::vector<double>& x, int ri, double* re
       break;
     case rSbPrior:
       sbErrorEvaluate(&p->sb_prior_meas[9 * r.index], &p->sb_prior_sqrt_info[81 * r.index], prm[0], rr, ja[0]);
+      break;
+    case rExtPrior:
+      poseErrorEvaluate(&p->extrinsics_prior_meas[7 * r.index], &p->extrinsics_prior_sqrt_info[36 * r.index], prm[0],
+                        rr, ja[0], nullptr);
       break;
     case rRelPose:  // no loss function (ViGraphEstimator.cpp:770, ViGraph.cpp:801)
       relPoseBlockEvaluate(p, r.index, prm[0], prm[1], rr, nullptr, nullptr, ja[0], ja[1]);
@@ -375,7 +400,7 @@ double evalResidual(Program& P, const std::vector<double>& x, int ri, double* re
     for (int k = 0; k < r.npb; ++k) {
       const PBlock& b = P.pbs[r.pb[k]];
       if (!b.active) continue;
-      if (b.kind == kPose) {
+      if (b.kind == kPose || b.kind == kExt) {
         double Jp[42];
         posePlusJacobian(prm[k], Jp);
         for (int i = 0; i < r.nres; ++i)
@@ -661,7 +686,10 @@ void buildReduced(const Program& P, const Linearization& L, const double* D, Red
   // over owners of f-block rows): every lhs / rhs row is accumulated by one thread, landmark by
   // landmark in e order, so the result does not depend on the thread count.
   struct FAcc { int fid; int foff; int loc; double W[27]; double H[81]; double g[9]; };
-  struct Chunk { std::vector<FAcc> f; double z[3]; };
+  // F^T F between two different f-blocks of one row (a reprojection error with variable
+  // extrinsics touches the pose and the extrinsics: SchurEliminator's EBlockRowOuterProduct)
+  struct Cross { int fa, fc; int la, lc; double H[81]; };
+  struct Chunk { std::vector<FAcc> f; std::vector<Cross> x; double z[3]; };
   std::vector<Chunk> chunks(P.ne);
   std::vector<int> failed(P.ne, 0);
   parallelFor(P.ne, nthreads, [&](int e) {
@@ -711,6 +739,23 @@ void buildReduced(const Program& P, const Linearization& L, const double* D, Red
             a->H[u * pb.loc + v] += s;
           }
         }
+        // F^T F with the row's other f-blocks
+        forEachJacBlock(P, ri, [&](const PBlock& pc, int col2) {
+          if (&pc == &eb || &pc == &pb) return;
+          const int id2 = (int)(&pc - &P.pbs[0]);
+          Cross* x = nullptr;
+          for (auto& y : chunks[e].x) if (y.fa == id && y.fc == id2) x = &y;
+          if (!x) {
+            chunks[e].x.push_back(Cross{id, id2, pb.loc, pc.loc, {0}});
+            x = &chunks[e].x.back();
+          }
+          for (int u = 0; u < pb.loc; ++u)
+            for (int v = 0; v < pc.loc; ++v) {
+              double s = 0;
+              for (int i = 0; i < r.nres; ++i) s += J[i * r.jcols + col + u] * J[i * r.jcols + col2 + v];
+              x->H[u * pc.loc + v] += s;
+            }
+        });
       });
     }
     if (D)
@@ -732,6 +777,12 @@ void buildReduced(const Program& P, const Linearization& L, const double* D, Red
     for (int e = 0; e < P.ne; ++e) {
       const Chunk& c = chunks[e];
       const double* inv = &R.einv[(size_t)e * 9];
+      for (const Cross& x : c.x) {
+        if (ownerOf[x.fa] != t) continue;
+        const int fa = P.fOffset[x.fa], fc = P.fOffset[x.fc];
+        for (int u = 0; u < x.la; ++u)
+          for (int v = 0; v < x.lc; ++v) R.lhs[(size_t)(fa + u) * fd + fc + v] += x.H[u * x.lc + v];
+      }
       for (const FAcc& a : c.f) {
         if (ownerOf[a.fid] != t) continue;
         for (int u = 0; u < a.loc; ++u) {
@@ -1166,14 +1217,13 @@ int oracle_check_jacobians(const okvisgpu_problem* p, int32_t kind, int32_t inde
   std::vector<std::vector<double>> blocks;
   std::vector<int> kinds;
   Camera cam{};
-  const double* extr = nullptr;
   int nres = 0;
   if (kind == 0) {
     blocks.push_back(std::vector<double>(&p->poses[7 * p->obs_pose[index]], &p->poses[7 * p->obs_pose[index]] + 7));
     blocks.push_back(std::vector<double>(&p->landmarks[4 * p->obs_landmark[index]], &p->landmarks[4 * p->obs_landmark[index]] + 4));
-    kinds = {kPose, kLm};
+    blocks.push_back(std::vector<double>(&p->extrinsics[7 * p->obs_camera[index]], &p->extrinsics[7 * p->obs_camera[index]] + 7));
+    kinds = {kPose, kLm, kPose};
     cam = P.cams[p->obs_camera[index]];
-    extr = &p->extrinsics[7 * p->obs_camera[index]];
     nres = 2;
   } else if (kind == 1) {
     const int* b = &p->imu_blocks[4 * index];
@@ -1203,8 +1253,9 @@ int oracle_check_jacobians(const okvisgpu_problem* p, int32_t kind, int32_t inde
     const double* prm[4];
     for (int i = 0; i < nb; ++i) prm[i] = bl[i].data();
     if (kind == 0) {
-      reprojectionEvaluate(cam, &p->obs_keypoint[2 * index], &p->obs_sqrt_info[4 * index], prm[0], prm[1], extr, r,
-                           nullptr, nullptr, nullptr, jmin ? jmin[0] : nullptr, jmin ? jmin[1] : nullptr, nullptr);
+      reprojectionEvaluate(cam, &p->obs_keypoint[2 * index], &p->obs_sqrt_info[4 * index], prm[0], prm[1], prm[2], r,
+                           nullptr, nullptr, nullptr, jmin ? jmin[0] : nullptr, jmin ? jmin[1] : nullptr,
+                           jmin ? jmin[2] : nullptr);
     } else if (kind == 1) {
       P.imus[index].evaluate(prm, r, nullptr, jmin, false);
     } else if (kind == 2) {
