@@ -95,8 +95,10 @@ typedef struct okvisgpu_imu_params { /* okvis::ImuParameters subset, okvis_commo
  *  [27..29]  acc_doubleintegral       [30..38]  dalpha_db_g
  *  [39..47]  dv_db_g                  [48..56]  dp_db_g
  *  [57..65]  speedAndBiases_ref_ (9)  [66..290] squareRootInformation_ (15x15 row-major)
- *  [291]     steps integrated by the last redo (informational)                               */
-#define OKVISGPU_IMU_STATE_DOUBLES 292
+ *  [291]     steps integrated by the last redo (informational)
+ *  [292..300] cross_ (row-major)       [301..525] P_delta_ (15x15, symmetric): what
+ *            ImuError::append continues from (ABI 4)                                          */
+#define OKVISGPU_IMU_STATE_DOUBLES 526
 
 typedef struct okvisgpu_problem {
   /* --- parameter blocks (written back in place by okvisgpu_solve / okvisgpu_get_params) */
@@ -313,6 +315,30 @@ typedef struct okvisgpu_twopose_edges {
  * stream; independent of the problem set with okvisgpu_set_problems. */
 int okvisgpu_twopose_compute(okvisgpu_ctx* ctx, const okvisgpu_twopose_edges* edges, double* delta_x,
                              double* sqrt_info, double* lin_point, double* H00, double* b0);
+
+/* ---------------------------------------------------------------- IMU-merge elimination
+ * ImuError::append (ImuError.cpp:63-255) for a batch of factors on the GPU: the step of
+ * ViGraphEstimator::eliminateStateByImuMerge (ViGraphEstimator.cpp:38-171) that extends the IMU
+ * link into an eliminated state k with the link out of it. Per factor: `state` is the link's
+ * preintegration state (OKVISGPU_IMU_STATE_DOUBLES layout, e.g. written back by a solve), t1_old its
+ * t1, t1_new the next link's t1, speed_biases the estimate of state k (the bias the appended part
+ * is integrated with), and the samples the next link's imuMeasurements(). On return `state` holds the
+ * merged link's state (t0 unchanged, t1 = t1_new; redo counter, redo flag and speedAndBiases_ref_
+ * unchanged, as in the reference) and steps[i] the integrated steps (-1: the samples do not reach
+ * t1_new, state untouched). The merged factor's samples are the link's followed by the appended ones
+ * newer than its last (ImuError.cpp:74-81); the caller rebuilds its problem with them. */
+typedef struct okvisgpu_imu_append_batch {
+  int32_t n;
+  okvisgpu_imu_params imu_params;
+  double* state;                    /* [n][OKVISGPU_IMU_STATE_DOUBLES] in/out                     */
+  const int64_t* t1_old_ns;         /* [n]                                                         */
+  const int64_t* t1_new_ns;         /* [n]                                                         */
+  const double* speed_biases;       /* [n][9]                                                      */
+  const int32_t* sample_begin;      /* [n+1] CSR of the appended samples                           */
+  const int64_t* sample_t_ns;       /* [n_samples]                                                 */
+  const double* sample_gyr_acc;     /* [n_samples][6]                                              */
+} okvisgpu_imu_append_batch;
+int okvisgpu_imu_append(okvisgpu_ctx* ctx, const okvisgpu_imu_append_batch* batch, int32_t* steps);
 
 /* ---------------------------------------------------------------- okvis Component graphs
  * Component::load (okvis_ceres/src/Component.cpp:50-383) as an okvisgpu_problem: states (pose and

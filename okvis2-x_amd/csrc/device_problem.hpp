@@ -20,7 +20,7 @@ namespace okg {
 constexpr int kCamDoubles = 13;       // per camera on the device: dist, fu, fv, cu, cv, 8 distortion parameters
 constexpr int kTile = 64;             // Cholesky tile (one 64x64 FP64 tile = 32 KiB of LDS)
 constexpr int kImuLin = 15 + 15 * 30; // per-IMU-factor linearisation record: r[15], J[15][30]
-constexpr int kImuState = 292;        // == OKVISGPU_IMU_STATE_DOUBLES
+constexpr int kImuState = 526;        // == OKVISGPU_IMU_STATE_DOUBLES
 
 // Linearisation record per observation (structure of arrays, plane-major):
 //   plane 0-1: r (Cauchy-corrected)   plane 2-13: J_pose 2x6   plane 14-19: J_lm 2x3

@@ -281,6 +281,11 @@ __device__ void groupJacobi(double* A, double* V, double* rot, int l, bool need)
 #ifndef OKG_IMU_OCC
 #define OKG_IMU_OCC 1
 #endif
+// APPEND: ImuError::append (ImuError.cpp:63-255) for a batch of factors (okvisgpu_imu_append): the
+// chain starts from the stored state (Delta_q, integrals, cross_, dv_db_g, P) at imu_t0 (= the old
+// t1), integrates the appended samples with the eliminated state's bias (sb[0] row blk[1]) up to
+// imu_t1, and writes the state and the new square-root information; no residual.
+template <bool APPEND>
 __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* __restrict__ Pp, int mode) {
   const DevProblem& P = *Pp;
   const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
@@ -297,17 +302,14 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
 
   int w = 0, xs = 0, lb = 0;
   bool live = f < P.n_imu;
-  if (live) {
+  if (live && !APPEND) {
     w = P.imu_win[f];
     live = evalSelect(P, w, mode, xs, lb) && !((P.imu_flags[f] & 2) && mode < 2);
   }
   const int fs = live ? f : 0;  // safe index for idle groups
 
   const int* blk = P.imu_blocks + 4 * fs;
-  const double* p0 = P.pose[xs] + 7 * (size_t)blk[0];
   const double* sb0 = P.sb[xs] + 9 * (size_t)blk[1];
-  const double* p1 = P.pose[xs] + 7 * (size_t)blk[2];
-  const double* sb1 = P.sb[xs] + 9 * (size_t)blk[3];
   double* state = P.imu_state + (size_t)fs * kImuState;
   const double* par = P.imu_par + 7 * w;
   const double a_max = par[0], g_max = par[1], sg_c = par[2], sa_c = par[3], sgw_c = par[4], saw_c = par[5],
@@ -321,12 +323,13 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   double Db[6];
   for (int k = 0; k < 6; ++k) Db[k] = sb0[3 + k] - state[57 + 3 + k];
   redo = redo || (sqrt(Db[0] * Db[0] + Db[1] * Db[1] + Db[2] * Db[2]) > 0.0003);
-  const bool doRedo = (redo && ((send - sbeg) < 50 || P.opt.redo_propagation_always)) || redoCounter == 0;
+  const bool doRedo =
+      APPEND || (redo && ((send - sbeg) < 50 || P.opt.redo_propagation_always)) || redoCounter == 0;
   // redoPreintegration returns -1 before touching any state when the samples do not cover t1
   // (ImuError.cpp:270-273): the old preintegration is kept.
   const bool covered = (send > sbeg) && P.imu_ts[send - 1] >= t1;
   const bool integrate = live && doRedo && covered;
-  if (live && doRedo) {
+  if (live && doRedo && !APPEND) {
     redoCounter++;
     for (int k = 0; k < 6; ++k) Db[k] = 0.0;
     redo = false;
@@ -342,6 +345,23 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   double Pc[15];  // column l of P
   for (int i = 0; i < 15; ++i) Pc[i] = 0.0;
   int steps = 0;
+  if (APPEND && integrate) {  // continue the chain of the stored preintegration
+    cdq = Q{state[2], state[3], state[4], state[5]};
+    for (int i = 0; i < 9; ++i) {
+      cCi[i] = state[6 + i];
+      cdvdbg[i] = state[39 + i];
+      cross[i] = state[292 + i];
+    }
+    for (int i = 0; i < 3; ++i) cai[i] = state[24 + i];
+    if (l < 9) {
+      aCdi = state[15 + l];
+      adadbg = state[30 + l];
+      adpdbg = state[48 + l];
+    }
+    if (l < 3) aadi = state[27 + l];
+    if (l < 15)
+      for (int i = 0; i < 15; ++i) Pc[i] = state[301 + i * 15 + l];
+  }
 
   // ---- redoPreintegration (ImuError.cpp:258-466), uniform trip count over the wavefront.
   // What a step needs that does not depend on the integration chain (its length, the interpolated
@@ -358,6 +378,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
     Nmax = max(Nmax, __shfl_xor(Nmax, 32, 64));
     bool started = false;                       // hasStarted: an earlier step was integrated
     double C[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};  // R(cdq), carried from step to step
+    if (APPEND) qrot(cdq, C);
     double* rec = sStep[g];
     for (int c0 = 0; c0 < Nmax; c0 += kImuGroup) {
       {
@@ -534,7 +555,8 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
       for (int i = 0; i < 9; ++i) {
         state[6 + i] = cCi[i];
         state[39 + i] = cdvdbg[i];
-        state[57 + i] = sb0[i];
+        state[292 + i] = cross[i];
+        if (!APPEND) state[57 + i] = sb0[i];  // append keeps speedAndBiases_ref_
       }
       for (int i = 0; i < 3; ++i) state[24 + i] = cai[i];
       state[291] = (double)steps;
@@ -557,6 +579,8 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   if (integrate) {
     for (int i = 0; i < 15; ++i) Pc[i] = (l < 15) ? 0.5 * Pc[i] + 0.5 * sB[i * 16 + l] : 0.0;
     for (int i = 0; i < 16; ++i) sA[l * 16 + i] = (i < 15) ? Pc[i] : 0.0;
+    if (l < 15)  // P_delta_ (symmetrised), kept for a later append
+      for (int i = 0; i < 15; ++i) state[301 + i * 15 + l] = Pc[i];
     for (int i = 0; i < 15; ++i) trace += (i == l) ? Pc[i] : 0.0;
   }
   trace = groupSum(trace);
@@ -627,6 +651,10 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
     for (int e = l; e < 225; e += kImuGroup) sA[(e / 15) * 16 + e % 15] = state[66 + e];
   }
   __syncthreads();  // state writes of the group visible to all its lanes
+  if (APPEND) return;  // uniform over the workgroup
+  const double* p0 = P.pose[xs] + 7 * (size_t)blk[0];
+  const double* p1 = P.pose[xs] + 7 * (size_t)blk[2];
+  const double* sb1 = P.sb[xs] + 9 * (size_t)blk[3];
   ImuPre pre;
   loadPre(state, pre);
   const bool success = live && (!integrate || steps > 0);
@@ -931,7 +959,8 @@ void launch_eval_obs(const DevProblem& P, int mode, hipStream_t s) {
   if (P.n_obs > 0) hipLaunchKernelGGL(k_eval_obs, dim3((P.n_obs + 255) / 256), dim3(256), 0, s, P.self, mode);
 }
 void launch_eval_imu(const DevProblem& P, int mode, hipStream_t s) {
-  if (P.n_imu > 0) hipLaunchKernelGGL(k_eval_imu, dim3((P.n_imu + kImuPerWG - 1) / kImuPerWG), dim3(64), 0, s, P.self, mode);
+  if (P.n_imu > 0)
+    hipLaunchKernelGGL(k_eval_imu<false>, dim3((P.n_imu + kImuPerWG - 1) / kImuPerWG), dim3(64), 0, s, P.self, mode);
 }
 void launch_eval_priors(const DevProblem& P, int mode, hipStream_t s) {
   const int np = P.n_pprior + P.n_sbprior + P.n_relpose;
@@ -941,6 +970,11 @@ void launch_eval(const DevProblem& P, int mode, hipStream_t s) {
   launch_eval_obs(P, mode, s);
   launch_eval_imu(P, mode, s);
   launch_eval_priors(P, mode, s);
+}
+
+void launch_imu_append(const DevProblem& P, hipStream_t s) {
+  if (P.n_imu > 0)
+    hipLaunchKernelGGL(k_eval_imu<true>, dim3((P.n_imu + kImuPerWG - 1) / kImuPerWG), dim3(64), 0, s, P.self, 0);
 }
 
 }  // namespace okg

@@ -1815,6 +1815,72 @@ int okvisgpu_eval_relpose(okvisgpu_ctx* c, int32_t window, double* r, double* J)
   });
 }
 
+int okvisgpu_imu_append(okvisgpu_ctx* c, const okvisgpu_imu_append_batch* A, int32_t* steps) {
+  if (!c || !A || A->n < 0) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "imu_append: bad arguments");
+  if (A->n == 0) return OKVISGPU_OK;
+  if (!A->state || !A->t1_old_ns || !A->t1_new_ns || !A->speed_biases || !A->sample_begin)
+    return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "imu_append: missing arrays");
+  return guarded(c, [&]() {
+    HIPCHK(hipSetDevice(c->device));
+    const int n = A->n;
+    if (A->sample_begin[0] != 0) throw ArgError{"imu_append: sample_begin must start at 0"};
+    for (int i = 0; i < n; ++i)
+      if (A->sample_begin[i + 1] < A->sample_begin[i]) throw ArgError{"imu_append: sample_begin not monotone"};
+    const int ns = A->sample_begin[n];
+    if (ns && (!A->sample_t_ns || !A->sample_gyr_acc)) throw ArgError{"imu_append: sample arrays missing"};
+    std::vector<int32_t> blk(4 * (size_t)n);
+    for (int i = 0; i < n; ++i) { blk[4 * i] = 0; blk[4 * i + 1] = i; blk[4 * i + 2] = 0; blk[4 * i + 3] = i; }
+    const okvisgpu_imu_params& ip = A->imu_params;
+    const double par[7] = {ip.a_max, ip.g_max, ip.sigma_g_c, ip.sigma_a_c, ip.sigma_gw_c, ip.sigma_aw_c, ip.g};
+    Arena M;
+    const size_t o_blk = M.reserve(blk.size() * 4), o_t0 = M.reserve(8 * (size_t)n), o_t1 = M.reserve(8 * (size_t)n),
+                 o_sb = M.reserve(4 * (size_t)(n + 1)), o_ts = M.reserve(8 * (size_t)std::max(1, ns)),
+                 o_ga = M.reserve(48 * (size_t)std::max(1, ns)), o_par = M.reserve(sizeof(par)),
+                 o_st = M.reserve(sizeof(double) * kImuState * n), o_bias = M.reserve(72 * (size_t)n),
+                 o_self = M.reserve(sizeof(DevProblem));
+    char* base = nullptr;
+    HIPCHK(hipMalloc(&base, M.size));
+    std::unique_ptr<char, void (*)(char*)> guard(base, [](char* p) { (void)hipFree(p); });
+    auto up = [&](size_t off, const void* src, size_t bytes) {
+      if (bytes) HIPCHK(hipMemcpyAsync(base + off, src, bytes, hipMemcpyHostToDevice, c->stream));
+    };
+    up(o_blk, blk.data(), blk.size() * 4);
+    up(o_t0, A->t1_old_ns, 8 * (size_t)n);
+    up(o_t1, A->t1_new_ns, 8 * (size_t)n);
+    up(o_sb, A->sample_begin, 4 * (size_t)(n + 1));
+    up(o_ts, A->sample_t_ns, 8 * (size_t)ns);
+    up(o_ga, A->sample_gyr_acc, 48 * (size_t)ns);
+    up(o_par, par, sizeof(par));
+    up(o_st, A->state, sizeof(double) * kImuState * n);
+    up(o_bias, A->speed_biases, 72 * (size_t)n);
+    // a descriptor holding only what the append mode of k_eval_imu reads
+    DevProblem D{};
+    D.n_imu = n;
+    D.imu_blocks = reinterpret_cast<const int32_t*>(base + o_blk);
+    D.imu_t0 = reinterpret_cast<const int64_t*>(base + o_t0);
+    D.imu_t1 = reinterpret_cast<const int64_t*>(base + o_t1);
+    D.imu_sbegin = reinterpret_cast<const int32_t*>(base + o_sb);
+    D.imu_ts = reinterpret_cast<const int64_t*>(base + o_ts);
+    D.imu_ga = reinterpret_cast<const double*>(base + o_ga);
+    D.imu_par = reinterpret_cast<const double*>(base + o_par);
+    D.imu_state = reinterpret_cast<double*>(base + o_st);
+    D.sb[0] = D.sb[1] = reinterpret_cast<double*>(base + o_bias);
+    D.self = reinterpret_cast<const DevProblem*>(base + o_self);
+    up(o_self, &D, sizeof(D));
+    launch_imu_append(D, c->stream);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(A->state, D.imu_state, sizeof(double) * kImuState * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (steps)
+      for (int i = 0; i < n; ++i) {
+        const int s0 = A->sample_begin[i], s1 = A->sample_begin[i + 1];
+        const bool covered = s1 > s0 && A->sample_t_ns[s1 - 1] >= A->t1_new_ns[i];
+        steps[i] = covered ? (int32_t)A->state[(size_t)i * kImuState + 291] : -1;
+      }
+    return (int)OKVISGPU_OK;
+  });
+}
+
 int okvisgpu_twopose_compute(okvisgpu_ctx* c, const okvisgpu_twopose_edges* E, double* delta_x, double* sqrt_info,
                              double* lin_point, double* H00, double* b0) {
   if (!c || !E || E->n_edges < 0) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "twopose_compute: bad arguments");

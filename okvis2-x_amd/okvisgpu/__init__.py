@@ -18,7 +18,7 @@ PKG_ROOT = os.path.dirname(_HERE)
 REPO_ROOT = os.path.dirname(PKG_ROOT)
 LIB_PATH = os.environ.get("OKVISGPU_LIB") or os.path.join(PKG_ROOT, "libokvisgpu.so")  # env: A/B builds
 
-IMU_STATE_DOUBLES = 292
+IMU_STATE_DOUBLES = 526
 
 DIST_NONE, DIST_RADTAN, DIST_EQUIDISTANT, DIST_RADTAN8 = 0, 1, 2, 3
 DENSE_SCHUR, SPARSE_NORMAL_CHOLESKY = 0, 1
@@ -111,6 +111,11 @@ class ProblemStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved_"}
 
 
+class ImuAppendBatch(C.Structure):
+    _fields_ = [("n", C.c_int32), ("imu_params", ImuParams), ("state", _dp), ("t1_old_ns", _lp), ("t1_new_ns", _lp),
+                ("speed_biases", _dp), ("sample_begin", _ip), ("sample_t_ns", _lp), ("sample_gyr_acc", _dp)]
+
+
 class TwoPoseEdges(C.Structure):
     _fields_ = [("n_edges", C.c_int32), ("ref_pose", _dp), ("other_pose", _dp),
                 ("n_cameras", C.c_int32), ("cameras", C.POINTER(Camera)), ("extrinsics", _dp),
@@ -130,7 +135,7 @@ EXPORTED_SYMBOLS = [
     "okvisgpu_profile_iteration", "okvisgpu_phase_name", "okvisgpu_kernel_count", "okvisgpu_kernel_name",
     "okvisgpu_time_kernel", "okvisgpu_eval_relpose", "okvisgpu_twopose_compute",
     "okvisgpu_graph_load", "okvisgpu_graph_problem", "okvisgpu_graph_ids", "okvisgpu_graph_destroy",
-    "okvisgpu_graph_save", "okvisgpu_get_stats", "okvisgpu_synth_true_extrinsics",
+    "okvisgpu_graph_save", "okvisgpu_get_stats", "okvisgpu_synth_true_extrinsics", "okvisgpu_imu_append",
 ]
 N_PHASES = 15
 
@@ -188,6 +193,7 @@ def lib():
         L.okvisgpu_graph_destroy.argtypes = [C.c_void_p]
         L.okvisgpu_graph_save.argtypes = [C.POINTER(Problem), _lp, C.c_char_p]
         L.okvisgpu_get_stats.argtypes = [C.c_void_p, C.POINTER(ProblemStats)]
+        L.okvisgpu_imu_append.argtypes = [C.c_void_p, C.POINTER(ImuAppendBatch), _ip]
         L.okvisgpu_twopose_compute.argtypes = [C.c_void_p, C.POINTER(TwoPoseEdges), _dp, _dp, _dp, _dp, _dp]
         _lib = L
     return _lib
@@ -496,6 +502,28 @@ class Context:
         J = np.zeros((n_relpose, 6, 12))
         self._check(lib().okvisgpu_eval_relpose(self.h, window, dptr(r), dptr(J)), "eval_relpose")
         return r, J
+
+    def imu_append(self, imu_params, state, t1_old, t1_new, speed_biases, sample_begin, sample_t, sample_ga):
+        """okvisgpu_imu_append (ImuError::append for a batch): `state` [n, IMU_STATE_DOUBLES] is updated
+        in place; returns the integrated steps per factor (-1: samples do not reach t1_new)."""
+        n = len(t1_old)
+        keep = [np.ascontiguousarray(t1_old, dtype=np.int64), np.ascontiguousarray(t1_new, dtype=np.int64),
+                np.ascontiguousarray(speed_biases, dtype=np.float64).reshape(n, 9),
+                np.ascontiguousarray(sample_begin, dtype=np.int32), np.ascontiguousarray(sample_t, dtype=np.int64),
+                np.ascontiguousarray(sample_ga, dtype=np.float64).reshape(-1, 6)]
+        assert state.dtype == np.float64 and state.flags["C_CONTIGUOUS"] and state.shape == (n, IMU_STATE_DOUBLES)
+        b = ImuAppendBatch()
+        b.n = n
+        b.imu_params = imu_params
+        b.state = dptr(state)
+        b.t1_old_ns, b.t1_new_ns = keep[0].ctypes.data_as(_lp), keep[1].ctypes.data_as(_lp)
+        b.speed_biases = dptr(keep[2])
+        b.sample_begin = keep[3].ctypes.data_as(_ip)
+        b.sample_t_ns = keep[4].ctypes.data_as(_lp)
+        b.sample_gyr_acc = dptr(keep[5])
+        steps = np.zeros(n, dtype=np.int32)
+        self._check(lib().okvisgpu_imu_append(self.h, C.byref(b), steps.ctypes.data_as(_ip)), "okvisgpu_imu_append")
+        return steps
 
     def twopose_compute(self, edges: "TwoPoseBatch"):
         """TwoPoseStandardGraphError::compute for every edge of the batch: dict of DeltaX_ [n,6],

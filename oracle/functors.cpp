@@ -316,6 +316,18 @@ void ImuError::loadState(const double* s) {
   }
   for (int i = 0; i < 225; ++i) sqrtInfo.a[i] = s[66 + i];
   lastSteps = (int)s[291];
+  // the append state (ABI 4): cross_ and P_delta_. The four dPdsigma_ of the last integration
+  // are not stored; P = sum_j sigma_j^2 dPdsigma_j, and every later use (append) is linear in
+  // them, so P is carried as dPdsigma_0 = P / sigma_g^2 (or through the first non-zero sigma).
+  for (int i = 0; i < 9; ++i) cross.a[i] = s[292 + i];
+  for (int i = 0; i < 225; ++i) P_delta.a[i] = s[301 + i];
+  const double sig[4] = {params.sigma_g_c, params.sigma_a_c, params.sigma_gw_c, params.sigma_aw_c};
+  for (int j = 0; j < 4; ++j) dPdsigma[j] = Mat<15, 15>::Zero();
+  for (int j = 0; j < 4; ++j)
+    if (sig[j] != 0.0) {
+      dPdsigma[j] = (1.0 / (sig[j] * sig[j])) * P_delta;
+      break;
+    }
 }
 void ImuError::storeState(double* s) const {
   s[0] = redoCounter;
@@ -335,6 +347,121 @@ void ImuError::storeState(double* s) const {
   }
   for (int i = 0; i < 225; ++i) s[66 + i] = sqrtInfo.a[i];
   s[291] = lastSteps;
+  for (int i = 0; i < 9; ++i) s[292 + i] = cross.a[i];
+  for (int i = 0; i < 225; ++i) s[301 + i] = P_delta.a[i];
+}
+
+// ImuError::append (ImuError.cpp:63-255). The reference loops over the appended deque `m` and
+// compares with the end of the merged member deque; the loop always leaves at nexttime == t_1
+// first because m covers t_1 (checked), which is what this restatement does.
+int ImuError::append(const double* sb, const std::vector<ImuSample>& m, long long t_1) {
+  // merge the deques (:74-81)
+  size_t first = 0;
+  while (first < m.size() && !(m[first].t > meas.back().t)) ++first;
+  meas.insert(meas.end(), m.begin() + first, m.end());
+  long long time = t1;
+  const long long end = t_1;
+  t1 = t_1;  // setT1
+  if (m.empty() || !(m.back().t >= end)) return -1;
+  const V3 bg = v3(sb[3], sb[4], sb[5]);
+  const V3 ba = v3(sb[6], sb[7], sb[8]);
+  bool hasStarted = false;
+  int i = 0;
+  const int N = (int)m.size();
+  for (int it = 0; it + 1 < N; ++it) {
+    V3 omega_S_0 = v3(m[it].g[0], m[it].g[1], m[it].g[2]);
+    V3 acc_S_0 = v3(m[it].a[0], m[it].a[1], m[it].a[2]);
+    V3 omega_S_1 = v3(m[it + 1].g[0], m[it + 1].g[1], m[it + 1].g[2]);
+    V3 acc_S_1 = v3(m[it + 1].a[0], m[it + 1].a[1], m[it + 1].a[2]);
+    long long nexttime = m[it + 1].t;
+    double dt = durToSec(nexttime - time);
+    if (end < nexttime) {
+      const double interval = durToSec(nexttime - m[it].t);
+      nexttime = t1;
+      dt = durToSec(nexttime - time);
+      const double r = dt / interval;
+      omega_S_1 = (1.0 - r) * omega_S_0 + r * omega_S_1;
+      acc_S_1 = (1.0 - r) * acc_S_0 + r * acc_S_1;
+    }
+    if (dt <= 0.0) continue;
+    if (!hasStarted) {
+      hasStarted = true;
+      const double r = dt / durToSec(nexttime - m[it].t);
+      omega_S_0 = r * omega_S_0 + (1.0 - r) * omega_S_1;
+      acc_S_0 = r * acc_S_0 + (1.0 - r) * acc_S_1;
+    }
+    double gyr_sat_mult = 1.0, acc_sat_mult = 1.0;
+    for (int k = 0; k < 3; ++k)
+      if (std::fabs(omega_S_0.a[k]) > params.g_max || std::fabs(omega_S_1.a[k]) > params.g_max) {
+        gyr_sat_mult *= 100; break;
+      }
+    for (int k = 0; k < 3; ++k)
+      if (std::fabs(acc_S_0.a[k]) > params.a_max || std::fabs(acc_S_1.a[k]) > params.a_max) {
+        acc_sat_mult *= 100; break;
+      }
+    // (:160-190) orientation, rotation (double) integrals
+    const V3 omega_S_true = 0.5 * (omega_S_0 + omega_S_1) - bg;
+    const double theta_half = omega_S_true.norm() * 0.5 * dt;
+    const double sinc_theta_half = sinc(theta_half);
+    const double cos_theta_half = std::cos(theta_half);
+    const V3 dqv = (sinc_theta_half * 0.5 * dt) * omega_S_true;
+    const Quat dq{dqv.a[0], dqv.a[1], dqv.a[2], cos_theta_half};
+    const Quat Delta_q_1 = qmul(Delta_q, dq);
+    const M3 C = qrot(Delta_q);
+    const M3 C_1 = qrot(Delta_q_1);
+    const V3 acc_S_true = 0.5 * (acc_S_0 + acc_S_1) - ba;
+    const M3 CC1 = C + C_1;
+    const M3 C_integral_1 = C_integral + (0.5 * dt) * CC1;
+    const V3 acc_integral_1 = acc_integral + (0.5 * dt) * (CC1 * acc_S_true);
+    C_doubleintegral += dt * C_integral + (0.25 * dt * dt) * CC1;
+    acc_doubleintegral += dt * acc_integral + (0.25 * dt * dt) * (CC1 * acc_S_true);
+    // (:192-200) Jacobian parts
+    const M3 Jr = rightJacobian(dt * omega_S_true);
+    dalpha_db_g += dt * (C_1 * Jr);
+    const M3 cross_1 = qrot(qinverse(dq)) * cross + dt * Jr;
+    const M3 acc_S_x = crossMx(acc_S_true);
+    const M3 X = C * acc_S_x * cross + C_1 * acc_S_x * cross_1;
+    const M3 dv_db_g_1 = dv_db_g + (0.5 * dt) * X;
+    dp_db_g += dt * dv_db_g + (0.25 * dt * dt) * X;
+    // (:202-233) covariance derivatives
+    Mat<15, 15> F = Mat<15, 15>::Identity();
+    F.setBlock(0, 3, -crossMx(dt * acc_integral + (0.25 * dt * dt) * (CC1 * acc_S_true)));
+    F.setBlock(0, 6, dt * M3::Identity());
+    F.setBlock(0, 9, dt * dv_db_g + (0.25 * dt * dt) * X);
+    F.setBlock(0, 12, -(dt * C_integral) + (0.25 * dt * dt) * CC1);
+    F.setBlock(3, 9, -(dt * C_1));
+    F.setBlock(6, 3, -crossMx((0.5 * dt) * (CC1 * acc_S_true)));
+    F.setBlock(6, 9, (0.5 * dt) * X);
+    F.setBlock(6, 12, -((0.5 * dt) * CC1));
+    Mat<15, 15> K[4];
+    for (int j = 0; j < 4; ++j) K[j] = Mat<15, 15>::Zero();
+    for (int k = 0; k < 3; ++k) {
+      K[0](3 + k, 3 + k) = gyr_sat_mult * dt;
+      K[1](k, k) = 0.5 * dt * dt * dt * acc_sat_mult * acc_sat_mult * acc_sat_mult;
+      K[1](6 + k, 6 + k) = acc_sat_mult * dt;
+      K[2](9 + k, 9 + k) = dt;
+      K[3](12 + k, 12 + k) = dt;
+    }
+    const Mat<15, 15> Ft = F.T();
+    for (int j = 0; j < 4; ++j) dPdsigma[j] = F * dPdsigma[j] * Ft + K[j];
+    Delta_q = Delta_q_1;
+    C_integral = C_integral_1;
+    acc_integral = acc_integral_1;
+    cross = cross_1;
+    dv_db_g = dv_db_g_1;
+    time = nexttime;
+    ++i;
+    if (nexttime == t1) break;
+  }
+  // (:236-252) weighting; speedAndBiases_ref_, redo_ and the redo counter are left as they are
+  for (int j = 0; j < 4; ++j) dPdsigma[j] = 0.5 * dPdsigma[j] + 0.5 * dPdsigma[j].T();
+  P_delta = (params.sigma_g_c * params.sigma_g_c) * dPdsigma[0];
+  P_delta += (params.sigma_a_c * params.sigma_a_c) * dPdsigma[1];
+  P_delta += (params.sigma_gw_c * params.sigma_gw_c) * dPdsigma[2];
+  P_delta += (params.sigma_aw_c * params.sigma_aw_c) * dPdsigma[3];
+  symmSqrtU(P_delta, sqrtInfo);
+  lastSteps = i;
+  return i;
 }
 
 // ImuError::redoPreintegration (ImuError.cpp:258-466), literal 4-derivative covariance recursion.

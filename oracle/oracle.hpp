@@ -76,6 +76,10 @@ class ImuError {
 
   ImuError();
   int redoPreintegration(const double* sb);                          // ImuError.cpp:258-466
+  // ImuError::append (ImuError.cpp:63-255): continue the preintegration from t1 to t_1 over the
+  // next link's measurements m with the eliminated state's speed/bias sb (IMU-merge elimination,
+  // ViGraphEstimator.cpp:38-171). Returns the integrated steps, -1 if m does not cover t_1.
+  int append(const double* sb, const std::vector<ImuSample>& m, long long t_1);
   // ImuError.cpp:797-1003. jac (ambient) J0 15x7, J1 15x9, J2 15x7, J3 15x9; jacMin 15x6,15x9,15x6,15x9.
   bool evaluate(const double* const* params, double* r, double** jac, double** jacMin,
                 bool redoAlways);
@@ -124,6 +128,11 @@ int oracle_eval_imu(const okvisgpu_problem* p, int32_t redo_always, double* r, d
 int oracle_check_jacobians(const okvisgpu_problem* p, int32_t kind, int32_t index, double delta,
                            double* max_rel);
 int oracle_eval_relpose(const okvisgpu_problem* p, double* r, double* J /*[n][6][12] minimal*/);
+/* IMU-merge elimination of the state between factors f and f+1 (ViGraphEstimator.cpp:38-171):
+ * factor f's ImuError (its state from p->imu_state, integrated first if never integrated) appended
+ * with factor f+1's measurements up to its t1 at the speed/bias sb (ImuError::append,
+ * ImuError.cpp:63-255). Writes the merged state [OKVISGPU_IMU_STATE_DOUBLES]; returns the steps. */
+int oracle_imu_merge(const okvisgpu_problem* p, int32_t f, const double* sb, double* state_out);
 int oracle_twopose_compute(const okvisgpu_twopose_edges* E, double* delta_x, double* sqrt_info, double* lin_point,
                            double* H00, double* b0);
 int oracle_project(const okvisgpu_camera* cam, const double* hp4, double* kp2, double* J24);

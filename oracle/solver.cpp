@@ -1185,6 +1185,23 @@ int oracle_eval_reprojection(const okvisgpu_problem* p, double* r, double* Jp, d
   return OKVISGPU_OK;
 }
 
+int oracle_imu_merge(const okvisgpu_problem* p, int32_t f, const double* sb, double* state_out) {
+  if (!p || f < 0 || f + 1 >= p->n_imu) return -2;
+  Program P;
+  buildProgram(p, P, true);
+  ImuError& e = P.imus[f];
+  if (e.redoCounter == 0) {  // first use integrates (ImuError.cpp:837)
+    const int* b = &p->imu_blocks[4 * f];
+    const double* prm[4] = {&p->poses[7 * b[0]], &p->speed_biases[9 * b[1]], &p->poses[7 * b[2]],
+                            &p->speed_biases[9 * b[3]]};
+    double rr[15];
+    e.evaluate(prm, rr, nullptr, nullptr, false);
+  }
+  const int steps = e.append(sb, P.imus[f + 1].meas, p->imu_t1_ns[f + 1]);
+  e.storeState(state_out);
+  return steps;
+}
+
 int oracle_eval_imu(const okvisgpu_problem* p, int32_t redo_always, double* r, double* J) {
   Program P;
   buildProgram(p, P, true);

@@ -36,6 +36,7 @@ def lib():
         L.oracle_pose_minus_jacobian.argtypes = [_dp, _dp]
         L.oracle_dense_cholesky.argtypes = [C.c_int32, _dp, C.c_int32]
         L.oracle_eval_relpose.argtypes = [P, _dp, _dp]
+        L.oracle_imu_merge.argtypes = [P, C.c_int32, _dp, _dp]
         L.oracle_twopose_compute.argtypes = [C.POINTER(og.TwoPoseEdges), _dp, _dp, _dp, _dp, _dp]
         _lib = L
     return _lib
@@ -102,3 +103,9 @@ def twopose_compute(batch):
                                       og.dptr(out["lin_point"]), og.dptr(out["H00"]), og.dptr(out["b0"]))
     assert rc == 0
     return out
+
+
+def imu_merge(problem_ptr, f, sb):
+    state = np.zeros(og.IMU_STATE_DOUBLES)
+    steps = lib().oracle_imu_merge(problem_ptr, f, og.dptr(np.ascontiguousarray(sb, dtype=np.float64)), og.dptr(state))
+    return state, steps
