@@ -30,10 +30,14 @@ _ARRAYS = {
     "relpose_blocks": (np.int32, (2,), "n_relpose"), "relpose_delta_x": (np.float64, (6,), "n_relpose"),
     "relpose_sqrt_info": (np.float64, (36,), "n_relpose"), "relpose_lin_point": (np.float64, (7,), "n_relpose"),
     "relpose_kind": (np.uint8, (), "n_relpose"),
+    "extrinsics_constant": (np.uint8, (), "n_cameras"),
+    "extrinsics_prior_camera": (np.int32, (), "n_extrinsics_priors"),
+    "extrinsics_prior_meas": (np.float64, (7,), "n_extrinsics_priors"),
+    "extrinsics_prior_sqrt_info": (np.float64, (36,), "n_extrinsics_priors"),
 }
 _PTR = {np.float64: _dp, np.int32: _ip, np.int64: _lp, np.uint8: _up}
 _COUNTS = ("n_poses", "n_speed_biases", "n_landmarks", "n_cameras", "n_observations", "n_imu", "n_pose_priors",
-           "n_sb_priors", "n_relpose")
+           "n_sb_priors", "n_relpose", "n_extrinsics_priors")
 
 
 class OwnedProblem:
@@ -62,7 +66,7 @@ class OwnedProblem:
             m = n[cnt]
             if not ptr or m == 0:
                 arr = np.zeros((m,) + shp, dtype=dt)
-                if k == "obs_cauchy":
+                if k in ("obs_cauchy", "extrinsics_constant"):  # NULL = Cauchy everywhere / constant T_SC
                     arr[:] = 1
                 setattr(self, k, arr)
                 continue
@@ -95,6 +99,10 @@ class OwnedProblem:
         s.n_pose_priors = len(self.pose_prior_block)
         s.n_sb_priors = len(self.sb_prior_block)
         s.n_relpose = len(self.relpose_blocks)
+        s.n_extrinsics_priors = len(self.extrinsics_prior_camera)
+        if len(self.extrinsics_constant) != len(self.cameras):  # default: constant extrinsics
+            self.extrinsics_constant = np.ones(len(self.cameras), np.uint8)
+            s.extrinsics_constant = self.extrinsics_constant.ctypes.data_as(_up) if len(self.cameras) else None
         self._cams = (og.Camera * max(1, len(self.cameras)))(*self.cameras)
         s.cameras = self._cams if self.cameras else None
         self.imu_sample_begin = np.ascontiguousarray(self.imu_sample_begin, dtype=np.int32)
