@@ -40,6 +40,23 @@ __device__ __forceinline__ double blockSum(double v, double* sh) {
   __syncthreads();
   return r;
 }
+// Strided per-thread loop over i = b + t, b + t + kRB, ... < e with the loads of U consecutive
+// iterations issued before any of them is consumed. A window's reductions run in one workgroup, so a
+// single window is a chain of dependent loads per thread; batching shortens it U-fold. use() sees the
+// elements in the order of the plain loop, so every sum is bitwise the same.
+template <int U, class Load, class Use>
+__device__ __forceinline__ void stridedBatched(int b, int e, Load load, Use use) {
+  int i = b + (int)threadIdx.x;
+  for (; i + (U - 1) * kRB < e; i += U * kRB) {
+    decltype(load(i)) v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = load(i + u * kRB);
+#pragma unroll
+    for (int u = 0; u < U; ++u) use(i + u * kRB, v[u]);
+  }
+  for (; i < e; i += kRB) use(i, load(i));
+}
+
 __device__ __forceinline__ double blockMax(double v, double* sh) {
   const int t = threadIdx.x;
   sh[t] = v;
@@ -73,115 +90,89 @@ __device__ __forceinline__ void jvAcc(double jc, double jg, double (&a)[3]) {
 // The companion (J_s step).r = step.(s g) uses the gradient g = J^T r already at hand.
 // Here the IMU factors, priors and relative-pose edges, one thread each; the reprojection residuals'
 // share is formed with the landmark back substitution (k_lm_backsub_jv, kernels_backsub.hip).
+// One 16-lane group per factor (IMU factor, pose prior, speed/bias prior, relative-pose edge, in
+// that order), lane = residual row: J_s v_c and J_s v_g of its row over the factor's free blocks,
+// then (jc^2, jg^2, jc jg) summed over the rows by a fixed shuffle tree.
 __global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int gid = (blockIdx.x * blockDim.x + threadIdx.x) >> 4, r = threadIdx.x & 15;
   const double* __restrict__ cF = P.vF;
   const double* __restrict__ yF = P.yF;
-  int u = t;
+  int u = gid, w = 0, nr = 0, nb = 0, ld = 0;
+  const double* J = nullptr;  // row-major rows of stride ld, columns of block q from col[q]
+  int off[4] = {-1, -1, -1, -1}, n[4] = {0, 0, 0, 0}, col[4] = {0, 0, 0, 0};
+  double* out = nullptr;
+  size_t ostride = 0;
+  bool live = false;
   if (u < P.n_imu) {
-    const int f = u;
-    const int w = P.imu_win[f];
-    if (!jvSelect(P, w)) return;
-    double a[3] = {0.0, 0.0, 0.0};
-    if (!(P.imu_flags[f] & 2)) {
-      const int lb = P.st[w].lcur;
-      const double* L = P.imu_lin[lb] + (size_t)f * kImuLin;
-      const int* blk = P.imu_blocks + 4 * f;
-      double vc[30], vg[30];
-      const size_t foff = P.win_foff[w];
-      const int offs[4] = {P.pose_f[blk[0]], P.sb_f[blk[1]], P.pose_f[blk[2]], P.sb_f[blk[3]]};
-      const int cols[4] = {0, 6, 15, 21}, ns[4] = {6, 9, 6, 9};
-      for (int q = 0; q < 4; ++q)
-        for (int c = 0; c < ns[q]; ++c) {
-          const size_t i = foff + offs[q] + c;
-          vc[cols[q] + c] = offs[q] >= 0 ? P.sF[i] * cF[i] : 0.0;
-          vg[cols[q] + c] = offs[q] >= 0 ? -P.sF[i] * yF[i] : 0.0;
-        }
-      for (int r = 0; r < 15; ++r) {
-        double jc = 0.0, jg = 0.0;
-        for (int c = 0; c < 30; ++c) {
-          jc += L[15 + r * 30 + c] * vc[c];
-          jg += L[15 + r * 30 + c] * vg[c];
-        }
-        jvAcc(jc, jg, a);
+    w = P.imu_win[u];
+    if (jvSelect(P, w)) {
+      live = true;
+      out = P.imu_jv + u;
+      ostride = P.n_imu;
+      if (!(P.imu_flags[u] & 2)) {
+        const int* blk = P.imu_blocks + 4 * u;
+        J = P.imu_lin[P.st[w].lcur] + (size_t)u * kImuLin + 15;
+        nr = 15; ld = 30; nb = 4;
+        off[0] = P.pose_f[blk[0]]; off[1] = P.sb_f[blk[1]]; off[2] = P.pose_f[blk[2]]; off[3] = P.sb_f[blk[3]];
+        n[0] = 6; n[1] = 9; n[2] = 6; n[3] = 9;
+        col[0] = 0; col[1] = 6; col[2] = 15; col[3] = 21;
       }
     }
-    for (int k = 0; k < 3; ++k) P.imu_jv[(size_t)k * P.n_imu + f] = a[k];
-    return;
-  }
-  u -= P.n_imu;
-  if (u < P.n_pprior) {
-    const int i = u;
-    const int w = P.pp_win[i];
-    if (!jvSelect(P, w)) return;
-    double a[3] = {0.0, 0.0, 0.0};
-    const int pf = P.pose_f[P.pp_block[i]];
-    if (pf >= 0) {
-      const double* L = P.pp_lin[P.st[w].lcur] + 42 * (size_t)i;
-      const size_t base = (size_t)P.win_foff[w] + pf;
-      for (int r = 0; r < 6; ++r) {
-        double jc = 0.0, jg = 0.0;
-        for (int c = 0; c < 6; ++c) {
-          jc += L[6 + r * 6 + c] * P.sF[base + c] * cF[base + c];
-          jg += L[6 + r * 6 + c] * (-P.sF[base + c] * yF[base + c]);
-        }
-        jvAcc(jc, jg, a);
+  } else if ((u -= P.n_imu) < P.n_pprior) {
+    w = P.pp_win[u];
+    if (jvSelect(P, w)) {
+      live = true;
+      out = P.pp_jv + u;
+      ostride = P.n_pprior;
+      J = P.pp_lin[P.st[w].lcur] + 42 * (size_t)u + 6;
+      nr = 6; ld = 6; nb = 1;
+      off[0] = P.pose_f[P.pp_block[u]]; n[0] = 6;
+    }
+  } else if ((u -= P.n_pprior) < P.n_sbprior) {
+    w = P.sbp_win[u];
+    if (jvSelect(P, w)) {
+      live = true;
+      out = P.sbp_jv + u;
+      ostride = P.n_sbprior;
+      J = P.sbp_lin[P.st[w].lcur] + 90 * (size_t)u + 9;
+      nr = 9; ld = 9; nb = 1;
+      off[0] = P.sb_f[P.sbp_block[u]]; n[0] = 9;
+    }
+  } else if ((u -= P.n_sbprior) < P.n_relpose) {
+    w = P.rp_win[u];
+    if (jvSelect(P, w)) {
+      live = true;
+      out = P.rp_jv + u;
+      ostride = P.n_relpose;
+      if (!(P.rp_flags[u] & 2)) {
+        J = P.rp_lin[P.st[w].lcur] + kRelPoseLin * (size_t)u + 6;
+        nr = 6; ld = 12; nb = 2;
+        off[0] = P.pose_f[P.rp_blocks[2 * u]]; off[1] = P.pose_f[P.rp_blocks[2 * u + 1]];
+        n[0] = 6; n[1] = 6; col[1] = 6;
       }
     }
-    for (int k = 0; k < 3; ++k) P.pp_jv[(size_t)k * P.n_pprior + i] = a[k];
-    return;
   }
-  u -= P.n_pprior;
-  if (u < P.n_sbprior) {
-    const int i = u;
-    const int w = P.sbp_win[i];
-    if (!jvSelect(P, w)) return;
-    double a[3] = {0.0, 0.0, 0.0};
-    const int sf = P.sb_f[P.sbp_block[i]];
-    if (sf >= 0) {
-      const double* L = P.sbp_lin[P.st[w].lcur] + 90 * (size_t)i;
-      const size_t base = (size_t)P.win_foff[w] + sf;
-      for (int r = 0; r < 9; ++r) {
-        double jc = 0.0, jg = 0.0;
-        for (int c = 0; c < 9; ++c) {
-          jc += L[9 + r * 9 + c] * P.sF[base + c] * cF[base + c];
-          jg += L[9 + r * 9 + c] * (-P.sF[base + c] * yF[base + c]);
-        }
-        jvAcc(jc, jg, a);
+  double jc = 0.0, jg = 0.0;
+  if (live && r < nr) {
+    const size_t foff = P.win_foff[w];
+    for (int q = 0; q < nb; ++q) {
+      if (off[q] < 0) continue;
+      for (int c = 0; c < n[q]; ++c) {
+        const size_t i = foff + off[q] + c;
+        const double jv = J[r * ld + col[q] + c];
+        jc += jv * (P.sF[i] * cF[i]);
+        jg += jv * (-P.sF[i] * yF[i]);
       }
     }
-    for (int k = 0; k < 3; ++k) P.sbp_jv[(size_t)k * P.n_sbprior + i] = a[k];
-    return;
   }
-  u -= P.n_sbprior;
-  if (u < P.n_relpose) {
-    const int i = u;
-    const int w = P.rp_win[i];
-    if (!jvSelect(P, w)) return;
-    double a[3] = {0.0, 0.0, 0.0};
-    if (!(P.rp_flags[i] & 2)) {
-      const double* L = P.rp_lin[P.st[w].lcur] + kRelPoseLin * (size_t)i;
-      const size_t foff = P.win_foff[w];
-      const int offs[2] = {P.pose_f[P.rp_blocks[2 * i]], P.pose_f[P.rp_blocks[2 * i + 1]]};
-      double vc[12], vg[12];
-      for (int q = 0; q < 2; ++q)
-        for (int c = 0; c < 6; ++c) {
-          const size_t j = foff + offs[q] + c;
-          vc[6 * q + c] = offs[q] >= 0 ? P.sF[j] * cF[j] : 0.0;
-          vg[6 * q + c] = offs[q] >= 0 ? -P.sF[j] * yF[j] : 0.0;
-        }
-      for (int r = 0; r < 6; ++r) {
-        double jc = 0.0, jg = 0.0;
-        for (int c = 0; c < 12; ++c) {
-          jc += L[6 + r * 12 + c] * vc[c];
-          jg += L[6 + r * 12 + c] * vg[c];
-        }
-        jvAcc(jc, jg, a);
-      }
-    }
-    for (int k = 0; k < 3; ++k) P.rp_jv[(size_t)k * P.n_relpose + i] = a[k];
-  }
+  double a[3] = {jc * jc, jg * jg, jc * jg};
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+#pragma unroll
+    for (int m = 8; m > 0; m >>= 1) a[k] += __shfl_xor(a[k], m, 64);
+  if (live && r == 0)
+    for (int k = 0; k < 3; ++k) out[(size_t)k * ostride] = a[k];
 }
 
 // Bookkeeping common to every iteration end (FinalizeIterationAndCheckIfMinimizerCanContinue):
@@ -217,10 +208,13 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
     if (mode == R_COST_CAND && !s.eval_cand) return;
     const int lb = (mode == R_COST_CAND) ? 1 - s.lcur : s.lcur;
     double c = 0.0, cf = 0.0;
-    for (int o = ob + t; o < oe; o += kRB) {
-      if (P.obs_flags[o] & 2) cf += P.obs_cost[lb][o];
-      else c += P.obs_cost[lb][o];
-    }
+    struct OC { double c; uint8_t f; };
+    const double* oc = P.obs_cost[lb];
+    stridedBatched<8>(ob, oe, [&](int o) { return OC{oc[o], P.obs_flags[o]}; },
+                      [&](int, const OC& v) {
+                        if (v.f & 2) cf += v.c;
+                        else c += v.c;
+                      });
     for (int f = ib + t; f < ie; f += kRB) {
       if (P.imu_flags[f] & 2) cf += P.imu_cost[lb][f];
       else c += P.imu_cost[lb][f];
@@ -299,7 +293,8 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     double acc = 0.0;
-    for (int v = vb + t; v < ve; v += kRB) acc += P.obs_jv[(size_t)k * P.n_visit + v];
+    const double* jv = P.obs_jv + (size_t)k * P.n_visit;
+    stridedBatched<8>(vb, ve, [&](int v) { return jv[v]; }, [&](int, double x) { acc += x; });
     for (int f = ib + t; f < ie; f += kRB) acc += P.imu_jv[(size_t)k * P.n_imu + f];
     for (int i = pb + t; i < pe; i += kRB) acc += P.pp_jv[(size_t)k * P.n_pprior + i];
     for (int i = sbb + t; i < sbe; i += kRB) acc += P.sbp_jv[(size_t)k * P.n_sbprior + i];
@@ -310,9 +305,18 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
   double g2 = 0.0;
   const int fo = P.win_foff[w], fd = P.win_fdim[w];
   for (int e = t; e < fd; e += kRB) g2 += P.dgF[fo + e] * P.dgF[fo + e];
-  for (int l = lmb + t; l < lme; l += kRB)
-    if (P.lm_free[l])
-      for (int c = 0; c < 3; ++c) g2 += P.dgL[3 * (size_t)l + c] * P.dgL[3 * (size_t)l + c];
+  struct LG { double d[3]; uint8_t f; };
+  stridedBatched<4>(lmb, lme,
+                    [&](int l) {
+                      LG v;
+                      v.f = P.lm_free[l];
+                      for (int c = 0; c < 3; ++c) v.d[c] = P.dgL[3 * (size_t)l + c];
+                      return v;
+                    },
+                    [&](int, const LG& v) {
+                      if (v.f)
+                        for (int c = 0; c < 3; ++c) g2 += v.d[c] * v.d[c];
+                    });
   g2 = blockSum(g2, sh);
   if (t == 0) {
     s.jcc = a[0];
@@ -365,17 +369,24 @@ __global__ __launch_bounds__(kRB) void k_gradnorm(const DevProblem* __restrict__
     }
   }
   const int l0 = P.win_lm_range[2 * w], l1 = P.win_lm_range[2 * w + 1];
-  for (int l = l0 + t; l < l1; l += kRB) {
-    if (!P.lm_free[l]) continue;
-    const double* x = P.lm[xs] + 4 * (size_t)l;
-    const double* g = P.lm_g + 3 * (size_t)l;
-    for (int k = 0; k < 4; ++k) x2 += x[k] * x[k];
-    for (int k = 0; k < 3; ++k) {
-      const double d = x[k] - (x[k] + (-g[k]));
-      mx = fmax(mx, fabs(d));
-      g2 += d * d;
-    }
-  }
+  struct LX { double x[4], g[3]; uint8_t f; };
+  stridedBatched<4>(l0, l1,
+                    [&](int l) {
+                      LX v;
+                      v.f = P.lm_free[l];
+                      for (int k = 0; k < 4; ++k) v.x[k] = P.lm[xs][4 * (size_t)l + k];
+                      for (int k = 0; k < 3; ++k) v.g[k] = P.lm_g[3 * (size_t)l + k];
+                      return v;
+                    },
+                    [&](int, const LX& v) {
+                      if (!v.f) return;
+                      for (int k = 0; k < 4; ++k) x2 += v.x[k] * v.x[k];
+                      for (int k = 0; k < 3; ++k) {
+                        const double d = v.x[k] - (v.x[k] + (-v.g[k]));
+                        mx = fmax(mx, fabs(d));
+                        g2 += d * d;
+                      }
+                    });
   mx = blockMax(mx, sh);
   g2 = blockSum(g2, sh);
   x2 = blockSum(x2, sh);
@@ -450,15 +461,25 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
     nn += b * b;
     gn += a * b;
   }
-  for (int l = l0 + t; l < l1; l += kRB) {
-    if (!P.lm_free[l]) continue;
-    for (int c = 0; c < 3; ++c) {
-      const double a = P.dgL[3 * (size_t)l + c], b = P.gnL[3 * (size_t)l + c];
-      gg += a * a;
-      nn += b * b;
-      gn += a * b;
-    }
-  }
+  struct LD { double a[3], b[3]; uint8_t f; };
+  stridedBatched<4>(l0, l1,
+                    [&](int l) {
+                      LD v;
+                      v.f = P.lm_free[l];
+                      for (int c = 0; c < 3; ++c) {
+                        v.a[c] = P.dgL[3 * (size_t)l + c];
+                        v.b[c] = P.gnL[3 * (size_t)l + c];
+                      }
+                      return v;
+                    },
+                    [&](int, const LD& v) {
+                      if (!v.f) return;
+                      for (int c = 0; c < 3; ++c) {
+                        gg += v.a[c] * v.a[c];
+                        nn += v.b[c] * v.b[c];
+                        gn += v.a[c] * v.b[c];
+                      }
+                    });
   gg = blockSum(gg, sh);
   nn = blockSum(nn, sh);
   gn = blockSum(gn, sh);
@@ -527,23 +548,37 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
       sn2 += (x[c] - yv) * (x[c] - yv);
     }
   }
-  for (int l = l0 + t; l < l1; l += kRB) {
-    if (!P.lm_free[l]) continue;
-    const double* x = P.lm[xs] + 4 * (size_t)l;
-    double* y = P.lm[xd] + 4 * (size_t)l;
-    for (int c = 0; c < 3; ++c) {
-      const size_t i = 3 * (size_t)l + c;
-      const double v = ca * P.dgL[i] + cb * P.gnL[i];
-      dn2 += v * v;
-      const double st = v / P.diagL[i];
-      P.stepL[i] = st;
-      jr += (st * P.sL[i]) * P.gL[i];
-      const double yv = x[c] + st * P.sL[i];
-      y[c] = yv;
-      sn2 += (x[c] - yv) * (x[c] - yv);
-    }
-    y[3] = x[3];
-  }
+  struct LS { double x[4], dg[3], gn[3], dia[3], sl[3], g[3]; uint8_t f; };
+  stridedBatched<4>(l0, l1,
+                    [&](int l) {
+                      LS v;
+                      v.f = P.lm_free[l];
+                      for (int k = 0; k < 4; ++k) v.x[k] = P.lm[xs][4 * (size_t)l + k];
+                      for (int c = 0; c < 3; ++c) {
+                        const size_t i = 3 * (size_t)l + c;
+                        v.dg[c] = P.dgL[i];
+                        v.gn[c] = P.gnL[i];
+                        v.dia[c] = P.diagL[i];
+                        v.sl[c] = P.sL[i];
+                        v.g[c] = P.gL[i];
+                      }
+                      return v;
+                    },
+                    [&](int l, const LS& v) {
+                      if (!v.f) return;
+                      double* y = P.lm[xd] + 4 * (size_t)l;
+                      for (int c = 0; c < 3; ++c) {
+                        const double vv = ca * v.dg[c] + cb * v.gn[c];
+                        dn2 += vv * vv;
+                        const double st = vv / v.dia[c];
+                        P.stepL[3 * (size_t)l + c] = st;
+                        jr += (st * v.sl[c]) * v.g[c];
+                        const double yv = v.x[c] + st * v.sl[c];
+                        y[c] = yv;
+                        sn2 += (v.x[c] - yv) * (v.x[c] - yv);
+                      }
+                      y[3] = v.x[3];
+                    });
   sn2 = blockSum(sn2, sh);
   dn2 = blockSum(dn2, sh);
   jr = blockSum(jr, sh);
@@ -574,8 +609,8 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
 }
 
 void launch_jv(const DevProblem& P, hipStream_t s) {
-  const int n = P.n_imu + P.n_pprior + P.n_sbprior + P.n_relpose;
-  if (n > 0) hipLaunchKernelGGL(k_jv, dim3((n + 255) / 256), dim3(256), 0, s, P.self);
+  const int n = P.n_imu + P.n_pprior + P.n_sbprior + P.n_relpose;  // 16-lane groups
+  if (n > 0) hipLaunchKernelGGL(k_jv, dim3((n + 15) / 16), dim3(256), 0, s, P.self);
 }
 void launch_reduce(const DevProblem& P, int mode, hipStream_t s) {
   hipLaunchKernelGGL(k_reduce, dim3(P.n_win), dim3(kRB), 0, s, P.self, mode);

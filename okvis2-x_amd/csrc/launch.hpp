@@ -22,6 +22,7 @@ void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t 
 void launch_gn_reduce(const DevProblem& P, hipStream_t s);    // lm_prep + zero S + assemble
 void launch_gn_backsub(const DevProblem& P, hipStream_t s);   // landmark back substitution + gn vectors
 void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s);
+void launch_imu_hess(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_lm_prep(const DevProblem& P, hipStream_t s);
 void launch_zero_S(const DevProblem& P, hipStream_t s);

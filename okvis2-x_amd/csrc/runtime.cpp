@@ -788,6 +788,8 @@ struct Arena {
 struct okvisgpu_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t side[2] = {nullptr, nullptr};  // fork streams of the captured iteration graph
+  std::vector<hipEvent_t> forkEv;
   std::string last_error;
   HostBatch B;
   std::vector<const okvisgpu_problem*> probs;
@@ -829,6 +831,9 @@ struct okvisgpu_ctx {
   ~okvisgpu_ctx() {
     if (iterGraph) (void)hipGraphExecDestroy(iterGraph);
     if (arena) (void)hipFree(arena);
+    for (hipEvent_t e : forkEv) (void)hipEventDestroy(e);
+    for (hipStream_t q : side)
+      if (q) (void)hipStreamDestroy(q);
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -1180,11 +1185,71 @@ struct okvisgpu_ctx {
     launch_gradnorm(P, 1, stream);
   }
 
+  // The captured iteration with the independent kernels of a phase on fork streams, so the graph
+  // runs them concurrently (the latency of a single window is a chain of small kernels); the data
+  // they touch is disjoint (eval: obs / IMU / prior records; linearisation: landmark groups / IMU
+  // Hessians; J*v: reprojection rows / factor rows; S tiles zeroed vs. landmark-group records;
+  // pose-pose vs. speed/bias blocks of S).
+  void launchIterationForked() {
+    size_t ne = 0;
+    auto ev = [&]() {
+      if (ne == forkEv.size()) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        forkEv.push_back(e);
+      }
+      return forkEv[ne++];
+    };
+    auto fork = [&](hipStream_t to) {
+      hipEvent_t e = ev();
+      HIPCHK(hipEventRecord(e, stream));
+      HIPCHK(hipStreamWaitEvent(to, e, 0));
+    };
+    auto join = [&](hipStream_t from) {
+      hipEvent_t e = ev();
+      HIPCHK(hipEventRecord(e, from));
+      HIPCHK(hipStreamWaitEvent(stream, e, 0));
+    };
+    // Gauss-Newton system: S tiles cleared while the stale Z is rebuilt; both assembly kernels
+    fork(side[0]);
+    launch_zero_S(P, side[0]);
+    launch_lm_prep(P, stream);
+    join(side[0]);
+    fork(side[0]);
+    launch_assemble_sb(P, side[0]);
+    launch_assemble_pp(P, stream);
+    join(side[0]);
+    launch_cholesky(P, stream);
+    launch_gn_finalize(P, stream);
+    fork(side[0]);
+    launch_jv(P, side[0]);
+    launch_lm_backsub(P, stream);
+    join(side[0]);
+    launch_reduce(P, R_JV, stream);
+    launch_dogleg(P, stream);
+    // candidate evaluation
+    fork(side[0]);
+    fork(side[1]);
+    launch_eval_imu(P, 1, side[0]);
+    launch_eval_priors(P, 1, side[1]);
+    launch_eval_obs(P, 1, stream);
+    join(side[0]);
+    join(side[1]);
+    launch_reduce(P, R_COST_CAND, stream);
+    // linearisation at the accepted point
+    fork(side[0]);
+    launch_imu_hess(P, 1, side[0]);
+    launch_lm_blocks(P, 1, stream);
+    join(side[0]);
+    launch_fgrad(P, 1, stream);
+    launch_gradnorm(P, 1, stream);
+  }
+
   void ensureGraph() {
     if (iterGraph) return;
     hipGraph_t g;
     HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-    launchIteration();
+    launchIterationForked();
     HIPCHK(hipStreamEndCapture(stream, &g));
     HIPCHK(hipGraphInstantiate(&iterGraph, g, nullptr, nullptr, 0));
     HIPCHK(hipGraphDestroy(g));
@@ -1275,6 +1340,7 @@ int okvisgpu_ctx_create(int32_t device, okvisgpu_ctx** out) {
     c->cuCount = prop.multiProcessorCount;
     c->ldsPerBlock = prop.sharedMemPerBlock;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (hipStream_t& q : c->side) HIPCHK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
     return (int)OKVISGPU_OK;
   });
   if (rc != OKVISGPU_OK) {
