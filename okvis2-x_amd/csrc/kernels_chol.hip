@@ -179,13 +179,106 @@ __device__ __forceinline__ void storeC16(double* c, int ldc, const dbl4& v, int 
   for (int r = 0; r < 4; ++r) c[((lane >> 4) + 4 * r) * ldc + (lane & 15)] = v[r];
 }
 
+// One 8-column sub-panel of the in-LDS 64x64 LLT on one wavefront (lane = row i of the tile; the
+// rows of the sub-panel's 8x8 diagonal block D are rows c0..c0+7). No cross-lane traffic in the
+// column chain: every lane loads D (LDS broadcast reads) and factors it redundantly in registers,
+// then solves its own row against it (row TRSM), so the 8 dependent pivots cost only the FP64
+// latency of rsqrt + scaling + the next pivot update. Writes L (rows >= c0, lower part), 1/L_cc
+// to sRl and the 8x8 diagonal block of X = L^-1 (lanes 0..7: one column each) to xd (row stride
+// kLd). Returns false (wave-uniform) at a non-positive pivot.
+__device__ __forceinline__ bool subPanel8(double* sA, double* xd, double* sRl, int c0, int lane) {
+  double D[8][8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int k = 0; k <= m; ++k) D[m][k] = sA[(c0 + m) * kLd + c0 + k];
+  const int i = lane;
+  double r[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = sA[i * kLd + c0 + k];
+  double rl[8], x[8];
+  bool bad = false;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const double d = D[c][c];
+    if (!(d > 0.0)) bad = true;  // wave-uniform (every lane holds the same D)
+    rl[c] = rsqrtRefined(d);
+#pragma unroll
+    for (int m = c + 1; m < 8; ++m) D[m][c] *= rl[c];
+    x[c] = r[c] * rl[c];
+#pragma unroll
+    for (int m = c + 1; m < 8; ++m) {
+      D[m][m] -= D[m][c] * D[m][c];  // next pivots first: they carry the chain
+      r[m] -= x[c] * D[m][c];
+    }
+#pragma unroll
+    for (int m = c + 2; m < 8; ++m)
+#pragma unroll
+      for (int k = c + 1; k < m; ++k) D[m][k] -= D[m][c] * D[k][c];
+  }
+  if (bad) return false;
+  // row i of L: all 8 entries below the diagonal block, entries k <= i - c0 inside it
+  // (x[i - c0] = r * rl = d * rl = L_ii, bit-identical to the redundant factor's L_ii)
+  if (i >= c0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (i >= c0 + 8 || k <= i - c0) sA[i * kLd + c0 + k] = x[k];
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sRl[c0 + k] = rl[k];
+  }
+  if (lane < 8) {
+    // column j = lane of inv(L_D): y_m = (delta_mj - sum_{k<m} L_mk y_k) / L_mm
+    double y[8];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      double v = (m == lane) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < m; ++k) v -= D[m][k] * y[k];
+      y[m] = v * rl[m];
+      xd[m * kLd + lane] = y[m];
+    }
+  }
+  return true;
+}
+
+// Rank-8 trailing update of the in-LDS tile after sub-panel c0: A_ij -= sum_k L_ik L_jk (k in the
+// sub-panel) for 16x16 output blocks at or right of column c0 + 8, lower block triangle, dealt to
+// nw wavefronts (this one is wg of nw). A block column that starts inside the sub-panel keeps its
+// left 8 columns (already final L), and the block row that starts there keeps its top 8 rows (the
+// upper triangle, where potrfWave stashes inverse blocks).
+__device__ __forceinline__ void trailing8(double* sA, int c0, int wg, int nw, int lane) {
+  const int cb0 = (c0 + 8) >> 4;
+  const bool part = ((c0 + 8) & 15) != 0;
+  const int lr = lane & 15, lk = lane >> 4;
+  int idx = 0;
+  for (int rb = cb0; rb < 4; ++rb)
+    for (int cb = cb0; cb <= rb; ++cb, ++idx) {
+      if (idx % nw != wg) continue;
+      double* C = sA + 16 * rb * kLd + 16 * cb;
+      dbl4 acc = loadC16(C, kLd, lane);
+      const dbl4 c0v = acc;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const double av = -sA[(16 * rb + lr) * kLd + c0 + 4 * q + lk];
+        const double bv = sA[(16 * cb + lr) * kLd + c0 + 4 * q + lk];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+      if (part && cb == cb0 && lr < 8) acc = c0v;
+      if (part && rb == cb0) {  // rows lk + 4 reg < 8: reg 0, 1
+        acc[0] = c0v[0];
+        acc[1] = c0v[1];
+      }
+      storeC16(C, kLd, acc, lane);
+    }
+}
+
 // Diagonal tile: L_kk (into S, lower), X = L_kk^-1 (into sX and the Linv store) and y_k = X rhs_k
-// (sy holds rhs_k on entry, y_k on exit; also written to work). Blocked right-looking LLT with
-// 16-column panels:
-//   panel p   wavefront 0, lane = row i >= 16p holding its 16 panel entries in registers; the 16
-//             column steps broadcast pivots and column entries with v_readlane (no barriers)
-//   update p  A22 -= L21 L21^T on the matrix cores, 16x16 output blocks over the 4 wavefronts
-// then X blockwise: the 4 diagonal 16x16 inverses in parallel (one per wavefront), and
+// (sy holds rhs_k on entry, y_k on exit; also written to work). Right-looking LLT in 8-column
+// sub-panels (subPanel8 on wavefront 0, the rank-8 trailing updates on the matrix cores of all 4
+// wavefronts), then X blockwise: the 8x8 diagonal inverses come out of the sub-panels, the 16x16
+// diagonal blocks are completed with X21 = -X22 L21 X11 (one wavefront each), and
 // X_ij = -X_ii (sum_{m=j}^{i-1} L_im X_mj) by sub-diagonal on the matrix cores.
 // Returns false (uniformly) at a non-positive pivot.
 // (one non-inlined instantiation per calling kernel: a shared callee gets a generic register
@@ -204,58 +297,36 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
   if (t == 0) *sFail = 0;
   __syncthreads();
   CLK(4)
-  for (int p = 0; p < 4; ++p) {
-    if (wave == 0) {
-      const int i = lane;
-      double a[16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) a[c] = sA[i * kLd + 16 * p + c];
-      bool bad = false;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const int col = 16 * p + c;
-        const double dcc = readlaneD(a[c], col);
-        if (!(dcc > 0.0)) bad = true;  // wave-uniform
-        const double rl = rsqrtRefined(dcc);
-        if (lane == 0) sRl[col] = rl;  // 1 / L_cc for the inverse
-        const double l = (i == col) ? dcc * rl : a[c] * rl;
-        a[c] = l;
-#pragma unroll
-        for (int j = c + 1; j < 16; ++j) a[j] -= l * readlaneD(l, 16 * p + j);
-      }
-#pragma unroll
-      for (int c = 0; c < 16; ++c)
-        if (i >= 16 * p + c) sA[i * kLd + 16 * p + c] = a[c];
-      if (bad && lane == 0) *sFail = 1;
-    }
+#pragma unroll 1
+  for (int s = 0; s < 8; ++s) {
+    if (wave == 0 && !subPanel8(sA, sX + 8 * s * kLd + 8 * s, sRl, 8 * s, lane) && lane == 0) *sFail = 1;
     __syncthreads();
     CLK(5)
     if (*sFail) return false;
-    int idx = 0;
-    for (int rb = p + 1; rb < 4; ++rb)
-      for (int cb = p + 1; cb <= rb; ++cb, ++idx) {
-        if ((idx & 3) != wave) continue;
-        double* C = sA + 16 * rb * kLd + 16 * cb;
-        dbl4 acc = loadC16(C, kLd, lane);
-        // acc -= L[rb, p] L[cb, p]^T : B[k][n] = L[16cb + n][16p + k]
-        mfma16<1>(sA + 16 * rb * kLd + 16 * p, kLd, sA + 16 * cb * kLd + 16 * p, 1, kLd, -1.0, acc, lane);
-        storeC16(C, kLd, acc, lane);
-      }
-    __syncthreads();
+    if (s < 7) {
+      trailing8(sA, 8 * s, wave, 4, lane);
+      __syncthreads();
+    }
     CLK(6)
   }
-  if (lane < 16) {  // diagonal 16x16 inverses, wavefront q, lane = column
-    const int q = wave, j = lane;
-    double x[16];
+  {  // X21 = -X22 (L21 X11) of the diagonal 16x16 block q = wave; lane = (row m, column j)
+    const int q = wave, m = lane >> 3, j = lane & 7;
+    const int b = 16 * q;
+    double tk[8];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      double v = (i == j) ? 1.0 : 0.0;
+    for (int k = 0; k < 8; ++k) tk[k] = 0.0;
+    double t = 0.0;
 #pragma unroll
-      for (int m = 0; m < i; ++m) v -= sA[(16 * q + i) * kLd + 16 * q + m] * x[m];
-      x[i] = (i >= j) ? v * sRl[16 * q + i] : 0.0;
-    }
+    for (int k = 0; k < 8; ++k) t += sA[(b + 8 + m) * kLd + b + k] * sX[(b + k) * kLd + b + j];
+    sX[(b + 8 + m) * kLd + b + j] = t;  // T = L21 X11 staged in place (this wavefront only)
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int i = 0; i < 16; ++i) sX[(16 * q + i) * kLd + 16 * q + j] = x[i];
+    for (int k = 0; k < 8; ++k) tk[k] = sX[(b + 8 + k) * kLd + b + j];
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v += sX[(b + 8 + m) * kLd + b + 8 + k] * tk[k];
+    __builtin_amdgcn_wave_barrier();
+    sX[(b + 8 + m) * kLd + b + j] = -v;
   }
   __syncthreads();
   CLK(7)
@@ -340,6 +411,7 @@ __device__ void panelTile(double* Aik, int64_t ld, double* worki, double* sA, co
 // exit; per block row I the 16 row loads of every non-zero tile below are issued together, then
 // x_I = X_II^T (y_I - sum_i L_iI^T x_i) with the stored diagonal inverse. Threads 0..255 work;
 // any further threads of the workgroup only take part in the barriers.
+template <bool UPPER>
 __device__ void backSubstituteY(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* Linv,
                                 const uint8_t* nz, double* sx, double* sA, double* sy, int t) {
   const bool act = t < 256;
@@ -350,7 +422,7 @@ __device__ void backSubstituteY(const DevProblem& P, int w, const double* S, int
     if (act) {
       for (int i = I + 1; i < T; ++i) {
         if (!nz[i * T + I]) continue;
-        const double* Lt = S + i * kTile * ld + I * kTile + col;
+        const double* Lt = UPPER ? S + I * kTile * ld + i * kTile + col : S + i * kTile * ld + I * kTile + col;
         double v[16];
 #pragma unroll
         for (int u = 0; u < 16; ++u) v[u] = Lt[(int64_t)(q + 4 * u) * ld];
@@ -381,14 +453,15 @@ __device__ void backSubstituteY(const DevProblem& P, int w, const double* S, int
 }
 
 // As backSubstituteY with y taken from work (global).
+template <bool UPPER>
 __device__ void backSubstitute(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* work,
                                const double* Linv, const uint8_t* nz, double* sx, double* sA, double* sy, int t) {
   for (int e = t; e < ld; e += blockDim.x) sx[e] = work[e];
   __syncthreads();
-  backSubstituteY(P, w, S, ld, T, Linv, nz, sx, sA, sy, t);
+  backSubstituteY<UPPER>(P, w, S, ld, T, Linv, nz, sx, sA, sy, t);
 }
 
-__global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__ Pp) {
+__global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int w = blockIdx.x;
   if (!cholSelect(P, w)) return;
@@ -443,7 +516,7 @@ __global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__
   }
   CLK(2)
   extern __shared__ double sxDyn[];
-  backSubstitute(P, w, S, ld, T, work, Linv, nz, sxDyn, sA, sy, t);
+  backSubstitute<false>(P, w, S, ld, T, work, Linv, nz, sxDyn, sA, sy, t);
   CLK(3)
 #ifdef OKG_CHOL_CLOCK
   if (blockIdx.x == 0 && t == 0)
@@ -453,8 +526,13 @@ __global__ __launch_bounds__(256) void k_cholesky(const DevProblem* __restrict__
 #endif
 }
 
-// ---- tile-parallel schedule: per step k one launch each for the diagonal tiles, the panel tiles
-// and the band updates of all windows (many workgroups per window), then the backward solves.
+// ---- tile-parallel schedule (few windows: spreads each window over many CUs). One launch per
+// step k over all windows' band updates of that step; every workgroup forms the panels it needs
+// itself (L_ik = A_ik X_k^T from the final A_ik and the stored X_k), so no launch sits between the
+// diagonal factor and the updates. A_ik stays in place during the step (other workgroups of the
+// same launch still read it): the workgroup of the diagonal update (i,i) writes L_ik to the
+// unused upper slot (k,i) of S and applies rhs_i -= L_ik y_k; the backward substitution of this
+// schedule reads L there. The workgroup of tile (k+1,k+1) factors it right after its update.
 __global__ __launch_bounds__(256) void k_chol_diag(const DevProblem* __restrict__ Pp, int k) {
   const DevProblem& P = *Pp;
   const int w = blockIdx.x;
@@ -478,31 +556,22 @@ __global__ __launch_bounds__(256) void k_chol_diag(const DevProblem* __restrict_
   if (t < kTile) sy[t] = work[k * kTile + t];
   __syncthreads();
   if (!potrfTile<1>(S + k * kTile * ld + k * kTile, ld, P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile,
-                 work + k * kTile, sA, sX, sy, sRl, &sFail, t))
+                    work + k * kTile, sA, sX, sy, sRl, &sFail, t))
     if (t == 0) P.st[w].gn_failed = 1;
 }
 
-__global__ __launch_bounds__(256) void k_chol_panel(const DevProblem* __restrict__ Pp, int k) {
-  const DevProblem& P = *Pp;
-  const int item = P.chol_panel_begin[k] + blockIdx.x;
-  const int w = P.chol_panel_items[2 * item], i = P.chol_panel_items[2 * item + 1];
-  if (!cholSelect(P, w)) return;
-  const int64_t ld = P.win_fpad[w];
-  double* work = P.fwdF + P.win_fwdoff[w];
-  __shared__ double sA[kTile * kLd];
-  __shared__ double sX[kTile * kLd];
-  __shared__ double sy[2 * kTile];
-  const int t = threadIdx.x;
-  const double* X = P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile;
-  loadTile(X, kTile, 0, 0, sX, t);
-  if (t < kTile) sy[t] = work[k * kTile + t];
-  __syncthreads();
-  panelRhsVector(sX, sy, sy + kTile, sA, t);
-  panelTile(P.S + P.win_soff[w] + i * kTile * ld + k * kTile, ld, work + i * kTile, sA, sX, sy + kTile, t);
+// acc (C layout) -> LDS tile [64][kLd]
+__device__ __forceinline__ void accToLds(double* s, const dbl4 acc[2][2], int t) {
+  const int wave = t >> 6, lane = t & 63;
+  const int r0 = 32 * (wave >> 1), c0 = 32 * (wave & 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) s[(r0 + 16 * a + (lane >> 4) + 4 * reg) * kLd + c0 + 16 * b + (lane & 15)] = acc[a][b][reg];
 }
 
-// band updates of step k; the workgroup owning tile (k+1,k+1) factors it right after its update
-// (mode bit 1), so the next diagonal overlaps the remaining updates of this step
 __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restrict__ Pp, int k) {
   const DevProblem& P = *Pp;
   const int item = P.chol_upd_begin[k] + blockIdx.x;
@@ -511,26 +580,51 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
   if (!cholSelect(P, w)) return;
   const int64_t ld = P.win_fpad[w];
   double* S = P.S + P.win_soff[w];
+  double* work = P.fwdF + P.win_fwdoff[w];
   __shared__ double sA[kTile * kLd];
   __shared__ double sX[kTile * kLd];
+  __shared__ double sB[kTile * kLd];
   __shared__ double sy[2 * kTile];
   __shared__ double sRl[kTile];
   __shared__ int sFail;
   const int t = threadIdx.x;
   if (mode & 1) {
+    // panels of step k: L_ik (and L_jk) = A (X_k)^T, operands staged in LDS
+    loadTile(P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile, kTile, 0, 0, sX, t);
     loadTile(S + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
-    if (j != i) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sX, t);
+    if (j != i) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sB, t);
+    if (i == j && t < kTile) sy[t] = work[k * kTile + t];
     __syncthreads();
+    // rhs_i -= L_ik y_k, formed as A_ik z with z = X_k^T y_k from the A_ik tile in LDS (the same
+    // operations as panelTile, so all schedules give the same bits)
+    if (i == j) panelRhsVector(sX, sy, sy + kTile, sB, t);
+    dbl4 li[2][2], lj[2][2];
+    mfmaTileNT(sA, sX, li, t);
+    if (j != i) mfmaTileNT(sB, sX, lj, t);
+    if (i == j) {
+      const int row = t >> 2, q = t & 3;
+      double a = 0.0;
+#pragma unroll
+      for (int cc = 16 * q; cc < 16 * q + 16; ++cc) a += sA[row * kLd + cc] * sy[kTile + cc];
+      a += __shfl_xor(a, 1, 64);
+      a += __shfl_xor(a, 2, 64);
+      if (q == 0) work[i * kTile + row] -= a;
+    }
+    __syncthreads();  // every wavefront has read A_ik / A_jk
+    accToLds(sA, li, t);
+    if (j != i) accToLds(sB, lj, t);
     double* Cij = S + i * kTile * ld + j * kTile;
-    dbl4 c[2][2], acc[2][2];
-    loadC(Cij, ld, c, t);  // read of the read-modify-write overlaps the MFMAs
-    mfmaTileNT(sA, j == i ? sA : sX, acc, t);
+    dbl4 c[2][2];
+    loadC(Cij, ld, c, t);  // read of the read-modify-write overlaps the barrier and the MFMAs
+    if (i == j) storeTile<false>(S + k * kTile * ld + i * kTile, ld, 0, 0, li, t);  // L_ik -> upper slot (k,i)
+    __syncthreads();
+    dbl4 acc[2][2];
+    mfmaTileNT(sA, j == i ? sA : sB, acc, t);
     storeTileSub(Cij, ld, c, acc, t);
   }
   if (!(mode & 2)) return;
-  double* work = P.fwdF + P.win_fwdoff[w];
   const int d = k + 1;
-  __syncthreads();
+  __syncthreads();  // also orders this workgroup's rhs_d update before the read below
   if (t < kTile) sy[t] = work[d * kTile + t];
   __syncthreads();
   if (!potrfTile<2>(S + d * kTile * ld + d * kTile, ld, P.Linv + P.win_linvoff[w] + (int64_t)d * kTile * kTile,
@@ -546,7 +640,7 @@ __global__ __launch_bounds__(256) void k_chol_bsub(const DevProblem* __restrict_
   __shared__ double sA[8 * kTile];
   __shared__ double sy[kTile];
   extern __shared__ double sxDyn[];
-  backSubstitute(P, w, P.S + P.win_soff[w], ld, (int)(ld / kTile), P.fwdF + P.win_fwdoff[w],
+  backSubstitute<true>(P, w, P.S + P.win_soff[w], ld, (int)(ld / kTile), P.fwdF + P.win_fwdoff[w],
                  P.Linv + P.win_linvoff[w], P.tile_nz + P.win_tnzoff[w], sxDyn, sA, sy, threadIdx.x);
 }
 
@@ -752,38 +846,16 @@ __device__ __forceinline__ bool potrfWave(double* sF, double* sX, double* sRl, d
                                        int* xFree, int xFreeNeed, int* fail, int lane) {
   CLK_INIT
   const bool clk = lane == 0;
+  // sX is still read by the MFMA wavefronts (X_{k-1}) during the sweep: the 8x8 diagonal inverse
+  // blocks are stashed in the unused upper triangle of sF (block s at rows 8s.., columns 8s+8..;
+  // the last one at rows 40.., columns 56..) and moved to sX after xFree
 #pragma unroll 1
-  for (int p = 0; p < 4; ++p) {
-    const int i = lane;
-    double a[16];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) a[c] = sF[i * kLd + 16 * p + c];
-    bool bad = false;
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      const int col = 16 * p + c;
-      const double dcc = readlaneD(a[c], col);
-      if (!(dcc > 0.0)) bad = true;  // wave-uniform
-      const double rl = rsqrtRefined(dcc);
-      if (lane == 0) sRl[col] = rl;
-      const double l = (i == col) ? dcc * rl : a[c] * rl;
-      a[c] = l;
-#pragma unroll
-      for (int j = c + 1; j < 16; ++j) a[j] -= l * readlaneD(l, 16 * p + j);
-    }
-    if (bad) return false;
-#pragma unroll
-    for (int c = 0; c < 16; ++c)
-      if (i >= 16 * p + c) sF[i * kLd + 16 * p + c] = a[c];
+  for (int s = 0; s < 8; ++s) {
+    double* xd = s < 7 ? sF + 8 * s * kLd + 8 * s + 8 : sF + 40 * kLd + 56;
+    if (!subPanel8(sF, xd, sRl, 8 * s, lane)) return false;
     __builtin_amdgcn_wave_barrier();
     CLKW(4, clk)
-    for (int rb = p + 1; rb < 4; ++rb)
-      for (int cb = p + 1; cb <= rb; ++cb) {
-        double* C = sF + 16 * rb * kLd + 16 * cb;
-        dbl4 acc = loadC16(C, kLd, lane);
-        mfma16<1>(sF + 16 * rb * kLd + 16 * p, kLd, sF + 16 * cb * kLd + 16 * p, 1, kLd, -1.0, acc, lane);
-        storeC16(C, kLd, acc, lane);
-      }
+    if (s < 7) trailing8(sF, 8 * s, 0, 1, lane);
     __builtin_amdgcn_wave_barrier();
     CLKW(5, clk)
   }
@@ -792,22 +864,28 @@ __device__ __forceinline__ bool potrfWave(double* sF, double* sX, double* sRl, d
 #pragma unroll 8
   for (int u = 0; u < 64; ++u) {
     const int e = lane + 64 * u;
-    sX[(e >> 6) * kLd + (e & 63)] = 0.0;
+    const int row = e >> 6, col = e & 63, sb = row >> 3;
+    // diagonal 8x8 blocks from the stash, zero elsewhere
+    const double* xd = sb < 7 ? sF + 8 * sb * kLd + 8 * sb + 8 : sF + 40 * kLd + 56;
+    sX[row * kLd + col] = (col >> 3) == sb ? xd[(row & 7) * kLd + (col & 7)] : 0.0;
   }
   __builtin_amdgcn_wave_barrier();
   CLKW(7, clk)
-  {  // the 4 diagonal 16x16 inverses, lane group q, lane = column j
-    const int q = lane >> 4, j = lane & 15;
-    double x[16];
+  for (int q = 0; q < 4; ++q) {  // X21 = -X22 (L21 X11) of diagonal block q; lane = (row m, column j)
+    const int m = lane >> 3, j = lane & 7, b = 16 * q;
+    double t = 0.0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      double v = (i == j) ? 1.0 : 0.0;
+    for (int k = 0; k < 8; ++k) t += sF[(b + 8 + m) * kLd + b + k] * sX[(b + k) * kLd + b + j];
+    sX[(b + 8 + m) * kLd + b + j] = t;
+    __builtin_amdgcn_wave_barrier();
+    double tk[8];
 #pragma unroll
-      for (int m = 0; m < i; ++m) v -= sF[(16 * q + i) * kLd + 16 * q + m] * x[m];
-      x[i] = (i >= j) ? v * sRl[16 * q + i] : 0.0;
-    }
+    for (int k = 0; k < 8; ++k) tk[k] = sX[(b + 8 + k) * kLd + b + j];
+    double v = 0.0;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) sX[(16 * q + i) * kLd + 16 * q + j] = x[i];
+    for (int k = 0; k < 8; ++k) v += sX[(b + 8 + m) * kLd + b + 8 + k] * tk[k];
+    __builtin_amdgcn_wave_barrier();
+    sX[(b + 8 + m) * kLd + b + j] = -v;
   }
   __builtin_amdgcn_wave_barrier();
   CLKW(8, clk)
@@ -1072,8 +1150,6 @@ void launch_cholesky(const DevProblem& P, hipStream_t s) {
   }
   hipLaunchKernelGGL(k_chol_diag, dim3(P.n_win), dim3(256), 0, s, P.self, 0);
   for (int k = 0; k < P.max_tiles; ++k) {
-    const int np = P.h_panel_begin[k + 1] - P.h_panel_begin[k];
-    if (np > 0) hipLaunchKernelGGL(k_chol_panel, dim3(np), dim3(256), 0, s, P.self, k);
     const int nu = P.h_upd_begin[k + 1] - P.h_upd_begin[k];
     if (nu > 0) hipLaunchKernelGGL(k_chol_update, dim3(nu), dim3(256), 0, s, P.self, k);
   }

@@ -1,0 +1,119 @@
+// Development micro-benchmark: FP64 dependent-chain latency and the 8-column sub-panel step of the
+// diagonal-tile LLT (kernels_chol.hip subPanel8 / trailing8), one workgroup, many repetitions.
+// hipcc --offload-arch=gfx950 -O3 -I okvis2-x_amd/csrc scripts/ubench_sub8.hip -o /tmp/ubench_sub8
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <vector>
+#include "device_problem.hpp"
+
+namespace okg {
+constexpr int kLd = kTile + 1;
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ double rsqrtRefined(double d) {
+  double r = __builtin_amdgcn_rsq(d);
+  const double h = 0.5 * d;
+  r = r * (1.5 - h * r * r);
+  r = r * (1.5 - h * r * r);
+  return r;
+}
+__device__ __forceinline__ dbl4 loadC16(const double* c, int ldc, int lane) {
+  dbl4 v;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = c[((lane >> 4) + 4 * r) * ldc + (lane & 15)];
+  return v;
+}
+__device__ __forceinline__ void storeC16(double* c, int ldc, const dbl4& v, int lane) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) c[((lane >> 4) + 4 * r) * ldc + (lane & 15)] = v[r];
+}
+#include "ubench_sub8_body.inc"
+}  // namespace okg
+using namespace okg;
+
+__global__ void k_chain(double* out, long long* cyc, int n) {
+  double a = out[threadIdx.x], b = 1.0000001;
+  long long t0 = clock64();
+  for (int i = 0; i < n; ++i) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) a = fma(a, b, 1e-9);
+  }
+  long long t1 = clock64();
+  out[threadIdx.x] = a;
+  if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+__global__ void k_rsq(double* out, long long* cyc, int n) {
+  double a = out[threadIdx.x] + 2.0;
+  long long t0 = clock64();
+  for (int i = 0; i < n; ++i) a = rsqrtRefined(a) + 1.5;
+  long long t1 = clock64();
+  out[threadIdx.x] = a;
+  if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+__global__ void k_mfma(double* out, long long* cyc, int n) {
+  dbl4 acc = {0, 0, 0, 0};
+  double a = out[threadIdx.x], b = 0.5;
+  long long t0 = clock64();
+  for (int i = 0; i < n; ++i) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+  long long t1 = clock64();
+  out[threadIdx.x] = acc[0] + acc[1] + acc[2] + acc[3];
+  if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+__global__ void k_sweep(const double* A, double* out, long long* cyc, int reps, int mode) {
+  __shared__ double sA[kTile * kLd], sX[kTile * kLd], sRl[kTile];
+  __shared__ int fail;
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  long long tsub = 0, ttr = 0;
+  for (int r = 0; r < reps; ++r) {
+    for (int e = t; e < kTile * kTile; e += blockDim.x) sA[(e >> 6) * kLd + (e & 63)] = A[e];
+    __syncthreads();
+    for (int s = 0; s < 8; ++s) {
+      long long t0 = clock64();
+      if (wave == 0) subPanel8(sA, sX + 8 * s * kLd + 8 * s, sRl, 8 * s, lane);
+      __syncthreads();
+      long long t1 = clock64();
+      if (s < 7 && mode == 0) trailing8(sA, 8 * s, wave, blockDim.x / 64, lane);
+      __syncthreads();
+      long long t2 = clock64();
+      tsub += t1 - t0;
+      ttr += t2 - t1;
+    }
+  }
+  for (int e = t; e < kTile * kTile; e += blockDim.x) out[e] = sA[(e >> 6) * kLd + (e & 63)];
+  if (t == 0) { cyc[0] = tsub; cyc[1] = ttr; }
+}
+
+int main() {
+  double *d, *o;
+  long long* c;
+  hipMalloc(&d, 64 * 64 * 8);
+  hipMalloc(&o, 64 * 64 * 8);
+  hipMalloc(&c, 64);
+  std::vector<double> A(64 * 64);
+  for (int i = 0; i < 64; ++i)
+    for (int j = 0; j < 64; ++j) A[i * 64 + j] = (i == j ? 64.0 : 0.0) + 1.0 / (1 + i + j);
+  hipMemcpy(d, A.data(), A.size() * 8, hipMemcpyHostToDevice);
+  hipMemcpy(o, A.data(), A.size() * 8, hipMemcpyHostToDevice);
+  long long h[2];
+  const int n = 1000;
+  k_chain<<<1, 64>>>(o, c, n);
+  hipMemcpy(h, c, 8, hipMemcpyDeviceToHost);
+  printf("fp64 fma dependent chain: %.2f cycles per op\n", (double)h[0] / (16.0 * n));
+  k_rsq<<<1, 64>>>(o, c, n);
+  hipMemcpy(h, c, 8, hipMemcpyDeviceToHost);
+  printf("rsqrtRefined + add chain: %.2f cycles per step\n", (double)h[0] / n);
+  k_mfma<<<1, 64>>>(o, c, n);
+  hipMemcpy(h, c, 8, hipMemcpyDeviceToHost);
+  printf("mfma_f64_16x16x4 dependent chain: %.2f cycles per op\n", (double)h[0] / (16.0 * n));
+  for (int mode = 0; mode < 2; ++mode) {
+    k_sweep<<<1, 256>>>(d, o, c, 100, mode);
+    hipMemcpy(h, c, 16, hipMemcpyDeviceToHost);
+    printf("sweep mode %d: subPanel8+bar %.0f cycles per sub-panel, trailing8+bar %.0f per sub-panel\n", mode,
+           h[0] / 800.0, h[1] / 800.0);
+  }
+  hipError_t e = hipDeviceSynchronize();
+  printf("%s\n", hipGetErrorString(e));
+  return 0;
+}
