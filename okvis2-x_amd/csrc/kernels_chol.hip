@@ -632,16 +632,92 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
     if (t == 0) P.st[w].gn_failed = 1;
 }
 
+// Backward substitution of the tile-parallel schedule (L_iI in the upper slot (I,i)), software
+// pipelined: the L and X operands of step I-1 do not depend on x, so their loads are issued
+// before step I's reductions (a single window is a chain of T steps, each otherwise waiting a full
+// memory latency). Same operations in the same order as backSubstituteY.
+constexpr int kBsPre = 4;  // prefetched tiles per step (further non-zero tiles are loaded in the step)
+struct BsOps {
+  double v[kBsPre][16];
+  double li[16];
+  int ti[kBsPre];
+  int n;
+};
+__device__ __forceinline__ void bsLoad(const double* S, int64_t ld, int T, const double* Linv, const uint8_t* nz, int I,
+                                       int col, int q, BsOps& o) {
+  o.n = 0;
+  int i = I + 1;
+#pragma unroll
+  for (int m = 0; m < kBsPre; ++m) {
+    while (i < T && !nz[i * T + I]) ++i;
+    o.ti[m] = i;
+    if (i < T) {
+      const double* Lt = S + I * kTile * ld + i * kTile + col;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) o.v[m][u] = Lt[(int64_t)(q + 4 * u) * ld];
+      ++o.n;
+      ++i;
+    }
+  }
+  const double* Li = Linv + (int64_t)I * kTile * kTile + col;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) o.li[u] = Li[(q + 4 * u) * kTile];
+}
+
 __global__ __launch_bounds__(256) void k_chol_bsub(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int w = blockIdx.x;
   if (!cholSelect(P, w)) return;
   const int64_t ld = P.win_fpad[w];
+  const int T = (int)(ld / kTile);
+  const double* S = P.S + P.win_soff[w];
+  const double* work = P.fwdF + P.win_fwdoff[w];
+  const double* Linv = P.Linv + P.win_linvoff[w];
   __shared__ double sA[8 * kTile];
   __shared__ double sy[kTile];
-  extern __shared__ double sxDyn[];
-  backSubstitute<true>(P, w, P.S + P.win_soff[w], ld, (int)(ld / kTile), P.fwdF + P.win_fwdoff[w],
-                 P.Linv + P.win_linvoff[w], P.tile_nz + P.win_tnzoff[w], sxDyn, sA, sy, threadIdx.x);
+  extern __shared__ double sx[];  // x (ld doubles), then the tile bitmap (T * T bytes)
+  uint8_t* nz = reinterpret_cast<uint8_t*>(sx + ld);
+  const int t = threadIdx.x, col = t & 63, q = t >> 6;
+  for (int e = t; e < T * T; e += 256) nz[e] = P.tile_nz[P.win_tnzoff[w] + e];
+  for (int e = t; e < ld; e += 256) sx[e] = work[e];
+  __syncthreads();
+  BsOps cur, nxt;
+  bsLoad(S, ld, T, Linv, nz, T - 1, col, q, cur);
+  for (int I = T - 1; I >= 0; --I) {
+    if (I > 0) bsLoad(S, ld, T, Linv, nz, I - 1, col, q, nxt);
+    double acc = 0.0;
+#pragma unroll
+    for (int m = 0; m < kBsPre; ++m)
+      if (m < cur.n) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc += cur.v[m][u] * sx[cur.ti[m] * kTile + q + 4 * u];
+      }
+    if (cur.n == kBsPre)  // non-zero tiles beyond the prefetched ones
+      for (int i = cur.ti[kBsPre - 1] + 1; i < T; ++i) {
+        if (!nz[i * T + I]) continue;
+        const double* Lt = S + I * kTile * ld + i * kTile + col;
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = Lt[(int64_t)(q + 4 * u) * ld];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) acc += v[u] * sx[i * kTile + q + 4 * u];
+      }
+    sA[q * kTile + col] = acc;
+    __syncthreads();
+    if (t < kTile) sy[t] = sx[I * kTile + t] - ((sA[t] + sA[kTile + t]) + (sA[2 * kTile + t] + sA[3 * kTile + t]));
+    __syncthreads();
+    double a = 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) a += (q + 4 * u >= col) ? cur.li[u] * sy[q + 4 * u] : 0.0;
+    sA[256 + q * kTile + col] = a;
+    __syncthreads();
+    if (t < kTile)
+      sx[I * kTile + t] = (sA[256 + t] + sA[256 + kTile + t]) + (sA[256 + 2 * kTile + t] + sA[256 + 3 * kTile + t]);
+    __syncthreads();
+    cur = nxt;
+  }
+  const int fdim = P.win_fdim[w];
+  for (int e = t; e < fdim; e += 256) P.yF[(size_t)P.win_foff[w] + e] = sx[e];
 }
 
 // ---- wave-specialised persistent schedule. A workgroup of 8 wavefronts holds two window slots
@@ -1153,7 +1229,8 @@ void launch_cholesky(const DevProblem& P, hipStream_t s) {
     const int nu = P.h_upd_begin[k + 1] - P.h_upd_begin[k];
     if (nu > 0) hipLaunchKernelGGL(k_chol_update, dim3(nu), dim3(256), 0, s, P.self, k);
   }
-  hipLaunchKernelGGL(k_chol_bsub, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
+  hipLaunchKernelGGL(k_chol_bsub, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad + P.max_tiles * P.max_tiles, s,
+                     P.self);
 }
 
 }  // namespace okg

@@ -507,20 +507,30 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
   const int xs = s.xcur, xd = 1 - s.xcur;
   double sn2 = 0.0, dn2 = 0.0, jr = 0.0;
   const int p0 = P.win_pose_range[2 * w], p1 = P.win_pose_range[2 * w + 1];
+  // (every operand of a block is loaded before its first store: the stores may alias the
+  // f-vectors for the compiler, and a single window is a chain of such rounds)
   for (int p = p0 + t; p < p1; p += kRB) {
     const int pf = P.pose_f[p];
     if (pf < 0) continue;
-    double delta[6];
+    double dg[6], gn[6], dia[6], sc[6], g[6], x[7];
     for (int c = 0; c < 6; ++c) {
       const size_t i = (size_t)foff + pf + c;
-      const double v = ca * P.dgF[i] + cb * P.gnF[i];
-      dn2 += v * v;
-      const double st = v / P.diagF[i];
-      P.stepF[i] = st;
-      delta[c] = st * P.sF[i];
-      jr += delta[c] * P.gF[i];
+      dg[c] = P.dgF[i];
+      gn[c] = P.gnF[i];
+      dia[c] = P.diagF[i];
+      sc[c] = P.sF[i];
+      g[c] = P.gF[i];
     }
-    const double* x = P.pose[xs] + 7 * (size_t)p;
+    for (int k = 0; k < 7; ++k) x[k] = P.pose[xs][7 * (size_t)p + k];
+    double delta[6];
+    for (int c = 0; c < 6; ++c) {
+      const double v = ca * dg[c] + cb * gn[c];
+      dn2 += v * v;
+      const double st = v / dia[c];
+      P.stepF[(size_t)foff + pf + c] = st;
+      delta[c] = st * sc[c];
+      jr += delta[c] * g[c];
+    }
     double* y = P.pose[xd] + 7 * (size_t)p;
     const Q dq = deltaQ(delta[3], delta[4], delta[5]);
     const Q q = qnormalize(qmul(dq, qnormalize(Q{x[3], x[4], x[5], x[6]})));
@@ -534,16 +544,24 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
   for (int b = b0 + t; b < b1; b += kRB) {
     const int sf = P.sb_f[b];
     if (sf < 0) continue;
-    const double* x = P.sb[xs] + 9 * (size_t)b;
     double* y = P.sb[xd] + 9 * (size_t)b;
+    double dg[9], gn[9], dia[9], sc[9], g[9], x[9];
     for (int c = 0; c < 9; ++c) {
       const size_t i = (size_t)foff + sf + c;
-      const double v = ca * P.dgF[i] + cb * P.gnF[i];
+      dg[c] = P.dgF[i];
+      gn[c] = P.gnF[i];
+      dia[c] = P.diagF[i];
+      sc[c] = P.sF[i];
+      g[c] = P.gF[i];
+      x[c] = P.sb[xs][9 * (size_t)b + c];
+    }
+    for (int c = 0; c < 9; ++c) {
+      const double v = ca * dg[c] + cb * gn[c];
       dn2 += v * v;
-      const double st = v / P.diagF[i];
-      P.stepF[i] = st;
-      jr += (st * P.sF[i]) * P.gF[i];
-      const double yv = x[c] + st * P.sF[i];
+      const double st = v / dia[c];
+      P.stepF[(size_t)foff + sf + c] = st;
+      jr += (st * sc[c]) * g[c];
+      const double yv = x[c] + st * sc[c];
       y[c] = yv;
       sn2 += (x[c] - yv) * (x[c] - yv);
     }

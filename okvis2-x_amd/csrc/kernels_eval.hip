@@ -821,9 +821,13 @@ __global__ __launch_bounds__(64) void k_eval_priors(const DevProblem* __restrict
     int xs, lb;
     if (!evalSelect(P, w, mode, xs, lb)) return;
     if (P.pose_f[P.pp_block[i]] < 0 && mode != 2) return;  // prior on a constant block: fixed_cost
-    const double* pose = P.pose[xs] + 7 * (size_t)P.pp_block[i];
-    const double* m = P.pp_meas + 7 * (size_t)i;
-    const double* L = P.pp_L + 36 * (size_t)i;
+    // all operands in registers before the first store (a single window is a latency chain)
+    double pose[7], m[7], L[36];
+    for (int k = 0; k < 7; ++k) {
+      pose[k] = P.pose[xs][7 * (size_t)P.pp_block[i] + k];
+      m[k] = P.pp_meas[7 * (size_t)i + k];
+    }
+    for (int k = 0; k < 36; ++k) L[k] = P.pp_L[36 * (size_t)i + k];
     const Q q = qnormalize(Q{pose[3], pose[4], pose[5], pose[6]});
     const Q dq = qmul(Q{m[3], m[4], m[5], m[6]}, qinv(q));
     const double e[6] = {m[0] - pose[0], m[1] - pose[1], m[2] - pose[2], 2 * dq.x, 2 * dq.y, 2 * dq.z};
@@ -855,12 +859,10 @@ __global__ __launch_bounds__(64) void k_eval_priors(const DevProblem* __restrict
     int xs, lb;
     if (!evalSelect(P, w, mode, xs, lb)) return;
     if (P.sb_f[P.sbp_block[i]] < 0 && mode != 2) return;
-    const double* sbv = P.sb[xs] + 9 * (size_t)P.sbp_block[i];
-    const double* m = P.sbp_meas + 9 * (size_t)i;
-    const double* L = P.sbp_L + 81 * (size_t)i;
+    double e[9], L[81];
+    for (int k = 0; k < 9; ++k) e[k] = P.sbp_meas[9 * (size_t)i + k] - P.sb[xs][9 * (size_t)P.sbp_block[i] + k];
+    for (int k = 0; k < 81; ++k) L[k] = P.sbp_L[81 * (size_t)i + k];
     double* lin = P.sbp_lin[lb] + 90 * (size_t)i;
-    double e[9];
-    for (int k = 0; k < 9; ++k) e[k] = m[k] - sbv[k];
     double c = 0;
     for (int r = 0; r < 9; ++r) {
       double s = 0;
@@ -886,7 +888,8 @@ __global__ __launch_bounds__(64) void k_eval_priors(const DevProblem* __restrict
   const double* p0 = P.pose[xs] + 7 * (size_t)P.rp_blocks[2 * k];
   const double* p1 = P.pose[xs] + 7 * (size_t)P.rp_blocks[2 * k + 1];
   const double* dx = P.rp_dx + 6 * (size_t)k;
-  const double* Jq = P.rp_J + 36 * (size_t)k;
+  double Jq[36];
+  for (int e = 0; e < 36; ++e) Jq[e] = P.rp_J[36 * (size_t)k + e];
   const double* lp = P.rp_lp + 7 * (size_t)k;
   const bool relErr = P.rp_kind[k] == 1;
   const Q q0 = qnormalize(Q{p0[3], p0[4], p0[5], p0[6]}), q1 = qnormalize(Q{p1[3], p1[4], p1[5], p1[6]});

@@ -1249,7 +1249,14 @@ struct okvisgpu_ctx {
     if (iterGraph) return;
     hipGraph_t g;
     HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-    launchIterationForked();
+    // Few windows: one stream (a cross-stream edge of the graph costs ~10 us, more than the
+    // overlap of a single window's small kernels gains: S50 1488 -> 1614 it/s); a full batch
+    // keeps the fork streams (2,048 S50 windows: 135.7k -> 138.5k window-it/s). Env override
+    // OKVISGPU_SERIAL_GRAPH=0|1 (measurements).
+    const char* ser = std::getenv("OKVISGPU_SERIAL_GRAPH");
+    const bool serial = ser && (ser[0] == '0' || ser[0] == '1') ? ser[0] == '1' : P.n_win < cuCount;
+    if (serial) launchIteration();
+    else launchIterationForked();
     HIPCHK(hipStreamEndCapture(stream, &g));
     HIPCHK(hipGraphInstantiate(&iterGraph, g, nullptr, nullptr, 0));
     HIPCHK(hipGraphDestroy(g));

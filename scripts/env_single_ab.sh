@@ -1,0 +1,17 @@
+#!/bin/bash
+# A/B of an environment knob: single-window rate and the default batched bench value.
+# Usage (via gpurun): bash scripts/env_single_ab.sh TAG VAR "v1 v2 ..."
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+TAG=$1; VAR=$2
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+for v in $3; do
+  env $VAR=$v timeout -k 10 120 python scripts/single_window.py 50 0 > $OUT/single_$v.txt 2>&1 || { cat $OUT/single_$v.txt; exit 1; }
+  env $VAR=$v timeout -k 10 300 python bench.py --no-cpu --no-latency --no-profile --steps 10 --warmup 3 > $OUT/bench_$v.json 2> $OUT/bench_$v.err || { echo "bench $v rc=$?"; tail -20 $OUT/bench_$v.err; exit 1; }
+  python3 -c "
+import json; d=json.loads(open('$OUT/bench_$v.json').read().strip().splitlines()[-1])
+print('$VAR=$v', open('$OUT/single_$v.txt').read().split(',')[0], '| batch', round(d['value']), 'ms/it', round(d['ms_per_step'],3))
+"
+done
