@@ -21,6 +21,7 @@
 // and B[l>>4][l&15]; result reg r of lane l is C[(l>>4) + 4r][l&15] (cdna_hip_programming.md §3).
 #include "device_problem.hpp"
 #include "launch.hpp"
+#include "okvisgpu_math.hpp"
 
 namespace okg {
 
@@ -63,7 +64,7 @@ __device__ __forceinline__ void loadTile(const double* A, int64_t ld, int r0, in
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int e = t + 256 * u, r = e >> 5, c = 2 * (e & 31);
-    v[u] = *reinterpret_cast<const double2*>(A + (int64_t)(r0 + r) * ld + c0 + c);
+    v[u] = *gmem(reinterpret_cast<const double2*>(A + (int64_t)(r0 + r) * ld + c0 + c));
   }
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
@@ -108,7 +109,7 @@ __device__ __forceinline__ void storeTile(double* A, int64_t ld, int r0g, int c0
       for (int reg = 0; reg < 4; ++reg) {
         const int rr = r0 + 16 * a + (lane >> 4) + 4 * reg;
         const int cc = c0 + 16 * b + (lane & 15);
-        double* dst = A + (int64_t)(r0g + rr) * ld + c0g + cc;
+        auto dst = gmemw(A + (int64_t)(r0g + rr) * ld + c0g + cc);
         if (SUB) *dst -= acc[a][b][reg];
         else *dst = acc[a][b][reg];
       }
@@ -124,7 +125,7 @@ __device__ __forceinline__ void loadC(const double* A, int64_t ld, dbl4 c[2][2],
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg)
-        c[a][b][reg] = A[(int64_t)(r0 + 16 * a + (lane >> 4) + 4 * reg) * ld + c0 + 16 * b + (lane & 15)];
+        c[a][b][reg] = gmem(A)[(int64_t)(r0 + 16 * a + (lane >> 4) + 4 * reg) * ld + c0 + 16 * b + (lane & 15)];
 }
 __device__ __forceinline__ void storeTileSub(double* A, int64_t ld, const dbl4 c[2][2], const dbl4 acc[2][2], int t) {
   const int wave = t >> 6, lane = t & 63;
@@ -135,7 +136,7 @@ __device__ __forceinline__ void storeTileSub(double* A, int64_t ld, const dbl4 c
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg)
-        A[(int64_t)(r0 + 16 * a + (lane >> 4) + 4 * reg) * ld + c0 + 16 * b + (lane & 15)] = c[a][b][reg] - acc[a][b][reg];
+        gmemw(A)[(int64_t)(r0 + 16 * a + (lane >> 4) + 4 * reg) * ld + c0 + 16 * b + (lane & 15)] = c[a][b][reg] - acc[a][b][reg];
 }
 
 __device__ __forceinline__ double readlaneD(double v, int lane) {  // v of `lane`, wave-uniform
@@ -143,6 +144,14 @@ __device__ __forceinline__ double readlaneD(double v, int lane) {  // v of `lane
   const int lo = __builtin_amdgcn_readlane((int)b, lane);
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Workgroup barrier that orders LDS only: __syncthreads() also waits for every outstanding global
+// load (vmcnt(0)), which defeats loads prefetched across the barrier.
+__device__ __forceinline__ void ldsBarrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 // 1/sqrt(d) to ~1 ulp: v_rsq_f64 (~5e-8 relative) refined by two Newton steps (measured on
@@ -401,64 +410,143 @@ __device__ void panelTile(double* Aik, int64_t ld, double* worki, double* sA, co
     for (int c = 16 * q; c < 16 * q + 16; ++c) a += sA[row * kLd + c] * sz[c];
     a += __shfl_xor(a, 1, 64);
     a += __shfl_xor(a, 2, 64);
-    if (q == 0) worki[row] -= a;
+    if (q == 0) gmemw(worki)[row] -= a;
   }
   __syncthreads();  // sA is free for the next panel
   storeTile<false>(Aik, ld, 0, 0, acc, t);
 }
 
-// Backward substitution x = L^-T y, x := y_F. sx (LDS, ld doubles) holds y on entry and x on
-// exit; per block row I the 16 row loads of every non-zero tile below are issued together, then
-// x_I = X_II^T (y_I - sum_i L_iI^T x_i) with the stored diagonal inverse. Threads 0..255 work;
-// any further threads of the workgroup only take part in the barriers.
-template <bool UPPER>
-__device__ void backSubstituteY(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* Linv,
-                                const uint8_t* nz, double* sx, double* sA, double* sy, int t) {
-  const bool act = t < 256;
-  const int col = t & 63, q = (t >> 6) & 3;
-  for (int I = T - 1; I >= 0; --I) {
-    double acc = 0.0;
-    double li[16];
-    if (act) {
-      for (int i = I + 1; i < T; ++i) {
-        if (!nz[i * T + I]) continue;
-        const double* Lt = UPPER ? S + I * kTile * ld + i * kTile + col : S + i * kTile * ld + I * kTile + col;
-        double v[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = Lt[(int64_t)(q + 4 * u) * ld];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) acc += v[u] * sx[i * kTile + q + 4 * u];
-      }
-      const double* Li = Linv + (int64_t)I * kTile * kTile + col;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) li[u] = Li[(q + 4 * u) * kTile];
-      sA[q * kTile + col] = acc;
-    }
-    __syncthreads();
-    if (t < kTile) sy[t] = sx[I * kTile + t] - ((sA[t] + sA[kTile + t]) + (sA[2 * kTile + t] + sA[3 * kTile + t]));
-    __syncthreads();
-    if (act) {
-      double a = 0.0;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) a += (q + 4 * u >= col) ? li[u] * sy[q + 4 * u] : 0.0;
-      sA[256 + q * kTile + col] = a;
-    }
-    __syncthreads();
-    if (t < kTile)
-      sx[I * kTile + t] = (sA[256 + t] + sA[256 + kTile + t]) + (sA[256 + 2 * kTile + t] + sA[256 + 3 * kTile + t]);
-    __syncthreads();
-  }
-  const int fdim = P.win_fdim[w];
-  for (int e = t; e < fdim; e += blockDim.x) P.yF[(size_t)P.win_foff[w] + e] = sx[e];
-}
 
-// As backSubstituteY with y taken from work (global).
+// Backward substitution x = L^-T y, x := y_F, with the stored diagonal inverses: per block row I
+// (from the last), x_I = X_II^T (y_I - sum_i L_iI^T x_i) over the non-zero tiles below. The work
+// of a step is laid out over 1024 virtual threads vt: column pair (2 cp, 2 cp + 1), cp = vt & 31,
+// rows rg + 32u (rg = vt >> 5, u < 2) of every operand tile (2 16-byte loads per tile), partials
+// summed over the 32 row groups in a fixed tree. The tile-parallel kernel runs them as real
+// threads (few registers per thread, so the next step's loads fit in flight); the persistent
+// kernel runs 4 per thread in the same order, so both give the same bits. UPPER: L_iI is stored
+// in the upper slot (I,i) (tile-parallel schedule), else at (i,I).
+constexpr int kBsThreads = 1024;
+constexpr int kBsPre = 3;  // operand tiles per step from the list (further ones are loaded in the step)
+struct BsOps {
+  double2 v[kBsPre][2];
+  double2 li[2];
+};
 template <bool UPPER>
+__device__ __forceinline__ const double* bsTile(const double* S, int64_t ld, int I, int i) {
+  return UPPER ? S + (int64_t)I * kTile * ld + i * kTile : S + (int64_t)i * kTile * ld + I * kTile;
+}
+// lst: count of non-zero tiles below I (capped at kBsPre), then their block rows ascending.
+// Loads are unconditional (an absent tile reads the diagonal one and is masked): loads under a
+// branch make the wait-count insertion fall back to vmcnt(0).
+template <bool UPPER>
+__device__ __forceinline__ void bsLoad(const double* S, int64_t ld, const double* Linv, const int* lst, int I, int vt,
+                                       BsOps& o) {
+  const int c2 = 2 * (vt & 31), rg = vt >> 5;
+#pragma unroll
+  for (int m = 0; m < kBsPre; ++m) {
+    const double* Lt = bsTile<UPPER>(S, ld, I, m < lst[0] ? lst[1 + m] : I) + c2;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) o.v[m][u] = *gmem(reinterpret_cast<const double2*>(Lt + (int64_t)(rg + 32 * u) * ld));
+  }
+  const double* Li = Linv + (int64_t)I * kTile * kTile + c2;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) o.li[u] = *gmem(reinterpret_cast<const double2*>(Li + (rg + 32 * u) * kTile));
+}
+__device__ __forceinline__ double sum32(const double* p) {  // p[64 k], k < 32, fixed tree
+  double a[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] = (p[kTile * k] + p[kTile * (k + 8)]) + (p[kTile * (k + 16)] + p[kTile * (k + 24)]);
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+// Non-zero tiles below I beyond the listed ones (rare; out of line, so the wait counts of the
+// pipelined loads around the call site stay exact).
+template <bool UPPER>
+__device__ __noinline__ double2 bsExtra(const double* S, int64_t ld, int T, const uint8_t* nz, int last, int I,
+                                        const double* sx, int vt, double ax, double ay) {
+  const int c2 = 2 * (vt & 31), rg = vt >> 5;
+  for (int i = last + 1; i < T; ++i) {
+    if (!nz[i * T + I]) continue;
+    const double* Lt = bsTile<UPPER>(S, ld, I, i) + c2;
+    const double* xi = sx + i * kTile + rg;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const double2 v = *gmem(reinterpret_cast<const double2*>(Lt + (int64_t)(rg + 32 * u) * ld));
+      ax += v.x * xi[32 * u];
+      ay += v.y * xi[32 * u];
+    }
+  }
+  return double2{ax, ay};
+}
+// Partial (L^T x) of virtual thread vt for step I -> sA[rg][c2..c2+1] (sx: y of unsolved rows, x of solved).
+template <bool UPPER>
+__device__ __forceinline__ void bsPartial(const double* S, int64_t ld, int T, const uint8_t* nz, const int* lst, int I,
+                                          const BsOps& c, const double* sx, double* sA, int vt) {
+  const int c2 = 2 * (vt & 31), rg = vt >> 5;
+  double ax = 0.0, ay = 0.0;
+#pragma unroll
+  for (int m = 0; m < kBsPre; ++m) {
+    const bool on = m < lst[0];
+    const double* xi = sx + (on ? lst[1 + m] : I) * kTile + rg;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {  // a masked tile adds exact zeros
+      ax += (on ? c.v[m][u].x : 0.0) * xi[32 * u];
+      ay += (on ? c.v[m][u].y : 0.0) * xi[32 * u];
+    }
+  }
+  if (lst[0] == kBsPre) {
+    const double2 e = bsExtra<UPPER>(S, ld, T, nz, lst[kBsPre], I, sx, vt, ax, ay);
+    ax = e.x;
+    ay = e.y;
+  }
+  sA[rg * kTile + c2] = ax;
+  sA[rg * kTile + c2 + 1] = ay;
+}
+// Partial (X_II^T y_I) of virtual thread vt -> sA (sy: y_I corrected).
+__device__ __forceinline__ void bsDiag(const BsOps& c, const double* sy, double* sA, int vt) {
+  const int c2 = 2 * (vt & 31), rg = vt >> 5;
+  double bx = 0.0, by = 0.0;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int r = rg + 32 * u;
+    bx += (r >= c2) ? c.li[u].x * sy[r] : 0.0;
+    by += (r >= c2 + 1) ? c.li[u].y * sy[r] : 0.0;
+  }
+  sA[rg * kTile + c2] = bx;
+  sA[rg * kTile + c2 + 1] = by;
+}
+// The non-zero tiles below block row I (bitmap nz), in the lst format of bsLoad.
+__device__ __forceinline__ void bsList(const uint8_t* nz, int T, int I, int* lst) {
+  int n = 0;
+  for (int i = I + 1; i < T && n < kBsPre; ++i)
+    if (nz[i * T + I]) lst[1 + n++] = i;
+  lst[0] = n;
+}
+// Persistent schedule (256 threads, 4 virtual threads each): y from work (global) into sx, then
+// the steps with operands loaded in-step. sA: >= 32 x 64 doubles.
 __device__ void backSubstitute(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* work,
                                const double* Linv, const uint8_t* nz, double* sx, double* sA, double* sy, int t) {
   for (int e = t; e < ld; e += blockDim.x) sx[e] = work[e];
   __syncthreads();
-  backSubstituteY<UPPER>(P, w, S, ld, T, Linv, nz, sx, sA, sy, t);
+  constexpr int kV = kBsThreads / 256;
+  for (int I = T - 1; I >= 0; --I) {
+    int lst[1 + kBsPre];
+    bsList(nz, T, I, lst);
+    BsOps c[kV];
+#pragma unroll
+    for (int k = 0; k < kV; ++k) bsLoad<false>(S, ld, Linv, lst, I, t + 256 * k, c[k]);
+#pragma unroll
+    for (int k = 0; k < kV; ++k) bsPartial<false>(S, ld, T, nz, lst, I, c[k], sx, sA, t + 256 * k);
+    __syncthreads();
+    if (t < kTile) sy[t] = sx[I * kTile + t] - sum32(sA + t);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kV; ++k) bsDiag(c[k], sy, sA, t + 256 * k);
+    __syncthreads();
+    if (t < kTile) sx[I * kTile + t] = sum32(sA + t);
+    __syncthreads();
+  }
+  const int fdim = P.win_fdim[w];
+  for (int e = t; e < fdim; e += blockDim.x) P.yF[(size_t)P.win_foff[w] + e] = sx[e];
 }
 
 __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restrict__ Pp) {
@@ -516,7 +604,7 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
   }
   CLK(2)
   extern __shared__ double sxDyn[];
-  backSubstitute<false>(P, w, S, ld, T, work, Linv, nz, sxDyn, sA, sy, t);
+  backSubstitute(P, w, S, ld, T, work, Linv, nz, sxDyn, sA, sy, t);
   CLK(3)
 #ifdef OKG_CHOL_CLOCK
   if (blockIdx.x == 0 && t == 0)
@@ -632,39 +720,14 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
     if (t == 0) P.st[w].gn_failed = 1;
 }
 
-// Backward substitution of the tile-parallel schedule (L_iI in the upper slot (I,i)), software
-// pipelined: the L and X operands of step I-1 do not depend on x, so their loads are issued
-// before step I's reductions (a single window is a chain of T steps, each otherwise waiting a full
-// memory latency). Same operations in the same order as backSubstituteY.
-constexpr int kBsPre = 4;  // prefetched tiles per step (further non-zero tiles are loaded in the step)
-struct BsOps {
-  double v[kBsPre][16];
-  double li[16];
-  int ti[kBsPre];
-  int n;
-};
-__device__ __forceinline__ void bsLoad(const double* S, int64_t ld, int T, const double* Linv, const uint8_t* nz, int I,
-                                       int col, int q, BsOps& o) {
-  o.n = 0;
-  int i = I + 1;
-#pragma unroll
-  for (int m = 0; m < kBsPre; ++m) {
-    while (i < T && !nz[i * T + I]) ++i;
-    o.ti[m] = i;
-    if (i < T) {
-      const double* Lt = S + I * kTile * ld + i * kTile + col;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) o.v[m][u] = Lt[(int64_t)(q + 4 * u) * ld];
-      ++o.n;
-      ++i;
-    }
-  }
-  const double* Li = Linv + (int64_t)I * kTile * kTile + col;
-#pragma unroll
-  for (int u = 0; u < 16; ++u) o.li[u] = Li[(q + 4 * u) * kTile];
-}
-
-__global__ __launch_bounds__(256) void k_chol_bsub(const DevProblem* __restrict__ Pp) {
+// Tile-parallel schedule's backward substitution: 512 threads (2 virtual threads each), software
+// pipelined. Step I-1's operands do not depend on x, so their loads are issued before step I's
+// reductions (a single window is a chain of T steps that would otherwise each wait a full memory
+// latency); two register sets, no copies; barriers order LDS only, so the loads stay in flight
+// across them. Same operations in the same order as backSubstitute.
+constexpr int kBsReal = 512;
+__global__ __launch_bounds__(kBsReal) void k_chol_bsub(const DevProblem* __restrict__ Pp) {
+  constexpr int kV = kBsThreads / kBsReal;
   const DevProblem& P = *Pp;
   const int w = blockIdx.x;
   if (!cholSelect(P, w)) return;
@@ -673,51 +736,51 @@ __global__ __launch_bounds__(256) void k_chol_bsub(const DevProblem* __restrict_
   const double* S = P.S + P.win_soff[w];
   const double* work = P.fwdF + P.win_fwdoff[w];
   const double* Linv = P.Linv + P.win_linvoff[w];
-  __shared__ double sA[8 * kTile];
+  __shared__ double sA[32 * kTile];
   __shared__ double sy[kTile];
-  extern __shared__ double sx[];  // x (ld doubles), then the tile bitmap (T * T bytes)
-  uint8_t* nz = reinterpret_cast<uint8_t*>(sx + ld);
-  const int t = threadIdx.x, col = t & 63, q = t >> 6;
-  for (int e = t; e < T * T; e += 256) nz[e] = P.tile_nz[P.win_tnzoff[w] + e];
-  for (int e = t; e < ld; e += 256) sx[e] = work[e];
+  // x (ld doubles), then per block row its tile list ((1 + kBsPre) ints), then the bitmap (T * T bytes)
+  extern __shared__ double sx[];
+  int* lists = reinterpret_cast<int*>(sx + ld);
+  uint8_t* nz = reinterpret_cast<uint8_t*>(lists + (1 + kBsPre) * T);
+  const int t = threadIdx.x;
+  CLK_INIT
+  for (int e = t; e < T * T; e += kBsReal) nz[e] = P.tile_nz[P.win_tnzoff[w] + e];
+  for (int e = t; e < ld; e += kBsReal) sx[e] = work[e];
+  if (t < T) bsList(P.tile_nz + P.win_tnzoff[w], T, t, lists + (1 + kBsPre) * t);
   __syncthreads();
-  BsOps cur, nxt;
-  bsLoad(S, ld, T, Linv, nz, T - 1, col, q, cur);
-  for (int I = T - 1; I >= 0; --I) {
-    if (I > 0) bsLoad(S, ld, T, Linv, nz, I - 1, col, q, nxt);
-    double acc = 0.0;
+  BsOps ping[kV], pong[kV];
+  auto load = [&](int I, BsOps* o) {
 #pragma unroll
-    for (int m = 0; m < kBsPre; ++m)
-      if (m < cur.n) {
+    for (int k = 0; k < kV; ++k) bsLoad<true>(S, ld, Linv, lists + (1 + kBsPre) * I, I, t + kBsReal * k, o[k]);
+  };
+  auto step = [&](int I, const BsOps* c) {
+    const int* lst = lists + (1 + kBsPre) * I;
 #pragma unroll
-        for (int u = 0; u < 16; ++u) acc += cur.v[m][u] * sx[cur.ti[m] * kTile + q + 4 * u];
-      }
-    if (cur.n == kBsPre)  // non-zero tiles beyond the prefetched ones
-      for (int i = cur.ti[kBsPre - 1] + 1; i < T; ++i) {
-        if (!nz[i * T + I]) continue;
-        const double* Lt = S + I * kTile * ld + i * kTile + col;
-        double v[16];
+    for (int k = 0; k < kV; ++k) bsPartial<true>(S, ld, T, nz, lst, I, c[k], sx, sA, t + kBsReal * k);
+    ldsBarrier();
+    if (t < kTile) sy[t] = sx[I * kTile + t] - sum32(sA + t);
+    ldsBarrier();
 #pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = Lt[(int64_t)(q + 4 * u) * ld];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) acc += v[u] * sx[i * kTile + q + 4 * u];
-      }
-    sA[q * kTile + col] = acc;
-    __syncthreads();
-    if (t < kTile) sy[t] = sx[I * kTile + t] - ((sA[t] + sA[kTile + t]) + (sA[2 * kTile + t] + sA[3 * kTile + t]));
-    __syncthreads();
-    double a = 0.0;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) a += (q + 4 * u >= col) ? cur.li[u] * sy[q + 4 * u] : 0.0;
-    sA[256 + q * kTile + col] = a;
-    __syncthreads();
-    if (t < kTile)
-      sx[I * kTile + t] = (sA[256 + t] + sA[256 + kTile + t]) + (sA[256 + 2 * kTile + t] + sA[256 + 3 * kTile + t]);
-    __syncthreads();
-    cur = nxt;
+    for (int k = 0; k < kV; ++k) bsDiag(c[k], sy, sA, t + kBsReal * k);
+    ldsBarrier();
+    if (t < kTile) sx[I * kTile + t] = sum32(sA + t);
+    ldsBarrier();
+  };
+  load(T - 1, ping);
+  CLK(12)
+  for (int I = T - 1; I >= 0; I -= 2) {  // (loads clamped, not skipped: no loads under a branch)
+    load(I > 0 ? I - 1 : 0, pong);
+    step(I, ping);
+    if (I == 0) break;
+    load(I > 1 ? I - 2 : 0, ping);
+    step(I - 1, pong);
   }
+  CLK(13)
   const int fdim = P.win_fdim[w];
-  for (int e = t; e < fdim; e += 256) P.yF[(size_t)P.win_foff[w] + e] = sx[e];
+  for (int e = t; e < fdim; e += kBsReal) P.yF[(size_t)P.win_foff[w] + e] = sx[e];
+#ifdef OKG_CHOL_CLOCK
+  if (blockIdx.x == 0 && t == 0) printf("BSUBCLK T=%d init %llu steps %llu (x10ns)\n", T, g_cholClk[12], g_cholClk[13]);
+#endif
 }
 
 // ---- wave-specialised persistent schedule. A workgroup of 8 wavefronts holds two window slots
@@ -803,7 +866,7 @@ __device__ __forceinline__ void gemmPair(const double* A, int lda, const double*
         fa[m][2 * u] = pa[2 * u];
         fa[m][2 * u + 1] = pa[2 * u + 1];
       } else {
-        const double2 v = *reinterpret_cast<const double2*>(pa + 2 * u);
+        const double2 v = *gmem(reinterpret_cast<const double2*>(pa + 2 * u));
         fa[m][2 * u] = v.x;
         fa[m][2 * u + 1] = v.y;
       }
@@ -811,7 +874,7 @@ __device__ __forceinline__ void gemmPair(const double* A, int lda, const double*
         fb[m][2 * u] = pb[2 * u];
         fb[m][2 * u + 1] = pb[2 * u + 1];
       } else {
-        const double2 v = *reinterpret_cast<const double2*>(pb + 2 * u);
+        const double2 v = *gmem(reinterpret_cast<const double2*>(pb + 2 * u));
         fb[m][2 * u] = v.x;
         fb[m][2 * u + 1] = v.y;
       }
@@ -844,7 +907,7 @@ __device__ __forceinline__ void storeBlock(double* C, int ld, int bi, const dbl4
   for (int reg = 0; reg < 4; ++reg) dst[4 * reg * ld] = acc[reg];
 }
 __device__ __forceinline__ dbl4 subFromBlock(const double* C, int ld, int bi, const dbl4& acc, int lane) {
-  const double* src = C + (16 * (bi >> 2) + (lane >> 4)) * ld + 16 * (bi & 3) + (lane & 15);
+  const auto src = gmem(C + (16 * (bi >> 2) + (lane >> 4)) * ld + 16 * (bi & 3) + (lane & 15));
   dbl4 r;
 #pragma unroll
   for (int reg = 0; reg < 4; ++reg) r[reg] = src[4 * reg * ld] - acc[reg];
@@ -908,7 +971,7 @@ __device__ __forceinline__ void updateBlocksLds(double* C, int ld, const double*
 __device__ __forceinline__ void stageTile(double* dst, const double* src, int ld, int gt, int nthr) {
   for (int e = gt; e < kTile * kTile / 2; e += nthr) {
     const int r = e >> 5, c = 2 * (e & 31);
-    const double2 v = *reinterpret_cast<const double2*>(src + r * ld + c);
+    const double2 v = *gmem(reinterpret_cast<const double2*>(src + r * ld + c));
     dst[r * kLd + c] = v.x;
     dst[r * kLd + c + 1] = v.y;
   }
@@ -1229,7 +1292,8 @@ void launch_cholesky(const DevProblem& P, hipStream_t s) {
     const int nu = P.h_upd_begin[k + 1] - P.h_upd_begin[k];
     if (nu > 0) hipLaunchKernelGGL(k_chol_update, dim3(nu), dim3(256), 0, s, P.self, k);
   }
-  hipLaunchKernelGGL(k_chol_bsub, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad + P.max_tiles * P.max_tiles, s,
+  hipLaunchKernelGGL(k_chol_bsub, dim3(P.n_win), dim3(kBsReal),
+                     sizeof(double) * P.max_fpad + sizeof(int) * (1 + kBsPre) * P.max_tiles + P.max_tiles * P.max_tiles, s,
                      P.self);
 }
 

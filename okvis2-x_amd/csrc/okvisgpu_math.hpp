@@ -26,6 +26,19 @@ template <typename T>
 __device__ __forceinline__ gptr<T> gmem(const T* p) {
   return (gptr<T>)p;
 }
+// Writable global pointer (global_store: counts in vmcnt only; a flat store also counts in
+// lgkmcnt, so every LDS wait would wait for it too).
+#if defined(__HIP_DEVICE_COMPILE__)
+template <typename T>
+using gwptr = __attribute__((address_space(1))) T*;
+#else
+template <typename T>
+using gwptr = T*;
+#endif
+template <typename T>
+__device__ __forceinline__ gwptr<T> gmemw(T* p) {
+  return (gwptr<T>)p;
+}
 
 struct Q {
   double x, y, z, w;

@@ -85,6 +85,64 @@ __global__ void k_sweep(const double* A, double* out, long long* cyc, int reps, 
   if (t == 0) { cyc[0] = tsub; cyc[1] = ttr; }
 }
 
+__global__ void k_clock(double* out, long long* cyc, int n) {
+  double a = out[threadIdx.x], b = 1.0000001;
+  long long t0 = clock64(), w0 = wall_clock64();
+  for (int i = 0; i < n; ++i) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) a = fma(a, b, 1e-9);
+  }
+  long long t1 = clock64(), w1 = wall_clock64();
+  out[threadIdx.x] = a;
+  if (threadIdx.x == 0) { cyc[0] = t1 - t0; cyc[1] = w1 - w0; }
+}
+
+__device__ __forceinline__ void ldsBarrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+__device__ __forceinline__ double sum32(const double* p) {
+  double a[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] = (p[64 * k] + p[64 * (k + 8)]) + (p[64 * (k + 16)] + p[64 * (k + 24)]);
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+// mode 0: full step (partials, 4 barriers, 2 sum32); 1: barriers only; 2: __syncthreads barriers only
+__global__ void k_bstep(double* out, long long* cyc, int n, int mode) {
+  __shared__ double sA[32 * 64], sx[768], sy[64];
+  const int t = threadIdx.x;
+  for (int e = t; e < 768; e += blockDim.x) sx[e] = e;
+  __syncthreads();
+  long long t0 = clock64();
+  for (int I = n - 1; I >= 0; --I) {
+    if (mode == 0) {
+      for (int k = 0; k < 2; ++k) {
+        const int vt = t + 512 * k, c2 = 2 * (vt & 31), rg = vt >> 5;
+        double ax = 0, ay = 0;
+        for (int m = 0; m < 3; ++m) { ax += sx[(m + 1) * 64 + rg] * 0.5; ay += sx[(m + 1) * 64 + rg + 32] * 0.25; }
+        sA[rg * 64 + c2] = ax; sA[rg * 64 + c2 + 1] = ay;
+      }
+      ldsBarrier();
+      if (t < 64) sy[t] = sx[(I % 12) * 64 + t] - sum32(sA + t);
+      ldsBarrier();
+      for (int k = 0; k < 2; ++k) {
+        const int vt = t + 512 * k, c2 = 2 * (vt & 31), rg = vt >> 5;
+        sA[rg * 64 + c2] = sy[rg] * 0.5; sA[rg * 64 + c2 + 1] = sy[rg + 32] * 0.5;
+      }
+      ldsBarrier();
+      if (t < 64) sx[(I % 12) * 64 + t] = sum32(sA + t) * 1e-3;
+      ldsBarrier();
+    } else if (mode == 1) {
+      ldsBarrier(); ldsBarrier(); ldsBarrier(); ldsBarrier();
+    } else {
+      __syncthreads(); __syncthreads(); __syncthreads(); __syncthreads();
+    }
+  }
+  long long t1 = clock64();
+  if (t == 0) { cyc[0] = t1 - t0; out[0] = sx[5]; }
+}
+
 int main() {
   double *d, *o;
   long long* c;
@@ -101,6 +159,12 @@ int main() {
   k_chain<<<1, 64>>>(o, c, n);
   hipMemcpy(h, c, 8, hipMemcpyDeviceToHost);
   printf("fp64 fma dependent chain: %.2f cycles per op\n", (double)h[0] / (16.0 * n));
+  for (int rep = 0; rep < 3; ++rep) {
+    k_clock<<<1, 64>>>(o, c, 20000);
+    hipMemcpy(h, c, 16, hipMemcpyDeviceToHost);
+    printf("clock64 %lld ticks over %lld wall ticks (%.0f MHz wall): shader clock %.0f MHz\n", h[0], h[1], 100.0,
+           100.0 * h[0] / h[1]);
+  }
   k_rsq<<<1, 64>>>(o, c, n);
   hipMemcpy(h, c, 8, hipMemcpyDeviceToHost);
   printf("rsqrtRefined + add chain: %.2f cycles per step\n", (double)h[0] / n);
@@ -113,6 +177,12 @@ int main() {
     printf("sweep mode %d: subPanel8+bar %.0f cycles per sub-panel, trailing8+bar %.0f per sub-panel\n", mode,
            h[0] / 800.0, h[1] / 800.0);
   }
+  for (int nt = 256; nt <= 1024; nt *= 2)
+    for (int mode = 0; mode < 3; ++mode) {
+      k_bstep<<<1, nt>>>(o, c, 120, mode);
+      hipMemcpy(h, c, 8, hipMemcpyDeviceToHost);
+      printf("bsub step threads %d mode %d: %.0f cycles per step\n", nt, mode, h[0] / 120.0);
+    }
   hipError_t e = hipDeviceSynchronize();
   printf("%s\n", hipGetErrorString(e));
   return 0;
