@@ -188,24 +188,44 @@ __device__ __forceinline__ void storeC16(double* c, int ldc, const dbl4& v, int 
   for (int r = 0; r < 4; ++r) c[((lane >> 4) + 4 * r) * ldc + (lane & 15)] = v[r];
 }
 
+struct WsFlags {
+  int xReady, diagReady, xFree, fail, gbar, sbar;
+};
+
+__device__ __forceinline__ int ldsAcquire(int* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void ldsRelease(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Wave-uniform wait for *p >= v; false once the factor wavefront reported a failed pivot.
+__device__ __forceinline__ bool waitFlag(int* p, int v, int* fail) {
+  for (;;) {
+    if (ldsAcquire(p) >= v) return true;
+    if (ldsAcquire(fail)) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+// Barrier of n wavefronts on a monotonic arrival counter (gen counts this wavefront's barriers).
+__device__ __forceinline__ void waveBarrier(int* ctr, int& gen, int n, int lane) {
+  ++gen;
+  if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (ldsAcquire(ctr) < gen * n) __builtin_amdgcn_s_sleep(1);
+}
+
 // One 8-column sub-panel of the in-LDS 64x64 LLT on one wavefront (lane = row i of the tile; the
 // rows of the sub-panel's 8x8 diagonal block D are rows c0..c0+7). No cross-lane traffic in the
 // column chain: every lane loads D (LDS broadcast reads) and factors it redundantly in registers,
-// then solves its own row against it (row TRSM), so the 8 dependent pivots cost only the FP64
-// latency of rsqrt + scaling + the next pivot update. Writes L (rows >= c0, lower part), 1/L_cc
-// to sRl and the 8x8 diagonal block of X = L^-1 (lanes 0..7: one column each) to xd (row stride
-// kLd). Returns false (wave-uniform) at a non-positive pivot.
-__device__ __forceinline__ bool subPanel8(double* sA, double* xd, double* sRl, int c0, int lane) {
+// then solves its own row r (the row's 8 entries of the sub-panel, updated) against it (row
+// TRSM), so the 8 dependent pivots cost only the FP64 latency of rsqrt + scaling + the next pivot
+// update. x: row i of L in the sub-panel (x[i - c0] = r * rl = d * rl = L_ii, bit-identical to the
+// redundant factor's L_ii). Returns false (wave-uniform) at a non-positive pivot.
+__device__ __forceinline__ bool chol8Row(const double* sA, int c0, double (&r)[8], double (&x)[8], double (&rl)[8]) {
   double D[8][8];
 #pragma unroll
   for (int m = 0; m < 8; ++m)
 #pragma unroll
     for (int k = 0; k <= m; ++k) D[m][k] = sA[(c0 + m) * kLd + c0 + k];
-  const int i = lane;
-  double r[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) r[k] = sA[i * kLd + c0 + k];
-  double rl[8], x[8];
   bool bad = false;
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
@@ -225,41 +245,57 @@ __device__ __forceinline__ bool subPanel8(double* sA, double* xd, double* sRl, i
 #pragma unroll
       for (int k = c + 1; k < m; ++k) D[m][k] -= D[m][c] * D[k][c];
   }
-  if (bad) return false;
-  // row i of L: all 8 entries below the diagonal block, entries k <= i - c0 inside it
-  // (x[i - c0] = r * rl = d * rl = L_ii, bit-identical to the redundant factor's L_ii)
+  return !bad;
+}
+// Row i of L for the sub-panel into the tile: all 8 entries below the diagonal block, entries
+// k <= i - c0 inside it.
+__device__ __forceinline__ void storeRow8(double* sA, int c0, const double (&x)[8], int i) {
   if (i >= c0) {
 #pragma unroll
     for (int k = 0; k < 8; ++k)
       if (i >= c0 + 8 || k <= i - c0) sA[i * kLd + c0 + k] = x[k];
   }
+}
+// 8x8 diagonal block of X = L^-1 from the final L_D in the tile and 1/L_cc (sRl): lanes 0..7, one
+// column j = lane each, y_m = (delta_mj - sum_{k<m} L_mk y_k) / L_mm, to xd (row stride kLd).
+__device__ __forceinline__ void inv8(const double* sA, const double* sRl, double* xd, int c0, int lane) {
+  if (lane >= 8) return;
+  double y[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    double v = (m == lane) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < m; ++k) v -= sA[(c0 + m) * kLd + c0 + k] * y[k];
+    y[m] = v * sRl[c0 + m];
+    xd[m * kLd + lane] = y[m];
+  }
+}
+// The whole sub-panel on one wavefront: factor, L into the tile, 1/L_cc to sRl and the 8x8
+// diagonal inverse block to xd. Returns false (wave-uniform) at a non-positive pivot.
+__device__ __forceinline__ bool subPanel8(double* sA, double* xd, double* sRl, int c0, int lane) {
+  double r[8], x[8], rl[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = sA[lane * kLd + c0 + k];
+  if (!chol8Row(sA, c0, r, x, rl)) return false;
+  storeRow8(sA, c0, x, lane);
   if (lane == 0) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) sRl[c0 + k] = rl[k];
   }
-  if (lane < 8) {
-    // column j = lane of inv(L_D): y_m = (delta_mj - sum_{k<m} L_mk y_k) / L_mm
-    double y[8];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      double v = (m == lane) ? 1.0 : 0.0;
-#pragma unroll
-      for (int k = 0; k < m; ++k) v -= D[m][k] * y[k];
-      y[m] = v * rl[m];
-      xd[m * kLd + lane] = y[m];
-    }
-  }
+  __builtin_amdgcn_wave_barrier();
+  inv8(sA, sRl, xd, c0, lane);
   return true;
 }
 
-// Rank-8 trailing update of the in-LDS tile after sub-panel c0: A_ij -= sum_k L_ik L_jk (k in the
-// sub-panel) for 16x16 output blocks at or right of column c0 + 8, lower block triangle, dealt to
-// nw wavefronts (this one is wg of nw). A block column that starts inside the sub-panel keeps its
-// left 8 columns (already final L), and the block row that starts there keeps its top 8 rows (the
-// upper triangle, where potrfWave stashes inverse blocks).
-__device__ __forceinline__ void trailing8(double* sA, int c0, int wg, int nw, int lane) {
-  const int cb0 = (c0 + 8) >> 4;
-  const bool part = ((c0 + 8) & 15) != 0;
+// Rank-8 trailing update of the in-LDS tile by sub-panel c0: A_ij -= sum_k L_ik L_jk (k in the
+// sub-panel) for the 16x16 output blocks of rows and columns >= cs (cs >= c0 + 8, a multiple of 8),
+// lower block triangle, dealt to nw wavefronts (this one is wg of nw). A block column that starts
+// before cs keeps its left 8 columns (already final L, or the next sub-panel's columns, which the
+// look-ahead wavefront may be updating: not written at all), and the block row that starts there
+// keeps its top 8 rows (the upper triangle, where potrfWave stashes inverse blocks).
+__device__ __forceinline__ void trailingFrom(double* sA, int c0, int cs, int wg, int nw, int lane) {
+  const int cb0 = cs >> 4;
+  const bool part = (cs & 15) != 0;
   const int lr = lane & 15, lk = lane >> 4;
   int idx = 0;
   for (int rb = cb0; rb < 4; ++rb)
@@ -267,20 +303,21 @@ __device__ __forceinline__ void trailing8(double* sA, int c0, int wg, int nw, in
       if (idx % nw != wg) continue;
       double* C = sA + 16 * rb * kLd + 16 * cb;
       dbl4 acc = loadC16(C, kLd, lane);
-      const dbl4 c0v = acc;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const double av = -sA[(16 * rb + lr) * kLd + c0 + 4 * q + lk];
         const double bv = sA[(16 * cb + lr) * kLd + c0 + 4 * q + lk];
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
       }
-      if (part && cb == cb0 && lr < 8) acc = c0v;
-      if (part && rb == cb0) {  // rows lk + 4 reg < 8: reg 0, 1
-        acc[0] = c0v[0];
-        acc[1] = c0v[1];
-      }
-      storeC16(C, kLd, acc, lane);
+      // masked entries are not written back at all: another wavefront may be updating them
+      if (part && cb == cb0 && lr < 8) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (!(part && rb == cb0 && r < 2)) C[(lk + 4 * r) * kLd + lr] = acc[r];  // rows lk + 4 r
     }
+}
+__device__ __forceinline__ void trailing8(double* sA, int c0, int wg, int nw, int lane) {
+  trailingFrom(sA, c0, c0 + 8, wg, nw, lane);
 }
 
 // Diagonal tile: L_kk (into S, lower), X = L_kk^-1 (into sX and the Linv store) and y_k = X rhs_k
@@ -294,7 +331,7 @@ __device__ __forceinline__ void trailing8(double* sA, int c0, int wg, int nw, in
 // budget that halves the persistent kernel's occupancy)
 template <int kCaller>
 __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX, double* sy,
-                                      double* sRl, int* sFail, int t) {
+                                      double* sRl, int* sFl, int t) {
   const int wave = t >> 6, lane = t & 63;
   CLK_INIT
   loadTile(Sg, ld, 0, 0, sA, t);
@@ -303,21 +340,70 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
     const int e = t + 256 * u;
     sX[(e >> 6) * kLd + (e & 63)] = 0.0;
   }
-  if (t == 0) *sFail = 0;
+  if (t < 4) sFl[t] = 0;  // sub-panels factored, trailing updates done, fail, barrier counter
   __syncthreads();
   CLK(4)
+  // Sweep with look-ahead: wavefront 0 runs the chain of the 8 sub-panel factorisations and
+  // applies each sub-panel's rank-8 update to the next sub-panel's 8 columns itself (VALU, its own
+  // row); wavefronts 1-3 apply it to the columns beyond (matrix cores) and form the 8x8 inverse
+  // blocks, one sub-panel behind, handing over through LDS flags.
+  if (wave == 0) {
+    const int i = lane;
+    double xp[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) xp[k] = 0.0;
 #pragma unroll 1
-  for (int s = 0; s < 8; ++s) {
-    if (wave == 0 && !subPanel8(sA, sX + 8 * s * kLd + 8 * s, sRl, 8 * s, lane) && lane == 0) *sFail = 1;
-    __syncthreads();
-    CLK(5)
-    if (*sFail) return false;
-    if (s < 7) {
-      trailing8(sA, 8 * s, wave, 4, lane);
-      __syncthreads();
+    for (int s = 0; s < 8; ++s) {
+      const int c0 = 8 * s;
+      CLK(25)
+      if (s >= 2 && !waitFlag(&sFl[1], s - 1, &sFl[2])) break;  // trailing update of sub-panel s-2
+      CLK(21)
+      double r[8], x[8], rl[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = sA[i * kLd + c0 + k];
+      if (s >= 1) {  // look-ahead update by sub-panel s-1: r -= L_i,s-1 L_(c0..c0+7),s-1^T
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+#pragma unroll
+          for (int c = 0; c < 8; ++c) r[m] -= xp[c] * sA[(c0 + m) * kLd + c0 - 8 + c];
+        if (i >= c0) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) sA[i * kLd + c0 + k] = r[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      CLK(22)
+      if (!chol8Row(sA, c0, r, x, rl)) {
+        if (lane == 0) ldsRelease(&sFl[2], 1);
+        break;
+      }
+      CLK(23)
+      storeRow8(sA, c0, x, i);
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sRl[c0 + k] = rl[k];
+        ldsRelease(&sFl[0], s + 1);
+      }
+      CLK(24)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) xp[k] = x[k];
     }
-    CLK(6)
+  } else {
+    const int g = wave - 1;
+    int gen = 0;
+#pragma unroll 1
+    for (int s = 0; s < 8; ++s) {
+      if (!waitFlag(&sFl[0], s + 1, &sFl[2])) break;
+      if (g == 0) inv8(sA, sRl, sX + 8 * s * kLd + 8 * s, 8 * s, lane);
+      if (s < 6) trailingFrom(sA, 8 * s, 8 * s + 16, g, 3, lane);
+      waveBarrier(&sFl[3], gen, 3, lane);
+      if (g == 0 && lane == 0) ldsRelease(&sFl[1], s + 1);
+    }
   }
+  __syncthreads();
+  CLK(5)
+  if (sFl[2]) return false;
+  CLK(6)
   {  // X21 = -X22 (L21 X11) of the diagonal 16x16 block q = wave; lane = (row m, column j)
     const int q = wave, m = lane >> 3, j = lane & 7;
     const int b = 16 * q;
@@ -563,7 +649,7 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
   __shared__ double sX[kTile * kLd];
   __shared__ double sy[2 * kTile];  // y_k | panel column scratch
   __shared__ double sRl[kTile];
-  __shared__ int sFail;
+  __shared__ int sFl[4];
   const int t = threadIdx.x;
   const int fdim = P.win_fdim[w];
   CLK_INIT
@@ -574,7 +660,7 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
     if (t < kTile) sy[t] = work[k * kTile + t];
     __syncthreads();
     if (!potrfTile<0>(S + k * kTile * ld + k * kTile, ld, Linv + (int64_t)k * kTile * kTile, work + k * kTile, sA, sX,
-                   sy, sRl, &sFail, t)) {
+                   sy, sRl, sFl, t)) {
       if (t == 0) P.st[w].gn_failed = 1;
       return;
     }
@@ -608,6 +694,8 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
   CLK(3)
 #ifdef OKG_CHOL_CLOCK
   if (blockIdx.x == 0 && t == 0)
+    printf("SWEEP wait %llu look %llu chol %llu store %llu\n", g_cholClk[21], g_cholClk[22], g_cholClk[23], g_cholClk[24]);
+  if (blockIdx.x == 0 && t == 0)
     printf("CHOLCLK T=%d potrf %llu panel %llu update %llu bsub %llu | load %llu pfac %llu ptrail %llu dinv %llu subd %llu store %llu y %llu (x10ns)\n",
            T, g_cholClk[0], g_cholClk[1], g_cholClk[2] + g_cholClk[11], g_cholClk[3], g_cholClk[4], g_cholClk[5], g_cholClk[6],
            g_cholClk[7], g_cholClk[8], g_cholClk[9], g_cholClk[10]);
@@ -634,7 +722,7 @@ __global__ __launch_bounds__(256) void k_chol_diag(const DevProblem* __restrict_
   __shared__ double sX[kTile * kLd];
   __shared__ double sy[2 * kTile];
   __shared__ double sRl[kTile];
-  __shared__ int sFail;
+  __shared__ int sFl[4];
   const int t = threadIdx.x;
   if (k == 0) {
     const int fdim = P.win_fdim[w];
@@ -644,7 +732,7 @@ __global__ __launch_bounds__(256) void k_chol_diag(const DevProblem* __restrict_
   if (t < kTile) sy[t] = work[k * kTile + t];
   __syncthreads();
   if (!potrfTile<1>(S + k * kTile * ld + k * kTile, ld, P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile,
-                    work + k * kTile, sA, sX, sy, sRl, &sFail, t))
+                    work + k * kTile, sA, sX, sy, sRl, sFl, t))
     if (t == 0) P.st[w].gn_failed = 1;
 }
 
@@ -674,7 +762,7 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
   __shared__ double sB[kTile * kLd];
   __shared__ double sy[2 * kTile];
   __shared__ double sRl[kTile];
-  __shared__ int sFail;
+  __shared__ int sFl[4];
   const int t = threadIdx.x;
   if (mode & 1) {
     // panels of step k: L_ik (and L_jk) = A (X_k)^T, operands staged in LDS
@@ -716,7 +804,7 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
   if (t < kTile) sy[t] = work[d * kTile + t];
   __syncthreads();
   if (!potrfTile<2>(S + d * kTile * ld + d * kTile, ld, P.Linv + P.win_linvoff[w] + (int64_t)d * kTile * kTile,
-                    work + d * kTile, sA, sX, sy, sRl, &sFail, t))
+                    work + d * kTile, sA, sX, sy, sRl, sFl, t))
     if (t == 0) P.st[w].gn_failed = 1;
 }
 
@@ -805,31 +893,6 @@ __global__ __launch_bounds__(kBsReal) void k_chol_bsub(const DevProblem* __restr
 constexpr int kSlotThreads = 256;
 constexpr int kWsThreads = 2 * kSlotThreads;
 constexpr int kMaxBlocksPerWave = 6;     // 16 blocks over >= 3 MFMA wavefronts
-
-struct WsFlags {
-  int xReady, diagReady, xFree, fail, gbar, sbar;
-};
-
-__device__ __forceinline__ int ldsAcquire(int* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void ldsRelease(int* p, int v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// Wave-uniform wait for *p >= v; false once the factor wavefront reported a failed pivot.
-__device__ __forceinline__ bool waitFlag(int* p, int v, int* fail) {
-  for (;;) {
-    if (ldsAcquire(p) >= v) return true;
-    if (ldsAcquire(fail)) return false;
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-// Barrier of n wavefronts on a monotonic arrival counter (gen counts this wavefront's barriers).
-__device__ __forceinline__ void waveBarrier(int* ctr, int& gen, int n, int lane) {
-  ++gen;
-  if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  while (ldsAcquire(ctr) < gen * n) __builtin_amdgcn_s_sleep(1);
-}
 
 // The n-th output block of MFMA wavefront g (of ng) in a full (16 blocks) or lower (10 blocks)
 // tile; -1 past the end. Block bi is (bi >> 2, bi & 3).

@@ -143,6 +143,28 @@ __global__ void k_bstep(double* out, long long* cyc, int n, int mode) {
   if (t == 0) { cyc[0] = t1 - t0; out[0] = sx[5]; }
 }
 
+// LDS latency: dependent chain of ds_read_b32 (index chasing), one wave; and a store->load round trip
+__global__ void k_ldslat(int* out, long long* cyc, int n) {
+  __shared__ int s[1024];
+  __shared__ double d[1024];
+  for (int e = threadIdx.x; e < 1024; e += blockDim.x) { s[e] = (e * 7 + 3) & 1023; d[e] = e; }
+  __syncthreads();
+  int j = threadIdx.x;
+  long long t0 = clock64();
+  for (int i = 0; i < n; ++i) j = s[j];
+  long long t1 = clock64();
+  double a = 1.0;
+  long long t2 = clock64();
+  for (int i = 0; i < n; ++i) {
+    d[threadIdx.x] = a;
+    __builtin_amdgcn_wave_barrier();
+    a = d[(threadIdx.x + 1) & 63] + 1.0;
+  }
+  long long t3 = clock64();
+  out[threadIdx.x] = j + (int)a;
+  if (threadIdx.x == 0) { cyc[0] = t1 - t0; cyc[1] = t3 - t2; }
+}
+
 int main() {
   double *d, *o;
   long long* c;
@@ -176,6 +198,13 @@ int main() {
     hipMemcpy(h, c, 16, hipMemcpyDeviceToHost);
     printf("sweep mode %d: subPanel8+bar %.0f cycles per sub-panel, trailing8+bar %.0f per sub-panel\n", mode,
            h[0] / 800.0, h[1] / 800.0);
+  }
+  {
+    int* oi;
+    hipMalloc(&oi, 4096);
+    k_ldslat<<<1, 64>>>(oi, c, 1000);
+    hipMemcpy(h, c, 16, hipMemcpyDeviceToHost);
+    printf("LDS dependent read chain: %.1f cycles; store->load round trip: %.1f cycles\n", h[0] / 1000.0, h[1] / 1000.0);
   }
   for (int nt = 256; nt <= 1024; nt *= 2)
     for (int mode = 0; mode < 3; ++mode) {
