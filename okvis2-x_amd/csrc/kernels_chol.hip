@@ -146,14 +146,6 @@ __device__ __forceinline__ double readlaneD(double v, int lane) {  // v of `lane
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// Workgroup barrier that orders LDS only: __syncthreads() also waits for every outstanding global
-// load (vmcnt(0)), which defeats loads prefetched across the barrier.
-__device__ __forceinline__ void ldsBarrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
 // 1/sqrt(d) to ~1 ulp: v_rsq_f64 (~5e-8 relative) refined by two Newton steps (measured on
 // gfx950: 2.3e-16 max relative error over d in [e^-40, e^40]).
 __device__ __forceinline__ double rsqrtRefined(double d) {

@@ -40,6 +40,14 @@ __device__ __forceinline__ gwptr<T> gmemw(T* p) {
   return (gwptr<T>)p;
 }
 
+// Workgroup barrier that orders LDS only: __syncthreads() also waits for every outstanding global
+// load (vmcnt(0)), which defeats loads prefetched across the barrier.
+__device__ __forceinline__ void ldsBarrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 struct Q {
   double x, y, z, w;
 };
