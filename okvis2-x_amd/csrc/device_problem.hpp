@@ -31,6 +31,7 @@ constexpr int kLmGroupVisits = 256;  // k_lm_visit: visits of one landmark group
 constexpr int kLmGroupMax = 64;      // landmarks per group
 constexpr int kLmPartStage = 2048;   // landmark-pair products per group (staged in LDS)
 constexpr int kImuHess = 465 + 30;  // packed upper J^T J (30x30) | J^T r
+constexpr int kGrpRed = 8;    // per landmark group: jcc | jgg | jcg | gg | nn | gn | pad
 constexpr int kVisitZ = 18;   // per visit: Z = s_p W s_l L^-T (6x3), k_lm_visit LDS only
 
 // contribution record types for the reduced-system assembly
@@ -115,7 +116,9 @@ struct DevProblem {
   const double* obs_L;             // [n_obs][4]
   double* obs_lin[2];              // [kObsLin][obs_stride]; lin[lcur] belongs to params X[xcur]
   double* obs_cost[2];             // [n_obs]
-  double* obs_jv;                  // [3][n_visit]: the visit's share of jcc | jgg | jcg
+  double* grp_red;                 // [n_lmg][kGrpRed]: per landmark group (k_lm_backsub_jv), fixed-order
+                                   // sums jcc | jgg | jcg over its residuals and |grad_l|^2 | |gn_l|^2 |
+                                   // grad_l . gn_l over its free landmarks (k_reduce, k_dogleg)
 
   // --- landmarks / visits
   const int32_t* lm_visit_begin;   // [n_lm+1] visits of landmark l
@@ -212,6 +215,7 @@ struct DevProblem {
   const int32_t* win_pose_range;   // [n_win][2]
   const int32_t* win_sb_range;
   const int32_t* win_lm_range;
+  const int32_t* win_lmg_range;    // [n_win][2] landmark groups of the window
   const int32_t* win_obs_range;
   const int32_t* win_imu_range;
   const int32_t* win_pp_range;

@@ -16,7 +16,8 @@
 //            to LDS for the visits
 //   visit    J_s v_c and J_s v_g of its 1-2 residuals (A re-read from L1/L2)
 // The f-block half of k_gn_finalize runs before (v_c of the poses); the IMU factors', priors' and
-// edges' J*v stay in k_jv.
+// edges' J*v stay in k_jv. The group's J*v forms and landmark norms leave as one fixed-order sum per
+// group (grp_red), so the per-window reductions read ~36 records instead of every visit and landmark.
 #include "device_problem.hpp"
 #include "launch.hpp"
 #include "okvisgpu_math.hpp"
@@ -113,6 +114,7 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
   __syncthreads();
 
   // ---- landmark: y_l = L^-T (zz - L^-1 s_l sum_v q_v), the dogleg vectors
+  double lred[3] = {0.0, 0.0, 0.0};
   if (t < l1 - l0) {
     const int L = l0 + t;
     double c6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -140,11 +142,17 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
         const size_t i = 3 * (size_t)L + a;
         const double dg = P.diagL[i];
         P.yL[i] = y;
-        P.gnL[i] = -dg * y;
+        const double gn = -dg * y;
+        P.gnL[i] = gn;
         const double gr = s3[a] * P.lm_g[i] / dg;
         const double vc = gr / dg;
         P.dgL[i] = gr;
         P.vL[i] = vc;
+        // this landmark's share of |gradient_|^2, |gauss_newton_step_|^2, gradient_ . gn (k_dogleg,
+        // k_reduce), summed per group below
+        lred[0] += gr * gr;
+        lred[1] += gn * gn;
+        lred[2] += gr * gn;
         c6[a] = s3[a] * vc;
         c6[3 + a] = -s3[a] * y;
       }
@@ -153,10 +161,9 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
     for (int i = 0; i < 6; ++i) sC[i][t] = c6[i];
   }
   __syncthreads();
-  if (!hasV) return;
 
   // ---- visit: J_s v_c and J_s v_g of its residuals (fixed residuals excluded)
-  const int u = l - l0;
+  const int u = hasV ? l - l0 : 0;
   double cl[3], gl[3];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
@@ -196,8 +203,23 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
       acc[2] += jc * jg;
     }
   }
+  // ---- the group's sums, fixed order: a shuffle tree per wavefront, then the 4 wavefronts
+  double red[6] = {acc[0], acc[1], acc[2], lred[0], lred[1], lred[2]};
 #pragma unroll
-  for (int k = 0; k < 3; ++k) P.obs_jv[(size_t)k * P.n_visit + v] = acc[k];
+  for (int k = 0; k < 6; ++k)
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) red[k] += __shfl_xor(red[k], m, 64);
+  __shared__ double sW[kLmGroupVisits / 64][6];
+  if ((t & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) sW[t >> 6][k] = red[k];
+  __syncthreads();
+  if (t < 6) {
+    double a = sW[0][t];
+#pragma unroll
+    for (int wv = 1; wv < kLmGroupVisits / 64; ++wv) a += sW[wv][t];
+    P.grp_red[(size_t)blockIdx.x * kGrpRed + t] = a;
+  }
 }
 
 void launch_lm_backsub(const DevProblem& P, hipStream_t s) {

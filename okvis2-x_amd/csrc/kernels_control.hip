@@ -287,14 +287,13 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
 
   // J*v reductions (once per GN step): jcc, jgg, jcg and the Cauchy alpha = |gradient_|^2 / jcc
   if (!(s.need_gn && !s.gn_failed)) return;
-  const int lmb = P.win_lm_range[2 * w], lme = P.win_lm_range[2 * w + 1];
-  const int vb = P.lm_visit_begin[lmb], ve = P.lm_visit_begin[lme];
+  // reprojection rows and landmark gradients: the landmark groups' sums (k_lm_backsub_jv)
+  const int gb = P.win_lmg_range[2 * w], ge = P.win_lmg_range[2 * w + 1];
   double a[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     double acc = 0.0;
-    const double* jv = P.obs_jv + (size_t)k * P.n_visit;
-    stridedBatched<8>(vb, ve, [&](int v) { return jv[v]; }, [&](int, double x) { acc += x; });
+    for (int g = gb + t; g < ge; g += kRB) acc += P.grp_red[(size_t)g * kGrpRed + k];
     for (int f = ib + t; f < ie; f += kRB) acc += P.imu_jv[(size_t)k * P.n_imu + f];
     for (int i = pb + t; i < pe; i += kRB) acc += P.pp_jv[(size_t)k * P.n_pprior + i];
     for (int i = sbb + t; i < sbe; i += kRB) acc += P.sbp_jv[(size_t)k * P.n_sbprior + i];
@@ -305,18 +304,7 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
   double g2 = 0.0;
   const int fo = P.win_foff[w], fd = P.win_fdim[w];
   for (int e = t; e < fd; e += kRB) g2 += P.dgF[fo + e] * P.dgF[fo + e];
-  struct LG { double d[3]; uint8_t f; };
-  stridedBatched<4>(lmb, lme,
-                    [&](int l) {
-                      LG v;
-                      v.f = P.lm_free[l];
-                      for (int c = 0; c < 3; ++c) v.d[c] = P.dgL[3 * (size_t)l + c];
-                      return v;
-                    },
-                    [&](int, const LG& v) {
-                      if (v.f)
-                        for (int c = 0; c < 3; ++c) g2 += v.d[c] * v.d[c];
-                    });
+  for (int g = gb + t; g < ge; g += kRB) g2 += P.grp_red[(size_t)g * kGrpRed + 3];
   g2 = blockSum(g2, sh);
   if (t == 0) {
     s.jcc = a[0];
@@ -453,7 +441,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
   if (sflag) return;
   const int foff = P.win_foff[w], fd = P.win_fdim[w];
   const int l0 = P.win_lm_range[2 * w], l1 = P.win_lm_range[2 * w + 1];
-  // pass 1: norms
+  // pass 1: norms (f-blocks here, landmarks as the landmark groups' sums of k_lm_backsub_jv)
   double gg = 0.0, nn = 0.0, gn = 0.0;
   for (int e = t; e < fd; e += kRB) {
     const double a = P.dgF[foff + e], b = P.gnF[foff + e];
@@ -461,25 +449,13 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
     nn += b * b;
     gn += a * b;
   }
-  struct LD { double a[3], b[3]; uint8_t f; };
-  stridedBatched<4>(l0, l1,
-                    [&](int l) {
-                      LD v;
-                      v.f = P.lm_free[l];
-                      for (int c = 0; c < 3; ++c) {
-                        v.a[c] = P.dgL[3 * (size_t)l + c];
-                        v.b[c] = P.gnL[3 * (size_t)l + c];
-                      }
-                      return v;
-                    },
-                    [&](int, const LD& v) {
-                      if (!v.f) return;
-                      for (int c = 0; c < 3; ++c) {
-                        gg += v.a[c] * v.a[c];
-                        nn += v.b[c] * v.b[c];
-                        gn += v.a[c] * v.b[c];
-                      }
-                    });
+  const int gb = P.win_lmg_range[2 * w], ge = P.win_lmg_range[2 * w + 1];
+  for (int g = gb + t; g < ge; g += kRB) {
+    const double* r = P.grp_red + (size_t)g * kGrpRed;
+    gg += r[3];
+    nn += r[4];
+    gn += r[5];
+  }
   gg = blockSum(gg, sh);
   nn = blockSum(nn, sh);
   gn = blockSum(gn, sh);

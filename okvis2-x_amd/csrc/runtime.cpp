@@ -98,6 +98,7 @@ struct HostBatch {
   // reduced structure
   std::vector<int32_t> win_foff, win_fdim, win_fpad;
   std::vector<int64_t> win_soff, win_linvoff, win_fwdoff;
+  std::vector<int32_t> win_lmg_range;
   std::vector<int32_t> win_pose_range, win_sb_range, win_lm_range, win_obs_range, win_imu_range, win_pp_range,
       win_sbp_range, win_rp_range;
   std::vector<int32_t> fb_win, fb_kind, fb_index, fb_off, fb_cbegin;
@@ -759,6 +760,21 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
   }
   B.lm_visit_begin.push_back((int)B.visit_pose.size());
   B.lmg_begin.push_back((int)B.lm_win.size());  // groups: begin of each, then the end
+  {  // each window's groups are contiguous (built window by window)
+    B.win_lmg_range.assign(2 * (size_t)B.n_win, 0);
+    const int ng = (int)B.lmg_begin.size() - 1;
+    std::vector<int> first(B.n_win, -1), last(B.n_win, -1);
+    for (int g = 0; g < ng; ++g) {
+      const int w = B.lm_win[B.lmg_begin[g]];
+      if (first[w] < 0) first[w] = g;
+      last[w] = g;
+    }
+    for (int w = 0; w < B.n_win; ++w)
+      if (first[w] >= 0) {
+        B.win_lmg_range[2 * w] = first[w];
+        B.win_lmg_range[2 * w + 1] = last[w] + 1;
+      }
+  }
   B.lmg_xbegin.push_back((int)B.xvisit_pose.size());
   B.xvisit_obs_begin.push_back((int)B.xvisit_obs.size());
   B.pe_obs_begin.push_back((int)B.pe_obs.size());
@@ -900,7 +916,7 @@ struct okvisgpu_ctx {
     const size_t o_obs_lin0 = scratch(sizeof(double) * kObsLin * D.obs_stride);
     const size_t o_obs_lin1 = scratch(sizeof(double) * kObsLin * D.obs_stride);
     const size_t o_obs_cost0 = scratch(sizeof(double) * D.n_obs), o_obs_cost1 = scratch(sizeof(double) * D.n_obs);
-    const size_t o_obs_jv = scratch(sizeof(double) * 3 * D.n_obs);
+    const size_t o_grp_red = scratch(sizeof(double) * kGrpRed * std::max<size_t>(1, B.lmg_begin.size()));
     const size_t o_lmvb = upl(B.lm_visit_begin), o_vpose = upl(B.visit_pose), o_vob = upl(B.visit_obs_begin),
                  o_vlm = upl(B.visit_lm), o_lmg_b = upl(B.lmg_begin);
     const size_t o_lmV = scratch(sizeof(double) * 6 * D.n_lm), o_lmg = scratch(sizeof(double) * 3 * D.n_lm),
@@ -947,7 +963,7 @@ struct okvisgpu_ctx {
                  o_rp_jv = scratch(sizeof(double) * 3 * D.n_relpose), o_wrpr = upl(B.win_rp_range);
     const size_t o_wfoff = upl(B.win_foff), o_wfdim = upl(B.win_fdim), o_wfpad = upl(B.win_fpad),
                  o_wsoff = upl(B.win_soff), o_wlinv = upl(B.win_linvoff), o_wfwd = upl(B.win_fwdoff), o_wpr = upl(B.win_pose_range), o_wsr = upl(B.win_sb_range),
-                 o_wlr = upl(B.win_lm_range), o_wor = upl(B.win_obs_range), o_wir = upl(B.win_imu_range),
+                 o_wlr = upl(B.win_lm_range), o_wlgr = upl(B.win_lmg_range), o_wor = upl(B.win_obs_range), o_wir = upl(B.win_imu_range),
                  o_wppr = upl(B.win_pp_range), o_wsbpr = upl(B.win_sbp_range);
     const size_t o_fbw = upl(B.fb_win), o_fbk = upl(B.fb_kind), o_fbi = upl(B.fb_index), o_fbo = upl(B.fb_off),
                  o_fbcb = upl(B.fb_cbegin), o_fbc = upl(B.fb_contrib);
@@ -987,7 +1003,7 @@ struct okvisgpu_ctx {
     D.obs_pose = ip(o_obs_pose); D.obs_lm = ip(o_obs_lm); D.obs_cam = ip(o_obs_cam); D.obs_win = ip(o_obs_win);
     D.obs_flags = up(o_obs_flags); D.obs_kp = dp(o_obs_kp); D.obs_L = dp(o_obs_L);
     D.obs_lin[0] = dp(o_obs_lin0); D.obs_lin[1] = dp(o_obs_lin1);
-    D.obs_cost[0] = dp(o_obs_cost0); D.obs_cost[1] = dp(o_obs_cost1); D.obs_jv = dp(o_obs_jv);
+    D.obs_cost[0] = dp(o_obs_cost0); D.obs_cost[1] = dp(o_obs_cost1); D.grp_red = dp(o_grp_red);
     D.lm_visit_begin = ip(o_lmvb); D.visit_pose = ip(o_vpose); D.visit_obs_begin = ip(o_vob); D.visit_lm = ip(o_vlm);
     D.lm_V = dp(o_lmV); D.lm_g = dp(o_lmg); D.lm_Linv = dp(o_lmVi); D.lm_zz = dp(o_lmz);
     D.part_gbegin = ip(o_pgb); D.part_cbegin = ip(o_pcb2); D.part_contrib = ip(o_pcon); D.part_S = dp(o_partS);
@@ -1011,7 +1027,7 @@ struct okvisgpu_ctx {
     D.sbp_lin[0] = dp(o_sbp_lin0); D.sbp_lin[1] = dp(o_sbp_lin1); D.sbp_cost[0] = dp(o_sbp_cost0);
     D.sbp_cost[1] = dp(o_sbp_cost1); D.sbp_jv = dp(o_sbp_jv);
     D.win_foff = ip(o_wfoff); D.win_fdim = ip(o_wfdim); D.win_fpad = ip(o_wfpad); D.win_soff = lp(o_wsoff);
-    D.win_pose_range = ip(o_wpr); D.win_sb_range = ip(o_wsr); D.win_lm_range = ip(o_wlr);
+    D.win_pose_range = ip(o_wpr); D.win_sb_range = ip(o_wsr); D.win_lm_range = ip(o_wlr); D.win_lmg_range = ip(o_wlgr);
     D.win_obs_range = ip(o_wor); D.win_imu_range = ip(o_wir); D.win_pp_range = ip(o_wppr);
     D.win_sbp_range = ip(o_wsbpr);
     D.win_rp_range = ip(o_wrpr);
