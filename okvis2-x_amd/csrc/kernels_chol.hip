@@ -323,10 +323,10 @@ __device__ __forceinline__ void trailing8(double* sA, int c0, int wg, int nw, in
 // budget that halves the persistent kernel's occupancy)
 template <int kCaller>
 __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX, double* sy,
-                                      double* sRl, int* sFl, int t) {
+                                      double* sRl, int* sFl, int t, bool haveTile) {
   const int wave = t >> 6, lane = t & 63;
   CLK_INIT
-  loadTile(Sg, ld, 0, 0, sA, t);
+  if (!haveTile) loadTile(Sg, ld, 0, 0, sA, t);  // (else the caller left S_kk in sA)
 #pragma unroll
   for (int u = 0; u < 16; ++u) {
     const int e = t + 256 * u;
@@ -652,7 +652,7 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
     if (t < kTile) sy[t] = work[k * kTile + t];
     __syncthreads();
     if (!potrfTile<0>(S + k * kTile * ld + k * kTile, ld, Linv + (int64_t)k * kTile * kTile, work + k * kTile, sA, sX,
-                   sy, sRl, sFl, t)) {
+                   sy, sRl, sFl, t, false)) {
       if (t == 0) P.st[w].gn_failed = 1;
       return;
     }
@@ -724,7 +724,7 @@ __global__ __launch_bounds__(256) void k_chol_diag(const DevProblem* __restrict_
   if (t < kTile) sy[t] = work[k * kTile + t];
   __syncthreads();
   if (!potrfTile<1>(S + k * kTile * ld + k * kTile, ld, P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile,
-                    work + k * kTile, sA, sX, sy, sRl, sFl, t))
+                    work + k * kTile, sA, sX, sy, sRl, sFl, t, false))
     if (t == 0) P.st[w].gn_failed = 1;
 }
 
@@ -762,6 +762,8 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
     loadTile(S + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
     if (j != i) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sB, t);
     if (i == j && t < kTile) sy[t] = work[k * kTile + t];
+    const int row = t >> 2, q = t & 3;
+    const double rhsOld = (i == j && q == 0) ? work[i * kTile + row] : 0.0;
     __syncthreads();
     // rhs_i -= L_ik y_k, formed as A_ik z with z = X_k^T y_k from the A_ik tile in LDS (the same
     // operations as panelTile, so all schedules give the same bits)
@@ -770,13 +772,16 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
     mfmaTileNT(sA, sX, li, t);
     if (j != i) mfmaTileNT(sB, sX, lj, t);
     if (i == j) {
-      const int row = t >> 2, q = t & 3;
       double a = 0.0;
 #pragma unroll
       for (int cc = 16 * q; cc < 16 * q + 16; ++cc) a += sA[row * kLd + cc] * sy[kTile + cc];
       a += __shfl_xor(a, 1, 64);
       a += __shfl_xor(a, 2, 64);
-      if (q == 0) work[i * kTile + row] -= a;
+      if (q == 0) {
+        const double nr = rhsOld - a;
+        gmemw(work)[i * kTile + row] = nr;
+        if (mode & 2) sRl[row] = nr;  // rhs_{k+1} for the factor below (sRl is free until then)
+      }
     }
     __syncthreads();  // every wavefront has read A_ik / A_jk
     accToLds(sA, li, t);
@@ -788,15 +793,34 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
     __syncthreads();
     dbl4 acc[2][2];
     mfmaTileNT(sA, j == i ? sA : sB, acc, t);
-    storeTileSub(Cij, ld, c, acc, t);
+    if (mode & 2) {
+      // tile (k+1,k+1): the updated S_dd goes straight to LDS for the factor (its global copy is
+      // overwritten by L_dd there), and so does rhs_d
+      __syncthreads();  // every wavefront has read L_ik from sA
+      const int wave = t >> 6, lane = t & 63;
+      const int r0 = 32 * (wave >> 1), cq = 32 * (wave & 1);
+#pragma unroll
+      for (int a2 = 0; a2 < 2; ++a2)
+#pragma unroll
+        for (int b2 = 0; b2 < 2; ++b2)
+#pragma unroll
+          for (int reg = 0; reg < 4; ++reg)
+            sA[(r0 + 16 * a2 + (lane >> 4) + 4 * reg) * kLd + cq + 16 * b2 + (lane & 15)] = c[a2][b2][reg] - acc[a2][b2][reg];
+      __syncthreads();
+      if (t < kTile) sy[t] = sRl[t];
+    } else {
+      storeTileSub(Cij, ld, c, acc, t);
+    }
   }
   if (!(mode & 2)) return;
   const int d = k + 1;
-  __syncthreads();  // also orders this workgroup's rhs_d update before the read below
-  if (t < kTile) sy[t] = work[d * kTile + t];
+  if (!(mode & 1)) {  // factor-only item: S_dd and rhs_d from global (written by earlier launches)
+    __syncthreads();
+    if (t < kTile) sy[t] = work[d * kTile + t];
+  }
   __syncthreads();
   if (!potrfTile<2>(S + d * kTile * ld + d * kTile, ld, P.Linv + P.win_linvoff[w] + (int64_t)d * kTile * kTile,
-                    work + d * kTile, sA, sX, sy, sRl, sFl, t))
+                    work + d * kTile, sA, sX, sy, sRl, sFl, t, (mode & 1) != 0))
     if (t == 0) P.st[w].gn_failed = 1;
 }
 
