@@ -16,6 +16,8 @@ vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for path in sys.argv[3:]:
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"].split("(")[0].replace("okg::", "").replace("void ", "")
+        # template arguments: the extrinsics flag (<..., false|true>) and bool-only specialisations
+        name = name.replace(", false>", ">").replace(", true>", ">").replace("<false>", "").replace("<true>", "")
         # the specialised k_lm_visit<mode> kernels under bench.py's table names
         name = {"k_lm_visit<1>": "k_lm_visit", "k_lm_visit<2>": "k_lm_visit_prep", "k_lm_visit<0>": "k_lm_visit_init"}.get(
             name, name)
