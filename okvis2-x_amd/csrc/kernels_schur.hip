@@ -55,6 +55,8 @@ __device__ __forceinline__ bool linSelect(const DevProblem& P, int w, int lin_mo
 //            (InvertPSDMatrix) -> L^-1, zz = L^-1 (s g), the dogleg diagonal D
 //   visit    Z = s_p W s_l L^-T and U z = Z zz, the operands of the Schur terms
 //            Y_a U_b^T = Z_a Z_b^T (the partial blocks below; Z never leaves the workgroup)
+// The barriers order LDS only (ldsBarrier): no thread reads global data another thread of the
+// workgroup wrote, and a full __syncthreads() would also wait for the segment / landmark stores.
 // mode 0: linearisation at iteration 0 (no Z: the pose scaling comes from k_fgrad afterwards);
 // mode 1: linearisation after an accepted step, Z for the new mu (WinState::z_mu);
 // mode 2: GN prep of windows whose Z is stale (mu raised by a retry or an invalid step): W is
@@ -182,7 +184,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   for (int i = 0; i < 6; ++i) sVg[i][t] = Vv[i];
 #pragma unroll
   for (int i = 0; i < 3; ++i) sVg[6 + i][t] = gl[i];
-  __syncthreads();
+  ldsBarrier();
   // ---- one thread per landmark of the group
   if (t < l1 - l0) {
     const int L = l0 + t;
@@ -277,7 +279,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
       }
     }
   }
-  __syncthreads();
+  ldsBarrier();
   // ---- segments: H | g of each (group, free pose) summed over its visits in visit order
   // (visits are scattered to their slots so that every segment is a contiguous LDS range)
   const int sg0 = P.seg_gbegin[blockIdx.x], nseg = P.seg_gbegin[blockIdx.x + 1] - sg0;
@@ -292,7 +294,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
           const int e = 9 * chunk + i;
           sR[i][slot] = e < 21 ? H[e] : gp[e - 21];
         }
-      __syncthreads();
+      ldsBarrier();
       for (int e = t; e < nseg * nval; e += kLmGroupVisits) {
         const int sgi = e / nval, i = e - sgi * nval;
         const int m0 = P.seg_range[2 * (sg0 + sgi)], m1 = P.seg_range[2 * (sg0 + sgi) + 1];
@@ -300,7 +302,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
         for (int m = m0; m < m1; ++m) a += sR[i][m];
         P.seg_hg[(size_t)(sg0 + sgi) * kSegHG + 9 * chunk + i] = a;
       }
-      __syncthreads();
+      ldsBarrier();
     }
   }
   if (mode == 0) return;
@@ -335,7 +337,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   if (slot >= 0)
 #pragma unroll
     for (int i = 0; i < 6; ++i) sR[i][slot] = o[kVisitZ + i];
-  __syncthreads();
+  ldsBarrier();
   for (int e = t; e < nseg * 6; e += kLmGroupVisits) {
     const int sgi = e / 6, i = e - sgi * 6;
     const int m0 = P.seg_range[2 * (sg0 + sgi)], m1 = P.seg_range[2 * (sg0 + sgi) + 1];
@@ -349,7 +351,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   const int pg0 = P.part_gbegin[blockIdx.x], npart = P.part_gbegin[blockIdx.x + 1] - pg0;
   const int pc0 = P.part_cbegin[pg0], npc = P.part_cbegin[pg0 + npart] - pc0;
   double* sZ = &sBuf[0][0];
-  __syncthreads();  // sR reads above are done
+  ldsBarrier();  // sR reads above are done
   {
     double2* zo = reinterpret_cast<double2*>(sZ + kVisitZ * t);
 #pragma unroll
@@ -359,7 +361,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   const bool staged = npc <= kLmPartStage;
   if (staged)
     for (int c = t; c < npc; c += kLmGroupVisits) sPC[c] = P.part_contrib[pc0 + c];
-  __syncthreads();
+  ldsBarrier();
   const auto gPC = gmem(P.part_contrib + pc0);
   for (int e = t; e < npart * 3; e += kLmGroupVisits) {
     const int pi = e / 3, h = e - pi * 3;
