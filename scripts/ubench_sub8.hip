@@ -165,6 +165,20 @@ __global__ void k_ldslat(int* out, long long* cyc, int n) {
   if (threadIdx.x == 0) { cyc[0] = t1 - t0; cyc[1] = t3 - t2; }
 }
 
+// global memory latency: dependent pointer chase over a buffer (hot: small, repeated; cold: large stride)
+__global__ void k_glat(const int* __restrict__ nxt, int* out, long long* cyc, int n) {
+  int j = 0;
+  long long t0 = clock64();
+  for (int i = 0; i < n; ++i) j = __builtin_nontemporal_load(nxt + j) + 0;
+  long long t1 = clock64();
+  out[0] = j;
+  cyc[0] = t1 - t0;
+}
+
+__global__ void k_empty(int* o) {
+  if (threadIdx.x == 0 && blockIdx.x == 0 && o[0] == 12345) o[1] = 1;
+}
+
 int main() {
   double *d, *o;
   long long* c;
@@ -206,12 +220,48 @@ int main() {
     hipMemcpy(h, c, 16, hipMemcpyDeviceToHost);
     printf("LDS dependent read chain: %.1f cycles; store->load round trip: %.1f cycles\n", h[0] / 1000.0, h[1] / 1000.0);
   }
+  {
+    const size_t N = 64u << 20;  // 256 MiB of ints
+    int* nx;
+    hipMalloc(&nx, N * 4);
+    std::vector<int> hn(N);
+    for (int mode = 0; mode < 2; ++mode) {
+      const size_t span = mode == 0 ? 4096 : N;      // hot (16 KiB) / cold (256 MiB)
+      const size_t stride = mode == 0 ? 33 : 1000003; // ints
+      for (size_t i = 0; i < N; ++i) hn[i] = 0;
+      size_t j = 0;
+      for (int k = 0; k < 4096; ++k) { size_t nj = (j + stride) % span; hn[j] = (int)nj; j = nj; }
+      hipMemcpy(nx, hn.data(), N * 4, hipMemcpyHostToDevice);
+      int* oo; hipMalloc(&oo, 64);
+      k_glat<<<1, 1>>>(nx, oo, c, 2000);
+      hipMemcpy(h, c, 8, hipMemcpyDeviceToHost);
+      printf("global dependent load (%s): %.0f cycles\n", mode == 0 ? "hot 16KiB" : "cold 256MiB", h[0] / 2000.0);
+    }
+  }
   for (int nt = 256; nt <= 1024; nt *= 2)
     for (int mode = 0; mode < 3; ++mode) {
       k_bstep<<<1, nt>>>(o, c, 120, mode);
       hipMemcpy(h, c, 8, hipMemcpyDeviceToHost);
       printf("bsub step threads %d mode %d: %.0f cycles per step\n", nt, mode, h[0] / 120.0);
     }
+  {  // per-launch cost of a chain of small kernels in a captured graph
+    int* oo; hipMalloc(&oo, 64); hipMemset(oo, 0, 64);
+    hipStream_t st; hipStreamCreate(&st);
+    for (int nb : {1, 64}) {
+      hipGraph_t g; hipGraphExec_t ge;
+      hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
+      for (int i = 0; i < 100; ++i) k_empty<<<nb, 256, 0, st>>>(oo);
+      hipStreamEndCapture(st, &g);
+      hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+      hipGraphLaunch(ge, st); hipStreamSynchronize(st);
+      hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
+      hipEventRecord(a, st);
+      for (int r = 0; r < 20; ++r) hipGraphLaunch(ge, st);
+      hipEventRecord(b, st); hipEventSynchronize(b);
+      float ms; hipEventElapsedTime(&ms, a, b);
+      printf("graph of 100 empty kernels (%d blocks): %.2f us per kernel\n", nb, ms * 1e3 / 2000.0);
+    }
+  }
   hipError_t e = hipDeviceSynchronize();
   printf("%s\n", hipGetErrorString(e));
   return 0;

@@ -194,6 +194,28 @@ def test_solve_is_deterministic(og, gpu_ctx):
     assert np.array_equal(Pa, w.poses())
 
 
+def test_forked_and_serial_graphs_agree(og, gpu_ctx, monkeypatch):
+    """The captured iteration with fork streams (batches of at least one window per CU) and the
+    single-stream one (fewer windows; runtime.cpp ensureGraph) run the same kernels on disjoint
+    data in a fixed order per buffer: bitwise-equal solves, also with mu retries (GN prep)."""
+    ws = [_window(og, seed=s) for s in (41, 42, 43)]
+    opts = og.default_options(max_num_iterations=6, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    res = []
+    for ser in ("0", "1"):
+        monkeypatch.setenv("OKVISGPU_SERIAL_GRAPH", ser)
+        for w in ws:
+            w.reset()
+        gpu_ctx.set_problems([w.problem for w in ws])  # drops the captured graph
+        s = gpu_ctx.solve(opts, len(ws))
+        res.append((s, [w.poses().copy() for w in ws], [w.landmarks().copy() for w in ws]))
+    for k in range(len(ws)):
+        assert res[0][0][k]["final_cost"] == res[1][0][k]["final_cost"]
+        assert res[0][0][k]["num_iterations"] == res[1][0][k]["num_iterations"] == 6
+        assert np.array_equal(res[0][1][k], res[1][1][k])
+        assert np.array_equal(res[0][2][k], res[1][2][k])
+
+
 def _close(sg, so, rel=1e-7):
     assert sg["num_iterations"] == so["num_iterations"], (sg, so)
     assert sg["termination"] == so["termination"], (sg, so)
