@@ -177,6 +177,20 @@ void validate(const okvisgpu_problem* p, int w) {
   }
 }
 
+// Development: host-time split of analyse() (OKG_ANALYSE_TIMING, scripts/analyse_bench.cpp).
+#ifdef OKG_ANALYSE_TIMING
+double g_atime[16];
+std::chrono::steady_clock::time_point g_alast;
+#define ATIME(i)                                                                                    \
+  {                                                                                                 \
+    const auto now = std::chrono::steady_clock::now();                                             \
+    g_atime[i] += std::chrono::duration<double, std::milli>(now - g_alast).count();                 \
+    g_alast = now;                                                                                  \
+  }
+#else
+#define ATIME(i)
+#endif
+
 // Build the batch. `constOverride` carries okvisgpu_set_block_constant() edits.
 void analyse(const std::vector<const okvisgpu_problem*>& probs,
              const std::map<std::tuple<int, int, int>, int>& constOverride, HostBatch& B) {
@@ -184,7 +198,26 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
   B.part_gbegin.push_back(0);
   B.n_win = (int)probs.size();
   B.probs = probs;
+  {  // capacity for the per-observation / per-landmark arrays of the whole batch (no regrowth)
+    size_t no = 0, nl = 0;
+    for (const okvisgpu_problem* p : probs) {
+      no += (size_t)std::max(0, p->n_observations);
+      nl += (size_t)std::max(0, p->n_landmarks);
+    }
+    for (auto* v : {&B.obs_pose, &B.obs_lm, &B.obs_cam, &B.obs_win, &B.obs_orig, &B.visit_pose, &B.visit_lm,
+                    &B.visit_obs_begin})
+      v->reserve(no + 1);
+    B.obs_flags.reserve(no);
+    B.obs_kp.reserve(2 * no);
+    B.obs_L.reserve(4 * no);
+    B.lm.reserve(4 * nl);
+    B.lm_perm.reserve(nl);
+    B.lm_visit_begin.reserve(nl + 1);
+    B.lm_win.reserve(nl);
+    B.lm_free.reserve(nl);
+  }
   for (int w = 0; w < B.n_win; ++w) {
+    ATIME(0)
     const okvisgpu_problem* p = probs[w];
     validate(p, w);
     const int pb = (int)B.pose_win.size(), sbb = (int)B.sb_win.size(), lb = (int)B.lm_win.size();
@@ -241,6 +274,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     for (int i = 0; i < npx; ++i) B.pose_win.push_back(w);
     for (int i = 0; i < p->n_speed_biases; ++i) B.sb_win.push_back(w);
     for (int i = 0; i < p->n_landmarks; ++i) B.lm_win.push_back(w);
+    ATIME(1)
     // active blocks: free and used by a residual block that is not entirely constant
     std::vector<uint8_t> pa(npx, 0), sa(p->n_speed_biases, 0), la(p->n_landmarks, 0);
     std::vector<uint8_t> ofix(p->n_observations), ifix(p->n_imu);
@@ -326,14 +360,31 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     B.linv_total += (int64_t)(fpad / kTile) * kTile * kTile;
     B.max_fpad = std::max(B.max_fpad, fpad);
 
+    ATIME(2)
     // observations sorted by (internal landmark, pose, camera, original index)
+    // (counting sort by landmark, then insertion sort of each landmark's few observations: the
+    // order of a stable sort on that key, in linear time)
     std::vector<int> order(p->n_observations);
-    std::iota(order.begin(), order.end(), 0);
-    std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
-      if (p->obs_landmark[a] != p->obs_landmark[b]) return inv[p->obs_landmark[a]] < inv[p->obs_landmark[b]];
-      if (p->obs_pose[a] != p->obs_pose[b]) return p->obs_pose[a] < p->obs_pose[b];
-      return p->obs_camera[a] < p->obs_camera[b];
-    });
+    {
+      std::vector<int> start(p->n_landmarks + 1, 0);
+      for (int o = 0; o < p->n_observations; ++o) ++start[inv[p->obs_landmark[o]] + 1];
+      for (int l = 0; l < p->n_landmarks; ++l) start[l + 1] += start[l];
+      std::vector<int> fill(start.begin(), start.end() - 1);
+      for (int o = 0; o < p->n_observations; ++o) order[fill[inv[p->obs_landmark[o]]]++] = o;
+      auto before = [&](int a, int b) {
+        if (p->obs_pose[a] != p->obs_pose[b]) return p->obs_pose[a] < p->obs_pose[b];
+        if (p->obs_camera[a] != p->obs_camera[b]) return p->obs_camera[a] < p->obs_camera[b];
+        return a < b;
+      };
+      for (int l = 0; l < p->n_landmarks; ++l)
+        for (int i = start[l] + 1; i < start[l + 1]; ++i) {
+          const int x = order[i];
+          int j = i - 1;
+          for (; j >= start[l] && before(x, order[j]); --j) order[j + 1] = order[j];
+          order[j + 1] = x;
+        }
+    }
+    ATIME(3)
     // visits and landmark -> visit ranges
     const int vBase = (int)B.visit_pose.size();
     std::vector<int> lmVisitBegin(p->n_landmarks + 1, 0);
@@ -374,6 +425,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       lmVisitBegin[p->n_landmarks] = acc;
       for (int l = 0; l < p->n_landmarks; ++l) B.lm_visit_begin.push_back(lmVisitBegin[l]);
     }
+    ATIME(4)
     // extrinsic visits: per landmark and variable camera, the landmark's (non-fixed) observations
     // through that camera (the extrinsics block is the third parameter block of their
     // ReprojectionErrors); global indices, in landmark order like the visits
@@ -401,6 +453,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       }
       lmXBegin[p->n_landmarks] = (int)B.xvisit_pose.size();
     }
+    ATIME(5)
     // landmark groups of k_lm_visit (consecutive whole landmarks of this window, <= kLmGroupVisits
     // visits and <= kLmGroupMax landmarks; one workgroup, one thread per visit) and their visit
     // segments: the visits of a group that belong to one free pose, pre-summed by k_lm_visit into
@@ -413,22 +466,31 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       // order, so a segment is a contiguous slot range [seg_range.x, seg_range.y)
       // A group's threads: its pose visits first (thread t = v - gv0), then its extrinsic visits
       // (thread t = nvg + xv - gx0).
+      std::vector<std::pair<int, int>> mem, gitems, gprod;  // scratch reused by every group
+      std::vector<int> glocal, gcount, gfill, fbLocal(std::max(1, (int)B.fb_off.size()), -1);
+      std::vector<int32_t> gsorted;
       auto closeGroup = [&](int gl0, int gl1) {
         const int gv0 = lmVisitBegin[gl0], gv1 = lmVisitBegin[gl1], nvg = gv1 - gv0;
         const int gx0 = lmXBegin[gl0], gx1 = lmXBegin[gl1];
-        std::map<int, std::vector<int>> mem;  // pose-kind block -> members (v >= 0 visit, -1 - xv extrinsic visit)
+        // members (v >= 0 visit, -1 - xv extrinsic visit) grouped by pose-kind block, ascending,
+        // each block's members in visit order
+        mem.clear();
         for (int v = gv0; v < gv1; ++v) {
           const int ps = B.visit_pose[v] - pb;
-          if (posef[ps] >= 0) mem[ps].push_back(v);
+          if (posef[ps] >= 0) mem.push_back({ps, v});
           else B.visit_slot[v] = -1;
         }
-        for (int xv = gx0; xv < gx1; ++xv) mem[B.xvisit_pose[xv] - pb].push_back(-1 - xv);
+        for (int xv = gx0; xv < gx1; ++xv) mem.push_back({B.xvisit_pose[xv] - pb, -1 - xv});
+        std::stable_sort(mem.begin(), mem.end(),
+                         [](const std::pair<int, int>& a, const std::pair<int, int>& b) { return a.first < b.first; });
         int slot = 0;
-        for (auto& kv : mem) {
-          segsAtPose[kv.first].push_back((int)B.seg_pose.size());
-          B.seg_pose.push_back(pb + kv.first);
+        for (size_t m = 0; m < mem.size();) {
+          const int ps = mem[m].first;
+          segsAtPose[ps].push_back((int)B.seg_pose.size());
+          B.seg_pose.push_back(pb + ps);
           B.seg_range.push_back(slot);
-          for (int v : kv.second) {
+          for (; m < mem.size() && mem[m].first == ps; ++m) {
+            const int v = mem[m].second;
             if (v >= 0) B.visit_slot[v] = slot++;
             else B.xvisit_slot[-1 - v] = slot++;
           }
@@ -437,8 +499,20 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
         // partial Schur blocks (k_lm_visit): per f-block pair (row >= col by f offset) the products
         // Z_a Z_b^T of the group's free landmarks; contributions packed as (a | b << 16), thread
         // offsets within the group
-        std::map<std::pair<int, int>, std::vector<int32_t>> gparts;
-        std::vector<std::pair<int, int>> items;  // (thread, f-block) of one landmark's free visits
+        // products keyed by f-block pair, in (row f-block, col f-block) order, each key's products
+        // in generation order: the group's f-blocks get dense local indices in ascending order and
+        // the products are counting-sorted by (local row, local col)
+        std::vector<std::pair<int, int>>& items = gitems;  // (thread, f-block) of one landmark's free visits
+        glocal.clear();
+        for (int v = gv0; v < gv1; ++v)
+          if (laNew[B.visit_lm[v] - lb] && poseFb[B.visit_pose[v] - pb] >= 0) glocal.push_back(poseFb[B.visit_pose[v] - pb]);
+        for (int xv = gx0; xv < gx1; ++xv)
+          if (laNew[B.xvisit_lm[xv] - lb]) glocal.push_back(poseFb[B.xvisit_pose[xv] - pb]);
+        std::sort(glocal.begin(), glocal.end());
+        glocal.erase(std::unique(glocal.begin(), glocal.end()), glocal.end());
+        const int nloc = (int)glocal.size();
+        for (int i = 0; i < nloc; ++i) fbLocal[glocal[i]] = i;
+        gprod.clear();
         for (int l = gl0; l < gl1; ++l) {
           if (!laNew[l]) continue;
           items.clear();
@@ -451,19 +525,27 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
           for (const auto& a : items)
             for (const auto& b : items) {
               if (B.fb_off[a.second] < B.fb_off[b.second]) continue;
-              gparts[std::make_pair(a.second, b.second)].push_back(a.first | (b.first << 16));
+              gprod.push_back({fbLocal[a.second] * nloc + fbLocal[b.second], a.first | (b.first << 16)});
             }
         }
+        gcount.assign((size_t)nloc * nloc + 1, 0);
+        for (const auto& x : gprod) ++gcount[x.first + 1];
+        for (int k = 0; k < nloc * nloc; ++k) gcount[k + 1] += gcount[k];
+        gsorted.resize(gprod.size());
+        gfill.assign(gcount.begin(), gcount.end() - 1);
+        for (const auto& x : gprod) gsorted[gfill[x.first]++] = x.second;
         // long blocks are split into chunks of <= kPartChunk products (separate records, summed
         // in order by k_assemble_pp) so that no k_lm_visit thread serialises a whole block
-        constexpr size_t kPartChunk = 24;  // measured: 6 / 12 / 24 / unsplit on 2048 S50 windows
-        for (auto& kv : gparts)
-          for (size_t c0 = 0; c0 < kv.second.size(); c0 += kPartChunk) {
-            const size_t c1 = std::min(kv.second.size(), c0 + kPartChunk);
-            partKeys.push_back(kv.first);
+        constexpr int kPartChunk = 24;  // measured: 6 / 12 / 24 / unsplit on 2048 S50 windows
+        for (int key = 0; key < nloc * nloc; ++key) {
+          const int k0 = gcount[key], k1 = gcount[key + 1];
+          for (int c0 = k0; c0 < k1; c0 += kPartChunk) {
+            const int c1 = std::min(k1, c0 + kPartChunk);
+            partKeys.push_back({glocal[key / nloc], glocal[key % nloc]});
             B.part_cbegin.push_back((int)B.part_contrib.size());
-            B.part_contrib.insert(B.part_contrib.end(), kv.second.begin() + c0, kv.second.begin() + c1);
+            B.part_contrib.insert(B.part_contrib.end(), gsorted.begin() + c0, gsorted.begin() + c1);
           }
+        }
         B.lmg_begin.push_back(lb + gl0);
         B.lmg_xbegin.push_back(gx0);
         B.seg_gbegin.push_back((int)B.seg_pose.size());
@@ -499,6 +581,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       }
       if (p->n_landmarks > 0) closeGroup(g0, p->n_landmarks);
     }
+    ATIME(6)
     // imu
     const int sBase = (int)B.imu_ts.size();
     for (int f = 0; f < p->n_imu; ++f) {
@@ -558,6 +641,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     appendN(B.win_sbp_range, r_sbp, 2);
     appendN(B.win_rp_range, r_rp, 2);
 
+    ATIME(7)
     // ---- f-block gradient / diagonal contribution lists
     const int nFb = (int)B.fb_win.size() - fbBase;
     std::vector<std::vector<Contrib>> fbc(nFb);
@@ -592,6 +676,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       B.fb_cbegin.push_back((int)B.fb_contrib.size());
       B.fb_contrib.insert(B.fb_contrib.end(), fbc[k].begin(), fbc[k].end());
     }
+    ATIME(8)
     // ---- block pairs (fi >= fj by reduced offset) and their contribution lists
     std::map<std::pair<int, int>, std::vector<Contrib>> pairs;
     auto key = [&](int fa, int fb2) {  // row = larger offset
@@ -652,6 +737,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
           pairs[key(fbs[u], fbs[v])].push_back(Contrib{C_RELPOSE, rpb + i, 6 * u, 6 * v});
         }
     }
+    ATIME(9)
     // diagonal pairs must exist for every f-block (they carry the damping, diag and rhs)
     for (int k = fbBase; k < (int)B.fb_win.size(); ++k) pairs[std::make_pair(k, k)];
     // tile-level structure of S and its symbolic LLT (fill within the envelope)
@@ -783,6 +869,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
   B.imu_sbegin.push_back((int)B.imu_ts.size());
   B.fb_cbegin.push_back((int)B.fb_contrib.size());
   B.pair_cbegin.push_back((int)B.pair_contrib.size());
+  ATIME(10)
 }
 
 // A single hipMalloc arena carved into the device arrays.
@@ -810,6 +897,9 @@ struct okvisgpu_ctx {
   HostBatch B;
   std::vector<const okvisgpu_problem*> probs;
   std::map<std::tuple<int, int, int>, int> constOverride;
+  void* hostStage = nullptr;  // pinned staging of the uploaded arrays (kept between set_problems)
+  size_t hostStageBytes = 0;
+  size_t arenaCap = 0;        // bytes allocated at `arena` (reused while a new batch fits)
   bool structureDirty = false;
   DevProblem P{};
   void* arena = nullptr;
@@ -847,6 +937,7 @@ struct okvisgpu_ctx {
   ~okvisgpu_ctx() {
     if (iterGraph) (void)hipGraphExecDestroy(iterGraph);
     if (arena) (void)hipFree(arena);
+    if (hostStage) (void)hipHostFree(hostStage);
     for (hipEvent_t e : forkEv) (void)hipEventDestroy(e);
     for (hipStream_t q : side)
       if (q) (void)hipStreamDestroy(q);
@@ -866,16 +957,19 @@ struct okvisgpu_ctx {
     haveProblem = false;
     inSolve = false;
     dropGraph();
+    const bool timing = std::getenv("OKVISGPU_BUILD_TIMING") != nullptr;  // development: host cost split
+    const auto tb0 = std::chrono::steady_clock::now();
     {
       HostBatch nb;
       analyse(probs, constOverride, nb);  // may throw: B is untouched until it succeeds
       B = std::move(nb);
     }
-    if (arena) {
-      HIPCHK(hipFree(arena));
-      arena = nullptr;
-    }
-    Arena A;
+    const auto tb1 = std::chrono::steady_clock::now();
+    // the uploaded arrays are laid out first (one contiguous host -> device copy from a pinned
+    // staging buffer), the scratch arrays after them (one memset); a scratch offset carries
+    // kScratchTag until the two regions are placed
+    constexpr size_t kScratchTag = size_t(1) << 62;
+    Arena A, AS;
     DevProblem& D = P;
     D = DevProblem{};
     D.n_win = B.n_win;
@@ -904,7 +998,7 @@ struct okvisgpu_ctx {
       ups.push_back(Up{off, vec.data(), bytes});
       return off;
     };
-    auto scratch = [&](size_t bytes) { return A.reserve(bytes); };
+    auto scratch = [&](size_t bytes) { return kScratchTag | AS.reserve(bytes); };
     const size_t o_pose0 = upl(B.pose), o_pose1 = upl(B.pose), o_sb0 = upl(B.sb), o_sb1 = upl(B.sb);
     const size_t o_lm0 = upl(B.lm), o_lm1 = upl(B.lm), o_extr = upl(B.extr), o_cam = upl(B.cam);
     const size_t o_pose_win = upl(B.pose_win), o_sb_win = upl(B.sb_win), o_lm_win = upl(B.lm_win);
@@ -984,17 +1078,44 @@ struct okvisgpu_ctx {
     for (int i = 0; i < 7; ++i) ol[i] = scratch(sizeof(double) * nl3);
     const size_t o_st = scratch(sizeof(WinState) * D.n_win);
     const size_t o_self = scratch(sizeof(DevProblem));
-    // ---- allocate + upload
-    HIPCHK(hipMalloc(&arena, A.size));
-    arenaBytes = A.size;
+    // ---- allocate (reusing the arena while the batch fits) + upload
+    const size_t upSize = (A.size + 255) & ~size_t(255);
+    const size_t total = upSize + AS.size;
+    if (!arena || total > arenaCap) {
+      if (arena) {
+        HIPCHK(hipFree(arena));
+        arena = nullptr;
+        arenaCap = 0;
+      }
+      HIPCHK(hipMalloc(&arena, total));
+      arenaCap = total;
+    }
+    arenaBytes = total;
     char* base = static_cast<char*>(arena);
-    HIPCHK(hipMemsetAsync(arena, 0, A.size, stream));
+    if (A.size > hostStageBytes) {
+      if (hostStage) HIPCHK(hipHostFree(hostStage));
+      hostStage = nullptr;
+      hostStageBytes = 0;
+      HIPCHK(hipHostMalloc(&hostStage, A.size, hipHostMallocDefault));
+      hostStageBytes = A.size;
+    }
+    HIPCHK(hipStreamSynchronize(stream));  // the staging buffer is free (previous upload done)
+    const auto tb2 = std::chrono::steady_clock::now();
     for (const Up& u : ups)
-      if (u.bytes) HIPCHK(hipMemcpyAsync(base + u.off, u.src, u.bytes, hipMemcpyHostToDevice, stream));
-    auto dp = [&](size_t off) { return reinterpret_cast<double*>(base + off); };
-    auto ip = [&](size_t off) { return reinterpret_cast<int32_t*>(base + off); };
-    auto lp = [&](size_t off) { return reinterpret_cast<int64_t*>(base + off); };
-    auto up = [&](size_t off) { return reinterpret_cast<uint8_t*>(base + off); };
+      if (u.bytes) std::memcpy(static_cast<char*>(hostStage) + u.off, u.src, u.bytes);
+    const auto tb3 = std::chrono::steady_clock::now();
+    if (timing) {
+      auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+      std::fprintf(stderr, "okvisgpu build: analyse %.3f ms, layout+alloc %.3f ms, stage %.3f ms (%zu B)\n", ms(tb0, tb1),
+                   ms(tb1, tb2), ms(tb2, tb3), A.size);
+    }
+    if (A.size) HIPCHK(hipMemcpyAsync(base, hostStage, A.size, hipMemcpyHostToDevice, stream));
+    HIPCHK(hipMemsetAsync(base + upSize, 0, AS.size, stream));
+    auto place = [&](size_t off) { return (off & kScratchTag) ? upSize + (off & ~kScratchTag) : off; };
+    auto dp = [&](size_t off) { return reinterpret_cast<double*>(base + place(off)); };
+    auto ip = [&](size_t off) { return reinterpret_cast<int32_t*>(base + place(off)); };
+    auto lp = [&](size_t off) { return reinterpret_cast<int64_t*>(base + place(off)); };
+    auto up = [&](size_t off) { return reinterpret_cast<uint8_t*>(base + place(off)); };
     D.pose[0] = dp(o_pose0); D.pose[1] = dp(o_pose1); D.sb[0] = dp(o_sb0); D.sb[1] = dp(o_sb1);
     D.lm[0] = dp(o_lm0); D.lm[1] = dp(o_lm1); D.extr = dp(o_extr); D.cam = dp(o_cam);
     D.pose_win = ip(o_pose_win); D.sb_win = ip(o_sb_win); D.lm_win = ip(o_lm_win);
@@ -1036,12 +1157,12 @@ struct okvisgpu_ctx {
     D.rp_lin[0] = dp(o_rp_lin0); D.rp_lin[1] = dp(o_rp_lin1);
     D.rp_cost[0] = dp(o_rp_cost0); D.rp_cost[1] = dp(o_rp_cost1); D.rp_jv = dp(o_rp_jv);
     D.fb_win = ip(o_fbw); D.fb_kind = ip(o_fbk); D.fb_index = ip(o_fbi); D.fb_off = ip(o_fbo);
-    D.fb_cbegin = ip(o_fbcb); D.fb_contrib = reinterpret_cast<const Contrib*>(base + o_fbc);
+    D.fb_cbegin = ip(o_fbcb); D.fb_contrib = reinterpret_cast<const Contrib*>(base + place(o_fbc));
     D.pair_win = ip(o_pw); D.pair_fi = ip(o_pfi); D.pair_fj = ip(o_pfj); D.pair_cbegin = ip(o_pcb);
-    D.pair_contrib = reinterpret_cast<const Contrib*>(base + o_pc);
+    D.pair_contrib = reinterpret_cast<const Contrib*>(base + place(o_pc));
     D.pair_runs = ip(o_pruns);
-    D.tile_nz = reinterpret_cast<const uint8_t*>(base + o_tnz);
-    D.win_tnzoff = reinterpret_cast<const int64_t*>(base + o_tnzoff);
+    D.tile_nz = reinterpret_cast<const uint8_t*>(base + place(o_tnz));
+    D.win_tnzoff = reinterpret_cast<const int64_t*>(base + place(o_tnzoff));
     D.chol_panel_items = ip(o_cpi); D.chol_panel_begin = ip(o_cpb);
     D.chol_upd_items = ip(o_cui); D.chol_upd_begin = ip(o_cub);
     D.h_panel_begin = B.chol_panel_begin.data();
@@ -1062,8 +1183,8 @@ struct okvisgpu_ctx {
     double** lv[7] = {&D.sL, &D.diagL, &D.stepL, &D.yL, &D.gnL, &D.dgL, &D.vL};
     for (int i = 0; i < 7; ++i) *lv[i] = dp(ol[i]);
     D.gL = D.lm_g;  // the landmark gradient is the accumulated J_l^T r
-    D.st = reinterpret_cast<WinState*>(base + o_st);
-    D.self = reinterpret_cast<const DevProblem*>(base + o_self);
+    D.st = reinterpret_cast<WinState*>(base + place(o_st));
+    D.self = reinterpret_cast<const DevProblem*>(base + place(o_self));
     HIPCHK(hipStreamSynchronize(stream));
     uploadDescriptor();
     haveProblem = true;
