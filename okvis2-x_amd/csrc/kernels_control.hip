@@ -191,6 +191,43 @@ __device__ void finalizeIteration(const DevProblem& P, WinState& s) {
   }
 }
 
+// J*v reductions of window w (once per GN step): jcc, jgg, jcg and the Cauchy alpha =
+// |gradient_|^2 / jcc, stored by thread 0 in the window state; every thread gets alpha.
+// Reprojection rows and landmark gradients come as the landmark groups' sums (k_lm_backsub_jv).
+__device__ double reduceJv(const DevProblem& P, int w, WinState& s, double* sh) {
+  const int t = threadIdx.x;
+  const int ib = P.win_imu_range[2 * w], ie = P.win_imu_range[2 * w + 1];
+  const int pb = P.win_pp_range[2 * w], pe = P.win_pp_range[2 * w + 1];
+  const int sbb = P.win_sbp_range[2 * w], sbe = P.win_sbp_range[2 * w + 1];
+  const int rpb = P.win_rp_range[2 * w], rpe = P.win_rp_range[2 * w + 1];
+  const int gb = P.win_lmg_range[2 * w], ge = P.win_lmg_range[2 * w + 1];
+  double a[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    double acc = 0.0;
+    for (int g = gb + t; g < ge; g += kRB) acc += P.grp_red[(size_t)g * kGrpRed + k];
+    for (int f = ib + t; f < ie; f += kRB) acc += P.imu_jv[(size_t)k * P.n_imu + f];
+    for (int i = pb + t; i < pe; i += kRB) acc += P.pp_jv[(size_t)k * P.n_pprior + i];
+    for (int i = sbb + t; i < sbe; i += kRB) acc += P.sbp_jv[(size_t)k * P.n_sbprior + i];
+    for (int i = rpb + t; i < rpe; i += kRB) acc += P.rp_jv[(size_t)k * P.n_relpose + i];
+    a[k] = blockSum(acc, sh);
+  }
+  // |gradient_|^2 over the window (f-vector + free landmarks)
+  double g2 = 0.0;
+  const int fo = P.win_foff[w], fd = P.win_fdim[w];
+  for (int e = t; e < fd; e += kRB) g2 += P.dgF[fo + e] * P.dgF[fo + e];
+  for (int g = gb + t; g < ge; g += kRB) g2 += P.grp_red[(size_t)g * kGrpRed + 3];
+  g2 = blockSum(g2, sh);
+  const double alpha = g2 / a[0];
+  if (t == 0) {
+    s.jcc = a[0];
+    s.jgg = a[1];
+    s.jcg = a[2];
+    s.alpha = alpha;
+  }
+  return alpha;
+}
+
 __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ Pp, int mode) {
   const DevProblem& P = *Pp;
   const int w = blockIdx.x;
@@ -285,33 +322,9 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
     return;
   }
 
-  // J*v reductions (once per GN step): jcc, jgg, jcg and the Cauchy alpha = |gradient_|^2 / jcc
+  // J*v reductions (once per GN step)
   if (!(s.need_gn && !s.gn_failed)) return;
-  // reprojection rows and landmark gradients: the landmark groups' sums (k_lm_backsub_jv)
-  const int gb = P.win_lmg_range[2 * w], ge = P.win_lmg_range[2 * w + 1];
-  double a[3];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    double acc = 0.0;
-    for (int g = gb + t; g < ge; g += kRB) acc += P.grp_red[(size_t)g * kGrpRed + k];
-    for (int f = ib + t; f < ie; f += kRB) acc += P.imu_jv[(size_t)k * P.n_imu + f];
-    for (int i = pb + t; i < pe; i += kRB) acc += P.pp_jv[(size_t)k * P.n_pprior + i];
-    for (int i = sbb + t; i < sbe; i += kRB) acc += P.sbp_jv[(size_t)k * P.n_sbprior + i];
-    for (int i = rpb + t; i < rpe; i += kRB) acc += P.rp_jv[(size_t)k * P.n_relpose + i];
-    a[k] = blockSum(acc, sh);
-  }
-  // |gradient_|^2 over the window (f-vector + free landmarks)
-  double g2 = 0.0;
-  const int fo = P.win_foff[w], fd = P.win_fdim[w];
-  for (int e = t; e < fd; e += kRB) g2 += P.dgF[fo + e] * P.dgF[fo + e];
-  for (int g = gb + t; g < ge; g += kRB) g2 += P.grp_red[(size_t)g * kGrpRed + 3];
-  g2 = blockSum(g2, sh);
-  if (t == 0) {
-    s.jcc = a[0];
-    s.jgg = a[1];
-    s.jcg = a[2];
-    s.alpha = g2 / a[0];
-  }
+  reduceJv(P, w, s, sh);
 }
 
 // |x - Plus(x, -g)| and |x| over the window's active blocks; gradient tolerance test.
@@ -407,6 +420,8 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
   __shared__ double sh[kRB];
   __shared__ int sflag;
   const int t = threadIdx.x;
+  const bool sflagGn = s.need_gn && !s.gn_failed;  // (read before thread 0 updates the state)
+  __syncthreads();
   if (t == 0) {
     sflag = 0;
     s.accepted = 0;
@@ -439,6 +454,10 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
   }
   __syncthreads();
   if (sflag) return;
+  // a new GN step: its J*v reduction first (formerly k_reduce R_JV, one launch fewer per
+  // iteration; the same workgroup per window, so a barrier orders it)
+  double alpha = s.alpha;
+  if (sflagGn) alpha = reduceJv(P, w, s, sh);
   const int foff = P.win_foff[w], fd = P.win_fdim[w];
   const int l0 = P.win_lm_range[2 * w], l1 = P.win_lm_range[2 * w + 1];
   // pass 1: norms (f-blocks here, landmarks as the landmark groups' sums of k_lm_backsub_jv)
@@ -460,7 +479,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
   nn = blockSum(nn, sh);
   gn = blockSum(gn, sh);
   const double gradient_norm = sqrt(gg), gauss_newton_norm = sqrt(nn);
-  const double radius = s.radius, alpha = s.alpha;
+  const double radius = s.radius;
   // step = ca * gradient_ + cb * gauss_newton_step_  (then divided by diagonal_)
   double ca, cb;
   int dcase;

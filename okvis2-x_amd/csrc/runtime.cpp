@@ -1314,7 +1314,6 @@ struct okvisgpu_ctx {
     launch_cholesky(P, stream);
     launch_gn_backsub(P, stream);
     launch_jv(P, stream);
-    launch_reduce(P, R_JV, stream);
     launch_dogleg(P, stream);
     launch_eval(P, 1, stream);
     launch_reduce(P, R_COST_CAND, stream);
@@ -1362,7 +1361,6 @@ struct okvisgpu_ctx {
     launch_jv(P, side[0]);
     launch_lm_backsub(P, stream);
     join(side[0]);
-    launch_reduce(P, R_JV, stream);
     launch_dogleg(P, stream);
     // candidate evaluation
     fork(side[0]);
@@ -1697,7 +1695,7 @@ int okvisgpu_profile_iteration(okvisgpu_ctx* c, double* ms) {
     launch_gn_finalize(P, s); mark(5);
     launch_lm_backsub(P, s); mark(4);
     launch_jv(P, s); mark(6);
-    launch_reduce(P, R_JV, s); mark(7);
+    mark(7);  // (the J*v reduction runs inside k_dogleg)
     launch_dogleg(P, s); mark(8);
     launch_eval_obs(P, 1, s); mark(9);
     launch_eval_imu(P, 1, s); mark(10);
