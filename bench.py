@@ -396,8 +396,7 @@ def main(argv=None):
         w.reset()
     ctx.synchronize()
     a = time.perf_counter()
-    ctx.update_params()
-    ctx.solve(opts)
+    ctx.solve(opts)  # okvisgpu_solve uploads the parameters itself
     pcie_s = time.perf_counter() - a
 
     value = args.windows * args.steps / elapsed

@@ -635,4 +635,24 @@ void launch_dogleg(const DevProblem& P, hipStream_t s) {
   hipLaunchKernelGGL(k_dogleg, dim3(P.n_win), dim3(kRB), 0, s, P.self);
 }
 
+// Write-back staging: a window whose current parameters are set 1 gets them copied into set 0, so
+// one device-to-host copy of set 0 holds every window's result (set 0 is then that window's
+// candidate buffer, which the next step overwrites before reading). One workgroup per window.
+__global__ __launch_bounds__(256) void k_select_current(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
+  const int w = blockIdx.x;
+  if (P.st[w].xcur != 1) return;
+  auto copy = [&](const int32_t* range, int stride, const double* src, double* dst) {
+    const int64_t b = (int64_t)range[2 * w] * stride, e = (int64_t)range[2 * w + 1] * stride;
+    for (int64_t i = b + threadIdx.x; i < e; i += blockDim.x) dst[i] = src[i];
+  };
+  copy(P.win_pose_range, 7, P.pose[1], P.pose[0]);
+  copy(P.win_sb_range, 9, P.sb[1], P.sb[0]);
+  copy(P.win_lm_range, 4, P.lm[1], P.lm[0]);
+}
+
+void launch_select_current(const DevProblem& P, hipStream_t s) {
+  if (P.n_win > 0) hipLaunchKernelGGL(k_select_current, dim3(P.n_win), dim3(256), 0, s, P.self);
+}
+
 }  // namespace okg

@@ -45,6 +45,7 @@ void launch_reduce(const DevProblem& P, int mode, hipStream_t s);
 void launch_jv(const DevProblem& P, hipStream_t s);
 void launch_gradnorm(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_dogleg(const DevProblem& P, hipStream_t s);
+void launch_select_current(const DevProblem& P, hipStream_t s);  // set 1 -> set 0 where xcur == 1
 
 // pose-graph edges (kernels_twopose.hip): TwoPoseStandardGraphError::compute, one wavefront per edge
 void launch_twopose_compute(const TwoPoseDev& T, hipStream_t s);

@@ -20,6 +20,7 @@
 #include <numeric>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/okvisgpu.h"
@@ -53,6 +54,30 @@ struct UnsupportedError {
 
 double nowS() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Per-window host copies (parameter staging / write-back) split over host threads: contiguous
+// window ranges, one thread per range. Small batches run on the calling thread. The thread count
+// follows OMP_NUM_THREADS (the job's CPU share) and is capped at 16.
+template <class F>
+void forWindows(int n, F&& fn) {
+  static const int cap = [] {
+    const char* e = std::getenv("OMP_NUM_THREADS");
+    int t = e ? std::atoi(e) : (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(t, 16));
+  }();
+  const int nt = std::min(cap, n / 64);
+  if (nt <= 1) {
+    for (int w = 0; w < n; ++w) fn(w);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(nt);
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&, t]() {
+      for (int w = (int)((int64_t)n * t / nt); w < (int)((int64_t)n * (t + 1) / nt); ++w) fn(w);
+    });
+  for (auto& x : th) x.join();
 }
 
 // Host mirror of everything uploaded (built by analyse()).
@@ -1242,56 +1267,79 @@ struct okvisgpu_ctx {
     HIPCHK(hipMemcpyAsync(P.st, s.data(), sizeof(WinState) * s.size(), hipMemcpyHostToDevice, stream));
   }
 
-  // Upload current host parameter values into both parameter sets (+ IMU state).
+  // Pinned staging for the parameter copies: the set_problems staging buffer (it holds both
+  // parameter sets and the IMU states, so it is large enough), grown if ever needed.
+  char* paramStage(size_t bytes) {
+    HIPCHK(hipStreamSynchronize(stream));  // no copy out of / into it is still in flight
+    if (bytes > hostStageBytes) {
+      if (hostStage) HIPCHK(hipHostFree(hostStage));
+      hostStage = nullptr;
+      hostStageBytes = 0;
+      HIPCHK(hipHostMalloc(&hostStage, bytes, hipHostMallocDefault));
+      hostStageBytes = bytes;
+    }
+    return static_cast<char*>(hostStage);
+  }
+
+  // Upload current host parameter values into both parameter sets (+ IMU state): the windows are
+  // packed into pinned memory in device order (host threads over windows), set 0 and the IMU
+  // states go up in one copy each, and set 1 is a device-side copy of set 0.
   void uploadParams() {
-    std::vector<double> pose, sb, lm, imu;
-    for (int w = 0; w < B.n_win; ++w) {
+    const size_t np = 7 * (size_t)P.n_pose, ns = 9 * (size_t)P.n_sb, nl = 4 * (size_t)P.n_lm,
+                 ni = (size_t)P.n_imu * kImuState;
+    double* pose = reinterpret_cast<double*>(paramStage((np + ns + nl + ni) * 8));
+    double *sb = pose + np, *lm = sb + ns, *imu = lm + nl;
+    forWindows(B.n_win, [&](int w) {
       const okvisgpu_problem* p = probs[w];
-      appendN(pose, p->poses, (size_t)7 * p->n_poses);
-      appendN(pose, p->extrinsics, (size_t)7 * p->n_cameras);
-      appendN(sb, p->speed_biases, (size_t)9 * p->n_speed_biases);
-      for (int k = 0; k < p->n_landmarks; ++k)
-        appendN(lm, &p->landmarks[4 * (size_t)B.lm_perm[B.lm_base[w] + k]], 4);
-      for (int f = 0; f < p->n_imu; ++f) {
-        if (p->imu_state) appendN(imu, &p->imu_state[(size_t)f * OKVISGPU_IMU_STATE_DOUBLES], OKVISGPU_IMU_STATE_DOUBLES);
-        else imu.insert(imu.end(), OKVISGPU_IMU_STATE_DOUBLES, 0.0);
-      }
-    }
-    for (int k = 0; k < 2; ++k) {
-      if (!pose.empty()) HIPCHK(hipMemcpyAsync(P.pose[k], pose.data(), pose.size() * 8, hipMemcpyHostToDevice, stream));
-      if (!sb.empty()) HIPCHK(hipMemcpyAsync(P.sb[k], sb.data(), sb.size() * 8, hipMemcpyHostToDevice, stream));
-      if (!lm.empty()) HIPCHK(hipMemcpyAsync(P.lm[k], lm.data(), lm.size() * 8, hipMemcpyHostToDevice, stream));
-    }
-    if (!imu.empty()) HIPCHK(hipMemcpyAsync(P.imu_state, imu.data(), imu.size() * 8, hipMemcpyHostToDevice, stream));
+      double* q = pose + 7 * (size_t)B.pose_base[w];
+      std::memcpy(q, p->poses, sizeof(double) * 7 * p->n_poses);
+      std::memcpy(q + 7 * (size_t)p->n_poses, p->extrinsics, sizeof(double) * 7 * p->n_cameras);
+      std::memcpy(sb + 9 * (size_t)B.sb_base[w], p->speed_biases, sizeof(double) * 9 * p->n_speed_biases);
+      double* l = lm + 4 * (size_t)B.lm_base[w];
+      const int* perm = &B.lm_perm[B.lm_base[w]];
+      for (int k = 0; k < p->n_landmarks; ++k) std::memcpy(l + 4 * (size_t)k, &p->landmarks[4 * (size_t)perm[k]], 32);
+      double* f = imu + (size_t)B.imu_base[w] * kImuState;
+      if (p->imu_state) std::memcpy(f, p->imu_state, sizeof(double) * kImuState * p->n_imu);
+      else std::memset(f, 0, sizeof(double) * kImuState * p->n_imu);
+    });
+    if (np) HIPCHK(hipMemcpyAsync(P.pose[0], pose, np * 8, hipMemcpyHostToDevice, stream));
+    if (ns) HIPCHK(hipMemcpyAsync(P.sb[0], sb, ns * 8, hipMemcpyHostToDevice, stream));
+    if (nl) HIPCHK(hipMemcpyAsync(P.lm[0], lm, nl * 8, hipMemcpyHostToDevice, stream));
+    if (ni) HIPCHK(hipMemcpyAsync(P.imu_state, imu, ni * 8, hipMemcpyHostToDevice, stream));
+    if (np) HIPCHK(hipMemcpyAsync(P.pose[1], P.pose[0], np * 8, hipMemcpyDeviceToDevice, stream));
+    if (ns) HIPCHK(hipMemcpyAsync(P.sb[1], P.sb[0], ns * 8, hipMemcpyDeviceToDevice, stream));
+    if (nl) HIPCHK(hipMemcpyAsync(P.lm[1], P.lm[0], nl * 8, hipMemcpyDeviceToDevice, stream));
     HIPCHK(hipStreamSynchronize(stream));
   }
 
-  // Write device results back into the caller's arrays (parameter set xcur of each window).
-  void downloadParams(const std::vector<WinState>& st) {
-    const size_t np = 7 * (size_t)P.n_pose, ns = 9 * (size_t)P.n_sb, nl = 4 * (size_t)P.n_lm;
-    std::vector<double> pose[2], sb[2], lm[2], imu((size_t)P.n_imu * kImuState);
-    for (int k = 0; k < 2; ++k) {
-      pose[k].resize(np); sb[k].resize(ns); lm[k].resize(nl);
-      if (np) HIPCHK(hipMemcpyAsync(pose[k].data(), P.pose[k], np * 8, hipMemcpyDeviceToHost, stream));
-      if (ns) HIPCHK(hipMemcpyAsync(sb[k].data(), P.sb[k], ns * 8, hipMemcpyDeviceToHost, stream));
-      if (nl) HIPCHK(hipMemcpyAsync(lm[k].data(), P.lm[k], nl * 8, hipMemcpyDeviceToHost, stream));
-    }
-    if (!imu.empty()) HIPCHK(hipMemcpyAsync(imu.data(), P.imu_state, imu.size() * 8, hipMemcpyDeviceToHost, stream));
+  // Write device results back into the caller's arrays: k_select_current gathers every window's
+  // current parameter set into set 0 (WinState::xcur on the device), then one copy per array into
+  // pinned memory and a threaded scatter into the windows' arrays.
+  void downloadParams() {
+    const size_t np = 7 * (size_t)P.n_pose, ns = 9 * (size_t)P.n_sb, nl = 4 * (size_t)P.n_lm,
+                 ni = (size_t)P.n_imu * kImuState;
+    double* pose = reinterpret_cast<double*>(paramStage((np + ns + nl + ni) * 8));
+    double *sb = pose + np, *lm = sb + ns, *imu = lm + nl;
+    launch_select_current(P, stream);
+    HIPCHK(hipGetLastError());
+    if (np) HIPCHK(hipMemcpyAsync(pose, P.pose[0], np * 8, hipMemcpyDeviceToHost, stream));
+    if (ns) HIPCHK(hipMemcpyAsync(sb, P.sb[0], ns * 8, hipMemcpyDeviceToHost, stream));
+    if (nl) HIPCHK(hipMemcpyAsync(lm, P.lm[0], nl * 8, hipMemcpyDeviceToHost, stream));
+    if (ni) HIPCHK(hipMemcpyAsync(imu, P.imu_state, ni * 8, hipMemcpyDeviceToHost, stream));
     HIPCHK(hipStreamSynchronize(stream));
-    for (int w = 0; w < B.n_win; ++w) {
+    forWindows(B.n_win, [&](int w) {
       const okvisgpu_problem* p = probs[w];
-      const int x = st.empty() ? 0 : st[w].xcur;
-      std::memcpy(p->poses, &pose[x][7 * (size_t)B.pose_base[w]], sizeof(double) * 7 * p->n_poses);
+      const double* q = pose + 7 * (size_t)B.pose_base[w];
+      std::memcpy(p->poses, q, sizeof(double) * 7 * p->n_poses);
       if (B.win_ext_free[w])  // variable extrinsics are written back like every other block
-        std::memcpy(p->extrinsics, &pose[x][7 * ((size_t)B.pose_base[w] + p->n_poses)], sizeof(double) * 7 * p->n_cameras);
-      std::memcpy(p->speed_biases, &sb[x][9 * (size_t)B.sb_base[w]], sizeof(double) * 9 * p->n_speed_biases);
-      for (int k = 0; k < p->n_landmarks; ++k)
-        std::memcpy(&p->landmarks[4 * (size_t)B.lm_perm[B.lm_base[w] + k]], &lm[x][4 * ((size_t)B.lm_base[w] + k)],
-                    sizeof(double) * 4);
+        std::memcpy(p->extrinsics, q + 7 * (size_t)p->n_poses, sizeof(double) * 7 * p->n_cameras);
+      std::memcpy(p->speed_biases, sb + 9 * (size_t)B.sb_base[w], sizeof(double) * 9 * p->n_speed_biases);
+      const double* l = lm + 4 * (size_t)B.lm_base[w];
+      const int* perm = &B.lm_perm[B.lm_base[w]];
+      for (int k = 0; k < p->n_landmarks; ++k) std::memcpy(&p->landmarks[4 * (size_t)perm[k]], l + 4 * (size_t)k, 32);
       if (p->imu_state && p->n_imu)
-        std::memcpy(p->imu_state, &imu[(size_t)B.imu_base[w] * kImuState],
-                    sizeof(double) * kImuState * p->n_imu);
-    }
+        std::memcpy(p->imu_state, imu + (size_t)B.imu_base[w] * kImuState, sizeof(double) * kImuState * p->n_imu);
+    });
   }
 
   std::vector<WinState> readStates() {
@@ -1542,7 +1590,7 @@ int okvisgpu_get_params(okvisgpu_ctx* c) {
   if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
   return guarded(c, [&]() {
     HIPCHK(hipSetDevice(c->device));
-    c->downloadParams(c->readStates());
+    c->downloadParams();
     return (int)OKVISGPU_OK;
   });
 }
@@ -1614,7 +1662,7 @@ int okvisgpu_solve_end(okvisgpu_ctx* c, okvisgpu_summary* sums) {
       ++c->replays;
       st = c->readStates();
     }
-    c->downloadParams(st);
+    c->downloadParams();
     c->inSolve = false;
     c->fillSummaries(st, sums);
     return (int)OKVISGPU_OK;
@@ -1658,7 +1706,7 @@ int okvisgpu_solve(okvisgpu_ctx* c, const okvisgpu_options* o, okvisgpu_summary*
       ++c->replays;
       st = c->readStates();
     }
-    c->downloadParams(st);
+    c->downloadParams();
     c->inSolve = false;
     c->fillSummaries(st, sums);
     return (int)OKVISGPU_OK;
@@ -1996,7 +2044,7 @@ int okvisgpu_eval_imu(okvisgpu_ctx* c, int32_t window, int32_t redo_always, doub
       if (J) for (int i = 0; i < 450; ++i) J[450 * (size_t)f + i] = lin[(size_t)f * kImuLin + 15 + i];
     }
     // keep the caller's ImuError state in sync (the evaluation may have re-integrated)
-    c->downloadParams(c->readStates());
+    c->downloadParams();
     return (int)OKVISGPU_OK;
   });
 }
