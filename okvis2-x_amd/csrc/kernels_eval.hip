@@ -161,6 +161,7 @@ __device__ void loadPre(const double* s, ImuPre& p) {
 constexpr int kImuGroup = 16;
 constexpr int kImuPerWG = 4;
 constexpr int kStepRec = 32;  // dt | dq (4) | a_true (3) | Jr (9) | R(dq)^T (9) | noise (5) | pad
+constexpr int kImuChunk = 8;  // step records formed per chunk (lanes 0..7), staged in the group's sA
 
 // F_delta (ImuError.cpp:395-410) of one step in LDS: non-identity 3x3 blocks
 constexpr int kF03 = 0, kF09 = 9, kF012 = 18, kF39 = 27, kF63 = 36, kF69 = 45, kF612 = 54, kFdt = 63;
@@ -279,7 +280,7 @@ __device__ void groupJacobi(double* A, double* V, double* rot, int l, bool need)
 }  // namespace
 
 #ifndef OKG_IMU_OCC
-#define OKG_IMU_OCC 1
+#define OKG_IMU_OCC 2
 #endif
 // APPEND: ImuError::append (ImuError.cpp:63-255) for a batch of factors (okvisgpu_imu_append): the
 // chain starts from the stored state (Delta_q, integrals, cross_, dv_db_g, P) at imu_t0 (= the old
@@ -291,14 +292,16 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
   const int f = blockIdx.x * kImuPerWG + g;
 
-  // per-group LDS: sA = symmetric P / Jacobi matrix / U (row-major 16x16), sB = transpose
-  // exchange / L (column-major) / Jacobi eigenvectors, sR = Jacobi rotations, sF = F_delta
-  __shared__ double sAll[kImuPerWG][2 * 256 + 32 + 64];
+  // per-group LDS: sA = step records of a chunk during the chain, then symmetric P / Jacobi
+  // matrix / U (row-major 16x16); sB = transpose exchange / L (column-major) / Jacobi eigenvectors;
+  // sF = F_delta during the chain, then the Jacobi rotations (sR). 18 KB per workgroup, so LDS
+  // admits two workgroups (waves) per SIMD.
+  __shared__ double sAll[kImuPerWG][2 * 256 + 64];
+  static_assert(kImuChunk * kStepRec <= 256, "a chunk's step records must fit the group's sA");
   double* sA = sAll[g];
   double* sB = sAll[g] + 256;
-  double* sR = sAll[g] + 512;
-  double* sF = sAll[g] + 544;
-  __shared__ double sStep[kImuPerWG][kImuGroup * kStepRec];  // per-step records of a chunk
+  double* sF = sAll[g] + 512;
+  double* sR = sF;
 
   int w = 0, xs = 0, lb = 0;
   bool live = f < P.n_imu;
@@ -379,15 +382,15 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
     bool started = false;                       // hasStarted: an earlier step was integrated
     double C[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};  // R(cdq), carried from step to step
     if (APPEND) qrot(cdq, C);
-    double* rec = sStep[g];
-    for (int c0 = 0; c0 < Nmax; c0 += kImuGroup) {
+    double* rec = sA;
+    for (int c0 = 0; c0 < Nmax; c0 += kImuChunk) {
       {
         const int it = c0 + l;
         bool ok = false;
         double dt = 0.0, om0[3] = {0, 0, 0}, ac0[3] = {0, 0, 0}, om1[3] = {0, 0, 0}, ac1[3] = {0, 0, 0};
         int64_t nexttime = 0;
         int s0 = sbeg;
-        if (it < N) {
+        if (l < kImuChunk && it < N) {
           s0 = sbeg + it;
           const int s1 = (it + 1 < N) ? s0 + 1 : s0;
           for (int k = 0; k < 3; ++k) {
@@ -421,8 +424,8 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
         }
         started = started || gm != 0;
         steps += __popc(gm);
-        double* R = rec + l * kStepRec;
-        R[0] = ok ? dt : 0.0;
+        double* R = rec + min(l, kImuChunk - 1) * kStepRec;
+        if (l < kImuChunk) R[0] = ok ? dt : 0.0;
         if (ok) {
           double gyr_sat = 1.0, acc_sat = 1.0;
           for (int k = 0; k < 3; ++k) {
@@ -456,7 +459,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
         }
       }
       __syncthreads();
-      const int nk = min(kImuGroup, Nmax - c0);
+      const int nk = min(kImuChunk, Nmax - c0);
       for (int k = 0; k < nk; ++k) {
         const double* R = rec + k * kStepRec;
         const double dt = R[0];
