@@ -130,6 +130,7 @@ struct DevProblem {
   double* lm_Linv;                 // [n_lm][9]  L^-1, L L^T = s V s + D^2 (lower triangular)
   double* lm_zz;                   // [n_lm][3]  L^-1 (s g)
   const int32_t* lmg_begin;        // [n_lmg+1] landmark groups of k_lm_visit (<= kLmGroupVisits visits each)
+  const int32_t* lmg_info;         // [n_lmg+1][4] {first landmark, first visit, window, first segment}
   int32_t n_lmg;
   // visit segments: the visits of one free pose inside one landmark group, pre-summed in k_lm_visit
   int32_t n_seg;

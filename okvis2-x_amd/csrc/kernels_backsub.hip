@@ -48,13 +48,15 @@ template <bool EXT>
 __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int t = threadIdx.x;
-  const int l0 = P.lmg_begin[blockIdx.x], l1 = P.lmg_begin[blockIdx.x + 1];
-  const int w = P.lm_win[l0];  // a group never spans windows
+  const int4* gi = reinterpret_cast<const int4*>(P.lmg_info) + blockIdx.x;
+  const int4 gi0 = gi[0], gi1 = gi[1];
+  const int l0 = gi0.x, l1 = gi1.x;
+  const int w = gi0.z;  // a group never spans windows
   const WinState& st = P.st[w];
   if (st.done || !st.need_gn || st.gn_failed) return;  // uniform
   __shared__ double sQ[3][kLmGroupVisits];
   __shared__ double sC[6][kLmGroupMax];  // per landmark: s v_c (3) | -s y_l (3)
-  const int v0 = P.lm_visit_begin[l0], v1 = P.lm_visit_begin[l1];
+  const int v0 = gi0.y, v1 = gi1.y;
   const int v = v0 + t;
   const bool hasV = v < v1;
   const int l = hasV ? P.visit_lm[v] : l0;

@@ -37,6 +37,21 @@ __device__ __forceinline__ int sym3(int a, int b) {
   return a * 3 - (a * (a - 1)) / 2 + (b - a);
 }
 
+// sum of x[m0..m1) as four interleaved partial sums (four LDS loads in flight, a quarter of the
+// dependent adds), combined in a fixed order
+__device__ __forceinline__ double rangeSum(const double* x, int m0, int m1) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int m = m0;
+  for (; m + 4 <= m1; m += 4) {
+    a0 += x[m];
+    a1 += x[m + 1];
+    a2 += x[m + 2];
+    a3 += x[m + 3];
+  }
+  for (; m < m1; ++m) a0 += x[m];
+  return (a0 + a1) + (a2 + a3);
+}
+
 __device__ __forceinline__ bool linSelect(const DevProblem& P, int w, int lin_mode) {
   const WinState& s = P.st[w];
   if (s.done) return false;
@@ -72,6 +87,34 @@ __device__ __forceinline__ bool lmVisitSelect(const DevProblem& P, int w, int mo
 #ifndef OKG_LMV_OCC
 #define OKG_LMV_OCC 3
 #endif
+// Development-only phase clock of k_lm_visit<1> (make OPT="-O3 -DOKG_LMV_CLOCK"): thread 0 of every
+// workgroup adds its s_memrealtime ticks (100 MHz) per phase with vector atomics; the last workgroup
+// prints the totals.
+#ifdef OKG_LMV_CLOCK
+__device__ unsigned long long g_lmvClk[8];
+__device__ unsigned int g_lmvDone;
+#define LCLK_INIT unsigned long long lclk = __builtin_amdgcn_s_memrealtime();
+#define LCLK(i)                                                                         \
+  if (mode == 1 && threadIdx.x == 0) {                                                  \
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();                    \
+    atomicAdd(&g_lmvClk[i], now - lclk);                                                \
+    lclk = now;                                                                         \
+  }
+#define LCLK_END                                                                        \
+  if (mode == 1 && threadIdx.x == 0) {                                                  \
+    __threadfence();                                                                    \
+    if (atomicAdd(&g_lmvDone, 1u) == gridDim.x - 1) {                                   \
+      printf("LMVCLK visit %llu lm %llu seg %llu z %llu stage %llu part %llu (x10ns, summed)\n", \
+             g_lmvClk[0], g_lmvClk[1], g_lmvClk[2], g_lmvClk[3], g_lmvClk[4], g_lmvClk[5]);       \
+      for (int i = 0; i < 8; ++i) g_lmvClk[i] = 0;                                      \
+      g_lmvDone = 0;                                                                    \
+    }                                                                                   \
+  }
+#else
+#define LCLK_INIT
+#define LCLK(i)
+#define LCLK_END
+#endif
 // (mode is a template parameter: each mode is its own specialised kernel, and rocprof reports them
 // apart — k_lm_visit<1> is the per-iteration linearisation, k_lm_visit<2> the GN prep)
 // EXT (batches with variable extrinsics): threads nvg.. of a group are its extrinsic visits — per
@@ -82,8 +125,9 @@ template <int mode, bool EXT>
 __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int t = threadIdx.x;
-  const int l0 = P.lmg_begin[blockIdx.x], l1 = P.lmg_begin[blockIdx.x + 1];
-  const int v0 = P.lm_visit_begin[l0], v1 = P.lm_visit_begin[l1];
+  const int4* gi = reinterpret_cast<const int4*>(P.lmg_info) + blockIdx.x;
+  const int4 gi0 = gi[0], gi1 = gi[1];
+  const int l0 = gi0.x, l1 = gi1.x, v0 = gi0.y, v1 = gi1.y;
   // sBuf rows 0..8: visit shares of V (6) | g_l (3); rows 9..17: visit values being summed into
   // segments; finally rows 0..17: the visits' Z for the partial Schur blocks
   __shared__ double sBuf[18][kLmGroupVisits];
@@ -91,8 +135,13 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   __shared__ int sPC[kLmPartStage];          // the group's landmark-pair products (a | b << 16)
   double (*sVg)[kLmGroupVisits] = sBuf;
   double (*sR)[kLmGroupVisits] = sBuf + 9;
-  const int w = P.lm_win[l0];                // a group never spans windows
+  const int w = gi0.z;                       // a group never spans windows
+#ifdef OKG_LMV_CLOCK
+  if (!lmVisitSelect(P, w, mode)) { LCLK_END return; }
+#else
   if (!lmVisitSelect(P, w, mode)) return;    // uniform
+#endif
+  LCLK_INIT
   const int v = v0 + t;
   const bool hasV = v < v1;
   const int nvg = v1 - v0;
@@ -103,6 +152,9 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   const bool lfree = P.lm_free[l] != 0;
   const int pose = hasV ? P.visit_pose[v] : (hasX ? P.xvisit_pose[xv] : 0);
   const int pf = P.pose_f[pose];
+  // segment bookkeeping, loaded up front (consumed after the landmark phase)
+  const int sg0 = gi0.w, nseg = gi1.w - sg0;
+  const int slot = hasV ? P.visit_slot[v] : (hasX ? P.xvisit_slot[xv] : -1);
   double W[18], H[21], gp[6], Vv[6], gl[3];
 #pragma unroll
   for (int i = 0; i < 18; ++i) W[i] = 0.0;
@@ -185,6 +237,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
 #pragma unroll
   for (int i = 0; i < 3; ++i) sVg[6 + i][t] = gl[i];
   ldsBarrier();
+  LCLK(0)
   // ---- one thread per landmark of the group
   if (t < l1 - l0) {
     const int L = l0 + t;
@@ -280,31 +333,30 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
     }
   }
   ldsBarrier();
-  // ---- segments: H | g of each (group, free pose) summed over its visits in visit order
-  // (visits are scattered to their slots so that every segment is a contiguous LDS range)
-  const int sg0 = P.seg_gbegin[blockIdx.x], nseg = P.seg_gbegin[blockIdx.x + 1] - sg0;
-  const int slot = hasV ? P.visit_slot[v] : (hasX ? P.xvisit_slot[xv] : -1);
+  LCLK(1)
+  // ---- segments: H | g of each (group, free pose) summed over its visits (visits are scattered
+  // to their slots so that every segment is a contiguous LDS range). The visit shares of V / g_l
+  // are consumed, so all 18 rows of sBuf take values: H[0..17], then H[18..20] | g_p.
   if (mode != 2) {
 #pragma unroll
-    for (int chunk = 0; chunk < 3; ++chunk) {
-      const int nval = 9;
+    for (int chunk = 0; chunk < 2; ++chunk) {
+      const int nval = chunk == 0 ? 18 : 9;
       if (slot >= 0)
 #pragma unroll
-        for (int i = 0; i < 9; ++i) {
-          const int e = 9 * chunk + i;
-          sR[i][slot] = e < 21 ? H[e] : gp[e - 21];
+        for (int i = 0; i < nval; ++i) {
+          const int e = 18 * chunk + i;
+          sBuf[i][slot] = e < 21 ? H[e] : gp[e - 21];
         }
       ldsBarrier();
       for (int e = t; e < nseg * nval; e += kLmGroupVisits) {
         const int sgi = e / nval, i = e - sgi * nval;
         const int m0 = P.seg_range[2 * (sg0 + sgi)], m1 = P.seg_range[2 * (sg0 + sgi) + 1];
-        double a = 0.0;
-        for (int m = m0; m < m1; ++m) a += sR[i][m];
-        P.seg_hg[(size_t)(sg0 + sgi) * kSegHG + 9 * chunk + i] = a;
+        P.seg_hg[(size_t)(sg0 + sgi) * kSegHG + 18 * chunk + i] = rangeSum(sBuf[i], m0, m1);
       }
       ldsBarrier();
     }
   }
+  LCLK(2)
   if (mode == 0) return;
   // ---- visit: Z = s_p W s_l L^-T (6x3) | U z = Z zz (6, summed into the segments)
   double o[kVisitZ + 6];
@@ -341,9 +393,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   for (int e = t; e < nseg * 6; e += kLmGroupVisits) {
     const int sgi = e / 6, i = e - sgi * 6;
     const int m0 = P.seg_range[2 * (sg0 + sgi)], m1 = P.seg_range[2 * (sg0 + sgi) + 1];
-    double a = 0.0;
-    for (int m = m0; m < m1; ++m) a += sR[i][m];
-    P.seg_uz[(size_t)(sg0 + sgi) * kSegUz + i] = a;
+    P.seg_uz[(size_t)(sg0 + sgi) * kSegUz + i] = rangeSum(sR[i], m0, m1);
   }
   // ---- partial Schur blocks: for each pose pair of the group, rows 2h, 2h+1 of sum Z_a Z_b^T over
   // the group's landmark-pair products (fixed order), from Z staged visit-major in LDS (144-byte
@@ -352,6 +402,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   const int pc0 = P.part_cbegin[pg0], npc = P.part_cbegin[pg0 + npart] - pc0;
   double* sZ = &sBuf[0][0];
   ldsBarrier();  // sR reads above are done
+  LCLK(3)
   {
     double2* zo = reinterpret_cast<double2*>(sZ + kVisitZ * t);
 #pragma unroll
@@ -362,6 +413,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   if (staged)
     for (int c = t; c < npc; c += kLmGroupVisits) sPC[c] = P.part_contrib[pc0 + c];
   ldsBarrier();
+  LCLK(4)
   const auto gPC = gmem(P.part_contrib + pc0);
   for (int e = t; e < npart * 3; e += kLmGroupVisits) {
     const int pi = e / 3, h = e - pi * 3;
@@ -388,6 +440,11 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
 #pragma unroll
     for (int q = 0; q < 6; ++q) out[q] = double2{acc[2 * q], acc[2 * q + 1]};
   }
+#ifdef OKG_LMV_CLOCK
+  __syncthreads();
+  LCLK(5)
+  LCLK_END
+#endif
 }
 
 // Pose-extrinsics cross blocks of F^T F (variable extrinsics only): per (free state pose, variable

@@ -104,6 +104,7 @@ struct HostBatch {
   std::vector<double> obs_kp, obs_L;
   // visits
   std::vector<int32_t> lm_visit_begin, visit_pose, visit_obs_begin, visit_lm, lmg_begin;
+  std::vector<int32_t> lmg_info;  // [n_lmg+1][4]: first landmark, first visit, window, first segment
   // visit segments: per landmark group, the visits of one free pose (k_lm_visit pre-sums them)
   std::vector<int32_t> seg_gbegin, seg_pose, seg_range, visit_slot;
   // partial Schur blocks: per landmark group and pose pair, sum of Z_a Z_b^T over the group's landmarks
@@ -886,6 +887,17 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
         B.win_lmg_range[2 * w + 1] = last[w] + 1;
       }
   }
+  {  // per-group record read with one 16-byte load (the terminal entry closes the last group)
+    const int ng = (int)B.lmg_begin.size() - 1;
+    B.lmg_info.resize(4 * (size_t)(ng + 1));
+    for (int g = 0; g <= ng; ++g) {
+      const int l0 = B.lmg_begin[g];
+      B.lmg_info[4 * (size_t)g + 0] = l0;
+      B.lmg_info[4 * (size_t)g + 1] = B.lm_visit_begin[l0];
+      B.lmg_info[4 * (size_t)g + 2] = g < ng ? B.lm_win[l0] : -1;
+      B.lmg_info[4 * (size_t)g + 3] = B.seg_gbegin[g];
+    }
+  }
   B.lmg_xbegin.push_back((int)B.xvisit_pose.size());
   B.xvisit_obs_begin.push_back((int)B.xvisit_obs.size());
   B.pe_obs_begin.push_back((int)B.pe_obs.size());
@@ -1037,7 +1049,7 @@ struct okvisgpu_ctx {
     const size_t o_obs_cost0 = scratch(sizeof(double) * D.n_obs), o_obs_cost1 = scratch(sizeof(double) * D.n_obs);
     const size_t o_grp_red = scratch(sizeof(double) * kGrpRed * std::max<size_t>(1, B.lmg_begin.size()));
     const size_t o_lmvb = upl(B.lm_visit_begin), o_vpose = upl(B.visit_pose), o_vob = upl(B.visit_obs_begin),
-                 o_vlm = upl(B.visit_lm), o_lmg_b = upl(B.lmg_begin);
+                 o_vlm = upl(B.visit_lm), o_lmg_b = upl(B.lmg_begin), o_lmg_info = upl(B.lmg_info);
     const size_t o_lmV = scratch(sizeof(double) * 6 * D.n_lm), o_lmg = scratch(sizeof(double) * 3 * D.n_lm),
                  o_lmVi = scratch(sizeof(double) * 9 * D.n_lm), o_lmz = scratch(sizeof(double) * 3 * D.n_lm);
     D.n_seg = (int)B.seg_pose.size();
@@ -1159,6 +1171,7 @@ struct okvisgpu_ctx {
     D.xvisit_pose = ip(o_xvp); D.xvisit_lm = ip(o_xvl); D.xvisit_obs_begin = ip(o_xvob); D.xvisit_obs = ip(o_xvo);
     D.xvisit_slot = ip(o_xvs); D.lmg_xbegin = ip(o_lmgx);
     D.pe_pose = ip(o_pep); D.pe_ext = ip(o_pee); D.pe_obs_begin = ip(o_peob); D.pe_obs = ip(o_peo); D.pe_H = dp(o_peH);
+    D.lmg_info = ip(o_lmg_info);
     D.lmg_begin = ip(o_lmg_b); D.n_lmg = B.lmg_begin.empty() ? 0 : (int)B.lmg_begin.size() - 1;
     D.imu_blocks = ip(o_imu_blocks); D.imu_win = ip(o_imu_win); D.imu_flags = up(o_imu_flags);
     D.imu_t0 = lp(o_imu_t0); D.imu_t1 = lp(o_imu_t1); D.imu_sbegin = ip(o_imu_sb); D.imu_ts = lp(o_imu_ts);
