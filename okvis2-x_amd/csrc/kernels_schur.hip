@@ -125,7 +125,7 @@ template <int mode, bool EXT>
 __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int t = threadIdx.x;
-  const int4* gi = reinterpret_cast<const int4*>(P.lmg_info) + blockIdx.x;
+  const auto gi = gmem(reinterpret_cast<const int4*>(P.lmg_info) + blockIdx.x);
   const int4 gi0 = gi[0], gi1 = gi[1];
   const int l0 = gi0.x, l1 = gi1.x, v0 = gi0.y, v1 = gi1.y;
   // sBuf rows 0..8: visit shares of V (6) | g_l (3); rows 9..17: visit values being summed into
@@ -136,25 +136,39 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   double (*sVg)[kLmGroupVisits] = sBuf;
   double (*sR)[kLmGroupVisits] = sBuf + 9;
   const int w = gi0.z;                       // a group never spans windows
-#ifdef OKG_LMV_CLOCK
-  if (!lmVisitSelect(P, w, mode)) { LCLK_END return; }
-#else
-  if (!lmVisitSelect(P, w, mode)) return;    // uniform
-#endif
-  LCLK_INIT
   const int v = v0 + t;
   const bool hasV = v < v1;
+  // the visit record (index clamped, loaded unconditionally): issued before the window test so
+  // that its latency overlaps the WinState load
+  const int vc = hasV ? v : v0;
+  const int vLm = gmem(P.visit_lm)[vc], vPose = gmem(P.visit_pose)[vc], vSlot = gmem(P.visit_slot)[vc];
+  const int obBeg = gmem(P.visit_obs_begin)[vc], obEnd = gmem(P.visit_obs_begin)[vc + 1];
+  // window test (lmVisitSelect) from one set of WinState loads, no short-circuit branches
+  const auto gst = gmem(P.st + w);
+  const int sDone = gst->done, sAcc = gst->accepted, sNeed = gst->need_gn, sFail = gst->gn_failed;
+  const int sLcur = gst->lcur, sXcur = gst->xcur;
+  const double sZmu = gst->z_mu, sMu = gst->mu;
+  const bool selW = mode == 0 ? !sDone : mode == 1 ? (!sDone & (sAcc != 0)) : (!sDone & (sNeed != 0) & !sFail & (sZmu != sMu));
+  // (the visit record is folded into the test, so the compiler issues its loads before the branch
+  // instead of after it: vc >> 31 is 0, so the second term is always false)
+  const bool skip = !selW | (((vLm ^ vPose ^ vSlot ^ obBeg ^ obEnd) & (vc >> 31)) != 0);
+#ifdef OKG_LMV_CLOCK
+  if (skip) { LCLK_END return; }
+#else
+  if (skip) return;    // uniform
+#endif
+  LCLK_INIT
   const int nvg = v1 - v0;
   const int xv = EXT ? P.lmg_xbegin[blockIdx.x] + t - nvg : 0;
   const bool hasX = EXT && t >= nvg && xv < P.lmg_xbegin[blockIdx.x + 1];
-  const int l = hasV ? P.visit_lm[v] : (hasX ? P.xvisit_lm[xv] : l0);
+  const int l = hasV ? vLm : (hasX ? P.xvisit_lm[xv] : l0);
   const bool sel = hasV;
-  const bool lfree = P.lm_free[l] != 0;
-  const int pose = hasV ? P.visit_pose[v] : (hasX ? P.xvisit_pose[xv] : 0);
-  const int pf = P.pose_f[pose];
-  // segment bookkeeping, loaded up front (consumed after the landmark phase)
+  const bool lfree = gmem(P.lm_free)[l] != 0;
+  const int pose = hasV ? vPose : (hasX ? P.xvisit_pose[xv] : 0);
+  const int pf = gmem(P.pose_f)[pose];
+  // segment bookkeeping (consumed after the landmark phase)
   const int sg0 = gi0.w, nseg = gi1.w - sg0;
-  const int slot = hasV ? P.visit_slot[v] : (hasX ? P.xvisit_slot[xv] : -1);
+  const int slot = hasV ? vSlot : (hasX ? P.xvisit_slot[xv] : -1);
   double W[18], H[21], gp[6], Vv[6], gl[3];
 #pragma unroll
   for (int i = 0; i < 18; ++i) W[i] = 0.0;
@@ -164,22 +178,38 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   for (int i = 0; i < 6; ++i) { gp[i] = 0.0; Vv[i] = 0.0; }
 #pragma unroll
   for (int i = 0; i < 3; ++i) gl[i] = 0.0;
-  if (sel) {
-    const WinState& st = P.st[w];
-    const auto lin = gmem(P.obs_lin[st.lcur]);
+  {
+    // (buffer pointers picked by select, not by indexing P's arrays with a loaded value: that would
+    // be one more dependent load)
+    const auto lin = gmem(sLcur ? P.obs_lin[1] : P.obs_lin[0]);
     const int64_t S = P.obs_stride;
     // linearisation point of lin[lcur]: params X[xcur]
-    const double* hp = P.lm[st.xcur] + 4 * (size_t)l;
-    const double* tw = P.pose[st.xcur] + 7 * (size_t)pose;
-    const double w4 = hp[3];
-    const double p3[3] = {hp[0] - tw[0] * w4, hp[1] - tw[1] * w4, hp[2] - tw[2] * w4};
-    for (int ob = P.visit_obs_begin[v]; ob < P.visit_obs_begin[v + 1]; ++ob) {
-      if (P.obs_flags[ob] & 2) continue;
-      double r[2], A[6], Jp[12], Jl[6];
-      r[0] = lin[0 * S + ob];
-      r[1] = lin[1 * S + ob];
+    const auto hp = gmem((sXcur ? P.lm[1] : P.lm[0]) + 4 * (size_t)l);
+    const auto tw = gmem((sXcur ? P.pose[1] : P.pose[0]) + 7 * (size_t)pose);
+    // first observation's flag and linearisation with the parameters, unconditionally (a clamped
+    // visit still has one); a masked observation contributes exact zeros (selects, no branch, so
+    // the loads are not sunk behind one)
+    double r0[2], A0[6];
+    const int fl0 = gmem(P.obs_flags)[obBeg];
+    r0[0] = lin[0 * S + obBeg];
+    r0[1] = lin[1 * S + obBeg];
 #pragma unroll
-      for (int k = 0; k < 6; ++k) A[k] = lin[(2 + k) * S + ob];
+    for (int k = 0; k < 6; ++k) A0[k] = lin[(2 + k) * S + obBeg];
+    const double hp4[4] = {hp[0], hp[1], hp[2], hp[3]}, tw3[3] = {tw[0], tw[1], tw[2]};
+    // all of the above are in flight together: the empty asm consumes them here, so none is sunk
+    // behind a branch on another's value
+    asm volatile("" ::"v"(r0[0]), "v"(r0[1]), "v"(A0[0]), "v"(A0[1]), "v"(A0[2]), "v"(A0[3]), "v"(A0[4]),
+                 "v"(A0[5]), "v"(hp4[0]), "v"(hp4[1]), "v"(hp4[2]), "v"(hp4[3]), "v"(tw3[0]), "v"(tw3[1]),
+                 "v"(tw3[2]), "v"(fl0));
+    const bool use0 = sel & !(fl0 & 2);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) r0[k] = use0 ? r0[k] : 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) A0[k] = use0 ? A0[k] : 0.0;
+    const double w4 = hp4[3];
+    const double p3[3] = {hp4[0] - tw3[0] * w4, hp4[1] - tw3[1] * w4, hp4[2] - tw3[2] * w4};
+    auto accumulate = [&](const double* r, const double* A) {
+      double Jp[12], Jl[6];
       obsJacobians(A, p3, w4, Jp, Jl);
       if (lfree) {
 #pragma unroll
@@ -200,6 +230,20 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
             for (int b2 = 0; b2 < 3; ++b2) W[a2 * 3 + b2] += Jp[a2] * Jl[b2] + Jp[6 + a2] * Jl[3 + b2];
         }
       }
+    };
+    accumulate(r0, A0);
+    for (int ob = obBeg + 1; sel && ob < obEnd; ++ob) {
+      double r[2], A[6];
+      const bool use = !(gmem(P.obs_flags)[ob] & 2);
+      r[0] = lin[0 * S + ob];
+      r[1] = lin[1 * S + ob];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) A[k] = lin[(2 + k) * S + ob];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) r[k] = use ? r[k] : 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) A[k] = use ? A[k] : 0.0;
+      accumulate(r, A);
     }
   }
   if (EXT && hasX) {  // extrinsic visit: H_ee, g_e, W_e over the landmark's observations via the camera
