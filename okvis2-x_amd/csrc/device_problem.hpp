@@ -30,6 +30,7 @@ constexpr int kSegUz = 8;    // per visit segment: sum U z (6) | pad
 constexpr int kLmGroupVisits = 256;  // k_lm_visit: visits of one landmark group (one workgroup)
 constexpr int kLmGroupMax = 64;      // landmarks per group
 constexpr int kLmPartStage = 2048;   // landmark-pair products per group (staged in LDS)
+constexpr int kLmgInfo = 8;          // ints per landmark-group record (lmg_info)
 constexpr int kImuHess = 465 + 30;  // packed upper J^T J (30x30) | J^T r
 constexpr int kGrpRed = 8;    // per landmark group: jcc | jgg | jcg | gg | nn | gn | pad
 constexpr int kVisitZ = 18;   // per visit: Z = s_p W s_l L^-T (6x3), k_lm_visit LDS only
@@ -130,7 +131,8 @@ struct DevProblem {
   double* lm_Linv;                 // [n_lm][9]  L^-1, L L^T = s V s + D^2 (lower triangular)
   double* lm_zz;                   // [n_lm][3]  L^-1 (s g)
   const int32_t* lmg_begin;        // [n_lmg+1] landmark groups of k_lm_visit (<= kLmGroupVisits visits each)
-  const int32_t* lmg_info;         // [n_lmg+1][4] {first landmark, first visit, window, first segment}
+  const int32_t* lmg_info;         // [n_lmg+1][kLmgInfo] {first landmark, first visit, window, first segment,
+                                   //  first partial block, first landmark-pair product, 0, 0}
   int32_t n_lmg;
   // visit segments: the visits of one free pose inside one landmark group, pre-summed in k_lm_visit
   int32_t n_seg;

@@ -48,8 +48,8 @@ template <bool EXT>
 __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int t = threadIdx.x;
-  const auto gi = gmem(reinterpret_cast<const int4*>(P.lmg_info) + blockIdx.x);
-  const int4 gi0 = gi[0], gi1 = gi[1];
+  const auto gi = gmem(reinterpret_cast<const int4*>(P.lmg_info + kLmgInfo * blockIdx.x));
+  const int4 gi0 = gi[0], gi1 = gi[kLmgInfo / 4];
   const int l0 = gi0.x, l1 = gi1.x;
   const int w = gi0.z;  // a group never spans windows
   const WinState& st = P.st[w];

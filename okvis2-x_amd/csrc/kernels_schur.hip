@@ -125,8 +125,8 @@ template <int mode, bool EXT>
 __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int t = threadIdx.x;
-  const auto gi = gmem(reinterpret_cast<const int4*>(P.lmg_info) + blockIdx.x);
-  const int4 gi0 = gi[0], gi1 = gi[1];
+  const auto gi = gmem(reinterpret_cast<const int4*>(P.lmg_info + kLmgInfo * blockIdx.x));
+  const int4 gi0 = gi[0], gi1 = gi[kLmgInfo / 4];
   const int l0 = gi0.x, l1 = gi1.x, v0 = gi0.y, v1 = gi1.y;
   // sBuf rows 0..8: visit shares of V (6) | g_l (3); rows 9..17: visit values being summed into
   // segments; finally rows 0..17: the visits' Z for the partial Schur blocks
@@ -158,6 +158,18 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   if (skip) return;    // uniform
 #endif
   LCLK_INIT
+  // the group's landmark-pair products go to LDS by DMA now (no registers held; they land with the
+  // visit loads below and are read in the last phase)
+  const int4 gp0 = gi[1], gp1 = gi[kLmgInfo / 4 + 1];
+  const int pg0 = gp0.x, npart = gp1.x - pg0, pc0 = gp0.y, npc = gp1.y - pc0;
+  const bool staged = npc <= kLmPartStage;
+  if (mode != 0 && staged && npc > 0) {
+    const int wv = t >> 6;
+    for (int c = 0; c < npc; c += kLmGroupVisits)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(P.part_contrib + pc0 + min(c + t, npc - 1)),
+          (__attribute__((address_space(3))) void*)(sPC + c + 64 * wv), 4, 0, 0);
+  }
   const int nvg = v1 - v0;
   const int xv = EXT ? P.lmg_xbegin[blockIdx.x] + t - nvg : 0;
   const bool hasX = EXT && t >= nvg && xv < P.lmg_xbegin[blockIdx.x + 1];
@@ -282,14 +294,37 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   for (int i = 0; i < 3; ++i) sVg[6 + i][t] = gl[i];
   ldsBarrier();
   LCLK(0)
+  // Operands of the later phases, issued now so that they land during the landmark phase: this
+  // thread's first segment ranges in the three segment passes (18, 9 and 6 values per segment) and
+  // the pose scaling of its visit (a valid dummy address when the pose is not free).
+  const auto gsr = gmem(reinterpret_cast<const int2*>(P.seg_range));
+  const int sgl = max(nseg - 1, 0);
+  const int2 rA = gsr[sg0 + min(t / 18, sgl)], rB = gsr[sg0 + min(t / 9, sgl)], rC = gsr[sg0 + min(t / 6, sgl)];
+  double spr[6];
+  {
+    const auto spp = gmem(pf >= 0 ? P.sF + (size_t)P.win_foff[w] + pf : P.pose[0]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) spr[i] = mode != 0 ? spp[i] : 0.0;
+  }
   // ---- one thread per landmark of the group
   if (t < l1 - l0) {
     const int L = l0 + t;
-    const int wL = P.lm_win[L];
-    WinState& st = P.st[wL];
-    if (lmVisitSelect(P, wL, mode)) {
-      if (mode == 1 && L == P.win_lm_range[2 * wL]) st.z_mu = st.mu;  // one writer per window
-      if (P.lm_free[L]) {
+    // (the window is w and already selected) the landmark's flag, visit range and scaling are
+    // loaded together and consumed at one point
+    const int lfreeL = gmem(P.lm_free)[L];
+    const int ub = gmem(P.lm_visit_begin)[L] - v0, ue = gmem(P.lm_visit_begin)[L + 1] - v0;
+    double s[3] = {1.0, 1.0, 1.0};
+    if (mode != 0) {
+      const auto sLp = gmem(P.sL + 3 * (size_t)L);
+      s[0] = sLp[0];
+      s[1] = sLp[1];
+      s[2] = sLp[2];
+    }
+    asm volatile("" ::"v"(lfreeL), "v"(ub), "v"(ue), "v"(s[0]), "v"(s[1]), "v"(s[2]));
+    WinState& st = P.st[w];
+    {
+      if (mode == 1 && L == P.win_lm_range[2 * w]) st.z_mu = sMu;  // one writer per window
+      if (lfreeL) {
         double V[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
         if (mode == 2) {
 #pragma unroll
@@ -297,7 +332,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
 #pragma unroll
           for (int i = 0; i < 3; ++i) g[i] = P.lm_g[3 * (size_t)L + i];
         } else {
-          for (int u = P.lm_visit_begin[L] - v0; u < P.lm_visit_begin[L + 1] - v0; ++u) {
+          for (int u = ub; u < ue; ++u) {
 #pragma unroll
             for (int i = 0; i < 6; ++i) V[i] += sVg[i][u];
 #pragma unroll
@@ -312,8 +347,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
               P.sL[3 * (size_t)L + a] = P.opt.jacobi_scaling ? 1.0 / (1.0 + sqrt(V[sym3(a, a)])) : 1.0;
         }
         if (mode != 0) {
-          const double* s = P.sL + 3 * (size_t)L;
-          const double mu = st.mu;
+          const double mu = sMu;
           double A[9];
           for (int a = 0; a < 3; ++a)
             for (int b = 0; b < 3; ++b) A[a * 3 + b] = s[a] * s[b] * V[sym3(a, b)];
@@ -378,6 +412,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   }
   ldsBarrier();
   LCLK(1)
+  asm volatile("" ::"v"(rA.x), "v"(rA.y), "v"(rB.x), "v"(rB.y), "v"(rC.x), "v"(rC.y));  // (not sunk into branches)
   // ---- segments: H | g of each (group, free pose) summed over its visits (visits are scattered
   // to their slots so that every segment is a contiguous LDS range). The visit shares of V / g_l
   // are consumed, so all 18 rows of sBuf take values: H[0..17], then H[18..20] | g_p.
@@ -392,7 +427,12 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
           sBuf[i][slot] = e < 21 ? H[e] : gp[e - 21];
         }
       ldsBarrier();
-      for (int e = t; e < nseg * nval; e += kLmGroupVisits) {
+      if (t < nseg * nval) {  // first pass: the prefetched range
+        const int sgi = t / nval, i = t - sgi * nval;
+        const int2 r = chunk == 0 ? rA : rB;
+        P.seg_hg[(size_t)(sg0 + sgi) * kSegHG + 18 * chunk + i] = rangeSum(sBuf[i], r.x, r.y);
+      }
+      for (int e = t + kLmGroupVisits; e < nseg * nval; e += kLmGroupVisits) {
         const int sgi = e / nval, i = e - sgi * nval;
         const int m0 = P.seg_range[2 * (sg0 + sgi)], m1 = P.seg_range[2 * (sg0 + sgi) + 1];
         P.seg_hg[(size_t)(sg0 + sgi) * kSegHG + 18 * chunk + i] = rangeSum(sBuf[i], m0, m1);
@@ -402,13 +442,14 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   }
   LCLK(2)
   if (mode == 0) return;
+  asm volatile("" ::"v"(spr[0]), "v"(spr[1]), "v"(spr[2]), "v"(spr[3]), "v"(spr[4]), "v"(spr[5]));
   // ---- visit: Z = s_p W s_l L^-T (6x3) | U z = Z zz (6, summed into the segments)
   double o[kVisitZ + 6];
 #pragma unroll
   for (int i = 0; i < kVisitZ + 6; ++i) o[i] = 0.0;
   if (pf >= 0 && lfree) {
     const int u = l - l0;
-    double Li[9], zz[3], s3[3], spr[6];
+    double Li[9], zz[3], s3[3];
 #pragma unroll
     for (int i = 0; i < 9; ++i) Li[i] = sLz[i][u];
 #pragma unroll
@@ -416,9 +457,6 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
       zz[i] = sLz[9 + i][u];
       s3[i] = sLz[12 + i][u];
     }
-    const auto sp = gmem(P.sF + (size_t)P.win_foff[w] + pf);
-#pragma unroll
-    for (int i = 0; i < 6; ++i) spr[i] = sp[i];
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
       const double u0 = spr[r] * W[r * 3 + 0] * s3[0], u1 = spr[r] * W[r * 3 + 1] * s3[1],
@@ -434,7 +472,11 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
 #pragma unroll
     for (int i = 0; i < 6; ++i) sR[i][slot] = o[kVisitZ + i];
   ldsBarrier();
-  for (int e = t; e < nseg * 6; e += kLmGroupVisits) {
+  if (t < nseg * 6) {  // first pass: the prefetched range
+    const int sgi = t / 6, i = t - sgi * 6;
+    P.seg_uz[(size_t)(sg0 + sgi) * kSegUz + i] = rangeSum(sR[i], rC.x, rC.y);
+  }
+  for (int e = t + kLmGroupVisits; e < nseg * 6; e += kLmGroupVisits) {
     const int sgi = e / 6, i = e - sgi * 6;
     const int m0 = P.seg_range[2 * (sg0 + sgi)], m1 = P.seg_range[2 * (sg0 + sgi) + 1];
     P.seg_uz[(size_t)(sg0 + sgi) * kSegUz + i] = rangeSum(sR[i], m0, m1);
@@ -442,8 +484,6 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   // ---- partial Schur blocks: for each pose pair of the group, rows 2h, 2h+1 of sum Z_a Z_b^T over
   // the group's landmark-pair products (fixed order), from Z staged visit-major in LDS (144-byte
   // records read with 16-byte LDS loads)
-  const int pg0 = P.part_gbegin[blockIdx.x], npart = P.part_gbegin[blockIdx.x + 1] - pg0;
-  const int pc0 = P.part_cbegin[pg0], npc = P.part_cbegin[pg0 + npart] - pc0;
   double* sZ = &sBuf[0][0];
   ldsBarrier();  // sR reads above are done
   LCLK(3)
@@ -453,9 +493,6 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
     for (int i = 0; i < kVisitZ / 2; ++i) zo[i] = double2{o[2 * i], o[2 * i + 1]};
   }
   // (a group of one landmark with more products than the stage holds streams them from HBM)
-  const bool staged = npc <= kLmPartStage;
-  if (staged)
-    for (int c = t; c < npc; c += kLmGroupVisits) sPC[c] = P.part_contrib[pc0 + c];
   ldsBarrier();
   LCLK(4)
   const auto gPC = gmem(P.part_contrib + pc0);
@@ -465,6 +502,7 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
     double acc[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) acc[i] = 0.0;
+#pragma unroll 2
     for (int c = c0; c < c1; ++c) {
       const int ab = staged ? sPC[c] : gPC[c], a = ab & 0xffff, b = ab >> 16;
       const double2* za2 = reinterpret_cast<const double2*>(sZ + kVisitZ * a + 6 * h);

@@ -104,7 +104,8 @@ struct HostBatch {
   std::vector<double> obs_kp, obs_L;
   // visits
   std::vector<int32_t> lm_visit_begin, visit_pose, visit_obs_begin, visit_lm, lmg_begin;
-  std::vector<int32_t> lmg_info;  // [n_lmg+1][4]: first landmark, first visit, window, first segment
+  std::vector<int32_t> lmg_info;  // [n_lmg+1][kLmgInfo]: first landmark, first visit, window, first segment,
+                                  // first partial block, first landmark-pair product
   // visit segments: per landmark group, the visits of one free pose (k_lm_visit pre-sums them)
   std::vector<int32_t> seg_gbegin, seg_pose, seg_range, visit_slot;
   // partial Schur blocks: per landmark group and pose pair, sum of Z_a Z_b^T over the group's landmarks
@@ -887,17 +888,6 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
         B.win_lmg_range[2 * w + 1] = last[w] + 1;
       }
   }
-  {  // per-group record read with one 16-byte load (the terminal entry closes the last group)
-    const int ng = (int)B.lmg_begin.size() - 1;
-    B.lmg_info.resize(4 * (size_t)(ng + 1));
-    for (int g = 0; g <= ng; ++g) {
-      const int l0 = B.lmg_begin[g];
-      B.lmg_info[4 * (size_t)g + 0] = l0;
-      B.lmg_info[4 * (size_t)g + 1] = B.lm_visit_begin[l0];
-      B.lmg_info[4 * (size_t)g + 2] = g < ng ? B.lm_win[l0] : -1;
-      B.lmg_info[4 * (size_t)g + 3] = B.seg_gbegin[g];
-    }
-  }
   B.lmg_xbegin.push_back((int)B.xvisit_pose.size());
   B.xvisit_obs_begin.push_back((int)B.xvisit_obs.size());
   B.pe_obs_begin.push_back((int)B.pe_obs.size());
@@ -906,6 +896,20 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
   B.imu_sbegin.push_back((int)B.imu_ts.size());
   B.fb_cbegin.push_back((int)B.fb_contrib.size());
   B.pair_cbegin.push_back((int)B.pair_contrib.size());
+  {  // per-group record (two 16-byte loads; the terminal entry closes the last group)
+    const int ng = (int)B.lmg_begin.size() - 1;
+    B.lmg_info.assign(kLmgInfo * (size_t)(ng + 1), 0);
+    for (int g = 0; g <= ng; ++g) {
+      const int l0 = B.lmg_begin[g];
+      int32_t* r = &B.lmg_info[kLmgInfo * (size_t)g];
+      r[0] = l0;
+      r[1] = B.lm_visit_begin[l0];
+      r[2] = g < ng ? B.lm_win[l0] : -1;
+      r[3] = B.seg_gbegin[g];
+      r[4] = B.part_gbegin[g];
+      r[5] = B.part_cbegin[B.part_gbegin[g]];
+    }
+  }
   ATIME(10)
 }
 
