@@ -52,39 +52,63 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
   const int4 gi0 = gi[0], gi1 = gi[kLmgInfo / 4];
   const int l0 = gi0.x, l1 = gi1.x;
   const int w = gi0.z;  // a group never spans windows
-  const WinState& st = P.st[w];
-  if (st.done || !st.need_gn || st.gn_failed) return;  // uniform
-  __shared__ double sQ[3][kLmGroupVisits];
-  __shared__ double sC[6][kLmGroupMax];  // per landmark: s v_c (3) | -s y_l (3)
   const int v0 = gi0.y, v1 = gi1.y;
   const int v = v0 + t;
   const bool hasV = v < v1;
-  const int l = hasV ? P.visit_lm[v] : l0;
-  const int pose = hasV ? P.visit_pose[v] : 0;
-  const int pf = hasV ? P.pose_f[pose] : -1;
-  const bool lfree = P.lm_free[l] != 0;
-  double cp[6], gp[6];
+  // The visit record (index clamped, loaded unconditionally) and the WinState fields are loaded
+  // together; the window test needs no short-circuit branch and consumes the visit record (vc >> 31
+  // is 0), so the compiler cannot sink those loads behind it (as in k_lm_visit).
+  const int vc = hasV ? v : v0;
+  const int vLm = gmem(P.visit_lm)[vc], vPose = gmem(P.visit_pose)[vc];
+  const int obB = gmem(P.visit_obs_begin)[vc], obE = gmem(P.visit_obs_begin)[vc + 1];
+  const auto gst = gmem(P.st + w);
+  const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed, sLcur = gst->lcur, sXcur = gst->xcur;
+  const bool skip = (sDone != 0) | (sNeed == 0) | (sFail != 0) | (((vLm ^ vPose ^ obB ^ obE) & (vc >> 31)) != 0);
+  if (skip) return;  // uniform
+  __shared__ double sQ[3][kLmGroupVisits];
+  __shared__ double sC[6][kLmGroupMax];  // per landmark: s v_c (3) | -s y_l (3)
+  const int l = hasV ? vLm : l0;
+  const int pose = hasV ? vPose : 0;
+  const int ob0 = hasV ? obB : 0, ob1 = hasV ? obE : 0;
+  // the landmark flag, the pose's f offset, the parameters and the first observation together
+  const auto lin = gmem(sLcur ? P.obs_lin[1] : P.obs_lin[0]);
+  const int64_t S = P.obs_stride;
+  const int lfreeI = gmem(P.lm_free)[l], pfI = gmem(P.pose_f)[pose];
+  const auto hpp = gmem((sXcur ? P.lm[1] : P.lm[0]) + 4 * (size_t)l);
+  const auto twp = gmem((sXcur ? P.pose[1] : P.pose[0]) + 7 * (size_t)pose);
+  const double hp[4] = {hpp[0], hpp[1], hpp[2], hpp[3]};
+  double tw[7];
 #pragma unroll
-  for (int c = 0; c < 6; ++c) {
-    cp[c] = 0.0;
-    gp[c] = 0.0;
-  }
-  if (pf >= 0) {
-    const size_t b = (size_t)P.win_foff[w] + pf;
+  for (int k = 0; k < 7; ++k) tw[k] = (EXT || k < 3) ? twp[k] : 0.0;
+  const int fl0 = gmem(P.obs_flags)[obB];
+  double A0[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) A0[k] = lin[(2 + k) * S + obB];
+  asm volatile("" ::"v"(lfreeI), "v"(pfI), "v"(hp[0]), "v"(hp[1]), "v"(hp[2]), "v"(hp[3]), "v"(tw[0]), "v"(tw[1]),
+               "v"(tw[2]), "v"(fl0), "v"(A0[0]), "v"(A0[1]), "v"(A0[2]), "v"(A0[3]), "v"(A0[4]), "v"(A0[5]));
+  const int xs = sXcur;
+  const int pf = hasV ? pfI : -1;
+  const bool lfree = lfreeI != 0;
+  // the pose's scaled step and gradient (a valid dummy address when the pose is not free)
+  double cp[6], gp[6];
+  {
+    const size_t b = pf >= 0 ? (size_t)P.win_foff[w] + pf : 0;
+    const auto sFp = gmem(P.sF + b), vFp = gmem(P.vF + b), yFp = gmem(P.yF + b);
+    double sc[6], vv[6], yy[6];
 #pragma unroll
     for (int c = 0; c < 6; ++c) {
-      const double sc = P.sF[b + c];
-      cp[c] = sc * P.vF[b + c];
-      gp[c] = -sc * P.yF[b + c];
+      sc[c] = sFp[c];
+      vv[c] = vFp[c];
+      yy[c] = yFp[c];
+    }
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      cp[c] = pf >= 0 ? sc[c] * vv[c] : 0.0;
+      gp[c] = pf >= 0 ? -sc[c] * yy[c] : 0.0;
     }
   }
-  const auto lin = gmem(P.obs_lin[st.lcur]);
-  const int64_t S = P.obs_stride;
-  const double* hp = P.lm[st.xcur] + 4 * (size_t)l;
-  const double* tw = P.pose[st.xcur] + 7 * (size_t)pose;
   const double w4 = hp[3];
   const double p3[3] = {hp[0] - tw[0] * w4, hp[1] - tw[1] * w4, hp[2] - tw[2] * w4};
-  const int ob0 = hasV ? P.visit_obs_begin[v] : 0, ob1 = hasV ? P.visit_obs_begin[v + 1] : 0;
   double C_WS[9];
   if (EXT) qrot(qnormalize(Q{tw[3], tw[4], tw[5], tw[6]}), C_WS);
 
@@ -92,13 +116,22 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
   double q[3] = {0.0, 0.0, 0.0};
   if ((pf >= 0 || EXT) && lfree)
     for (int o = ob0; o < ob1; ++o) {
-      if (P.obs_flags[o] & 2) continue;
+      // (a masked observation contributes exact zeros: selects, so no load sits behind a branch)
       double A[6], Jp[12], Jl[6];
+      int fl = fl0;
 #pragma unroll
-      for (int k = 0; k < 6; ++k) A[k] = lin[(2 + k) * S + o];
+      for (int k = 0; k < 6; ++k) A[k] = A0[k];
+      if (o != ob0) {
+        fl = gmem(P.obs_flags)[o];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) A[k] = lin[(2 + k) * S + o];
+      }
+      const bool use = !(fl & 2);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) A[k] = use ? A[k] : 0.0;
       obsJacobians(A, p3, w4, Jp, Jl);
       ExtTerm X;
-      const bool hasE = EXT && loadExtTerm(P, o, w, st.xcur, C_WS, p3, w4, A, X);
+      const bool hasE = EXT && loadExtTerm(P, o, w, xs, C_WS, p3, w4, A, X);
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
         double jg = 0.0;
@@ -113,40 +146,49 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
     }
 #pragma unroll
   for (int a = 0; a < 3; ++a) sQ[a][t] = q[a];
-  __syncthreads();
+  ldsBarrier();
 
   // ---- landmark: y_l = L^-T (zz - L^-1 s_l sum_v q_v), the dogleg vectors
   double lred[3] = {0.0, 0.0, 0.0};
   if (t < l1 - l0) {
     const int L = l0 + t;
     double c6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    if (P.lm_free[L]) {
+    // every operand of the landmark is loaded up front, together (stores to the output vectors
+    // below would otherwise keep later loads from being hoisted above them)
+    const int lf = gmem(P.lm_free)[L];
+    const int mb = gmem(P.lm_visit_begin)[L] - v0, me = gmem(P.lm_visit_begin)[L + 1] - v0;
+    double li[9], s3[3], zz[3], dgv[3], lg[3];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) li[i] = gmem(P.lm_Linv)[9 * (size_t)L + i];  // lower triangular
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const size_t i = 3 * (size_t)L + a;
+      s3[a] = gmem(P.sL)[i];
+      zz[a] = gmem(P.lm_zz)[i];
+      dgv[a] = gmem(P.diagL)[i];
+      lg[a] = gmem(P.lm_g)[i];
+    }
+    if (lf) {
       double qs[3] = {0.0, 0.0, 0.0};
-      for (int m = P.lm_visit_begin[L] - v0; m < P.lm_visit_begin[L + 1] - v0; ++m)
+      for (int m = mb; m < me; ++m)
 #pragma unroll
         for (int a = 0; a < 3; ++a) qs[a] += sQ[a][m];
-      double li[9], s3[3], u[3];
+      double u[3];
 #pragma unroll
-      for (int i = 0; i < 9; ++i) li[i] = P.lm_Linv[9 * (size_t)L + i];  // lower triangular
+      for (int a = 0; a < 3; ++a) qs[a] *= s3[a];
 #pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        s3[a] = P.sL[3 * (size_t)L + a];
-        qs[a] *= s3[a];
-      }
-#pragma unroll
-      for (int a = 0; a < 3; ++a)
-        u[a] = P.lm_zz[3 * (size_t)L + a] - (li[a * 3] * qs[0] + li[a * 3 + 1] * qs[1] + li[a * 3 + 2] * qs[2]);
+      for (int a = 0; a < 3; ++a) u[a] = zz[a] - (li[a * 3] * qs[0] + li[a * 3 + 1] * qs[1] + li[a * 3 + 2] * qs[2]);
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
         double y = 0.0;
 #pragma unroll
         for (int c = a; c < 3; ++c) y += li[c * 3 + a] * u[c];
         const size_t i = 3 * (size_t)L + a;
-        const double dg = P.diagL[i];
+        const double dg = dgv[a];
         P.yL[i] = y;
         const double gn = -dg * y;
         P.gnL[i] = gn;
-        const double gr = s3[a] * P.lm_g[i] / dg;
+        const double gr = s3[a] * lg[a] / dg;
         const double vc = gr / dg;
         P.dgL[i] = gr;
         P.vL[i] = vc;
@@ -162,7 +204,7 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
 #pragma unroll
     for (int i = 0; i < 6; ++i) sC[i][t] = c6[i];
   }
-  __syncthreads();
+  ldsBarrier();
 
   // ---- visit: J_s v_c and J_s v_g of its residuals (fixed residuals excluded)
   const int u = hasV ? l - l0 : 0;
@@ -174,13 +216,15 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
   }
   double acc[3] = {0.0, 0.0, 0.0};
   for (int o = ob0; o < ob1; ++o) {
-    if (P.obs_flags[o] & 2) continue;
     double A[6], Jp[12], Jl[6];
+    const bool use = !(gmem(P.obs_flags)[o] & 2);
 #pragma unroll
     for (int k = 0; k < 6; ++k) A[k] = lin[(2 + k) * S + o];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) A[k] = use ? A[k] : 0.0;
     obsJacobians(A, p3, w4, Jp, Jl);
     ExtTerm X;
-    const bool hasE = EXT && loadExtTerm(P, o, w, st.xcur, C_WS, p3, w4, A, X);
+    const bool hasE = EXT && loadExtTerm(P, o, w, xs, C_WS, p3, w4, A, X);
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       double jc = 0.0, jg = 0.0;
@@ -215,7 +259,7 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
   if ((t & 63) == 0)
 #pragma unroll
     for (int k = 0; k < 6; ++k) sW[t >> 6][k] = red[k];
-  __syncthreads();
+  ldsBarrier();
   if (t < 6) {
     double a = sW[0][t];
 #pragma unroll
