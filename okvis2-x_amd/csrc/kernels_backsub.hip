@@ -71,11 +71,11 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
   const int pose = hasV ? vPose : 0;
   const int ob0 = hasV ? obB : 0, ob1 = hasV ? obE : 0;
   // the landmark flag, the pose's f offset, the parameters and the first observation together
-  const auto lin = gmem(sLcur ? P.obs_lin[1] : P.obs_lin[0]);
+  const auto lin = gmem(pick2(sLcur, P.obs_lin[0], P.obs_lin[1]));
   const int64_t S = P.obs_stride;
   const int lfreeI = gmem(P.lm_free)[l], pfI = gmem(P.pose_f)[pose];
-  const auto hpp = gmem((sXcur ? P.lm[1] : P.lm[0]) + 4 * (size_t)l);
-  const auto twp = gmem((sXcur ? P.pose[1] : P.pose[0]) + 7 * (size_t)pose);
+  const auto hpp = gmem(pick2(sXcur, P.lm[0], P.lm[1]) + 4 * (size_t)l);
+  const auto twp = gmem(pick2(sXcur, P.pose[0], P.pose[1]) + 7 * (size_t)pose);
   const double hp[4] = {hpp[0], hpp[1], hpp[2], hpp[3]};
   double tw[7];
 #pragma unroll

@@ -45,18 +45,38 @@ __global__ __launch_bounds__(256) void k_eval_obs(const DevProblem* __restrict__
   const DevProblem& P = *Pp;
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= P.n_obs) return;
-  const int w = P.obs_win[o];
-  int xs, lb;
-  if (!evalSelect(P, w, mode, xs, lb)) return;
-  uint8_t flags = P.obs_flags[o];
-  if ((flags & 2) && mode < 2) return;  // fixed residual: only evaluated once (fixed_cost)
-  if (mode == 3) flags &= ~1;           // raw functor output (parity hook): no loss
+  // The observation's record (indices, flags, keypoint, information) is loaded together with no
+  // branch in between; the window test (evalSelect) reads the WinState fields at once and consumes
+  // the record (o >> 31 is 0), so none of these loads is sunk behind it.
+  const int w = gmem(P.obs_win)[o], op = gmem(P.obs_pose)[o], ol = gmem(P.obs_lm)[o], ci = gmem(P.obs_cam)[o];
+  uint8_t flags = gmem(P.obs_flags)[o];
+  const auto Lp = gmem(P.obs_L + 4 * (size_t)o);
+  const auto mp = gmem(P.obs_kp + 2 * (size_t)o);
+  const double L[4] = {Lp[0], Lp[1], Lp[2], Lp[3]}, m[2] = {mp[0], mp[1]};
+  const auto gst = gmem(P.st + w);
+  const int sDone = gst->done, sCand = gst->eval_cand, sX = gst->xcur, sL = gst->lcur;
+  const bool sel = (sDone == 0) & (mode != 1 || sCand != 0) & !((flags & 2) && mode < 2);
+  const int cpose = gmem(P.cam_pose)[ci];
+  const auto cp = gmem(P.cam + kCamDoubles * ci);
+  const Cam cam = Cam{(int)cp[0], cp[1], cp[2], cp[3], cp[4], cp[5], cp[6], cp[7], cp[8], cp[9], cp[10], cp[11], cp[12]};
+  asm volatile("" ::"v"(L[0]), "v"(L[1]), "v"(L[2]), "v"(L[3]), "v"(m[0]), "v"(m[1]), "v"(sX), "v"(sL), "v"(cam.fu),
+               "v"(cam.fv), "v"(cam.cu), "v"(cam.cv));
+  if (!sel | (((op ^ ol ^ ci ^ (int)flags ^ cpose ^ cam.dist) & (o >> 31)) != 0)) return;  // (fixed: fixed_cost only)
+  const int xs = mode == 1 ? 1 - sX : sX, lb = mode == 1 ? 1 - sL : sL;
+  if (mode == 3) flags &= ~1;  // raw functor output (parity hook): no loss
 
-  const double* pose = P.pose[xs] + 7 * (size_t)P.obs_pose[o];
-  const double* hp = P.lm[xs] + 4 * (size_t)P.obs_lm[o];
-  const int ci = P.obs_cam[o];
-  const double* ex = P.pose[xs] + 7 * (size_t)P.cam_pose[ci];  // T_SC: a pose-kind block (variable or not)
-  const Cam cam = loadCam(P.cam + kCamDoubles * ci);
+  const double* X = pick2(xs, P.pose[0], P.pose[1]);
+  const auto posep = gmem(X + 7 * (size_t)op);
+  const auto hpp = gmem(pick2(xs, P.lm[0], P.lm[1]) + 4 * (size_t)ol);
+  const auto exp_ = gmem(X + 7 * (size_t)cpose);  // T_SC: a pose-kind block (variable or not)
+  double pose[7], hp[4], ex[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    pose[k] = posep[k];
+    ex[k] = exp_[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) hp[k] = hpp[k];
 
   double C_WS[9], C_SC[9];
   qrot(qnormalize(Q{pose[3], pose[4], pose[5], pose[6]}), C_WS);
@@ -72,8 +92,6 @@ __global__ __launch_bounds__(256) void k_eval_obs(const DevProblem* __restrict__
 
   double kp[2], Jh[6];
   projectHomogeneous(cam, hC[0], hC[1], hC[2], w4, kp, Jh, true);
-  const double* L = P.obs_L + 4 * (size_t)o;
-  const double* m = P.obs_kp + 2 * (size_t)o;
   const double e0 = m[0] - kp[0], e1 = m[1] - kp[1];
   double r0 = L[0] * e0 + L[1] * e1;
   double r1 = L[2] * e0 + L[3] * e1;
@@ -109,13 +127,13 @@ __global__ __launch_bounds__(256) void k_eval_obs(const DevProblem* __restrict__
   }
   // stored: r and A (both Cauchy-scaled); the pose/landmark Jacobians follow from A and the
   // linearisation point (obsJacobians)
-  double* lin = P.obs_lin[lb];
+  double* lin = pick2(lb, P.obs_lin[0], P.obs_lin[1]);
   const int64_t S = P.obs_stride;
   lin[0 * S + o] = r0 * sc;
   lin[1 * S + o] = r1 * sc;
 #pragma unroll
   for (int k = 0; k < 6; ++k) lin[(2 + k) * S + o] = A[k] * sc;
-  P.obs_cost[lb][o] = cost;
+  pick2(lb, P.obs_cost[0], P.obs_cost[1])[o] = cost;
 }
 
 // ------------------------------------------------------------------------------------ IMU

@@ -193,11 +193,11 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   {
     // (buffer pointers picked by select, not by indexing P's arrays with a loaded value: that would
     // be one more dependent load)
-    const auto lin = gmem(sLcur ? P.obs_lin[1] : P.obs_lin[0]);
+    const auto lin = gmem(pick2(sLcur, P.obs_lin[0], P.obs_lin[1]));
     const int64_t S = P.obs_stride;
     // linearisation point of lin[lcur]: params X[xcur]
-    const auto hp = gmem((sXcur ? P.lm[1] : P.lm[0]) + 4 * (size_t)l);
-    const auto tw = gmem((sXcur ? P.pose[1] : P.pose[0]) + 7 * (size_t)pose);
+    const auto hp = gmem(pick2(sXcur, P.lm[0], P.lm[1]) + 4 * (size_t)l);
+    const auto tw = gmem(pick2(sXcur, P.pose[0], P.pose[1]) + 7 * (size_t)pose);
     // first observation's flag and linearisation with the parameters, unconditionally (a clamped
     // visit still has one); a masked observation contributes exact zeros (selects, no branch, so
     // the loads are not sunk behind one)

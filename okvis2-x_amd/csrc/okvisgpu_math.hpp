@@ -40,6 +40,18 @@ __device__ __forceinline__ gwptr<T> gmemw(T* p) {
   return (gwptr<T>)p;
 }
 
+// One of two buffer pointers (parameter set / linearisation buffer xcur, lcur) picked by a loaded
+// flag. The pointers are made opaque first: otherwise the select of P.x[0] / P.x[1] is folded into
+// an indexed load P.x[flag], one more dependent load before the data.
+template <typename T>
+__device__ __forceinline__ T* pick2(int flag, T* p0, T* p1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+s"(p0));
+  asm("" : "+s"(p1));
+#endif
+  return flag ? p1 : p0;
+}
+
 // Workgroup barrier that orders LDS only: __syncthreads() also waits for every outstanding global
 // load (vmcnt(0)), which defeats loads prefetched across the barrier.
 __device__ __forceinline__ void ldsBarrier() {
