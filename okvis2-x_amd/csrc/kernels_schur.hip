@@ -616,16 +616,22 @@ __global__ __launch_bounds__(64) void k_fgrad(const DevProblem* __restrict__ Pp,
   const DevProblem& P = *Pp;
   const int fb = blockIdx.x;
   if (fb >= P.n_fblock) return;
-  const int w = P.fb_win[fb];
-  if (!linSelect(P, w, lin_mode)) return;
   const int lane = threadIdx.x;
-  const int lb = P.st[w].lcur;
-  const int n = P.fb_kind[fb] == 0 ? 6 : 9;
+  // the f-block record, then the window state with this lane's first contribution, consumed (empty
+  // asm) before the window test so that no load is sunk behind it
+  const int w = gmem(P.fb_win)[fb], kind = gmem(P.fb_kind)[fb];
+  const int c0 = gmem(P.fb_cbegin)[fb], c1 = gmem(P.fb_cbegin)[fb + 1];
+  const auto gst = gmem(P.st + w);
+  const int sDone = gst->done, sAcc = gst->accepted, lb = gst->lcur;
+  const Contrib cFirst = gmem(P.fb_contrib)[min(c0 + lane, max(c1 - 1, c0))];
+  asm volatile("" ::"v"(cFirst.type), "v"(cFirst.a), "v"(cFirst.b), "v"(lb));
+  if ((sDone != 0) | (lin_mode == 1 && sAcc == 0)) return;  // linSelect
+  const int n = kind == 0 ? 6 : 9;
   double g[9], hd[9];
 #pragma unroll
   for (int c = 0; c < 9; ++c) { g[c] = 0.0; hd[c] = 0.0; }
-  for (int k = P.fb_cbegin[fb] + lane; k < P.fb_cbegin[fb + 1]; k += 64) {
-    const Contrib cb = P.fb_contrib[k];
+  for (int k = c0 + lane; k < c1; k += 64) {
+    const Contrib cb = k == c0 + lane ? cFirst : P.fb_contrib[k];
     if (cb.type == C_VISIT) {
       const double* H = P.seg_hg + (size_t)cb.a * kSegHG;
       const double* gp = H + 21;
@@ -727,14 +733,27 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (item >= P.n_asm_pp) return;
-  const int k = P.asm_pp_items[item];
+  const int k = gmem(P.asm_pp_items)[item];
   if (k < 0) return;
-  const int w = P.pair_win[k];
-  if (!gnSelect(P, w)) return;
+  // the pair record in one round of loads; then the window state, the first round of descriptors
+  // and the block offsets in the next, all consumed (empty asm) before the window test, so no load
+  // is sunk behind it
+  const int w = gmem(P.pair_win)[k];
+  const int cb = gmem(P.pair_cbegin)[k], ce = gmem(P.pair_cbegin)[k + 1];
+  const int2 runs = gmem(reinterpret_cast<const int2*>(P.pair_runs))[k];
+  const int pb = runs.x, ob = runs.y;
+  const int fi = gmem(P.pair_fi)[k], fj = gmem(P.pair_fj)[k];
+  const auto pc = gmem(P.pair_contrib);
+  const auto gst = gmem(P.st + w);
+  const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed, lb = gst->lcur;
+  const double sMu = gst->mu;
+  const int myc0 = min(cb + lane, max(pb - 1, cb));
+  const int da0 = pc[myc0].a, db0 = pc[myc0].b;
+  const int foff = gmem(P.win_foff)[w], offi = gmem(P.fb_off)[fi], offj = gmem(P.fb_off)[fj];
+  asm volatile("" ::"v"(da0), "v"(db0), "v"(foff), "v"(offi), "v"(offj), "v"(cb), "v"(ce), "v"(lb), "v"(sMu));
+  if ((sDone != 0) | (sNeed == 0) | (sFail != 0)) return;
   const int g = lane / 6, r = lane - 6 * (lane / 6);
   const bool inGroup = g < kGroups;
-  const int cb = P.pair_cbegin[k], pb = P.pair_runs[2 * k], ob = P.pair_runs[2 * k + 1], ce = P.pair_cbegin[k + 1];
-  const auto pc = gmem(P.pair_contrib);
   const auto vhg = gmem(P.seg_hg);
   const auto suz = gmem(P.seg_uz);
   double H[6], Sc[6], uz = 0.0;
@@ -746,7 +765,7 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
   // visits (diagonal pairs): row r of H_v, and (U_v z_l)_r
   for (int base = cb; base < pb; base += 64) {
     const int myc = min(base + lane, pb - 1);
-    const int da = pc[myc].a, db = pc[myc].b;
+    const int da = base == cb ? da0 : pc[myc].a, db = base == cb ? db0 : pc[myc].b;
     const int nstep = min(64, pb - base);
     for (int st = 0; st < nstep; st += kGroups) {
       const int k0 = st + g;
@@ -774,7 +793,6 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
     }
   }
   // factor blocks (IMU, relative pose, pose prior): row r of J_i^T J_j
-  const int lb = P.st[w].lcur;
   for (int c = ob + g0; c < ce; c += kGroups) {
     const Contrib C = pc[c];
     if (C.type == C_IMU) {
@@ -813,9 +831,6 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
     uz += __shfl(uz, src, 64);
   }
   if (lane >= 6) return;
-  const int fi = P.pair_fi[k], fj = P.pair_fj[k];
-  const int foff = P.win_foff[w];
-  const int offi = P.fb_off[fi], offj = P.fb_off[fj];
   const bool diag = fi == fj;
   const double si = P.sF[(size_t)foff + offi + r];
   double* Srow = P.S + P.win_soff[w] + (int64_t)(offi + r) * P.win_fpad[w] + offj;
@@ -827,7 +842,7 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
       const size_t idx = (size_t)foff + offi + r;
       const double dg = sqrt(fmin(fmax(si * si * P.hdF[idx], P.opt.min_lm_diagonal), P.opt.max_lm_diagonal));
       P.diagF[idx] = dg;
-      const double d = dg * sqrt(P.st[w].mu);
+      const double d = dg * sqrt(sMu);
       val += d * d;
     }
     Srow[q] = val;
@@ -846,19 +861,25 @@ __global__ __launch_bounds__(256) void k_assemble_sb(const DevProblem* __restric
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (item >= P.n_asm_sb) return;
-  const int k = P.asm_sb_items[item];
-  const int w = P.pair_win[k];
-  if (!gnSelect(P, w)) return;
-  const int lb = P.st[w].lcur;
-  const int fi = P.pair_fi[k], fj = P.pair_fj[k];
-  const int ni = P.fb_kind[fi] == 0 ? 6 : 9, nj = P.fb_kind[fj] == 0 ? 6 : 9;
-  const int foff = P.win_foff[w];
-  const int offi = P.fb_off[fi], offj = P.fb_off[fj];
+  const int k = gmem(P.asm_sb_items)[item];
+  // the pair record, then the window state and the block offsets, consumed (empty asm) before the
+  // window test so that no load is sunk behind it
+  const int w = gmem(P.pair_win)[k], fi = gmem(P.pair_fi)[k], fj = gmem(P.pair_fj)[k];
+  const int cb = gmem(P.pair_cbegin)[k], ce = gmem(P.pair_cbegin)[k + 1];
+  const auto gst = gmem(P.st + w);
+  const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed, lb = gst->lcur;
+  const double sMu = gst->mu;
+  const int ki = gmem(P.fb_kind)[fi], kj = gmem(P.fb_kind)[fj];
+  const int offi = gmem(P.fb_off)[fi], offj = gmem(P.fb_off)[fj];
+  const int foff = gmem(P.win_foff)[w], ld = gmem(P.win_fpad)[w];
+  const int64_t soff = gmem(P.win_soff)[w];
+  asm volatile("" ::"v"(ki), "v"(kj), "v"(offi), "v"(offj), "v"(foff), "v"(ld), "v"(soff), "v"(cb), "v"(ce),
+               "v"(lb), "v"(sMu));
+  if ((sDone != 0) | (sNeed == 0) | (sFail != 0)) return;  // gnSelect
+  const int ni = ki == 0 ? 6 : 9, nj = kj == 0 ? 6 : 9;
   const bool diag = fi == fj;
-  const int cb = P.pair_cbegin[k], ce = P.pair_cbegin[k + 1];
-  double* S = P.S + P.win_soff[w];
-  const int ld = P.win_fpad[w];
-  const double smu = sqrt(P.st[w].mu);
+  double* S = P.S + soff;
+  const double smu = sqrt(sMu);
   for (int e = lane; e < ni * nj; e += 64) {
     const int r = e / nj, q = e - r * nj;
     double H = 0.0;
