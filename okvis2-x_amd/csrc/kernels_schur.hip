@@ -610,13 +610,15 @@ __global__ __launch_bounds__(256) void k_imu_hess(const DevProblem* __restrict__
   }
 }
 
-// One wavefront per f-block: lanes stride over the contribution list, then a fixed xor-tree
-// reduction (deterministic).
-__global__ __launch_bounds__(64) void k_fgrad(const DevProblem* __restrict__ Pp, int lin_mode) {
+// A 16-lane group per f-block (16 per 256-thread workgroup; a pose has ~10 contributions): lanes
+// stride over the contribution list, then a fixed xor-tree reduction over the group (deterministic).
+constexpr int kFgLanes = 16;
+__global__ __launch_bounds__(256) void k_fgrad(const DevProblem* __restrict__ Pp, int lin_mode) {
   const DevProblem& P = *Pp;
-  const int fb = blockIdx.x;
-  if (fb >= P.n_fblock) return;
-  const int lane = threadIdx.x;
+  const int fbRaw = blockIdx.x * (256 / kFgLanes) + (threadIdx.x / kFgLanes);
+  const int lane = threadIdx.x & (kFgLanes - 1);
+  const bool inRange = fbRaw < P.n_fblock;
+  const int fb = inRange ? fbRaw : 0;
   // the f-block record, then the window state with this lane's first contribution, consumed (empty
   // asm) before the window test so that no load is sunk behind it
   const int w = gmem(P.fb_win)[fb], kind = gmem(P.fb_kind)[fb];
@@ -625,12 +627,15 @@ __global__ __launch_bounds__(64) void k_fgrad(const DevProblem* __restrict__ Pp,
   const int sDone = gst->done, sAcc = gst->accepted, lb = gst->lcur;
   const Contrib cFirst = gmem(P.fb_contrib)[min(c0 + lane, max(c1 - 1, c0))];
   asm volatile("" ::"v"(cFirst.type), "v"(cFirst.a), "v"(cFirst.b), "v"(lb));
-  if ((sDone != 0) | (lin_mode == 1 && sAcc == 0)) return;  // linSelect
+  // (groups of other f-blocks share the wavefront: a group that is not selected contributes nothing
+  // and stores nothing, but takes part in the shuffles)
+  const bool live = inRange & (sDone == 0) & !(lin_mode == 1 && sAcc == 0);  // linSelect
+  if (!__any(live)) return;
   const int n = kind == 0 ? 6 : 9;
   double g[9], hd[9];
 #pragma unroll
   for (int c = 0; c < 9; ++c) { g[c] = 0.0; hd[c] = 0.0; }
-  for (int k = c0 + lane; k < c1; k += 64) {
+  for (int k = c0 + lane; live && k < c1; k += kFgLanes) {
     const Contrib cb = k == c0 + lane ? cFirst : P.fb_contrib[k];
     if (cb.type == C_VISIT) {
       const double* H = P.seg_hg + (size_t)cb.a * kSegHG;
@@ -684,11 +689,11 @@ __global__ __launch_bounds__(64) void k_fgrad(const DevProblem* __restrict__ Pp,
 #pragma unroll
   for (int c = 0; c < 9; ++c)
 #pragma unroll
-    for (int sh = 32; sh > 0; sh >>= 1) {
+    for (int sh = kFgLanes / 2; sh > 0; sh >>= 1) {
       g[c] += __shfl_xor(g[c], sh, 64);
       hd[c] += __shfl_xor(hd[c], sh, 64);
     }
-  if (lane != 0) return;
+  if (lane != 0 || !live) return;
   const size_t base = (size_t)P.win_foff[w] + P.fb_off[fb];
   for (int c = 0; c < n; ++c) {
     P.gF[base + c] = g[c];
@@ -962,7 +967,9 @@ void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
   if (P.n_pe > 0) hipLaunchKernelGGL(k_pose_extr, dim3((P.n_pe + 255) / 256), dim3(256), 0, s, P.self, lin_mode);
 }
 void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s) {
-  if (P.n_fblock > 0) hipLaunchKernelGGL(k_fgrad, dim3(P.n_fblock), dim3(64), 0, s, P.self, lin_mode);
+  if (P.n_fblock > 0)
+    hipLaunchKernelGGL(k_fgrad, dim3((P.n_fblock + 256 / kFgLanes - 1) / (256 / kFgLanes)), dim3(256), 0, s, P.self,
+                       lin_mode);
 }
 void launch_imu_hess(const DevProblem& P, int lin_mode, hipStream_t s) {
   if (P.n_imu > 0) hipLaunchKernelGGL(k_imu_hess, dim3((P.n_imu + 3) / 4), dim3(256), 0, s, P.self, lin_mode);
