@@ -30,6 +30,9 @@ constexpr int kSegUz = 8;    // per visit segment: sum U z (6) | pad
 constexpr int kLmGroupVisits = 256;  // k_lm_visit: visits of one landmark group (one workgroup)
 constexpr int kLmGroupMax = 64;      // landmarks per group
 constexpr int kLmPartStage = 2048;   // landmark-pair products per group (staged in LDS)
+constexpr int kAsmLightMax = 24;     // contributions of a pose-pose pair assembled by a 16-lane quarter
+constexpr int kManyWindows = 64;     // batches from this size use the fewer-workgroup layouts (light
+                                     // pairs, several S tiles per workgroup); below it latency rules
 constexpr int kLmgInfo = 8;          // ints per landmark-group record (lmg_info)
 constexpr int kImuHess = 465 + 30;  // packed upper J^T J (30x30) | J^T r
 constexpr int kGrpRed = 8;    // per landmark group: jcc | jgg | jcg | gg | nn | gn | pad
@@ -233,6 +236,8 @@ struct DevProblem {
   const int32_t* asm_pp_items;      // pose-pose pairs, one per wavefront, XCD-grouped order (-1 = pad)
   const int32_t* asm_sb_items;      // pairs with a speed/bias block, one per wavefront
   int32_t n_asm_pp, n_asm_sb;
+  const int32_t* asm_ppl_items;     // light pose-pose pairs (off-diagonal, few contributions): 16 lanes each
+  int32_t n_asm_ppl;
   const int32_t* pair_win;         // [n_pair]
   const int32_t* pair_fi;          // global f-block index (row, fi >= fj)
   const int32_t* pair_fj;

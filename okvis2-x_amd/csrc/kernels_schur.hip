@@ -138,17 +138,19 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   const int w = gi0.z;                       // a group never spans windows
   const int v = v0 + t;
   const bool hasV = v < v1;
-  // the visit record (index clamped, loaded unconditionally): issued before the window test so
-  // that its latency overlaps the WinState load
-  const int vc = hasV ? v : v0;
-  const int vLm = gmem(P.visit_lm)[vc], vPose = gmem(P.visit_pose)[vc], vSlot = gmem(P.visit_slot)[vc];
-  const int obBeg = gmem(P.visit_obs_begin)[vc], obEnd = gmem(P.visit_obs_begin)[vc + 1];
   // window test (lmVisitSelect) from one set of WinState loads, no short-circuit branches
   const auto gst = gmem(P.st + w);
   const int sDone = gst->done, sAcc = gst->accepted, sNeed = gst->need_gn, sFail = gst->gn_failed;
   const int sLcur = gst->lcur, sXcur = gst->xcur;
   const double sZmu = gst->z_mu, sMu = gst->mu;
   const bool selW = mode == 0 ? !sDone : mode == 1 ? (!sDone & (sAcc != 0)) : (!sDone & (sNeed != 0) & !sFail & (sZmu != sMu));
+  // GN prep concerns few windows: test first, so that the other groups exit without loading
+  if (mode == 2 && !selW) return;  // uniform
+  // the visit record (index clamped, loaded unconditionally); in modes 0 / 1 it is issued before
+  // the window test so that its latency overlaps the WinState load
+  const int vc = hasV ? v : v0;
+  const int vLm = gmem(P.visit_lm)[vc], vPose = gmem(P.visit_pose)[vc], vSlot = gmem(P.visit_slot)[vc];
+  const int obBeg = gmem(P.visit_obs_begin)[vc], obEnd = gmem(P.visit_obs_begin)[vc + 1];
   // (the visit record is folded into the test, so the compiler issues its loads before the branch
   // instead of after it: vc >> 31 is 0, so the second term is always false)
   const bool skip = !selW | (((vLm ^ vPose ^ vSlot ^ obBeg ^ obEnd) & (vc >> 31)) != 0);
@@ -707,18 +709,29 @@ __device__ __forceinline__ bool gnSelect(const DevProblem& P, int w) {
   return !s.done && s.need_gn && !s.gn_failed;
 }
 
-// Clears the structurally non-zero tiles of S (one workgroup per tile; padded diagonal = 1). Zero
-// tiles are never written by the factorisation and stay zero from the initial arena clear.
-__global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ Pp) {
+// Clears the structurally non-zero tiles of S (kZeroTiles consecutive tiles per workgroup; padded
+// diagonal = 1). Zero tiles are never written by the factorisation and stay zero from the initial
+// arena clear. Each tile's record and window are loaded before any test, 16-byte stores.
+constexpr int kZeroTiles = 4;  // (one per workgroup below kManyWindows windows: latency)
+__global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ Pp, int per) {
   const DevProblem& P = *Pp;
-  const int item = blockIdx.x;
-  const int w = P.tile_items[3 * item], ti = P.tile_items[3 * item + 1], tj = P.tile_items[3 * item + 2];
-  if (!gnSelect(P, w)) return;
-  const int fpad = P.win_fpad[w], fdim = P.win_fdim[w];
-  double* S = P.S + P.win_soff[w];
-  for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
-    const int r = ti * kTile + (e >> 6), c = tj * kTile + (e & 63);
-    S[(int64_t)r * fpad + c] = (r == c && r >= fdim) ? 1.0 : 0.0;
+  const auto ti3 = gmem(P.tile_items);
+  for (int u = 0; u < per; ++u) {
+    const int item = blockIdx.x * per + u;
+    if (item >= P.n_tiles) return;
+    const int w = ti3[3 * item], ti = ti3[3 * item + 1], tj = ti3[3 * item + 2];
+    const auto gst = gmem(P.st + w);
+    const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed;
+    const int fpad = gmem(P.win_fpad)[w], fdim = gmem(P.win_fdim)[w];
+    const int64_t soff = gmem(P.win_soff)[w];
+    asm volatile("" ::"v"(fpad), "v"(fdim), "v"(soff));
+    if ((sDone != 0) | (sNeed == 0) | (sFail != 0)) continue;  // gnSelect (uniform)
+    double* S = P.S + soff;
+    for (int e = threadIdx.x; e < kTile * kTile / 2; e += 256) {
+      const int r = ti * kTile + (e >> 5), c = tj * kTile + 2 * (e & 31);
+      const double2 v{(r == c && r >= fdim) ? 1.0 : 0.0, (r == c + 1 && r >= fdim) ? 1.0 : 0.0};
+      *gmemw(reinterpret_cast<double2*>(S + (int64_t)r * fpad + c)) = v;
+    }
   }
 }
 
@@ -859,6 +872,89 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
   }
 }
 
+// k_assemble_pp_light: off-diagonal pose-pose pairs with few contributions (no visits; partial
+// blocks, then factor blocks; <= kAsmLightMax). A 16-lane quarter of a wavefront per pair: 2 groups
+// of 6 lanes (one per row) take alternate contributions, one fixed combining step. Same sums as
+// k_assemble_pp with kGroups = 2.
+constexpr int kPplLanes = 16, kPplGroups = 2;
+__global__ __launch_bounds__(256) void k_assemble_pp_light(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
+  const int lane = threadIdx.x & 63, sub = threadIdx.x & (kPplLanes - 1);
+  const int item = (blockIdx.x * 256 + threadIdx.x) / kPplLanes;
+  const int kRaw = item < P.n_asm_ppl ? gmem(P.asm_ppl_items)[item] : -1;
+  const bool has = kRaw >= 0;
+  const int k = has ? kRaw : 0;
+  // the pair record, then the window state and offsets, consumed before any test (no loads sunk)
+  const int w = gmem(P.pair_win)[k];
+  const int ce = gmem(P.pair_cbegin)[k + 1];
+  const int2 runs = gmem(reinterpret_cast<const int2*>(P.pair_runs))[k];
+  const int pb = runs.x, ob = runs.y;
+  const int fi = gmem(P.pair_fi)[k], fj = gmem(P.pair_fj)[k];
+  const auto pc = gmem(P.pair_contrib);
+  const auto gst = gmem(P.st + w);
+  const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed, lb = gst->lcur;
+  const int g = sub / 6, r = sub - 6 * (sub / 6);
+  const int cFirst = min(pb + g, max(ce - 1, pb));
+  const Contrib C0 = pc[cFirst];
+  const int foff = gmem(P.win_foff)[w], offi = gmem(P.fb_off)[fi], offj = gmem(P.fb_off)[fj];
+  asm volatile("" ::"v"(C0.type), "v"(C0.a), "v"(C0.b), "v"(C0.c), "v"(foff), "v"(offi), "v"(offj), "v"(lb));
+  const bool live = has & (sDone == 0) & (sNeed != 0) & (sFail == 0);  // gnSelect
+  if (!__any(live)) return;
+  const int g0 = (live && g < kPplGroups) ? g : 1 << 29;  // lanes 12..15 of a quarter idle
+  double H[6], Sc[6];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) { H[q] = 0.0; Sc[q] = 0.0; }
+  const auto ps = gmem(P.part_S);
+  for (int c = pb + g0; c < ob; c += kPplGroups) {
+    const int a = c == cFirst ? C0.a : pc[c].a;
+    const auto R2 = reinterpret_cast<gptr<double2>>(ps + (size_t)a * 36 + 6 * r);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const double2 v = R2[q];
+      Sc[2 * q] += v.x;
+      Sc[2 * q + 1] += v.y;
+    }
+  }
+  for (int c = ob + g0; c < ce; c += kPplGroups) {
+    const Contrib C = c == cFirst ? C0 : pc[c];
+    if (C.type == C_IMU) {
+      const auto Hf = gmem(P.imu_H + (size_t)C.a * kImuHess);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) H[q] += Hf[sym30(C.b + r, C.c + q)];
+    } else if (C.type == C_RELPOSE) {
+      const double* L = P.rp_lin[lb] + kRelPoseLin * (size_t)C.a + 6;
+      for (int k2 = 0; k2 < 6; ++k2) {
+        const double jr = L[k2 * 12 + C.b + r];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) H[q] += jr * L[k2 * 12 + C.c + q];
+      }
+    } else if (C.type == C_PEXT) {
+      const auto Hx = gmem(P.pe_H + 36 * (size_t)C.a + 6 * r);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) H[q] += Hx[q];
+    } else {  // C_PPRIOR
+      const double* L = P.pp_lin[lb] + 42 * (size_t)C.a + 6;
+      for (int k2 = 0; k2 < 6; ++k2) {
+        const double jr = L[k2 * 6 + r];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) H[q] += jr * L[k2 * 6 + q];
+      }
+    }
+  }
+  // group 0 += group 1
+  const int src = min(lane + 6, 63);
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    H[q] += __shfl(H[q], src, 64);
+    Sc[q] += __shfl(Sc[q], src, 64);
+  }
+  if (sub >= 6 || !live) return;
+  const double si = P.sF[(size_t)foff + offi + r];
+  double* Srow = P.S + P.win_soff[w] + (int64_t)(offi + r) * P.win_fpad[w] + offj;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) Srow[q] = si * P.sF[(size_t)foff + offj + q] * H[q] - Sc[q];
+}
+
 // k_assemble_sb: pairs with a speed/bias block (6x9, 9x9): few contributions (IMU factors,
 // speed/bias priors), one entry per lane.
 __global__ __launch_bounds__(256) void k_assemble_sb(const DevProblem* __restrict__ Pp) {
@@ -958,6 +1054,9 @@ void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s) {
 }
 void launch_assemble_pp(const DevProblem& P, hipStream_t s) {
   if (P.n_asm_pp > 0) hipLaunchKernelGGL(k_assemble_pp, dim3((P.n_asm_pp + 3) / 4), dim3(256), 0, s, P.self);
+  if (P.n_asm_ppl > 0)
+    hipLaunchKernelGGL(k_assemble_pp_light, dim3((P.n_asm_ppl + 256 / kPplLanes - 1) / (256 / kPplLanes)), dim3(256), 0,
+                       s, P.self);
 }
 void launch_assemble_sb(const DevProblem& P, hipStream_t s) {
   if (P.n_asm_sb > 0) hipLaunchKernelGGL(k_assemble_sb, dim3((P.n_asm_sb + 3) / 4), dim3(256), 0, s, P.self);
@@ -981,7 +1080,8 @@ void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t 
 }
 void launch_lm_prep(const DevProblem& P, hipStream_t s) { launch_lm_visit(P, 2, s); }
 void launch_zero_S(const DevProblem& P, hipStream_t s) {
-  if (P.n_tiles > 0) hipLaunchKernelGGL(k_zero_S, dim3(P.n_tiles), dim3(256), 0, s, P.self);
+  const int per = P.n_win >= kManyWindows ? kZeroTiles : 1;
+  if (P.n_tiles > 0) hipLaunchKernelGGL(k_zero_S, dim3((P.n_tiles + per - 1) / per), dim3(256), 0, s, P.self, per);
 }
 void launch_assemble(const DevProblem& P, hipStream_t s) {
   launch_assemble_pp(P, s);

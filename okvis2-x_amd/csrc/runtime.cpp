@@ -131,7 +131,7 @@ struct HostBatch {
   std::vector<int32_t> fb_win, fb_kind, fb_index, fb_off, fb_cbegin;
   std::vector<Contrib> fb_contrib;
   std::vector<int32_t> pair_win, pair_fi, pair_fj, pair_cbegin, pair_runs;
-  std::vector<int32_t> asm_pp_items, asm_sb_items;
+  std::vector<int32_t> asm_pp_items, asm_sb_items, asm_ppl_items;
   std::vector<int32_t> chol_panel_items, chol_panel_begin, chol_upd_items, chol_upd_begin, tile_items;
   int64_t n_band_updates = 0;
   std::vector<Contrib> pair_contrib;
@@ -839,27 +839,37 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
   // assembly work lists: pose-pose pairs (one wavefront each, 4 per workgroup) are grouped so
   // that workgroups b, b+8, ... (one XCD under round-robin placement; speed only) walk the pairs of
   // the same windows and share their visit blocks in that XCD's L2
+  // Off-diagonal pairs with few contributions (no visits; partial blocks and factor blocks only)
+  // take a 16-lane quarter of a wavefront each (k_assemble_pp_light, 16 per workgroup).
   {
-    constexpr int kWavesPerWG = 4, kXcd = 8;
+    constexpr int kXcd = 8;
     const int nq = B.n_win >= kXcd ? kXcd : 1;
-    std::vector<std::vector<int32_t>> q(nq);
+    std::vector<std::vector<int32_t>> q(nq), ql(nq);
     for (int k = 0; k < (int)B.pair_win.size(); ++k) {
       const bool pp = B.fb_kind[B.pair_fi[k]] == 0 && B.fb_kind[B.pair_fj[k]] == 0;
-      if (pp) q[B.pair_win[k] % nq].push_back(k);
-      else B.asm_sb_items.push_back(k);
+      const int kend = k + 1 < (int)B.pair_cbegin.size() ? B.pair_cbegin[k + 1] : (int)B.pair_contrib.size();
+      const bool light = B.n_win >= kManyWindows && B.pair_fi[k] != B.pair_fj[k] &&
+                         B.pair_runs[2 * k] == B.pair_cbegin[k] && kend - B.pair_cbegin[k] <= kAsmLightMax;
+      if (!pp) B.asm_sb_items.push_back(k);
+      else if (light) ql[B.pair_win[k] % nq].push_back(k);
+      else q[B.pair_win[k] % nq].push_back(k);
     }
-    std::vector<size_t> pos(nq, 0);
-    bool more = true;
-    while (more) {
-      more = false;
-      for (int x = 0; x < nq; ++x)
-        for (int i = 0; i < kWavesPerWG; ++i) {
-          const bool has = pos[x] < q[x].size();
-          B.asm_pp_items.push_back(has ? q[x][pos[x]++] : -1);
-        }
-      for (int x = 0; x < nq; ++x) more = more || pos[x] < q[x].size();
-    }
-    while (!B.asm_pp_items.empty() && B.asm_pp_items.back() < 0) B.asm_pp_items.pop_back();
+    auto interleave = [&](std::vector<std::vector<int32_t>>& qq, int perWG, std::vector<int32_t>& out) {
+      std::vector<size_t> pos(nq, 0);
+      bool more = true;
+      while (more) {
+        more = false;
+        for (int x = 0; x < nq; ++x)
+          for (int i = 0; i < perWG; ++i) {
+            const bool has = pos[x] < qq[x].size();
+            out.push_back(has ? qq[x][pos[x]++] : -1);
+          }
+        for (int x = 0; x < nq; ++x) more = more || pos[x] < qq[x].size();
+      }
+      while (!out.empty() && out.back() < 0) out.pop_back();
+    };
+    interleave(q, 4, B.asm_pp_items);
+    interleave(ql, 16, B.asm_ppl_items);
   }
   for (int w = 0; w < B.n_win; ++w) {
     B.win_tnzoff.push_back((int64_t)B.tile_nz.size());
@@ -1106,7 +1116,7 @@ struct okvisgpu_ctx {
                  o_pc = upl(B.pair_contrib);
     const size_t o_pruns = upl(B.pair_runs);
     const size_t o_tnz = upl(B.tile_nz), o_tnzoff = upl(B.win_tnzoff);
-    const size_t o_app = upl(B.asm_pp_items), o_asb = upl(B.asm_sb_items);
+    const size_t o_app = upl(B.asm_pp_items), o_asb = upl(B.asm_sb_items), o_appl = upl(B.asm_ppl_items);
     const size_t o_ti = upl(B.tile_items);
     const size_t o_cpi = upl(B.chol_panel_items), o_cpb = upl(B.chol_panel_begin), o_cui = upl(B.chol_upd_items),
                  o_cub = upl(B.chol_upd_begin);
@@ -1213,6 +1223,7 @@ struct okvisgpu_ctx {
     D.chol_pairs = 0;
     D.asm_pp_items = ip(o_app); D.asm_sb_items = ip(o_asb);
     D.n_asm_pp = (int)B.asm_pp_items.size(); D.n_asm_sb = (int)B.asm_sb_items.size();
+    D.asm_ppl_items = ip(o_appl); D.n_asm_ppl = (int)B.asm_ppl_items.size();
     D.tile_items = ip(o_ti);
     D.n_tiles = (int)(B.tile_items.size() / 3);
     D.S = dp(o_S);
@@ -1803,8 +1814,9 @@ double kernelWork(const HostBatch& B, const DevProblem& P, int k) {
   switch (k) {
     case K_ASSEMBLE_PP: {
       double desc = 0, pairs = 0;
-      for (int it : B.asm_pp_items)
-        if (it >= 0) { desc += B.pair_cbegin[it + 1] - B.pair_cbegin[it]; pairs += 1; }
+      for (const auto* list : {&B.asm_pp_items, &B.asm_ppl_items})
+        for (int it : *list)
+          if (it >= 0) { desc += B.pair_cbegin[it + 1] - B.pair_cbegin[it]; pairs += 1; }
       return desc * 16 + (double)P.n_part * 36 * d8 + (double)P.n_seg * (21 + 6) * d8 + pairs * (36 + 12) * d8;
     }
     case K_ASSEMBLE_SB: {

@@ -134,3 +134,22 @@ def test_relpose_cholesky_schedules(og, oracle, gpu_ctx):
             P0 = w.poses().copy()
         _close(sg, so)
         assert np.abs(P[:, :3] - P0[:, :3]).max() <= 1e-6
+
+
+def test_wide_band_schedules_bitwise(og, oracle, gpu_ctx):
+    """Edges 30 keyframes apart give columns of S with more non-zero tiles below the diagonal than
+    the back substitution keeps in its prefetch list (kBsPre = 3): the persistent and tile-parallel
+    schedules must still agree bitwise, and both with the oracle."""
+    w = _relpose_window(og, 40, 1600, 12000, n_relpose=4, stride=30, seed=45)
+    res = []
+    for sched in (1, 2):
+        w.reset()
+        gpu_ctx.set_problems([w.problem])
+        sg = gpu_ctx.solve(_opts(og, 4, cholesky_schedule=sched), 1)[0]
+        res.append((sg, w.poses().copy()))
+    assert res[0][0]["final_cost"] == res[1][0]["final_cost"]
+    assert np.array_equal(res[0][1], res[1][1])
+    w.reset()
+    so = oracle.solve(w.problem_ptr(), _opts(og, 4))
+    _close(res[0][0], so)
+    assert np.abs(res[0][1][:, :3] - w.poses()[:, :3]).max() <= 1e-6
