@@ -504,7 +504,12 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
     double acc[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) acc[i] = 0.0;
-#pragma unroll 2
+#ifndef OKG_PART_UNROLL
+#define OKG_PART_UNROLL 2
+#endif
+#define OKG_PRAGMA(x) _Pragma(#x)
+#define OKG_UNROLL(n) OKG_PRAGMA(unroll n)
+    OKG_UNROLL(OKG_PART_UNROLL)
     for (int c = c0; c < c1; ++c) {
       const int ab = staged ? sPC[c] : gPC[c], a = ab & 0xffff, b = ab >> 16;
       const double2* za2 = reinterpret_cast<const double2*>(sZ + kVisitZ * a + 6 * h);
