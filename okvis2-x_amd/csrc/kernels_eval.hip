@@ -590,82 +590,86 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
     if (l < 3) state[27 + l] = aadi;
   }
 
-  // ---- square-root information of P (PseudoInverse.hpp:132-158)
-  // symmetrise (ImuError.cpp:441): sB holds P column-major; the symmetric P is kept row-major
-  // (16x16 with a decoupled zero pad) in sA for the eigen fallback
-  if (integrate && l < 15)
-    for (int i = 0; i < 15; ++i) sB[l * 16 + i] = Pc[i];
-  __syncthreads();
-  double trace = 0.0;
-  if (integrate) {
-    for (int i = 0; i < 15; ++i) Pc[i] = (l < 15) ? 0.5 * Pc[i] + 0.5 * sB[i * 16 + l] : 0.0;
-    for (int i = 0; i < 16; ++i) sA[l * 16 + i] = (i < 15) ? Pc[i] : 0.0;
-    if (l < 15)  // P_delta_ (symmetrised), kept for a later append
-      for (int i = 0; i < 15; ++i) state[301 + i * 15 + l] = Pc[i];
-    for (int i = 0; i < 15; ++i) trace += (i == l) ? Pc[i] : 0.0;
-  }
-  trace = groupSum(trace);
-  __syncthreads();
-  // right-looking Cholesky P = L L^T in LDS: sB (column-major) starts as P, lane j owns column j
-  bool ok = true;
-  if (integrate)
-    for (int i = 0; i < 16; ++i) sB[l * 16 + i] = (l < 15 && i < 15) ? Pc[i] : 0.0;
-  __syncthreads();
-  for (int k = 0; k < 15; ++k) {
-    if (integrate && l >= k && l < 15) {
-      const double d = sB[k * 16 + k];
-      if (!(d > 0.0)) ok = false;
-      const double v = sB[k * 16 + l] / sqrt(d);
-      sB[k * 16 + l] = v;
+  // (skipped by a workgroup none of whose factors re-integrated: the common case once the biases
+  // have settled; the workgroup is one wavefront, so the test is uniform)
+  if (__any(integrate)) {
+    // ---- square-root information of P (PseudoInverse.hpp:132-158)
+    // symmetrise (ImuError.cpp:441): sB holds P column-major; the symmetric P is kept row-major
+    // (16x16 with a decoupled zero pad) in sA for the eigen fallback
+    if (integrate && l < 15)
+      for (int i = 0; i < 15; ++i) sB[l * 16 + i] = Pc[i];
+    __syncthreads();
+    double trace = 0.0;
+    if (integrate) {
+      for (int i = 0; i < 15; ++i) Pc[i] = (l < 15) ? 0.5 * Pc[i] + 0.5 * sB[i * 16 + l] : 0.0;
+      for (int i = 0; i < 16; ++i) sA[l * 16 + i] = (i < 15) ? Pc[i] : 0.0;
+      if (l < 15)  // P_delta_ (symmetrised), kept for a later append
+        for (int i = 0; i < 15; ++i) state[301 + i * 15 + l] = Pc[i];
+      for (int i = 0; i < 15; ++i) trace += (i == l) ? Pc[i] : 0.0;
     }
+    trace = groupSum(trace);
     __syncthreads();
-    if (integrate && l > k && l < 15) {
-      const double ljk = sB[k * 16 + l];
-      for (int i = l; i < 15; ++i) sB[l * 16 + i] -= sB[k * 16 + i] * ljk;
+    // right-looking Cholesky P = L L^T in LDS: sB (column-major) starts as P, lane j owns column j
+    bool ok = true;
+    if (integrate)
+      for (int i = 0; i < 16; ++i) sB[l * 16 + i] = (l < 15 && i < 15) ? Pc[i] : 0.0;
+    __syncthreads();
+    for (int k = 0; k < 15; ++k) {
+      if (integrate && l >= k && l < 15) {
+        const double d = sB[k * 16 + k];
+        if (!(d > 0.0)) ok = false;
+        const double v = sB[k * 16 + l] / sqrt(d);
+        sB[k * 16 + l] = v;
+      }
+      __syncthreads();
+      if (integrate && l > k && l < 15) {
+        const double ljk = sB[k * 16 + l];
+        for (int i = l; i < 15; ++i) sB[l * 16 + i] -= sB[k * 16 + i] * ljk;
+      }
+      __syncthreads();
     }
+    // U = L^-1 in place (column-major, backward over columns):
+    //   U(j,j) = 1/L(j,j),  U(i,j) = -U(j,j) sum_{m=j+1..i} U(i,m) L(m,j)   (i > j)
+    for (int j = 14; j >= 0; --j) {
+      double acc = 0.0, ujj = 0.0;
+      if (integrate && l >= j && l < 15) {
+        ujj = 1.0 / sB[j * 16 + j];
+        for (int m = j + 1; m <= l; ++m) acc += sB[m * 16 + l] * sB[j * 16 + m];
+      }
+      __syncthreads();
+      if (integrate && l >= j && l < 15) sB[j * 16 + l] = (l == j) ? ujj : -ujj * acc;
+      __syncthreads();
+    }
+    double fro = 0.0;
+    if (integrate && l < 15)
+      for (int i = l; i < 15; ++i) fro += sB[l * 16 + i] * sB[l * 16 + i];
+    fro = groupSum(fro);
+    ok = groupSum(ok ? 0.0 : 1.0) == 0.0;
+    const double eps = DBL_EPSILON;
+    const bool needEig = integrate && !(ok && fro > 0.0 && 1.0 / fro > 4.0 * fmax(eps, eps * 15.0 * trace));
+    __syncthreads();
+    if (__any(needEig)) {
+      // clamped eigenvalues possible: the reference's eigen-decomposition (cyclic Jacobi) of the
+      // symmetric P kept in sA; eigenvectors into sB, then U = diag(clamped lambda^-1/2) V^T
+      groupJacobi(sA, sB, sR, l, needEig);
+      double urow[15];
+      if (needEig && l < 15) {
+        double lmax = -1e300;
+        for (int i = 0; i < 15; ++i) lmax = fmax(lmax, sA[i * 16 + i]);
+        const double tol = fmax(eps, eps * 15.0 * lmax);
+        const double li = sA[l * 16 + l];
+        const double s = sqrt(li > tol ? 1.0 / li : 1.0 / tol);
+        for (int j = 0; j < 15; ++j) urow[j] = s * sB[j * 16 + l];
+      }
+      __syncthreads();
+      if (needEig && l < 15)
+        for (int j = 0; j < 15; ++j) sA[l * 16 + j] = urow[j];
+    }
+    // Cholesky path: U (column-major in sB, lower triangular) -> row-major sA
+    if (integrate && !needEig && l < 15)
+      for (int i = 0; i < 15; ++i) sA[i * 16 + l] = (i >= l) ? sB[l * 16 + i] : 0.0;
     __syncthreads();
   }
-  // U = L^-1 in place (column-major, backward over columns):
-  //   U(j,j) = 1/L(j,j),  U(i,j) = -U(j,j) sum_{m=j+1..i} U(i,m) L(m,j)   (i > j)
-  for (int j = 14; j >= 0; --j) {
-    double acc = 0.0, ujj = 0.0;
-    if (integrate && l >= j && l < 15) {
-      ujj = 1.0 / sB[j * 16 + j];
-      for (int m = j + 1; m <= l; ++m) acc += sB[m * 16 + l] * sB[j * 16 + m];
-    }
-    __syncthreads();
-    if (integrate && l >= j && l < 15) sB[j * 16 + l] = (l == j) ? ujj : -ujj * acc;
-    __syncthreads();
-  }
-  double fro = 0.0;
-  if (integrate && l < 15)
-    for (int i = l; i < 15; ++i) fro += sB[l * 16 + i] * sB[l * 16 + i];
-  fro = groupSum(fro);
-  ok = groupSum(ok ? 0.0 : 1.0) == 0.0;
-  const double eps = DBL_EPSILON;
-  const bool needEig = integrate && !(ok && fro > 0.0 && 1.0 / fro > 4.0 * fmax(eps, eps * 15.0 * trace));
-  __syncthreads();
-  if (__any(needEig)) {
-    // clamped eigenvalues possible: the reference's eigen-decomposition (cyclic Jacobi) of the
-    // symmetric P kept in sA; eigenvectors into sB, then U = diag(clamped lambda^-1/2) V^T
-    groupJacobi(sA, sB, sR, l, needEig);
-    double urow[15];
-    if (needEig && l < 15) {
-      double lmax = -1e300;
-      for (int i = 0; i < 15; ++i) lmax = fmax(lmax, sA[i * 16 + i]);
-      const double tol = fmax(eps, eps * 15.0 * lmax);
-      const double li = sA[l * 16 + l];
-      const double s = sqrt(li > tol ? 1.0 / li : 1.0 / tol);
-      for (int j = 0; j < 15; ++j) urow[j] = s * sB[j * 16 + l];
-    }
-    __syncthreads();
-    if (needEig && l < 15)
-      for (int j = 0; j < 15; ++j) sA[l * 16 + j] = urow[j];
-  }
-  // Cholesky path: U (column-major in sB, lower triangular) -> row-major sA
-  if (integrate && !needEig && l < 15)
-    for (int i = 0; i < 15; ++i) sA[i * 16 + l] = (i >= l) ? sB[l * 16 + i] : 0.0;
-  __syncthreads();
   if (integrate) {
     for (int e = l; e < 225; e += kImuGroup) state[66 + e] = sA[(e / 15) * 16 + e % 15];
   } else if (live) {
