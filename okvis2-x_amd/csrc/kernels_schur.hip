@@ -87,6 +87,11 @@ __device__ __forceinline__ bool lmVisitSelect(const DevProblem& P, int w, int mo
 #ifndef OKG_LMV_OCC
 #define OKG_LMV_OCC 3
 #endif
+#ifndef OKG_PART_ROWS
+#define OKG_PART_ROWS 2
+#endif
+constexpr int kPartRows = OKG_PART_ROWS, kPartThreads = 6 / kPartRows;  // partial-block rows per thread
+static_assert(kPartRows == 2 || kPartRows == 3, "OKG_PART_ROWS must be 2 or 3");
 // Development-only phase clock of k_lm_visit<1> (make OPT="-O3 -DOKG_LMV_CLOCK"): thread 0 of every
 // workgroup adds its s_memrealtime ticks (100 MHz) per phase with vector atomics; the last workgroup
 // prints the totals.
@@ -302,6 +307,9 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   const auto gsr = gmem(reinterpret_cast<const int2*>(P.seg_range));
   const int sgl = max(nseg - 1, 0);
   const int2 rA = gsr[sg0 + min(t / 18, sgl)], rB = gsr[sg0 + min(t / 9, sgl)], rC = gsr[sg0 + min(t / 6, sgl)];
+  // (and this thread's first partial block's product range)
+  const int pfi = npart > 0 ? pg0 + min(t / kPartThreads, npart - 1) : 0;  // (index 1 exists: >= 8-byte arrays)
+  const int pcA = gmem(P.part_cbegin)[pfi], pcB = gmem(P.part_cbegin)[pfi + 1];
   double spr[6];
   {
     const auto spp = gmem(pf >= 0 ? P.sF + (size_t)P.win_foff[w] + pf : P.pose[0]);
@@ -414,7 +422,8 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   }
   ldsBarrier();
   LCLK(1)
-  asm volatile("" ::"v"(rA.x), "v"(rA.y), "v"(rB.x), "v"(rB.y), "v"(rC.x), "v"(rC.y));  // (not sunk into branches)
+  asm volatile("" ::"v"(rA.x), "v"(rA.y), "v"(rB.x), "v"(rB.y), "v"(rC.x), "v"(rC.y), "v"(pcA),
+               "v"(pcB));  // (not sunk into branches)
   // ---- segments: H | g of each (group, free pose) summed over its visits (visits are scattered
   // to their slots so that every segment is a contiguous LDS range). The visit shares of V / g_l
   // are consumed, so all 18 rows of sBuf take values: H[0..17], then H[18..20] | g_p.
@@ -498,12 +507,13 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
   ldsBarrier();
   LCLK(4)
   const auto gPC = gmem(P.part_contrib + pc0);
-  for (int e = t; e < npart * 3; e += kLmGroupVisits) {
-    const int pi = e / 3, h = e - pi * 3;
-    const int c0 = P.part_cbegin[pg0 + pi] - pc0, c1 = P.part_cbegin[pg0 + pi + 1] - pc0;
-    double acc[12];
+  // kPartRows rows of the 6x6 block per thread (kPartThreads = 6 / kPartRows threads per block)
+  for (int e = t; e < npart * kPartThreads; e += kLmGroupVisits) {
+    const int pi = e / kPartThreads, h = e - pi * kPartThreads;
+    const int c0 = (e == t ? pcA : P.part_cbegin[pg0 + pi]) - pc0, c1 = (e == t ? pcB : P.part_cbegin[pg0 + pi + 1]) - pc0;
+    double acc[6 * kPartRows];
 #pragma unroll
-    for (int i = 0; i < 12; ++i) acc[i] = 0.0;
+    for (int i = 0; i < 6 * kPartRows; ++i) acc[i] = 0.0;
 #ifndef OKG_PART_UNROLL
 #define OKG_PART_UNROLL 2
 #endif
@@ -512,22 +522,28 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
     OKG_UNROLL(OKG_PART_UNROLL)
     for (int c = c0; c < c1; ++c) {
       const int ab = staged ? sPC[c] : gPC[c], a = ab & 0xffff, b = ab >> 16;
-      const double2* za2 = reinterpret_cast<const double2*>(sZ + kVisitZ * a + 6 * h);
+      const double* zaP = sZ + kVisitZ * a + 3 * kPartRows * h;
       const double2* zb2 = reinterpret_cast<const double2*>(sZ + kVisitZ * b);
-      double za[6], zb[18];
+      double za[3 * kPartRows], zb[18];
+      if (kPartRows == 2) {  // 16-byte aligned: 3 x 16-byte loads
+        const double2* za2 = reinterpret_cast<const double2*>(zaP);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) { const double2 v = za2[i]; za[2 * i] = v.x; za[2 * i + 1] = v.y; }
+        for (int i = 0; i < 3; ++i) { const double2 v = za2[i]; za[2 * i] = v.x; za[2 * i + 1] = v.y; }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 3 * kPartRows; ++i) za[i] = zaP[i];
+      }
 #pragma unroll
       for (int i = 0; i < 9; ++i) { const double2 v = zb2[i]; zb[2 * i] = v.x; zb[2 * i + 1] = v.y; }
 #pragma unroll
-      for (int rr = 0; rr < 2; ++rr)
+      for (int rr = 0; rr < kPartRows; ++rr)
 #pragma unroll
         for (int q = 0; q < 6; ++q)
           acc[rr * 6 + q] += za[3 * rr] * zb[3 * q] + za[3 * rr + 1] * zb[3 * q + 1] + za[3 * rr + 2] * zb[3 * q + 2];
     }
-    double2* out = reinterpret_cast<double2*>(P.part_S + (size_t)(pg0 + pi) * 36 + 12 * h);
+    double2* out = reinterpret_cast<double2*>(P.part_S + (size_t)(pg0 + pi) * 36 + 6 * kPartRows * h);
 #pragma unroll
-    for (int q = 0; q < 6; ++q) out[q] = double2{acc[2 * q], acc[2 * q + 1]};
+    for (int q = 0; q < 3 * kPartRows; ++q) out[q] = double2{acc[2 * q], acc[2 * q + 1]};
   }
 #ifdef OKG_LMV_CLOCK
   __syncthreads();
