@@ -104,21 +104,62 @@ __global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp) {
   double* out = nullptr;
   size_t ostride = 0;
   bool live = false;
-  if (u < P.n_imu) {
-    w = P.imu_win[u];
-    if (jvSelect(P, w)) {
-      live = true;
-      out = P.imu_jv + u;
-      ostride = P.n_imu;
-      if (!(P.imu_flags[u] & 2)) {
-        const int* blk = P.imu_blocks + 4 * u;
-        J = P.imu_lin[P.st[w].lcur] + (size_t)u * kImuLin + 15;
-        nr = 15; ld = 30; nb = 4;
-        off[0] = P.pose_f[blk[0]]; off[1] = P.sb_f[blk[1]]; off[2] = P.pose_f[blk[2]]; off[3] = P.sb_f[blk[3]];
-        n[0] = 6; n[1] = 9; n[2] = 6; n[3] = 9;
-        col[0] = 0; col[1] = 6; col[2] = 15; col[3] = 21;
-      }
+  // IMU factors (the bulk): every operand in three rounds of loads, no branch on a loaded value
+  // before they are issued. Lane r holds row r of the 15x30 Jacobian; lanes r and r + 16 of the
+  // group form the scaled direction vectors of columns r and r + 16, exchanged through LDS.
+  __shared__ double sVc[256 / 16][32][2];
+  if (gid < P.n_imu) {
+    const int f = gid, grp = threadIdx.x >> 4;
+    const int fw = gmem(P.imu_win)[f], ffl = gmem(P.imu_flags)[f];
+    const int4 blk = gmem(reinterpret_cast<const int4*>(P.imu_blocks))[f];
+    const auto gst = gmem(P.st + fw);
+    const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed, lcur = gst->lcur;
+    const int o0 = gmem(P.pose_f)[blk.x], o1 = gmem(P.sb_f)[blk.y], o2 = gmem(P.pose_f)[blk.z], o3 = gmem(P.sb_f)[blk.w];
+    const int foff = gmem(P.win_foff)[fw];
+    const bool fl = (sDone == 0) & (sNeed != 0) & (sFail == 0), act = fl & !(ffl & 2);
+    // this lane's two columns (c = r, r + 16 < 30): block offset and position
+    double vcv[2], vgv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = r + 16 * h;
+      const int q = c < 6 ? 0 : c < 15 ? 1 : c < 21 ? 2 : 3;
+      const int cq = c - (q == 0 ? 0 : q == 1 ? 6 : q == 2 ? 15 : 21);
+      const int oq = q == 0 ? o0 : q == 1 ? o1 : q == 2 ? o2 : o3;
+      const bool ok = act && c < 30 && oq >= 0;
+      const size_t i = ok ? (size_t)foff + oq + cq : 0;
+      const double sc = gmem(P.sF)[i], cv = gmem(cF)[i], yv = gmem(yF)[i];
+      vcv[h] = ok ? sc * cv : 0.0;
+      vgv[h] = ok ? -sc * yv : 0.0;
     }
+    const auto Jr = gmem(pick2(lcur, P.imu_lin[0], P.imu_lin[1]) + (size_t)(act ? f : 0) * kImuLin + 15 +
+                         30 * (size_t)min(r, 14));
+    double jr[30];
+#pragma unroll
+    for (int c = 0; c < 30; ++c) jr[c] = Jr[c];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      sVc[grp][r + 16 * h][0] = vcv[h];
+      sVc[grp][r + 16 * h][1] = vgv[h];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double jc0 = 0.0, jg0 = 0.0;
+#pragma unroll
+    for (int c = 0; c < 30; ++c) {
+      jc0 += jr[c] * sVc[grp][c][0];
+      jg0 += jr[c] * sVc[grp][c][1];
+    }
+    double a3[3] = {r < 15 ? jc0 * jc0 : 0.0, r < 15 ? jg0 * jg0 : 0.0, r < 15 ? jc0 * jg0 : 0.0};
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int m = 8; m > 0; m >>= 1) a3[k] += __shfl_xor(a3[k], m, 64);
+    if (fl && r == 0)
+      for (int k = 0; k < 3; ++k) P.imu_jv[(size_t)k * P.n_imu + f] = a3[k];
+    return;
+  }
+  if (u < P.n_imu) {
   } else if ((u -= P.n_imu) < P.n_pprior) {
     w = P.pp_win[u];
     if (jvSelect(P, w)) {

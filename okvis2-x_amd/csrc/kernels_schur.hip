@@ -821,14 +821,28 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
     }
   }
   // partial Schur blocks of the landmark groups: row r of sum Z_a Z_b^T (= Y_a U_b^T)
+  // (two of the lane's contributions per round (80 VGPRs): descriptors, then rows, each round in flight
+  // together; clamped indices, masked sums, same order as one by one)
   const auto ps = gmem(P.part_S);
-  for (int c = pb + g0; c < ob; c += kGroups) {
-    const auto R2 = reinterpret_cast<gptr<double2>>(ps + (size_t)pc[c].a * 36 + 6 * r);
+  for (int c = pb + g0; c < ob; c += 2 * kGroups) {
+    int ai[2];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const double2 v = R2[q];
-      Sc[2 * q] += v.x;
-      Sc[2 * q + 1] += v.y;
+    for (int u = 0; u < 2; ++u) ai[u] = pc[min(c + u * kGroups, ob - 1)].a;
+    double2 v[2][3];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const auto R2 = reinterpret_cast<gptr<double2>>(ps + (size_t)ai[u] * 36 + 6 * r);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) v[u][q] = R2[q];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool ok = c + u * kGroups < ob;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        Sc[2 * q] += ok ? v[u][q].x : 0.0;
+        Sc[2 * q + 1] += ok ? v[u][q].y : 0.0;
+      }
     }
   }
   // factor blocks (IMU, relative pose, pose prior): row r of J_i^T J_j
@@ -925,15 +939,28 @@ __global__ __launch_bounds__(256) void k_assemble_pp_light(const DevProblem* __r
   double H[6], Sc[6];
 #pragma unroll
   for (int q = 0; q < 6; ++q) { H[q] = 0.0; Sc[q] = 0.0; }
+  // partial blocks, four of the lane's contributions per round: their descriptors, then their rows,
+  // each round of loads in flight together (clamped indices, masked sums; same order as one by one)
   const auto ps = gmem(P.part_S);
-  for (int c = pb + g0; c < ob; c += kPplGroups) {
-    const int a = c == cFirst ? C0.a : pc[c].a;
-    const auto R2 = reinterpret_cast<gptr<double2>>(ps + (size_t)a * 36 + 6 * r);
+  for (int c = pb + g0; c < ob; c += 4 * kPplGroups) {
+    int ai[4];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const double2 v = R2[q];
-      Sc[2 * q] += v.x;
-      Sc[2 * q + 1] += v.y;
+    for (int u = 0; u < 4; ++u) ai[u] = pc[min(c + u * kPplGroups, ob - 1)].a;
+    double2 v[4][3];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const auto R2 = reinterpret_cast<gptr<double2>>(ps + (size_t)ai[u] * 36 + 6 * r);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) v[u][q] = R2[q];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = c + u * kPplGroups < ob;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        Sc[2 * q] += ok ? v[u][q].x : 0.0;
+        Sc[2 * q + 1] += ok ? v[u][q].y : 0.0;
+      }
     }
   }
   for (int c = ob + g0; c < ce; c += kPplGroups) {
