@@ -1072,17 +1072,33 @@ __global__ __launch_bounds__(256) void k_gn_finalize(const DevProblem* __restric
   const DevProblem& P = *Pp;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= P.n_fblock) return;
-  const int w = P.fb_win[t];
-  if (!gnSelect(P, w)) return;
-  const int n = P.fb_kind[t] == 0 ? 6 : 9;
-  const size_t base = (size_t)P.win_foff[w] + P.fb_off[t];
-  for (int c = 0; c < n; ++c) {
+  // the block record and window state, then all of the block's operands (loads before the stores:
+  // the output vectors may alias the inputs as far as the compiler knows)
+  const int w = gmem(P.fb_win)[t], kind = gmem(P.fb_kind)[t], fo = gmem(P.fb_off)[t];
+  const auto gst = gmem(P.st + w);
+  const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed;
+  const int foff = gmem(P.win_foff)[w];
+  asm volatile("" ::"v"(kind), "v"(fo), "v"(foff));
+  if ((sDone != 0) | (sNeed == 0) | (sFail != 0)) return;  // gnSelect
+  const int n = kind == 0 ? 6 : 9;
+  const size_t base = (size_t)foff + fo;
+  double dg[9], y[9], sc[9], g[9];
+#pragma unroll
+  for (int c = 0; c < 9; ++c) {
+    const size_t i = base + (c < n ? c : 0);
+    dg[c] = gmem(P.diagF)[i];
+    y[c] = gmem(P.yF)[i];
+    sc[c] = gmem(P.sF)[i];
+    g[c] = gmem(P.gF)[i];
+  }
+#pragma unroll
+  for (int c = 0; c < 9; ++c) {
+    if (c >= n) break;
     const size_t i = base + c;
-    const double dg = P.diagF[i];
-    P.gnF[i] = -dg * P.yF[i];
-    const double gr = P.sF[i] * P.gF[i] / dg;
+    P.gnF[i] = -dg[c] * y[c];
+    const double gr = sc[c] * g[c] / dg[c];
     P.dgF[i] = gr;
-    P.vF[i] = gr / dg;
+    P.vF[i] = gr / dg[c];
   }
 }
 
