@@ -321,34 +321,56 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   double* sF = sAll[g] + 512;
   double* sR = sF;
 
-  int w = 0, xs = 0, lb = 0;
-  bool live = f < P.n_imu;
-  if (live && !APPEND) {
-    w = P.imu_win[f];
-    live = evalSelect(P, w, mode, xs, lb) && !((P.imu_flags[f] & 2) && mode < 2);
+  // The factor's record, the head of its stored state and the window state are loaded in two
+  // rounds (clamped index) and consumed at one point before any test, so that no load waits behind
+  // a branch on another (evalSelect restated branch-free).
+  const bool inR = f < P.n_imu;
+  const int fc = inR ? f : 0;
+  // (the append batch carries no window data: no window, flags or WinState are read there)
+  const int wR = APPEND ? 0 : gmem(P.imu_win)[fc];
+  const int flR = APPEND ? 0 : gmem(P.imu_flags)[fc];
+  const int4 blkR = gmem(reinterpret_cast<const int4*>(P.imu_blocks))[fc];
+  const int64_t t0 = gmem(P.imu_t0)[fc], t1 = gmem(P.imu_t1)[fc];
+  const int sbeg = gmem(P.imu_sbegin)[fc], send = gmem(P.imu_sbegin)[fc + 1];
+  const auto stR = gmem(P.imu_state + (size_t)fc * kImuState);
+  const double st0 = stR[0], st1 = stR[1];
+  double bref[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) bref[k] = stR[57 + 3 + k];
+  int sDone = 0, sCand = 0, sX = 0, sL = 0;
+  if (!APPEND) {
+    const auto gst = gmem(P.st + wR);
+    sDone = gst->done;
+    sCand = gst->eval_cand;
+    sX = gst->xcur;
+    sL = gst->lcur;
   }
-  const int fs = live ? f : 0;  // safe index for idle groups
+  const auto parp = gmem(P.imu_par + 7 * wR);
+  const double a_max = parp[0], g_max = parp[1], sg_c = parp[2], sa_c = parp[3], sgw_c = parp[4], saw_c = parp[5],
+               gmag = parp[6];
+  const int64_t tsLast = gmem(P.imu_ts)[max(send - 1, 0)];
+  asm volatile("" ::"v"(flR), "v"(blkR.y), "v"(t0), "v"(t1), "v"(st0), "v"(st1), "v"(bref[0]), "v"(bref[5]),
+               "v"(sDone), "v"(sCand), "v"(sX), "v"(sL), "v"(a_max), "v"(gmag), "v"(tsLast));
+  const bool live = inR && (APPEND || ((sDone == 0) & (mode != 1 || sCand != 0) & !((flR & 2) && mode < 2)));
+  const int w = APPEND ? 0 : wR;
+  const int xs = APPEND ? 0 : (mode == 1 ? 1 - sX : sX), lb = APPEND ? 0 : (mode == 1 ? 1 - sL : sL);
+  const int fs = live ? f : 0;  // safe index for idle groups (writes are all under live)
 
   const int* blk = P.imu_blocks + 4 * fs;
-  const double* sb0 = P.sb[xs] + 9 * (size_t)blk[1];
+  const auto sb0 = gmem(pick2(xs, P.sb[0], P.sb[1]) + 9 * (size_t)blkR.y);
   double* state = P.imu_state + (size_t)fs * kImuState;
-  const double* par = P.imu_par + 7 * w;
-  const double a_max = par[0], g_max = par[1], sg_c = par[2], sa_c = par[3], sgw_c = par[4], saw_c = par[5],
-               gmag = par[6];
-  const int64_t t0 = P.imu_t0[fs], t1 = P.imu_t1[fs];
-  const int sbeg = P.imu_sbegin[fs], send = P.imu_sbegin[fs + 1];
 
   // ---- re-preintegration decision (ImuError.cpp:833-859)
-  int redoCounter = (int)state[0];
-  bool redo = state[1] != 0.0;
+  int redoCounter = (int)st0;
+  bool redo = st1 != 0.0;
   double Db[6];
-  for (int k = 0; k < 6; ++k) Db[k] = sb0[3 + k] - state[57 + 3 + k];
+  for (int k = 0; k < 6; ++k) Db[k] = sb0[3 + k] - bref[k];
   redo = redo || (sqrt(Db[0] * Db[0] + Db[1] * Db[1] + Db[2] * Db[2]) > 0.0003);
   const bool doRedo =
       APPEND || (redo && ((send - sbeg) < 50 || P.opt.redo_propagation_always)) || redoCounter == 0;
   // redoPreintegration returns -1 before touching any state when the samples do not cover t1
   // (ImuError.cpp:270-273): the old preintegration is kept.
-  const bool covered = (send > sbeg) && P.imu_ts[send - 1] >= t1;
+  const bool covered = (send > sbeg) && tsLast >= t1;
   const bool integrate = live && doRedo && covered;
   if (live && doRedo && !APPEND) {
     redoCounter++;
@@ -677,9 +699,9 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   }
   __syncthreads();  // state writes of the group visible to all its lanes
   if (APPEND) return;  // uniform over the workgroup
-  const double* p0 = P.pose[xs] + 7 * (size_t)blk[0];
-  const double* p1 = P.pose[xs] + 7 * (size_t)blk[2];
-  const double* sb1 = P.sb[xs] + 9 * (size_t)blk[3];
+  const double* p0 = pick2(xs, P.pose[0], P.pose[1]) + 7 * (size_t)blk[0];
+  const double* p1 = pick2(xs, P.pose[0], P.pose[1]) + 7 * (size_t)blk[2];
+  const double* sb1 = pick2(xs, P.sb[0], P.sb[1]) + 9 * (size_t)blk[3];
   ImuPre pre;
   loadPre(state, pre);
   const bool success = live && (!integrate || steps > 0);
