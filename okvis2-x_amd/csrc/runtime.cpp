@@ -419,21 +419,32 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     {
       int prevL = -1, prevP = -1;
       std::vector<int> vcount(p->n_landmarks, 0);
+      // per-observation arrays written in place (sized once; push_back per element dominated)
+      const size_t nob = (size_t)p->n_observations;
+      for (auto* v : {&B.obs_pose, &B.obs_lm, &B.obs_cam, &B.obs_win, &B.obs_orig}) v->resize(ob + nob);
+      B.obs_flags.resize(ob + nob);
+      B.obs_kp.resize(2 * (ob + nob));
+      B.obs_L.resize(4 * (ob + nob));
+      int32_t *oPose = B.obs_pose.data() + ob, *oLm = B.obs_lm.data() + ob, *oCam = B.obs_cam.data() + ob,
+              *oWin = B.obs_win.data() + ob, *oOrig = B.obs_orig.data() + ob;
+      uint8_t* oFl = B.obs_flags.data() + ob;
+      double *oKp = B.obs_kp.data() + 2 * (size_t)ob, *oL = B.obs_L.data() + 4 * (size_t)ob;
       for (int k = 0; k < p->n_observations; ++k) {
         const int o = order[k];
-        const int l = inv[p->obs_landmark[o]], ps = p->obs_pose[o];
-        B.obs_pose.push_back(pb + ps);
-        B.obs_lm.push_back(lb + l);
-        B.obs_cam.push_back(cb + p->obs_camera[o]);
-        B.obs_win.push_back(w);
-        B.obs_orig.push_back(o);
+        const int l = inv[p->obs_landmark[o]], ps = p->obs_pose[o], cam = p->obs_camera[o];
+        oPose[k] = pb + ps;
+        oLm[k] = lb + l;
+        oCam[k] = cb + cam;
+        oWin[k] = w;
+        oOrig[k] = o;
         uint8_t fl = 0;
         if (p->obs_cauchy ? p->obs_cauchy[o] != 0 : true) fl |= 1;
         if (ofix[o]) fl |= 2;
-        if (posef[np + p->obs_camera[o]] >= 0) fl |= 4;  // variable extrinsics
-        B.obs_flags.push_back(fl);
-        appendN(B.obs_kp, &p->obs_keypoint[2 * o], 2);
-        appendN(B.obs_L, &p->obs_sqrt_info[4 * o], 4);
+        if (posef[np + cam] >= 0) fl |= 4;  // variable extrinsics
+        oFl[k] = fl;
+        oKp[2 * k] = p->obs_keypoint[2 * o];
+        oKp[2 * k + 1] = p->obs_keypoint[2 * o + 1];
+        for (int i = 0; i < 4; ++i) oL[4 * k + i] = p->obs_sqrt_info[4 * o + i];
         if (l != prevL || ps != prevP) {
           B.visit_pose.push_back(pb + ps);
           B.visit_lm.push_back(lb + l);
