@@ -300,6 +300,34 @@ __device__ void groupJacobi(double* A, double* V, double* rot, int l, bool need)
 #ifndef OKG_IMU_OCC
 #define OKG_IMU_OCC 2
 #endif
+// Development-only phase clock of k_eval_imu (make OPT="-O3 -DOKG_IMU_CLOCK"): lane 0 of every
+// workgroup adds its s_memrealtime ticks (100 MHz) per phase with vector atomics; the last
+// workgroup prints the totals.
+#ifdef OKG_IMU_CLOCK
+__device__ unsigned long long g_imuClk[8];
+__device__ unsigned int g_imuDone;
+#define ICLK_INIT unsigned long long iclk = __builtin_amdgcn_s_memrealtime();
+#define ICLK(i)                                                                         \
+  if (!APPEND && threadIdx.x == 0) {                                                    \
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();                    \
+    atomicAdd(&g_imuClk[i], now - iclk);                                                \
+    iclk = now;                                                                         \
+  }
+#define ICLK_END                                                                        \
+  if (!APPEND && threadIdx.x == 0) {                                                    \
+    __threadfence();                                                                    \
+    if (atomicAdd(&g_imuDone, 1u) == gridDim.x - 1) {                                   \
+      printf("IMUCLK pro %llu chain %llu state %llu sqrt %llu resid %llu jac %llu (x10ns)\n", g_imuClk[0], \
+             g_imuClk[1], g_imuClk[2], g_imuClk[3], g_imuClk[4], g_imuClk[5]);         \
+      for (int i = 0; i < 8; ++i) g_imuClk[i] = 0;                                      \
+      g_imuDone = 0;                                                                    \
+    }                                                                                   \
+  }
+#else
+#define ICLK_INIT
+#define ICLK(i)
+#define ICLK_END
+#endif
 // APPEND: ImuError::append (ImuError.cpp:63-255) for a batch of factors (okvisgpu_imu_append): the
 // chain starts from the stored state (Delta_q, integrals, cross_, dv_db_g, P) at imu_t0 (= the old
 // t1), integrates the appended samples with the eliminated state's bias (sb[0] row blk[1]) up to
@@ -309,6 +337,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   const DevProblem& P = *Pp;
   const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
   const int f = blockIdx.x * kImuPerWG + g;
+  ICLK_INIT
 
   // per-group LDS: sA = step records of a chunk during the chain, then symmetric P / Jacobi
   // matrix / U (row-major 16x16); sB = transpose exchange / L (column-major) / Jacobi eigenvectors;
@@ -406,6 +435,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
       for (int i = 0; i < 15; ++i) Pc[i] = state[301 + i * 15 + l];
   }
 
+  ICLK(0)
   // ---- redoPreintegration (ImuError.cpp:258-466), uniform trip count over the wavefront.
   // What a step needs that does not depend on the integration chain (its length, the interpolated
   // samples, dq = exp(w dt), the right Jacobian of w dt, R(dq)^T, the noise terms) is formed for 16
@@ -590,6 +620,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
       }
     }
   }
+  ICLK(1)
   // new preintegration state (ImuError.hpp:273-304 members) straight from the chain registers;
   // the distributed accumulators are written by their owner lanes
   if (integrate) {
@@ -612,6 +643,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
     if (l < 3) state[27 + l] = aadi;
   }
 
+  ICLK(2)
   // (skipped by a workgroup none of whose factors re-integrated: the common case once the biases
   // have settled; the workgroup is one wavefront, so the test is uniform)
   if (__any(integrate)) {
@@ -698,6 +730,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
     for (int e = l; e < 225; e += kImuGroup) sA[(e / 15) * 16 + e % 15] = state[66 + e];
   }
   __syncthreads();  // state writes of the group visible to all its lanes
+  ICLK(3)
   if (APPEND) return;  // uniform over the workgroup
   const double* p0 = pick2(xs, P.pose[0], P.pose[1]) + 7 * (size_t)blk[0];
   const double* p1 = pick2(xs, P.pose[0], P.pose[1]) + 7 * (size_t)blk[2];
@@ -817,6 +850,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   const double c2 = groupSum(l < 15 ? rr * rr : 0.0);
   if (live && l == 0) P.imu_cost[lb][f] = 0.5 * c2;
   __syncthreads();
+  ICLK(4)
   // J = U [F0 | F1]; lane l computes columns l and l + 16 of the 15 x 30 Jacobian. Column j of
   // [F0 | F1] has at most three non-zero 3-blocks: (block row, staged block, sign, or identity).
   if (live) {
@@ -856,6 +890,10 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
       }
     }
   }
+#ifdef OKG_IMU_CLOCK
+  ICLK(5)
+  ICLK_END
+#endif
 }
 
 // ------------------------------------------------------------------------------------ priors
