@@ -6,8 +6,10 @@ A step = one trust-region iteration (Ceres semantics: linearise + Schur-reduce +
 candidate evaluation + accept/reject) of EVERY window in the job's batch of independent synthetic
 S50 windows (50 keyframes, 2,000 landmarks, 16,000 reprojections, 49 IMU factors).
 value = (windows x timed iterations) / wall time of the timed region, max over ranks
-(window-iterations per second, whole job). Strong scaling: the total window count is fixed and
-split across ranks (one process per GPU, no data-path collective). At the end of the
+(window-iterations per second, whole job). Weak scaling: every rank solves its own batch of
+--windows-per-gpu independent windows (2,048 by default, distinct seeds across ranks; one process
+per GPU, no data-path collective). --windows T fixes the job total instead (strong
+scaling, T split across ranks). At the end of the
 run the per-window summaries and final poses are all-gathered to rank 0 over RCCL (§8e), outside
 the timed region, and rank 0 checks that every window of the job ran every iteration.
 
@@ -116,10 +118,19 @@ PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
 
 def rank_windows(total, world, rank):
-    """This rank's share of the fixed total window count (strong scaling)."""
+    """This rank's contiguous share of the job's windows."""
     per = [total // world + (1 if r < total % world else 0) for r in range(world)]
     start = sum(per[:rank])
     return list(range(start, start + per[rank]))
+
+
+def job_windows(args, world):
+    """Resolve the job's window count: --windows fixes the total (strong scaling), else every rank
+    holds --windows-per-gpu windows (weak scaling). Returns True for strong scaling."""
+    strong = args.windows is not None
+    if not strong:
+        args.windows = args.windows_per_gpu * world
+    return strong
 
 
 def aggregate(dist, elapsed, early, device):
@@ -251,7 +262,8 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--windows", type=int, default=2048, help="total windows in the job (strong scaling)")
+    ap.add_argument("--windows-per-gpu", type=int, default=2048, help="windows per rank (weak scaling, default)")
+    ap.add_argument("--windows", type=int, default=None, help="fixed job total split across ranks (strong scaling)")
     ap.add_argument("--config", default="s50", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-threads", type=int, default=3, help="realtime_num_threads (okvis2.yaml:93)")
     ap.add_argument("--cpu-iters", type=int, default=None, help="default: warmup + steps")
@@ -318,6 +330,7 @@ def dry_run(args, world, rank):
         import torch.distributed as tdist
         tdist.init_process_group("gloo")
         dist = tdist
+    job_windows(args, world)
     mine = rank_windows(args.windows, world, rank)
     rows = np.array([[i, 0.0, float(i), args.warmup + args.steps, 1, 0] for i in mine]).reshape(-1, len(SUMMARY_COLS))
     got = gather_rows(dist, rows, args.windows, "cpu")
@@ -356,7 +369,8 @@ def main(argv=None):
         assert dist.get_world_size() == args.gpus
     cfg = CONFIGS[args.config]
 
-    # ---- this rank's share of the fixed total (strong scaling)
+    # ---- this rank's windows: its own batch (weak scaling) or a share of a fixed total (strong)
+    strong = job_windows(args, world)
     mine = rank_windows(args.windows, world, rank)
     windows = make_windows(cfg, mine)
     ctx = og.Context(local_rank)
@@ -409,7 +423,7 @@ def main(argv=None):
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (EuRoC stereo rig, 200 Hz IMU, seeded windows; SURVEY.md §8d)",

@@ -115,6 +115,20 @@ def test_launcher_starts_n_ranks():
     assert d == {"world": 2, "gpus": 2, "windows": 9, "in_order": True, "master_addr": "127.0.0.1"}
 
 
+def test_launcher_weak_scaling_default():
+    """Without --windows every rank holds --windows-per-gpu windows of its own (weak scaling): the
+    job total grows with the rank count and the gather still returns every window in order."""
+    import json
+    import subprocess
+    env = dict(os.environ, OKVISGPU_BENCH_DRYRUN="1")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--windows-per-gpu", "5"],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert d == {"world": 2, "gpus": 2, "windows": 10, "in_order": True, "master_addr": "127.0.0.1"}
+
+
 def test_world_size_mismatch_is_an_error():
     import subprocess
     env = dict(os.environ, OKVISGPU_BENCH_DRYRUN="1", WORLD_SIZE="1")
