@@ -333,7 +333,7 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
     sX[(e >> 6) * kLd + (e & 63)] = 0.0;
   }
   if (t < 4) sFl[t] = 0;  // sub-panels factored, trailing updates done, fail, barrier counter
-  __syncthreads();
+  ldsBarrier();
   CLK(4)
   // Sweep with look-ahead: wavefront 0 runs the chain of the 8 sub-panel factorisations and
   // applies each sub-panel's rank-8 update to the next sub-panel's 8 columns itself (VALU, its own
@@ -392,7 +392,7 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
       if (g == 0 && lane == 0) ldsRelease(&sFl[1], s + 1);
     }
   }
-  __syncthreads();
+  ldsBarrier();
   CLK(5)
   if (sFl[2]) return false;
   CLK(6)
@@ -415,7 +415,7 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
     __builtin_amdgcn_wave_barrier();
     sX[(b + 8 + m) * kLd + b + j] = -v;
   }
-  __syncthreads();
+  ldsBarrier();
   CLK(7)
   for (int d = 1; d < 4; ++d) {  // sub-diagonal d: X_ij, i = j + d, wavefront j
     const int j = wave, i = wave + d;
@@ -429,7 +429,7 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
       mfma16<1>(sX + 16 * i * kLd + 16 * i, kLd, Xij, kLd, 1, -1.0, x, lane);
       storeC16(Xij, kLd, x, lane);
     }
-    __syncthreads();
+    ldsBarrier();
   }
   CLK(8)
 #pragma unroll
@@ -440,7 +440,9 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
     *reinterpret_cast<double2*>(Li + r * kTile + c) =
         double2{(c <= r) ? sX[r * kLd + c] : 0.0, (c + 1 <= r) ? sX[r * kLd + c + 1] : 0.0};
   }
-  __syncthreads();
+  // LDS-only barriers from here: the L_kk / X / y stores stay in flight (no reader in this
+  // workgroup before a later full barrier or the end of the launch)
+  ldsBarrier();
   CLK(9)
   {  // y_k = X rhs_k: row t & 63, quarter t >> 6 of the columns, partials through LDS
     const int row = t & 63, qq = t >> 6;
@@ -449,13 +451,13 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
     for (int j = 16 * qq; j < 16 * qq + 16; ++j) y += (j <= row) ? sX[row * kLd + j] * sy[j] : 0.0;
     sA[qq * kTile + row] = y;  // sA is free once L_kk has been stored
   }
-  __syncthreads();
+  ldsBarrier();
   if (t < kTile) {
     const double y = (sA[t] + sA[kTile + t]) + (sA[2 * kTile + t] + sA[3 * kTile + t]);
     sy[t] = y;
     workk[t] = y;
   }
-  __syncthreads();
+  ldsBarrier();
   CLK(10)
   return true;
 }
@@ -468,9 +470,9 @@ __device__ void panelRhsVector(const double* sX, const double* sy, double* sz, d
 #pragma unroll
   for (int r = 16 * q; r < 16 * q + 16; ++r) a += (r >= c) ? sX[r * kLd + c] * sy[r] : 0.0;
   sP[q * kTile + c] = a;
-  __syncthreads();
+  ldsBarrier();
   if (t < kTile) sz[t] = (sP[t] + sP[kTile + t]) + (sP[2 * kTile + t] + sP[3 * kTile + t]);
-  __syncthreads();
+  ldsBarrier();
 }
 
 // L_ik = A_ik X^T (X = L_kk^-1 in sX) stored over A_ik, and rhs_i -= A_ik z (z = X^T y_k in sz),
@@ -478,7 +480,7 @@ __device__ void panelRhsVector(const double* sX, const double* sy, double* sz, d
 __device__ void panelTile(double* Aik, int64_t ld, double* worki, double* sA, const double* sX, const double* sz,
                           int t) {
   loadTile(Aik, ld, 0, 0, sA, t);
-  __syncthreads();
+  ldsBarrier();  // LDS-only: the previous panel's L / rhs stores stay in flight
   dbl4 acc[2][2];
   mfmaTileNT(sA, sX, acc, t);
   {
@@ -490,7 +492,7 @@ __device__ void panelTile(double* Aik, int64_t ld, double* worki, double* sA, co
     a += __shfl_xor(a, 2, 64);
     if (q == 0) gmemw(worki)[row] -= a;
   }
-  __syncthreads();  // sA is free for the next panel
+  ldsBarrier();  // sA is free for the next panel
   storeTile<false>(Aik, ld, 0, 0, acc, t);
 }
 
@@ -650,7 +652,7 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
   for (int k = 0; k < T; ++k) {
     CLK(11)
     if (t < kTile) sy[t] = work[k * kTile + t];
-    __syncthreads();
+    __syncthreads();  // full: the factor and the panels read the tiles the last band update stored
     if (!potrfTile<0>(S + k * kTile * ld + k * kTile, ld, Linv + (int64_t)k * kTile * kTile, work + k * kTile, sA, sX,
                    sy, sRl, sFl, t, false)) {
       if (t == 0) P.st[w].gn_failed = 1;
@@ -661,6 +663,7 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
     panelRhsVector(sX, sy, sy + kTile, sA, t);
     for (int i = k + 1; i < T; ++i)
       if (nz[i * T + k]) panelTile(S + i * kTile * ld + k * kTile, ld, work + i * kTile, sA, sX, sy + kTile, t);
+    __syncthreads();  // full barrier: the band update reads the L_ik just stored
     CLK(1)
     // ---- trailing band update: A_ij -= L_ik L_jk^T, k < j <= i, both tiles non-zero. The A_ij
     // read of the read-modify-write is issued before the MFMAs, so its latency overlaps them.
@@ -670,13 +673,13 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
       for (int j = k + 1; j <= i; ++j) {
         if (!nz[j * T + k]) continue;
         if (j != i) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sX, t);
-        __syncthreads();
+        ldsBarrier();
         double* Cij = S + i * kTile * ld + j * kTile;
         dbl4 c[2][2], acc[2][2];
         loadC(Cij, ld, c, t);
         mfmaTileNT(sA, j == i ? sA : sX, acc, t);
         storeTileSub(Cij, ld, c, acc, t);
-        __syncthreads();
+        ldsBarrier();  // LDS-only: the updated tiles are read from the next step on, after full barriers
       }
     }
   }
@@ -783,20 +786,20 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
         if (mode & 2) sRl[row] = nr;  // rhs_{k+1} for the factor below (sRl is free until then)
       }
     }
-    __syncthreads();  // every wavefront has read A_ik / A_jk
+    ldsBarrier();  // every wavefront has read A_ik / A_jk (LDS-only: the rhs store stays in flight)
     accToLds(sA, li, t);
     if (j != i) accToLds(sB, lj, t);
     double* Cij = S + i * kTile * ld + j * kTile;
     dbl4 c[2][2];
     loadC(Cij, ld, c, t);  // read of the read-modify-write overlaps the barrier and the MFMAs
     if (i == j) storeTile<false>(S + k * kTile * ld + i * kTile, ld, 0, 0, li, t);  // L_ik -> upper slot (k,i)
-    __syncthreads();
+    ldsBarrier();  // no reader of the upper slot in this launch
     dbl4 acc[2][2];
     mfmaTileNT(sA, j == i ? sA : sB, acc, t);
     if (mode & 2) {
       // tile (k+1,k+1): the updated S_dd goes straight to LDS for the factor (its global copy is
       // overwritten by L_dd there), and so does rhs_d
-      __syncthreads();  // every wavefront has read L_ik from sA
+      ldsBarrier();  // every wavefront has read L_ik from sA
       const int wave = t >> 6, lane = t & 63;
       const int r0 = 32 * (wave >> 1), cq = 32 * (wave & 1);
 #pragma unroll
