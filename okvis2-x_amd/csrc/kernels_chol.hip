@@ -462,6 +462,19 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
   return true;
 }
 
+// c - acc (C layout) -> LDS tile [64][kLd]
+__device__ __forceinline__ void accSubToLds(double* s, const dbl4 c[2][2], const dbl4 acc[2][2], int t) {
+  const int wave = t >> 6, lane = t & 63;
+  const int r0 = 32 * (wave >> 1), c0 = 32 * (wave & 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg)
+        s[(r0 + 16 * a + (lane >> 4) + 4 * reg) * kLd + c0 + 16 * b + (lane & 15)] = c[a][b][reg] - acc[a][b][reg];
+}
+
 // z = X^T y_k (X = L_kk^-1 lower in sX, y_k in sy), so that the forward substitution update of
 // every panel is rhs_i -= L_ik y_k = A_ik z. Partials of four row quarters via sP (4 x 64).
 __device__ void panelRhsVector(const double* sX, const double* sy, double* sz, double* sP, int t) {
@@ -649,12 +662,13 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
   CLK_INIT
   for (int e = t; e < ld; e += 256) work[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
   __syncthreads();
+  bool haveDiag = false;  // S_kk (updated by the previous step) already in sA
   for (int k = 0; k < T; ++k) {
     CLK(11)
     if (t < kTile) sy[t] = work[k * kTile + t];
     __syncthreads();  // full: the factor and the panels read the tiles the last band update stored
     if (!potrfTile<0>(S + k * kTile * ld + k * kTile, ld, Linv + (int64_t)k * kTile * kTile, work + k * kTile, sA, sX,
-                   sy, sRl, sFl, t, false)) {
+                   sy, sRl, sFl, t, haveDiag)) {
       if (t == 0) P.st[w].gn_failed = 1;
       return;
     }
@@ -667,18 +681,42 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
     CLK(1)
     // ---- trailing band update: A_ij -= L_ik L_jk^T, k < j <= i, both tiles non-zero. The A_ij
     // read of the read-modify-write is issued before the MFMAs, so its latency overlaps them.
-    for (int i = k + 1; i < T; ++i) {
+    // Block rows from the bottom: the L_jk staged in sX for a lower row is reused as the row
+    // operand when its own row comes (one staging per L tile on a 2-tile band instead of 3), and
+    // the last update, S_(k+1)(k+1), goes to sA for the next factor instead of through global
+    // memory. Independent tiles, the same operations: the same bits in any order.
+    int xHeld = -1;  // block row of the L tile in sX
+    haveDiag = false;
+    for (int i = T - 1; i > k; --i) {
       if (!nz[i * T + k]) continue;
-      loadTile(S + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
+      const bool aInX = xHeld == i;
+      const double* aBuf = aInX ? sX : sA;
+      if (!aInX) loadTile(S + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
       for (int j = k + 1; j <= i; ++j) {
         if (!nz[j * T + k]) continue;
-        if (j != i) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sX, t);
+        const double* bBuf = aBuf;
+        if (j != i) {
+          if (aInX) {
+            loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sA, t);
+            bBuf = sA;
+          } else {
+            if (xHeld != j) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sX, t);
+            xHeld = j;
+            bBuf = sX;
+          }
+        }
         ldsBarrier();
         double* Cij = S + i * kTile * ld + j * kTile;
         dbl4 c[2][2], acc[2][2];
         loadC(Cij, ld, c, t);
-        mfmaTileNT(sA, j == i ? sA : sX, acc, t);
-        storeTileSub(Cij, ld, c, acc, t);
+        mfmaTileNT(aBuf, bBuf, acc, t);
+        if (i == k + 1) {  // (then j == i) the next diagonal tile: c - acc straight into sA
+          ldsBarrier();    // every wavefront has read its operands
+          accSubToLds(sA, c, acc, t);
+          haveDiag = true;  // its global copy is overwritten by L_(k+1)(k+1) there
+        } else {
+          storeTileSub(Cij, ld, c, acc, t);
+        }
         ldsBarrier();  // LDS-only: the updated tiles are read from the next step on, after full barriers
       }
     }
