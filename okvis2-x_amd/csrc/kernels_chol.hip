@@ -190,19 +190,24 @@ __device__ __forceinline__ int ldsAcquire(int* p) {
 __device__ __forceinline__ void ldsRelease(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// Poll interval of the LDS flag waits (s_sleep units of 64 clocks; build knob: 0, 1 and 2 measured
+// within noise of each other at 2,048 windows and on one window).
+#ifndef OKG_WAIT_SLEEP
+#define OKG_WAIT_SLEEP 1
+#endif
 // Wave-uniform wait for *p >= v; false once the factor wavefront reported a failed pivot.
 __device__ __forceinline__ bool waitFlag(int* p, int v, int* fail) {
   for (;;) {
     if (ldsAcquire(p) >= v) return true;
     if (ldsAcquire(fail)) return false;
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(OKG_WAIT_SLEEP);
   }
 }
 // Barrier of n wavefronts on a monotonic arrival counter (gen counts this wavefront's barriers).
 __device__ __forceinline__ void waveBarrier(int* ctr, int& gen, int n, int lane) {
   ++gen;
   if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  while (ldsAcquire(ctr) < gen * n) __builtin_amdgcn_s_sleep(1);
+  while (ldsAcquire(ctr) < gen * n) __builtin_amdgcn_s_sleep(OKG_WAIT_SLEEP);
 }
 
 // One 8-column sub-panel of the in-LDS 64x64 LLT on one wavefront (lane = row i of the tile; the
