@@ -317,7 +317,8 @@ __device__ __forceinline__ void trailing8(double* sA, int c0, int wg, int nw, in
   trailingFrom(sA, c0, c0 + 8, wg, nw, lane);
 }
 
-// Diagonal tile: L_kk (into S, lower), X = L_kk^-1 (into sX and the Linv store) and y_k = X rhs_k
+// Diagonal tile: L_kk (in sA only: every later use of the diagonal goes through X, so L_kk is
+// never stored), X = L_kk^-1 (into sX and the Linv store) and y_k = X rhs_k
 // (sy holds rhs_k on entry, y_k on exit; also written to work). Right-looking LLT in 8-column
 // sub-panels (subPanel8 on wavefront 0, the rank-8 trailing updates on the matrix cores of all 4
 // wavefronts), then X blockwise: the 8x8 diagonal inverses come out of the sub-panels, the 16x16
@@ -440,12 +441,10 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int e = t + 256 * u, r = e >> 5, c = 2 * (e & 31);
-    if (c <= r) Sg[(int64_t)r * ld + c] = sA[r * kLd + c];
-    if (c + 1 <= r) Sg[(int64_t)r * ld + c + 1] = sA[r * kLd + c + 1];
     *reinterpret_cast<double2*>(Li + r * kTile + c) =
         double2{(c <= r) ? sX[r * kLd + c] : 0.0, (c + 1 <= r) ? sX[r * kLd + c + 1] : 0.0};
   }
-  // LDS-only barriers from here: the L_kk / X / y stores stay in flight (no reader in this
+  // LDS-only barriers from here: the X / y stores stay in flight (no reader in this
   // workgroup before a later full barrier or the end of the launch)
   ldsBarrier();
   CLK(9)
@@ -718,7 +717,7 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
         if (i == k + 1) {  // (then j == i) the next diagonal tile: c - acc straight into sA
           ldsBarrier();    // every wavefront has read its operands
           accSubToLds(sA, c, acc, t);
-          haveDiag = true;  // its global copy is overwritten by L_(k+1)(k+1) there
+          haveDiag = true;  // its global copy is stale from here on and never read
         } else {
           storeTileSub(Cij, ld, c, acc, t);
         }
@@ -841,7 +840,7 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
     mfmaTileNT(sA, j == i ? sA : sB, acc, t);
     if (mode & 2) {
       // tile (k+1,k+1): the updated S_dd goes straight to LDS for the factor (its global copy is
-      // overwritten by L_dd there), and so does rhs_d
+      // stale from here on and never read), and so does rhs_d
       ldsBarrier();  // every wavefront has read L_ik from sA
       const int wave = t >> 6, lane = t & 63;
       const int r0 = 32 * (wave >> 1), cq = 32 * (wave & 1);
