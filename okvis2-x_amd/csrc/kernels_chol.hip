@@ -441,8 +441,11 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int e = t + 256 * u, r = e >> 5, c = 2 * (e & 31);
-    *reinterpret_cast<double2*>(Li + r * kTile + c) =
-        double2{(c <= r) ? sX[r * kLd + c] : 0.0, (c + 1 <= r) ? sX[r * kLd + c + 1] : 0.0};
+    // the persistent schedule's backward substitution masks the upper triangle of X (bsDiag), so
+    // it stores the lower one only; the tile-parallel update kernels stage X whole for the MFMAs
+    if (kCaller != 0 || c <= r)
+      *reinterpret_cast<double2*>(Li + r * kTile + c) =
+          double2{(c <= r) ? sX[r * kLd + c] : 0.0, (c + 1 <= r) ? sX[r * kLd + c + 1] : 0.0};
   }
   // LDS-only barriers from here: the X / y stores stay in flight (no reader in this
   // workgroup before a later full barrier or the end of the launch)
