@@ -510,7 +510,7 @@ __device__ void panelTile(double* Aik, int64_t ld, double* worki, double* sA, co
     for (int c = 16 * q; c < 16 * q + 16; ++c) a += sA[row * kLd + c] * sz[c];
     a += __shfl_xor(a, 1, 64);
     a += __shfl_xor(a, 2, 64);
-    if (q == 0) gmemw(worki)[row] -= a;
+    if (q == 0) worki[row] -= a;  // rhs_i in LDS
   }
   ldsBarrier();  // sA is free for the next panel
   storeTile<false>(Aik, ld, 0, 0, acc, t);
@@ -621,11 +621,11 @@ __device__ __forceinline__ void bsList(const uint8_t* nz, int T, int I, int* lst
     if (nz[i * T + I]) lst[1 + n++] = i;
   lst[0] = n;
 }
-// Persistent schedule (256 threads, 4 virtual threads each): y from work (global) into sx, then
+// Persistent schedule (256 threads, 4 virtual threads each): y already in sx (LDS), then
 // the steps with operands loaded in-step. sA: >= 32 x 64 doubles.
-__device__ void backSubstitute(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* work,
-                               const double* Linv, const uint8_t* nz, double* sx, double* sA, double* sy, int t) {
-  for (int e = t; e < ld; e += blockDim.x) sx[e] = work[e];
+__device__ void backSubstitute(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* Linv,
+                               const uint8_t* nz, double* sx, double* sA, double* sy, int t) {
+  // sx already holds y (the persistent kernel keeps the whole forward substitution in LDS)
   __syncthreads();
   constexpr int kV = kBsThreads / 256;
   for (int I = T - 1; I >= 0; --I) {
@@ -667,23 +667,27 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
   const int t = threadIdx.x;
   const int fdim = P.win_fdim[w];
   CLK_INIT
-  for (int e = t; e < ld; e += 256) work[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
+  // rhs / y of the whole window in LDS (sxDyn, ld doubles) for the forward substitution, the
+  // panels' rhs updates and the backward substitution (no global round trip per step)
+  extern __shared__ double sxDyn[];
+  for (int e = t; e < ld; e += 256) sxDyn[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
   __syncthreads();
   bool haveDiag = false;  // S_kk (updated by the previous step) already in sA
   for (int k = 0; k < T; ++k) {
     CLK(11)
-    if (t < kTile) sy[t] = work[k * kTile + t];
+    if (t < kTile) sy[t] = sxDyn[k * kTile + t];
     __syncthreads();  // full: the factor and the panels read the tiles the last band update stored
     if (!potrfTile<0>(S + k * kTile * ld + k * kTile, ld, Linv + (int64_t)k * kTile * kTile, work + k * kTile, sA, sX,
                    sy, sRl, sFl, t, haveDiag)) {
       if (t == 0) P.st[w].gn_failed = 1;
       return;
     }
+    if (t < kTile) sxDyn[k * kTile + t] = sy[t];  // y_k (ordered before its readers by the barriers below)
     CLK(0)
     // ---- panel: L_ik = A_ik X^T, rhs_i -= L_ik y_k = A_ik X^T y_k
     panelRhsVector(sX, sy, sy + kTile, sA, t);
     for (int i = k + 1; i < T; ++i)
-      if (nz[i * T + k]) panelTile(S + i * kTile * ld + k * kTile, ld, work + i * kTile, sA, sX, sy + kTile, t);
+      if (nz[i * T + k]) panelTile(S + i * kTile * ld + k * kTile, ld, sxDyn + i * kTile, sA, sX, sy + kTile, t);
     __syncthreads();  // full barrier: the band update reads the L_ik just stored
     CLK(1)
     // ---- trailing band update: A_ij -= L_ik L_jk^T, k < j <= i, both tiles non-zero. The A_ij
@@ -729,8 +733,7 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
     }
   }
   CLK(2)
-  extern __shared__ double sxDyn[];
-  backSubstitute(P, w, S, ld, T, work, Linv, nz, sxDyn, sA, sy, t);
+  backSubstitute(P, w, S, ld, T, Linv, nz, sxDyn, sA, sy, t);
   CLK(3)
 #ifdef OKG_CHOL_CLOCK
   if (blockIdx.x == 0 && t == 0)
