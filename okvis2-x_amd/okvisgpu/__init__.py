@@ -284,6 +284,27 @@ class SynthWindow:
             pass
 
 
+def imu_append_batch(imu_params, state, t1_old, t1_new, speed_biases, sample_begin, sample_t, sample_ga):
+    """An okvisgpu_imu_append_batch over numpy arrays: (struct, arrays it points into). `state`
+    [n, IMU_STATE_DOUBLES] float64 C-contiguous is referenced, not copied (updated in place)."""
+    n = len(t1_old)
+    keep = [np.ascontiguousarray(t1_old, dtype=np.int64), np.ascontiguousarray(t1_new, dtype=np.int64),
+            np.ascontiguousarray(speed_biases, dtype=np.float64).reshape(n, 9),
+            np.ascontiguousarray(sample_begin, dtype=np.int32), np.ascontiguousarray(sample_t, dtype=np.int64),
+            np.ascontiguousarray(sample_ga, dtype=np.float64).reshape(-1, 6)]
+    assert state.dtype == np.float64 and state.flags["C_CONTIGUOUS"] and state.shape == (n, IMU_STATE_DOUBLES)
+    b = ImuAppendBatch()
+    b.n = n
+    b.imu_params = imu_params
+    b.state = dptr(state)
+    b.t1_old_ns, b.t1_new_ns = keep[0].ctypes.data_as(_lp), keep[1].ctypes.data_as(_lp)
+    b.speed_biases = dptr(keep[2])
+    b.sample_begin = keep[3].ctypes.data_as(_ip)
+    b.sample_t_ns = keep[4].ctypes.data_as(_lp)
+    b.sample_gyr_acc = dptr(keep[5])
+    return b, keep
+
+
 class TwoPoseBatch:
     """Owns the arrays of an okvisgpu_twopose_edges batch (TwoPoseStandardGraphError::compute inputs).
 
@@ -506,22 +527,9 @@ class Context:
     def imu_append(self, imu_params, state, t1_old, t1_new, speed_biases, sample_begin, sample_t, sample_ga):
         """okvisgpu_imu_append (ImuError::append for a batch): `state` [n, IMU_STATE_DOUBLES] is updated
         in place; returns the integrated steps per factor (-1: samples do not reach t1_new)."""
-        n = len(t1_old)
-        keep = [np.ascontiguousarray(t1_old, dtype=np.int64), np.ascontiguousarray(t1_new, dtype=np.int64),
-                np.ascontiguousarray(speed_biases, dtype=np.float64).reshape(n, 9),
-                np.ascontiguousarray(sample_begin, dtype=np.int32), np.ascontiguousarray(sample_t, dtype=np.int64),
-                np.ascontiguousarray(sample_ga, dtype=np.float64).reshape(-1, 6)]
-        assert state.dtype == np.float64 and state.flags["C_CONTIGUOUS"] and state.shape == (n, IMU_STATE_DOUBLES)
-        b = ImuAppendBatch()
-        b.n = n
-        b.imu_params = imu_params
-        b.state = dptr(state)
-        b.t1_old_ns, b.t1_new_ns = keep[0].ctypes.data_as(_lp), keep[1].ctypes.data_as(_lp)
-        b.speed_biases = dptr(keep[2])
-        b.sample_begin = keep[3].ctypes.data_as(_ip)
-        b.sample_t_ns = keep[4].ctypes.data_as(_lp)
-        b.sample_gyr_acc = dptr(keep[5])
-        steps = np.zeros(n, dtype=np.int32)
+        b, keep = imu_append_batch(imu_params, state, t1_old, t1_new, speed_biases, sample_begin, sample_t,
+                                   sample_ga)
+        steps = np.zeros(b.n, dtype=np.int32)
         self._check(lib().okvisgpu_imu_append(self.h, C.byref(b), steps.ctypes.data_as(_ip)), "okvisgpu_imu_append")
         return steps
 

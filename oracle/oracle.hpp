@@ -135,6 +135,8 @@ int oracle_eval_relpose(const okvisgpu_problem* p, double* r, double* J /*[n][6]
 int oracle_imu_merge(const okvisgpu_problem* p, int32_t f, const double* sb, double* state_out);
 int oracle_twopose_compute(const okvisgpu_twopose_edges* E, double* delta_x, double* sqrt_info, double* lin_point,
                            double* H00, double* b0);
+/* okvisgpu_imu_append on the CPU: same batch, same in/out state layout, steps[n] (-1 untouched). */
+int oracle_imu_append(const okvisgpu_imu_append_batch* b, int32_t* steps);
 int oracle_project(const okvisgpu_camera* cam, const double* hp4, double* kp2, double* J24);
 void oracle_pose_plus(const double* x, const double* delta, double* out);
 void oracle_pose_plus_jacobian(const double* x, double* J76);

@@ -1202,6 +1202,38 @@ int oracle_imu_merge(const okvisgpu_problem* p, int32_t f, const double* sb, dou
   return steps;
 }
 
+// okvisgpu_imu_append semantics on the CPU (ImuError::append, ImuError.cpp:63-255, for a batch):
+// every factor continues from its stored state (t1 = t1_old) over the given samples to t1_new with
+// the eliminated state's speed/bias; -1 leaves the state untouched.
+int oracle_imu_append(const okvisgpu_imu_append_batch* b, int32_t* steps) {
+  if (!b || b->n < 0 || (b->n > 0 && (!b->state || !b->sample_begin || !b->speed_biases))) return -2;
+  for (int f = 0; f < b->n; ++f) {
+    oracle::ImuError e;
+    e.params = b->imu_params;
+    double* st = b->state + (size_t)f * OKVISGPU_IMU_STATE_DOUBLES;
+    e.loadState(st);
+    std::vector<oracle::ImuSample> m;
+    for (int s = b->sample_begin[f]; s < b->sample_begin[f + 1]; ++s) {
+      oracle::ImuSample x;
+      x.t = b->sample_t_ns[s];
+      for (int k = 0; k < 3; ++k) {
+        x.g[k] = b->sample_gyr_acc[6 * s + k];
+        x.a[k] = b->sample_gyr_acc[6 * s + 3 + k];
+      }
+      m.push_back(x);
+    }
+    int n = -1;
+    if (!m.empty()) {
+      e.meas.push_back(m.front());  // the link's own samples only feed the merged deque
+      e.t1 = b->t1_old_ns[f];
+      n = e.append(&b->speed_biases[9 * f], m, b->t1_new_ns[f]);
+      if (n >= 0) e.storeState(st);
+    }
+    if (steps) steps[f] = n;
+  }
+  return OKVISGPU_OK;
+}
+
 int oracle_eval_imu(const okvisgpu_problem* p, int32_t redo_always, double* r, double* J) {
   Program P;
   buildProgram(p, P, true);

@@ -38,6 +38,7 @@ def lib():
         L.oracle_eval_relpose.argtypes = [P, _dp, _dp]
         L.oracle_imu_merge.argtypes = [P, C.c_int32, _dp, _dp]
         L.oracle_twopose_compute.argtypes = [C.POINTER(og.TwoPoseEdges), _dp, _dp, _dp, _dp, _dp]
+        L.oracle_imu_append.argtypes = [C.POINTER(og.ImuAppendBatch), _ip]
         _lib = L
     return _lib
 
@@ -103,6 +104,15 @@ def twopose_compute(batch):
                                       og.dptr(out["lin_point"]), og.dptr(out["H00"]), og.dptr(out["b0"]))
     assert rc == 0
     return out
+
+
+def imu_append(imu_params, state, t1_old, t1_new, speed_biases, sample_begin, sample_t, sample_ga):
+    """okvisgpu_imu_append semantics on the CPU (state updated in place; steps, -1 = untouched)."""
+    b, keep = og.imu_append_batch(imu_params, state, t1_old, t1_new, speed_biases, sample_begin, sample_t, sample_ga)
+    steps = np.zeros(b.n, dtype=np.int32)
+    rc = lib().oracle_imu_append(C.byref(b), steps.ctypes.data_as(_ip))
+    assert rc == 0
+    return steps
 
 
 def imu_merge(problem_ptr, f, sb):

@@ -87,6 +87,62 @@ def test_final_ba_size_500kf(og, oracle, gpu_ctx):
     _solve_both(og, oracle, gpu_ctx, w, _zero_tol(og, 2, num_threads=8), rel=1e-6)
 
 
+def test_final_ba_hilti_500kf(og, oracle, gpu_ctx):
+    """BASELINE config 4 as okvis runs it (ViSlamBackend::doFinalBa, ViSlamBackend.cpp:2005-2164) on a
+    Hilti-shaped 500-keyframe graph: equidistant cameras (config/hilti22), both extrinsics variable
+    with their PoseError priors (do_extrinsics: true, config/hilti22/okvis2.yaml:82-83), everything
+    unfrozen (:2026-2033), redoPropagationAlways (:2036), SPARSE_NORMAL_CHOLESKY (ViGraph.cpp:248),
+    and the pass sequence of optimiseFullGraph twice (:2041,2059; :1971-2003):
+      1a  loop-closure RelativePoseErrors (keyframes 460.. back to 0..; 100 x information,
+          :1985-1986) with function_tolerance 1e-3 for numIter/3 iterations (:1988-1989);
+      1b  constraints removed, function_tolerance 1e-6 (:1990-1997);
+      2   speed/bias prior removed (:2044), extrinsics soft-constrained at their estimate (:2050-2052),
+          optimiseFullGraph again (:2059).
+    Iteration counts are cut (3 / 3 / 3 instead of 33 / 100 / 100) so the oracle finishes in
+    seconds; GPU and oracle each carry their own estimates (and IMU states) from pass to pass."""
+    from _problem import OwnedProblem
+    from test_gpu_parity import CAMERA_MODELS, _switch_camera_model
+    w = og.SynthWindow(500, 20000, 160000, seed=48, n_relpose=30, relpose_stride=460, relpose_kind=1,
+                       do_extrinsics=1)
+    _switch_camera_model(oracle, w, *CAMERA_MODELS["equidistant"])
+    q = OwnedProblem.copy_of(w.problem)
+    assert q.relpose_blocks[:, 1].min() - q.relpose_blocks[:, 0].max() >= 400 and np.all(q.extrinsics_constant == 0)
+    q.relpose_sqrt_info *= 10.0                        # 100 x information
+    q.bind()
+    gpu, cpu = q, OwnedProblem.copy_of(q.struct)
+    base = dict(linear_solver=og.SPARSE_NORMAL_CHOLESKY, redo_propagation_always=1, num_threads=16,
+                gradient_tolerance=1e-10, parameter_tolerance=1e-8)
+    passes = [("1a", dict(max_num_iterations=3, function_tolerance=1e-3)),
+              ("1b", dict(max_num_iterations=3, function_tolerance=1e-6)),
+              ("2", dict(max_num_iterations=3, function_tolerance=1e-6))]
+    for name, kw in passes:
+        if name == "1b":
+            for p in (gpu, cpu):                       # removeRelativePoseConstraint
+                p.relpose_blocks, p.relpose_delta_x = p.relpose_blocks[:0], p.relpose_delta_x[:0]
+                p.relpose_sqrt_info, p.relpose_lin_point = p.relpose_sqrt_info[:0], p.relpose_lin_point[:0]
+                p.relpose_kind = p.relpose_kind[:0]
+                p.bind()
+        if name == "2":
+            for p in (gpu, cpu):                       # removeSpeedAndBiasPrior + softConstrainExtrinsics
+                p.sb_prior_block, p.sb_prior_meas, p.sb_prior_sqrt_info = (
+                    p.sb_prior_block[:0], p.sb_prior_meas[:0], p.sb_prior_sqrt_info[:0])
+                p.extrinsics_prior_meas = p.extrinsics.copy()
+                p.extrinsics_prior_sqrt_info = np.tile(np.diag([100.0] * 6).reshape(-1), (len(p.extrinsics), 1))
+                p.bind()
+        opts = og.default_options(**base, **kw)
+        gpu_ctx.set_problems([gpu.struct])
+        sg = gpu_ctx.solve(opts)[0]
+        so = oracle.solve(cpu.ptr(), opts)
+        _close(sg, so, rel=1e-7)
+        assert sg["num_successful_steps"] == so["num_successful_steps"], (name, sg, so)
+        dp = np.abs(gpu.poses[:, :3] - cpu.poses[:, :3]).max()
+        de = np.abs(gpu.extrinsics[:, :3] - cpu.extrinsics[:, :3]).max()
+        print(f"final BA pass {name}: {sg['num_iterations']} it, {sg['termination']}, cost {sg['final_cost']:.10g} "
+              f"(rel {abs(sg['final_cost'] - so['final_cost']) / so['final_cost']:.2e}), max pose dev {dp:.2e} m, "
+              f"extrinsics dev {de:.2e} m")
+        assert dp <= 1e-6 and de <= 1e-6, (name, dp, de)
+
+
 def test_equidistant_s50(og, oracle, gpu_ctx):
     """S50 with the Hilti camera model (EquidistantDistortion, config/hilti22)."""
     from test_gpu_parity import CAMERA_MODELS, _switch_camera_model

@@ -1,0 +1,109 @@
+"""The okvis realtime sliding-window SEQUENCE (BASELINE config 3's shape, synthetic): one realtime
+solve per frame, then the marginalisation strategy -- IMU-merge elimination of non-keyframes
+(okvisgpu_imu_append), conversion of the least-covisible keyframe into pose-graph edges
+(okvisgpu_twopose_compute), freezing of old states -- chained over 28 frames
+(okvisgpu.sliding_window; ViSlamBackend.cpp:555-1010, ViGraphEstimator.cpp:38-171,216-298,334-610).
+
+CPU: the sequence on the oracle backend exercises every strategy branch and tracks the ground truth.
+GPU: the same sequence on okvisgpu and on the oracle, each carrying its own estimates from frame to
+frame: every frame's solve must take the same iterations / termination / successful steps, with
+poses, landmarks, IMU preintegration and the created edges agreeing (tolerances below)."""
+import numpy as np
+import pytest
+
+from okvisgpu.sliding_window import GpuBackend, SlidingWindow, World
+from _sequence import OracleBackend
+
+N_FRAMES = 30
+# shortened freeze horizon (reference: 12 pose-graph frames, 2 s) so that freezing starts inside
+# the 30-frame sequence; the structure of the strategy is unchanged
+STRATEGY = dict(num_keyframes=5, num_imu_frames=3, num_realtime_pose_graph_frames=4, min_delta_t=0.5)
+
+
+def _run(world, backend, n=N_FRAMES, on_step=None):
+    sw = SlidingWindow(world, backend, **STRATEGY)
+    sums = []
+    for k in range(n):
+        if k < 2:
+            sw.add_frame(k)
+            continue
+        sums.append(sw.step(k))
+        if on_step:
+            on_step(k, sw)
+    return sw, sums
+
+
+@pytest.fixture(scope="module")
+def world(og):
+    return World(N_FRAMES, 900, 7200, seed=20251101)
+
+
+def test_oracle_sequence_strategy(world):
+    """Every branch of the strategy runs: IMU merges of every non-keyframe, keyframe conversion with
+    MST edges (incl. a second edge from one conversion), freezing; the window stays bounded and the
+    estimate tracks the ground truth."""
+    sw, sums = _run(world, OracleBackend())
+    kinds = [e[0] for e in sw.log]
+    assert kinds.count("imu_merge") >= 12
+    assert kinds.count("to_pose_graph") >= 8 and kinds.count("edge") >= 9 and kinds.count("freeze") >= 3
+    assert all(np.isfinite(s["final_cost"]) for s in sums)
+    assert max(s["n_free_poses"] for s in sums) <= 14
+    ids = sw.ids()
+    P = np.array([sw.states[i].pose[:3] for i in ids])
+    assert np.abs(P - world.gt_poses[ids, :3]).max() < 0.1
+    # non-keyframes are gone, keyframes remain (as keyframes, pose-graph or frozen frames)
+    assert all(i % 2 == 0 for i in ids[:-STRATEGY["num_imu_frames"]])
+
+
+@pytest.mark.gpu
+def test_gpu_sequence_matches_oracle(og, world):
+    """28 chained realtime solves + strategy, okvisgpu vs the oracle, each on its own estimates."""
+    ref_states = {}
+
+    def keep(k, sw):
+        ref_states[k] = ({i: (s.pose.copy(), s.sb.copy()) for i, s in sw.states.items()},
+                         {l: v.copy() for l, v in sw.landmarks.items()},
+                         {e: (v.delta_x.copy(), v.sqrt_info.copy(), v.lin_point.copy()) for e, v in sw.edges.items()},
+                         {l: v.state.copy() for l, v in sw.links.items()})
+
+    cpu, cpu_sums = _run(world, OracleBackend(), on_step=keep)
+    gpu_backend = GpuBackend(0)
+    worst = {"pose": 0.0, "lm": 0.0, "cost": 0.0, "edge_info": 0.0, "imu_info": 0.0}
+
+    def check(k, sw):
+        states, lms, edges, links = ref_states[k]
+        assert sorted(states) == sw.ids() and sorted(edges) == sorted(sw.edges)
+        dp = max(np.abs(sw.states[i].pose[:3] - states[i][0][:3]).max() for i in states)
+        worst["pose"] = max(worst["pose"], dp)
+        assert dp <= 1e-6, (k, dp)
+        # landmarks with observable depth (information-weighted check left to the per-window tests)
+        dl = np.array([np.abs(sw.landmarks[l][:3] - lms[l][:3]).max() for l in lms])
+        near = np.array([np.linalg.norm(lms[l][:3] - sw.states[sw.ids()[-1]].pose[:3]) < 25 for l in lms])
+        worst["lm"] = max(worst["lm"], float(dl[near].max()) if near.any() else 0.0)
+        assert dl[near].max() <= 1e-5, (k, dl[near].max())
+        for e, (dx, J, lin) in edges.items():
+            g = sw.edges[e]
+            Ig, Ic = g.sqrt_info.T @ g.sqrt_info, J.T @ J
+            rel = np.abs(Ig - Ic).max() / np.abs(Ic).max()
+            worst["edge_info"] = max(worst["edge_info"], rel)
+            assert rel <= 1e-6, (k, e, rel)
+            assert np.abs(g.lin_point - lin).max() <= 1e-6
+        for l, st in links.items():
+            Ug, Uc = sw.links[l].state[66:291].reshape(15, 15), st[66:291].reshape(15, 15)
+            Ig, Ic = Ug.T @ Ug, Uc.T @ Uc
+            rel = np.abs(Ig - Ic).max() / np.abs(Ic).max()
+            worst["imu_info"] = max(worst["imu_info"], rel)
+            assert rel <= 1e-6, (k, l, rel)
+
+    try:
+        gpu, gpu_sums = _run(world, gpu_backend, on_step=check)
+    finally:
+        gpu_backend.close()
+    assert gpu.log == cpu.log
+    for k, (g, c) in enumerate(zip(gpu_sums, cpu_sums)):
+        assert (g["num_iterations"], g["termination"], g["num_successful_steps"]) == \
+            (c["num_iterations"], c["termination"], c["num_successful_steps"]), (k, g, c)
+        rel = abs(g["final_cost"] - c["final_cost"]) / c["final_cost"]
+        worst["cost"] = max(worst["cost"], rel)
+        assert rel <= 1e-7, (k, rel)
+    print(f"sequence of {len(gpu_sums)} solves: worst GPU-vs-oracle deviations {worst}")
