@@ -6,10 +6,11 @@ A step = one trust-region iteration (Ceres semantics: linearise + Schur-reduce +
 candidate evaluation + accept/reject) of EVERY window in the job's batch of independent synthetic
 S50 windows (50 keyframes, 2,000 landmarks, 16,000 reprojections, 49 IMU factors).
 value = (windows x timed iterations) / wall time of the timed region, max over ranks
-(window-iterations per second, whole job). Weak scaling: every rank solves its own batch of
---windows-per-gpu independent windows (2,048 by default, distinct seeds across ranks; one process
-per GPU, no data-path collective). --windows T fixes the job total instead (strong
-scaling, T split across ranks). At the end of the
+(window-iterations per second, whole job). Strong scaling (BASELINE.json north_star: ">=6x strong
+scaling at 8 GPUs on batched independent windows"): the job is a fixed batch of --windows
+independent windows (2,048 by default) split across the ranks, one process per GPU and no
+data-path collective. --windows-per-gpu W instead gives every rank its own W
+windows (weak scaling, distinct seeds across ranks). At the end of the
 run the per-window summaries and final poses are all-gathered to rank 0 over RCCL (§8e), outside
 the timed region, and rank 0 checks that every window of the job ran every iteration.
 
@@ -43,6 +44,7 @@ sys.path.insert(0, os.path.join(REPO, "okvis2-x_amd"))
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X FP64 matrix (spec; SURVEY.md §8d, not in the gfx950 guide)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 SEED0 = 20251015
+DEFAULT_WINDOWS = 2048         # the job's fixed batch of independent S50 windows (strong scaling)
 METRIC = "Gauss-Newton iters/sec on 50-KF/2000-landmark window; ATE vs CPU ref"
 
 CONFIGS = {
@@ -125,12 +127,17 @@ def rank_windows(total, world, rank):
 
 
 def job_windows(args, world):
-    """Resolve the job's window count: --windows fixes the total (strong scaling), else every rank
-    holds --windows-per-gpu windows (weak scaling). Returns True for strong scaling."""
-    strong = args.windows is not None
-    if not strong:
+    """Resolve the job's window count: --windows-per-gpu gives every rank its own batch (weak
+    scaling), else the job is --windows windows split across the ranks (strong scaling, the
+    default). Returns True for strong scaling."""
+    if args.windows_per_gpu is not None:
+        if args.windows is not None:
+            raise SystemExit("bench.py: --windows and --windows-per-gpu are exclusive")
         args.windows = args.windows_per_gpu * world
-    return strong
+        return False
+    if args.windows is None:
+        args.windows = DEFAULT_WINDOWS
+    return True
 
 
 def aggregate(dist, elapsed, early, device):
@@ -262,8 +269,9 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--windows-per-gpu", type=int, default=2048, help="windows per rank (weak scaling, default)")
-    ap.add_argument("--windows", type=int, default=None, help="fixed job total split across ranks (strong scaling)")
+    ap.add_argument("--windows", type=int, default=None,
+                    help=f"job total split across ranks (strong scaling, default {DEFAULT_WINDOWS})")
+    ap.add_argument("--windows-per-gpu", type=int, default=None, help="windows per rank instead (weak scaling)")
     ap.add_argument("--config", default="s50", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-threads", type=int, default=3, help="realtime_num_threads (okvis2.yaml:93)")
     ap.add_argument("--cpu-iters", type=int, default=None, help="default: warmup + steps")

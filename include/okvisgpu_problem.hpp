@@ -418,8 +418,19 @@ class Problem {
     if ((index = indexIn(poseIdx_, v)) >= 0) kind = 0;
     else if ((index = indexIn(sbIdx_, v)) >= 0) kind = 1;
     else if ((index = indexIn(lmIdx_, v)) >= 0) kind = 2;
+    else if ((index = extrinsicsCamera(v)) >= 0) kind = 3;  // ViSlamBackend.cpp:866-872 freeze
     if (kind < 0 || dirty_ || !uploaded_) dirty_ = true;  // structure rebuilt at the next Solve anyway
     else constDirty_[{kind, index}] = c ? 1 : 0;
+  }
+  // The ABI camera of an extrinsics block (-1: none, or shared by several cameras).
+  int extrinsicsCamera(const double* v) const {
+    int ci = -1;
+    for (size_t i = 0; i < extrPtr_.size(); ++i)
+      if (extrPtr_[i] == v) {
+        if (ci >= 0) return -1;
+        ci = (int)i;
+      }
+    return ci;
   }
   int ensureContext() {
     if (ctx_) return OKVISGPU_OK;
@@ -528,7 +539,13 @@ class Problem {
         A_.rp_kind.push_back(1);
       }
     }
-    // cameras / extrinsics (one ABI camera per distinct (extrinsics block, intrinsics) pair)
+    // cameras / extrinsics (one ABI camera per distinct (extrinsics block, intrinsics) pair). A
+    // variable extrinsics block is ONE Ceres block: seen with two intrinsics it would become two
+    // independently optimised ABI blocks, so that graph is rejected.
+    for (size_t i = 0; i < cams.size(); ++i)
+      for (size_t j = 0; j < i; ++j)
+        if (cams[i].extr == cams[j].extr && !params_[cams[i].extr].constant)
+          throw Unsupported("a variable extrinsics block observed with two different camera intrinsics");
     extrPtr_.clear();
     for (const Cam& c : cams) {
       A_.cams.push_back(c.cam);

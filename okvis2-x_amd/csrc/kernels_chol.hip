@@ -319,7 +319,9 @@ __device__ __forceinline__ void trailing8(double* sA, int c0, int wg, int nw, in
 
 // Diagonal tile: L_kk (in sA only: every later use of the diagonal goes through X, so L_kk is
 // never stored), X = L_kk^-1 (into sX and the Linv store) and y_k = X rhs_k
-// (sy holds rhs_k on entry, y_k on exit; also written to work). Right-looking LLT in 8-column
+// (sy holds rhs_k on entry, y_k on exit; the tile-parallel callers also write it to workk, the
+// forward-substitution vector in global memory; the persistent kernel keeps y in LDS and passes
+// no workk). Right-looking LLT in 8-column
 // sub-panels (subPanel8 on wavefront 0, the rank-8 trailing updates on the matrix cores of all 4
 // wavefronts), then X blockwise: the 8x8 diagonal inverses come out of the sub-panels, the 16x16
 // diagonal blocks are completed with X21 = -X22 L21 X11 (one wavefront each), and
@@ -462,7 +464,7 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
   if (t < kTile) {
     const double y = (sA[t] + sA[kTile + t]) + (sA[2 * kTile + t] + sA[3 * kTile + t]);
     sy[t] = y;
-    workk[t] = y;
+    if (kCaller != 0) workk[t] = y;
   }
   ldsBarrier();
   CLK(10)
@@ -656,7 +658,6 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
   const int64_t ld = P.win_fpad[w];
   const int T = (int)(ld / kTile);
   double* S = P.S + P.win_soff[w];
-  double* work = P.fwdF + P.win_fwdoff[w];
   double* Linv = P.Linv + P.win_linvoff[w];
   const uint8_t* nz = P.tile_nz + P.win_tnzoff[w];
   __shared__ double sA[kTile * kLd];
@@ -677,7 +678,7 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
     CLK(11)
     if (t < kTile) sy[t] = sxDyn[k * kTile + t];
     __syncthreads();  // full: the factor and the panels read the tiles the last band update stored
-    if (!potrfTile<0>(S + k * kTile * ld + k * kTile, ld, Linv + (int64_t)k * kTile * kTile, work + k * kTile, sA, sX,
+    if (!potrfTile<0>(S + k * kTile * ld + k * kTile, ld, Linv + (int64_t)k * kTile * kTile, nullptr, sA, sX,
                    sy, sRl, sFl, t, haveDiag)) {
       if (t == 0) P.st[w].gn_failed = 1;
       return;
@@ -1402,6 +1403,12 @@ bool cholesky_ws_fits(int max_fpad, size_t lds_per_block) {
   hipFuncAttributes attr;
   if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky_ws)) != hipSuccess) return false;
   return attr.sharedSizeBytes + 2 * sizeof(double) * (size_t)max_fpad <= lds_per_block;
+}
+
+bool cholesky_persistent_fits(int max_fpad, size_t lds_per_block) {
+  hipFuncAttributes attr;
+  if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky)) != hipSuccess) return false;
+  return attr.sharedSizeBytes + sizeof(double) * (size_t)max_fpad <= lds_per_block;
 }
 
 void launch_cholesky(const DevProblem& P, hipStream_t s) {

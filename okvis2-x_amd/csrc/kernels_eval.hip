@@ -178,8 +178,19 @@ __device__ void loadPre(const double* s, ImuPre& p) {
 // reference's clamp exactly.
 constexpr int kImuGroup = 16;
 constexpr int kImuPerWG = 4;
-constexpr int kStepRec = 32;  // dt | dq (4) | a_true (3) | Jr (9) | R(dq)^T (9) | noise (5) | pad
-constexpr int kImuChunk = 8;  // step records formed per chunk (lanes 0..7), staged in the group's sA
+constexpr int kStepRec = 26;  // dt | dq (4) | a_true (3) | Jr (9) | R(dq)^T (9)
+constexpr int kImuK = 4;      // integration steps per chunk
+constexpr int kFStride = 64;  // F_delta blocks of one step (offsets below) | dt
+// per-group LDS (doubles) during the chain: step records, Delta_q and cross_ after each step (slot
+// 0 = before the chunk), C_1 Jr, C + C_1, (C + C_1) a, X, F_delta, noise; the P exchange (15 x 16)
+// reuses the first 240. After the chain: P / U (sA, 256), L / eigenvectors (sB, 256), Jacobi
+// rotations (sR, 64).
+constexpr int kLRec = 0, kLQ1 = kLRec + kImuK * kStepRec, kLCr = kLQ1 + 4 * (kImuK + 1),
+              kLCj = kLCr + 9 * (kImuK + 1), kLM = 0, kLCc = 240, kLCa = kLCc + 9 * kImuK, kLXx = kLCa + 3 * kImuK,
+              kLF = kLXx + 9 * kImuK, kLNz = kLF + kFStride * kImuK, kLCarry = kLNz + 5 * kImuK,
+              kImuLds = kLCarry + 13;
+static_assert(kLCj + 9 * kImuK <= kLCc && 15 * 16 <= kLCc, "chain records / P exchange overlap the sums");
+static_assert(kImuLds >= 2 * 256 + 64, "the square-root phase needs sA, sB and sR");
 
 // F_delta (ImuError.cpp:395-410) of one step in LDS: non-identity 3x3 blocks
 constexpr int kF03 = 0, kF09 = 9, kF012 = 18, kF39 = 27, kF63 = 36, kF69 = 45, kF612 = 54, kFdt = 63;
@@ -339,16 +350,14 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   const int f = blockIdx.x * kImuPerWG + g;
   ICLK_INIT
 
-  // per-group LDS: sA = step records of a chunk during the chain, then symmetric P / Jacobi
-  // matrix / U (row-major 16x16); sB = transpose exchange / L (column-major) / Jacobi eigenvectors;
-  // sF = F_delta during the chain, then the Jacobi rotations (sR). 18 KB per workgroup, so LDS
-  // admits two workgroups (waves) per SIMD.
-  __shared__ double sAll[kImuPerWG][2 * 256 + 64];
-  static_assert(kImuChunk * kStepRec <= 256, "a chunk's step records must fit the group's sA");
-  double* sA = sAll[g];
-  double* sB = sAll[g] + 256;
-  double* sF = sAll[g] + 512;
-  double* sR = sF;
+  // per-group LDS: the chain's records (layout at kLRec..kLNz above), then symmetric P / Jacobi
+  // matrix / U (sA, row-major 16x16); L (column-major) / Jacobi eigenvectors (sB); Jacobi rotations
+  // (sR). 19 KB per workgroup: two workgroups (waves) per SIMD.
+  __shared__ double sAll[kImuPerWG][kImuLds];
+  double* sG = sAll[g];
+  double* sA = sG;
+  double* sB = sG + 256;
+  double* sR = sG + 512;
 
   // The factor's record, the head of its stored state and the window state are loaded in two
   // rounds (clamped index) and consumed at one point before any test, so that no load waits behind
@@ -374,12 +383,10 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
     sX = gst->xcur;
     sL = gst->lcur;
   }
-  const auto parp = gmem(P.imu_par + 7 * wR);
-  const double a_max = parp[0], g_max = parp[1], sg_c = parp[2], sa_c = parp[3], sgw_c = parp[4], saw_c = parp[5],
-               gmag = parp[6];
+  const auto parp = gmem(P.imu_par + 7 * wR);  // (read where needed: nothing held across the chain)
   const int64_t tsLast = gmem(P.imu_ts)[max(send - 1, 0)];
   asm volatile("" ::"v"(flR), "v"(blkR.y), "v"(t0), "v"(t1), "v"(st0), "v"(st1), "v"(bref[0]), "v"(bref[5]),
-               "v"(sDone), "v"(sCand), "v"(sX), "v"(sL), "v"(a_max), "v"(gmag), "v"(tsLast));
+               "v"(sDone), "v"(sCand), "v"(sX), "v"(sL), "v"(tsLast));
   const bool live = inR && (APPEND || ((sDone == 0) & (mode != 1 || sCand != 0) & !((flR & 2) && mode < 2)));
   const int w = APPEND ? 0 : wR;
   const int xs = APPEND ? 0 : (mode == 1 ? 1 - sX : sX), lb = APPEND ? 0 : (mode == 1 ? 1 - sL : sL);
@@ -392,75 +399,101 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   // ---- re-preintegration decision (ImuError.cpp:833-859)
   int redoCounter = (int)st0;
   bool redo = st1 != 0.0;
-  double Db[6];
-  for (int k = 0; k < 6; ++k) Db[k] = sb0[3 + k] - bref[k];
-  redo = redo || (sqrt(Db[0] * Db[0] + Db[1] * Db[1] + Db[2] * Db[2]) > 0.0003);
+  {
+    const double d0 = sb0[3] - bref[0], d1 = sb0[4] - bref[1], d2 = sb0[5] - bref[2];
+    redo = redo || (sqrt(d0 * d0 + d1 * d1 + d2 * d2) > 0.0003);
+  }
   const bool doRedo =
       APPEND || (redo && ((send - sbeg) < 50 || P.opt.redo_propagation_always)) || redoCounter == 0;
   // redoPreintegration returns -1 before touching any state when the samples do not cover t1
   // (ImuError.cpp:270-273): the old preintegration is kept.
   const bool covered = (send > sbeg) && tsLast >= t1;
   const bool integrate = live && doRedo && covered;
-  if (live && doRedo && !APPEND) {
+  const bool resetDb = live && doRedo && !APPEND;  // Delta_b is zero after a redo (ImuError.cpp:855)
+  if (resetDb) {
     redoCounter++;
-    for (int k = 0; k < 6; ++k) Db[k] = 0.0;
     redo = false;
   }
 
-  // chain state needed by every step (replicated across the group); the pure accumulators
-  // C_dint, acc_dint, dalpha_db_g, dp_db_g are distributed: lane e < 9 holds component e.
-  Q cdq{0, 0, 0, 1};
-  double cCi[9], cai[3], cdvdbg[9], cross[9];
-  double aCdi = 0.0, aadi = 0.0, adadbg = 0.0, adpdbg = 0.0;
-  for (int i = 0; i < 9; ++i) { cCi[i] = 0; cdvdbg[i] = 0; cross[i] = 0; }
-  for (int i = 0; i < 3; ++i) cai[i] = 0;
+  // Chain ownership (phase-split integration, below): the quaternion / cross_ chain is carried in
+  // every lane's registers (lane 0 stores it); the pure accumulators are distributed: lane e < 9
+  // owns component e of C_integral (aCi), C_doubleintegral (aCdi), dalpha_db_g, dv_db_g and
+  // dp_db_g, lanes 9..11 own acc_integral (aCi) and acc_doubleintegral (aCdi) component e - 9;
+  // lane l < 15 owns column l of P.
+  double aCi = 0.0, aCdi = 0.0, adadbg = 0.0, advdbg = 0.0, adpdbg = 0.0;
   double Pc[15];  // column l of P
   for (int i = 0; i < 15; ++i) Pc[i] = 0.0;
   int steps = 0;
+  double* const carry = sG + kLCarry;  // Delta_q (4) | cross_ (9) between chunks
+  if (l == 0) {
+    carry[0] = 0.0; carry[1] = 0.0; carry[2] = 0.0; carry[3] = 1.0;
+    for (int i = 0; i < 9; ++i) carry[4 + i] = 0.0;
+  }
   if (APPEND && integrate) {  // continue the chain of the stored preintegration
-    cdq = Q{state[2], state[3], state[4], state[5]};
-    for (int i = 0; i < 9; ++i) {
-      cCi[i] = state[6 + i];
-      cdvdbg[i] = state[39 + i];
-      cross[i] = state[292 + i];
-    }
-    for (int i = 0; i < 3; ++i) cai[i] = state[24 + i];
+    if (l == 0)
+      for (int i = 0; i < 4; ++i) carry[i] = state[2 + i];
+    if (l == 0)
+      for (int i = 0; i < 9; ++i) carry[4 + i] = state[292 + i];
     if (l < 9) {
+      aCi = state[6 + l];
       aCdi = state[15 + l];
       adadbg = state[30 + l];
+      advdbg = state[39 + l];
       adpdbg = state[48 + l];
+    } else if (l < 12) {
+      aCi = state[24 + l - 9];
+      aCdi = state[27 + l - 9];
     }
-    if (l < 3) aadi = state[27 + l];
     if (l < 15)
       for (int i = 0; i < 15; ++i) Pc[i] = state[301 + i * 15 + l];
   }
 
   ICLK(0)
-  // ---- redoPreintegration (ImuError.cpp:258-466), uniform trip count over the wavefront.
-  // What a step needs that does not depend on the integration chain (its length, the interpolated
-  // samples, dq = exp(w dt), the right Jacobian of w dt, R(dq)^T, the noise terms) is formed for 16
-  // steps at a time, one step per lane, and staged in LDS; the sequential chain only does products.
-  // The integration time before step `it` is t0 for the first sample and max(t0, min(ts[it], t1))
-  // after it: where the previous step ended, or unchanged when that step was skipped for dt <= 0
-  // (ImuError.cpp:339). Steps after the one that reaches t1 then have dt = 0 as well.
+  // ---- redoPreintegration (ImuError.cpp:258-466), uniform trip count over the wavefront, in
+  // chunks of kImuK steps and five phases per chunk, so that no phase holds more than its own
+  // working set in registers (the single-pass form carried ~140 live doubles per lane and spilled):
+  //  R  (lane k, parallel)  step record: dt, interpolated samples, dq = exp(w dt), Jr(w dt),
+  //                         R(dq)^T, the noise of the step. The integration time before step `it`
+  //                         is t0 for the first sample and max(t0, min(ts[it], t1)) after it: where
+  //                         the previous step ended, or unchanged when that step was skipped for
+  //                         dt <= 0 (ImuError.cpp:339); steps after the one reaching t1 get dt = 0.
+  //  Q  (sequential)        Delta_q <- Delta_q dq and cross_ <- R(dq)^T cross_ + Jr dt, the only
+  //                         products on the chain (ImuError.cpp:352-392), stored per step;
+  //  I  (lane k, parallel)  C, C_1, C + C_1, (C + C_1) a, C_1 Jr, X (ImuError.cpp:360-392) and the
+  //                         F_delta blocks that need no running sum;
+  //  S  (lane = component)  the running sums (C_integral, acc_integral, their double integrals,
+  //                         dalpha/dv/dp_db_g) and the F_delta blocks that read them (:395-410);
+  //  P  (lane = column)     P <- F P F^T + Q (ImuError.cpp:412-426).
   {
-    const double bg[3] = {sb0[3], sb0[4], sb0[5]}, ba[3] = {sb0[6], sb0[7], sb0[8]};
     const int N = integrate ? send - sbeg : 0;
     int Nmax = N;
     Nmax = max(Nmax, __shfl_xor(Nmax, 16, 64));
     Nmax = max(Nmax, __shfl_xor(Nmax, 32, 64));
-    bool started = false;                       // hasStarted: an earlier step was integrated
-    double C[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};  // R(cdq), carried from step to step
-    if (APPEND) qrot(cdq, C);
-    double* rec = sA;
-    for (int c0 = 0; c0 < Nmax; c0 += kImuChunk) {
+    bool started = false;  // hasStarted: an earlier step was integrated
+    double* const rec = sG + kLRec;
+    double* const q1 = sG + kLQ1;
+    double* const cr = sG + kLCr;
+    double* const cj = sG + kLCj;
+    double* const cc = sG + kLCc;
+    double* const ca = sG + kLCa;
+    double* const xx = sG + kLXx;
+    double* const Fs = sG + kLF;
+    double* const nz = sG + kLNz;
+    double* const v03 = sG + kLRec;  // (phase S -> F03; the records are consumed by then)
+    double* const M = sG + kLM;      // (phase P; aliases the records, q1, cr and cj)
+    for (int c0 = 0; c0 < Nmax; c0 += kImuK) {
+      const int nk = min(kImuK, Nmax - c0);
+      // ---- R
       {
+        const double bg[3] = {sb0[3], sb0[4], sb0[5]}, ba[3] = {sb0[6], sb0[7], sb0[8]};
+        const double a_max = parp[0], g_max = parp[1], sg_c = parp[2], sa_c = parp[3], sgw_c = parp[4],
+                     saw_c = parp[5];
         const int it = c0 + l;
         bool ok = false;
         double dt = 0.0, om0[3] = {0, 0, 0}, ac0[3] = {0, 0, 0}, om1[3] = {0, 0, 0}, ac1[3] = {0, 0, 0};
         int64_t nexttime = 0;
         int s0 = sbeg;
-        if (l < kImuChunk && it < N) {
+        if (l < kImuK && it < N) {
           s0 = sbeg + it;
           const int s1 = (it + 1 < N) ? s0 + 1 : s0;
           for (int k = 0; k < 3; ++k) {
@@ -494,8 +527,11 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
         }
         started = started || gm != 0;
         steps += __popc(gm);
-        double* R = rec + min(l, kImuChunk - 1) * kStepRec;
-        if (l < kImuChunk) R[0] = ok ? dt : 0.0;
+        double* R = rec + min(l, kImuK - 1) * kStepRec;
+        if (l < kImuK) {
+          R[0] = ok ? dt : 0.0;
+          Fs[l * kFStride + kFdt] = ok ? dt : 0.0;
+        }
         if (ok) {
           double gyr_sat = 1.0, acc_sat = 1.0;
           for (int k = 0; k < 3; ++k) {
@@ -521,126 +557,168 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
             R[17 + i] = Rdqi[i];
           }
           // discrete noise of this step on the diagonal (ImuError.cpp:412-426, summed over sigma)
-          R[26] = sa_c * sa_c * (0.5 * dt * dt * dt * acc_sat * acc_sat * acc_sat);
-          R[27] = sg_c * sg_c * (gyr_sat * dt);
-          R[28] = sa_c * sa_c * (acc_sat * dt);
-          R[29] = sgw_c * sgw_c * dt;
-          R[30] = saw_c * saw_c * dt;
+          double* z = nz + l * 5;
+          z[0] = sa_c * sa_c * (0.5 * dt * dt * dt * acc_sat * acc_sat * acc_sat);
+          z[1] = sg_c * sg_c * (gyr_sat * dt);
+          z[2] = sa_c * sa_c * (acc_sat * dt);
+          z[3] = sgw_c * sgw_c * dt;
+          z[4] = saw_c * saw_c * dt;
         }
       }
       __syncthreads();
-      const int nk = min(kImuChunk, Nmax - c0);
+      // ---- Q: the two product chains (every lane computes them; lane 0 stores)
+      {
+      Q cdq{carry[0], carry[1], carry[2], carry[3]};
+      double cross[9];
+      for (int i = 0; i < 9; ++i) cross[i] = carry[4 + i];
+      if (l == 0) {
+        q1[0] = cdq.x; q1[1] = cdq.y; q1[2] = cdq.z; q1[3] = cdq.w;
+        for (int i = 0; i < 9; ++i) cr[i] = cross[i];
+      }
       for (int k = 0; k < nk; ++k) {
         const double* R = rec + k * kStepRec;
         const double dt = R[0];
-        const bool doStep = dt > 0.0;  // uniform over the group
-        double qa0 = 0, qg = 0, qa = 0, qbg = 0, qba = 0;
-        if (doStep) {
-          const Q dq{R[1], R[2], R[3], R[4]};
-          const double a_true[3] = {R[5], R[6], R[7]};
-          const Q dq1 = qmul(cdq, dq);
-          double C1[9], CC1[9];
-          qrot(dq1, C1);
-          for (int i = 0; i < 9; ++i) CC1[i] = C[i] + C1[i];
-          double CCa[3];
-          mv3(CC1, a_true, CCa);
-          const double hdt2 = 0.25 * dt * dt;
-          double tmp[9];
-          if (l == 0) {
-            double v[3], mx[9];
-            for (int i = 0; i < 3; ++i) v[i] = cai[i] * dt + hdt2 * CCa[i];
-            crossMx(v, mx);
-            for (int i = 0; i < 9; ++i) sF[kF03 + i] = -mx[i];
-            for (int i = 0; i < 3; ++i) v[i] = 0.5 * dt * CCa[i];
-            crossMx(v, mx);
-            for (int i = 0; i < 9; ++i) sF[kF63 + i] = -mx[i];
-            for (int i = 0; i < 9; ++i) {
-              sF[kF012 + i] = -cCi[i] * dt + hdt2 * CC1[i];
-              sF[kF39 + i] = -dt * C1[i];
-              sF[kF612 + i] = -0.5 * dt * CC1[i];
-            }
-            sF[kFdt] = dt;
-          }
-          for (int i = 0; i < 9; ++i) tmp[i] = cCi[i] * dt + hdt2 * CC1[i];
-          aCdi += pick9(tmp, l);
-          for (int i = 0; i < 3; ++i) tmp[i] = cai[i] * dt + hdt2 * CCa[i];
-          aadi += (l == 0) ? tmp[0] : ((l == 1) ? tmp[1] : tmp[2]);
-          for (int i = 0; i < 9; ++i) cCi[i] += 0.5 * dt * CC1[i];
-          for (int i = 0; i < 3; ++i) cai[i] += 0.5 * dt * CCa[i];
-          double Jr[9], Rdqi[9];
-          for (int i = 0; i < 9; ++i) {
-            Jr[i] = R[8 + i];
-            Rdqi[i] = R[17 + i];
-          }
-          mm3(C1, Jr, tmp);
-          adadbg += pick9(tmp, l) * dt;
-          double cross1[9];
+        if (dt > 0.0) {  // uniform over the group
+          cdq = qmul(cdq, Q{R[1], R[2], R[3], R[4]});
+          double Rdqi[9], tmp[9];
+          for (int i = 0; i < 9; ++i) Rdqi[i] = R[17 + i];
           mm3(Rdqi, cross, tmp);
-          for (int i = 0; i < 9; ++i) cross1[i] = tmp[i] + Jr[i] * dt;
-          double ax[9], t1m[9], X[9];
-          crossMx(a_true, ax);
-          mm3(C, ax, tmp);
-          mm3(tmp, cross, t1m);
-          mm3(C1, ax, tmp);
-          mm3(tmp, cross1, X);
-          for (int i = 0; i < 9; ++i) X[i] += t1m[i];
-          for (int i = 0; i < 9; ++i) tmp[i] = dt * cdvdbg[i] + hdt2 * X[i];
-          if (l == 0)
-            for (int i = 0; i < 9; ++i) {
-              sF[kF09 + i] = tmp[i];
-              sF[kF69 + i] = 0.5 * dt * X[i];
-            }
-          adpdbg += pick9(tmp, l);
-          for (int i = 0; i < 9; ++i) {
-            cdvdbg[i] += 0.5 * dt * X[i];
-            cross[i] = cross1[i];
-            C[i] = C1[i];
-          }
-          cdq = dq1;
-          qa0 = R[26]; qg = R[27]; qa = R[28]; qbg = R[29]; qba = R[30];
+          for (int i = 0; i < 9; ++i) cross[i] = tmp[i] + R[8 + i] * dt;
         }
-        __syncthreads();
-        // P <- F P F^T + Q : M = F P (column l), exchange rows, P' = F M^T (column l)
+        if (l == 0) {
+          double* qo = q1 + 4 * (k + 1);
+          qo[0] = cdq.x; qo[1] = cdq.y; qo[2] = cdq.z; qo[3] = cdq.w;
+          for (int i = 0; i < 9; ++i) cr[9 * (k + 1) + i] = cross[i];
+        }
+      }
+      if (l == 0) {
+        carry[0] = cdq.x; carry[1] = cdq.y; carry[2] = cdq.z; carry[3] = cdq.w;
+        for (int i = 0; i < 9; ++i) carry[4 + i] = cross[i];
+      }
+      }
+      __syncthreads();
+      // ---- I: step l's products
+      if (l < nk) {
+        const double* R = rec + l * kStepRec;
+        const double dt = R[0];
+        if (dt > 0.0) {
+          double C[9], C1[9], CC1[9], CCa[3], tmp[9], t1m[9], X[9], ax[9];
+          const double* qa = q1 + 4 * l;
+          qrot(Q{qa[0], qa[1], qa[2], qa[3]}, C);
+          qrot(Q{qa[4], qa[5], qa[6], qa[7]}, C1);
+          for (int i = 0; i < 9; ++i) CC1[i] = C[i] + C1[i];
+          const double a_true[3] = {R[5], R[6], R[7]};
+          mv3(CC1, a_true, CCa);
+          double Jr[9];
+          for (int i = 0; i < 9; ++i) Jr[i] = R[8 + i];
+          mm3(C1, Jr, tmp);
+          for (int i = 0; i < 9; ++i) cj[9 * l + i] = tmp[i];
+          crossMx(a_true, ax);
+          double crk[9];
+          for (int i = 0; i < 9; ++i) crk[i] = cr[9 * l + i];
+          mm3(C, ax, tmp);
+          mm3(tmp, crk, t1m);
+          for (int i = 0; i < 9; ++i) crk[i] = cr[9 * (l + 1) + i];
+          mm3(C1, ax, tmp);
+          mm3(tmp, crk, X);
+          for (int i = 0; i < 9; ++i) X[i] += t1m[i];
+          double* F = Fs + l * kFStride;
+          double v[3], mx[9];
+          for (int i = 0; i < 3; ++i) v[i] = 0.5 * dt * CCa[i];
+          crossMx(v, mx);
+          for (int i = 0; i < 9; ++i) {
+            cc[9 * l + i] = CC1[i];
+            xx[9 * l + i] = X[i];
+            F[kF39 + i] = -dt * C1[i];
+            F[kF63 + i] = -mx[i];
+            F[kF69 + i] = 0.5 * dt * X[i];
+            F[kF612 + i] = -0.5 * dt * CC1[i];
+          }
+          for (int i = 0; i < 3; ++i) ca[3 * l + i] = CCa[i];
+        }
+      }
+      __syncthreads();
+      // ---- S: running sums, component-distributed
+      for (int k = 0; k < nk; ++k) {
+        double* F = Fs + k * kFStride;
+        const double dt = F[kFdt];
+        if (dt > 0.0 && l < 12) {
+          const double hdt2 = 0.25 * dt * dt;
+          if (l < 9) {
+            const double c = cc[9 * k + l], x = xx[9 * k + l];
+            F[kF012 + l] = -aCi * dt + hdt2 * c;
+            aCdi += aCi * dt + hdt2 * c;
+            aCi += 0.5 * dt * c;
+            adadbg += cj[9 * k + l] * dt;
+            const double t = dt * advdbg + hdt2 * x;
+            F[kF09 + l] = t;
+            adpdbg += t;
+            advdbg += 0.5 * dt * x;
+          } else {
+            const double c = ca[3 * k + l - 9];
+            const double v = aCi * dt + hdt2 * c;
+            v03[3 * k + l - 9] = v;
+            aCdi += v;
+            aCi += 0.5 * dt * c;
+          }
+        }
+      }
+      __syncthreads();
+      if (l < nk) {  // F03 = -[acc_integral dt + dt^2/4 (C + C_1) a]x
+        double* F = Fs + l * kFStride;
+        if (F[kFdt] > 0.0) {
+          double mx[9];
+          crossMx(v03 + 3 * l, mx);
+          for (int i = 0; i < 9; ++i) F[kF03 + i] = -mx[i];
+        }
+      }
+      __syncthreads();
+      // ---- P <- F P F^T + Q : M = F P (column l), exchange rows, P' = F M^T (column l)
+      for (int k = 0; k < nk; ++k) {
+        const double* F = Fs + k * kFStride;
+        const bool doStep = F[kFdt] > 0.0;  // uniform over the group
         if (doStep && l < 15) {
           double Mc[15];
-          applyF(sF, Pc, Mc);
-          for (int i = 0; i < 15; ++i) sB[l * 16 + i] = Mc[i];  // column l of M
+          applyF(F, Pc, Mc);
+          for (int i = 0; i < 15; ++i) M[l * 16 + i] = Mc[i];  // column l of M
         }
         __syncthreads();
         if (doStep && l < 15) {
           double Mr[15];
-          for (int j = 0; j < 15; ++j) Mr[j] = sB[j * 16 + l];  // row l of M
-          applyF(sF, Mr, Pc);
-          for (int i = 0; i < 15; ++i) {
-            const double q = i < 3 ? qa0 : (i < 6 ? qg : (i < 9 ? qa : (i < 12 ? qbg : qba)));
-            Pc[i] += (i == l) ? q : 0.0;
-          }
+          for (int j = 0; j < 15; ++j) Mr[j] = M[j * 16 + l];  // row l of M
+          applyF(F, Mr, Pc);
+          const double* z = nz + k * 5;
+          const double q = l < 3 ? z[0] : (l < 6 ? z[1] : (l < 9 ? z[2] : (l < 12 ? z[3] : z[4])));
+          for (int i = 0; i < 15; ++i) Pc[i] += (i == l) ? q : 0.0;
         }
         __syncthreads();
       }
     }
   }
   ICLK(1)
-  // new preintegration state (ImuError.hpp:273-304 members) straight from the chain registers;
-  // the distributed accumulators are written by their owner lanes
+  // new preintegration state (ImuError.hpp:273-304 members) from the chain registers and the
+  // component owners
+  double Db[6];  // Delta_b of the residual (ImuError.cpp:841-859), zero after a redo
+  for (int k = 0; k < 6; ++k) Db[k] = resetDb ? 0.0 : sb0[3 + k] - stR[60 + k];
   if (integrate) {
     if (l == 0) {
-      state[2] = cdq.x; state[3] = cdq.y; state[4] = cdq.z; state[5] = cdq.w;
+      for (int i = 0; i < 4; ++i) state[2 + i] = carry[i];
       for (int i = 0; i < 9; ++i) {
-        state[6 + i] = cCi[i];
-        state[39 + i] = cdvdbg[i];
-        state[292 + i] = cross[i];
+        state[292 + i] = carry[4 + i];
         if (!APPEND) state[57 + i] = sb0[i];  // append keeps speedAndBiases_ref_
       }
-      for (int i = 0; i < 3; ++i) state[24 + i] = cai[i];
       state[291] = (double)steps;
     }
     if (l < 9) {
+      state[6 + l] = aCi;
       state[15 + l] = aCdi;
       state[30 + l] = adadbg;
+      state[39 + l] = advdbg;
       state[48 + l] = adpdbg;
+    } else if (l < 12) {
+      state[24 + l - 9] = aCi;
+      state[27 + l - 9] = aCdi;
     }
-    if (l < 3) state[27 + l] = aadi;
   }
 
   ICLK(2)
@@ -757,7 +835,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
     double C0[9];
     qrot(q0, C0);  // C_WS_0 ; C_S0_W = C0^T
     double dp[3], dv[3];
-    const double gW[3] = {0.0, 0.0, gmag};
+    const double gW[3] = {0.0, 0.0, parp[6]};
     for (int k = 0; k < 3; ++k) {
       dp[k] = p0[k] - p1[k] + sb0[k] * Dt - 0.5 * gW[k] * Dt * Dt;
       dv[k] = sb0[k] - sb1[k] - gW[k] * Dt;

@@ -37,6 +37,7 @@ void launch_gn_finalize(const DevProblem& P, hipStream_t s);
 // (kernels_chol.hip)
 // wave-specialised Cholesky: does its LDS (static + 2 windows' solve vectors) fit a workgroup?
 bool cholesky_ws_fits(int max_fpad, size_t lds_per_block);
+bool cholesky_persistent_fits(int max_fpad, size_t lds_per_block);
 void launch_cholesky(const DevProblem& P, hipStream_t s);
 
 // trust-region control (kernels_control.hip)

@@ -970,6 +970,7 @@ struct okvisgpu_ctx {
   int cuCount = 256;
   size_t ldsPerBlock = 65536;
   bool wsFits() const { return cholesky_ws_fits(P.max_fpad, ldsPerBlock); }
+  bool persistentFits() const { return cholesky_persistent_fits(P.max_fpad, ldsPerBlock); }
   bool haveProblem = false;
   // split-solve state
   bool inSolve = false;
@@ -1284,6 +1285,9 @@ struct okvisgpu_ctx {
     int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 3 ? o.cholesky_schedule : 0;
     if (sched == 0) sched = P.n_win >= cuCount ? 1 : (2 * P.n_win >= cuCount && wsFits() ? 3 : 2);
     if (sched == 3 && !wsFits()) sched = 2;
+    // the persistent kernel keeps the window's rhs / y in dynamic LDS next to its static tiles:
+    // a reduced dimension beyond what fits falls back to the tile-parallel launches
+    if (sched == 1 && !persistentFits()) sched = 2;
     if (sched != P.chol_schedule && iterGraph) {
       (void)hipGraphExecDestroy(iterGraph);
       iterGraph = nullptr;

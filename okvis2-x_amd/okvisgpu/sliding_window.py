@@ -153,6 +153,7 @@ class SlidingWindow:
         self.links: dict[tuple, ImuLink] = {}
         self.landmarks: dict[int, np.ndarray] = {}
         self.obs: dict[tuple, tuple] = {}             # (frame, camera, landmark) -> (kp, sqrt_info)
+        self.pending: dict[int, dict] = {}            # landmark -> observations not yet in the graph
         self.edges: dict[tuple, Edge] = {}            # (reference, other) -> pose-graph edge
         self.key_frames: set[int] = set()
         self.imu_frames: set[int] = set()
@@ -176,15 +177,40 @@ class SlidingWindow:
             self.links[(prev, k)] = ImuLink(int(w.frame_t[prev]), int(w.frame_t[k]), ts.copy(), ga.copy())
         self.states[k] = State(int(w.frame_t[k]), w.init_poses[k].copy(), sb,
                                is_keyframe=(k % self.keyframe_every == 0))
+        # The synthetic frontend: a landmark enters the graph once it has two observations (the
+        # frontend triangulates before ViGraph::addLandmark / addObservation); later observations of
+        # a landmark in the graph go straight in.
+        in_graph = {lm for (_, _, lm) in self.obs}
         for cam, lm, kp, L in w.frame_obs[k]:
-            if lm not in self.landmarks:
-                self.landmarks[lm] = w.init_lms[lm].copy()
-            self.obs[(k, cam, lm)] = (kp, L)
+            if lm in in_graph:
+                self.obs[(k, cam, lm)] = (kp, L)
+                continue
+            pend = self.pending.setdefault(lm, {})
+            pend[(k, cam, lm)] = (kp, L)
+            if len(pend) >= 2:
+                if lm not in self.landmarks:
+                    self.landmarks[lm] = w.init_lms[lm].copy()
+                self.obs.update(self.pending.pop(lm))
+                in_graph.add(lm)
         self.imu_frames.add(k)
 
     def remove_all_observations(self, sid):
         for key in [key for key in self.obs if key[0] == sid]:
             del self.obs[key]
+        for lm in list(self.pending):
+            self.pending[lm] = {k: v for k, v in self.pending[lm].items() if k[0] != sid}
+            if not self.pending[lm]:
+                del self.pending[lm]
+
+    def clean_unobserved_landmarks(self):
+        """ViGraph::cleanUnobservedLandmarks (ViGraph.cpp:1914-1940, called by the frontend every
+        frame, Frontend.cpp:1140): a landmark left with one observation loses it."""
+        count = {}
+        for key in self.obs:
+            count.setdefault(key[2], []).append(key)
+        for lm, keys in count.items():
+            if len(keys) == 1:
+                del self.obs[keys[0]]
 
     def covisibilities(self):
         """ViGraph::computeCovisibilities (ViGraph.cpp:727-763): per landmark, every pair of distinct
@@ -272,7 +298,10 @@ class SlidingWindow:
     def optimise(self):
         """ViSlamBackend::optimiseRealtimeGraph -> ViGraph::optimise (DENSE_SCHUR)."""
         P, ids, lm_ids, links = self.build_problem()
-        s = self.backend.solve(P.struct, self.options)
+        return self.absorb(P, ids, lm_ids, links, self.backend.solve(P.struct, self.options))
+
+    def absorb(self, P, ids, lm_ids, links, s):
+        """Take a solved problem's estimates (and IMU states) back into the graph."""
         for i, sid in enumerate(ids):
             self.states[sid].pose[:] = P.poses[i]
             self.states[sid].sb[:] = P.speed_biases[i]
@@ -492,6 +521,7 @@ class SlidingWindow:
     def step(self, k):
         """One frame: add it, solve the realtime window, apply the marginalisation strategy."""
         self.add_frame(k)
+        self.clean_unobserved_landmarks()
         s = self.optimise()
         self.apply_strategy()
         return s
@@ -517,6 +547,13 @@ class _OwnedProblem:
         self.cameras = []
         self.imu_params = ImuParams()
         self.struct = Problem()
+
+    def snapshot(self):
+        return {k: getattr(self, k).copy() for k in ("poses", "speed_biases", "landmarks", "imu_state")}
+
+    def restore(self, snap):
+        for k, v in snap.items():
+            getattr(self, k)[...] = v
 
     def bind(self):
         s = self.struct

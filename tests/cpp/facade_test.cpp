@@ -207,6 +207,26 @@ int cpuTests() {
   threw = false;
   try { okvisgpu::CauchyLoss c2(2.0); (void)c2; } catch (const okvisgpu::Unsupported&) { threw = true; }
   CHECK(threw);
+  // one VARIABLE extrinsics block seen with two different intrinsics would become two independent
+  // ABI blocks: rejected (a constant one is fine: two ABI cameras sharing the same constant T_SC)
+  {
+    okvisgpu::Problem Q;
+    double Ta[7] = {0, 0, 0, 0, 0, 0, 1}, Ex[7] = {0, 0, 0, 0, 0, 0, 1}, La[4] = {0, 0, 5, 1};
+    Q.AddParameterBlock(Ta, 7, &pm);
+    Q.AddParameterBlock(Ex, 7, &pm);
+    Q.AddParameterBlock(La, 4, &hm);
+    okvisgpu_camera cam2 = cam;
+    cam2.fu = 351;
+    okvisgpu::ReprojectionError ea(cam, kp, Li), eb(cam2, kp, Li);
+    Q.AddResidualBlock(&ea, &cauchy, Ta, La, Ex);
+    Q.AddResidualBlock(&eb, &cauchy, Ta, La, Ex);
+    Q.SetParameterBlockConstant(Ex);
+    CHECK(Q.view().n_cameras == 2);
+    Q.SetParameterBlockVariable(Ex);
+    threw = false;
+    try { (void)Q.view(); } catch (const okvisgpu::Unsupported&) { threw = true; }
+    CHECK(threw);
+  }
   // no device in this container: Solve reports the C ABI's status instead of crashing
   int32_t ndev = 0;
   okvisgpu_device_count(&ndev);
@@ -312,6 +332,23 @@ int windowVsDirect() {
   CHECK(frozen);
   CHECK(std::fabs(sa.final_cost - sb.final_cost) <= 1e-9 * sb.final_cost && dev <= 1e-9);
   std::printf("after freezing pose 3: cost %.12g / %.12g, max pose deviation %.3g\n", sa.final_cost, sb.final_cost, dev);
+  // online calibration switched on between solves (ViGraph::setExtrinsicsVariable, ViGraph.cpp:1733-1739):
+  // the facade queues okvisgpu_set_block_constant kind 3 (no problem re-upload) like the direct caller
+  P.SetParameterBlockVariable(&pa->extrinsics[0]);
+  CHECK(okvisgpu_set_block_constant(ctx, 0, 3, 0, 0) == OKVISGPU_OK);
+  CHECK(P.Solve(zeroTol(3), &sa) == OKVISGPU_OK);
+  CHECK(okvisgpu_update_params(ctx) == OKVISGPU_OK);
+  CHECK(okvisgpu_solve(ctx, &o3, &sb) == OKVISGPU_OK);
+  dev = 0;
+  for (int i = 0; i < 7 * pa->n_poses; ++i) dev = std::max(dev, std::fabs(pa->poses[i] - pb->poses[i]));
+  double dext = 0, moved = 0;
+  for (int i = 0; i < 7; ++i) {
+    dext = std::max(dext, std::fabs(pa->extrinsics[i] - pb->extrinsics[i]));
+    moved = std::max(moved, std::fabs(pa->extrinsics[i] - pa->extrinsics[7 + i]));
+  }
+  CHECK(std::fabs(sa.final_cost - sb.final_cost) <= 1e-9 * sb.final_cost && dev <= 1e-9 && dext <= 1e-9);
+  std::printf("after T_SC0 variable: cost %.12g / %.12g, max pose deviation %.3g, extrinsics %.3g\n", sa.final_cost,
+              sb.final_cost, dev, dext);
   okvisgpu_ctx_destroy(ctx);
   okvisgpu_synth_destroy(wa);
   okvisgpu_synth_destroy(wb);

@@ -115,9 +115,27 @@ def test_launcher_starts_n_ranks():
     assert d == {"world": 2, "gpus": 2, "windows": 9, "in_order": True, "master_addr": "127.0.0.1"}
 
 
-def test_launcher_weak_scaling_default():
-    """Without --windows every rank holds --windows-per-gpu windows of its own (weak scaling): the
-    job total grows with the rank count and the gather still returns every window in order."""
+def test_launcher_strong_scaling_default():
+    """Without --windows / --windows-per-gpu the job is the fixed 2,048-window batch split across the
+    ranks (strong scaling, BASELINE north_star), gathered in window order."""
+    import json
+    import subprocess
+    env = dict(os.environ, OKVISGPU_BENCH_DRYRUN="1")
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert d == {"world": 2, "gpus": 2, "windows": bench.DEFAULT_WINDOWS, "in_order": True,
+                 "master_addr": "127.0.0.1"}
+    args = bench.parse_args([])
+    assert bench.job_windows(args, 8) is True and args.windows == 2048
+    assert len(bench.rank_windows(args.windows, 8, 7)) == 256
+
+
+def test_launcher_weak_scaling():
+    """--windows-per-gpu: every rank holds that many windows of its own (weak scaling): the job
+    total grows with the rank count and the gather still returns every window in order."""
     import json
     import subprocess
     env = dict(os.environ, OKVISGPU_BENCH_DRYRUN="1")
