@@ -180,17 +180,21 @@ constexpr int kImuGroup = 16;
 constexpr int kImuPerWG = 4;
 constexpr int kStepRec = 26;  // dt | dq (4) | a_true (3) | Jr (9) | R(dq)^T (9)
 constexpr int kImuK = 4;      // integration steps per chunk
-constexpr int kFStride = 64;  // F_delta blocks of one step (offsets below) | dt
+constexpr int kFStride = 66;  // F_delta blocks of one step (offsets below) | dt | pad (lanes writing
+                              // consecutive steps fall on different LDS banks)
+constexpr int kS = 17;        // row stride of the 16x16 LDS matrices: lanes walking a column hit
+                              // distinct banks (a stride of 16 doubles put every other lane on one)
 // per-group LDS (doubles) during the chain: step records, Delta_q and cross_ after each step (slot
-// 0 = before the chunk), C_1 Jr, C + C_1, (C + C_1) a, X, F_delta, noise; the P exchange (15 x 16)
-// reuses the first 240. After the chain: P / U (sA, 256), L / eigenvectors (sB, 256), Jacobi
-// rotations (sR, 64).
+// 0 = before the chunk), C_1 Jr, C + C_1, (C + C_1) a, X, F_delta, noise; the P exchange (15 x kS)
+// reuses the first 255. After the chain: P / U (sA, 16 x kS), L / eigenvectors (sB, 16 x kS),
+// Jacobi rotations (sR, 32).
 constexpr int kLRec = 0, kLQ1 = kLRec + kImuK * kStepRec, kLCr = kLQ1 + 4 * (kImuK + 1),
-              kLCj = kLCr + 9 * (kImuK + 1), kLM = 0, kLCc = 240, kLCa = kLCc + 9 * kImuK, kLXx = kLCa + 3 * kImuK,
+              kLCj = kLCr + 9 * (kImuK + 1), kLM = 0, kLCc = 256, kLCa = kLCc + 9 * kImuK, kLXx = kLCa + 3 * kImuK,
               kLF = kLXx + 9 * kImuK, kLNz = kLF + kFStride * kImuK, kLCarry = kLNz + 5 * kImuK,
               kImuLds = kLCarry + 13;
-static_assert(kLCj + 9 * kImuK <= kLCc && 15 * 16 <= kLCc, "chain records / P exchange overlap the sums");
-static_assert(kImuLds >= 2 * 256 + 64, "the square-root phase needs sA, sB and sR");
+static_assert(kLCj + 9 * kImuK <= kLCc && 15 * kS <= kLCc, "chain records / P exchange overlap the sums");
+static_assert(kImuLds >= 32 * kS + 32, "the square-root phase needs sA, sB and sR");
+static_assert(kImuLds * 8 * 4 <= 20480, "LDS for eight workgroups (two waves per SIMD) per CU");
 
 // F_delta (ImuError.cpp:395-410) of one step in LDS: non-identity 3x3 blocks
 constexpr int kF03 = 0, kF09 = 9, kF012 = 18, kF39 = 27, kF63 = 36, kF69 = 45, kF612 = 54, kFdt = 63;
@@ -236,13 +240,13 @@ __device__ __forceinline__ double groupSum(double v) {  // sum over the 16 lanes
 // Cyclic Jacobi with round-robin ordering on the 16x16 (15 + decoupled pad) symmetric matrix A of
 // every group with `need` set; V receives the eigenvectors. Uniform control flow over the wave.
 __device__ void groupJacobi(double* A, double* V, double* rot, int l, bool need) {
-  for (int e = l; e < 256; e += kImuGroup) V[e] = ((e >> 4) == (e & 15)) ? 1.0 : 0.0;
+  for (int e = l; e < 256; e += kImuGroup) V[(e >> 4) * kS + (e & 15)] = ((e >> 4) == (e & 15)) ? 1.0 : 0.0;
   __syncthreads();
   bool run = need;
   for (int sweep = 0; sweep < 100; ++sweep) {
     double off = 0.0, dg = 0.0;
     for (int j = 0; j < 16; ++j) {
-      const double a = A[l * 16 + j];
+      const double a = A[l * kS + j];
       if (j == l) dg += a * a;
       else if (l < j) off += a * a;
     }
@@ -256,10 +260,10 @@ __device__ void groupJacobi(double* A, double* V, double* rot, int l, bool need)
         if (l == 0) { p = 15; q = round; }
         else { p = (round + l) % 15; q = (round + 15 - l) % 15; }
         if (p > q) { const int t = p; p = q; q = t; }
-        const double apq = A[p * 16 + q];
+        const double apq = A[p * kS + q];
         double c = 1.0, s = 0.0;
         if (apq != 0.0) {
-          const double app = A[p * 16 + p], aqq = A[q * 16 + q];
+          const double app = A[p * kS + p], aqq = A[q * kS + q];
           const double theta = (aqq - app) / (2.0 * apq);
           const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
           c = 1.0 / sqrt(t * t + 1.0);
@@ -277,9 +281,9 @@ __device__ void groupJacobi(double* A, double* V, double* rot, int l, bool need)
           double* M = (t < 128) ? A : V;
           const double c = rot[k * 4], s = rot[k * 4 + 1];
           const int p = (int)rot[k * 4 + 2], q = (int)rot[k * 4 + 3];
-          const double mp = M[row * 16 + p], mq = M[row * 16 + q];
-          M[row * 16 + p] = c * mp - s * mq;
-          M[row * 16 + q] = s * mp + c * mq;
+          const double mp = M[row * kS + p], mq = M[row * kS + q];
+          M[row * kS + p] = c * mp - s * mq;
+          M[row * kS + q] = s * mp + c * mq;
         }
       }
       __syncthreads();
@@ -288,17 +292,17 @@ __device__ void groupJacobi(double* A, double* V, double* rot, int l, bool need)
           const int k = t >> 4, col = t & 15;
           const double c = rot[k * 4], s = rot[k * 4 + 1];
           const int p = (int)rot[k * 4 + 2], q = (int)rot[k * 4 + 3];
-          const double mp = A[p * 16 + col], mq = A[q * 16 + col];
-          A[p * 16 + col] = c * mp - s * mq;
-          A[q * 16 + col] = s * mp + c * mq;
+          const double mp = A[p * kS + col], mq = A[q * kS + col];
+          A[p * kS + col] = c * mp - s * mq;
+          A[q * kS + col] = s * mp + c * mq;
         }
       }
       __syncthreads();
       if (run && l < 8) {
         const int p = (int)rot[l * 4 + 2], q = (int)rot[l * 4 + 3];
         if (rot[l * 4 + 1] != 0.0) {
-          A[p * 16 + q] = 0.0;
-          A[q * 16 + p] = 0.0;
+          A[p * kS + q] = 0.0;
+          A[q * kS + p] = 0.0;
         }
       }
       __syncthreads();
@@ -315,7 +319,7 @@ __device__ void groupJacobi(double* A, double* V, double* rot, int l, bool need)
 // workgroup adds its s_memrealtime ticks (100 MHz) per phase with vector atomics; the last
 // workgroup prints the totals.
 #ifdef OKG_IMU_CLOCK
-__device__ unsigned long long g_imuClk[8];
+__device__ unsigned long long g_imuClk[12];
 __device__ unsigned int g_imuDone;
 #define ICLK_INIT unsigned long long iclk = __builtin_amdgcn_s_memrealtime();
 #define ICLK(i)                                                                         \
@@ -328,9 +332,10 @@ __device__ unsigned int g_imuDone;
   if (!APPEND && threadIdx.x == 0) {                                                    \
     __threadfence();                                                                    \
     if (atomicAdd(&g_imuDone, 1u) == gridDim.x - 1) {                                   \
-      printf("IMUCLK pro %llu chain %llu state %llu sqrt %llu resid %llu jac %llu (x10ns)\n", g_imuClk[0], \
-             g_imuClk[1], g_imuClk[2], g_imuClk[3], g_imuClk[4], g_imuClk[5]);         \
-      for (int i = 0; i < 8; ++i) g_imuClk[i] = 0;                                      \
+      printf("IMUCLK pro %llu chain %llu state %llu sqrt %llu resid %llu jac %llu | R %llu Q %llu I %llu S %llu " \
+             "P %llu (x10ns)\n", g_imuClk[0], g_imuClk[1], g_imuClk[2], g_imuClk[3], g_imuClk[4], g_imuClk[5], \
+             g_imuClk[6], g_imuClk[7], g_imuClk[8], g_imuClk[9], g_imuClk[10]);                               \
+      for (int i = 0; i < 12; ++i) g_imuClk[i] = 0;                                     \
       g_imuDone = 0;                                                                    \
     }                                                                                   \
   }
@@ -356,8 +361,8 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   __shared__ double sAll[kImuPerWG][kImuLds];
   double* sG = sAll[g];
   double* sA = sG;
-  double* sB = sG + 256;
-  double* sR = sG + 512;
+  double* sB = sG + 16 * kS;
+  double* sR = sG + 32 * kS;
 
   // The factor's record, the head of its stored state and the window state are loaded in two
   // rounds (clamped index) and consumed at one point before any test, so that no load waits behind
@@ -545,12 +550,21 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
           }
           const double theta_half =
               sqrt(w_true[0] * w_true[0] + w_true[1] * w_true[1] + w_true[2] * w_true[2]) * 0.5 * dt;
-          const double sth = sinc(theta_half) * 0.5 * dt;
-          const Q dq{sth * w_true[0], sth * w_true[1], sth * w_true[2], cos(theta_half)};
+          double sh, ch;  // one sincos for dq and the right Jacobian
+          sincos(theta_half, &sh, &ch);
+          double sincv;  // ode::sinc (ode.hpp:34-46)
+          if (fabs(theta_half) > 1.0e-6) {
+            sincv = sh / theta_half;
+          } else {
+            const double x_2 = theta_half * theta_half, x_4 = x_2 * x_2, x_6 = x_2 * x_2 * x_2;
+            sincv = 1.0 - (1.0 / 6.0) * x_2 + (1.0 / 120.0) * x_4 - (1.0 / 5040.0) * x_6;
+          }
+          const double sth = sincv * 0.5 * dt;
+          const Q dq{sth * w_true[0], sth * w_true[1], sth * w_true[2], ch};
           R[1] = dq.x; R[2] = dq.y; R[3] = dq.z; R[4] = dq.w;
           const double wdt[3] = {w_true[0] * dt, w_true[1] * dt, w_true[2] * dt};
           double Jr[9], Rdqi[9];
-          rightJacobian(wdt, Jr);  // Jacobian parts (ImuError.cpp:385-392)
+          rightJacobianHalf(wdt, sh, ch, Jr);  // Jacobian parts (ImuError.cpp:385-392)
           qrot(qinv(dq), Rdqi);
           for (int i = 0; i < 9; ++i) {
             R[8 + i] = Jr[i];
@@ -566,6 +580,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
         }
       }
       __syncthreads();
+      ICLK(6)
       // ---- Q: the two product chains (every lane computes them; lane 0 stores)
       {
       Q cdq{carry[0], carry[1], carry[2], carry[3]};
@@ -597,6 +612,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
       }
       }
       __syncthreads();
+      ICLK(7)
       // ---- I: step l's products
       if (l < nk) {
         const double* R = rec + l * kStepRec;
@@ -638,6 +654,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
         }
       }
       __syncthreads();
+      ICLK(8)
       // ---- S: running sums, component-distributed
       for (int k = 0; k < nk; ++k) {
         double* F = Fs + k * kFStride;
@@ -664,6 +681,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
         }
       }
       __syncthreads();
+      ICLK(9)
       if (l < nk) {  // F03 = -[acc_integral dt + dt^2/4 (C + C_1) a]x
         double* F = Fs + l * kFStride;
         if (F[kFdt] > 0.0) {
@@ -680,12 +698,12 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
         if (doStep && l < 15) {
           double Mc[15];
           applyF(F, Pc, Mc);
-          for (int i = 0; i < 15; ++i) M[l * 16 + i] = Mc[i];  // column l of M
+          for (int i = 0; i < 15; ++i) M[l * kS + i] = Mc[i];  // column l of M
         }
         __syncthreads();
         if (doStep && l < 15) {
           double Mr[15];
-          for (int j = 0; j < 15; ++j) Mr[j] = M[j * 16 + l];  // row l of M
+          for (int j = 0; j < 15; ++j) Mr[j] = M[j * kS + l];  // row l of M
           applyF(F, Mr, Pc);
           const double* z = nz + k * 5;
           const double q = l < 3 ? z[0] : (l < 6 ? z[1] : (l < 9 ? z[2] : (l < 12 ? z[3] : z[4])));
@@ -693,6 +711,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
         }
         __syncthreads();
       }
+      ICLK(10)
     }
   }
   ICLK(1)
@@ -729,12 +748,12 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
     // symmetrise (ImuError.cpp:441): sB holds P column-major; the symmetric P is kept row-major
     // (16x16 with a decoupled zero pad) in sA for the eigen fallback
     if (integrate && l < 15)
-      for (int i = 0; i < 15; ++i) sB[l * 16 + i] = Pc[i];
+      for (int i = 0; i < 15; ++i) sB[l * kS + i] = Pc[i];
     __syncthreads();
     double trace = 0.0;
     if (integrate) {
-      for (int i = 0; i < 15; ++i) Pc[i] = (l < 15) ? 0.5 * Pc[i] + 0.5 * sB[i * 16 + l] : 0.0;
-      for (int i = 0; i < 16; ++i) sA[l * 16 + i] = (i < 15) ? Pc[i] : 0.0;
+      for (int i = 0; i < 15; ++i) Pc[i] = (l < 15) ? 0.5 * Pc[i] + 0.5 * sB[i * kS + l] : 0.0;
+      for (int i = 0; i < 16; ++i) sA[l * kS + i] = (i < 15) ? Pc[i] : 0.0;
       if (l < 15)  // P_delta_ (symmetrised), kept for a later append
         for (int i = 0; i < 15; ++i) state[301 + i * 15 + l] = Pc[i];
       for (int i = 0; i < 15; ++i) trace += (i == l) ? Pc[i] : 0.0;
@@ -744,19 +763,19 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
     // right-looking Cholesky P = L L^T in LDS: sB (column-major) starts as P, lane j owns column j
     bool ok = true;
     if (integrate)
-      for (int i = 0; i < 16; ++i) sB[l * 16 + i] = (l < 15 && i < 15) ? Pc[i] : 0.0;
+      for (int i = 0; i < 16; ++i) sB[l * kS + i] = (l < 15 && i < 15) ? Pc[i] : 0.0;
     __syncthreads();
     for (int k = 0; k < 15; ++k) {
       if (integrate && l >= k && l < 15) {
-        const double d = sB[k * 16 + k];
+        const double d = sB[k * kS + k];
         if (!(d > 0.0)) ok = false;
-        const double v = sB[k * 16 + l] / sqrt(d);
-        sB[k * 16 + l] = v;
+        const double v = sB[k * kS + l] / sqrt(d);
+        sB[k * kS + l] = v;
       }
       __syncthreads();
       if (integrate && l > k && l < 15) {
-        const double ljk = sB[k * 16 + l];
-        for (int i = l; i < 15; ++i) sB[l * 16 + i] -= sB[k * 16 + i] * ljk;
+        const double ljk = sB[k * kS + l];
+        for (int i = l; i < 15; ++i) sB[l * kS + i] -= sB[k * kS + i] * ljk;
       }
       __syncthreads();
     }
@@ -765,16 +784,16 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
     for (int j = 14; j >= 0; --j) {
       double acc = 0.0, ujj = 0.0;
       if (integrate && l >= j && l < 15) {
-        ujj = 1.0 / sB[j * 16 + j];
-        for (int m = j + 1; m <= l; ++m) acc += sB[m * 16 + l] * sB[j * 16 + m];
+        ujj = 1.0 / sB[j * kS + j];
+        for (int m = j + 1; m <= l; ++m) acc += sB[m * kS + l] * sB[j * kS + m];
       }
       __syncthreads();
-      if (integrate && l >= j && l < 15) sB[j * 16 + l] = (l == j) ? ujj : -ujj * acc;
+      if (integrate && l >= j && l < 15) sB[j * kS + l] = (l == j) ? ujj : -ujj * acc;
       __syncthreads();
     }
     double fro = 0.0;
     if (integrate && l < 15)
-      for (int i = l; i < 15; ++i) fro += sB[l * 16 + i] * sB[l * 16 + i];
+      for (int i = l; i < 15; ++i) fro += sB[l * kS + i] * sB[l * kS + i];
     fro = groupSum(fro);
     ok = groupSum(ok ? 0.0 : 1.0) == 0.0;
     const double eps = DBL_EPSILON;
@@ -787,25 +806,25 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
       double urow[15];
       if (needEig && l < 15) {
         double lmax = -1e300;
-        for (int i = 0; i < 15; ++i) lmax = fmax(lmax, sA[i * 16 + i]);
+        for (int i = 0; i < 15; ++i) lmax = fmax(lmax, sA[i * kS + i]);
         const double tol = fmax(eps, eps * 15.0 * lmax);
-        const double li = sA[l * 16 + l];
+        const double li = sA[l * kS + l];
         const double s = sqrt(li > tol ? 1.0 / li : 1.0 / tol);
-        for (int j = 0; j < 15; ++j) urow[j] = s * sB[j * 16 + l];
+        for (int j = 0; j < 15; ++j) urow[j] = s * sB[j * kS + l];
       }
       __syncthreads();
       if (needEig && l < 15)
-        for (int j = 0; j < 15; ++j) sA[l * 16 + j] = urow[j];
+        for (int j = 0; j < 15; ++j) sA[l * kS + j] = urow[j];
     }
     // Cholesky path: U (column-major in sB, lower triangular) -> row-major sA
     if (integrate && !needEig && l < 15)
-      for (int i = 0; i < 15; ++i) sA[i * 16 + l] = (i >= l) ? sB[l * 16 + i] : 0.0;
+      for (int i = 0; i < 15; ++i) sA[i * kS + l] = (i >= l) ? sB[l * kS + i] : 0.0;
     __syncthreads();
   }
   if (integrate) {
-    for (int e = l; e < 225; e += kImuGroup) state[66 + e] = sA[(e / 15) * 16 + e % 15];
+    for (int e = l; e < 225; e += kImuGroup) state[66 + e] = sA[(e / 15) * kS + e % 15];
   } else if (live) {
-    for (int e = l; e < 225; e += kImuGroup) sA[(e / 15) * 16 + e % 15] = state[66 + e];
+    for (int e = l; e < 225; e += kImuGroup) sA[(e / 15) * kS + e % 15] = state[66 + e];
   }
   __syncthreads();  // state writes of the group visible to all its lanes
   ICLK(3)
@@ -922,7 +941,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   double* lin = P.imu_lin[lb] + fl * kImuLin;
   double rr = 0.0;
   if (live && l < 15) {
-    for (int k = 0; k < 15; ++k) rr += sA[l * 16 + k] * err[k];
+    for (int k = 0; k < 15; ++k) rr += sA[l * kS + k] * err[k];
     lin[l] = rr;
   }
   const double c2 = groupSum(l < 15 ? rr * rr : 0.0);
@@ -959,10 +978,10 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
         if (success) {
           for (int t = 0; t < nt; ++t) {
             const double* Bk = sB + tblk[t] * 9;
-            const double* Ui = sA + i * 16 + trow[t];
+            const double* Ui = sA + i * kS + trow[t];
             acc += tsc[t] * (Ui[0] * Bk[0 * 3 + c] + Ui[1] * Bk[1 * 3 + c] + Ui[2] * Bk[2 * 3 + c]);
           }
-          if (idrow >= 0) acc += idv * sA[i * 16 + idrow];
+          if (idrow >= 0) acc += idv * sA[i * kS + idrow];
         }
         lin[15 + i * 30 + j] = acc;
       }

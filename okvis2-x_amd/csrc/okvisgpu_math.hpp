@@ -154,8 +154,33 @@ OKG_HD void rightJacobian(const double p[3], double J[9]) {
   J[0] += 1.0; J[4] += 1.0; J[8] += 1.0;
 }
 
+// rightJacobian with sin / cos of Phi from sin / cos of Phi / 2 (one sincos per IMU step, shared
+// with dq = exp(w dt / 2)): 1 - cos Phi = 2 sin^2(Phi/2) and sin Phi = 2 sin(Phi/2) cos(Phi/2), equal
+// to the reference's a, b up to rounding (the form above loses ~1e-10 of a to cancellation at the
+// small angles of one IMU step; either way a few 1e-16 of J).
+OKG_HD void rightJacobianHalf(const double p[3], double sh, double ch, double J[9]) {
+  const double Phi = sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
+  double X[9], X2[9];
+  crossMx(p, X);
+  mm3(X, X, X2);
+  double a, b;
+  if (Phi < 1.0e-4) {
+    a = -0.5;
+    b = 1.0 / 6.0;
+  } else {
+    const double Phi2 = Phi * Phi, Phi3 = Phi2 * Phi;
+    a = -(2.0 * sh * sh) / Phi2;
+    b = (Phi - 2.0 * sh * ch) / Phi3;
+  }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) J[i] = a * X[i] + b * X2[i];
+  J[0] += 1.0; J[4] += 1.0; J[8] += 1.0;
+}
+
 // okvis::Duration::toSec of a signed nanosecond difference (Duration.hpp:107-109)
 OKG_HD double durToSec(int64_t dns) {
+  // sec = 0 for [0, 1 s): the same double as (double)0 + 1e-9 * nsec, without the 64-bit division
+  if (dns >= 0 && dns < 1000000000LL) return 1e-9 * (double)dns;
   int64_t sec = dns / 1000000000LL;
   int64_t nsec = dns % 1000000000LL;
   if (nsec < 0) { nsec += 1000000000LL; sec -= 1; }

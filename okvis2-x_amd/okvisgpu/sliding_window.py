@@ -548,6 +548,9 @@ class _OwnedProblem:
         self.imu_params = ImuParams()
         self.struct = Problem()
 
+    def ptr(self):
+        return C.pointer(self.struct)
+
     def snapshot(self):
         return {k: getattr(self, k).copy() for k in ("poses", "speed_biases", "landmarks", "imu_state")}
 
