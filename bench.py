@@ -117,6 +117,21 @@ def ate(P, gt):
 
 
 PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
+PMC_CALIB = os.path.join(REPO, "profiles", "r03_pmc_calib.json")
+
+
+def pmc_mfma():
+    """MFMA counters of k_cholesky on this workload (scripts/gpu_pmc_calib.sh ->
+    profiles/r03_pmc_calib.json): the busy fraction of the matrix cores and the FLOPs the counted
+    v_mfma_f64_16x16x4f64 instructions perform, or None."""
+    try:
+        with open(PMC_CALIB) as f:
+            d = json.load(f)["k_cholesky_mfma"]
+        return {"mfma_busy_frac": d["mfma_busy_frac"], "mfma_flops_per_dispatch": d["mfma_flops"],
+                "source": "profiles/r03_pmc_calib.json (SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_F64, "
+                          "GRBM_GUI_ACTIVE; 2,048 S50 windows)"}
+    except (OSError, KeyError, ValueError, TypeError):
+        return None
 
 
 def rank_windows(total, world, rank):
@@ -480,6 +495,9 @@ def main(argv=None):
                 "kernel": dominant, "bound": d["bound"], "achieved": d["achieved"], "peak": d["peak"],
                 "unit": "GB/s" if d["bound"] == "hbm" else "TFLOP/s", "frac": d["frac"],
                 "traffic": traffic,
+                "traffic_calibration": "FETCH_SIZE x2, WRITE_SIZE x1: measured for this code's 16-B, 8-B and "
+                                       "tile-row access shapes (scripts/pmc_calib.hip, profiles/r03_pmc_calib.json)",
+                "counters": pmc_mfma() if dominant == "k_cholesky" else None,
                 "work_per_iteration": d["work"], "ms_per_iteration": d["ms"],
                 "frac_survey_8d": survey.get(dominant, {}).get("frac") if d["bound"] == "hbm" else None,
                 "method": f"HIP events on the context stream, {args.kernel_reps} launches of one iteration's "

@@ -1,7 +1,8 @@
 """Turn rocprofv3 --pmc passes (scripts/gpu_pmc.sh) into profiles/pmc_traffic.json: HBM bytes per
-dispatch of each kernel. FETCH_SIZE / WRITE_SIZE are in KiB; FETCH_SIZE is doubled per the gfx950
-calibration of MI355X_MICROARCH.md (HBM section: it reports half the bytes of 16-byte-per-lane
-reads); other access widths are uncalibrated there, so the figure is an estimate.
+dispatch of each kernel. FETCH_SIZE / WRITE_SIZE are in KiB; FETCH_SIZE is doubled, WRITE_SIZE taken
+as is: the calibration of scripts/pmc_calib.hip (profiles/r03_pmc_calib.json) measured exactly these
+factors for every access shape these kernels use (16 B and 8 B per lane, the Cholesky's tile rows),
+on a buffer four times the Infinity Cache.
 
 Usage: pmc_traffic.py OUT.json WINDOWS pass1.csv pass2.csv ... (WINDOWS = windows in the profiled
 batch; bench.py scales bytes_per_window_iteration by its own windows per GPU)."""
@@ -40,6 +41,6 @@ for k, d in vals.items():
     if "bytes_per_iteration" in kern[k]:
         kern[k]["bytes_per_window_iteration"] = kern[k]["bytes_per_iteration"] / windows
 json.dump({"source": sys.argv[3:], "windows": windows,
-           "correction": "FETCH_SIZE x2 (gfx950, 16 B/lane calibration), KiB -> bytes",
+           "correction": "FETCH_SIZE x2, WRITE_SIZE x1 (calibrated: profiles/r03_pmc_calib.json), KiB -> bytes",
            "kernels": kern}, open(out, "w"), indent=1, sort_keys=True)
 print(json.dumps({k: round(v["bytes_per_dispatch"] / 1e9, 3) for k, v in kern.items()}, indent=0))
