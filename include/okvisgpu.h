@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OKVISGPU_ABI_VERSION 4
+#define OKVISGPU_ABI_VERSION 5
 
 /* ---------------------------------------------------------------- status codes */
 typedef enum okvisgpu_status {
@@ -99,6 +99,20 @@ typedef struct okvisgpu_imu_params { /* okvis::ImuParameters subset, okvis_commo
  *  [292..300] cross_ (row-major)       [301..525] P_delta_ (15x15, symmetric): what
  *            ImuError::append continues from (ABI 4)                                          */
 #define OKVISGPU_IMU_STATE_DOUBLES 526
+
+/* Host-evaluated residual block (ABI 5; SURVEY.md §8b fallback): the contract of
+ * ::ceres::CostFunction::Evaluate(parameters, residuals, jacobians) plus the caller's user pointer
+ * and the factor's index within its window. parameters[k] holds the ambient values of the factor's
+ * k-th parameter block (pose-kind 7, speed/bias 9); residuals[dim]; jacobians[k] the row-major
+ * dim x ambient-size Jacobian of block k (always requested: the backend evaluates r and J together
+ * at every point it evaluates). The backend applies the pose manifold itself (PoseManifold plus
+ * Jacobian, PoseLocalParameterization.cpp:56-68), as Ceres does for a block with a manifold.
+ * Return nonzero on success; 0 makes the evaluation fail (a candidate point is then rejected, as
+ * Ceres does with candidate_cost = max; a failure at the initial point ends the window's solve with
+ * OKVISGPU_FAILURE). Called concurrently from up to options.num_threads host threads. */
+typedef int (*okvisgpu_host_evaluate_fn)(void* user, int32_t factor, const double* const* parameters,
+                                         double* residuals, double** jacobians);
+#define OKVISGPU_HOST_MAX_RESIDUALS 15
 
 typedef struct okvisgpu_problem {
   /* --- parameter blocks (written back in place by okvisgpu_solve / okvisgpu_get_params) */
@@ -177,6 +191,25 @@ typedef struct okvisgpu_problem {
   const int32_t* extrinsics_prior_camera; /* [n] camera index                                   */
   const double* extrinsics_prior_meas;    /* [n][7]                                             */
   const double* extrinsics_prior_sqrt_info; /* [n][36] row-major                                */
+
+  /* --- ABI 5: residual blocks evaluated on the host (SURVEY.md §8b "host-evaluated fallback"):
+   * any residual the GPU path has no functor for (GpsErrorSynchronous/Asynchronous,
+   * GpsErrorAsynchronous.hpp:42-55; RelativePoseError-like user factors) whose parameter blocks are
+   * pose-kind or speed/bias blocks: at most 2 pose-kind and 2 speed/bias blocks, all distinct, at most
+   * OKVISGPU_HOST_MAX_RESIDUALS residuals. Each point the solver evaluates (initial point, every
+   * candidate) gathers the blocks' values on the device, calls host_evaluate on options.num_threads
+   * host threads, and uploads r and the minimal Jacobian, which are accumulated into the reduced
+   * system like any device-evaluated factor. Factors on landmarks are not supported
+   * (OKVISGPU_ERR_UNSUPPORTED). n_host = 0 (the zero-initialised struct) = none. */
+  int32_t n_host;
+  const int32_t* host_dim;          /* [n] residual dimension, 1..OKVISGPU_HOST_MAX_RESIDUALS     */
+  const int32_t* host_param_kind;   /* [n][4] parameter block k in the functor's order: 0 pose-kind
+                                       (index < n_poses: a state's pose; n_poses + c: camera c's
+                                       extrinsics), 1 speed/bias, -1 none (trailing)             */
+  const int32_t* host_param_index;  /* [n][4]                                                      */
+  const uint8_t* host_cauchy;       /* [n] 1 = CauchyLoss(1.0) (may be NULL = no loss)            */
+  okvisgpu_host_evaluate_fn host_evaluate;
+  void* host_user;
 } okvisgpu_problem;
 
 /* ---------------------------------------------------------------- solver options / summary */
@@ -405,6 +438,10 @@ int okvisgpu_eval_reprojection(okvisgpu_ctx* ctx, int32_t window, double* r, dou
 int okvisgpu_eval_imu(okvisgpu_ctx* ctx, int32_t window, int32_t redo_always, double* r, double* J);
 /*   relative pose: r [n_relpose][6], J [n_relpose][6][12] minimal (reference pose 6, other pose 6) */
 int okvisgpu_eval_relpose(okvisgpu_ctx* ctx, int32_t window, double* r, double* J);
+/*   host-evaluated blocks, through the device path (gather, host_evaluate, upload; no loss):
+ *   r [n_host][15], J [n_host][15][30] minimal in the IMU column layout (first pose-kind block 0..5,
+ *   first speed/bias 6..14, second pose-kind 15..20, second speed/bias 21..29), rows >= dim zero. */
+int okvisgpu_eval_host(okvisgpu_ctx* ctx, int32_t window, double* r, double* J);
 
 /* ---------------------------------------------------------------- synthetic windows
  * Host-side generator of the synthetic sliding windows the benchmark is quoted on:

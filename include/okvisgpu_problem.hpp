@@ -18,9 +18,12 @@
 // (okvis_ceres/include/okvis/ceres/ErrorInterface.hpp:78) names them: "ReprojectionError",
 // "ImuError", "PoseError", "SpeedAndBiasError", "TwoPoseStandardGraphError(Const)",
 // "RelativePoseError". The term classes below carry the constants the adapter reads from the okvis
-// functors' getters. Any other cost function (GPS, SubmapICP, depth, ...) is
-// rejected at AddResidualBlock with an okvisgpu::Unsupported exception (OKVISGPU_ERR_UNSUPPORTED):
-// the caller keeps its Ceres solve for such a graph.
+// functors' getters (fromOkvisReprojectionError / fromOkvisImuError read them).
+// Any other cost function on pose-kind / speed-bias blocks (GPS, user factors) joins the solve as a
+// HostCostFunction (or HostFunctor<F> around the caller's ceres::CostFunction-shaped functor): the
+// §8b host-evaluated fallback. Cost functions the fallback cannot take either (landmark blocks:
+// depth, SubmapICP) are rejected at AddResidualBlock with okvisgpu::Unsupported
+// (OKVISGPU_ERR_UNSUPPORTED): the caller keeps its Ceres solve for such a graph.
 //
 // Ownership: like `Problem::Options{DO_NOT_TAKE_OWNERSHIP}` (ViGraph.cpp:239-247), the facade never
 // deletes cost functions, losses or manifolds; parameter memory stays the caller's and is read
@@ -30,6 +33,7 @@
 #pragma once
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -199,6 +203,75 @@ class RelativePoseError final : public CostFunction {
   double T_AB[7], sqrt_info[36];
 };
 
+// Host-evaluated residual (ABI 5, SURVEY.md §8b fallback): any cost function the GPU path has no
+// functor for (GpsErrorSynchronous / GpsErrorAsynchronous, user factors) on pose-kind (7, state pose
+// or extrinsics) and speed/bias (9) blocks, at most 2 of each, <= 15 residuals. Evaluate has the
+// ::ceres::CostFunction::Evaluate contract: ambient Jacobians (the backend applies the blocks'
+// PoseManifold), return false on failure. It is called from up to options.num_threads host threads
+// at every point the solver evaluates; CauchyLoss(1) may be attached at AddResidualBlock.
+class HostCostFunction : public CostFunction {
+ public:
+  std::string typeInfo() const override { return "HostCostFunction"; }
+  virtual bool Evaluate(double const* const* parameters, double* residuals, double** jacobians) const = 0;
+};
+
+// A ceres::CostFunction-shaped functor object (okvis' GpsErrorAsynchronous, a
+// ceres::SizedCostFunction, ...) used as a host cost function through its own getters, so the call
+// site keeps its type: F must provide Evaluate(double const* const*, double*, double**) const,
+// num_residuals() and parameter_block_sizes() (ceres::CostFunction), and typeInfo()
+// (ErrorInterface.hpp:78). The functor is not owned.
+template <class F>
+class HostFunctor final : public HostCostFunction {
+ public:
+  explicit HostFunctor(const F* functor) : f_(functor) {}
+  std::string typeInfo() const override { return f_->typeInfo(); }
+  int residualDim() const override { return (int)f_->num_residuals(); }
+  std::vector<int> parameterBlockSizes() const override {
+    const auto& s = f_->parameter_block_sizes();
+    return std::vector<int>(s.begin(), s.end());
+  }
+  bool Evaluate(double const* const* parameters, double* residuals, double** jacobians) const override {
+    return f_->Evaluate(parameters, residuals, jacobians);
+  }
+
+ private:
+  const F* f_;
+};
+
+// ---- okvis functors -> GPU-evaluated terms, through the functors' getters (templates: no okvis /
+// Eigen types are named here; anything with the getters' shape works)
+// ReprojectionError<PinholeCamera<D>>: measurement() (2-vector), information() (2x2)
+// (ReprojectionErrorBase.hpp:75-91, ReprojectionError.hpp:94-105); squareRootInformation_ =
+// LLT(information).matrixL()^T (ReprojectionError.hpp:49-57). The camera is the caller's
+// okvisgpu_camera of cameraGeometry_ (its intrinsics).
+template <class E>
+ReprojectionError fromOkvisReprojectionError(const E& e, const okvisgpu_camera& camera) {
+  const auto& m = e.measurement();
+  const auto& I = e.information();
+  const double kp[2] = {(double)m(0), (double)m(1)};
+  const double l00 = std::sqrt((double)I(0, 0)), l10 = (double)I(1, 0) / l00;
+  const double l11 = std::sqrt((double)I(1, 1) - l10 * l10);
+  const double L[4] = {l00, l10, 0.0, l11};  // L^T row-major
+  return ReprojectionError(camera, kp, L);
+}
+// ImuError: imuParameters(), imuMeasurements() (deque of Measurement<ImuSensorReadings>), t0(), t1()
+// (ImuError.hpp:89-92,216-224); time stamps through okvis::Time::toNSec().
+template <class E>
+ImuError fromOkvisImuError(const E& e) {
+  const auto& p = e.imuParameters();
+  okvisgpu_imu_params ip;
+  ip.a_max = p.a_max; ip.g_max = p.g_max; ip.sigma_g_c = p.sigma_g_c; ip.sigma_a_c = p.sigma_a_c;
+  ip.sigma_gw_c = p.sigma_gw_c; ip.sigma_aw_c = p.sigma_aw_c; ip.g = p.g;
+  std::vector<int64_t> t;
+  std::vector<double> ga;
+  for (const auto& m : e.imuMeasurements()) {
+    t.push_back((int64_t)m.timeStamp.toNSec());
+    for (int k = 0; k < 3; ++k) ga.push_back((double)m.measurement.gyroscopes(k));
+    for (int k = 0; k < 3; ++k) ga.push_back((double)m.measurement.accelerometers(k));
+  }
+  return ImuError(std::move(t), std::move(ga), ip, (int64_t)e.t0().toNSec(), (int64_t)e.t1().toNSec());
+}
+
 // ---------------------------------------------------------------- Problem
 struct ResidualBlock;
 using ResidualBlockId = ResidualBlock*;
@@ -267,9 +340,23 @@ class Problem {
     static const std::set<std::string> known = {"ReprojectionError", "ImuError", "PoseError", "SpeedAndBiasError",
                                                 "TwoPoseStandardGraphError", "TwoPoseStandardGraphErrorConst",
                                                 "RelativePoseError"};
-    if (!known.count(t)) throw Unsupported("cost function \"" + t + "\" has no GPU evaluation (keep the Ceres solve)");
-    if (loss && t != "ReprojectionError") throw Unsupported(t + " with a loss function (okvis adds none)");
+    const bool host = dynamic_cast<const HostCostFunction*>(cost) != nullptr;
+    if (!host && !known.count(t))
+      throw Unsupported("cost function \"" + t + "\" has no GPU evaluation (wrap it in a HostCostFunction)");
+    if (loss && !host && t != "ReprojectionError") throw Unsupported(t + " with a loss function (okvis adds none)");
     const std::vector<int> sizes = cost->parameterBlockSizes();
+    if (host) {  // the §8b fallback's limits (okvisgpu.h host_*)
+      int np = 0, ns = 0;
+      for (int s : sizes) {
+        if (s == 7) ++np;
+        else if (s == 9) ++ns;
+        else throw Unsupported(t + ": host-evaluated blocks must be pose-kind (7) or speed/bias (9)");
+      }
+      if (np > 2 || ns > 2 || sizes.empty())
+        throw Unsupported(t + ": host-evaluated factors take 1-4 blocks, at most 2 of each kind");
+      if (cost->residualDim() < 1 || cost->residualDim() > OKVISGPU_HOST_MAX_RESIDUALS)
+        throw Unsupported(t + ": host-evaluated factors have 1-15 residuals");
+    }
     if (sizes.size() != blocks.size()) throw Error("AddResidualBlock: " + t + " expects " + std::to_string(sizes.size()) + " blocks");
     for (size_t k = 0; k < blocks.size(); ++k) {
       auto it = params_.find(blocks[k]);
@@ -559,6 +646,32 @@ class Problem {
         if (extrPtr_[i] == e) { ci = (int)i; break; }
       A_.ep_cam.push_back(ci);
     }
+    // host-evaluated residuals: blocks as (kind, index) in the functor's order; an extrinsics block
+    // is the pose-kind block n_poses + camera
+    hostTerms_.clear();
+    for (const auto& r : residuals_) {
+      const auto* h = dynamic_cast<const HostCostFunction*>(r->cost);
+      if (!h) continue;
+      int32_t kind[4] = {-1, -1, -1, -1}, idx[4] = {-1, -1, -1, -1};
+      for (size_t k = 0; k < r->blocks.size(); ++k) {
+        double* b = r->blocks[k];
+        if (params_[b].size == 9) {
+          kind[k] = 1;
+          idx[k] = indexIn(sbIdx_, b);
+          continue;
+        }
+        kind[k] = 0;
+        if ((idx[k] = indexIn(poseIdx_, b)) >= 0) continue;
+        const int c = extrinsicsCamera(b);
+        if (c < 0) throw Unsupported(h->typeInfo() + ": an extrinsics block shared by several cameras");
+        idx[k] = (int32_t)posePtr_.size() + c;
+      }
+      A_.host_kind.insert(A_.host_kind.end(), kind, kind + 4);
+      A_.host_index.insert(A_.host_index.end(), idx, idx + 4);
+      A_.host_dim.push_back(h->residualDim());
+      A_.host_cauchy.push_back(r->loss != nullptr);
+      hostTerms_.push_back(h);
+    }
     gatherValues();
     okvisgpu_problem& P = view_;
     std::memset(&P, 0, sizeof(P));
@@ -609,7 +722,22 @@ class Problem {
     P.extrinsics_prior_camera = A_.ep_cam.data();
     P.extrinsics_prior_meas = A_.ep_meas.data();
     P.extrinsics_prior_sqrt_info = A_.ep_L.data();
+    P.n_host = (int32_t)hostTerms_.size();
+    P.host_dim = A_.host_dim.data();
+    P.host_param_kind = A_.host_kind.data();
+    P.host_param_index = A_.host_index.data();
+    P.host_cauchy = A_.host_cauchy.data();
+    P.host_evaluate = &Problem::hostTrampoline;
+    P.host_user = this;
     built_ = true;
+  }
+  static int hostTrampoline(void* user, int32_t factor, const double* const* parameters, double* residuals,
+                            double** jacobians) {
+    try {
+      return static_cast<const Problem*>(user)->hostTerms_[factor]->Evaluate(parameters, residuals, jacobians) ? 1 : 0;
+    } catch (...) {  // no exception crosses the C ABI: an evaluation failure
+      return 0;
+    }
   }
   // caller's parameter memory -> SoA (before a solve)
   void gatherValues() {
@@ -639,8 +767,9 @@ class Problem {
   struct Arrays {
     std::vector<double> pose, sb, lm, extr, obs_kp, obs_L, imu_ga, imu_state, pp_meas, pp_L, sbp_meas, sbp_L, rp_dx,
         rp_J, rp_lp, ep_meas, ep_L;
-    std::vector<uint8_t> pose_c, sb_c, lm_c, extr_c, obs_cauchy, rp_kind;
-    std::vector<int32_t> obs_pose, obs_lm, obs_cam, imu_blocks, imu_begin, pp_block, sbp_block, rp_blocks, ep_cam;
+    std::vector<uint8_t> pose_c, sb_c, lm_c, extr_c, obs_cauchy, rp_kind, host_cauchy;
+    std::vector<int32_t> obs_pose, obs_lm, obs_cam, imu_blocks, imu_begin, pp_block, sbp_block, rp_blocks, ep_cam,
+        host_kind, host_index, host_dim;
     std::vector<int64_t> imu_t0, imu_t1, imu_ts;
     std::vector<okvisgpu_camera> cams;
     std::vector<double*> ep_cam_ptr;
@@ -657,6 +786,7 @@ class Problem {
   std::map<double*, int> poseIdx_, sbIdx_, lmIdx_;
   std::vector<double*> posePtr_, sbPtr_, lmPtr_, extrPtr_;
   std::vector<ImuError*> imuTerms_;
+  std::vector<const HostCostFunction*> hostTerms_;
   Arrays A_;
   okvisgpu_problem view_{};
 };

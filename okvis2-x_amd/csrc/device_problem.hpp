@@ -21,6 +21,10 @@ constexpr int kCamDoubles = 13;       // per camera on the device: dist, fu, fv,
 constexpr int kTile = 64;             // Cholesky tile (one 64x64 FP64 tile = 32 KiB of LDS)
 constexpr int kImuLin = 15 + 15 * 30; // per-IMU-factor linearisation record: r[15], J[15][30]
 constexpr int kImuState = 526;        // == OKVISGPU_IMU_STATE_DOUBLES
+// host-evaluated factor records: in = live flag (0 idle, 1 + linearisation buffer) | pad | slot
+// values pose0 (7) @8, sb0 (9) @15, pose1 (7) @24, sb1 (9) @31; out = cost | r[15] | J[15][30]
+constexpr int kHostIn = 40;
+constexpr int kHostOut = 1 + kImuLin;
 
 // Linearisation record per observation (structure of arrays, plane-major):
 //   plane 0-1: r (Cauchy-corrected)   plane 2-13: J_pose 2x6   plane 14-19: J_lm 2x3
@@ -168,10 +172,14 @@ struct DevProblem {
   const int32_t* pe_obs;
   double* pe_H;                    // [n_pe][36] sum J_e^T J_p (row-major, rows = extrinsics)
 
-  // --- IMU factors
-  const int32_t* imu_blocks;       // [n_imu][4] global pose0 sb0 pose1 sb1
-  const int32_t* imu_win;
-  const uint8_t* imu_flags;        // bit1 fixed
+  // --- IMU factors [0, n_imu) and host-evaluated factors [n_imu, n_fac) (okvisgpu_problem host_*,
+  // ABI 5): both are <= 15-row factors on <= 2 pose-kind + 2 speed/bias blocks in the same column
+  // layout, so the linearisation, J^T J, assembly, J*v and cost kernels treat them alike; only the
+  // evaluation differs (k_eval_imu on the device; k_host_gather -> host callback -> k_host_scatter)
+  int32_t n_host, n_fac;
+  const int32_t* imu_blocks;       // [n_fac][4] global pose0 sb0 pose1 sb1 (host factors: -1 = unused slot)
+  const int32_t* imu_win;          // [n_fac]
+  const uint8_t* imu_flags;        // [n_fac] bit1 fixed
   const int64_t* imu_t0;
   const int64_t* imu_t1;
   const int32_t* imu_sbegin;       // [n_imu+1]
@@ -179,10 +187,13 @@ struct DevProblem {
   const double* imu_ga;            // [n_samples][6]
   const double* imu_par;           // [n_win][7]: a_max g_max sigma_g_c sigma_a_c sigma_gw_c sigma_aw_c g
   double* imu_state;               // [n_imu][kImuState]
-  double* imu_lin[2];              // [n_imu][kImuLin]
-  double* imu_cost[2];             // [n_imu]
-  double* imu_H;                   // [n_imu][kImuHess] of the linearisation lin[lcur] (k_imu_hess)
-  double* imu_jv;                  // [3][n_imu]
+  double* imu_lin[2];              // [n_fac][kImuLin]
+  double* imu_cost[2];             // [n_fac]
+  double* imu_H;                   // [n_fac][kImuHess] of the linearisation lin[lcur] (k_imu_hess)
+  double* imu_jv;                  // [3][n_fac]
+  const int32_t* win_host_range;   // [n_win][2] host factors of the window (global factor indices)
+  double* host_in;                 // [n_host][kHostIn] gathered evaluation points (k_host_gather)
+  double* host_out;                // [n_host][kHostOut] host results, uploaded (k_host_scatter)
 
   // --- priors
   const int32_t* pp_block;         // [n_pprior] global pose

@@ -108,13 +108,15 @@ __global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp) {
   // before they are issued. Lane r holds row r of the 15x30 Jacobian; lanes r and r + 16 of the
   // group form the scaled direction vectors of columns r and r + 16, exchanged through LDS.
   __shared__ double sVc[256 / 16][32][2];
-  if (gid < P.n_imu) {
+  if (gid < P.n_fac) {
     const int f = gid, grp = threadIdx.x >> 4;
     const int fw = gmem(P.imu_win)[f], ffl = gmem(P.imu_flags)[f];
     const int4 blk = gmem(reinterpret_cast<const int4*>(P.imu_blocks))[f];
     const auto gst = gmem(P.st + fw);
     const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed, lcur = gst->lcur;
-    const int o0 = gmem(P.pose_f)[blk.x], o1 = gmem(P.sb_f)[blk.y], o2 = gmem(P.pose_f)[blk.z], o3 = gmem(P.sb_f)[blk.w];
+    // (a host-evaluated factor marks unused slots -1: clamped load, offset -1)
+    const int o0 = blk.x < 0 ? -1 : gmem(P.pose_f)[max(blk.x, 0)], o1 = blk.y < 0 ? -1 : gmem(P.sb_f)[max(blk.y, 0)],
+              o2 = blk.z < 0 ? -1 : gmem(P.pose_f)[max(blk.z, 0)], o3 = blk.w < 0 ? -1 : gmem(P.sb_f)[max(blk.w, 0)];
     const int foff = gmem(P.win_foff)[fw];
     const bool fl = (sDone == 0) & (sNeed != 0) & (sFail == 0), act = fl & !(ffl & 2);
     // this lane's two columns (c = r, r + 16 < 30): block offset and position
@@ -156,11 +158,11 @@ __global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp) {
 #pragma unroll
       for (int m = 8; m > 0; m >>= 1) a3[k] += __shfl_xor(a3[k], m, 64);
     if (fl && r == 0)
-      for (int k = 0; k < 3; ++k) P.imu_jv[(size_t)k * P.n_imu + f] = a3[k];
+      for (int k = 0; k < 3; ++k) P.imu_jv[(size_t)k * P.n_fac + f] = a3[k];
     return;
   }
-  if (u < P.n_imu) {
-  } else if ((u -= P.n_imu) < P.n_pprior) {
+  if (u < P.n_fac) {
+  } else if ((u -= P.n_fac) < P.n_pprior) {
     w = P.pp_win[u];
     if (jvSelect(P, w)) {
       live = true;
@@ -238,6 +240,7 @@ __device__ void finalizeIteration(const DevProblem& P, WinState& s) {
 __device__ double reduceJv(const DevProblem& P, int w, WinState& s, double* sh) {
   const int t = threadIdx.x;
   const int ib = P.win_imu_range[2 * w], ie = P.win_imu_range[2 * w + 1];
+  const int hb = P.win_host_range[2 * w], he = P.win_host_range[2 * w + 1];
   const int pb = P.win_pp_range[2 * w], pe = P.win_pp_range[2 * w + 1];
   const int sbb = P.win_sbp_range[2 * w], sbe = P.win_sbp_range[2 * w + 1];
   const int rpb = P.win_rp_range[2 * w], rpe = P.win_rp_range[2 * w + 1];
@@ -247,7 +250,8 @@ __device__ double reduceJv(const DevProblem& P, int w, WinState& s, double* sh) 
   for (int k = 0; k < 3; ++k) {
     double acc = 0.0;
     for (int g = gb + t; g < ge; g += kRB) acc += P.grp_red[(size_t)g * kGrpRed + k];
-    for (int f = ib + t; f < ie; f += kRB) acc += P.imu_jv[(size_t)k * P.n_imu + f];
+    for (int f = ib + t; f < ie; f += kRB) acc += P.imu_jv[(size_t)k * P.n_fac + f];
+    for (int f = hb + t; f < he; f += kRB) acc += P.imu_jv[(size_t)k * P.n_fac + f];
     for (int i = pb + t; i < pe; i += kRB) acc += P.pp_jv[(size_t)k * P.n_pprior + i];
     for (int i = sbb + t; i < sbe; i += kRB) acc += P.sbp_jv[(size_t)k * P.n_sbprior + i];
     for (int i = rpb + t; i < rpe; i += kRB) acc += P.rp_jv[(size_t)k * P.n_relpose + i];
@@ -294,6 +298,11 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
                         else c += v.c;
                       });
     for (int f = ib + t; f < ie; f += kRB) {
+      if (P.imu_flags[f] & 2) cf += P.imu_cost[lb][f];
+      else c += P.imu_cost[lb][f];
+    }
+    const int hb = P.win_host_range[2 * w], he = P.win_host_range[2 * w + 1];
+    for (int f = hb + t; f < he; f += kRB) {
       if (P.imu_flags[f] & 2) cf += P.imu_cost[lb][f];
       else c += P.imu_cost[lb][f];
     }
@@ -663,7 +672,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
 }
 
 void launch_jv(const DevProblem& P, hipStream_t s) {
-  const int n = P.n_imu + P.n_pprior + P.n_sbprior + P.n_relpose;  // 16-lane groups
+  const int n = P.n_fac + P.n_pprior + P.n_sbprior + P.n_relpose;  // 16-lane groups
   if (n > 0) hipLaunchKernelGGL(k_jv, dim3((n + 15) / 16), dim3(256), 0, s, P.self);
 }
 void launch_reduce(const DevProblem& P, int mode, hipStream_t s) {

@@ -1139,6 +1139,58 @@ __global__ __launch_bounds__(64) void k_eval_priors(const DevProblem* __restrict
   P.rp_cost[lb][k] = 0.5 * c;
 }
 
+// ------------------------------------------------------------------- host-evaluated factors (ABI 5)
+// The §8b fallback: k_host_gather packs the evaluation point of every host factor the eval mode
+// selects (evalSelect of k_eval_imu: window running, candidate pending for mode 1, fixed factors at
+// the initial point only) into host_in; the runtime copies it to pinned memory, evaluates the
+// callbacks on host threads (runtime.cpp HostEval) and copies the results back into host_out;
+// k_host_scatter then writes r, J and the cost into the factor's IMU-layout linearisation record,
+// from where the J^T J, assembly, J*v and cost kernels take it like an IMU factor's.
+__global__ __launch_bounds__(64) void k_host_gather(const DevProblem* __restrict__ Pp, int mode) {
+  const DevProblem& P = *Pp;
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= P.n_host) return;
+  const int f = P.n_imu + h;
+  const int w = P.imu_win[f], fl = P.imu_flags[f];
+  const WinState& s = P.st[w];
+  const bool live = !s.done && (mode != 1 || s.eval_cand) && !((fl & 2) && mode < 2);
+  const int xs = mode == 1 ? 1 - s.xcur : s.xcur, lb = mode == 1 ? 1 - s.lcur : s.lcur;
+  double* in = P.host_in + (size_t)h * kHostIn;
+  in[0] = live ? 1.0 + lb : 0.0;
+  in[1] = (double)mode;
+  if (!live) return;
+  const int4 blk = reinterpret_cast<const int4*>(P.imu_blocks)[f];
+  const int slot[4] = {blk.x, blk.y, blk.z, blk.w};
+  const int at[4] = {8, 15, 24, 31};
+  for (int q = 0; q < 4; ++q) {
+    if (slot[q] < 0) continue;
+    const int n = (q & 1) ? 9 : 7;
+    const double* src = ((q & 1) ? P.sb[xs] : P.pose[xs]) + (size_t)n * slot[q];
+    for (int k = 0; k < n; ++k) in[at[q] + k] = src[k];
+  }
+}
+
+// One wavefront per host factor: the uploaded cost | r | J into lin[lb] / cost[lb].
+__global__ __launch_bounds__(256) void k_host_scatter(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
+  const int h = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (h >= P.n_host) return;
+  const double flag = P.host_in[(size_t)h * kHostIn];
+  if (flag == 0.0) return;
+  const int lb = (int)flag - 1, f = P.n_imu + h;
+  const double* out = P.host_out + (size_t)h * kHostOut;
+  double* lin = P.imu_lin[lb] + (size_t)f * kImuLin;
+  for (int e = lane; e < kImuLin; e += 64) lin[e] = out[1 + e];
+  if (lane == 0) P.imu_cost[lb][f] = out[0];
+}
+
+void launch_host_gather(const DevProblem& P, int mode, hipStream_t s) {
+  if (P.n_host > 0) hipLaunchKernelGGL(k_host_gather, dim3((P.n_host + 63) / 64), dim3(64), 0, s, P.self, mode);
+}
+void launch_host_scatter(const DevProblem& P, hipStream_t s) {
+  if (P.n_host > 0) hipLaunchKernelGGL(k_host_scatter, dim3((P.n_host + 3) / 4), dim3(256), 0, s, P.self);
+}
+
 // ------------------------------------------------------------------------------------ launchers
 void launch_eval_obs(const DevProblem& P, int mode, hipStream_t s) {
   if (P.n_obs > 0) hipLaunchKernelGGL(k_eval_obs, dim3((P.n_obs + 255) / 256), dim3(256), 0, s, P.self, mode);

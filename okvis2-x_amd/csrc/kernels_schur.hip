@@ -608,7 +608,7 @@ __global__ __launch_bounds__(256) void k_imu_hess(const DevProblem* __restrict__
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int f = blockIdx.x * 4 + wv;
   __shared__ double sJ[4][kImuLin];
-  if (f >= P.n_imu) return;
+  if (f >= P.n_fac) return;
   const int w = P.imu_win[f];
   if (!linSelect(P, w, lin_mode) || (P.imu_flags[f] & 2)) return;
   const auto L = gmem(P.imu_lin[P.st[w].lcur] + (size_t)f * kImuLin);
@@ -1135,7 +1135,7 @@ void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s) {
                        lin_mode);
 }
 void launch_imu_hess(const DevProblem& P, int lin_mode, hipStream_t s) {
-  if (P.n_imu > 0) hipLaunchKernelGGL(k_imu_hess, dim3((P.n_imu + 3) / 4), dim3(256), 0, s, P.self, lin_mode);
+  if (P.n_fac > 0) hipLaunchKernelGGL(k_imu_hess, dim3((P.n_fac + 3) / 4), dim3(256), 0, s, P.self, lin_mode);
 }
 void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
   launch_lm_blocks(P, lin_mode, s);

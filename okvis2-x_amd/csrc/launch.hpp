@@ -16,6 +16,10 @@ void launch_eval_priors(const DevProblem& P, int mode, hipStream_t s);
 // ImuError::append for a batch (P: n_imu, imu_blocks {0, f, 0, f}, imu_t0 = old t1, imu_t1 = new t1,
 // imu_sbegin / imu_ts / imu_ga = appended samples, imu_par (one row), imu_state, sb[0] = biases)
 void launch_imu_append(const DevProblem& P, hipStream_t s);
+// host-evaluated factors: gather the evaluation points (host_in), scatter the uploaded results
+// (host_out) into the linearisation records; the host step between them is the runtime's
+void launch_host_gather(const DevProblem& P, int mode, hipStream_t s);
+void launch_host_scatter(const DevProblem& P, hipStream_t s);
 
 // landmark / reduced-system kernels (kernels_schur.hip); lin_mode 0 = init, 1 = accepted only
 void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t s);

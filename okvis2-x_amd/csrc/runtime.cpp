@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <cfloat>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -115,6 +117,13 @@ struct HostBatch {
   std::vector<uint8_t> imu_flags;
   std::vector<int64_t> imu_t0, imu_t1, imu_ts;
   std::vector<double> imu_ga, imu_par, imu_state;
+  // host-evaluated factors (ABI 5): global factor index n_imu_total + h, after every IMU factor;
+  // slot[k] = IMU-layout slot (0 pose0, 1 sb0, 2 pose1, 3 sb1) of the functor's k-th block
+  struct HostFactor { int win, local, np, dim; int8_t slot[4]; uint8_t cauchy; };
+  int n_imu_total = 0;
+  std::vector<HostFactor> hf;
+  std::vector<int32_t> host_blocks, host_win, win_host_range;
+  std::vector<uint8_t> host_flags;
   // priors
   std::vector<int32_t> pp_block, pp_win, sbp_block, sbp_win;
   std::vector<double> pp_meas, pp_L, sbp_meas, sbp_L;
@@ -202,6 +211,40 @@ void validate(const okvisgpu_problem* p, int w) {
       if (p->relpose_kind && p->relpose_kind[i] > 1) bad("unknown relative-pose kind");
     }
   }
+  if (p->n_host < 0) bad("negative count");
+  if (p->n_host) {
+    if (!p->host_dim || !p->host_param_kind || !p->host_param_index || !p->host_evaluate)
+      bad("host factor arrays / host_evaluate missing");
+    for (int h = 0; h < p->n_host; ++h) {
+      const std::string f = "host factor " + std::to_string(h) + ": ";
+      if (p->host_dim[h] < 1 || p->host_dim[h] > OKVISGPU_HOST_MAX_RESIDUALS) bad(f + "residual dimension out of range");
+      int np = 0, ns = 0, nb = 0;
+      for (int k = 0; k < 4; ++k) {
+        const int kind = p->host_param_kind[4 * h + k], idx = p->host_param_index[4 * h + k];
+        if (kind < 0) break;
+        ++nb;
+        if (kind == 0) {
+          if (idx < 0 || idx >= p->n_poses + p->n_cameras) bad(f + "pose-kind block out of range");
+          ++np;
+        } else if (kind == 1) {
+          if (idx < 0 || idx >= p->n_speed_biases) bad(f + "speed/bias block out of range");
+          ++ns;
+        } else {
+          throw UnsupportedError{"window " + std::to_string(w) + ": " + f +
+                                 "only pose-kind and speed/bias blocks can be host-evaluated"};
+        }
+        for (int j = 0; j < k; ++j)
+          if (p->host_param_kind[4 * h + j] == kind && p->host_param_index[4 * h + j] == idx)
+            bad(f + "parameter block repeated");
+      }
+      for (int k = nb; k < 4; ++k)
+        if (p->host_param_kind[4 * h + k] >= 0) bad(f + "parameter blocks must be leading (kind -1 = none)");
+      if (nb == 0) bad(f + "no parameter block");
+      if (np > 2 || ns > 2)
+        throw UnsupportedError{"window " + std::to_string(w) + ": " + f +
+                               "more than 2 pose-kind or 2 speed/bias blocks"};
+    }
+  }
 }
 
 // Development: host-time split of analyse() (OKG_ANALYSE_TIMING, scripts/analyse_bench.cpp).
@@ -243,6 +286,8 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     B.lm_win.reserve(nl);
     B.lm_free.reserve(nl);
   }
+  B.n_imu_total = 0;  // host factors are numbered after every IMU factor of the batch
+  for (const okvisgpu_problem* p : probs) B.n_imu_total += std::max(0, p->n_imu);
   for (int w = 0; w < B.n_win; ++w) {
     ATIME(0)
     const okvisgpu_problem* p = probs[w];
@@ -339,6 +384,30 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       rfix[i] = pc[a] && pc[b];
       if (!pc[a]) pa[a] = 1;
       if (!pc[b]) pa[b] = 1;
+    }
+    // host-evaluated factors: IMU-layout slots (pose-kind blocks fill slots 0 then 2, speed/bias
+    // blocks 1 then 3, in the functor's order) and window-local block per slot (-1 unused)
+    const int hfBase = (int)B.hf.size();
+    std::vector<std::array<int, 4>> hslot(p->n_host);
+    std::vector<uint8_t> hfix(p->n_host);
+    for (int h = 0; h < p->n_host; ++h) {
+      HostBatch::HostFactor F{w, h, 0, p->host_dim[h], {-1, -1, -1, -1}, (uint8_t)(p->host_cauchy && p->host_cauchy[h])};
+      std::array<int, 4>& s = hslot[h];
+      s = {-1, -1, -1, -1};
+      int npk = 0, nsb = 0;
+      bool allConst = true;
+      for (int k = 0; k < 4 && p->host_param_kind[4 * h + k] >= 0; ++k) {
+        const int kind = p->host_param_kind[4 * h + k], idx = p->host_param_index[4 * h + k];
+        const int q = kind == 0 ? 2 * npk++ : 1 + 2 * nsb++;
+        F.slot[k] = (int8_t)q;
+        F.np = k + 1;
+        s[q] = idx;
+        const bool c = kind == 0 ? pc[idx] != 0 : sc[idx] != 0;
+        allConst = allConst && c;
+        if (!c) (kind == 0 ? pa[idx] : sa[idx]) = 1;
+      }
+      hfix[h] = allConst;
+      B.hf.push_back(F);
     }
     // f-blocks in the reduced ordering: pose i, then speed/bias i
     std::vector<int> posef(npx, -1), sbf(p->n_speed_biases, -1), poseFb(npx, -1), sbFb(p->n_speed_biases, -1);
@@ -646,6 +715,20 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       if (p->imu_state) appendN(B.imu_state, &p->imu_state[(size_t)f * OKVISGPU_IMU_STATE_DOUBLES], OKVISGPU_IMU_STATE_DOUBLES);
       else B.imu_state.insert(B.imu_state.end(), OKVISGPU_IMU_STATE_DOUBLES, 0.0);
     }
+    // host-evaluated factors (global pose-kind / speed-bias indices per slot)
+    const int hgBase = B.n_imu_total + hfBase;  // global factor index of this window's first
+    for (int h = 0; h < p->n_host; ++h) {
+      const std::array<int, 4>& s = hslot[h];
+      const int32_t gb[4] = {s[0] < 0 ? -1 : pb + s[0], s[1] < 0 ? -1 : sbb + s[1], s[2] < 0 ? -1 : pb + s[2],
+                             s[3] < 0 ? -1 : sbb + s[3]};
+      appendN(B.host_blocks, gb, 4);
+      B.host_win.push_back(w);
+      B.host_flags.push_back(hfix[h] ? 2 : 0);
+    }
+    {
+      const int r_host[2] = {hgBase, hgBase + p->n_host};
+      appendN(B.win_host_range, r_host, 2);
+    }
     // priors
     for (const PPrior& q : pps) {
       B.pp_block.push_back(pb + q.blk);
@@ -695,6 +778,18 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       for (int q = 0; q < 4; ++q)
         if (fbs[q] >= 0) fbc[fbs[q] - fbBase].push_back(Contrib{C_IMU, ib + f, imuCol[q], imuCol[q]});
     }
+    // host factors' slot f-blocks (-1: unused slot or constant block)
+    auto hostFbs = [&](int h, int* fbs) {
+      const std::array<int, 4>& s = hslot[h];
+      for (int q = 0; q < 4; ++q) fbs[q] = s[q] < 0 ? -1 : (q & 1) ? sbFb[s[q]] : poseFb[s[q]];
+    };
+    for (int h = 0; h < p->n_host; ++h) {
+      if (hfix[h]) continue;
+      int fbs[4];
+      hostFbs(h, fbs);
+      for (int q = 0; q < 4; ++q)
+        if (fbs[q] >= 0) fbc[fbs[q] - fbBase].push_back(Contrib{C_IMU, hgBase + h, imuCol[q], imuCol[q]});
+    }
     for (size_t i = 0; i < pps.size(); ++i) {
       const int fb = poseFb[pps[i].blk];
       if (fb >= 0) fbc[fb - fbBase].push_back(Contrib{C_PPRIOR, ppb + (int)i, 0, 0});
@@ -736,6 +831,17 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
           if (fbs[u] < 0 || fbs[v] < 0) continue;
           if (B.fb_off[fbs[u]] < B.fb_off[fbs[v]]) continue;
           pairs[key(fbs[u], fbs[v])].push_back(Contrib{C_IMU, ib + f, imuCol[u], imuCol[v]});
+        }
+    }
+    for (int h = 0; h < p->n_host; ++h) {
+      if (hfix[h]) continue;
+      int fbs[4];
+      hostFbs(h, fbs);
+      for (int u = 0; u < 4; ++u)
+        for (int v = 0; v < 4; ++v) {
+          if (fbs[u] < 0 || fbs[v] < 0) continue;
+          if (B.fb_off[fbs[u]] < B.fb_off[fbs[v]]) continue;
+          pairs[key(fbs[u], fbs[v])].push_back(Contrib{C_IMU, hgBase + h, imuCol[u], imuCol[v]});
         }
     }
     for (size_t i = 0; i < pps.size(); ++i) {
@@ -915,6 +1021,10 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
   B.part_cbegin.push_back((int)B.part_contrib.size());
   B.visit_obs_begin.push_back((int)B.obs_win.size());
   B.imu_sbegin.push_back((int)B.imu_ts.size());
+  // host-evaluated factors share the IMU factors' per-factor arrays, after all of them
+  B.imu_blocks.insert(B.imu_blocks.end(), B.host_blocks.begin(), B.host_blocks.end());
+  B.imu_win.insert(B.imu_win.end(), B.host_win.begin(), B.host_win.end());
+  B.imu_flags.insert(B.imu_flags.end(), B.host_flags.begin(), B.host_flags.end());
   B.fb_cbegin.push_back((int)B.fb_contrib.size());
   B.pair_cbegin.push_back((int)B.pair_contrib.size());
   {  // per-group record (two 16-byte loads; the terminal entry closes the last group)
@@ -977,6 +1087,12 @@ struct okvisgpu_ctx {
   okvisgpu_options opts{};
   int replays = 0;
   double solveT0 = 0.0;
+  // host-evaluated factors (ABI 5): pinned copies of host_in / host_out and per-factor failure
+  // flags of the last evaluation, written by hostEvaluate() on the HIP callback thread
+  double* hostIn = nullptr;
+  double* hostOut = nullptr;
+  int hostBufFactors = 0;
+  std::vector<uint8_t> hostFail;
 
   void fillSummaries(const std::vector<WinState>& st, okvisgpu_summary* sums) {
     if (!sums) return;
@@ -1001,6 +1117,8 @@ struct okvisgpu_ctx {
     if (iterGraph) (void)hipGraphExecDestroy(iterGraph);
     if (arena) (void)hipFree(arena);
     if (hostStage) (void)hipHostFree(hostStage);
+    if (hostIn) (void)hipHostFree(hostIn);
+    if (hostOut) (void)hipHostFree(hostOut);
     for (hipEvent_t e : forkEv) (void)hipEventDestroy(e);
     for (hipStream_t q : side)
       if (q) (void)hipStreamDestroy(q);
@@ -1012,6 +1130,147 @@ struct okvisgpu_ctx {
       (void)hipGraphExecDestroy(iterGraph);
       iterGraph = nullptr;
     }
+  }
+
+  // ---- host-evaluated factors (SURVEY.md §8b fallback) ------------------------------------------
+  // Every evaluation point (initial, each candidate) runs, in stream order: k_host_gather (the
+  // blocks' values of the factors the eval mode selects) -> copy to pinned memory -> host node
+  // (hostEvaluate: the caller's Evaluate on options.num_threads threads, manifold + loss applied
+  // here) -> copy back -> k_host_scatter into the IMU-layout linearisation records. All of it is
+  // graph-capturable (the host step is a host node of the captured iteration).
+  void ensureHostBuffers() {
+    hostFail.assign((size_t)P.n_host, 0);
+    if (P.n_host <= hostBufFactors) return;
+    if (hostIn) HIPCHK(hipHostFree(hostIn));
+    if (hostOut) HIPCHK(hipHostFree(hostOut));
+    hostIn = hostOut = nullptr;
+    hostBufFactors = 0;
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&hostIn), sizeof(double) * kHostIn * P.n_host, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&hostOut), sizeof(double) * kHostOut * P.n_host, hipHostMallocDefault));
+    hostBufFactors = P.n_host;
+  }
+
+  // PoseManifold plus Jacobian at x, 7x6 row-major (PoseLocalParameterization.cpp:56-68): the
+  // minimal Jacobian of a pose-kind block is J_ambient * this, as Ceres applies a block's manifold.
+  static void posePlusJacobian(const double* x, double* J) {
+    for (int i = 0; i < 42; ++i) J[i] = 0.0;
+    J[0 * 6 + 0] = J[1 * 6 + 1] = J[2 * 6 + 2] = 1.0;
+    const double qx = x[3], qy = x[4], qz = x[5], qw = x[6];
+    const double Q[4][3] = {{qw, qz, -qy}, {-qz, qw, qx}, {qy, -qx, qw}, {-qx, -qy, -qz}};  // oplus(q), cols 0..2
+    for (int r = 0; r < 4; ++r)
+      for (int c = 0; c < 3; ++c) J[(3 + r) * 6 + 3 + c] = Q[r][c] * 0.5;
+  }
+
+  // One host factor: Evaluate at the gathered point; r and the minimal Jacobian (IMU column
+  // layout), Cauchy-corrected (the Corrector's rho'' < 0 branch: both scaled by sqrt(rho')) unless
+  // mode 3 (raw evaluation), into its host_out record. Failure: cost +inf, r = J = 0.
+  void hostEvaluateOne(int h) {
+    const double* in = hostIn + (size_t)h * kHostIn;
+    double* out = hostOut + (size_t)h * kHostOut;
+    if (in[0] == 0.0) return;
+    const int mode = (int)in[1];
+    const HostBatch::HostFactor& F = B.hf[h];
+    const okvisgpu_problem* p = probs[F.win];
+    static const int at[4] = {8, 15, 24, 31}, col[4] = {0, 6, 15, 21};
+    const double* prm[4] = {nullptr, nullptr, nullptr, nullptr};
+    double amb[4][OKVISGPU_HOST_MAX_RESIDUALS * 9];
+    double* jac[4] = {nullptr, nullptr, nullptr, nullptr};
+    double r[OKVISGPU_HOST_MAX_RESIDUALS];
+    for (int k = 0; k < F.np; ++k) {
+      prm[k] = in + at[F.slot[k]];
+      jac[k] = amb[k];
+      std::memset(amb[k], 0, sizeof(amb[k]));
+    }
+    std::memset(r, 0, sizeof(r));
+    std::memset(out, 0, sizeof(double) * kHostOut);
+    int ok = 0;
+    try {
+      ok = p->host_evaluate(p->host_user, F.local, prm, r, jac);
+    } catch (...) {
+      ok = 0;
+    }
+    hostFail[h] = ok ? 0 : 1;
+    if (!ok) {
+      out[0] = HUGE_VAL;
+      return;
+    }
+    double sq = 0.0;
+    for (int i = 0; i < F.dim; ++i) sq += r[i] * r[i];
+    double cost = 0.5 * sq, scale = 1.0;
+    if (F.cauchy && mode != 3) {  // CauchyLoss(1): rho = log(1 + s), rho' = 1 / (1 + s)
+      const double sum = 1.0 + sq, inv = 1.0 / sum;
+      cost = 0.5 * std::log(sum);
+      scale = std::sqrt(std::max(DBL_MIN, inv));
+    }
+    out[0] = cost;
+    for (int i = 0; i < F.dim; ++i) out[1 + i] = r[i] * scale;
+    double* J = out + 1 + 15;
+    for (int k = 0; k < F.np; ++k) {
+      const int q = F.slot[k];
+      if (q & 1) {  // speed/bias: identity manifold
+        for (int i = 0; i < F.dim; ++i)
+          for (int c = 0; c < 9; ++c) J[i * 30 + col[q] + c] = amb[k][i * 9 + c] * scale;
+      } else {
+        double Jp[42];
+        posePlusJacobian(prm[k], Jp);
+        for (int i = 0; i < F.dim; ++i)
+          for (int c = 0; c < 6; ++c) {
+            double s = 0.0;
+            for (int a = 0; a < 7; ++a) s += amb[k][i * 7 + a] * Jp[a * 6 + c];
+            J[i * 30 + col[q] + c] = s * scale;
+          }
+      }
+    }
+  }
+
+  void hostEvaluate() {
+    const int n = P.n_host;
+    const int nt = std::min(std::max(1, std::min(16, opts.num_threads)), n / 8);
+    if (nt <= 1) {
+      for (int h = 0; h < n; ++h) hostEvaluateOne(h);
+      return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(nt);
+    for (int t = 0; t < nt; ++t)
+      th.emplace_back([this, n, nt, t]() {
+        for (int h = (int)((int64_t)n * t / nt); h < (int)((int64_t)n * (t + 1) / nt); ++h) hostEvaluateOne(h);
+      });
+    for (auto& x : th) x.join();
+  }
+  static void hostEvaluateCallback(void* self) { static_cast<okvisgpu_ctx*>(self)->hostEvaluate(); }
+
+  void evalHost(int mode, hipStream_t s) {
+    if (P.n_host == 0) return;
+    launch_host_gather(P, mode, s);
+    HIPCHK(hipMemcpyAsync(hostIn, P.host_in, sizeof(double) * kHostIn * P.n_host, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipLaunchHostFunc(s, hostEvaluateCallback, this));
+    HIPCHK(hipMemcpyAsync(P.host_out, hostOut, sizeof(double) * kHostOut * P.n_host, hipMemcpyHostToDevice, s));
+    launch_host_scatter(P, s);
+  }
+  // every residual of the batch at one evaluation point (mode: launch.hpp)
+  void evalAll(int mode, hipStream_t s) {
+    launch_eval(P, mode, s);
+    evalHost(mode, s);
+  }
+  // after the initial evaluation: a window whose host factor failed there ends with FAILURE
+  // (Ceres: "Residual and Jacobian evaluation failed" at iteration 0)
+  void failInitialHostEvaluations() {
+    if (P.n_host == 0) return;
+    HIPCHK(hipStreamSynchronize(stream));
+    std::vector<uint8_t> bad(P.n_win, 0);
+    bool any = false;
+    for (int h = 0; h < P.n_host; ++h)
+      if (hostFail[h]) any = bad[B.hf[h].win] = 1;
+    if (!any) return;
+    std::vector<WinState> st = readStates();
+    for (int w = 0; w < P.n_win; ++w)
+      if (bad[w]) {
+        st[w].done = 1;
+        st[w].termination = OKVISGPU_FAILURE;
+      }
+    HIPCHK(hipMemcpyAsync(P.st, st.data(), sizeof(WinState) * st.size(), hipMemcpyHostToDevice, stream));
+    HIPCHK(hipStreamSynchronize(stream));
   }
 
   // (Re)build the device problem. Nothing of the previous batch survives a failure: the context
@@ -1041,7 +1300,9 @@ struct okvisgpu_ctx {
     D.n_lm = (int)B.lm_win.size();
     D.n_obs = (int)B.obs_win.size();
     D.n_visit = (int)B.visit_pose.size();
-    D.n_imu = (int)B.imu_win.size();
+    D.n_imu = B.n_imu_total;
+    D.n_host = (int)B.hf.size();
+    D.n_fac = D.n_imu + D.n_host;
     D.n_pprior = (int)B.pp_win.size();
     D.n_sbprior = (int)B.sbp_win.size();
     D.n_relpose = (int)B.rp_win.size();
@@ -1095,11 +1356,13 @@ struct okvisgpu_ctx {
                  o_imu_t0 = upl(B.imu_t0), o_imu_t1 = upl(B.imu_t1), o_imu_sb = upl(B.imu_sbegin),
                  o_imu_ts = upl(B.imu_ts), o_imu_ga = upl(B.imu_ga), o_imu_par = upl(B.imu_par),
                  o_imu_state = upl(B.imu_state);
-    const size_t o_imu_lin0 = scratch(sizeof(double) * kImuLin * D.n_imu),
-                 o_imu_lin1 = scratch(sizeof(double) * kImuLin * D.n_imu);
-    const size_t o_imu_cost0 = scratch(sizeof(double) * D.n_imu), o_imu_cost1 = scratch(sizeof(double) * D.n_imu),
-                 o_imu_jv = scratch(sizeof(double) * 3 * D.n_imu),
-                 o_imu_H = scratch(sizeof(double) * kImuHess * D.n_imu);
+    const size_t o_imu_lin0 = scratch(sizeof(double) * kImuLin * D.n_fac),
+                 o_imu_lin1 = scratch(sizeof(double) * kImuLin * D.n_fac);
+    const size_t o_imu_cost0 = scratch(sizeof(double) * D.n_fac), o_imu_cost1 = scratch(sizeof(double) * D.n_fac),
+                 o_imu_jv = scratch(sizeof(double) * 3 * D.n_fac),
+                 o_imu_H = scratch(sizeof(double) * kImuHess * D.n_fac);
+    const size_t o_whr = upl(B.win_host_range), o_host_in = scratch(sizeof(double) * kHostIn * D.n_host),
+                 o_host_out = scratch(sizeof(double) * kHostOut * D.n_host);
     const size_t o_pp_block = upl(B.pp_block), o_pp_win = upl(B.pp_win), o_pp_meas = upl(B.pp_meas),
                  o_pp_L = upl(B.pp_L);
     const size_t o_pp_lin0 = scratch(sizeof(double) * 42 * D.n_pprior), o_pp_lin1 = scratch(sizeof(double) * 42 * D.n_pprior),
@@ -1205,6 +1468,7 @@ struct okvisgpu_ctx {
     D.imu_lin[0] = dp(o_imu_lin0); D.imu_lin[1] = dp(o_imu_lin1);
     D.imu_cost[0] = dp(o_imu_cost0); D.imu_cost[1] = dp(o_imu_cost1); D.imu_jv = dp(o_imu_jv);
     D.imu_H = dp(o_imu_H);
+    D.win_host_range = ip(o_whr); D.host_in = dp(o_host_in); D.host_out = dp(o_host_out);
     D.pp_block = ip(o_pp_block); D.pp_win = ip(o_pp_win); D.pp_meas = dp(o_pp_meas); D.pp_L = dp(o_pp_L);
     D.pp_lin[0] = dp(o_pp_lin0); D.pp_lin[1] = dp(o_pp_lin1); D.pp_cost[0] = dp(o_pp_cost0);
     D.pp_cost[1] = dp(o_pp_cost1); D.pp_jv = dp(o_pp_jv);
@@ -1252,6 +1516,7 @@ struct okvisgpu_ctx {
     D.self = reinterpret_cast<const DevProblem*>(base + place(o_self));
     HIPCHK(hipStreamSynchronize(stream));
     uploadDescriptor();
+    ensureHostBuffers();
     haveProblem = true;
     structureDirty = false;
   }
@@ -1393,7 +1658,7 @@ struct okvisgpu_ctx {
   }
 
   void launchInit(int evalMode) {
-    launch_eval(P, evalMode, stream);
+    evalAll(evalMode, stream);
     launch_reduce(P, R_COST_INIT, stream);
     launch_linearization_blocks(P, 0, stream);
     launch_gradnorm(P, 0, stream);
@@ -1406,7 +1671,7 @@ struct okvisgpu_ctx {
     launch_gn_backsub(P, stream);
     launch_jv(P, stream);
     launch_dogleg(P, stream);
-    launch_eval(P, 1, stream);
+    evalAll(1, stream);
     launch_reduce(P, R_COST_CAND, stream);
     launch_linearization_blocks(P, 1, stream);
     launch_gradnorm(P, 1, stream);
@@ -1458,6 +1723,7 @@ struct okvisgpu_ctx {
     fork(side[1]);
     launch_eval_imu(P, 1, side[0]);
     launch_eval_priors(P, 1, side[1]);
+    evalHost(1, side[1]);
     launch_eval_obs(P, 1, stream);
     join(side[0]);
     join(side[1]);
@@ -1665,6 +1931,7 @@ int okvisgpu_solve_begin(okvisgpu_ctx* c, const okvisgpu_options* o) {
     c->uploadParams();
     c->resetStates(1e-8);
     c->launchInit(2);
+    c->failInitialHostEvaluations();
     c->ensureGraph();
     c->inSolve = true;
     return (int)OKVISGPU_OK;
@@ -1990,7 +2257,7 @@ int okvisgpu_evaluate(okvisgpu_ctx* c, int32_t window, double* cost) {
     okvisgpu_default_options(&o);
     c->setOptions(o);
     c->resetStates(1e-8);
-    launch_eval(c->P, 2, c->stream);
+    c->evalAll(2, c->stream);
     launch_reduce(c->P, R_COST_INIT, c->stream);
     HIPCHK(hipGetLastError());
     auto st = c->readStates();
@@ -2115,6 +2382,30 @@ int okvisgpu_eval_relpose(okvisgpu_ctx* c, int32_t window, double* r, double* J)
   });
 }
 
+int okvisgpu_eval_host(okvisgpu_ctx* c, int32_t window, double* r, double* J) {
+  if (!c) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");
+  if (window < 0 || window >= c->P.n_win) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "bad window");
+  return guarded(c, [&]() {
+    HIPCHK(hipSetDevice(c->device));
+    c->resetStates(1e-8);
+    c->evalHost(3, c->stream);
+    HIPCHK(hipGetLastError());
+    const int h0 = c->B.win_host_range[2 * window], n = c->B.win_host_range[2 * window + 1] - h0;
+    std::vector<double> lin((size_t)kImuLin * std::max(1, n));
+    if (n) HIPCHK(hipMemcpyAsync(lin.data(), c->P.imu_lin[0] + (size_t)h0 * kImuLin, (size_t)kImuLin * n * 8,
+                                 hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int f = 0; f < n; ++f) {
+      if (r) for (int i = 0; i < 15; ++i) r[15 * f + i] = lin[(size_t)f * kImuLin + i];
+      if (J) for (int i = 0; i < 450; ++i) J[450 * (size_t)f + i] = lin[(size_t)f * kImuLin + 15 + i];
+    }
+    for (int f = 0; f < n; ++f)
+      if (c->hostFail[h0 - c->P.n_imu + f]) return fail(c, OKVISGPU_ERR_NUMERICAL, "host_evaluate failed");
+    return (int)OKVISGPU_OK;
+  });
+}
+
 int okvisgpu_imu_append(okvisgpu_ctx* c, const okvisgpu_imu_append_batch* A, int32_t* steps) {
   if (!c || !A || A->n < 0) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "imu_append: bad arguments");
   if (A->n == 0) return OKVISGPU_OK;
@@ -2156,6 +2447,7 @@ int okvisgpu_imu_append(okvisgpu_ctx* c, const okvisgpu_imu_append_batch* A, int
     // a descriptor holding only what the append mode of k_eval_imu reads
     DevProblem D{};
     D.n_imu = n;
+    D.n_fac = n;
     D.imu_blocks = reinterpret_cast<const int32_t*>(base + o_blk);
     D.imu_t0 = reinterpret_cast<const int64_t*>(base + o_t0);
     D.imu_t1 = reinterpret_cast<const int64_t*>(base + o_t1);

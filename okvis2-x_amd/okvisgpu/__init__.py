@@ -42,6 +42,11 @@ class ImuParams(C.Structure):
                 ("g", C.c_double)]
 
 
+# okvisgpu_host_evaluate_fn (ABI 5): (user, factor, parameters, residuals, jacobians) -> nonzero = ok
+HOST_EVALUATE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int32, C.POINTER(_dp), _dp, C.POINTER(_dp))
+HOST_MAX_RESIDUALS = 15
+
+
 class Problem(C.Structure):
     _fields_ = [
         ("n_poses", C.c_int32), ("poses", _dp), ("pose_constant", _up),
@@ -61,7 +66,36 @@ class Problem(C.Structure):
         ("relpose_sqrt_info", _dp), ("relpose_lin_point", _dp), ("relpose_kind", _up),
         ("extrinsics_constant", _up), ("n_extrinsics_priors", C.c_int32), ("extrinsics_prior_camera", _ip),
         ("extrinsics_prior_meas", _dp), ("extrinsics_prior_sqrt_info", _dp),
+        ("n_host", C.c_int32), ("host_dim", _ip), ("host_param_kind", _ip), ("host_param_index", _ip),
+        ("host_cauchy", _up), ("host_evaluate", HOST_EVALUATE_FN), ("host_user", C.c_void_p),
     ]
+
+
+def host_evaluate(fn, block_sizes):
+    """Wrap a Python cost function as an okvisgpu_host_evaluate_fn (the §8b host fallback).
+
+    fn(factor, params) -> (r, jacobians) or None (evaluation failure): params is the list of the
+    factor's parameter blocks (numpy copies, ambient: 7 pose-kind / 9 speed-bias), r the residual
+    vector, jacobians one ambient [dim, size] array per block (ceres::CostFunction::Evaluate
+    semantics). block_sizes[factor] = the blocks' ambient sizes. Keep the returned object alive as
+    long as a problem points at it."""
+    def cb(_user, factor, params, residuals, jacobians):
+        try:
+            sizes = block_sizes[factor]
+            out = fn(factor, [np.ctypeslib.as_array(params[k], shape=(n,)).copy() for k, n in enumerate(sizes)])
+            if out is None:
+                return 0
+            r, J = out
+            r = np.asarray(r, dtype=np.float64)
+            np.ctypeslib.as_array(residuals, shape=(len(r),))[:] = r
+            if jacobians:
+                for k, n in enumerate(sizes):
+                    if jacobians[k]:
+                        np.ctypeslib.as_array(jacobians[k], shape=(len(r) * n,))[:] = np.asarray(J[k]).reshape(-1)
+            return 1
+        except Exception:  # a Python error is an evaluation failure, never an unwinding through C
+            return 0
+    return HOST_EVALUATE_FN(cb)
 
 
 class Options(C.Structure):
@@ -136,6 +170,7 @@ EXPORTED_SYMBOLS = [
     "okvisgpu_time_kernel", "okvisgpu_eval_relpose", "okvisgpu_twopose_compute",
     "okvisgpu_graph_load", "okvisgpu_graph_problem", "okvisgpu_graph_ids", "okvisgpu_graph_destroy",
     "okvisgpu_graph_save", "okvisgpu_get_stats", "okvisgpu_synth_true_extrinsics", "okvisgpu_imu_append",
+    "okvisgpu_eval_host",
 ]
 N_PHASES = 15
 
@@ -185,6 +220,7 @@ def lib():
         L.okvisgpu_kernel_name.restype = C.c_char_p
         L.okvisgpu_time_kernel.argtypes = [C.c_void_p, C.c_int32, C.c_int32, _dp, _dp, C.POINTER(C.c_int32)]
         L.okvisgpu_eval_relpose.argtypes = [C.c_void_p, C.c_int32, _dp, _dp]
+        L.okvisgpu_eval_host.argtypes = [C.c_void_p, C.c_int32, _dp, _dp]
         L.okvisgpu_graph_load.argtypes = [C.c_char_p, C.POINTER(Camera), C.c_int32, C.POINTER(ImuParams),
                                           C.POINTER(C.c_void_p)]
         L.okvisgpu_graph_problem.argtypes = [C.c_void_p]
@@ -522,6 +558,14 @@ class Context:
         r = np.zeros((n_relpose, 6))
         J = np.zeros((n_relpose, 6, 12))
         self._check(lib().okvisgpu_eval_relpose(self.h, window, dptr(r), dptr(J)), "eval_relpose")
+        return r, J
+
+    def eval_host(self, n_host, window=0):
+        """Host-evaluated factors through the device path (gather, callback, upload), no loss:
+        r [n, 15], minimal J [n, 15, 30] in the IMU column layout."""
+        r = np.zeros((n_host, 15))
+        J = np.zeros((n_host, 15, 30))
+        self._check(lib().okvisgpu_eval_host(self.h, window, dptr(r), dptr(J)), "eval_host")
         return r, J
 
     def imu_append(self, imu_params, state, t1_old, t1_new, speed_biases, sample_begin, sample_t, sample_ga):

@@ -128,6 +128,8 @@ int oracle_eval_imu(const okvisgpu_problem* p, int32_t redo_always, double* r, d
 int oracle_check_jacobians(const okvisgpu_problem* p, int32_t kind, int32_t index, double delta,
                            double* max_rel);
 int oracle_eval_relpose(const okvisgpu_problem* p, double* r, double* J /*[n][6][12] minimal*/);
+/* host-evaluated factors (ABI 5), no loss: r [n][15], J [n][15][30] minimal in the IMU column layout */
+int oracle_eval_host(const okvisgpu_problem* p, double* r, double* J);
 /* IMU-merge elimination of the state between factors f and f+1 (ViGraphEstimator.cpp:38-171):
  * factor f's ImuError (its state from p->imu_state, integrated first if never integrated) appended
  * with factor f+1's measurements up to its t1 at the speed/bias sb (ImuError::append,

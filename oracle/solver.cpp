@@ -9,6 +9,7 @@
 // Gauss-Newton step with mu in [1e-8, 1], radius update 0.25/0.75), Corrector for CauchyLoss,
 // SchurComplementSolver with dense LLT of the reduced camera matrix. Per-iterate parity with real
 // Ceres is UNPINNED (no Ceres in this container); see DESIGN.md.
+#include <atomic>
 #include <chrono>
 #include <cfloat>
 #include <condition_variable>
@@ -27,7 +28,7 @@ namespace oracle {
 namespace {
 
 enum Kind { kPose = 0, kSb = 1, kLm = 2, kExt = 3 };  // kExt: extrinsics T_SC (PoseParameterBlock + PoseManifold)
-enum RKind { rReproj = 0, rImu = 1, rPosePrior = 2, rSbPrior = 3, rRelPose = 4, rExtPrior = 5 };
+enum RKind { rReproj = 0, rImu = 1, rPosePrior = 2, rSbPrior = 3, rRelPose = 4, rExtPrior = 5, rHost = 6 };
 
 struct PBlock {
   int kind, index;
@@ -67,6 +68,7 @@ struct Program {
   std::vector<int> noERows;      // non-fixed residual blocks touching no e-block
   std::vector<double> constVals; // ambient values of constant blocks (by pblock id offset)
   std::vector<int> constOff;
+  std::atomic<int> hostFailures{0};  // host_evaluate calls that returned 0 (ABI 5 host factors)
 };
 
 const double* blockValues(const Program& P, const std::vector<double>& x, int id) {
@@ -128,6 +130,17 @@ void buildProgram(const okvisgpu_problem* p, Program& P, bool loadImuState) {
     addR(rRelPose, i, 6, {P.poseBase + p->relpose_blocks[2 * i], P.poseBase + p->relpose_blocks[2 * i + 1]});
   for (int i = 0; i < p->n_extrinsics_priors; ++i)  // PoseError on T_SC (ViGraph.cpp:372-382)
     addR(rExtPrior, i, 6, {P.extBase + p->extrinsics_prior_camera[i]});
+  // host-evaluated residual blocks (ABI 5): a user CostFunction on pose-kind / speed-bias blocks,
+  // in the functor's parameter order (Ceres ResidualBlock with the blocks' manifolds)
+  for (int h = 0; h < p->n_host; ++h) {
+    RBlock r;
+    r.kind = rHost; r.index = h; r.nres = p->host_dim[h]; r.npb = 0;
+    for (int k = 0; k < 4 && p->host_param_kind[4 * h + k] >= 0; ++k) {
+      const int kind = p->host_param_kind[4 * h + k], idx = p->host_param_index[4 * h + k];
+      r.pb[r.npb++] = kind == 1 ? P.sbBase + idx : idx < p->n_poses ? P.poseBase + idx : P.extBase + idx - p->n_poses;
+    }
+    P.rbs.push_back(r);
+  }
 
   // Active blocks (Ceres Program::RemoveFixedBlocks: unused or constant blocks removed).
   for (RBlock& r : P.rbs) {
@@ -379,6 +392,19 @@ double evalResidual(Program& P, const std::vector<double>& x, int ri, double* re
     case rRelPose:  // no loss function (ViGraphEstimator.cpp:770, ViGraph.cpp:801)
       relPoseBlockEvaluate(p, r.index, prm[0], prm[1], rr, nullptr, nullptr, ja[0], ja[1]);
       break;
+    case rHost: {  // the caller's Evaluate; Jacobians always requested (okvisgpu.h host_evaluate)
+      double* jall[4] = {ambJ[0], ambJ[1], ambJ[2], ambJ[3]};
+      for (int k = 0; k < 4; ++k) std::memset(ambJ[k], 0, sizeof(ambJ[k]));
+      for (int i = 0; i < 15; ++i) rr[i] = 0.0;
+      if (!p->host_evaluate(p->host_user, r.index, prm, rr, jall)) {  // Ceres: cost = max, step rejected
+        P.hostFailures.fetch_add(1);
+        if (res) for (int i = 0; i < r.nres; ++i) res[i] = 0.0;
+        if (jac) for (int i = 0; i < r.nres * r.jcols; ++i) jac[i] = 0.0;
+        return HUGE_VAL;
+      }
+      useLoss = p->host_cauchy ? p->host_cauchy[r.index] != 0 : false;
+      break;
+    }
   }
   double sq = 0;
   for (int i = 0; i < r.nres; ++i) sq += rr[i] * rr[i];
@@ -1009,6 +1035,17 @@ struct Minimizer {
     x_norm = vnorm(x);
     evaluateGradientAndJacobian(0);
     S->initial_cost = x_cost + fixed;
+    if (P.hostFailures.load() != 0) {  // initial evaluation failed: the solve ends there
+      S->final_cost = x_cost + fixed;
+      S->num_iterations = 0;
+      S->num_successful_steps = 1;
+      S->num_unsuccessful_steps = 0;
+      S->termination_type = OKVISGPU_FAILURE;
+      S->total_time_s = nowS() - t_start;
+      S->final_radius = radius;
+      S->final_mu = mu;
+      return;
+    }
     minimum_cost = std::numeric_limits<double>::max();
     int iteration = 0, num_succ = 0, num_unsucc = 0, consecutive_invalid = 0;
     bool step_successful = true;
@@ -1376,6 +1413,52 @@ int oracle_eval_relpose(const okvisgpu_problem* p, double* r, double* J) {
           J[72 * i + rr * 12 + c] = J0[rr * 6 + c];
           J[72 * i + rr * 12 + 6 + c] = J1[rr * 6 + c];
         }
+  }
+  return OKVISGPU_OK;
+}
+
+// Host-evaluated factors at the problem's values, no loss: r [n][15], minimal J [n][15][30] in the
+// IMU column layout (k-th pose-kind block of the functor at 0 / 15, k-th speed/bias at 6 / 21),
+// the manifold applied as Ceres' ResidualBlock does (ambient J times the plus Jacobian).
+int oracle_eval_host(const okvisgpu_problem* p, double* r, double* J) {
+  for (int h = 0; h < p->n_host; ++h) {
+    const double* prm[4] = {nullptr, nullptr, nullptr, nullptr};
+    double amb[4][15 * 9] = {};
+    double* ja[4] = {amb[0], amb[1], amb[2], amb[3]};
+    int col[4] = {0, 0, 0, 0}, kind[4] = {0, 0, 0, 0}, nb = 0, npk = 0, nsb = 0;
+    for (; nb < 4 && p->host_param_kind[4 * h + nb] >= 0; ++nb) {
+      kind[nb] = p->host_param_kind[4 * h + nb];
+      const int idx = p->host_param_index[4 * h + nb];
+      if (kind[nb] == 0) {
+        prm[nb] = idx < p->n_poses ? &p->poses[7 * idx] : &p->extrinsics[7 * (idx - p->n_poses)];
+        col[nb] = npk++ == 0 ? 0 : 15;
+      } else {
+        prm[nb] = &p->speed_biases[9 * idx];
+        col[nb] = nsb++ == 0 ? 6 : 21;
+      }
+    }
+    double rr[15] = {};
+    const int dim = p->host_dim[h];
+    if (!p->host_evaluate(p->host_user, h, prm, rr, ja)) return OKVISGPU_ERR_NUMERICAL;
+    if (r) for (int i = 0; i < 15; ++i) r[15 * h + i] = i < dim ? rr[i] : 0.0;
+    if (!J) continue;
+    double* Jh = J + 450 * (size_t)h;
+    for (int i = 0; i < 450; ++i) Jh[i] = 0.0;
+    for (int k = 0; k < nb; ++k) {
+      if (kind[k] == 1) {
+        for (int i = 0; i < dim; ++i)
+          for (int c = 0; c < 9; ++c) Jh[i * 30 + col[k] + c] = amb[k][i * 9 + c];
+        continue;
+      }
+      double Jp[42];
+      posePlusJacobian(prm[k], Jp);
+      for (int i = 0; i < dim; ++i)
+        for (int c = 0; c < 6; ++c) {
+          double s = 0;
+          for (int a = 0; a < 7; ++a) s += amb[k][i * 7 + a] * Jp[a * 6 + c];
+          Jh[i * 30 + col[k] + c] = s;
+        }
+    }
   }
   return OKVISGPU_OK;
 }

@@ -36,6 +36,7 @@ def lib():
         L.oracle_pose_minus_jacobian.argtypes = [_dp, _dp]
         L.oracle_dense_cholesky.argtypes = [C.c_int32, _dp, C.c_int32]
         L.oracle_eval_relpose.argtypes = [P, _dp, _dp]
+        L.oracle_eval_host.argtypes = [P, _dp, _dp]
         L.oracle_imu_merge.argtypes = [P, C.c_int32, _dp, _dp]
         L.oracle_twopose_compute.argtypes = [C.POINTER(og.TwoPoseEdges), _dp, _dp, _dp, _dp, _dp]
         L.oracle_imu_append.argtypes = [C.POINTER(og.ImuAppendBatch), _ip]
@@ -94,6 +95,14 @@ def eval_relpose(problem_ptr, n):
     J = np.zeros((n, 6, 12))
     lib().oracle_eval_relpose(problem_ptr, og.dptr(r), og.dptr(J))
     return r, J
+
+
+def eval_host(problem_ptr, n):
+    """Host-evaluated factors (ABI 5), no loss: r [n, 15], minimal J [n, 15, 30] (IMU column layout)."""
+    r = np.zeros((n, 15))
+    J = np.zeros((n, 15, 30))
+    rc = lib().oracle_eval_host(problem_ptr, og.dptr(r), og.dptr(J))
+    return r, J, rc
 
 
 def twopose_compute(batch):

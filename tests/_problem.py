@@ -34,10 +34,12 @@ _ARRAYS = {
     "extrinsics_prior_camera": (np.int32, (), "n_extrinsics_priors"),
     "extrinsics_prior_meas": (np.float64, (7,), "n_extrinsics_priors"),
     "extrinsics_prior_sqrt_info": (np.float64, (36,), "n_extrinsics_priors"),
+    "host_dim": (np.int32, (), "n_host"), "host_param_kind": (np.int32, (4,), "n_host"),
+    "host_param_index": (np.int32, (4,), "n_host"), "host_cauchy": (np.uint8, (), "n_host"),
 }
 _PTR = {np.float64: _dp, np.int32: _ip, np.int64: _lp, np.uint8: _up}
 _COUNTS = ("n_poses", "n_speed_biases", "n_landmarks", "n_cameras", "n_observations", "n_imu", "n_pose_priors",
-           "n_sb_priors", "n_relpose", "n_extrinsics_priors")
+           "n_sb_priors", "n_relpose", "n_extrinsics_priors", "n_host")
 
 
 class OwnedProblem:
@@ -53,6 +55,7 @@ class OwnedProblem:
         self.imu_sample_t_ns = np.zeros(0, dtype=np.int64)
         self.imu_sample_gyr_acc = np.zeros((0, 6))
         self.imu_params = og.ImuParams()
+        self.host_fn = None  # og.host_evaluate(...) callback of the host factors (ABI 5)
         self.struct = og.Problem()
         self.bind()
 
@@ -100,6 +103,8 @@ class OwnedProblem:
         s.n_sb_priors = len(self.sb_prior_block)
         s.n_relpose = len(self.relpose_blocks)
         s.n_extrinsics_priors = len(self.extrinsics_prior_camera)
+        s.n_host = len(self.host_dim)
+        s.host_evaluate = self.host_fn if self.host_fn is not None else og.HOST_EVALUATE_FN()
         if len(self.extrinsics_constant) != len(self.cameras):  # default: constant extrinsics
             self.extrinsics_constant = np.ones(len(self.cameras), np.uint8)
             s.extrinsics_constant = self.extrinsics_constant.ctypes.data_as(_up) if len(self.cameras) else None

@@ -78,11 +78,105 @@ okvisgpu_options zeroTol(int iters) {
   return o;
 }
 
-// a cost function the GPU path does not know (GPS / SubmapICP stand-in)
+// a cost function the GPU path does not know and that is no HostCostFunction either
 struct OtherError final : okvisgpu::CostFunction {
   std::string typeInfo() const override { return "GpsErrorSynchronous"; }
   int residualDim() const override { return 3; }
   std::vector<int> parameterBlockSizes() const override { return {7}; }
+};
+
+void skew(const double v[3], double S[9]) {
+  S[0] = 0; S[1] = -v[2]; S[2] = v[1]; S[3] = v[2]; S[4] = 0; S[5] = -v[0]; S[6] = -v[1]; S[7] = v[0]; S[8] = 0;
+}
+// PoseManifold lift Jacobian (6x7, PoseLocalParameterization.cpp:89-103): I3 | 2 oplus(q^-1)_{0:3,:}
+void liftJacobian(const double* T, double L[42]) {
+  for (int i = 0; i < 42; ++i) L[i] = 0.0;
+  L[0] = L[8] = L[16] = 1.0;
+  const double x = -T[3], y = -T[4], z = -T[5], w = T[6];
+  const double Q[3][4] = {{w, z, -y, x}, {-z, w, x, y}, {y, -x, w, z}};
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 4; ++c) L[(3 + r) * 7 + 3 + c] = 2.0 * Q[r][c];
+}
+
+// A ceres::SizedCostFunction<3, 7, 9, 7>-shaped functor with okvis' GpsErrorAsynchronous block
+// layout (GpsErrorAsynchronous.hpp:42-55): pose T_WS, speed/bias, alignment T_GW;
+// r = (p_meas - (R_GW (r_WS + v dt + R_WS r_SA) + r_GW)) / sigma, ambient Jacobians = minimal x lift
+// (how okvis' functors produce them). Used through okvisgpu::HostFunctor<GpsFunctor>.
+struct GpsFunctor {
+  double meas[3] = {0, 0, 0}, dt = 0.02, r_SA[3] = {0.05, -0.02, 0.1}, sigma = 0.05;
+  std::vector<int32_t> sizes{7, 9, 7};
+  std::string typeInfo() const { return "GpsErrorAsynchronous"; }
+  int num_residuals() const { return 3; }
+  const std::vector<int32_t>& parameter_block_sizes() const { return sizes; }
+  void predict(const double* T, const double* sb, const double* G, double pG[3], double a[3], double pW[3],
+               double RG[9]) const {
+    double RS[9];
+    rot(Quat{T[3], T[4], T[5], T[6]}, RS);
+    rot(Quat{G[3], G[4], G[5], G[6]}, RG);
+    for (int i = 0; i < 3; ++i) a[i] = RS[3 * i] * r_SA[0] + RS[3 * i + 1] * r_SA[1] + RS[3 * i + 2] * r_SA[2];
+    for (int i = 0; i < 3; ++i) pW[i] = T[i] + sb[i] * dt + a[i];
+    for (int i = 0; i < 3; ++i) pG[i] = RG[3 * i] * pW[0] + RG[3 * i + 1] * pW[1] + RG[3 * i + 2] * pW[2] + G[i];
+  }
+  bool Evaluate(double const* const* p, double* r, double** J) const {
+    double pG[3], a[3], pW[3], RG[9];
+    predict(p[0], p[1], p[2], pG, a, pW, RG);
+    const double s = 1.0 / sigma;
+    for (int i = 0; i < 3; ++i) r[i] = s * (meas[i] - pG[i]);
+    if (!J) return true;
+    double Sa[9], RSa[9], g[3], Sg[9];
+    skew(a, Sa);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) RSa[3 * i + j] = RG[3 * i] * Sa[j] + RG[3 * i + 1] * Sa[3 + j] + RG[3 * i + 2] * Sa[6 + j];
+    for (int i = 0; i < 3; ++i) g[i] = RG[3 * i] * pW[0] + RG[3 * i + 1] * pW[1] + RG[3 * i + 2] * pW[2];
+    skew(g, Sg);
+    double Jt[18], Jg[18];  // minimal 3x6
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        Jt[6 * i + j] = -s * RG[3 * i + j];
+        Jt[6 * i + 3 + j] = s * RSa[3 * i + j];
+        Jg[6 * i + j] = i == j ? -s : 0.0;
+        Jg[6 * i + 3 + j] = s * Sg[3 * i + j];
+      }
+    const double* mins[3] = {Jt, nullptr, Jg};
+    for (int k = 0; k < 3; k += 2) {
+      if (!J[k]) continue;
+      double L[42];
+      liftJacobian(p[k], L);
+      for (int i = 0; i < 3; ++i)
+        for (int c = 0; c < 7; ++c) {
+          double v = 0;
+          for (int m = 0; m < 6; ++m) v += mins[k][6 * i + m] * L[m * 7 + c];
+          J[k][7 * i + c] = v;
+        }
+    }
+    if (J[1])
+      for (int i = 0; i < 3; ++i)
+        for (int c = 0; c < 9; ++c) J[1][9 * i + c] = c < 3 ? -s * RG[3 * i + c] * dt : 0.0;
+    return true;
+  }
+};
+
+// okvis-shaped functor getters for the fromOkvis* adapters (Eigen-like call operators)
+struct Vec { double v[3]; double operator()(int i) const { return v[i]; } };
+struct Mat2 { double m[4]; double operator()(int r, int c) const { return m[2 * r + c]; } };
+struct MockReprojection {
+  Vec meas{{310.5, 120.25, 0}};
+  Mat2 info{{4.0, 1.0, 1.0, 9.0}};
+  const Vec& measurement() const { return meas; }
+  const Mat2& information() const { return info; }
+};
+struct MockTime { int64_t ns; int64_t toNSec() const { return ns; } };
+struct MockReadings { Vec gyroscopes, accelerometers; };
+struct MockImuMeasurement { MockTime timeStamp; MockReadings measurement; };
+struct MockImuParameters { double a_max = 176, g_max = 7.8, sigma_g_c = 12e-4, sigma_a_c = 8e-3, sigma_gw_c = 4e-6,
+                           sigma_aw_c = 4e-5, g = 9.81007; };
+struct MockImu {
+  MockImuParameters p;
+  std::vector<MockImuMeasurement> m{{{100}, {{{0.1, 0.2, 0.3}}, {{1, 2, 9.8}}}}, {{200}, {{{0.4, 0.5, 0.6}}, {{3, 4, 9.7}}}}};
+  const MockImuParameters& imuParameters() const { return p; }
+  const std::vector<MockImuMeasurement>& imuMeasurements() const { return m; }
+  MockTime t0() const { return {120}; }
+  MockTime t1() const { return {180}; }
 };
 
 // Records an okvisgpu_problem (e.g. a synthetic window) into a facade, block by block and residual
@@ -190,6 +284,59 @@ int cpuTests() {
   CHECK(v.obs_pose[2] == 1 && v.obs_landmark[1] == 1 && v.obs_cauchy[0] == 1 && v.extrinsics_constant[0] == 1);
   CHECK(v.imu_blocks[0] == 0 && v.imu_blocks[1] == 0 && v.imu_blocks[2] == 1 && v.imu_blocks[3] == 1);
   CHECK(v.imu_sample_begin[1] == 3 && v.imu_t1_ns[0] == 9000000);
+  // §8b host fallback: a ceres-shaped functor through HostFunctor<F> keeps its call site; the view
+  // carries its blocks (functor order, extrinsics as pose-kind n_poses + camera) and a trampoline
+  // that reaches the functor
+  {
+    GpsFunctor f;
+    bool hthrew = false;
+    okvisgpu::HostFunctor<GpsFunctor> hf(&f);
+    CHECK(hf.typeInfo() == "GpsErrorAsynchronous" && hf.residualDim() == 3 && hf.parameterBlockSizes().size() == 3);
+    auto rg = P.AddResidualBlock(&hf, nullptr, T0, sb0, Tsc);
+    const okvisgpu_problem& w = P.view();
+    CHECK(w.n_host == 1 && w.host_dim[0] == 3 && w.host_cauchy[0] == 0);
+    CHECK(w.host_param_kind[0] == 0 && w.host_param_kind[1] == 1 && w.host_param_kind[2] == 0 && w.host_param_kind[3] == -1);
+    CHECK(w.host_param_index[0] == 0 && w.host_param_index[1] == 0 && w.host_param_index[2] == w.n_poses);
+    const double* prm[3] = {T0, sb0, Tsc};
+    double r1[3], r2[3], Ja[21], Jb[27], Jc[21];
+    double* jac[3] = {Ja, Jb, Jc};
+    CHECK(w.host_evaluate(w.host_user, 0, prm, r1, jac) == 1);
+    f.Evaluate(prm, r2, nullptr);
+    CHECK(r1[0] == r2[0] && r1[1] == r2[1] && r1[2] == r2[2]);
+    P.RemoveResidualBlock(rg);
+    CHECK(P.view().n_host == 0);
+    // the fallback's limits: no landmark block, at most 2 pose-kind blocks
+    struct LmHost final : okvisgpu::HostCostFunction {
+      int residualDim() const override { return 1; }
+      std::vector<int> parameterBlockSizes() const override { return {7, 4}; }
+      bool Evaluate(double const* const*, double*, double**) const override { return true; }
+    } lmh;
+    struct ThreePoses final : okvisgpu::HostCostFunction {
+      int residualDim() const override { return 6; }
+      std::vector<int> parameterBlockSizes() const override { return {7, 7, 7}; }
+      bool Evaluate(double const* const*, double*, double**) const override { return true; }
+    } tp;
+    hthrew = false;
+    try { P.AddResidualBlock(&lmh, nullptr, T1, L1); } catch (const okvisgpu::Unsupported&) { hthrew = true; }
+    CHECK(hthrew);
+    hthrew = false;
+    try { P.AddResidualBlock(&tp, nullptr, T0, T1, Tsc); } catch (const okvisgpu::Unsupported&) { hthrew = true; }
+    CHECK(hthrew);
+  }
+  // okvis functors through their getters (ReprojectionErrorBase.hpp:75-91, ImuError.hpp:89-92,216-224)
+  {
+    const MockReprojection mr;
+    const okvisgpu::ReprojectionError re = okvisgpu::fromOkvisReprojectionError(mr, cam);
+    CHECK(re.keypoint[0] == 310.5 && re.keypoint[1] == 120.25);
+    const double* U = re.sqrt_info;  // U^T U = information, U upper triangular
+    CHECK(U[2] == 0.0 && std::fabs(U[0] * U[0] - 4.0) < 1e-15 && std::fabs(U[0] * U[1] - 1.0) < 1e-15 &&
+          std::fabs(U[1] * U[1] + U[3] * U[3] - 9.0) < 1e-14);
+    const MockImu mi;
+    const okvisgpu::ImuError ie = okvisgpu::fromOkvisImuError(mi);
+    CHECK(ie.t0_ns == 120 && ie.t1_ns == 180 && ie.sample_t_ns.size() == 2 && ie.sample_t_ns[1] == 200);
+    CHECK(ie.gyr_acc.size() == 12 && ie.gyr_acc[0] == 0.1 && ie.gyr_acc[5] == 9.8 && ie.gyr_acc[11] == 9.7);
+    CHECK(ie.params.sigma_gw_c == 4e-6 && ie.params.g == 9.81007);
+  }
   // removal (RemoveParameterBlock drops its residual blocks too)
   P.RemoveResidualBlock(r01);
   CHECK(P.NumResidualBlocks() == 5);
@@ -355,6 +502,71 @@ int windowVsDirect() {
   return 0;
 }
 
+// §8b fallback end to end: an S10 window plus one GpsFunctor per keyframe on (pose k, speed/bias k,
+// camera 0's constant T_SC as the alignment block), through the facade (HostFunctor<GpsFunctor>) and
+// through the C ABI directly (host_* arrays + a C callback): same solve.
+int gpsHostFallback() {
+  okvisgpu_synth_config cfg;
+  okvisgpu_synth_default_config(&cfg, 10, 500, 4000, 20251016u);
+  okvisgpu_synth_window *wa = nullptr, *wb = nullptr;
+  CHECK(okvisgpu_synth_create(&cfg, &wa) == OKVISGPU_OK && okvisgpu_synth_create(&cfg, &wb) == OKVISGPU_OK);
+  const okvisgpu_problem* pa = okvisgpu_synth_problem(wa);
+  const okvisgpu_problem* pb = okvisgpu_synth_problem(wb);
+  const int n = pa->n_poses;
+  std::vector<double> gt(7 * n), gsb(9 * n);
+  CHECK(okvisgpu_synth_ground_truth(wa, gt.data(), nullptr, gsb.data()) == OKVISGPU_OK);
+  std::vector<GpsFunctor> gps(n);
+  for (int k = 0; k < n; ++k) {  // measurements from the ground truth, aligned by T_SC0
+    gps[k].dt = 0.005 * k;
+    double pG[3], a[3], pW[3], RG[9];
+    gps[k].predict(&gt[7 * k], &gsb[9 * k], &pa->extrinsics[0], pG, a, pW, RG);
+    for (int i = 0; i < 3; ++i) gps[k].meas[i] = pG[i] + 0.01 * ((k + i) % 3 - 1);
+  }
+  okvisgpu::Problem P;
+  Recorded R;
+  record(P, pa, R);
+  std::vector<std::unique_ptr<okvisgpu::HostFunctor<GpsFunctor>>> hf;
+  for (int k = 0; k < n; ++k) {
+    hf.emplace_back(new okvisgpu::HostFunctor<GpsFunctor>(&gps[k]));
+    P.AddResidualBlock(hf.back().get(), nullptr, &pa->poses[7 * k], &pa->speed_biases[9 * k], &pa->extrinsics[0]);
+  }
+  okvisgpu_options o = zeroTol(8);
+  o.num_threads = 2;
+  okvisgpu_summary sa, sb;
+  CHECK(P.Solve(o, &sa) == OKVISGPU_OK);
+  // the same through the C ABI
+  okvisgpu_problem q = *pb;
+  std::vector<int32_t> dim(n, 3), kind, idx;
+  for (int k = 0; k < n; ++k) {
+    kind.insert(kind.end(), {0, 1, 0, -1});
+    idx.insert(idx.end(), {k, k, pb->n_poses + 0, -1});
+  }
+  q.n_host = n;
+  q.host_dim = dim.data();
+  q.host_param_kind = kind.data();
+  q.host_param_index = idx.data();
+  q.host_cauchy = nullptr;
+  q.host_user = &gps;
+  q.host_evaluate = [](void* user, int32_t f, const double* const* prm, double* r, double** J) -> int {
+    return (*static_cast<std::vector<GpsFunctor>*>(user))[f].Evaluate(prm, r, J) ? 1 : 0;
+  };
+  okvisgpu_ctx* ctx = nullptr;
+  CHECK(okvisgpu_ctx_create(0, &ctx) == OKVISGPU_OK);
+  CHECK(okvisgpu_set_problems(ctx, &q, 1) == OKVISGPU_OK);
+  CHECK(okvisgpu_solve(ctx, &o, &sb) == OKVISGPU_OK);
+  double dev = 0;
+  for (int i = 0; i < 7 * n; ++i) dev = std::max(dev, std::fabs(pa->poses[i] - pb->poses[i]));
+  CHECK(sa.num_iterations == sb.num_iterations && sa.termination_type == sb.termination_type);
+  CHECK(std::fabs(sa.final_cost - sb.final_cost) <= 1e-9 * sb.final_cost && dev <= 1e-9);
+  CHECK(sa.final_cost < 1e-2 * sa.initial_cost);
+  std::printf("S10 + GPS host factors, facade vs C ABI: cost %.12g / %.12g (initial %.6g), max pose deviation %.3g\n",
+              sa.final_cost, sb.final_cost, sa.initial_cost, dev);
+  okvisgpu_ctx_destroy(ctx);
+  okvisgpu_synth_destroy(wa);
+  okvisgpu_synth_destroy(wb);
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -362,6 +574,7 @@ int main(int argc, char** argv) {
   if (mode == "cpu") return cpuTests();
   for (uint64_t seed = 1; seed <= 5; ++seed) reprojectionScene(seed);
   windowVsDirect();
+  gpsHostFallback();
   std::printf("facade_test gpu %s\n", g_fail ? "FAILED" : "ok");
   return g_fail ? 1 : 0;
 }
