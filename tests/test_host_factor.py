@@ -7,7 +7,8 @@ shape: pose 7 / speed-bias 9 / alignment pose 7; tests/_gps.py) on S10 synthetic
 CPU: the oracle's restatement (Ceres ResidualBlock with manifolds) gets the minimal Jacobian right
 (numeric differentiation on the manifold), solves the window, and handles evaluation failure
 (initial point: FAILURE; candidate: rejected step, Ceres' candidate_cost = max).
-GPU: okvisgpu's gather -> host callback -> upload path reproduces the oracle bit for bit at the
+GPU: okvisgpu's gather -> host callback -> upload path reproduces the oracle (r bit for bit, J to
+1e-14) at the
 functor level and the solve's iterations / termination / estimates across single windows, batches
 (threaded host evaluation, forked iteration graph), fixed factors and failures."""
 import ctypes as C
@@ -109,9 +110,10 @@ def test_gpu_host_factor_validation(og):
 
 
 @pytest.mark.gpu
-def test_gpu_eval_host_matches_oracle_bitwise(og):
-    """Functor level: gathered parameters, the callback and the ambient -> minimal conversion give
-    r and J identical to the oracle's (same arithmetic order: 0 ulp)."""
+def test_gpu_eval_host_matches_oracle(og):
+    """Functor level: gathered parameters and the callback give r identical to the oracle's (0 ulp);
+    the ambient -> minimal conversion J = J_amb * PlusJacobian agrees to 1e-14 relative (same
+    operation order; the two host compilers contract the products into FMAs differently)."""
     P, fac, _ = gps_window()
     rc_ref, Jc_ref, rc = _oracle.eval_host(P.ptr(), N_KF)
     assert rc == 0
@@ -122,7 +124,8 @@ def test_gpu_eval_host_matches_oracle_bitwise(og):
     finally:
         ctx.close()
     print(f"eval_host max |diff|: r {np.abs(r - rc_ref).max():.1e}, J {np.abs(J - Jc_ref).max():.1e}")
-    assert np.array_equal(r, rc_ref) and np.array_equal(J, Jc_ref)
+    assert np.array_equal(r, rc_ref)
+    assert np.abs(J - Jc_ref).max() <= 1e-14 * np.abs(Jc_ref).max()
 
 
 def _solve_both(probs, options, **ctx_opts):
