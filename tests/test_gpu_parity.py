@@ -1,12 +1,15 @@
 """GPU parity tests: the HIP path (through the C ABI) against the CPU oracle on identical inputs.
 
-Tolerances (FP64 on both sides; different but equivalent operation orders):
-  * reprojection residuals / minimal Jacobians: 1e-9 relative to the block norm (fused GPU
-    formula vs the reference's 4x4-matrix chain);
+Tolerances (FP64 on both sides; different but equivalent operation orders). Every test records
+the deviation it measured (conftest `parity`; OKVISGPU_PARITY_REPORT writes them, the round's copy
+is profiles/r03_parity.json):
+  * reprojection residuals / minimal Jacobians: 1e-12 relative to the block norm (fused GPU
+    formula vs the reference's 4x4-matrix chain; measured 1e-15);
   * IMU factor: only basis-invariant quantities (J^T J, J^T r, cost) are compared, because the
-    pseudo-inverse square root's eigenvector basis is arbitrary; 1e-7 relative;
-  * reduced camera system S / rhs: 1e-8 relative to max|S| (landmark elimination sums in another
-    order, Jacobi scaling applied to blocks instead of to J columns);
+    pseudo-inverse square root's eigenvector basis is arbitrary; 1e-12 relative
+    (measured 3e-15);
+  * reduced camera system S / rhs: 1e-11 relative to max|S| (landmark elimination sums in another
+    order, Jacobi scaling applied to blocks instead of to J columns; measured 1.2e-13);
   * full solves: final cost 1e-7 relative, poses within 1e-6 m / 1e-6 rad (the parity contract of
     SURVEY.md §8c).
 """
@@ -20,18 +23,32 @@ def _window(og, kf=10, lm=500, obs=4000, seed=20251015):
     return og.SynthWindow(kf, lm, obs, seed=seed)
 
 
-def test_reprojection_functor_parity(og, oracle, gpu_ctx):
-    w = _window(og)
+def _block_rel(a, b, n):
+    """max over observations of |a - b| / |b| (Frobenius norms of the per-observation blocks)."""
+    err = np.linalg.norm((a - b).reshape(n, -1), axis=1)
+    ref = np.linalg.norm(b.reshape(n, -1), axis=1)
+    return float(np.max(err / np.maximum(ref, 1e-300)))
+
+
+def _reprojection_parity(gpu_ctx, oracle, w, parity, tag):
     n = w.problem.n_observations
     gpu_ctx.set_problems([w.problem])
     r, Jp, Jl = gpu_ctx.eval_reprojection(n)
     r0, Jp0, Jl0 = oracle.eval_reprojection(w.problem_ptr(), n)
-    scale = np.abs(r0).max()
-    assert np.abs(r - r0).max() <= 1e-9 * scale
-    for a, b in ((Jp, Jp0), (Jl, Jl0)):
-        err = np.linalg.norm((a - b).reshape(n, -1), axis=1)
-        ref = np.linalg.norm(b.reshape(n, -1), axis=1)
-        assert np.all(err <= 1e-9 * ref + 1e-12), f"max rel {np.max(err / ref)}"
+    parity(f"{tag} reprojection r (max abs / max |r|)", np.abs(r - r0).max() / np.abs(r0).max(), R_TOL)
+    parity(f"{tag} reprojection J_pose (block rel)", _block_rel(Jp, Jp0, n), J_TOL)
+    parity(f"{tag} reprojection J_landmark (block rel)", _block_rel(Jl, Jl0, n), J_TOL)
+
+
+# reprojection functor bounds: the GPU forms r and J from a fused chain (C_CW, L Jh, no 4x4
+# matrices) where the reference multiplies the 4x4 transformation chain; both FP64. Measured on
+# MI355X (profiles/r03_parity.json): r 8e-15, J 1e-15 relative -- the bound keeps ~100x headroom.
+R_TOL = 1e-12
+J_TOL = 1e-12
+
+
+def test_reprojection_functor_parity(og, oracle, gpu_ctx, parity):
+    _reprojection_parity(gpu_ctx, oracle, _window(og), parity, "radtan")
 
 
 EQUIDISTANT_TEST = (-0.0041, 0.0063, -0.0067, 0.0023)
@@ -59,7 +76,7 @@ def _switch_camera_model(oracle, w, kind, params):
 
 
 @pytest.mark.parametrize("distortion", sorted(CAMERA_MODELS))
-def test_distortion_models_parity(og, oracle, gpu_ctx, distortion):
+def test_distortion_models_parity(og, oracle, gpu_ctx, distortion, parity):
     """The other camera models of PinholeCamera<D> (NoDistortion, EquidistantDistortion.hpp:87-188,
     RadialTangentialDistortion8.hpp:88-170): functor outputs and a short full solve against the
     oracle."""
@@ -67,14 +84,7 @@ def test_distortion_models_parity(og, oracle, gpu_ctx, distortion):
     assert og.DIST_EQUIDISTANT == 2 and og.DIST_RADTAN8 == 3
     _switch_camera_model(oracle, w, *CAMERA_MODELS[distortion])
     p = w.problem
-    n = p.n_observations
-    gpu_ctx.set_problems([p])
-    r, Jp, Jl = gpu_ctx.eval_reprojection(n)
-    r0, Jp0, Jl0 = oracle.eval_reprojection(w.problem_ptr(), n)
-    assert np.abs(r - r0).max() <= 1e-9 * np.abs(r0).max()
-    for a, b in ((Jp, Jp0), (Jl, Jl0)):
-        err = np.linalg.norm((a - b).reshape(n, -1), axis=1)
-        assert np.all(err <= 1e-9 * np.linalg.norm(b.reshape(n, -1), axis=1) + 1e-12)
+    _reprojection_parity(gpu_ctx, oracle, w, parity, distortion)
     opts = og.default_options(max_num_iterations=4, function_tolerance=0.0, gradient_tolerance=0.0,
                               parameter_tolerance=0.0)
     sg = gpu_ctx.solve(opts, 1)[0]
@@ -82,26 +92,31 @@ def test_distortion_models_parity(og, oracle, gpu_ctx, distortion):
     w.reset()
     so = oracle.solve(w.problem_ptr(), opts)
     assert sg["num_iterations"] == so["num_iterations"]
-    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-6 * so["final_cost"], (sg, so)
-    assert np.abs(P[:, :3] - w.poses()[:, :3]).max() <= 1e-6
+    parity(f"{distortion} 4-iteration solve final cost (rel)", abs(sg["final_cost"] - so["final_cost"]) / so["final_cost"], 1e-6)
+    parity(f"{distortion} 4-iteration solve poses (m)", np.abs(P[:, :3] - w.poses()[:, :3]).max(), 1e-6)
 
 
-def test_imu_functor_invariants(og, oracle, gpu_ctx):
+def test_imu_functor_invariants(og, oracle, gpu_ctx, parity):
     w = _window(og)
     p = w.problem
     gpu_ctx.set_problems([w.problem])
     r, J = gpu_ctx.eval_imu(p.n_imu)
     w.reset()
     r0, J0 = oracle.eval_imu(w.problem_ptr(), p.n_imu)
+    eH = eg = ec = 0.0
     for f in range(p.n_imu):
         H, H0 = J[f].T @ J[f], J0[f].T @ J0[f]
         g, g0 = J[f].T @ r[f], J0[f].T @ r0[f]
-        assert np.linalg.norm(H - H0) <= 1e-7 * np.linalg.norm(H0)
-        assert np.linalg.norm(g - g0) <= 1e-7 * np.linalg.norm(g0) + 1e-9
-        assert abs(r[f] @ r[f] - r0[f] @ r0[f]) <= 1e-7 * (r0[f] @ r0[f]) + 1e-12
+        eH = max(eH, np.linalg.norm(H - H0) / np.linalg.norm(H0))
+        eg = max(eg, np.linalg.norm(g - g0) / (np.linalg.norm(g0) + 1e-300))
+        ec = max(ec, abs(r[f] @ r[f] - r0[f] @ r0[f]) / (r0[f] @ r0[f]))
+    tag = "imu"
+    parity(f"{tag} J^T J (Frobenius rel)", eH, 1e-12)
+    parity(f"{tag} J^T r (rel)", eg, 1e-12)
+    parity(f"{tag} |r|^2 (rel)", ec, 1e-12)
 
 
-def test_imu_functor_pseudo_inverse(og, oracle, gpu_ctx):
+def test_imu_functor_pseudo_inverse(og, oracle, gpu_ctx, parity):
     """Zero bias random-walk densities make the preintegrated covariance singular, so the
     square-root information takes the clamped eigen-decomposition branch of
     PseudoInverse::symmSqrtU (PseudoInverse.hpp:132-158) instead of the Cholesky shortcut."""
@@ -113,16 +128,21 @@ def test_imu_functor_pseudo_inverse(og, oracle, gpu_ctx):
     r, J = gpu_ctx.eval_imu(p.n_imu)
     w.reset()
     r0, J0 = oracle.eval_imu(w.problem_ptr(), p.n_imu)
+    eH = eg = ec = 0.0
     for f in range(p.n_imu):
         H, H0 = J[f].T @ J[f], J0[f].T @ J0[f]
         g, g0 = J[f].T @ r[f], J0[f].T @ r0[f]
-        assert np.linalg.norm(H - H0) <= 1e-6 * np.linalg.norm(H0)
-        assert np.linalg.norm(g - g0) <= 1e-6 * np.linalg.norm(g0) + 1e-9
-        assert abs(r[f] @ r[f] - r0[f] @ r0[f]) <= 1e-6 * (r0[f] @ r0[f]) + 1e-12
+        eH = max(eH, np.linalg.norm(H - H0) / np.linalg.norm(H0))
+        eg = max(eg, np.linalg.norm(g - g0) / (np.linalg.norm(g0) + 1e-300))
+        ec = max(ec, abs(r[f] @ r[f] - r0[f] @ r0[f]) / (r0[f] @ r0[f]))
+    tag = "imu pseudo-inverse branch"
+    parity(f"{tag} J^T J (Frobenius rel)", eH, 1e-12)
+    parity(f"{tag} J^T r (rel)", eg, 1e-12)
+    parity(f"{tag} |r|^2 (rel)", ec, 1e-12)
 
 
 @pytest.mark.parametrize("mu", [0.0, 1e-8, 1e-2])
-def test_linearize_reduce_parity(og, oracle, gpu_ctx, mu):
+def test_linearize_reduce_parity(og, oracle, gpu_ctx, mu, parity):
     w = _window(og)
     gpu_ctx.set_problems([w.problem])
     S, rhs, cost = gpu_ctx.linearize_reduce(0, True, mu)
@@ -130,9 +150,9 @@ def test_linearize_reduce_parity(og, oracle, gpu_ctx, mu):
     S0, rhs0, cost0, rc = oracle.linearize_reduce(w.problem_ptr(), True, mu)
     assert rc == 0
     assert S.shape == S0.shape
-    assert abs(cost - cost0) <= 1e-10 * cost0
-    assert np.abs(S - S0).max() <= 1e-8 * np.abs(S0).max(), np.abs(S - S0).max() / np.abs(S0).max()
-    assert np.abs(rhs - rhs0).max() <= 1e-8 * np.abs(rhs0).max(), np.abs(rhs - rhs0).max() / np.abs(rhs0).max()
+    parity("S10 initial cost (rel)", abs(cost - cost0) / cost0, 1e-12)
+    parity(f"S10 reduced system S, mu={mu} (max abs / max |S|)", np.abs(S - S0).max() / np.abs(S0).max(), 1e-11)
+    parity(f"S10 reduced rhs, mu={mu} (max abs / max |rhs|)", np.abs(rhs - rhs0).max() / np.abs(rhs0).max(), 1e-11)
 
 
 def _rot_err(q, q0):
@@ -146,7 +166,7 @@ def _rot_err(q, q0):
 
 
 @pytest.mark.parametrize("iters", [1, 3, 10])
-def test_solve_parity_s10(og, oracle, gpu_ctx, iters):
+def test_solve_parity_s10(og, oracle, gpu_ctx, iters, parity):
     w = _window(og)
     opts = og.default_options(max_num_iterations=iters, function_tolerance=0.0, gradient_tolerance=0.0,
                               parameter_tolerance=0.0)
@@ -162,9 +182,10 @@ def test_solve_parity_s10(og, oracle, gpu_ctx, iters):
     # One GN step from a far initial point amplifies rounding by the reduced system's condition
     # number (~1e8): 1e-7 relative after the first step; later iterations contract towards the same
     # optimum and the 3- and 10-iteration cases also hold this bound.
-    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-7 * so["final_cost"], (sg, so)
-    assert np.abs(P[:, :3] - P0[:, :3]).max() <= 1e-6
-    assert max(_rot_err(P[i, 3:], P0[i, 3:]) for i in range(len(P))) <= 1e-6
+    parity(f"S10 {iters}-iteration solve final cost (rel)", abs(sg["final_cost"] - so["final_cost"]) / so["final_cost"], 1e-7)
+    parity(f"S10 {iters}-iteration solve positions (m)", np.abs(P[:, :3] - P0[:, :3]).max(), 1e-6)
+    parity(f"S10 {iters}-iteration solve rotations (rad)", max(_rot_err(P[i, 3:], P0[i, 3:]) for i in range(len(P))), 1e-6)
+    parity(f"S10 {iters}-iteration solve landmarks (m)", np.abs(L[:, :3] / L[:, 3:] - L0[:, :3] / L0[:, 3:]).max(), 1e-3)
 
 
 def test_batched_windows_match_single(og, gpu_ctx):

@@ -110,7 +110,7 @@ def test_gpu_host_factor_validation(og):
 
 
 @pytest.mark.gpu
-def test_gpu_eval_host_matches_oracle(og):
+def test_gpu_eval_host_matches_oracle(og, parity):
     """Functor level: gathered parameters and the callback give r identical to the oracle's (0 ulp);
     the ambient -> minimal conversion J = J_amb * PlusJacobian agrees to 1e-14 relative (same
     operation order; the two host compilers contract the products into FMAs differently)."""
@@ -123,9 +123,8 @@ def test_gpu_eval_host_matches_oracle(og):
         r, J = ctx.eval_host(N_KF)
     finally:
         ctx.close()
-    print(f"eval_host max |diff|: r {np.abs(r - rc_ref).max():.1e}, J {np.abs(J - Jc_ref).max():.1e}")
-    assert np.array_equal(r, rc_ref)
-    assert np.abs(J - Jc_ref).max() <= 1e-14 * np.abs(Jc_ref).max()
+    parity("host factor r (max abs diff)", np.abs(r - rc_ref).max(), 0.0)
+    parity("host factor minimal J (max abs / max |J|)", np.abs(J - Jc_ref).max() / np.abs(Jc_ref).max(), 1e-14)
 
 
 def _solve_both(probs, options, **ctx_opts):
@@ -146,7 +145,7 @@ def _solve_both(probs, options, **ctx_opts):
     return gsum, csum, gpu, cpu
 
 
-def _assert_parity(gsum, csum, gpu, cpu, tag):
+def _assert_parity(parity, gsum, csum, gpu, cpu, tag):
     worst_p = worst_c = 0.0
     for w, (g, c) in enumerate(zip(gsum, csum)):
         assert (g["num_iterations"], g["termination"], g["num_successful_steps"], g["num_unsuccessful_steps"]) == \
@@ -154,29 +153,29 @@ def _assert_parity(gsum, csum, gpu, cpu, tag):
         if np.isfinite(c["final_cost"]):
             worst_c = max(worst_c, abs(g["final_cost"] - c["final_cost"]) / c["final_cost"])
         worst_p = max(worst_p, float(np.abs(gpu[w][0][:, :3] - cpu[w][0][:, :3]).max()))
-    print(f"{tag}: {len(gsum)} windows, worst pose dev {worst_p:.2e} m, cost rel {worst_c:.2e}")
-    assert worst_p <= 1e-6 and worst_c <= 1e-7
+    parity(f"host factors, {tag}: positions (m)", worst_p, 1e-6)
+    parity(f"host factors, {tag}: final cost (rel)", worst_c, 1e-7)
 
 
 @pytest.mark.gpu
-def test_gpu_gps_window_solve_parity(og):
+def test_gpu_gps_window_solve_parity(og, parity):
     P, _, _ = gps_window()
     o = og.default_options(max_num_iterations=10, num_threads=2)
-    _assert_parity(*_solve_both([P], o), "S10 + GPS")
+    _assert_parity(parity, *_solve_both([P], o), "S10 + GPS")
 
 
 @pytest.mark.gpu
-def test_gpu_gps_batch_forked_graph_parity(og, monkeypatch):
+def test_gpu_gps_batch_forked_graph_parity(og, monkeypatch, parity):
     """24 windows, 240 host factors evaluated on 4 host threads, inside the forked iteration graph
     (forced with OKVISGPU_SERIAL_GRAPH=0); every fifth window with a constant alignment block."""
     monkeypatch.setenv("OKVISGPU_SERIAL_GRAPH", "0")
     probs = [gps_window(seed=100 + i, t_gw_variable=(i % 5 != 0))[0] for i in range(24)]
     o = og.default_options(max_num_iterations=10, num_threads=4)
-    _assert_parity(*_solve_both(probs, o), "24 x (S10 + GPS), forked graph")
+    _assert_parity(parity, *_solve_both(probs, o), "24 x (S10 + GPS), forked graph")
 
 
 @pytest.mark.gpu
-def test_gpu_host_fixed_factors_parity(og):
+def test_gpu_host_fixed_factors_parity(og, parity):
     """Host factors whose blocks are all constant (frozen states 0-1, constant alignment) contribute
     fixed cost only (evaluated at the initial point, excluded from the reduced system), as Ceres
     removes fully-constant residual blocks; the other GPS factors stay in the solve."""
@@ -185,11 +184,11 @@ def test_gpu_host_fixed_factors_parity(og):
     P.speed_bias_constant[:2] = 1
     P.bind()
     o = og.default_options(max_num_iterations=8)
-    _assert_parity(*_solve_both([P], o), "fixed host factors")
+    _assert_parity(parity, *_solve_both([P], o), "fixed host factors")
 
 
 @pytest.mark.gpu
-def test_gpu_host_failure_parity(og):
+def test_gpu_host_failure_parity(og, parity):
     """Failure at the initial point (window ends with FAILURE, parameters untouched) and at
     candidates (rejected steps) give the oracle's summaries; the other windows of the batch are
     unaffected."""
@@ -203,4 +202,4 @@ def test_gpu_host_failure_parity(og):
     gsum, csum, gpu, cpu = _solve_both([P0, P1, P2], o)
     assert gsum[0]["termination"] == "FAILURE" and np.array_equal(gpu[0][0], x0)
     assert gsum[1]["num_unsuccessful_steps"] >= 1
-    _assert_parity(gsum, csum, gpu, cpu, "host evaluation failures")
+    _assert_parity(parity, gsum, csum, gpu, cpu, "host evaluation failures")

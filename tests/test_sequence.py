@@ -89,7 +89,7 @@ def test_oracle_sequence_conditioning(world):
 
 
 @pytest.mark.gpu
-def test_gpu_sequence_matches_oracle(og, oracle, world):
+def test_gpu_sequence_matches_oracle(og, oracle, world, parity):
     """28 chained realtime solves + strategy, okvisgpu vs the oracle, each on its own estimates."""
     ref_states = {}
 
@@ -151,3 +151,6 @@ def test_gpu_sequence_matches_oracle(og, oracle, world):
         worst["cost"] = max(worst["cost"], rel)
         assert rel <= 1e-7, (k, rel)
     print(f"sequence of {len(gpu_sums)} solves: worst GPU-vs-oracle deviations {worst}")
+    bounds = {"pose": 1e-6, "lm": 1e-5, "lm_maha": 1e-4, "cost": 1e-7, "edge_info": 1e-6, "imu_info": 1e-6}
+    for k, v in worst.items():
+        parity(f"sequence (28 solves + strategy): {k}", v, bounds[k])
