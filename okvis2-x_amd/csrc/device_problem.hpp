@@ -75,7 +75,8 @@ struct WinState {
   int32_t eval_cand;               // candidate must be evaluated this iteration
   int32_t step_valid;
   int32_t accepted;
-  int32_t pad_[3];
+  int32_t s_dirty;                 // S holds a factorisation (set by the Cholesky, cleared once zeroed)
+  int32_t pad_[2];
 };
 
 // Options mirrored on the device (okvisgpu_options subset used inside kernels).
@@ -92,6 +93,7 @@ struct DevOptions {
 struct DevProblem {
   const DevProblem* self;          // device-resident copy of this descriptor (what kernels receive)
   int32_t n_win, n_pose, n_sb, n_lm, n_obs, n_visit, n_imu, n_pprior, n_sbprior, n_cam;
+  int32_t cu_count;                // compute units of the device (persistent-style grids)
   int32_t n_fblock, n_pair;
   int32_t max_fpad, max_tiles;     // largest padded reduced dimension / its 64-tile count
   int64_t obs_stride;              // plane stride of the obs linearisation SoA (>= n_obs)

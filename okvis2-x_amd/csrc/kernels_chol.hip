@@ -362,10 +362,12 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
 #pragma unroll
       for (int k = 0; k < 8; ++k) r[k] = sA[i * kLd + c0 + k];
       if (s >= 1) {  // look-ahead update by sub-panel s-1: r -= L_i,s-1 L_(c0..c0+7),s-1^T
+        // (c outer: the 8 independent chains r[m] interleave, so no FMA waits on the previous one's
+        // result; every r[m] still sums over c in order, the same bits)
 #pragma unroll
-        for (int m = 0; m < 8; ++m)
+        for (int c = 0; c < 8; ++c)
 #pragma unroll
-          for (int c = 0; c < 8; ++c) r[m] -= xp[c] * sA[(c0 + m) * kLd + c0 - 8 + c];
+          for (int m = 0; m < 8; ++m) r[m] -= xp[c] * sA[(c0 + m) * kLd + c0 - 8 + c];
         if (i >= c0) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) sA[i * kLd + c0 + k] = r[k];
@@ -655,6 +657,7 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
   const DevProblem& P = *Pp;
   const int w = blockIdx.x;
   if (!cholSelect(P, w)) return;
+  if (threadIdx.x == 0) P.st[w].s_dirty = 1;  // S of this window is consumed from here on (k_zero_S after)
   const int64_t ld = P.win_fpad[w];
   const int T = (int)(ld / kTile);
   double* S = P.S + P.win_soff[w];
@@ -769,6 +772,7 @@ __global__ __launch_bounds__(256) void k_chol_diag(const DevProblem* __restrict_
   __shared__ int sFl[4];
   const int t = threadIdx.x;
   if (k == 0) {
+    if (t == 0) P.st[w].s_dirty = 1;  // S of this window is consumed from here on (k_zero_S after)
     const int fdim = P.win_fdim[w];
     for (int e = t; e < ld; e += 256) work[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
     __syncthreads();
@@ -1252,6 +1256,7 @@ __global__ __launch_bounds__(kWsThreads, 2) void k_cholesky_ws(const DevProblem*
   __syncthreads();  // the only workgroup-wide barrier: from here on a slot never waits on the other
   const int w = pairs ? 2 * blockIdx.x + slot : blockIdx.x;
   if ((!pairs && wid == 4) || w >= P.n_win || !cholSelect(P, w)) return;
+  if (t == 0) P.st[w].s_dirty = 1;  // S of this window is consumed from here on (k_zero_S after)
   double* sF = sFs[slot];
   double* sX = sXs[slot];
   double* sRl = sRls[slot];

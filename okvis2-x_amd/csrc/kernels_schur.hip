@@ -20,6 +20,7 @@
 //   k_assemble_sb one wavefront per block pair involving a speed/bias block (one entry per lane).
 //   k_gn_finalize Gauss-Newton step / dogleg gradient of the f-blocks in the dogleg-scaled space
 //                 (the landmarks' back substitution and vectors: k_lm_backsub_jv, kernels_backsub.hip).
+#include <algorithm>
 #include <cfloat>
 
 #include "device_problem.hpp"
@@ -126,11 +127,11 @@ __device__ unsigned int g_lmvDone;
 // (landmark, variable camera) J_e of the landmark's observations through that camera
 // (implementation/ReprojectionError.hpp:186-214, extrJacobian), giving W_e, H_ee, g_e, and so Z_e and
 // the products with the pose visits' Z exactly like a pose visit; V / g_l come from the pose visits.
+// (the body of one landmark group grp; the kernels below run it per workgroup or per window loop)
 template <int mode, bool EXT>
-__global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const DevProblem* __restrict__ Pp) {
-  const DevProblem& P = *Pp;
+__device__ __forceinline__ void lmVisitGroup(const DevProblem& P, const int grp) {
   const int t = threadIdx.x;
-  const auto gi = gmem(reinterpret_cast<const int4*>(P.lmg_info + kLmgInfo * blockIdx.x));
+  const auto gi = gmem(reinterpret_cast<const int4*>(P.lmg_info + kLmgInfo * grp));
   const int4 gi0 = gi[0], gi1 = gi[kLmgInfo / 4];
   const int l0 = gi0.x, l1 = gi1.x, v0 = gi0.y, v1 = gi1.y;
   // sBuf rows 0..8: visit shares of V (6) | g_l (3); rows 9..17: visit values being summed into
@@ -178,8 +179,8 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
           (__attribute__((address_space(3))) void*)(sPC + c + 64 * wv), 4, 0, 0);
   }
   const int nvg = v1 - v0;
-  const int xv = EXT ? P.lmg_xbegin[blockIdx.x] + t - nvg : 0;
-  const bool hasX = EXT && t >= nvg && xv < P.lmg_xbegin[blockIdx.x + 1];
+  const int xv = EXT ? P.lmg_xbegin[grp] + t - nvg : 0;
+  const bool hasX = EXT && t >= nvg && xv < P.lmg_xbegin[grp + 1];
   const int l = hasV ? vLm : (hasX ? P.xvisit_lm[xv] : l0);
   const bool sel = hasV;
   const bool lfree = gmem(P.lm_free)[l] != 0;
@@ -552,6 +553,32 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const 
 #endif
 }
 
+template <int mode, bool EXT>
+__global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_visit(const DevProblem* __restrict__ Pp) {
+  lmVisitGroup<mode, EXT>(*Pp, blockIdx.x);
+}
+
+// GN prep of a large batch: after the first iteration hardly any window needs it (Z is formed for
+// the new mu by the linearisation; only retries and invalid steps raise mu), so a workgroup per
+// landmark group would dispatch ~30 groups per window that all exit (2,048 S50 windows: 0.43 ms of
+// dispatch per iteration). Instead a grid of resident workgroups loops over the windows and runs the
+// groups of a selected window one after another (same body, same operations).
+template <bool EXT>
+__global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lm_prep_windows(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
+  for (int w = blockIdx.x; w < P.n_win; w += gridDim.x) {
+    const auto gst = gmem(P.st + w);
+    const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed;
+    const double sZmu = gst->z_mu, sMu = gst->mu;
+    if (sDone | !sNeed | sFail | (sZmu == sMu)) continue;  // lmVisitSelect (uniform)
+    const int g0 = P.win_lmg_range[2 * w], g1 = P.win_lmg_range[2 * w + 1];
+    for (int g = g0; g < g1; ++g) {
+      lmVisitGroup<2, EXT>(P, g);
+      __syncthreads();  // the next group's LDS writes wait for this group's readers
+    }
+  }
+}
+
 // Pose-extrinsics cross blocks of F^T F (variable extrinsics only): per (free state pose, variable
 // camera) the sum over their observations of J_e^T J_p (6x6, rows = extrinsics), one thread each, in
 // observation order. The landmark terms of the same block come from k_lm_visit's partial blocks.
@@ -734,7 +761,11 @@ __device__ __forceinline__ bool gnSelect(const DevProblem& P, int w) {
 // diagonal = 1). Zero tiles are never written by the factorisation and stay zero from the initial
 // arena clear. Each tile's record and window are loaded before any test, 16-byte stores.
 constexpr int kZeroTiles = 4;  // (one per workgroup below kManyWindows windows: latency)
-__global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ Pp, int per) {
+// post = 0: the windows about to assemble (gnSelect; the eager paths); post = 1: the windows whose
+// Cholesky consumed S in this iteration (WinState::s_dirty, cleared by k_gradnorm at the iteration's
+// end) -- the captured iteration clears S right after the factorisation, on a fork stream that runs
+// beside the back substitution and the candidate evaluation, so the next assembly finds it zeroed.
+__global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ Pp, int per, int post) {
   const DevProblem& P = *Pp;
   const auto ti3 = gmem(P.tile_items);
   for (int u = 0; u < per; ++u) {
@@ -742,11 +773,11 @@ __global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ P
     if (item >= P.n_tiles) return;
     const int w = ti3[3 * item], ti = ti3[3 * item + 1], tj = ti3[3 * item + 2];
     const auto gst = gmem(P.st + w);
-    const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed;
+    const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed, sDirty = gst->s_dirty;
     const int fpad = gmem(P.win_fpad)[w], fdim = gmem(P.win_fdim)[w];
     const int64_t soff = gmem(P.win_soff)[w];
     asm volatile("" ::"v"(fpad), "v"(fdim), "v"(soff));
-    if ((sDone != 0) | (sNeed == 0) | (sFail != 0)) continue;  // gnSelect (uniform)
+    if (post ? (sDirty == 0) : ((sDone != 0) | (sNeed == 0) | (sFail != 0))) continue;  // (uniform)
     double* S = P.S + soff;
     for (int e = threadIdx.x; e < kTile * kTile / 2; e += 256) {
       const int r = ti * kTile + (e >> 5), c = tj * kTile + 2 * (e & 31);
@@ -1106,6 +1137,12 @@ __global__ __launch_bounds__(256) void k_gn_finalize(const DevProblem* __restric
 void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s) {
   if (P.n_lmg <= 0) return;
   const dim3 g(P.n_lmg), b(kLmGroupVisits);
+  if (mode == 2 && P.n_win >= kManyWindows) {  // window loop over resident workgroups
+    const dim3 gw(std::min(P.n_win, P.cu_count * OKG_LMV_OCC));
+    if (P.n_xvisit > 0) hipLaunchKernelGGL((k_lm_prep_windows<true>), gw, b, 0, s, P.self);
+    else hipLaunchKernelGGL((k_lm_prep_windows<false>), gw, b, 0, s, P.self);
+    return;
+  }
   if (P.n_xvisit > 0) {
     if (mode == 0) hipLaunchKernelGGL((k_lm_visit<0, true>), g, b, 0, s, P.self);
     else if (mode == 1) hipLaunchKernelGGL((k_lm_visit<1, true>), g, b, 0, s, P.self);
@@ -1143,9 +1180,9 @@ void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t 
   launch_fgrad(P, lin_mode, s);
 }
 void launch_lm_prep(const DevProblem& P, hipStream_t s) { launch_lm_visit(P, 2, s); }
-void launch_zero_S(const DevProblem& P, hipStream_t s) {
+void launch_zero_S(const DevProblem& P, hipStream_t s, int post) {
   const int per = P.n_win >= kManyWindows ? kZeroTiles : 1;
-  if (P.n_tiles > 0) hipLaunchKernelGGL(k_zero_S, dim3((P.n_tiles + per - 1) / per), dim3(256), 0, s, P.self, per);
+  if (P.n_tiles > 0) hipLaunchKernelGGL(k_zero_S, dim3((P.n_tiles + per - 1) / per), dim3(256), 0, s, P.self, per, post);
 }
 void launch_assemble(const DevProblem& P, hipStream_t s) {
   launch_assemble_pp(P, s);

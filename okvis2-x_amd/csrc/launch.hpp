@@ -29,7 +29,9 @@ void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_imu_hess(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_lm_prep(const DevProblem& P, hipStream_t s);
-void launch_zero_S(const DevProblem& P, hipStream_t s);
+// post = 0: windows about to assemble; post = 1: windows whose Cholesky ran (after it, beside the
+// rest of the iteration; the captured iteration's only zeroing)
+void launch_zero_S(const DevProblem& P, hipStream_t s, int post = 0);
 void launch_assemble(const DevProblem& P, hipStream_t s);
 void launch_lm_backsub(const DevProblem& P, hipStream_t s);  // kernels_backsub.hip: + landmark dogleg vectors, J*v
 void launch_assemble_pp(const DevProblem& P, hipStream_t s);

@@ -1063,7 +1063,7 @@ struct Arena {
 struct okvisgpu_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t side[2] = {nullptr, nullptr};  // fork streams of the captured iteration graph
+  hipStream_t side[3] = {nullptr, nullptr, nullptr};  // fork streams of the captured iteration graph
   std::vector<hipEvent_t> forkEv;
   std::string last_error;
   HostBatch B;
@@ -1300,6 +1300,7 @@ struct okvisgpu_ctx {
     D.n_lm = (int)B.lm_win.size();
     D.n_obs = (int)B.obs_win.size();
     D.n_visit = (int)B.visit_pose.size();
+    D.cu_count = cuCount;
     D.n_imu = B.n_imu_total;
     D.n_host = (int)B.hf.size();
     D.n_fac = D.n_imu + D.n_host;
@@ -1666,8 +1667,10 @@ struct okvisgpu_ctx {
   }
 
   void launchIteration() {
-    launch_gn_reduce(P, stream);
+    launch_lm_prep(P, stream);
+    launch_assemble(P, stream);  // (S was cleared after the previous factorisation: post zeroing)
     launch_cholesky(P, stream);
+    launch_zero_S(P, stream, 1);
     launch_gn_backsub(P, stream);
     launch_jv(P, stream);
     launch_dogleg(P, stream);
@@ -1702,16 +1705,17 @@ struct okvisgpu_ctx {
       HIPCHK(hipEventRecord(e, from));
       HIPCHK(hipStreamWaitEvent(stream, e, 0));
     };
-    // Gauss-Newton system: S tiles cleared while the stale Z is rebuilt; both assembly kernels
-    fork(side[0]);
-    launch_zero_S(P, side[0]);
+    // Gauss-Newton system: the stale Z rebuilt (few windows after the first iteration); both
+    // assembly kernels (S was cleared right after the previous factorisation, below)
     launch_lm_prep(P, stream);
-    join(side[0]);
     fork(side[0]);
     launch_assemble_sb(P, side[0]);
     launch_assemble_pp(P, stream);
     join(side[0]);
     launch_cholesky(P, stream);
+    // S of the factored windows cleared beside the rest of the iteration (joined at its end)
+    fork(side[2]);
+    launch_zero_S(P, side[2], 1);
     launch_gn_finalize(P, stream);
     fork(side[0]);
     launch_jv(P, side[0]);
@@ -1734,6 +1738,7 @@ struct okvisgpu_ctx {
     launch_lm_blocks(P, 1, stream);
     join(side[0]);
     launch_fgrad(P, 1, stream);
+    join(side[2]);  // k_gradnorm clears WinState::s_dirty
     launch_gradnorm(P, 1, stream);
   }
 
@@ -1930,6 +1935,7 @@ int okvisgpu_solve_begin(okvisgpu_ctx* c, const okvisgpu_options* o) {
     c->dropGraph();  // options are baked into the captured kernel arguments
     c->uploadParams();
     c->resetStates(1e-8);
+    launch_zero_S(c->P, c->stream, 0);  // every window: the iteration clears S after factorising only
     c->launchInit(2);
     c->failInitialHostEvaluations();
     c->ensureGraph();
@@ -2050,6 +2056,7 @@ int okvisgpu_profile_iteration(okvisgpu_ctx* c, double* ms) {
     launch_zero_S(P, s); mark(1);
     launch_assemble(P, s); mark(2);
     launch_cholesky(P, s); mark(3);
+    launch_zero_S(P, s, 1); mark(1);
     launch_gn_finalize(P, s); mark(5);
     launch_lm_backsub(P, s); mark(4);
     launch_jv(P, s); mark(6);

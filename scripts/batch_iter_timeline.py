@@ -1,5 +1,5 @@
 """One batched iteration of a rocprofv3 kernel trace (the bench's timed loop) as a timeline: start
-offset, duration and end of every kernel relative to the iteration's k_zero_S. Usage:
+offset, duration and end of every kernel relative to the iteration's first kernel. Usage:
 batch_iter_timeline.py run_kernel_trace.csv [iteration index among the large k_zero_S launches]"""
 import csv
 import sys
@@ -13,7 +13,12 @@ rows.sort()
 # iteration marker: the first kernel of the captured iteration (k_zero_S before round 3, then the
 # assembly), the batch's launches (largest grid) only
 names = {r[2] for r in rows}
-mark = "k_zero_S" if sum(r[2] == "k_zero_S" for r in rows) > 4 else "k_assemble_sb"
+if "k_lm_prep_windows<false>" in names:  # round 3: S cleared after the factorisation, prep first
+    mark = "k_lm_prep_windows<false>"
+elif sum(r[2] == "k_zero_S" for r in rows) > 4 and "k_lm_visit<2, false>" not in names:
+    mark = "k_zero_S"
+else:
+    mark = "k_lm_visit<2, false>"
 gmax = max(r[3] for r in rows if r[2] == mark)
 zs = [i for i, r in enumerate(rows) if r[2] == mark and r[3] == gmax]
 # the bench's batched solve: begin (iteration 0), warm-up + timed iterations, then the PCIe-inclusive
