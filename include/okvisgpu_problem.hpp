@@ -22,7 +22,7 @@
 // Any other cost function on pose-kind / speed-bias blocks (GPS, user factors) joins the solve as a
 // HostCostFunction (or HostFunctor<F> around the caller's ceres::CostFunction-shaped functor): the
 // §8b host-evaluated fallback. Cost functions the fallback cannot take either (landmark blocks:
-// depth, SubmapICP) are rejected at AddResidualBlock with okvisgpu::Unsupported
+// OneSidedDepthError) are rejected at AddResidualBlock with okvisgpu::Unsupported
 // (OKVISGPU_ERR_UNSUPPORTED): the caller keeps its Ceres solve for such a graph.
 //
 // Ownership: like `Problem::Options{DO_NOT_TAKE_OWNERSHIP}` (ViGraph.cpp:239-247), the facade never

@@ -75,8 +75,7 @@ struct WinState {
   int32_t eval_cand;               // candidate must be evaluated this iteration
   int32_t step_valid;
   int32_t accepted;
-  int32_t s_dirty;                 // S holds a factorisation (set by the Cholesky, cleared once zeroed)
-  int32_t pad_[2];
+  int32_t pad_[3];
 };
 
 // Options mirrored on the device (okvisgpu_options subset used inside kernels).
@@ -266,6 +265,8 @@ struct DevProblem {
   // window is block-banded and LLT creates no fill outside its envelope, so only structurally
   // non-zero 64x64 tiles are zeroed, factored and updated (bitwise identical to the dense LLT).
   const int32_t* tile_items;         // (w, i, j) every structurally non-zero tile (i >= j)
+  const uint64_t* tile_mask;         // [n_tiles][64] per tile row: the columns some block pair of the
+                                     // assembly writes (bit c = tile column c)
   // tile-parallel schedule (few windows): per step k, the panel tiles (w, i) and the band updates
   // (w, i, j) of all windows; begin offsets per k, host copies for the launch sizes
   const int32_t* chol_panel_items;

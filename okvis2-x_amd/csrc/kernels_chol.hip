@@ -657,7 +657,6 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
   const DevProblem& P = *Pp;
   const int w = blockIdx.x;
   if (!cholSelect(P, w)) return;
-  if (threadIdx.x == 0) P.st[w].s_dirty = 1;  // S of this window is consumed from here on (k_zero_S after)
   const int64_t ld = P.win_fpad[w];
   const int T = (int)(ld / kTile);
   double* S = P.S + P.win_soff[w];
@@ -772,7 +771,6 @@ __global__ __launch_bounds__(256) void k_chol_diag(const DevProblem* __restrict_
   __shared__ int sFl[4];
   const int t = threadIdx.x;
   if (k == 0) {
-    if (t == 0) P.st[w].s_dirty = 1;  // S of this window is consumed from here on (k_zero_S after)
     const int fdim = P.win_fdim[w];
     for (int e = t; e < ld; e += 256) work[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
     __syncthreads();
@@ -1256,7 +1254,6 @@ __global__ __launch_bounds__(kWsThreads, 2) void k_cholesky_ws(const DevProblem*
   __syncthreads();  // the only workgroup-wide barrier: from here on a slot never waits on the other
   const int w = pairs ? 2 * blockIdx.x + slot : blockIdx.x;
   if ((!pairs && wid == 4) || w >= P.n_win || !cholSelect(P, w)) return;
-  if (t == 0) P.st[w].s_dirty = 1;  // S of this window is consumed from here on (k_zero_S after)
   double* sF = sFs[slot];
   double* sX = sXs[slot];
   double* sRl = sRls[slot];

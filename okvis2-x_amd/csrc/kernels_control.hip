@@ -382,7 +382,6 @@ __global__ __launch_bounds__(kRB) void k_gradnorm(const DevProblem* __restrict__
   const DevProblem& P = *Pp;
   const int w = blockIdx.x;
   WinState& s = P.st[w];
-  if (threadIdx.x == 0) s.s_dirty = 0;  // (k_zero_S of this iteration has run: joined before)
   if (s.done) return;
   if (lin_mode == 1 && !s.accepted) return;
   __shared__ double sh[kRB];

@@ -757,15 +757,17 @@ __device__ __forceinline__ bool gnSelect(const DevProblem& P, int w) {
   return !s.done && s.need_gn && !s.gn_failed;
 }
 
-// Clears the structurally non-zero tiles of S (kZeroTiles consecutive tiles per workgroup; padded
-// diagonal = 1). Zero tiles are never written by the factorisation and stay zero from the initial
-// arena clear. Each tile's record and window are loaded before any test, 16-byte stores.
+// Clears the structurally non-zero tiles of S of the windows about to assemble (gnSelect;
+// kZeroTiles consecutive tiles per workgroup; padded diagonal = 1). Zero tiles are never written by
+// the factorisation and stay zero from the initial arena clear. Each tile's record and window are
+// loaded before any test, 16-byte stores.
+//   fill = 0: every entry (solve start, the eager paths);
+//   fill = 1: only the entries no block pair of the assembly writes (DevProblem::tile_mask: the fill
+//             inside the tile envelope and the padding, ~3/4 of the tiles' area for S50) -- disjoint
+//             from the assembly's stores, so the captured iteration runs it beside the assembly
+//             kernels instead of on the path.
 constexpr int kZeroTiles = 4;  // (one per workgroup below kManyWindows windows: latency)
-// post = 0: the windows about to assemble (gnSelect; the eager paths); post = 1: the windows whose
-// Cholesky consumed S in this iteration (WinState::s_dirty, cleared by k_gradnorm at the iteration's
-// end) -- the captured iteration clears S right after the factorisation, on a fork stream that runs
-// beside the back substitution and the candidate evaluation, so the next assembly finds it zeroed.
-__global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ Pp, int per, int post) {
+__global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ Pp, int per, int fill) {
   const DevProblem& P = *Pp;
   const auto ti3 = gmem(P.tile_items);
   for (int u = 0; u < per; ++u) {
@@ -773,16 +775,22 @@ __global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ P
     if (item >= P.n_tiles) return;
     const int w = ti3[3 * item], ti = ti3[3 * item + 1], tj = ti3[3 * item + 2];
     const auto gst = gmem(P.st + w);
-    const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed, sDirty = gst->s_dirty;
+    const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed;
     const int fpad = gmem(P.win_fpad)[w], fdim = gmem(P.win_fdim)[w];
     const int64_t soff = gmem(P.win_soff)[w];
     asm volatile("" ::"v"(fpad), "v"(fdim), "v"(soff));
-    if (post ? (sDirty == 0) : ((sDone != 0) | (sNeed == 0) | (sFail != 0))) continue;  // (uniform)
+    if ((sDone != 0) | (sNeed == 0) | (sFail != 0)) continue;  // gnSelect (uniform)
     double* S = P.S + soff;
+    const auto mrow = gmem(P.tile_mask + (size_t)kTile * item);
     for (int e = threadIdx.x; e < kTile * kTile / 2; e += 256) {
-      const int r = ti * kTile + (e >> 5), c = tj * kTile + 2 * (e & 31);
+      const int rl = e >> 5, cl = 2 * (e & 31);
+      const int r = ti * kTile + rl, c = tj * kTile + cl;
       const double2 v{(r == c && r >= fdim) ? 1.0 : 0.0, (r == c + 1 && r >= fdim) ? 1.0 : 0.0};
-      *gmemw(reinterpret_cast<double2*>(S + (int64_t)r * fpad + c)) = v;
+      double* dst = S + (int64_t)r * fpad + c;
+      const unsigned cov = fill ? (unsigned)(mrow[rl] >> cl) & 3u : 0u;  // covered entries of the pair
+      if (cov == 0u) *gmemw(reinterpret_cast<double2*>(dst)) = v;
+      else if (cov == 2u) *gmemw(dst) = v.x;
+      else if (cov == 1u) *gmemw(dst + 1) = v.y;
     }
   }
 }
@@ -1153,9 +1161,9 @@ void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s) {
     else hipLaunchKernelGGL((k_lm_visit<2, false>), g, b, 0, s, P.self);
   }
 }
-void launch_assemble_pp(const DevProblem& P, hipStream_t s) {
-  if (P.n_asm_pp > 0) hipLaunchKernelGGL(k_assemble_pp, dim3((P.n_asm_pp + 3) / 4), dim3(256), 0, s, P.self);
-  if (P.n_asm_ppl > 0)
+void launch_assemble_pp(const DevProblem& P, hipStream_t s, int which) {
+  if (P.n_asm_pp > 0 && which != 2) hipLaunchKernelGGL(k_assemble_pp, dim3((P.n_asm_pp + 3) / 4), dim3(256), 0, s, P.self);
+  if (P.n_asm_ppl > 0 && which != 1)
     hipLaunchKernelGGL(k_assemble_pp_light, dim3((P.n_asm_ppl + 256 / kPplLanes - 1) / (256 / kPplLanes)), dim3(256), 0,
                        s, P.self);
 }
@@ -1180,9 +1188,9 @@ void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t 
   launch_fgrad(P, lin_mode, s);
 }
 void launch_lm_prep(const DevProblem& P, hipStream_t s) { launch_lm_visit(P, 2, s); }
-void launch_zero_S(const DevProblem& P, hipStream_t s, int post) {
+void launch_zero_S(const DevProblem& P, hipStream_t s, int fill) {
   const int per = P.n_win >= kManyWindows ? kZeroTiles : 1;
-  if (P.n_tiles > 0) hipLaunchKernelGGL(k_zero_S, dim3((P.n_tiles + per - 1) / per), dim3(256), 0, s, P.self, per, post);
+  if (P.n_tiles > 0) hipLaunchKernelGGL(k_zero_S, dim3((P.n_tiles + per - 1) / per), dim3(256), 0, s, P.self, per, fill);
 }
 void launch_assemble(const DevProblem& P, hipStream_t s) {
   launch_assemble_pp(P, s);

@@ -142,6 +142,7 @@ struct HostBatch {
   std::vector<int32_t> pair_win, pair_fi, pair_fj, pair_cbegin, pair_runs;
   std::vector<int32_t> asm_pp_items, asm_sb_items, asm_ppl_items;
   std::vector<int32_t> chol_panel_items, chol_panel_begin, chol_upd_items, chol_upd_begin, tile_items;
+  std::vector<uint64_t> tile_mask;
   int64_t n_band_updates = 0;
   std::vector<Contrib> pair_contrib;
   int64_t s_total = 0, linv_total = 0, fwd_total = 0;
@@ -998,6 +999,31 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       for (int j = 0; j <= i; ++j)
         if (B.tileNz[w][(size_t)i * T + j]) { B.tile_items.push_back(w); B.tile_items.push_back(i); B.tile_items.push_back(j); }
   }
+  {  // per non-zero tile row: the columns some block pair writes (k_zero_S fill mode clears the rest)
+    const size_t nt = B.tile_items.size() / 3;
+    B.tile_mask.assign(nt * kTile, 0ull);
+    std::vector<std::vector<int32_t>> itemOf(B.n_win);
+    for (size_t it = 0; it < nt; ++it) {
+      const int w = B.tile_items[3 * it], i = B.tile_items[3 * it + 1], j = B.tile_items[3 * it + 2];
+      if (itemOf[w].empty()) itemOf[w].assign((size_t)B.tileT[w] * B.tileT[w], -1);
+      itemOf[w][(size_t)i * B.tileT[w] + j] = (int32_t)it;
+    }
+    for (size_t k = 0; k < B.pair_win.size(); ++k) {
+      const int w = B.pair_win[k], fi = B.pair_fi[k], fj = B.pair_fj[k], T = B.tileT[w];
+      const int oi = B.fb_off[fi], ni = B.fb_kind[fi] == 0 ? 6 : 9, oj = B.fb_off[fj], nj = B.fb_kind[fj] == 0 ? 6 : 9;
+      for (int r = oi; r < oi + ni; ++r) {
+        for (int c0 = oj; c0 < oj + nj;) {
+          const int tj = c0 / kTile, c1 = std::min(oj + nj, (tj + 1) * kTile);
+          if (tj > r / kTile) break;  // a diagonal block's upper part across a tile border: upper tile
+          const int it = itemOf[w][(size_t)(r / kTile) * T + tj];
+          if (it < 0) throw std::logic_error("block pair outside the non-zero tiles");
+          const int n = c1 - c0, lo = c0 % kTile;
+          B.tile_mask[(size_t)it * kTile + r % kTile] |= (n == 64 ? ~0ull : ((1ull << n) - 1ull) << lo);
+          c0 = c1;
+        }
+      }
+    }
+  }
   B.lm_visit_begin.push_back((int)B.visit_pose.size());
   B.lmg_begin.push_back((int)B.lm_win.size());  // groups: begin of each, then the end
   {  // each window's groups are contiguous (built window by window)
@@ -1393,7 +1419,7 @@ struct okvisgpu_ctx {
     const size_t o_pruns = upl(B.pair_runs);
     const size_t o_tnz = upl(B.tile_nz), o_tnzoff = upl(B.win_tnzoff);
     const size_t o_app = upl(B.asm_pp_items), o_asb = upl(B.asm_sb_items), o_appl = upl(B.asm_ppl_items);
-    const size_t o_ti = upl(B.tile_items);
+    const size_t o_ti = upl(B.tile_items), o_tmask = upl(B.tile_mask);
     const size_t o_cpi = upl(B.chol_panel_items), o_cpb = upl(B.chol_panel_begin), o_cui = upl(B.chol_upd_items),
                  o_cub = upl(B.chol_upd_begin);
     const size_t nf = std::max(1, B.f_total), nl3 = std::max<size_t>(1, (size_t)3 * D.n_lm);
@@ -1502,6 +1528,7 @@ struct okvisgpu_ctx {
     D.n_asm_pp = (int)B.asm_pp_items.size(); D.n_asm_sb = (int)B.asm_sb_items.size();
     D.asm_ppl_items = ip(o_appl); D.n_asm_ppl = (int)B.asm_ppl_items.size();
     D.tile_items = ip(o_ti);
+    D.tile_mask = reinterpret_cast<const uint64_t*>(base + place(o_tmask));
     D.n_tiles = (int)(B.tile_items.size() / 3);
     D.S = dp(o_S);
     D.Linv = dp(o_Linv);
@@ -1544,12 +1571,14 @@ struct okvisgpu_ctx {
     d.min_relative_decrease = o.min_relative_decrease;
     d.min_lm_diagonal = o.min_lm_diagonal;
     d.max_lm_diagonal = o.max_lm_diagonal;
-    // Cholesky schedule (measured on MI355X, S50 windows): below half a window per CU the
-    // tile-parallel launches spread each window over many CUs; up to one window per CU the
-    // wave-specialised kernel (one workgroup per window, factorisation overlapped with the MFMA
-    // tiles); beyond that the plain persistent kernel (two windows per CU)
+    // Cholesky schedule (measured on MI355X, S50 windows, round 3: bench window-it/s of schedules
+    // 1 / 2 / 3 at 16: 20.3k / 24.6k / 18.6k, 64: 64.5k / 70.9k / 58.6k, 128: 102.2k / 92.8k / 92.6k,
+    // 192: 129.1k / 109.1k / 116.5k, 256: 155.6k / - / 140.4k, 2,048: 189.9k / - / 153.5k): below
+    // half a window per CU the tile-parallel launches spread each window over many CUs; from there
+    // the persistent kernel. The wave-specialised kernel no longer wins anywhere since the
+    // persistent kernel's sub-panel look-ahead; it stays selectable (cholesky_schedule = 3).
     int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 3 ? o.cholesky_schedule : 0;
-    if (sched == 0) sched = P.n_win >= cuCount ? 1 : (2 * P.n_win >= cuCount && wsFits() ? 3 : 2);
+    if (sched == 0) sched = 2 * P.n_win >= cuCount ? 1 : 2;
     if (sched == 3 && !wsFits()) sched = 2;
     // the persistent kernel keeps the window's rhs / y in dynamic LDS next to its static tiles:
     // a reduced dimension beyond what fits falls back to the tile-parallel launches
@@ -1668,9 +1697,9 @@ struct okvisgpu_ctx {
 
   void launchIteration() {
     launch_lm_prep(P, stream);
-    launch_assemble(P, stream);  // (S was cleared after the previous factorisation: post zeroing)
+    launch_zero_S(P, stream, 1);  // the tile entries the assembly does not write
+    launch_assemble(P, stream);
     launch_cholesky(P, stream);
-    launch_zero_S(P, stream, 1);
     launch_gn_backsub(P, stream);
     launch_jv(P, stream);
     launch_dogleg(P, stream);
@@ -1705,17 +1734,21 @@ struct okvisgpu_ctx {
       HIPCHK(hipEventRecord(e, from));
       HIPCHK(hipStreamWaitEvent(stream, e, 0));
     };
-    // Gauss-Newton system: the stale Z rebuilt (few windows after the first iteration); both
-    // assembly kernels (S was cleared right after the previous factorisation, below)
+    // Gauss-Newton system: the stale Z rebuilt (few windows after the first iteration), then the
+    // assembly kernels and the clearing of the tile entries they do not write, on four streams
+    // (disjoint entries of S)
     launch_lm_prep(P, stream);
     fork(side[0]);
-    launch_assemble_sb(P, side[0]);
-    launch_assemble_pp(P, stream);
-    join(side[0]);
-    launch_cholesky(P, stream);
-    // S of the factored windows cleared beside the rest of the iteration (joined at its end)
+    fork(side[1]);
     fork(side[2]);
     launch_zero_S(P, side[2], 1);
+    launch_assemble_sb(P, side[0]);
+    launch_assemble_pp(P, side[1], 2);
+    launch_assemble_pp(P, stream, 1);
+    join(side[0]);
+    join(side[1]);
+    join(side[2]);
+    launch_cholesky(P, stream);
     launch_gn_finalize(P, stream);
     fork(side[0]);
     launch_jv(P, side[0]);
@@ -1738,7 +1771,6 @@ struct okvisgpu_ctx {
     launch_lm_blocks(P, 1, stream);
     join(side[0]);
     launch_fgrad(P, 1, stream);
-    join(side[2]);  // k_gradnorm clears WinState::s_dirty
     launch_gradnorm(P, 1, stream);
   }
 
@@ -1935,7 +1967,7 @@ int okvisgpu_solve_begin(okvisgpu_ctx* c, const okvisgpu_options* o) {
     c->dropGraph();  // options are baked into the captured kernel arguments
     c->uploadParams();
     c->resetStates(1e-8);
-    launch_zero_S(c->P, c->stream, 0);  // every window: the iteration clears S after factorising only
+    launch_zero_S(c->P, c->stream, 0);  // every entry (the iteration then clears only the fill)
     c->launchInit(2);
     c->failInitialHostEvaluations();
     c->ensureGraph();
@@ -2056,7 +2088,6 @@ int okvisgpu_profile_iteration(okvisgpu_ctx* c, double* ms) {
     launch_zero_S(P, s); mark(1);
     launch_assemble(P, s); mark(2);
     launch_cholesky(P, s); mark(3);
-    launch_zero_S(P, s, 1); mark(1);
     launch_gn_finalize(P, s); mark(5);
     launch_lm_backsub(P, s); mark(4);
     launch_jv(P, s); mark(6);
