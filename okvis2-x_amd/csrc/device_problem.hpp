@@ -265,8 +265,6 @@ struct DevProblem {
   // window is block-banded and LLT creates no fill outside its envelope, so only structurally
   // non-zero 64x64 tiles are zeroed, factored and updated (bitwise identical to the dense LLT).
   const int32_t* tile_items;         // (w, i, j) every structurally non-zero tile (i >= j)
-  const uint64_t* tile_mask;         // [n_tiles][64] per tile row: the columns some block pair of the
-                                     // assembly writes (bit c = tile column c)
   // tile-parallel schedule (few windows): per step k, the panel tiles (w, i) and the band updates
   // (w, i, j) of all windows; begin offsets per k, host copies for the launch sizes
   const int32_t* chol_panel_items;

@@ -757,17 +757,16 @@ __device__ __forceinline__ bool gnSelect(const DevProblem& P, int w) {
   return !s.done && s.need_gn && !s.gn_failed;
 }
 
-// Clears the structurally non-zero tiles of S of the windows about to assemble (gnSelect;
-// kZeroTiles consecutive tiles per workgroup; padded diagonal = 1). Zero tiles are never written by
-// the factorisation and stay zero from the initial arena clear. Each tile's record and window are
-// loaded before any test, 16-byte stores.
-//   fill = 0: every entry (solve start, the eager paths);
-//   fill = 1: only the entries no block pair of the assembly writes (DevProblem::tile_mask: the fill
-//             inside the tile envelope and the padding, ~3/4 of the tiles' area for S50) -- disjoint
-//             from the assembly's stores, so the captured iteration runs it beside the assembly
-//             kernels instead of on the path.
+// Clears the structurally non-zero tiles of S (kZeroTiles consecutive tiles per workgroup; padded
+// diagonal = 1). Zero tiles are never written by the factorisation and stay zero from the initial
+// arena clear. Each tile's record and window are loaded before any test, 16-byte stores.
+//   tail = 0: the windows about to assemble (gnSelect; solve start and the eager paths);
+//   tail = 1: every window not done, launched after the candidate's cost reduction of the captured
+//             iteration, beside the linearisation: S is dead from there on (a rejected step reuses
+//             the stored GN step, a failed factorisation retries after a fresh assembly), so the
+//             next iteration's assembly finds it clear and the clear is off the critical path.
 constexpr int kZeroTiles = 4;  // (one per workgroup below kManyWindows windows: latency)
-__global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ Pp, int per, int fill) {
+__global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ Pp, int per, int tail) {
   const DevProblem& P = *Pp;
   const auto ti3 = gmem(P.tile_items);
   for (int u = 0; u < per; ++u) {
@@ -775,22 +774,17 @@ __global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ P
     if (item >= P.n_tiles) return;
     const int w = ti3[3 * item], ti = ti3[3 * item + 1], tj = ti3[3 * item + 2];
     const auto gst = gmem(P.st + w);
-    const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed;
+    const int sDone = gst->done, sNeed = gst->need_gn | tail, sFail = gst->gn_failed & (tail ^ 1);
     const int fpad = gmem(P.win_fpad)[w], fdim = gmem(P.win_fdim)[w];
     const int64_t soff = gmem(P.win_soff)[w];
     asm volatile("" ::"v"(fpad), "v"(fdim), "v"(soff));
-    if ((sDone != 0) | (sNeed == 0) | (sFail != 0)) continue;  // gnSelect (uniform)
+    if ((sDone != 0) | (sNeed == 0) | (sFail != 0)) continue;  // uniform
     double* S = P.S + soff;
-    const auto mrow = gmem(P.tile_mask + (size_t)kTile * item);
     for (int e = threadIdx.x; e < kTile * kTile / 2; e += 256) {
       const int rl = e >> 5, cl = 2 * (e & 31);
       const int r = ti * kTile + rl, c = tj * kTile + cl;
       const double2 v{(r == c && r >= fdim) ? 1.0 : 0.0, (r == c + 1 && r >= fdim) ? 1.0 : 0.0};
-      double* dst = S + (int64_t)r * fpad + c;
-      const unsigned cov = fill ? (unsigned)(mrow[rl] >> cl) & 3u : 0u;  // covered entries of the pair
-      if (cov == 0u) *gmemw(reinterpret_cast<double2*>(dst)) = v;
-      else if (cov == 2u) *gmemw(dst) = v.x;
-      else if (cov == 1u) *gmemw(dst + 1) = v.y;
+      *gmemw(reinterpret_cast<double2*>(S + (int64_t)r * fpad + c)) = v;
     }
   }
 }
@@ -1161,9 +1155,9 @@ void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s) {
     else hipLaunchKernelGGL((k_lm_visit<2, false>), g, b, 0, s, P.self);
   }
 }
-void launch_assemble_pp(const DevProblem& P, hipStream_t s, int which) {
-  if (P.n_asm_pp > 0 && which != 2) hipLaunchKernelGGL(k_assemble_pp, dim3((P.n_asm_pp + 3) / 4), dim3(256), 0, s, P.self);
-  if (P.n_asm_ppl > 0 && which != 1)
+void launch_assemble_pp(const DevProblem& P, hipStream_t s) {
+  if (P.n_asm_pp > 0) hipLaunchKernelGGL(k_assemble_pp, dim3((P.n_asm_pp + 3) / 4), dim3(256), 0, s, P.self);
+  if (P.n_asm_ppl > 0)
     hipLaunchKernelGGL(k_assemble_pp_light, dim3((P.n_asm_ppl + 256 / kPplLanes - 1) / (256 / kPplLanes)), dim3(256), 0,
                        s, P.self);
 }
@@ -1188,9 +1182,9 @@ void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t 
   launch_fgrad(P, lin_mode, s);
 }
 void launch_lm_prep(const DevProblem& P, hipStream_t s) { launch_lm_visit(P, 2, s); }
-void launch_zero_S(const DevProblem& P, hipStream_t s, int fill) {
+void launch_zero_S(const DevProblem& P, hipStream_t s, int tail) {
   const int per = P.n_win >= kManyWindows ? kZeroTiles : 1;
-  if (P.n_tiles > 0) hipLaunchKernelGGL(k_zero_S, dim3((P.n_tiles + per - 1) / per), dim3(256), 0, s, P.self, per, fill);
+  if (P.n_tiles > 0) hipLaunchKernelGGL(k_zero_S, dim3((P.n_tiles + per - 1) / per), dim3(256), 0, s, P.self, per, tail);
 }
 void launch_assemble(const DevProblem& P, hipStream_t s) {
   launch_assemble_pp(P, s);

@@ -29,14 +29,12 @@ void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_imu_hess(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_lm_prep(const DevProblem& P, hipStream_t s);
-// the non-zero tiles of the windows about to assemble: fill = 0 every entry; fill = 1 only the
-// entries the assembly does not write (beside the assembly kernels)
-void launch_zero_S(const DevProblem& P, hipStream_t s, int fill = 0);
+// the non-zero tiles of S: tail = 0 of the windows about to assemble; tail = 1 of every window not
+// done (end of the captured iteration, S dead)
+void launch_zero_S(const DevProblem& P, hipStream_t s, int tail = 0);
 void launch_assemble(const DevProblem& P, hipStream_t s);
 void launch_lm_backsub(const DevProblem& P, hipStream_t s);  // kernels_backsub.hip: + landmark dogleg vectors, J*v
-// which: 0 both pose-pose kernels, 1 the wavefront-per-pair one, 2 the light pairs (disjoint blocks:
-// the captured iteration runs them on two streams)
-void launch_assemble_pp(const DevProblem& P, hipStream_t s, int which = 0);
+void launch_assemble_pp(const DevProblem& P, hipStream_t s);
 void launch_assemble_sb(const DevProblem& P, hipStream_t s);
 void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s);  // 0/1: linearisation, 2: GN prep
 void launch_gn_finalize(const DevProblem& P, hipStream_t s);

@@ -142,7 +142,6 @@ struct HostBatch {
   std::vector<int32_t> pair_win, pair_fi, pair_fj, pair_cbegin, pair_runs;
   std::vector<int32_t> asm_pp_items, asm_sb_items, asm_ppl_items;
   std::vector<int32_t> chol_panel_items, chol_panel_begin, chol_upd_items, chol_upd_begin, tile_items;
-  std::vector<uint64_t> tile_mask;
   int64_t n_band_updates = 0;
   std::vector<Contrib> pair_contrib;
   int64_t s_total = 0, linv_total = 0, fwd_total = 0;
@@ -999,31 +998,6 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       for (int j = 0; j <= i; ++j)
         if (B.tileNz[w][(size_t)i * T + j]) { B.tile_items.push_back(w); B.tile_items.push_back(i); B.tile_items.push_back(j); }
   }
-  {  // per non-zero tile row: the columns some block pair writes (k_zero_S fill mode clears the rest)
-    const size_t nt = B.tile_items.size() / 3;
-    B.tile_mask.assign(nt * kTile, 0ull);
-    std::vector<std::vector<int32_t>> itemOf(B.n_win);
-    for (size_t it = 0; it < nt; ++it) {
-      const int w = B.tile_items[3 * it], i = B.tile_items[3 * it + 1], j = B.tile_items[3 * it + 2];
-      if (itemOf[w].empty()) itemOf[w].assign((size_t)B.tileT[w] * B.tileT[w], -1);
-      itemOf[w][(size_t)i * B.tileT[w] + j] = (int32_t)it;
-    }
-    for (size_t k = 0; k < B.pair_win.size(); ++k) {
-      const int w = B.pair_win[k], fi = B.pair_fi[k], fj = B.pair_fj[k], T = B.tileT[w];
-      const int oi = B.fb_off[fi], ni = B.fb_kind[fi] == 0 ? 6 : 9, oj = B.fb_off[fj], nj = B.fb_kind[fj] == 0 ? 6 : 9;
-      for (int r = oi; r < oi + ni; ++r) {
-        for (int c0 = oj; c0 < oj + nj;) {
-          const int tj = c0 / kTile, c1 = std::min(oj + nj, (tj + 1) * kTile);
-          if (tj > r / kTile) break;  // a diagonal block's upper part across a tile border: upper tile
-          const int it = itemOf[w][(size_t)(r / kTile) * T + tj];
-          if (it < 0) throw std::logic_error("block pair outside the non-zero tiles");
-          const int n = c1 - c0, lo = c0 % kTile;
-          B.tile_mask[(size_t)it * kTile + r % kTile] |= (n == 64 ? ~0ull : ((1ull << n) - 1ull) << lo);
-          c0 = c1;
-        }
-      }
-    }
-  }
   B.lm_visit_begin.push_back((int)B.visit_pose.size());
   B.lmg_begin.push_back((int)B.lm_win.size());  // groups: begin of each, then the end
   {  // each window's groups are contiguous (built window by window)
@@ -1419,7 +1393,7 @@ struct okvisgpu_ctx {
     const size_t o_pruns = upl(B.pair_runs);
     const size_t o_tnz = upl(B.tile_nz), o_tnzoff = upl(B.win_tnzoff);
     const size_t o_app = upl(B.asm_pp_items), o_asb = upl(B.asm_sb_items), o_appl = upl(B.asm_ppl_items);
-    const size_t o_ti = upl(B.tile_items), o_tmask = upl(B.tile_mask);
+    const size_t o_ti = upl(B.tile_items);
     const size_t o_cpi = upl(B.chol_panel_items), o_cpb = upl(B.chol_panel_begin), o_cui = upl(B.chol_upd_items),
                  o_cub = upl(B.chol_upd_begin);
     const size_t nf = std::max(1, B.f_total), nl3 = std::max<size_t>(1, (size_t)3 * D.n_lm);
@@ -1528,7 +1502,6 @@ struct okvisgpu_ctx {
     D.n_asm_pp = (int)B.asm_pp_items.size(); D.n_asm_sb = (int)B.asm_sb_items.size();
     D.asm_ppl_items = ip(o_appl); D.n_asm_ppl = (int)B.asm_ppl_items.size();
     D.tile_items = ip(o_ti);
-    D.tile_mask = reinterpret_cast<const uint64_t*>(base + place(o_tmask));
     D.n_tiles = (int)(B.tile_items.size() / 3);
     D.S = dp(o_S);
     D.Linv = dp(o_Linv);
@@ -1697,7 +1670,7 @@ struct okvisgpu_ctx {
 
   void launchIteration() {
     launch_lm_prep(P, stream);
-    launch_zero_S(P, stream, 1);  // the tile entries the assembly does not write
+    launch_zero_S(P, stream, 0);
     launch_assemble(P, stream);
     launch_cholesky(P, stream);
     launch_gn_backsub(P, stream);
@@ -1739,15 +1712,9 @@ struct okvisgpu_ctx {
     // (disjoint entries of S)
     launch_lm_prep(P, stream);
     fork(side[0]);
-    fork(side[1]);
-    fork(side[2]);
-    launch_zero_S(P, side[2], 1);
     launch_assemble_sb(P, side[0]);
-    launch_assemble_pp(P, side[1], 2);
-    launch_assemble_pp(P, stream, 1);
+    launch_assemble_pp(P, stream);
     join(side[0]);
-    join(side[1]);
-    join(side[2]);
     launch_cholesky(P, stream);
     launch_gn_finalize(P, stream);
     fork(side[0]);
@@ -1765,6 +1732,10 @@ struct okvisgpu_ctx {
     join(side[0]);
     join(side[1]);
     launch_reduce(P, R_COST_CAND, stream);
+    // S is dead once the step is decided: cleared for the next iteration's assembly beside the
+    // linearisation (k_zero_S tail mode; solve_begin clears it for the first iteration)
+    fork(side[2]);
+    launch_zero_S(P, side[2], 1);
     // linearisation at the accepted point
     fork(side[0]);
     launch_imu_hess(P, 1, side[0]);
@@ -1772,6 +1743,7 @@ struct okvisgpu_ctx {
     join(side[0]);
     launch_fgrad(P, 1, stream);
     launch_gradnorm(P, 1, stream);
+    join(side[2]);
   }
 
   void ensureGraph() {
@@ -1967,7 +1939,7 @@ int okvisgpu_solve_begin(okvisgpu_ctx* c, const okvisgpu_options* o) {
     c->dropGraph();  // options are baked into the captured kernel arguments
     c->uploadParams();
     c->resetStates(1e-8);
-    launch_zero_S(c->P, c->stream, 0);  // every entry (the iteration then clears only the fill)
+    launch_zero_S(c->P, c->stream, 0);  // the first iteration's S (the forked graph clears it at its end)
     c->launchInit(2);
     c->failInitialHostEvaluations();
     c->ensureGraph();

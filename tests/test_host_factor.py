@@ -188,10 +188,13 @@ def test_gpu_host_fixed_factors_parity(og, parity):
 
 
 @pytest.mark.gpu
-def test_gpu_host_failure_parity(og, parity):
+@pytest.mark.parametrize("serial", ["1", "0"])
+def test_gpu_host_failure_parity(og, parity, monkeypatch, serial):
     """Failure at the initial point (window ends with FAILURE, parameters untouched) and at
     candidates (rejected steps) give the oracle's summaries; the other windows of the batch are
-    unaffected."""
+    unaffected. Both captured graphs: the forked one clears S at the end of every iteration for the
+    next (k_zero_S tail mode), which the rejected steps of window 1 exercise."""
+    monkeypatch.setenv("OKVISGPU_SERIAL_GRAPH", serial)
     P0, _, _ = gps_window(seed=11, fail=lambda h, prm: h == 3)
     P1, f1, _ = gps_window(seed=12)
     G0 = P1.poses[N_KF].copy()
@@ -202,4 +205,4 @@ def test_gpu_host_failure_parity(og, parity):
     gsum, csum, gpu, cpu = _solve_both([P0, P1, P2], o)
     assert gsum[0]["termination"] == "FAILURE" and np.array_equal(gpu[0][0], x0)
     assert gsum[1]["num_unsuccessful_steps"] >= 1
-    _assert_parity(parity, gsum, csum, gpu, cpu, "host evaluation failures")
+    _assert_parity(parity, gsum, csum, gpu, cpu, f"host evaluation failures, serial graph {serial}")
