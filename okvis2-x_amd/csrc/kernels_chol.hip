@@ -49,6 +49,22 @@ __device__ unsigned long long g_cholClk[32];
 #define CLK(i)
 #define CLKW(i, cond)
 #endif
+// Development-only phase cut of potrfTile (scripts/ubench_ptile.hip): return after phase n.
+#ifdef OKG_POTRF_STOP
+#define POTRF_STOP(n) \
+  if (OKG_POTRF_STOP == (n)) return true;
+#else
+#define POTRF_STOP(n)
+#endif
+// Development-only sweep timeline (scripts/ubench_ptile.hip, -DOKG_SWEEP_TRACE): lane 0 of the
+// sweep wavefronts of workgroup 0 stores s_memtime at each hand-over point.
+#ifdef OKG_SWEEP_TRACE
+__device__ unsigned long long g_sweepT[2][8][8];
+#define STR(a, s, i) \
+  if (lane == 0) sTr[a][s][i] = __builtin_amdgcn_s_memtime();
+#else
+#define STR(a, s, i)
+#endif
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
@@ -190,24 +206,45 @@ __device__ __forceinline__ int ldsAcquire(int* p) {
 __device__ __forceinline__ void ldsRelease(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// LDS flags with LDS-only ordering (the diagonal tile's hand-overs, where only LDS data is passed
+// between wavefronts): the fences are restricted to the local address space. A release at
+// workgroup scope also waits for every outstanding global store of the wavefront (vmcnt(0)),
+// which stalled the X-storing wavefronts by ~2k cycles per hand-over.
+__device__ __forceinline__ int ldsAcquireL(int* p) {
+  const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  return v;
+}
+__device__ __forceinline__ void ldsReleaseL(int* p, int v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 // Poll interval of the LDS flag waits (s_sleep units of 64 clocks; build knob: 0, 1 and 2 measured
 // within noise of each other at 2,048 windows and on one window).
 #ifndef OKG_WAIT_SLEEP
 #define OKG_WAIT_SLEEP 1
 #endif
 // Wave-uniform wait for *p >= v; false once the factor wavefront reported a failed pivot.
+template <bool LOCAL = false>
 __device__ __forceinline__ bool waitFlag(int* p, int v, int* fail) {
   for (;;) {
-    if (ldsAcquire(p) >= v) return true;
-    if (ldsAcquire(fail)) return false;
+    if ((LOCAL ? ldsAcquireL(p) : ldsAcquire(p)) >= v) return true;
+    if (LOCAL ? ldsAcquireL(fail) : ldsAcquire(fail)) return false;
     __builtin_amdgcn_s_sleep(OKG_WAIT_SLEEP);
   }
 }
 // Barrier of n wavefronts on a monotonic arrival counter (gen counts this wavefront's barriers).
+template <bool LOCAL = false>
 __device__ __forceinline__ void waveBarrier(int* ctr, int& gen, int n, int lane) {
   ++gen;
-  if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  while (ldsAcquire(ctr) < gen * n) __builtin_amdgcn_s_sleep(OKG_WAIT_SLEEP);
+  if (LOCAL) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (ldsAcquireL(ctr) < gen * n) __builtin_amdgcn_s_sleep(OKG_WAIT_SLEEP);
+  } else {
+    if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (ldsAcquire(ctr) < gen * n) __builtin_amdgcn_s_sleep(OKG_WAIT_SLEEP);
+  }
 }
 
 // One 8-column sub-panel of the in-LDS 64x64 LLT on one wavefront (lane = row i of the tile; the
@@ -257,15 +294,25 @@ __device__ __forceinline__ void storeRow8(double* sA, int c0, const double (&x)[
 // column j = lane each, y_m = (delta_mj - sum_{k<m} L_mk y_k) / L_mm, to xd (row stride kLd).
 __device__ __forceinline__ void inv8(const double* sA, const double* sRl, double* xd, int c0, int lane) {
   if (lane >= 8) return;
+  // every operand into registers before the first store (xd may alias sA for the compiler, so a
+  // load after a store would wait for it: one LDS round trip per row)
+  double L[8][8], rl[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    rl[m] = sRl[c0 + m];
+#pragma unroll
+    for (int k = 0; k < m; ++k) L[m][k] = sA[(c0 + m) * kLd + c0 + k];
+  }
   double y[8];
 #pragma unroll
   for (int m = 0; m < 8; ++m) {
     double v = (m == lane) ? 1.0 : 0.0;
 #pragma unroll
-    for (int k = 0; k < m; ++k) v -= sA[(c0 + m) * kLd + c0 + k] * y[k];
-    y[m] = v * sRl[c0 + m];
-    xd[m * kLd + lane] = y[m];
+    for (int k = 0; k < m; ++k) v -= L[m][k] * y[k];
+    y[m] = v * rl[m];
   }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) xd[m * kLd + lane] = y[m];
 }
 // The whole sub-panel on one wavefront: factor, L into the tile, 1/L_cc to sRl and the 8x8
 // diagonal inverse block to xd. Returns false (wave-uniform) at a non-positive pivot.
@@ -317,15 +364,84 @@ __device__ __forceinline__ void trailing8(double* sA, int c0, int wg, int nw, in
   trailingFrom(sA, c0, c0 + 8, wg, nw, lane);
 }
 
+// X = L^-1 of the in-LDS diagonal tile by 16-row block rows (sX holds X, sA the final L):
+// X21 = -X22 (L21 X11) of the diagonal 16x16 block q, whose 8x8 diagonal inverses are in sX
+// (one wavefront; lane = (row m, column j)).
+__device__ __forceinline__ void xDiag16(const double* sA, double* sX, int q, int lane) {
+  const int m = lane >> 3, j = lane & 7;
+  const int b = 16 * q;
+  double t = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t += sA[(b + 8 + m) * kLd + b + k] * sX[(b + k) * kLd + b + j];
+  sX[(b + 8 + m) * kLd + b + j] = t;  // T = L21 X11 staged in place (this wavefront only)
+  __builtin_amdgcn_wave_barrier();
+  double tk[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) tk[k] = sX[(b + 8 + k) * kLd + b + j];
+  double v = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v += sX[(b + 8 + m) * kLd + b + 8 + k] * tk[k];
+  __builtin_amdgcn_wave_barrier();
+  sX[(b + 8 + m) * kLd + b + j] = -v;
+}
+// X_qj = -X_qq (sum_{m=j}^{q-1} L_qm X_mj), j < q, on the matrix cores (one wavefront).
+__device__ __forceinline__ void xOffDiag16(const double* sA, double* sX, int q, int j, int lane) {
+  dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+  for (int m = j; m < q; ++m)  // T = sum L_qm X_mj   (B[k][n] = X[16m + k][16j + n])
+    mfma16<1>(sA + 16 * q * kLd + 16 * m, kLd, sX + 16 * m * kLd + 16 * j, kLd, 1, 1.0, acc, lane);
+  double* Xqj = sX + 16 * q * kLd + 16 * j;
+  storeC16(Xqj, kLd, acc, lane);  // T staged in the (q, j) block (this wavefront only)
+  dbl4 x = dbl4{0.0, 0.0, 0.0, 0.0};
+  mfma16<1>(sX + 16 * q * kLd + 16 * q, kLd, Xqj, kLd, 1, -1.0, x, lane);
+  storeC16(Xqj, kLd, x, lane);
+}
+// y_r = sum_{j <= r} X_rj rhs_j for the 16 rows of block q (rhs in sy[0..63], y to sy[64 + r]):
+// lane = (row r, quarter p of the columns j = p mod 4), fixed butterfly over the quarters.
+__device__ __forceinline__ void yBlock16(const double* sX, double* sy, int q, int lane) {
+  const int r = 16 * q + (lane & 15), p = lane >> 4;
+  double xv[16], rv[16];
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {  // all operands first (columns beyond r are masked)
+    xv[it] = sX[r * kLd + p + 4 * it];
+    rv[it] = sy[p + 4 * it];
+  }
+  double a = 0.0;
+#pragma unroll
+  for (int it = 0; it < 16; ++it) a += (p + 4 * it <= r) ? xv[it] * rv[it] : 0.0;
+  a += __shfl_xor(a, 16, 64);
+  a += __shfl_xor(a, 32, 64);
+  if (p == 0) sy[kTile + r] = a;
+}
+// The 16 rows of block q of X to Li (row-major 64 x 64) by three wavefronts (g < 3). The persistent
+// schedule's backward substitution masks the upper triangle of X (bsDiag), so it stores the lower
+// one only; the tile-parallel update kernels stage X whole for the MFMAs (zeros stored).
+template <int kCaller>
+__device__ __forceinline__ void xStoreRows16(const double* sX, double* Li, int q, int g, int lane) {
+  double2 v[3];
+#pragma unroll
+  for (int it = 0; it < 3; ++it) {  // loads first, then the stores
+    const int e = min(64 * g + lane + 192 * it, 511), r = 16 * q + (e >> 5), c = 2 * (e & 31);
+    v[it] = double2{(c <= r) ? sX[r * kLd + c] : 0.0, (c + 1 <= r) ? sX[r * kLd + c + 1] : 0.0};
+  }
+#pragma unroll
+  for (int it = 0; it < 3; ++it) {
+    const int e = 64 * g + lane + 192 * it, r = 16 * q + (e >> 5), c = 2 * (e & 31);
+    if (e < 512 && (kCaller != 0 || c <= r)) *reinterpret_cast<double2*>(Li + r * kTile + c) = v[it];
+  }
+}
+
 // Diagonal tile: L_kk (in sA only: every later use of the diagonal goes through X, so L_kk is
 // never stored), X = L_kk^-1 (into sX and the Linv store) and y_k = X rhs_k
 // (sy holds rhs_k on entry, y_k on exit; the tile-parallel callers also write it to workk, the
 // forward-substitution vector in global memory; the persistent kernel keeps y in LDS and passes
 // no workk). Right-looking LLT in 8-column
-// sub-panels (subPanel8 on wavefront 0, the rank-8 trailing updates on the matrix cores of all 4
-// wavefronts), then X blockwise: the 8x8 diagonal inverses come out of the sub-panels, the 16x16
-// diagonal blocks are completed with X21 = -X22 L21 X11 (one wavefront each), and
-// X_ij = -X_ii (sum_{m=j}^{i-1} L_im X_mj) by sub-diagonal on the matrix cores.
+// sub-panels (the chain on wavefront 0, the rank-8 trailing updates on the matrix cores of
+// wavefronts 1-3), and X by 16-row block rows as soon as the sweep has passed them, on wavefronts
+// 1-3 while wavefront 0 factors the next sub-panels: the 8x8 diagonal inverses come out of the
+// sub-panels, X21 = -X22 L21 X11 completes the 16x16 diagonal block (xDiag16) and
+// X_qj = -X_qq (sum_{m=j}^{q-1} L_qm X_mj) the rest of the block row on the matrix cores
+// (xOffDiag16); y_q and the Linv store of the block row follow. Only block row 3 remains after
+// the sweep (one isolated tile, scripts/ubench_ptile.hip: 24.0 -> 22.6 us).
 // Returns false (uniformly) at a non-positive pivot.
 // (one non-inlined instantiation per calling kernel: a shared callee gets a generic register
 // budget that halves the persistent kernel's occupancy)
@@ -334,6 +450,9 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
                                       double* sRl, int* sFl, int t, bool haveTile) {
   const int wave = t >> 6, lane = t & 63;
   CLK_INIT
+#ifdef OKG_SWEEP_TRACE
+  __shared__ unsigned long long sTr[2][8][8];
+#endif
   if (!haveTile) loadTile(Sg, ld, 0, 0, sA, t);  // (else the caller left S_kk in sA)
 #pragma unroll
   for (int u = 0; u < 16; ++u) {
@@ -356,8 +475,10 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
     for (int s = 0; s < 8; ++s) {
       const int c0 = 8 * s;
       CLK(25)
-      if (s >= 2 && !waitFlag(&sFl[1], s - 1, &sFl[2])) break;  // trailing update of sub-panel s-2
+      STR(0, s, 0)
+      if (s >= 2 && !waitFlag<true>(&sFl[1], s - 1, &sFl[2])) break;  // trailing update of sub-panel s-2
       CLK(21)
+      STR(0, s, 1)
       double r[8], x[8], rl[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) r[k] = sA[i * kLd + c0 + k];
@@ -375,18 +496,21 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
         __builtin_amdgcn_wave_barrier();
       }
       CLK(22)
+      STR(0, s, 2)
       if (!chol8Row(sA, c0, r, x, rl)) {
-        if (lane == 0) ldsRelease(&sFl[2], 1);
+        if (lane == 0) ldsReleaseL(&sFl[2], 1);
         break;
       }
       CLK(23)
+      STR(0, s, 3)
       storeRow8(sA, c0, x, i);
       if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) sRl[c0 + k] = rl[k];
-        ldsRelease(&sFl[0], s + 1);
+        ldsReleaseL(&sFl[0], s + 1);
       }
       CLK(24)
+      STR(0, s, 4)
 #pragma unroll
       for (int k = 0; k < 8; ++k) xp[k] = x[k];
     }
@@ -395,76 +519,44 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
     int gen = 0;
 #pragma unroll 1
     for (int s = 0; s < 8; ++s) {
-      if (!waitFlag(&sFl[0], s + 1, &sFl[2])) break;
+      if (!waitFlag<true>(&sFl[0], s + 1, &sFl[2])) break;
+      if (g == 0) { STR(1, s, 0) }
+#ifndef OKG_SWEEP_SOLO
       if (g == 0) inv8(sA, sRl, sX + 8 * s * kLd + 8 * s, 8 * s, lane);
+      if (g == 0) { STR(1, s, 1) }
       if (s < 6) trailingFrom(sA, 8 * s, 8 * s + 16, g, 3, lane);
-      waveBarrier(&sFl[3], gen, 3, lane);
-      if (g == 0 && lane == 0) ldsRelease(&sFl[1], s + 1);
+#endif
+      if (g == 0) { STR(1, s, 2) }
+      waveBarrier<true>(&sFl[3], gen, 3, lane);
+      if (g == 0) { STR(1, s, 3) }
+      if (g == 0 && lane == 0) ldsReleaseL(&sFl[1], s + 1);
+      if (s & 1) {
+        // the 16 columns of block q are factored: block row q of X, y_q and the X store of those
+        // rows, in the shadow of wavefront 0's next sub-panels (only block row 3 follows the sweep)
+        const int q = s >> 1;
+        if (g == 0) xDiag16(sA, sX, q, lane);
+        waveBarrier<true>(&sFl[3], gen, 3, lane);
+        if (g == 0) { STR(1, s, 4) }
+        if (g < q) xOffDiag16(sA, sX, q, g, lane);
+        waveBarrier<true>(&sFl[3], gen, 3, lane);
+        if (g == 0) { STR(1, s, 5) }
+        if (g == 0) yBlock16(sX, sy, q, lane);
+        xStoreRows16<kCaller>(sX, Li, q, g, lane);
+        if (g == 0) { STR(1, s, 6) }
+      }
     }
   }
   ldsBarrier();
   CLK(5)
+#ifdef OKG_SWEEP_TRACE
+  if (blockIdx.x == 0 && t < 128) g_sweepT[t >> 6][(t >> 3) & 7][t & 7] = sTr[t >> 6][(t >> 3) & 7][t & 7];
+#endif
   if (sFl[2]) return false;
-  CLK(6)
-  {  // X21 = -X22 (L21 X11) of the diagonal 16x16 block q = wave; lane = (row m, column j)
-    const int q = wave, m = lane >> 3, j = lane & 7;
-    const int b = 16 * q;
-    double tk[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) tk[k] = 0.0;
-    double t = 0.0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) t += sA[(b + 8 + m) * kLd + b + k] * sX[(b + k) * kLd + b + j];
-    sX[(b + 8 + m) * kLd + b + j] = t;  // T = L21 X11 staged in place (this wavefront only)
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int k = 0; k < 8; ++k) tk[k] = sX[(b + 8 + k) * kLd + b + j];
-    double v = 0.0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v += sX[(b + 8 + m) * kLd + b + 8 + k] * tk[k];
-    __builtin_amdgcn_wave_barrier();
-    sX[(b + 8 + m) * kLd + b + j] = -v;
-  }
-  ldsBarrier();
-  CLK(7)
-  for (int d = 1; d < 4; ++d) {  // sub-diagonal d: X_ij, i = j + d, wavefront j
-    const int j = wave, i = wave + d;
-    if (i < 4) {
-      dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
-      for (int m = j; m < i; ++m)  // T = sum L_im X_mj   (B[k][n] = X[16m + k][16j + n])
-        mfma16<1>(sA + 16 * i * kLd + 16 * m, kLd, sX + 16 * m * kLd + 16 * j, kLd, 1, 1.0, acc, lane);
-      double* Xij = sX + 16 * i * kLd + 16 * j;
-      storeC16(Xij, kLd, acc, lane);  // T staged in the (i, j) block (this wavefront only)
-      dbl4 x = dbl4{0.0, 0.0, 0.0, 0.0};
-      mfma16<1>(sX + 16 * i * kLd + 16 * i, kLd, Xij, kLd, 1, -1.0, x, lane);
-      storeC16(Xij, kLd, x, lane);
-    }
-    ldsBarrier();
-  }
-  CLK(8)
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int e = t + 256 * u, r = e >> 5, c = 2 * (e & 31);
-    // the persistent schedule's backward substitution masks the upper triangle of X (bsDiag), so
-    // it stores the lower one only; the tile-parallel update kernels stage X whole for the MFMAs
-    if (kCaller != 0 || c <= r)
-      *reinterpret_cast<double2*>(Li + r * kTile + c) =
-          double2{(c <= r) ? sX[r * kLd + c] : 0.0, (c + 1 <= r) ? sX[r * kLd + c + 1] : 0.0};
-  }
+  POTRF_STOP(1)
   // LDS-only barriers from here: the X / y stores stay in flight (no reader in this
   // workgroup before a later full barrier or the end of the launch)
-  ldsBarrier();
-  CLK(9)
-  {  // y_k = X rhs_k: row t & 63, quarter t >> 6 of the columns, partials through LDS
-    const int row = t & 63, qq = t >> 6;
-    double y = 0.0;
-#pragma unroll
-    for (int j = 16 * qq; j < 16 * qq + 16; ++j) y += (j <= row) ? sX[row * kLd + j] * sy[j] : 0.0;
-    sA[qq * kTile + row] = y;  // sA is free once L_kk has been stored
-  }
-  ldsBarrier();
   if (t < kTile) {
-    const double y = (sA[t] + sA[kTile + t]) + (sA[2 * kTile + t] + sA[3 * kTile + t]);
+    const double y = sy[kTile + t];
     sy[t] = y;
     if (kCaller != 0) workk[t] = y;
   }
