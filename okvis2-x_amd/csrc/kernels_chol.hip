@@ -745,7 +745,10 @@ __device__ void backSubstitute(const DevProblem& P, int w, const double* S, int6
   for (int e = t; e < fdim; e += blockDim.x) P.yF[(size_t)P.win_foff[w] + e] = sx[e];
 }
 
-__global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restrict__ Pp) {
+#ifndef OKG_CHOL_OCC
+#define OKG_CHOL_OCC 2
+#endif
+__global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int w = blockIdx.x;
   if (!cholSelect(P, w)) return;
@@ -781,10 +784,15 @@ __global__ __launch_bounds__(256, 2) void k_cholesky(const DevProblem* __restric
     CLK(0)
     // ---- panel: L_ik = A_ik X^T, rhs_i -= L_ik y_k = A_ik X^T y_k
     panelRhsVector(sX, sy, sy + kTile, sA, t);
+#ifndef OKG_CHOL_SKIP_PANEL  // (development-only phase cut: timing builds)
     for (int i = k + 1; i < T; ++i)
       if (nz[i * T + k]) panelTile(S + i * kTile * ld + k * kTile, ld, sxDyn + i * kTile, sA, sX, sy + kTile, t);
+#endif
     __syncthreads();  // full barrier: the band update reads the L_ik just stored
     CLK(1)
+#ifdef OKG_CHOL_SKIP_UPDATE
+    continue;
+#endif
     // ---- trailing band update: A_ij -= L_ik L_jk^T, k < j <= i, both tiles non-zero. The A_ij
     // read of the read-modify-write is issued before the MFMAs, so its latency overlaps them.
     // Block rows from the bottom: the L_jk staged in sX for a lower row is reused as the row

@@ -199,19 +199,26 @@ static_assert(kImuLds * 8 * 4 <= 20480, "LDS for eight workgroups (two waves per
 // F_delta (ImuError.cpp:395-410) of one step in LDS: non-identity 3x3 blocks
 constexpr int kF03 = 0, kF09 = 9, kF012 = 18, kF39 = 27, kF63 = 36, kF69 = 45, kF612 = 54, kFdt = 63;
 
+// Row r of -[w]x times u, the zero entry of the row skipped: the two remaining products in the
+// column order of the full row (F03 and F63 are such blocks; their slots hold w only, 3 LDS reads
+// per applyF instead of 9).
+__device__ __forceinline__ double negSkewRow(const double* w, int r, double u0, double u1, double u2) {
+  return r == 0 ? w[2] * u1 + (-w[1]) * u2 : (r == 1 ? (-w[2]) * u0 + w[0] * u2 : w[1] * u0 + (-w[0]) * u1);
+}
 // out = F v   (block rows: 0 dp, 1 dalpha, 2 dv, 3 bg, 4 ba); F read from LDS (group broadcast)
 __device__ __forceinline__ void applyF(const double* F, const double* v, double* out) {
   const double dt = F[kFdt];
+  const double w03[3] = {F[kF03], F[kF03 + 1], F[kF03 + 2]}, w63[3] = {F[kF63], F[kF63 + 1], F[kF63 + 2]};
 #pragma unroll
   for (int r = 0; r < 3; ++r) {
     double a = v[r];
-    a += F[kF03 + r * 3 + 0] * v[3] + F[kF03 + r * 3 + 1] * v[4] + F[kF03 + r * 3 + 2] * v[5];
+    a += negSkewRow(w03, r, v[3], v[4], v[5]);
     a += dt * v[6 + r];
     a += F[kF09 + r * 3 + 0] * v[9] + F[kF09 + r * 3 + 1] * v[10] + F[kF09 + r * 3 + 2] * v[11];
     a += F[kF012 + r * 3 + 0] * v[12] + F[kF012 + r * 3 + 1] * v[13] + F[kF012 + r * 3 + 2] * v[14];
     out[r] = a;
     out[3 + r] = v[3 + r] + F[kF39 + r * 3 + 0] * v[9] + F[kF39 + r * 3 + 1] * v[10] + F[kF39 + r * 3 + 2] * v[11];
-    double c = F[kF63 + r * 3 + 0] * v[3] + F[kF63 + r * 3 + 1] * v[4] + F[kF63 + r * 3 + 2] * v[5];
+    double c = negSkewRow(w63, r, v[3], v[4], v[5]);
     c += v[6 + r];
     c += F[kF69 + r * 3 + 0] * v[9] + F[kF69 + r * 3 + 1] * v[10] + F[kF69 + r * 3 + 2] * v[11];
     c += F[kF612 + r * 3 + 0] * v[12] + F[kF612 + r * 3 + 1] * v[13] + F[kF612 + r * 3 + 2] * v[14];
@@ -484,7 +491,6 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
     double* const xx = sG + kLXx;
     double* const Fs = sG + kLF;
     double* const nz = sG + kLNz;
-    double* const v03 = sG + kLRec;  // (phase S -> F03; the records are consumed by then)
     double* const M = sG + kLM;      // (phase P; aliases the records, q1, cr and cj)
     for (int c0 = 0; c0 < Nmax; c0 += kImuK) {
       const int nk = min(kImuK, Nmax - c0);
@@ -639,14 +645,11 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
           mm3(tmp, crk, X);
           for (int i = 0; i < 9; ++i) X[i] += t1m[i];
           double* F = Fs + l * kFStride;
-          double v[3], mx[9];
-          for (int i = 0; i < 3; ++i) v[i] = 0.5 * dt * CCa[i];
-          crossMx(v, mx);
+          for (int i = 0; i < 3; ++i) F[kF63 + i] = 0.5 * dt * CCa[i];  // F63 = -[0.5 dt (C + C_1) a]x
           for (int i = 0; i < 9; ++i) {
             cc[9 * l + i] = CC1[i];
             xx[9 * l + i] = X[i];
             F[kF39 + i] = -dt * C1[i];
-            F[kF63 + i] = -mx[i];
             F[kF69 + i] = 0.5 * dt * X[i];
             F[kF612 + i] = -0.5 * dt * CC1[i];
           }
@@ -674,7 +677,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
           } else {
             const double c = ca[3 * k + l - 9];
             const double v = aCi * dt + hdt2 * c;
-            v03[3 * k + l - 9] = v;
+            F[kF03 + l - 9] = v;  // F03 = -[acc_integral dt + dt^2/4 (C + C_1) a]x, held as its vector
             aCdi += v;
             aCi += 0.5 * dt * c;
           }
@@ -682,15 +685,6 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
       }
       __syncthreads();
       ICLK(9)
-      if (l < nk) {  // F03 = -[acc_integral dt + dt^2/4 (C + C_1) a]x
-        double* F = Fs + l * kFStride;
-        if (F[kFdt] > 0.0) {
-          double mx[9];
-          crossMx(v03 + 3 * l, mx);
-          for (int i = 0; i < 9; ++i) F[kF03 + i] = -mx[i];
-        }
-      }
-      __syncthreads();
       // ---- P <- F P F^T + Q : M = F P (column l), exchange rows, P' = F M^T (column l)
       for (int k = 0; k < nk; ++k) {
         const double* F = Fs + k * kFStride;
