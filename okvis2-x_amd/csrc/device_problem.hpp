@@ -273,7 +273,7 @@ struct DevProblem {
   const int32_t* chol_upd_begin;
   const int32_t* h_panel_begin;
   const int32_t* h_upd_begin;
-  int32_t chol_schedule;             // 1 persistent per window, 2 tile-parallel, 3 wave-specialised (host-resolved)
+  int32_t chol_schedule;             // 1 persistent per window, 2 tile-parallel, 3 wave-specialised, 4 persistent wide (host-resolved)
   int32_t chol_pairs;                // schedule 3: two windows per workgroup
   const uint8_t* tile_nz;            // per window T x T (row-major) structural non-zero flags of L
   const int64_t* win_tnzoff;         // [n_win] offset of the window's flags in tile_nz

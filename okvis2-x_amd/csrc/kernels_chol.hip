@@ -364,6 +364,18 @@ __device__ __forceinline__ void trailing8(double* sA, int c0, int wg, int nw, in
   trailingFrom(sA, c0, c0 + 8, wg, nw, lane);
 }
 
+// 64x64 global tile (row stride ld) -> LDS [64][kLd] by DMA (global_load_lds, 4 bytes per lane:
+// one instruction moves half a row, 64 dwords, to a contiguous LDS range), half rows dealt to the
+// ng wavefronts (this one is g). Completion is counted by vmcnt.
+__device__ __forceinline__ void dmaTile(const double* src, int64_t ld, double* dst, int g, int ng, int lane) {
+  for (int h = g; h < 2 * kTile; h += ng) {
+    const int row = h >> 1, half = h & 1;
+    const uint32_t* gs = reinterpret_cast<const uint32_t*>(src + (int64_t)row * ld + 32 * half) + lane;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gs,
+                                     (__attribute__((address_space(3))) void*)(dst + row * kLd + 32 * half), 4, 0, 0);
+  }
+}
+
 // X = L^-1 of the in-LDS diagonal tile by 16-row block rows (sX holds X, sA the final L):
 // X21 = -X22 (L21 X11) of the diagonal 16x16 block q, whose 8x8 diagonal inverses are in sX
 // (one wavefront; lane = (row m, column j)).
@@ -447,7 +459,8 @@ __device__ __forceinline__ void xStoreRows16(const double* sX, double* Li, int q
 // budget that halves the persistent kernel's occupancy)
 template <int kCaller>
 __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX, double* sy,
-                                      double* sRl, int* sFl, int t, bool haveTile) {
+                                      double* sRl, int* sFl, int t, bool haveTile, const double* pfA0 = nullptr,
+                                      const double* pfA1 = nullptr, double* sP = nullptr) {
   const int wave = t >> 6, lane = t & 63;
   CLK_INIT
 #ifdef OKG_SWEEP_TRACE
@@ -517,6 +530,10 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
   } else {
     const int g = wave - 1;
     int gen = 0;
+    // wide persistent schedule: the step's panel tiles A_ik go to LDS by DMA (no registers) while
+    // wavefront 0 runs the sweep
+    if (kCaller == 3 && pfA0) dmaTile(pfA0, ld, sP, g, 3, lane);
+    if (kCaller == 3 && pfA1) dmaTile(pfA1, ld, sP + kTile * kLd, g, 3, lane);
 #pragma unroll 1
     for (int s = 0; s < 8; ++s) {
       if (!waitFlag<true>(&sFl[0], s + 1, &sFl[2])) break;
@@ -545,6 +562,7 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
         if (g == 0) { STR(1, s, 6) }
       }
     }
+    if (kCaller == 3 && pfA0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the panel tiles have landed in LDS
   }
   ldsBarrier();
   CLK(5)
@@ -580,7 +598,7 @@ __device__ __forceinline__ void accSubToLds(double* s, const dbl4 c[2][2], const
 
 // z = X^T y_k (X = L_kk^-1 lower in sX, y_k in sy), so that the forward substitution update of
 // every panel is rhs_i -= L_ik y_k = A_ik z. Partials of four row quarters via sP (4 x 64).
-__device__ void panelRhsVector(const double* sX, const double* sy, double* sz, double* sP, int t) {
+__device__ __forceinline__ void panelRhsVector(const double* sX, const double* sy, double* sz, double* sP, int t) {
   const int c = t & 63, q = t >> 6;
   double a = 0.0;
 #pragma unroll
@@ -593,7 +611,7 @@ __device__ void panelRhsVector(const double* sX, const double* sy, double* sz, d
 
 // L_ik = A_ik X^T (X = L_kk^-1 in sX) stored over A_ik, and rhs_i -= A_ik z (z = X^T y_k in sz),
 // the row products formed from the A_ik tile in LDS while the MFMAs run.
-__device__ void panelTile(double* Aik, int64_t ld, double* worki, double* sA, const double* sX, const double* sz,
+__device__ __forceinline__ void panelTile(double* Aik, int64_t ld, double* worki, double* sA, const double* sX, const double* sz,
                           int t) {
   loadTile(Aik, ld, 0, 0, sA, t);
   ldsBarrier();  // LDS-only: the previous panel's L / rhs stores stay in flight
@@ -719,7 +737,7 @@ __device__ __forceinline__ void bsList(const uint8_t* nz, int T, int I, int* lst
 }
 // Persistent schedule (256 threads, 4 virtual threads each): y already in sx (LDS), then
 // the steps with operands loaded in-step. sA: >= 32 x 64 doubles.
-__device__ void backSubstitute(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* Linv,
+__device__ __forceinline__ void backSubstitute(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* Linv,
                                const uint8_t* nz, double* sx, double* sA, double* sy, int t) {
   // sx already holds y (the persistent kernel keeps the whole forward substitution in LDS)
   __syncthreads();
@@ -892,6 +910,101 @@ __device__ __forceinline__ void accToLds(double* s, const dbl4 acc[2][2], int t)
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) s[(r0 + 16 * a + (lane >> 4) + 4 * reg) * kLd + c0 + 16 * b + (lane & 15)] = acc[a][b][reg];
+}
+
+// ---- wide persistent schedule (schedule 4, up to one window per CU): k_cholesky with the step's
+// panel tiles in LDS. One workgroup per CU leaves LDS for two more tiles: the panel tiles A_ik of
+// step k are moved to LDS by DMA on wavefronts 1-3 during the diagonal factor, each panel's L_ik
+// replaces its A_ik there (and is stored for the backward substitution), and the band updates take
+// both operands from LDS: no global operand load on the step's chain except a third panel tile
+// (staged in sA) and the C tiles of the read-modify-writes (issued before the MFMAs as in
+// k_cholesky). The same operations in the same
+// order as k_cholesky: the same bits (test_cholesky_schedules_agree). Requires at most
+// kCholWidePanels non-zero tiles below every diagonal tile (host-checked, cholesky_wide_fits).
+__global__ __launch_bounds__(256, 1) void k_cholesky_wide(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
+  const int w = blockIdx.x;
+  if (!cholSelect(P, w)) return;
+  const int64_t ld = P.win_fpad[w];
+  const int T = (int)(ld / kTile);
+  double* S = P.S + P.win_soff[w];
+  double* Linv = P.Linv + P.win_linvoff[w];
+  const uint8_t* nz = P.tile_nz + P.win_tnzoff[w];
+  __shared__ double sA[kTile * kLd];
+  __shared__ double sX[kTile * kLd];
+  __shared__ double sP[2 * kTile * kLd];
+  __shared__ double sy[2 * kTile];
+  __shared__ double sRl[kTile];
+  __shared__ int sFl[4];
+  const int t = threadIdx.x;
+  const int fdim = P.win_fdim[w];
+  extern __shared__ double sxDyn[];
+  for (int e = t; e < ld; e += 256) sxDyn[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
+  __syncthreads();
+  bool haveDiag = false;
+  for (int k = 0; k < T; ++k) {
+    int pr[kCholWidePanels], np = 0;  // the step's panel rows, ascending
+    for (int i = k + 1; i < T && np < kCholWidePanels; ++i)
+      if (nz[i * T + k]) pr[np++] = i;
+    // panel b's tile: b < 2 in sP (moved there by DMA during the factor), b == 2 staged in sA
+    // (free after the factor; its L is last used by the updates of its own, the bottom, row, so
+    // the next diagonal tile can take sA afterwards)
+    auto pbuf = [&](int b) { return b < 2 ? sP + b * kTile * kLd : sA; };
+    if (t < kTile) sy[t] = sxDyn[k * kTile + t];
+    __syncthreads();  // full: the factor and the DMA read the tiles the last band update stored
+    if (!potrfTile<3>(S + k * kTile * ld + k * kTile, ld, Linv + (int64_t)k * kTile * kTile, nullptr, sA, sX, sy, sRl,
+                      sFl, t, haveDiag, np > 0 ? S + pr[0] * kTile * ld + k * kTile : nullptr,
+                      np > 1 ? S + pr[1] * kTile * ld + k * kTile : nullptr, sP)) {
+      if (t == 0) P.st[w].gn_failed = 1;
+      return;
+    }
+    if (t < kTile) sxDyn[k * kTile + t] = sy[t];
+    // ---- panels from LDS: L_ik = A_ik X^T replaces A_ik in sP (and goes to S), rhs_i -= A_ik z
+    panelRhsVector(sX, sy, sy + kTile, sA, t);
+    for (int b = 0; b < np; ++b) {
+      double* sPb = pbuf(b);
+      if (b == 2) {
+        loadTile(S + pr[b] * kTile * ld + k * kTile, ld, 0, 0, sA, t);
+        ldsBarrier();
+      }
+      dbl4 acc[2][2];
+      mfmaTileNT(sPb, sX, acc, t);
+      {
+        const int row = t >> 2, q = t & 3;
+        double a = 0.0;
+#pragma unroll
+        for (int c = 16 * q; c < 16 * q + 16; ++c) a += sPb[row * kLd + c] * sy[kTile + c];
+        a += __shfl_xor(a, 1, 64);
+        a += __shfl_xor(a, 2, 64);
+        if (q == 0) sxDyn[pr[b] * kTile + row] -= a;
+      }
+      ldsBarrier();  // every wavefront has read A_ik
+      accToLds(sPb, acc, t);
+      storeTile<false>(S + pr[b] * kTile * ld + k * kTile, ld, 0, 0, acc, t);
+    }
+    ldsBarrier();  // the L tiles in sP are complete
+    // ---- band update A_ij -= L_ik L_jk^T from the L tiles in LDS, block rows from the bottom
+    haveDiag = false;
+    for (int bi = np - 1; bi >= 0; --bi) {
+      const int i = pr[bi];
+      for (int bj = 0; bj <= bi; ++bj) {
+        const int j = pr[bj];
+        double* Cij = S + i * kTile * ld + j * kTile;
+        dbl4 c[2][2], acc[2][2];
+        loadC(Cij, ld, c, t);
+        mfmaTileNT(pbuf(bi), pbuf(bj), acc, t);
+        if (i == k + 1) {  // (then j == i) the next diagonal tile: c - acc straight into sA
+          ldsBarrier();    // every wavefront has read its operands (sA may hold panel 2's L)
+          accSubToLds(sA, c, acc, t);
+          haveDiag = true;
+        } else {
+          storeTileSub(Cij, ld, c, acc, t);
+        }
+      }
+    }
+  }
+  __syncthreads();  // the L stores of the last steps are read back by the backward substitution
+  backSubstitute(P, w, S, ld, T, Linv, nz, sxDyn, sA, sy, t);
 }
 
 __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restrict__ Pp, int k) {
@@ -1507,6 +1620,12 @@ bool cholesky_ws_fits(int max_fpad, size_t lds_per_block) {
   return attr.sharedSizeBytes + 2 * sizeof(double) * (size_t)max_fpad <= lds_per_block;
 }
 
+bool cholesky_wide_fits(int max_fpad, size_t lds_per_block) {
+  hipFuncAttributes attr;
+  if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky_wide)) != hipSuccess) return false;
+  return attr.sharedSizeBytes + sizeof(double) * (size_t)max_fpad <= lds_per_block;
+}
+
 bool cholesky_persistent_fits(int max_fpad, size_t lds_per_block) {
   hipFuncAttributes attr;
   if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky)) != hipSuccess) return false;
@@ -1517,6 +1636,10 @@ void launch_cholesky(const DevProblem& P, hipStream_t s) {
   if (P.n_win == 0) return;
   if (P.chol_schedule == 1) {
     hipLaunchKernelGGL(k_cholesky, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
+    return;
+  }
+  if (P.chol_schedule == 4) {
+    hipLaunchKernelGGL(k_cholesky_wide, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
     return;
   }
   if (P.chol_schedule == 3) {

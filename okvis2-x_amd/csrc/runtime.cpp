@@ -151,6 +151,7 @@ struct HostBatch {
   std::vector<int> tileT;
   int f_total = 0;
   int max_fpad = 0;
+  int max_panels = 0;  // most non-zero tiles below a diagonal tile (panels of one Cholesky step)
 };
 
 template <class T>
@@ -991,6 +992,12 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
   for (int w = 0; w < B.n_win; ++w) {
     B.win_tnzoff.push_back((int64_t)B.tile_nz.size());
     B.tile_nz.insert(B.tile_nz.end(), B.tileNz[w].begin(), B.tileNz[w].end());
+    const int T = B.tileT[w];
+    for (int k = 0; k < T; ++k) {
+      int np = 0;
+      for (int i = k + 1; i < T; ++i) np += B.tileNz[w][(size_t)i * T + k] ? 1 : 0;
+      B.max_panels = std::max(B.max_panels, np);
+    }
   }
   for (int w = 0; w < B.n_win; ++w) {
     const int T = B.tileT[w];
@@ -1081,6 +1088,8 @@ struct okvisgpu_ctx {
   size_t ldsPerBlock = 65536;
   bool wsFits() const { return cholesky_ws_fits(P.max_fpad, ldsPerBlock); }
   bool persistentFits() const { return cholesky_persistent_fits(P.max_fpad, ldsPerBlock); }
+  static constexpr bool kAutoWide = false;  // schedule 4 picked automatically (pending its A/B)
+  bool wideFits() const { return B.max_panels <= kCholWidePanels && cholesky_wide_fits(P.max_fpad, ldsPerBlock); }
   bool haveProblem = false;
   // split-solve state
   bool inSolve = false;
@@ -1550,8 +1559,11 @@ struct okvisgpu_ctx {
     // half a window per CU the tile-parallel launches spread each window over many CUs; from there
     // the persistent kernel. The wave-specialised kernel no longer wins anywhere since the
     // persistent kernel's sub-panel look-ahead; it stays selectable (cholesky_schedule = 3).
-    int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 3 ? o.cholesky_schedule : 0;
-    if (sched == 0) sched = 2 * P.n_win >= cuCount ? 1 : 2;
+    // Up to one window per CU the persistent kernel runs as the wide variant (schedule 4: one
+    // workgroup per CU anyway, so its extra LDS costs no occupancy; round 3, 256 S50 windows).
+    int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 4 ? o.cholesky_schedule : 0;
+    if (sched == 0) sched = 2 * P.n_win >= cuCount ? (kAutoWide && P.n_win <= cuCount && wideFits() ? 4 : 1) : 2;
+    if (sched == 4 && !wideFits()) sched = 1;
     if (sched == 3 && !wsFits()) sched = 2;
     // the persistent kernel keeps the window's rhs / y in dynamic LDS next to its static tiles:
     // a reduced dimension beyond what fits falls back to the tile-parallel launches
