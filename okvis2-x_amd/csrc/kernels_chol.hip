@@ -921,7 +921,10 @@ __device__ __forceinline__ void accToLds(double* s, const dbl4 acc[2][2], int t)
 // k_cholesky). The same operations in the same
 // order as k_cholesky: the same bits (test_cholesky_schedules_agree). Requires at most
 // kCholWidePanels non-zero tiles below every diagonal tile (host-checked, cholesky_wide_fits).
-__global__ __launch_bounds__(256, 1) void k_cholesky_wide(const DevProblem* __restrict__ Pp) {
+#ifndef OKG_WIDE_OCC
+#define OKG_WIDE_OCC 1
+#endif
+__global__ __launch_bounds__(256, OKG_WIDE_OCC) void k_cholesky_wide(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int w = blockIdx.x;
   if (!cholSelect(P, w)) return;
