@@ -791,4 +791,57 @@ class Problem {
   okvisgpu_problem view_{};
 };
 
+// ---- the ::ceres::Solve(options_, problem_.get(), &summary_) call shape (ViGraph.cpp:1884), so the
+// call site keeps its ceres::Solver::Options / Summary objects. Templates over the caller's types
+// (no Ceres type is named here): the options fields okvis sets or relies on (ViGraph.cpp:248-249,
+// 1854-1861; Ceres defaults otherwise) are read by their ceres::Solver::Options names. The linear
+// solver is passed as a flag (the caller compares `options_.linear_solver_type == ::ceres::
+// DENSE_SCHUR`), the trust region is DOGLEG (ViGraph.cpp:249), and the CeresIterationCallback
+// time limit / iteration minimum (CeresIterationCallback.cpp:30-38) come as arguments. The summary
+// fields are written under their ceres::Solver::Summary names; termination_type is cast to the
+// member's enum (okvisgpu_termination follows ceres::TerminationType: CONVERGENCE, NO_CONVERGENCE,
+// FAILURE, USER_SUCCESS).
+template <class SolverOptions>
+okvisgpu_options toOptions(const SolverOptions& o, bool denseSchur = true, double timeLimitS = -1.0,
+                           int minIterations = 0) {
+  okvisgpu_options r;
+  okvisgpu_default_options(&r);
+  r.max_num_iterations = o.max_num_iterations;
+  r.num_threads = o.num_threads;
+  r.linear_solver = denseSchur ? OKVISGPU_DENSE_SCHUR : OKVISGPU_SPARSE_NORMAL_CHOLESKY;
+  r.trust_region_strategy = OKVISGPU_DOGLEG;
+  r.jacobi_scaling = o.jacobi_scaling ? 1 : 0;
+  r.function_tolerance = o.function_tolerance;
+  r.gradient_tolerance = o.gradient_tolerance;
+  r.parameter_tolerance = o.parameter_tolerance;
+  r.initial_trust_region_radius = o.initial_trust_region_radius;
+  r.max_trust_region_radius = o.max_trust_region_radius;
+  r.min_trust_region_radius = o.min_trust_region_radius;
+  r.min_relative_decrease = o.min_relative_decrease;
+  r.min_lm_diagonal = o.min_lm_diagonal;
+  r.max_lm_diagonal = o.max_lm_diagonal;
+  r.max_num_consecutive_invalid_steps = o.max_num_consecutive_invalid_steps;
+  r.verbose = o.minimizer_progress_to_stdout ? 1 : 0;
+  r.time_limit_s = timeLimitS;
+  r.min_iterations = minIterations;
+  return r;
+}
+template <class SolverSummary>
+void toSummary(const okvisgpu_summary& s, SolverSummary* out) {
+  out->initial_cost = s.initial_cost;
+  out->final_cost = s.final_cost;
+  out->num_successful_steps = s.num_successful_steps;
+  out->num_unsuccessful_steps = s.num_unsuccessful_steps;
+  out->termination_type = static_cast<decltype(out->termination_type)>(s.termination_type);
+  out->total_time_in_seconds = s.total_time_s;
+}
+template <class SolverOptions, class SolverSummary>
+int Solve(const SolverOptions& options, Problem* problem, SolverSummary* summary, bool denseSchur = true,
+          double timeLimitS = -1.0, int minIterations = 0) {
+  okvisgpu_summary s;
+  const int rc = problem->Solve(toOptions(options, denseSchur, timeLimitS, minIterations), &s);
+  if (rc == OKVISGPU_OK && summary) toSummary(s, summary);
+  return rc;
+}
+
 }  // namespace okvisgpu

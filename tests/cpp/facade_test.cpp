@@ -70,6 +70,22 @@ double rotErr(Quat a, Quat b) {  // 2 |vec(a b^-1)|
   return 2 * std::sqrt(d.x * d.x + d.y * d.y + d.z * d.z);
 }
 
+// Stand-ins with the member names (and defaults) of ceres::Solver::Options / Summary that okvis
+// uses (Ceres is not in this image): the ::ceres::Solve-shaped facade call is a template over them.
+enum class CeresLikeTermination { CONVERGENCE, NO_CONVERGENCE, FAILURE, USER_SUCCESS, USER_FAILURE };
+struct CeresLikeOptions {
+  int max_num_iterations = 50, num_threads = 1, max_num_consecutive_invalid_steps = 5;
+  bool jacobi_scaling = true, minimizer_progress_to_stdout = false;
+  double function_tolerance = 1e-6, gradient_tolerance = 1e-10, parameter_tolerance = 1e-8;
+  double initial_trust_region_radius = 1e4, max_trust_region_radius = 1e16, min_trust_region_radius = 1e-32;
+  double min_relative_decrease = 1e-3, min_lm_diagonal = 1e-6, max_lm_diagonal = 1e32;
+};
+struct CeresLikeSummary {
+  double initial_cost = -1, final_cost = -1, total_time_in_seconds = -1;
+  int num_successful_steps = -1, num_unsuccessful_steps = -1;
+  CeresLikeTermination termination_type = CeresLikeTermination::FAILURE;
+};
+
 okvisgpu_options zeroTol(int iters) {
   okvisgpu_options o;
   okvisgpu_default_options(&o);
@@ -374,12 +390,44 @@ int cpuTests() {
     try { (void)Q.view(); } catch (const okvisgpu::Unsupported&) { threw = true; }
     CHECK(threw);
   }
+  // ::ceres::Solve-shaped call: the ceres::Solver::Options / Summary member names okvis uses
+  {
+    CeresLikeOptions co;
+    co.max_num_iterations = 7;
+    co.num_threads = 3;
+    co.function_tolerance = 1e-3;
+    co.minimizer_progress_to_stdout = true;
+    const okvisgpu_options o = okvisgpu::toOptions(co, false, 0.05, 2);
+    okvisgpu_options d;
+    okvisgpu_default_options(&d);
+    CHECK(o.max_num_iterations == 7 && o.num_threads == 3 && o.function_tolerance == 1e-3 && o.verbose == 1);
+    CHECK(o.linear_solver == OKVISGPU_SPARSE_NORMAL_CHOLESKY && o.trust_region_strategy == OKVISGPU_DOGLEG);
+    CHECK(o.time_limit_s == 0.05 && o.min_iterations == 2);
+    // every other field keeps the Ceres default the mock carries (= the C ABI's defaults)
+    CHECK(o.gradient_tolerance == d.gradient_tolerance && o.parameter_tolerance == d.parameter_tolerance);
+    CHECK(o.initial_trust_region_radius == d.initial_trust_region_radius &&
+          o.max_trust_region_radius == d.max_trust_region_radius &&
+          o.min_trust_region_radius == d.min_trust_region_radius);
+    CHECK(o.min_relative_decrease == d.min_relative_decrease && o.min_lm_diagonal == d.min_lm_diagonal &&
+          o.max_lm_diagonal == d.max_lm_diagonal && o.jacobi_scaling == d.jacobi_scaling &&
+          o.max_num_consecutive_invalid_steps == d.max_num_consecutive_invalid_steps);
+    okvisgpu_summary s{};
+    s.initial_cost = 3.0; s.final_cost = 1.0; s.num_successful_steps = 4; s.num_unsuccessful_steps = 2;
+    s.termination_type = OKVISGPU_USER_SUCCESS; s.total_time_s = 0.5;
+    CeresLikeSummary cs;
+    okvisgpu::toSummary(s, &cs);
+    CHECK(cs.initial_cost == 3.0 && cs.final_cost == 1.0 && cs.num_successful_steps == 4 &&
+          cs.num_unsuccessful_steps == 2 && cs.termination_type == CeresLikeTermination::USER_SUCCESS &&
+          cs.total_time_in_seconds == 0.5);
+  }
   // no device in this container: Solve reports the C ABI's status instead of crashing
   int32_t ndev = 0;
   okvisgpu_device_count(&ndev);
   if (ndev == 0) {
     okvisgpu_summary s;
     CHECK(P.Solve(zeroTol(2), &s) == OKVISGPU_ERR_DEVICE);
+    CeresLikeSummary cs;
+    CHECK(okvisgpu::Solve(CeresLikeOptions{}, &P, &cs) == OKVISGPU_ERR_DEVICE);
   }
   std::printf("facade_test cpu %s\n", g_fail ? "FAILED" : "ok");
   return g_fail ? 1 : 0;
