@@ -955,9 +955,14 @@ __global__ __launch_bounds__(256, OKG_WIDE_OCC) void k_cholesky_wide(const DevPr
     auto pbuf = [&](int b) { return b < 2 ? sP + b * kTile * kLd : sA; };
     if (t < kTile) sy[t] = sxDyn[k * kTile + t];
     __syncthreads();  // full: the factor and the DMA read the tiles the last band update stored
+#ifdef OKG_WIDE_NODMA  // (development A/B: panel tiles loaded at panel time instead of during the factor)
+    constexpr bool kDma = false;
+#else
+    constexpr bool kDma = true;
+#endif
     if (!potrfTile<3>(S + k * kTile * ld + k * kTile, ld, Linv + (int64_t)k * kTile * kTile, nullptr, sA, sX, sy, sRl,
-                      sFl, t, haveDiag, np > 0 ? S + pr[0] * kTile * ld + k * kTile : nullptr,
-                      np > 1 ? S + pr[1] * kTile * ld + k * kTile : nullptr, sP)) {
+                      sFl, t, haveDiag, kDma && np > 0 ? S + pr[0] * kTile * ld + k * kTile : nullptr,
+                      kDma && np > 1 ? S + pr[1] * kTile * ld + k * kTile : nullptr, sP)) {
       if (t == 0) P.st[w].gn_failed = 1;
       return;
     }
@@ -966,8 +971,8 @@ __global__ __launch_bounds__(256, OKG_WIDE_OCC) void k_cholesky_wide(const DevPr
     panelRhsVector(sX, sy, sy + kTile, sA, t);
     for (int b = 0; b < np; ++b) {
       double* sPb = pbuf(b);
-      if (b == 2) {
-        loadTile(S + pr[b] * kTile * ld + k * kTile, ld, 0, 0, sA, t);
+      if (b == 2 || !kDma) {
+        loadTile(S + pr[b] * kTile * ld + k * kTile, ld, 0, 0, sPb, t);
         ldsBarrier();
       }
       dbl4 acc[2][2];
