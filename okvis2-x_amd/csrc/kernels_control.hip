@@ -28,17 +28,31 @@ constexpr int kRB = OKG_RB;  // per-window workgroup size (k_reduce, k_gradnorm,
 static_assert((kRB & (kRB - 1)) == 0 && kRB >= 64 && kRB <= 1024,
               "OKG_RB must be a power of two in [64, 1024] (blockSum / blockMax tree reductions)");
 
-__device__ __forceinline__ double blockSum(double v, double* sh) {
+// Fixed-order tree reductions over the workgroup. The barriers order LDS only (ldsBarrier): a
+// __syncthreads() also waited for every global store still in flight (k_dogleg's Plus pass leaves
+// thousands), and N values reduced together share one tree's barriers: per value the same
+// additions in the same order as a separate tree, so the same bits.
+template <int N>
+__device__ __forceinline__ void blockSumN(double (&v)[N], double* sh) {  // sh: N * kRB doubles
   const int t = threadIdx.x;
-  sh[t] = v;
-  __syncthreads();
+#pragma unroll
+  for (int n = 0; n < N; ++n) sh[n * kRB + t] = v[n];
+  ldsBarrier();
   for (int s = kRB / 2; s > 0; s >>= 1) {
-    if (t < s) sh[t] += sh[t + s];
-    __syncthreads();
+    if (t < s) {
+#pragma unroll
+      for (int n = 0; n < N; ++n) sh[n * kRB + t] += sh[n * kRB + t + s];
+    }
+    ldsBarrier();
   }
-  const double r = sh[0];
-  __syncthreads();
-  return r;
+#pragma unroll
+  for (int n = 0; n < N; ++n) v[n] = sh[n * kRB];
+  ldsBarrier();
+}
+__device__ __forceinline__ double blockSum(double v, double* sh) {
+  double a[1] = {v};
+  blockSumN<1>(a, sh);
+  return a[0];
 }
 // Strided per-thread loop over i = b + t, b + t + kRB, ... < e with the loads of U consecutive
 // iterations issued before any of them is consumed. A window's reductions run in one workgroup, so a
@@ -60,13 +74,13 @@ __device__ __forceinline__ void stridedBatched(int b, int e, Load load, Use use)
 __device__ __forceinline__ double blockMax(double v, double* sh) {
   const int t = threadIdx.x;
   sh[t] = v;
-  __syncthreads();
+  ldsBarrier();
   for (int s = kRB / 2; s > 0; s >>= 1) {
     if (t < s) sh[t] = fmax(sh[t], sh[t + s]);
-    __syncthreads();
+    ldsBarrier();
   }
   const double r = sh[0];
-  __syncthreads();
+  ldsBarrier();
   return r;
 }
 
@@ -255,8 +269,9 @@ __device__ double reduceJv(const DevProblem& P, int w, WinState& s, double* sh) 
     for (int i = pb + t; i < pe; i += kRB) acc += P.pp_jv[(size_t)k * P.n_pprior + i];
     for (int i = sbb + t; i < sbe; i += kRB) acc += P.sbp_jv[(size_t)k * P.n_sbprior + i];
     for (int i = rpb + t; i < rpe; i += kRB) acc += P.rp_jv[(size_t)k * P.n_relpose + i];
-    a[k] = blockSum(acc, sh);
+    a[k] = acc;
   }
+  blockSumN<3>(a, sh);
   // |gradient_|^2 over the window (f-vector + free landmarks)
   double g2 = 0.0;
   const int fo = P.win_foff[w], fd = P.win_fdim[w];
@@ -278,7 +293,7 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
   const int w = blockIdx.x;
   WinState& s = P.st[w];
   if (s.done) return;
-  __shared__ double sh[kRB];
+  __shared__ double sh[3 * kRB];
   const int t = threadIdx.x;
   const int ob = P.win_obs_range[2 * w], oe = P.win_obs_range[2 * w + 1];
   const int ib = P.win_imu_range[2 * w], ie = P.win_imu_range[2 * w + 1];
@@ -318,8 +333,12 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
       if (P.rp_flags[i] & 2) cf += P.rp_cost[lb][i];
       else c += P.rp_cost[lb][i];
     }
-    c = blockSum(c, sh);
-    cf = blockSum(cf, sh);
+    {
+      double r2[2] = {c, cf};
+      blockSumN<2>(r2, sh);
+      c = r2[0];
+      cf = r2[1];
+    }
     if (t != 0) return;
     if (mode == R_COST_CAND) {
       // fixed residuals are not re-evaluated at candidates; their cost is fixed_cost
@@ -384,7 +403,7 @@ __global__ __launch_bounds__(kRB) void k_gradnorm(const DevProblem* __restrict__
   WinState& s = P.st[w];
   if (s.done) return;
   if (lin_mode == 1 && !s.accepted) return;
-  __shared__ double sh[kRB];
+  __shared__ double sh[3 * kRB];
   const int t = threadIdx.x;
   const int xs = s.xcur;
   const int foff = P.win_foff[w];
@@ -439,8 +458,12 @@ __global__ __launch_bounds__(kRB) void k_gradnorm(const DevProblem* __restrict__
                       }
                     });
   mx = blockMax(mx, sh);
-  g2 = blockSum(g2, sh);
-  x2 = blockSum(x2, sh);
+  {
+    double r2[2] = {g2, x2};
+    blockSumN<2>(r2, sh);
+    g2 = r2[0];
+    x2 = r2[1];
+  }
   if (t != 0) return;
   s.grad_max_norm = mx;
   s.grad_norm = sqrt(g2);
@@ -467,7 +490,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
   const int w = blockIdx.x;
   WinState& s = P.st[w];
   if (s.done) return;
-  __shared__ double sh[kRB];
+  __shared__ double sh[3 * kRB];
   __shared__ int sflag;
   const int t = threadIdx.x;
   const bool sflagGn = s.need_gn && !s.gn_failed;  // (read before thread 0 updates the state)
@@ -525,9 +548,13 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
     nn += r[4];
     gn += r[5];
   }
-  gg = blockSum(gg, sh);
-  nn = blockSum(nn, sh);
-  gn = blockSum(gn, sh);
+  {
+    double r3[3] = {gg, nn, gn};
+    blockSumN<3>(r3, sh);
+    gg = r3[0];
+    nn = r3[1];
+    gn = r3[2];
+  }
   const double gradient_norm = sqrt(gg), gauss_newton_norm = sqrt(nn);
   const double radius = s.radius;
   // step = ca * gradient_ + cb * gauss_newton_step_  (then divided by diagonal_)
@@ -642,9 +669,13 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
                       }
                       y[3] = v.x[3];
                     });
-  sn2 = blockSum(sn2, sh);
-  dn2 = blockSum(dn2, sh);
-  jr = blockSum(jr, sh);
+  {
+    double r3[3] = {sn2, dn2, jr};
+    blockSumN<3>(r3, sh);
+    sn2 = r3[0];
+    dn2 = r3[1];
+    jr = r3[2];
+  }
   if (t != 0) return;
   s.dogleg_step_norm = (dcase == 1) ? gauss_newton_norm : (dcase == 2) ? radius : sqrt(dn2);
   s.step_norm = sqrt(sn2);
