@@ -109,7 +109,12 @@ typedef struct okvisgpu_imu_params { /* okvis::ImuParameters subset, okvis_commo
  * Jacobian, PoseLocalParameterization.cpp:56-68), as Ceres does for a block with a manifold.
  * Return nonzero on success; 0 makes the evaluation fail (a candidate point is then rejected, as
  * Ceres does with candidate_cost = max; a failure at the initial point ends the window's solve with
- * OKVISGPU_FAILURE). Called concurrently from up to options.num_threads host threads. */
+ * OKVISGPU_FAILURE). Called concurrently from up to options.num_threads host threads.
+ * The calls are made from a host node of the context's captured iteration graph (hipLaunchHostFunc):
+ * the HIP runtime's callback thread fans them out to the context's persistent worker threads while
+ * the context's stream waits. A callback must therefore not call HIP or any okvisgpu_* function (it
+ * would wait on the stream it is blocking: deadlock); it may only read its parameters and its own
+ * data and write residuals / jacobians. */
 typedef int (*okvisgpu_host_evaluate_fn)(void* user, int32_t factor, const double* const* parameters,
                                          double* residuals, double** jacobians);
 #define OKVISGPU_HOST_MAX_RESIDUALS 15

@@ -125,7 +125,10 @@ class ReprojectionError final : public CostFunction {
 
 // ImuError (ImuError.cpp:63-1003): parameters (pose0, sb0, pose1, sb1). `state` is the functor's
 // mutable preintegration state (OKVISGPU_IMU_STATE_DOUBLES layout), written back after a solve.
-class ImuError final : public CostFunction {
+// A term that is a live view of an okvis ImuError object (OkvisImuError<E> below) overrides the
+// hooks: pull() refreshes samples, times and state from the object when the graph is flattened,
+// pullState() the state before every solve, pushState() writes the solved state back into it.
+class ImuError : public CostFunction {
  public:
   ImuError(std::vector<int64_t> sample_t_ns, std::vector<double> gyr_acc, const okvisgpu_imu_params& params,
            int64_t t0_ns, int64_t t1_ns)
@@ -136,6 +139,9 @@ class ImuError final : public CostFunction {
   std::string typeInfo() const override { return "ImuError"; }
   int residualDim() const override { return 15; }
   std::vector<int> parameterBlockSizes() const override { return {7, 9, 7, 9}; }
+  virtual void pull() {}
+  virtual void pullState() {}
+  virtual void pushState() {}
   std::vector<int64_t> sample_t_ns;
   std::vector<double> gyr_acc;
   okvisgpu_imu_params params;
@@ -254,22 +260,232 @@ ReprojectionError fromOkvisReprojectionError(const E& e, const okvisgpu_camera& 
   const double L[4] = {l00, l10, 0.0, l11};  // L^T row-major
   return ReprojectionError(camera, kp, L);
 }
-// ImuError: imuParameters(), imuMeasurements() (deque of Measurement<ImuSensorReadings>), t0(), t1()
-// (ImuError.hpp:89-92,216-224); time stamps through okvis::Time::toNSec().
+// ---- okvis functor internals. The members okvis keeps the solver state in are protected and have
+// no getters (ImuError.hpp:266-305, TwoPoseGraphError.hpp:178,283-284,364-372,
+// RelativePoseError.hpp:148-150, PoseError.hpp:166-170, SpeedAndBiasError.hpp:163-168). Each
+// accessor below is a class derived from the okvis functor type E that is never instantiated:
+// naming a protected member through it (&Members::Delta_q_) forms a pointer to E's member that
+// applies to any E object ([class.protected]), so the okvis headers stay unpatched. Eigen objects
+// are used only through their call operators / coefficient accessors (m(r, c), v(i), q.x(), ...).
+namespace okvis_access {
+template <class M>
+void matIn(const M& m, int R, int Cn, double* out) {
+  for (int r = 0; r < R; ++r)
+    for (int c = 0; c < Cn; ++c) out[r * Cn + c] = (double)m(r, c);
+}
+template <class M>
+void matOut(const double* in, int R, int Cn, M& m) {
+  for (int r = 0; r < R; ++r)
+    for (int c = 0; c < Cn; ++c) m(r, c) = in[r * Cn + c];
+}
+template <class V>
+void vecIn(const V& v, int n, double* out) {
+  for (int i = 0; i < n; ++i) out[i] = (double)v(i);
+}
+template <class T>  // kinematics::Transformation: coeffs() = [r_AB, q_AB xyzw] (Transformation.hpp:122-123)
+void transformationIn(const T& t, double* out) {
+  const auto& c = t.coeffs();
+  for (int i = 0; i < 7; ++i) out[i] = (double)c(i);
+}
+
+// okvis::ceres::ImuError's preintegration members <-> the OKVISGPU_IMU_STATE_DOUBLES blob.
 template <class E>
-ImuError fromOkvisImuError(const E& e) {
+struct ImuErrorMembers : E {
+  static void read(const E& e, double* s) {
+    for (int i = 0; i < OKVISGPU_IMU_STATE_DOUBLES; ++i) s[i] = 0.0;
+    s[0] = (double)(e.*(&ImuErrorMembers::redoCounter_));
+    s[1] = (e.*(&ImuErrorMembers::redo_)) ? 1.0 : 0.0;
+    const auto& q = e.*(&ImuErrorMembers::Delta_q_);
+    s[2] = q.x(); s[3] = q.y(); s[4] = q.z(); s[5] = q.w();
+    matIn(e.*(&ImuErrorMembers::C_integral_), 3, 3, s + 6);
+    matIn(e.*(&ImuErrorMembers::C_doubleintegral_), 3, 3, s + 15);
+    vecIn(e.*(&ImuErrorMembers::acc_integral_), 3, s + 24);
+    vecIn(e.*(&ImuErrorMembers::acc_doubleintegral_), 3, s + 27);
+    matIn(e.*(&ImuErrorMembers::dalpha_db_g_), 3, 3, s + 30);
+    matIn(e.*(&ImuErrorMembers::dv_db_g_), 3, 3, s + 39);
+    matIn(e.*(&ImuErrorMembers::dp_db_g_), 3, 3, s + 48);
+    vecIn(e.*(&ImuErrorMembers::speedAndBiases_ref_), 9, s + 57);
+    matIn(e.*(&ImuErrorMembers::squareRootInformation_), 15, 15, s + 66);
+    matIn(e.*(&ImuErrorMembers::cross_), 3, 3, s + 292);
+    matIn(e.*(&ImuErrorMembers::P_delta_), 15, 15, s + 301);
+  }
+  // The members are `mutable` in okvis, but a pointer to member cannot modify a const object
+  // ([expr.mptr.oper]), hence E&. information_ = U^T U as redoPreintegration / append set it
+  // (ImuError.cpp:463,252). dPdsigma_ (the four covariance derivatives ImuError::append continues
+  // from, ImuError.cpp:220-223,242-248) is written as P_delta_ / sigma_k^2 in the slot of the first
+  // non-zero noise density and zero in the others: append's recursion is linear in them, so it then
+  // continues P_delta_ exactly as from the four separate matrices.
+  static void write(const double* s, E& e) {
+    e.*(&ImuErrorMembers::redoCounter_) = (int)s[0];
+    e.*(&ImuErrorMembers::redo_) = s[1] != 0.0;
+    auto& q = e.*(&ImuErrorMembers::Delta_q_);
+    q.x() = s[2]; q.y() = s[3]; q.z() = s[4]; q.w() = s[5];
+    matOut(s + 6, 3, 3, e.*(&ImuErrorMembers::C_integral_));
+    matOut(s + 15, 3, 3, e.*(&ImuErrorMembers::C_doubleintegral_));
+    auto& ai = e.*(&ImuErrorMembers::acc_integral_);
+    auto& ad = e.*(&ImuErrorMembers::acc_doubleintegral_);
+    for (int i = 0; i < 3; ++i) { ai(i) = s[24 + i]; ad(i) = s[27 + i]; }
+    matOut(s + 30, 3, 3, e.*(&ImuErrorMembers::dalpha_db_g_));
+    matOut(s + 39, 3, 3, e.*(&ImuErrorMembers::dv_db_g_));
+    matOut(s + 48, 3, 3, e.*(&ImuErrorMembers::dp_db_g_));
+    auto& sb = e.*(&ImuErrorMembers::speedAndBiases_ref_);
+    for (int i = 0; i < 9; ++i) sb(i) = s[57 + i];
+    matOut(s + 66, 15, 15, e.*(&ImuErrorMembers::squareRootInformation_));
+    matOut(s + 292, 3, 3, e.*(&ImuErrorMembers::cross_));
+    matOut(s + 301, 15, 15, e.*(&ImuErrorMembers::P_delta_));
+    const double* U = s + 66;
+    auto& info = e.*(&ImuErrorMembers::information_);
+    for (int r = 0; r < 15; ++r)
+      for (int c = 0; c < 15; ++c) {
+        double v = 0.0;
+        for (int k = 0; k < 15; ++k) v += U[k * 15 + r] * U[k * 15 + c];
+        info(r, c) = v;
+      }
+    const auto& p = e.imuParameters();
+    const double sig[4] = {(double)p.sigma_g_c, (double)p.sigma_a_c, (double)p.sigma_gw_c, (double)p.sigma_aw_c};
+    int k0 = -1;
+    for (int k = 0; k < 4 && k0 < 0; ++k)
+      if (sig[k] != 0.0) k0 = k;
+    auto& dP = e.*(&ImuErrorMembers::dPdsigma_);
+    dP.resize(4);
+    for (int k = 0; k < 4; ++k)
+      for (int r = 0; r < 15; ++r)
+        for (int c = 0; c < 15; ++c) dP[k](r, c) = k == k0 ? s[301 + 15 * r + c] / (sig[k] * sig[k]) : 0.0;
+  }
+};
+
+// TwoPoseStandardGraphError(Const): DeltaX_, J_, linearisationPoint_T_S0S1_.
+template <class E>
+struct TwoPoseMembers : E {
+  static void read(const E& e, double* delta_x, double* J, double* lin_point) {
+    vecIn(e.*(&TwoPoseMembers::DeltaX_), 6, delta_x);
+    matIn(e.*(&TwoPoseMembers::J_), 6, 6, J);
+    transformationIn(e.*(&TwoPoseMembers::linearisationPoint_T_S0S1_), lin_point);
+  }
+};
+// RelativePoseError: T_AB_, squareRootInformation_ (RelativePoseError.hpp:148-150).
+template <class E>
+struct RelativePoseMembers : E {
+  static void read(const E& e, double* T_AB, double* sqrt_info) {
+    transformationIn(e.*(&RelativePoseMembers::T_AB_), T_AB);
+    matIn(e.*(&RelativePoseMembers::squareRootInformation_), 6, 6, sqrt_info);
+  }
+};
+// PoseError: measurement_, squareRootInformation_ (PoseError.hpp:166-170). The stored square root
+// is the one Evaluate uses; the diagonal constructor (PoseError.cpp:34-39) sets it to sqrt(diag),
+// which for the first-state prior's zero yaw/pitch entries (ViGraph.cpp:348-368) is not an LLT of
+// information() (singular), so the member is read rather than recomputed.
+template <class E>
+struct PoseErrorMembers : E {
+  static void read(const E& e, double* meas, double* sqrt_info) {
+    transformationIn(e.*(&PoseErrorMembers::measurement_), meas);
+    matIn(e.*(&PoseErrorMembers::squareRootInformation_), 6, 6, sqrt_info);
+  }
+};
+// SpeedAndBiasError: measurement_, squareRootInformation_ (SpeedAndBiasError.hpp:163-167).
+template <class E>
+struct SpeedAndBiasMembers : E {
+  static void read(const E& e, double* meas, double* sqrt_info) {
+    vecIn(e.*(&SpeedAndBiasMembers::measurement_), 9, meas);
+    matIn(e.*(&SpeedAndBiasMembers::squareRootInformation_), 9, 9, sqrt_info);
+  }
+};
+
+template <class E>
+okvisgpu_imu_params imuParams(const E& e) {  // imuParameters() (ImuError.hpp:216-218)
   const auto& p = e.imuParameters();
   okvisgpu_imu_params ip;
   ip.a_max = p.a_max; ip.g_max = p.g_max; ip.sigma_g_c = p.sigma_g_c; ip.sigma_a_c = p.sigma_a_c;
   ip.sigma_gw_c = p.sigma_gw_c; ip.sigma_aw_c = p.sigma_aw_c; ip.g = p.g;
-  std::vector<int64_t> t;
-  std::vector<double> ga;
+  return ip;
+}
+template <class E>  // imuMeasurements() (ImuError.hpp:221-223): okvis::Time stamps via toNSec()
+void imuSamples(const E& e, std::vector<int64_t>& t, std::vector<double>& ga) {
+  t.clear();
+  ga.clear();
   for (const auto& m : e.imuMeasurements()) {
     t.push_back((int64_t)m.timeStamp.toNSec());
     for (int k = 0; k < 3; ++k) ga.push_back((double)m.measurement.gyroscopes(k));
     for (int k = 0; k < 3; ++k) ga.push_back((double)m.measurement.accelerometers(k));
   }
-  return ImuError(std::move(t), std::move(ga), ip, (int64_t)e.t0().toNSec(), (int64_t)e.t1().toNSec());
+}
+}  // namespace okvis_access
+
+// A live view of an okvis ImuError object as a GPU-evaluated term: samples, t0 / t1 and the whole
+// preintegration state are read from the object when the graph is flattened (so a factor that okvis
+// already evaluated keeps its linearisation point, redo flag and counter: ImuError.cpp:834-858), the
+// state again before every solve (ImuError::append between solves, ImuError.cpp:63-255), and the
+// solved state is written back into the object after the solve, as Ceres' in-place evaluation
+// leaves it there. The object is not owned.
+template <class E>
+class OkvisImuError final : public ImuError {
+ public:
+  explicit OkvisImuError(E* e)
+      : ImuError({}, {}, okvis_access::imuParams(*e), (int64_t)e->t0().toNSec(), (int64_t)e->t1().toNSec()), e_(e) {
+    pull();
+  }
+  void pull() override {
+    params = okvis_access::imuParams(*e_);
+    t0_ns = (int64_t)e_->t0().toNSec();
+    t1_ns = (int64_t)e_->t1().toNSec();
+    okvis_access::imuSamples(*e_, sample_t_ns, gyr_acc);
+    pullState();
+  }
+  void pullState() override { okvis_access::ImuErrorMembers<E>::read(*e_, state.data()); }
+  void pushState() override { okvis_access::ImuErrorMembers<E>::write(state.data(), *e_); }
+  E* object() const { return e_; }
+
+ private:
+  E* e_;
+};
+
+// ImuError: imuParameters(), imuMeasurements() (deque of Measurement<ImuSensorReadings>), t0(), t1()
+// (ImuError.hpp:89-92,216-224) and, through the accessor, the preintegration state. A copy: the
+// solved state stays in the returned term (use OkvisImuError<E> to write it back into the object).
+template <class E>
+ImuError fromOkvisImuError(const E& e) {
+  std::vector<int64_t> t;
+  std::vector<double> ga;
+  okvis_access::imuSamples(e, t, ga);
+  ImuError r(std::move(t), std::move(ga), okvis_access::imuParams(e), (int64_t)e.t0().toNSec(),
+             (int64_t)e.t1().toNSec());
+  okvis_access::ImuErrorMembers<E>::read(e, r.state.data());
+  return r;
+}
+// Writes a term's solved state into the okvis object (what OkvisImuError::pushState does).
+template <class E>
+void toOkvisImuError(const ImuError& term, E& e) {
+  okvis_access::ImuErrorMembers<E>::write(term.state.data(), e);
+}
+// TwoPoseStandardGraphError / TwoPoseStandardGraphErrorConst (the kind from typeInfo(),
+// TwoPoseGraphError.hpp:360-362): DeltaX_, J_, linearisationPoint_T_S0S1_. These are constant
+// during a solve (compute() / the const clone set them), so nothing is written back.
+template <class E>
+TwoPoseGraphError fromOkvisTwoPoseGraphError(const E& e) {
+  double dx[6], J[36], lp[7];
+  okvis_access::TwoPoseMembers<E>::read(e, dx, J, lp);
+  return TwoPoseGraphError(dx, J, lp, std::string(e.typeInfo()) == "TwoPoseStandardGraphErrorConst");
+}
+// RelativePoseError (ViGraph::addRelativePoseConstraint, ViGraph.cpp:786-808).
+template <class E>
+RelativePoseError fromOkvisRelativePoseError(const E& e) {
+  double T[7], L[36];
+  okvis_access::RelativePoseMembers<E>::read(e, T, L);
+  return RelativePoseError(T, L);
+}
+// PoseError: the first-state and extrinsics priors (ViGraph.cpp:348-386).
+template <class E>
+PoseError fromOkvisPoseError(const E& e) {
+  double m[7], L[36];
+  okvis_access::PoseErrorMembers<E>::read(e, m, L);
+  return PoseError(m, L);
+}
+// SpeedAndBiasError: the first-state speed / bias prior (ViGraph.cpp:363-370).
+template <class E>
+SpeedAndBiasError fromOkvisSpeedAndBiasError(const E& e) {
+  double m[9], L[81];
+  okvis_access::SpeedAndBiasMembers<E>::read(e, m, L);
+  return SpeedAndBiasError(m, L);
 }
 
 // ---------------------------------------------------------------- Problem
@@ -344,6 +560,8 @@ class Problem {
     if (!host && !known.count(t))
       throw Unsupported("cost function \"" + t + "\" has no GPU evaluation (wrap it in a HostCostFunction)");
     if (loss && !host && t != "ReprojectionError") throw Unsupported(t + " with a loss function (okvis adds none)");
+    if (loss && !dynamic_cast<const CauchyLoss*>(loss))  // the device applies CauchyLoss(1) only
+      throw Unsupported(t + " with loss \"" + loss->name() + "\" (only CauchyLoss(1) is evaluated)");
     const std::vector<int> sizes = cost->parameterBlockSizes();
     if (host) {  // the §8b fallback's limits (okvisgpu.h host_*)
       int np = 0, ns = 0;
@@ -579,6 +797,7 @@ class Problem {
         A_.obs_cauchy.push_back(r->loss != nullptr);
       } else if (t == "ImuError") {
         auto* e = static_cast<ImuError*>(r->cost);
+        e->pull();  // a live view re-reads its okvis object (samples may have grown by append)
         const int32_t b[4] = {pidx(r->blocks[0], "ImuError"), sidx(r->blocks[1]), pidx(r->blocks[2], "ImuError"),
                               sidx(r->blocks[3])};
         A_.imu_blocks.insert(A_.imu_blocks.end(), b, b + 4);
@@ -749,9 +968,11 @@ class Problem {
     for (size_t i = 0; i < lmPtr_.size(); ++i) std::memcpy(&A_.lm[4 * i], lmPtr_[i], 4 * sizeof(double));
     for (size_t i = 0; i < extrPtr_.size() && 7 * i < A_.extr.size(); ++i)
       std::memcpy(&A_.extr[7 * i], extrPtr_[i], 7 * sizeof(double));
-    for (size_t f = 0; f < imuTerms_.size(); ++f)
+    for (size_t f = 0; f < imuTerms_.size(); ++f) {
+      imuTerms_[f]->pullState();
       std::memcpy(&A_.imu_state[f * OKVISGPU_IMU_STATE_DOUBLES], imuTerms_[f]->state.data(),
                   OKVISGPU_IMU_STATE_DOUBLES * sizeof(double));
+    }
   }
   // SoA -> caller's parameter memory (after a solve): the in-place write-back of Ceres
   void scatterValues() {
@@ -759,9 +980,11 @@ class Problem {
     for (size_t i = 0; i < sbPtr_.size(); ++i) std::memcpy(sbPtr_[i], &A_.sb[9 * i], 9 * sizeof(double));
     for (size_t i = 0; i < lmPtr_.size(); ++i) std::memcpy(lmPtr_[i], &A_.lm[4 * i], 4 * sizeof(double));
     for (size_t i = 0; i < extrPtr_.size(); ++i) std::memcpy(extrPtr_[i], &A_.extr[7 * i], 7 * sizeof(double));
-    for (size_t f = 0; f < imuTerms_.size(); ++f)
+    for (size_t f = 0; f < imuTerms_.size(); ++f) {
       std::memcpy(imuTerms_[f]->state.data(), &A_.imu_state[f * OKVISGPU_IMU_STATE_DOUBLES],
                   OKVISGPU_IMU_STATE_DOUBLES * sizeof(double));
+      imuTerms_[f]->pushState();  // into the okvis object of a live view
+    }
   }
 
   struct Arrays {

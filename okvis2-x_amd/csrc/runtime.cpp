@@ -14,11 +14,14 @@
 #include <cfloat>
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <numeric>
 #include <stdexcept>
 #include <string>
@@ -1067,6 +1070,60 @@ struct Arena {
 
 }  // namespace
 
+// Persistent host worker threads of one context: the host-evaluated factors (ABI 5) are evaluated
+// at every point the solver evaluates, from the HIP callback thread of the iteration graph's host
+// node, so the workers are created once (grown on demand) instead of per evaluation. run(n, f)
+// calls f(0..n-1) on n workers and returns when all are done.
+class HostWorkers {
+ public:
+  ~HostWorkers() {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      stop_ = true;
+    }
+    wake_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void run(int n, const std::function<void(int)>& f) {
+    while ((int)th_.size() < n) {
+      const int id = (int)th_.size();
+      th_.emplace_back([this, id]() { loop(id); });
+    }
+    std::unique_lock<std::mutex> l(m_);
+    job_ = &f;
+    njob_ = n;
+    pending_ = n;
+    ++gen_;
+    wake_.notify_all();
+    done_.wait(l, [&]() { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void loop(int id) {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> l(m_);
+    for (;;) {
+      wake_.wait(l, [&]() { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      if (id >= njob_) continue;
+      const std::function<void(int)>* f = job_;
+      l.unlock();
+      (*f)(id);
+      l.lock();
+      if (--pending_ == 0) done_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable wake_, done_;
+  const std::function<void(int)>* job_ = nullptr;
+  int njob_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 struct okvisgpu_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -1102,6 +1159,7 @@ struct okvisgpu_ctx {
   double* hostOut = nullptr;
   int hostBufFactors = 0;
   std::vector<uint8_t> hostFail;
+  HostWorkers hostWorkers;
 
   void fillSummaries(const std::vector<WinState>& st, okvisgpu_summary* sums) {
     if (!sums) return;
@@ -1239,13 +1297,9 @@ struct okvisgpu_ctx {
       for (int h = 0; h < n; ++h) hostEvaluateOne(h);
       return;
     }
-    std::vector<std::thread> th;
-    th.reserve(nt);
-    for (int t = 0; t < nt; ++t)
-      th.emplace_back([this, n, nt, t]() {
-        for (int h = (int)((int64_t)n * t / nt); h < (int)((int64_t)n * (t + 1) / nt); ++h) hostEvaluateOne(h);
-      });
-    for (auto& x : th) x.join();
+    hostWorkers.run(nt, [this, n, nt](int t) {
+      for (int h = (int)((int64_t)n * t / nt); h < (int)((int64_t)n * (t + 1) / nt); ++h) hostEvaluateOne(h);
+    });
   }
   static void hostEvaluateCallback(void* self) { static_cast<okvisgpu_ctx*>(self)->hostEvaluate(); }
 
@@ -2079,7 +2133,8 @@ int okvisgpu_profile_iteration(okvisgpu_ctx* c, double* ms) {
     launch_dogleg(P, s); mark(8);
     launch_eval_obs(P, 1, s); mark(9);
     launch_eval_imu(P, 1, s); mark(10);
-    launch_eval_priors(P, 1, s); mark(11);
+    launch_eval_priors(P, 1, s);
+    c->evalHost(1, s); mark(11);  // host-evaluated factors at the candidate (counted with the priors)
     launch_reduce(P, R_COST_CAND, s); mark(12);
     launch_linearization_blocks(P, 1, s); mark(13);
     launch_gradnorm(P, 1, s); mark(14);
@@ -2284,6 +2339,11 @@ int okvisgpu_evaluate(okvisgpu_ctx* c, int32_t window, double* cost) {
     HIPCHK(hipGetLastError());
     auto st = c->readStates();
     if (cost) *cost = st[window].x_cost + st[window].fixed_cost;
+    // a failed host_evaluate leaves +inf in the cost; report it like okvisgpu_eval_host does
+    // (ceres::Problem::Evaluate returns false)
+    const int h0 = c->B.win_host_range[2 * window], h1 = c->B.win_host_range[2 * window + 1];
+    for (int h = h0; h < h1; ++h)
+      if (c->hostFail[h - c->P.n_imu]) return fail(c, OKVISGPU_ERR_NUMERICAL, "host_evaluate failed");
     return (int)OKVISGPU_OK;
   });
 }

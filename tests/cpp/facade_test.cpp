@@ -181,20 +181,6 @@ struct MockReprojection {
   const Vec& measurement() const { return meas; }
   const Mat2& information() const { return info; }
 };
-struct MockTime { int64_t ns; int64_t toNSec() const { return ns; } };
-struct MockReadings { Vec gyroscopes, accelerometers; };
-struct MockImuMeasurement { MockTime timeStamp; MockReadings measurement; };
-struct MockImuParameters { double a_max = 176, g_max = 7.8, sigma_g_c = 12e-4, sigma_a_c = 8e-3, sigma_gw_c = 4e-6,
-                           sigma_aw_c = 4e-5, g = 9.81007; };
-struct MockImu {
-  MockImuParameters p;
-  std::vector<MockImuMeasurement> m{{{100}, {{{0.1, 0.2, 0.3}}, {{1, 2, 9.8}}}}, {{200}, {{{0.4, 0.5, 0.6}}, {{3, 4, 9.7}}}}};
-  const MockImuParameters& imuParameters() const { return p; }
-  const std::vector<MockImuMeasurement>& imuMeasurements() const { return m; }
-  MockTime t0() const { return {120}; }
-  MockTime t1() const { return {180}; }
-};
-
 // Records an okvisgpu_problem (e.g. a synthetic window) into a facade, block by block and residual
 // by residual, the way ViGraph adds them; parameter memory = the problem's own arrays.
 struct Recorded {
@@ -339,7 +325,7 @@ int cpuTests() {
     try { P.AddResidualBlock(&tp, nullptr, T0, T1, Tsc); } catch (const okvisgpu::Unsupported&) { hthrew = true; }
     CHECK(hthrew);
   }
-  // okvis functors through their getters (ReprojectionErrorBase.hpp:75-91, ImuError.hpp:89-92,216-224)
+  // okvis functors through their getters (ReprojectionErrorBase.hpp:75-91)
   {
     const MockReprojection mr;
     const okvisgpu::ReprojectionError re = okvisgpu::fromOkvisReprojectionError(mr, cam);
@@ -347,11 +333,8 @@ int cpuTests() {
     const double* U = re.sqrt_info;  // U^T U = information, U upper triangular
     CHECK(U[2] == 0.0 && std::fabs(U[0] * U[0] - 4.0) < 1e-15 && std::fabs(U[0] * U[1] - 1.0) < 1e-15 &&
           std::fabs(U[1] * U[1] + U[3] * U[3] - 9.0) < 1e-14);
-    const MockImu mi;
-    const okvisgpu::ImuError ie = okvisgpu::fromOkvisImuError(mi);
-    CHECK(ie.t0_ns == 120 && ie.t1_ns == 180 && ie.sample_t_ns.size() == 2 && ie.sample_t_ns[1] == 200);
-    CHECK(ie.gyr_acc.size() == 12 && ie.gyr_acc[0] == 0.1 && ie.gyr_acc[5] == 9.8 && ie.gyr_acc[11] == 9.7);
-    CHECK(ie.params.sigma_gw_c == 4e-6 && ie.params.g == 9.81007);
+    // (fromOkvisImuError also reads the protected preintegration state: okvis_roundtrip.cpp, against
+    // stand-ins with okvis' member layout)
   }
   // removal (RemoveParameterBlock drops its residual blocks too)
   P.RemoveResidualBlock(r01);

@@ -206,3 +206,90 @@ def test_gpu_host_failure_parity(og, parity, monkeypatch, serial):
     assert gsum[0]["termination"] == "FAILURE" and np.array_equal(gpu[0][0], x0)
     assert gsum[1]["num_unsuccessful_steps"] >= 1
     _assert_parity(parity, gsum, csum, gpu, cpu, f"host evaluation failures, serial graph {serial}")
+
+
+def _cauchy_window(seed=21):
+    """S10 + GPS with CauchyLoss(1) on every other factor and three gross GPS outliers (2 m on
+    keyframes 1, 4, 7, against sigma 0.05 m), so the loss changes both the cost and the step."""
+    P, fac, T_GW = gps_window(seed=seed)
+    P.host_cauchy[::2] = 1
+    P.host_cauchy[[1, 7]] = 1
+    fac.meas[[1, 4, 7]] += np.array([2.0, -2.0, 1.5])
+    P.bind()
+    return P, fac
+
+
+def test_oracle_host_cauchy_semantics(og):
+    """The oracle's Corrector on host factors: cost 0.5 log(1 + |r|^2) and r, J scaled by
+    sqrt(rho') = 1 / sqrt(1 + |r|^2) (Ceres' Corrector with rho'' < 0: TwoPoseGraphError.cpp:292-337
+    restates it), against the raw evaluation of the same factors."""
+    P, fac = _cauchy_window()
+    cost = _oracle.evaluate(P.ptr())
+    P.host_cauchy[:] = 0
+    P.bind()
+    raw = _oracle.evaluate(P.ptr())
+    expect = 0.0
+    for h in range(N_KF):
+        r, _ = fac.evaluate(h, [P.poses[h], P.speed_biases[h], P.poses[N_KF]])
+        s = float(r @ r)
+        expect += (0.5 * np.log1p(s) if h in (0, 1, 2, 4, 6, 7, 8) else 0.5 * s) - 0.5 * s
+    assert abs((cost - raw) - expect) <= 1e-9 * abs(raw)
+
+
+@pytest.mark.gpu
+def test_gpu_host_cauchy_parity(og, parity):
+    """Host factors with CauchyLoss(1) (host_cauchy = 1): the runtime's Corrector scaling and
+    0.5 log(1 + s) cost against the oracle, at the initial point (okvisgpu_evaluate) and in a solve."""
+    P, _ = _cauchy_window()
+    c_ref = _oracle.evaluate(P.ptr())
+    ctx = og.Context(0)
+    try:
+        ctx.set_problems([P.struct])
+        c_gpu = ctx.evaluate(0)
+    finally:
+        ctx.close()
+    parity("host factors, Cauchy: initial cost (rel)", abs(c_gpu - c_ref) / c_ref, 1e-12)
+    o = og.default_options(max_num_iterations=10, num_threads=2)
+    _assert_parity(parity, *_solve_both([P], o), "S10 + GPS with Cauchy")
+
+
+@pytest.mark.gpu
+def test_gpu_evaluate_reports_host_failure(og):
+    """okvisgpu_evaluate (ceres::Problem::Evaluate) with a failing host factor returns
+    OKVISGPU_ERR_NUMERICAL, as okvisgpu_eval_host does, instead of OK with an infinite cost."""
+    P, _, _ = gps_window(seed=11, fail=lambda h, prm: h == 3)
+    ctx = og.Context(0)
+    try:
+        ctx.set_problems([P.struct])
+        with pytest.raises(og.OkvisGpuError) as e:
+            ctx.evaluate(0)
+        assert "host_evaluate failed" in str(e.value)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_profile_iteration_with_host_factors(og):
+    """okvisgpu_profile_iteration runs a real iteration of the live solve: with host factors its
+    candidate evaluation includes them, so the solve it advanced matches a solve without profiling."""
+    opts = og.default_options(max_num_iterations=6, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    res = []
+    for profile in (False, True):
+        P, _, _ = gps_window(seed=31)
+        ctx = og.Context(0)
+        try:
+            ctx.set_problems([P.struct])
+            ctx.solve_begin(opts)
+            for it in range(6):
+                if profile and it in (1, 3):
+                    ctx.profile_iteration()
+                else:
+                    ctx.solve_iterate(1)
+            s = ctx.solve_end()[0]
+        finally:
+            ctx.close()
+        res.append((s, P.poses.copy()))
+    (s0, x0), (s1, x1) = res
+    assert s0["num_iterations"] == s1["num_iterations"] and s0["final_cost"] == s1["final_cost"], (s0, s1)
+    assert np.array_equal(x0, x1)
