@@ -1,6 +1,6 @@
 """The oracle as a sliding-window backend (test infrastructure): the same three calls the okvisgpu
 backend answers (okvisgpu_solve / okvisgpu_imu_append / okvisgpu_twopose_compute), answered by the
-CPU restatement, so that okvisgpu.sliding_window can run one sequence on each and compare."""
+CPU restatement, so that _sliding_window can run one sequence on each and compare."""
 import ctypes as C
 
 import _oracle

@@ -1,4 +1,4 @@
-"""The okvis realtime sliding-window sequence driven through the okvisgpu C ABI (host logic only).
+"""TEST INFRASTRUCTURE (the config-3 harness; not part of the product package). The okvis realtime sliding-window sequence driven through the okvisgpu C ABI (host logic only).
 
 This is the CALLER of the accelerated path, restated so that a whole okvis VIO run (BASELINE config
 3, "EuRoC MH_05 full sliding-window VIO": one realtime solve per frame, then marginalisation) can be
@@ -39,7 +39,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from . import (IMU_STATE_DOUBLES, Camera, Context, ImuParams, Problem, SynthWindow, TwoPoseBatch,
+from okvisgpu import (IMU_STATE_DOUBLES, Camera, Context, ImuParams, Problem, SynthWindow, TwoPoseBatch,
                default_options, dptr)
 
 _ip = C.POINTER(C.c_int32)
@@ -538,7 +538,8 @@ class _OwnedProblem:
           "pose_prior_meas": np.float64, "pose_prior_sqrt_info": np.float64, "sb_prior_block": np.int32,
           "sb_prior_meas": np.float64, "sb_prior_sqrt_info": np.float64, "relpose_blocks": np.int32,
           "relpose_delta_x": np.float64, "relpose_sqrt_info": np.float64, "relpose_lin_point": np.float64,
-          "relpose_kind": np.uint8}
+          "relpose_kind": np.uint8, "extrinsics_constant": np.uint8, "extrinsics_prior_camera": np.int32,
+          "extrinsics_prior_meas": np.float64, "extrinsics_prior_sqrt_info": np.float64}
     _PTR = {np.float64: C.POINTER(C.c_double), np.int32: _ip, np.int64: _lp, np.uint8: _up}
 
     def __init__(self):
@@ -573,6 +574,7 @@ class _OwnedProblem:
         s.n_pose_priors = len(self.pose_prior_block)
         s.n_sb_priors = len(self.sb_prior_block)
         s.n_relpose = len(self.relpose_blocks)
+        s.n_extrinsics_priors = len(self.extrinsics_prior_camera)
         self._cams = (Camera * max(1, len(self.cameras)))(*self.cameras)
         s.cameras = self._cams
         if s.n_imu == 0:

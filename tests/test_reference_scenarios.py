@@ -78,3 +78,58 @@ def test_gpu_imu_scene(og, oracle, gpu_ctx, seed, redo_always):
     assert sg["termination"] == so["termination"], (sg, so)
     assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-6 * so["final_cost"] + 1e-9, (sg, so)
     assert np.abs(est[:3] - p.poses[1][:3]).max() <= 1e-6
+
+
+# ---------------------------------------------------------------- TestViGraph2.cpp:31-221
+VIGRAPH2_CASES = [0, 1, 2, 3]
+
+
+def _vigraph2_check(w, pose, sb):
+    assert np.linalg.norm(sb - w.gt_sb) < 0.04                            # TestViGraph2.cpp:216-217
+    assert rot_err(w.gt_poses[-1, 3:], pose[3:]) < 1e-2                   # :218-219
+    assert np.linalg.norm(w.gt_poses[-1, :3] - pose[:3]) < 1e-1           # :220-221
+
+
+@pytest.mark.parametrize("case", VIGRAPH2_CASES)
+def test_oracle_vigraph2_thresholds(og, case):
+    """The ViGraph-level scene (two equidistant test cameras, 100 Hz IMU, landmark grid, 9 frames of
+    optimise(2, 4) with IMU-merge elimination and a pose-graph conversion, then optimise(10, 4)) on
+    the oracle, held to the reference's thresholds."""
+    from _ref_scenarios import ViGraph2Run, ViGraph2World
+    from _sequence import OracleBackend
+    w = ViGraph2World(case, seed=100 + case)
+    run = ViGraph2Run(w, OracleBackend())
+    pose, sb = run.run()
+    _vigraph2_check(w, pose, sb)
+    kinds = [e[0] for e in run.sw.log]
+    assert kinds.count("imu_merge") == 2 and kinds.count("edge") == (0 if w.do_extrinsics else 1)
+    assert run.summaries[-1]["termination"] == "CONVERGENCE"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", VIGRAPH2_CASES)
+def test_gpu_vigraph2(og, case, parity):
+    """The same scene through okvisgpu (its own estimates, IMU states and edges from frame to
+    frame): the reference's thresholds, and every solve against the oracle's run of the scene."""
+    from _ref_scenarios import ViGraph2Run, ViGraph2World
+    from _sequence import OracleBackend
+    from _sliding_window import GpuBackend
+    cpu = ViGraph2Run(ViGraph2World(case, seed=100 + case), OracleBackend())
+    pose_c, sb_c = cpu.run()
+    backend = GpuBackend(0)
+    try:
+        w = ViGraph2World(case, seed=100 + case)
+        gpu = ViGraph2Run(w, backend)
+        pose_g, sb_g = gpu.run()
+    finally:
+        backend.close()
+    _vigraph2_check(w, pose_g, sb_g)
+    assert gpu.sw.log == cpu.sw.log
+    worst = 0.0
+    for k, (g, c) in enumerate(zip(gpu.summaries, cpu.summaries)):
+        assert (g["num_iterations"], g["termination"], g["num_successful_steps"]) == \
+            (c["num_iterations"], c["termination"], c["num_successful_steps"]), (k, g, c)
+        worst = max(worst, abs(g["final_cost"] - c["final_cost"]) / c["final_cost"])
+    parity(f"TestViGraph2 case {case}: cost (rel, every solve)", worst, 1e-7)
+    parity(f"TestViGraph2 case {case}: last pose (m)", np.abs(pose_g[:3] - pose_c[:3]).max(), 1e-6)
+    parity(f"TestViGraph2 case {case}: last speed/bias", np.abs(sb_g - sb_c).max(), 1e-6)

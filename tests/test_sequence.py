@@ -2,7 +2,7 @@
 solve per frame, then the marginalisation strategy -- IMU-merge elimination of non-keyframes
 (okvisgpu_imu_append), conversion of the least-covisible keyframe into pose-graph edges
 (okvisgpu_twopose_compute), freezing of old states -- chained over 28 frames after a 6-frame start
-(okvisgpu.sliding_window; ViSlamBackend.cpp:555-1010, ViGraphEstimator.cpp:38-171,216-298,334-610).
+(tests/_sliding_window.py; ViSlamBackend.cpp:555-1010, ViGraphEstimator.cpp:38-171,216-298,334-610).
 
 CPU: the sequence on the oracle backend exercises every strategy branch and tracks the ground truth.
 GPU: the same sequence on okvisgpu and on the oracle, each carrying its own estimates from frame to
@@ -11,7 +11,7 @@ poses, landmarks, IMU preintegration and the created edges agreeing (tolerances 
 import numpy as np
 import pytest
 
-from okvisgpu.sliding_window import GpuBackend, SlidingWindow, World
+from _sliding_window import GpuBackend, SlidingWindow, World
 from _sequence import OracleBackend
 
 N_FRAMES = 34
