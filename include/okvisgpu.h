@@ -238,11 +238,9 @@ typedef struct okvisgpu_options {   /* ::ceres::Solver::Options fields okvis set
   int32_t redo_propagation_always;  /* ImuError::redoPropagationAlways (ViSlamBackend.cpp:2036)  */
   int32_t num_threads;              /* host threads (reference path / host evaluation)          */
   int32_t verbose;
-  int32_t cholesky_schedule;        /* 0 auto, 1 one persistent workgroup per window (more        */
-                                    /* windows than CUs), 2 tile-parallel launches per step (few  */
-                                    /* windows), 3 wave-specialised workgroup per window, 4 the   */
-                                    /* persistent kernel with the step's panel tiles kept in LDS  */
-                                    /* (up to one window per CU; same bits as 1)                  */
+  int32_t cholesky_schedule;        /* 0 auto, 1 one persistent workgroup per window (from half a */
+                                    /* window per CU), 2 tile-parallel launches per step (fewer   */
+                                    /* windows); both give the same bits. Other values: auto.     */
 } okvisgpu_options;
 
 typedef struct okvisgpu_summary {   /* ::ceres::Solver::Summary subset */

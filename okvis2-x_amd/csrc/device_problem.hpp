@@ -19,6 +19,7 @@ namespace okg {
 
 constexpr int kCamDoubles = 13;       // per camera on the device: dist, fu, fv, cu, cv, 8 distortion parameters
 constexpr int kTile = 64;             // Cholesky tile (one 64x64 FP64 tile = 32 KiB of LDS)
+constexpr int16_t kNoUpdate = 32767;  // tile_fu of a tile no band update writes
 constexpr int kImuLin = 15 + 15 * 30; // per-IMU-factor linearisation record: r[15], J[15][30]
 constexpr int kImuState = 526;        // == OKVISGPU_IMU_STATE_DOUBLES
 // host-evaluated factor records: in = live flag (0 idle, 1 + linearisation buffer) | pad | slot
@@ -258,7 +259,10 @@ struct DevProblem {
   const Contrib* pair_contrib;
 
   // --- f-vectors (window-concatenated, reduced ordering) and landmark vectors
-  double* S;                       // sum over windows fpad^2
+  double* S;                       // sum over windows fpad^2: the assembled reduced matrix (the
+                                   // factorisation never writes it: its entries outside the
+                                   // assembled blocks stay zero from the build, no clearing per iteration)
+  double* W;                       // same layout: the factorisation's working tiles (updated tiles, L)
   double* Linv;                    // per window (fpad/64) inverses of the 64x64 diagonal factors
   const int64_t* win_linvoff;      // [n_win] offset into Linv
   // tile-level symbolic factorisation (host analysis): the reduced camera matrix of a sliding
@@ -273,9 +277,10 @@ struct DevProblem {
   const int32_t* chol_upd_begin;
   const int32_t* h_panel_begin;
   const int32_t* h_upd_begin;
-  int32_t chol_schedule;             // 1 persistent per window, 2 tile-parallel, 3 wave-specialised, 4 persistent wide (host-resolved)
-  int32_t chol_pairs;                // schedule 3: two windows per workgroup
+  int32_t chol_schedule;             // 1 persistent per window, 2 tile-parallel (host-resolved)
   const uint8_t* tile_nz;            // per window T x T (row-major) structural non-zero flags of L
+  const int16_t* tile_fu;            // per window T x T (same offsets): the first step whose band update
+                                     // writes tile (i, j) (kNoUpdate if none): before it the tile is read from S
   const int64_t* win_tnzoff;         // [n_win] offset of the window's flags in tile_nz
   int32_t n_tiles;
   double* fwdF;                    // per window fpad: forward-substitution work vector

@@ -49,28 +49,30 @@ __device__ unsigned long long g_cholClk[32];
 #define CLK(i)
 #define CLKW(i, cond)
 #endif
-// Development-only phase cut of potrfTile (scripts/ubench_ptile.hip): return after phase n.
-#ifdef OKG_POTRF_STOP
-#define POTRF_STOP(n) \
-  if (OKG_POTRF_STOP == (n)) return true;
-#else
-#define POTRF_STOP(n)
-#endif
-// Development-only sweep timeline (scripts/ubench_ptile.hip, -DOKG_SWEEP_TRACE): lane 0 of the
-// sweep wavefronts of workgroup 0 stores s_memtime at each hand-over point.
-#ifdef OKG_SWEEP_TRACE
-__device__ unsigned long long g_sweepT[2][8][8];
-#define STR(a, s, i) \
-  if (lane == 0) sTr[a][s][i] = __builtin_amdgcn_s_memtime();
-#else
-#define STR(a, s, i)
-#endif
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ bool cholSelect(const DevProblem& P, int w) {
   const WinState& s = P.st[w];
   return !s.done && s.need_gn && !s.gn_failed;
+}
+
+// Tile (i, j) as the factorisation sees it at step k: the assembled S until the first band update
+// has written it (step tile_fu), the working copy W from then on. Every factorisation write (band
+// updates, panels L_ik, the tile-parallel schedule's upper-slot L) goes to W, so S keeps the
+// assembled blocks and zeros and is never cleared per iteration.
+struct TileSrc {
+  const double* S;
+  const double* W;
+  const int16_t* fu;
+  int T;
+  int64_t ld;
+  __device__ __forceinline__ const double* at(int i, int j, int k) const {
+    return (fu[i * T + j] < k ? W : S) + (int64_t)i * kTile * ld + j * kTile;
+  }
+};
+__device__ __forceinline__ TileSrc tileSrc(const DevProblem& P, int w, int64_t ld) {
+  return TileSrc{P.S + P.win_soff[w], P.W + P.win_soff[w], P.tile_fu + P.win_tnzoff[w], (int)(ld / kTile), ld};
 }
 
 // 64x64 global tile (row stride ld) -> LDS [64][kLd]: all 8 16-byte loads of a thread are issued
@@ -155,13 +157,6 @@ __device__ __forceinline__ void storeTileSub(double* A, int64_t ld, const dbl4 c
         gmemw(A)[(int64_t)(r0 + 16 * a + (lane >> 4) + 4 * reg) * ld + c0 + 16 * b + (lane & 15)] = c[a][b][reg] - acc[a][b][reg];
 }
 
-__device__ __forceinline__ double readlaneD(double v, int lane) {  // v of `lane`, wave-uniform
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)b, lane);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
 // 1/sqrt(d) to ~1 ulp: v_rsq_f64 (~5e-8 relative) refined by two Newton steps (measured on
 // gfx950: 2.3e-16 max relative error over d in [e^-40, e^40]).
 __device__ __forceinline__ double rsqrtRefined(double d) {
@@ -195,10 +190,6 @@ __device__ __forceinline__ void storeC16(double* c, int ldc, const dbl4& v, int 
 #pragma unroll
   for (int r = 0; r < 4; ++r) c[((lane >> 4) + 4 * r) * ldc + (lane & 15)] = v[r];
 }
-
-struct WsFlags {
-  int xReady, diagReady, xFree, fail, gbar, sbar;
-};
 
 __device__ __forceinline__ int ldsAcquire(int* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -364,18 +355,6 @@ __device__ __forceinline__ void trailing8(double* sA, int c0, int wg, int nw, in
   trailingFrom(sA, c0, c0 + 8, wg, nw, lane);
 }
 
-// 64x64 global tile (row stride ld) -> LDS [64][kLd] by DMA (global_load_lds, 4 bytes per lane:
-// one instruction moves half a row, 64 dwords, to a contiguous LDS range), half rows dealt to the
-// ng wavefronts (this one is g). Completion is counted by vmcnt.
-__device__ __forceinline__ void dmaTile(const double* src, int64_t ld, double* dst, int g, int ng, int lane) {
-  for (int h = g; h < 2 * kTile; h += ng) {
-    const int row = h >> 1, half = h & 1;
-    const uint32_t* gs = reinterpret_cast<const uint32_t*>(src + (int64_t)row * ld + 32 * half) + lane;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gs,
-                                     (__attribute__((address_space(3))) void*)(dst + row * kLd + 32 * half), 4, 0, 0);
-  }
-}
-
 // X = L^-1 of the in-LDS diagonal tile by 16-row block rows (sX holds X, sA the final L):
 // X21 = -X22 (L21 X11) of the diagonal 16x16 block q, whose 8x8 diagonal inverses are in sX
 // (one wavefront; lane = (row m, column j)).
@@ -458,14 +437,10 @@ __device__ __forceinline__ void xStoreRows16(const double* sX, double* Li, int q
 // (one non-inlined instantiation per calling kernel: a shared callee gets a generic register
 // budget that halves the persistent kernel's occupancy)
 template <int kCaller>
-__device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX, double* sy,
-                                      double* sRl, int* sFl, int t, bool haveTile, const double* pfA0 = nullptr,
-                                      const double* pfA1 = nullptr, double* sP = nullptr) {
+__device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX, double* sy,
+                                      double* sRl, int* sFl, int t, bool haveTile) {
   const int wave = t >> 6, lane = t & 63;
   CLK_INIT
-#ifdef OKG_SWEEP_TRACE
-  __shared__ unsigned long long sTr[2][8][8];
-#endif
   if (!haveTile) loadTile(Sg, ld, 0, 0, sA, t);  // (else the caller left S_kk in sA)
 #pragma unroll
   for (int u = 0; u < 16; ++u) {
@@ -479,7 +454,13 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
   // applies each sub-panel's rank-8 update to the next sub-panel's 8 columns itself (VALU, its own
   // row); wavefronts 1-3 apply it to the columns beyond (matrix cores) and form the 8x8 inverse
   // blocks, one sub-panel behind, handing over through LDS flags.
+#ifdef OKG_FACTOR_PRIO  // (A/B knob: the whole factoring workgroup ahead of the co-resident one)
+  __builtin_amdgcn_s_setprio(OKG_FACTOR_PRIO);
+#endif
   if (wave == 0) {
+#ifdef OKG_CHAIN_PRIO  // (A/B knob: issue priority of the sweep wavefront over co-resident waves)
+    __builtin_amdgcn_s_setprio(OKG_CHAIN_PRIO);
+#endif
     const int i = lane;
     double xp[8];
 #pragma unroll
@@ -488,10 +469,8 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
     for (int s = 0; s < 8; ++s) {
       const int c0 = 8 * s;
       CLK(25)
-      STR(0, s, 0)
       if (s >= 2 && !waitFlag<true>(&sFl[1], s - 1, &sFl[2])) break;  // trailing update of sub-panel s-2
       CLK(21)
-      STR(0, s, 1)
       double r[8], x[8], rl[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) r[k] = sA[i * kLd + c0 + k];
@@ -509,13 +488,11 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
         __builtin_amdgcn_wave_barrier();
       }
       CLK(22)
-      STR(0, s, 2)
       if (!chol8Row(sA, c0, r, x, rl)) {
         if (lane == 0) ldsReleaseL(&sFl[2], 1);
         break;
       }
       CLK(23)
-      STR(0, s, 3)
       storeRow8(sA, c0, x, i);
       if (lane == 0) {
 #pragma unroll
@@ -523,29 +500,18 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
         ldsReleaseL(&sFl[0], s + 1);
       }
       CLK(24)
-      STR(0, s, 4)
 #pragma unroll
       for (int k = 0; k < 8; ++k) xp[k] = x[k];
     }
   } else {
     const int g = wave - 1;
     int gen = 0;
-    // wide persistent schedule: the step's panel tiles A_ik go to LDS by DMA (no registers) while
-    // wavefront 0 runs the sweep
-    if (kCaller == 3 && pfA0) dmaTile(pfA0, ld, sP, g, 3, lane);
-    if (kCaller == 3 && pfA1) dmaTile(pfA1, ld, sP + kTile * kLd, g, 3, lane);
 #pragma unroll 1
     for (int s = 0; s < 8; ++s) {
       if (!waitFlag<true>(&sFl[0], s + 1, &sFl[2])) break;
-      if (g == 0) { STR(1, s, 0) }
-#ifndef OKG_SWEEP_SOLO
       if (g == 0) inv8(sA, sRl, sX + 8 * s * kLd + 8 * s, 8 * s, lane);
-      if (g == 0) { STR(1, s, 1) }
       if (s < 6) trailingFrom(sA, 8 * s, 8 * s + 16, g, 3, lane);
-#endif
-      if (g == 0) { STR(1, s, 2) }
       waveBarrier<true>(&sFl[3], gen, 3, lane);
-      if (g == 0) { STR(1, s, 3) }
       if (g == 0 && lane == 0) ldsReleaseL(&sFl[1], s + 1);
       if (s & 1) {
         // the 16 columns of block q are factored: block row q of X, y_q and the X store of those
@@ -553,24 +519,19 @@ __device__ __noinline__ bool potrfTile(double* Sg, int64_t ld, double* Li, doubl
         const int q = s >> 1;
         if (g == 0) xDiag16(sA, sX, q, lane);
         waveBarrier<true>(&sFl[3], gen, 3, lane);
-        if (g == 0) { STR(1, s, 4) }
         if (g < q) xOffDiag16(sA, sX, q, g, lane);
         waveBarrier<true>(&sFl[3], gen, 3, lane);
-        if (g == 0) { STR(1, s, 5) }
         if (g == 0) yBlock16(sX, sy, q, lane);
         xStoreRows16<kCaller>(sX, Li, q, g, lane);
-        if (g == 0) { STR(1, s, 6) }
       }
     }
-    if (kCaller == 3 && pfA0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the panel tiles have landed in LDS
   }
+#if defined(OKG_CHAIN_PRIO) || defined(OKG_FACTOR_PRIO)
+  __builtin_amdgcn_s_setprio(0);
+#endif
   ldsBarrier();
   CLK(5)
-#ifdef OKG_SWEEP_TRACE
-  if (blockIdx.x == 0 && t < 128) g_sweepT[t >> 6][(t >> 3) & 7][t & 7] = sTr[t >> 6][(t >> 3) & 7][t & 7];
-#endif
   if (sFl[2]) return false;
-  POTRF_STOP(1)
   // LDS-only barriers from here: the X / y stores stay in flight (no reader in this
   // workgroup before a later full barrier or the end of the launch)
   if (t < kTile) {
@@ -611,7 +572,7 @@ __device__ __forceinline__ void panelRhsVector(const double* sX, const double* s
 
 // L_ik = A_ik X^T (X = L_kk^-1 in sX) stored over A_ik, and rhs_i -= A_ik z (z = X^T y_k in sz),
 // the row products formed from the A_ik tile in LDS while the MFMAs run.
-__device__ __forceinline__ void panelTile(double* Aik, int64_t ld, double* worki, double* sA, const double* sX, const double* sz,
+__device__ __forceinline__ void panelTile(const double* Aik, double* Lik, int64_t ld, double* worki, double* sA, const double* sX, const double* sz,
                           int t) {
   loadTile(Aik, ld, 0, 0, sA, t);
   ldsBarrier();  // LDS-only: the previous panel's L / rhs stores stay in flight
@@ -627,7 +588,7 @@ __device__ __forceinline__ void panelTile(double* Aik, int64_t ld, double* worki
     if (q == 0) worki[row] -= a;  // rhs_i in LDS
   }
   ldsBarrier();  // sA is free for the next panel
-  storeTile<false>(Aik, ld, 0, 0, acc, t);
+  storeTile<false>(Lik, ld, 0, 0, acc, t);
 }
 
 
@@ -772,7 +733,8 @@ __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem
   if (!cholSelect(P, w)) return;
   const int64_t ld = P.win_fpad[w];
   const int T = (int)(ld / kTile);
-  double* S = P.S + P.win_soff[w];
+  const TileSrc cur = tileSrc(P, w, ld);
+  double* W = P.W + P.win_soff[w];
   double* Linv = P.Linv + P.win_linvoff[w];
   const uint8_t* nz = P.tile_nz + P.win_tnzoff[w];
   __shared__ double sA[kTile * kLd];
@@ -793,7 +755,7 @@ __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem
     CLK(11)
     if (t < kTile) sy[t] = sxDyn[k * kTile + t];
     __syncthreads();  // full: the factor and the panels read the tiles the last band update stored
-    if (!potrfTile<0>(S + k * kTile * ld + k * kTile, ld, Linv + (int64_t)k * kTile * kTile, nullptr, sA, sX,
+    if (!potrfTile<0>(cur.at(k, k, k), ld, Linv + (int64_t)k * kTile * kTile, nullptr, sA, sX,
                    sy, sRl, sFl, t, haveDiag)) {
       if (t == 0) P.st[w].gn_failed = 1;
       return;
@@ -802,15 +764,11 @@ __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem
     CLK(0)
     // ---- panel: L_ik = A_ik X^T, rhs_i -= L_ik y_k = A_ik X^T y_k
     panelRhsVector(sX, sy, sy + kTile, sA, t);
-#ifndef OKG_CHOL_SKIP_PANEL  // (development-only phase cut: timing builds)
     for (int i = k + 1; i < T; ++i)
-      if (nz[i * T + k]) panelTile(S + i * kTile * ld + k * kTile, ld, sxDyn + i * kTile, sA, sX, sy + kTile, t);
-#endif
+      if (nz[i * T + k])
+        panelTile(cur.at(i, k, k), W + i * kTile * ld + k * kTile, ld, sxDyn + i * kTile, sA, sX, sy + kTile, t);
     __syncthreads();  // full barrier: the band update reads the L_ik just stored
     CLK(1)
-#ifdef OKG_CHOL_SKIP_UPDATE
-    continue;
-#endif
     // ---- trailing band update: A_ij -= L_ik L_jk^T, k < j <= i, both tiles non-zero. The A_ij
     // read of the read-modify-write is issued before the MFMAs, so its latency overlaps them.
     // Block rows from the bottom: the L_jk staged in sX for a lower row is reused as the row
@@ -823,24 +781,24 @@ __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem
       if (!nz[i * T + k]) continue;
       const bool aInX = xHeld == i;
       const double* aBuf = aInX ? sX : sA;
-      if (!aInX) loadTile(S + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
+      if (!aInX) loadTile(W + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
       for (int j = k + 1; j <= i; ++j) {
         if (!nz[j * T + k]) continue;
         const double* bBuf = aBuf;
         if (j != i) {
           if (aInX) {
-            loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sA, t);
+            loadTile(W + j * kTile * ld + k * kTile, ld, 0, 0, sA, t);
             bBuf = sA;
           } else {
-            if (xHeld != j) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sX, t);
+            if (xHeld != j) loadTile(W + j * kTile * ld + k * kTile, ld, 0, 0, sX, t);
             xHeld = j;
             bBuf = sX;
           }
         }
         ldsBarrier();
-        double* Cij = S + i * kTile * ld + j * kTile;
+        double* Cij = W + i * kTile * ld + j * kTile;
         dbl4 c[2][2], acc[2][2];
-        loadC(Cij, ld, c, t);
+        loadC(cur.at(i, j, k), ld, c, t);
         mfmaTileNT(aBuf, bBuf, acc, t);
         if (i == k + 1) {  // (then j == i) the next diagonal tile: c - acc straight into sA
           ldsBarrier();    // every wavefront has read its operands
@@ -854,7 +812,7 @@ __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem
     }
   }
   CLK(2)
-  backSubstitute(P, w, S, ld, T, Linv, nz, sxDyn, sA, sy, t);
+  backSubstitute(P, w, W, ld, T, Linv, nz, sxDyn, sA, sy, t);
   CLK(3)
 #ifdef OKG_CHOL_CLOCK
   if (blockIdx.x == 0 && t == 0)
@@ -880,7 +838,7 @@ __global__ __launch_bounds__(256) void k_chol_diag(const DevProblem* __restrict_
   const int64_t ld = P.win_fpad[w];
   const int T = (int)(ld / kTile);
   if (k >= T) return;
-  double* S = P.S + P.win_soff[w];
+  const TileSrc cur = tileSrc(P, w, ld);
   double* work = P.fwdF + P.win_fwdoff[w];
   __shared__ double sA[kTile * kLd];
   __shared__ double sX[kTile * kLd];
@@ -895,7 +853,7 @@ __global__ __launch_bounds__(256) void k_chol_diag(const DevProblem* __restrict_
   }
   if (t < kTile) sy[t] = work[k * kTile + t];
   __syncthreads();
-  if (!potrfTile<1>(S + k * kTile * ld + k * kTile, ld, P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile,
+  if (!potrfTile<1>(cur.at(k, k, k), ld, P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile,
                     work + k * kTile, sA, sX, sy, sRl, sFl, t, false))
     if (t == 0) P.st[w].gn_failed = 1;
 }
@@ -912,109 +870,6 @@ __device__ __forceinline__ void accToLds(double* s, const dbl4 acc[2][2], int t)
       for (int reg = 0; reg < 4; ++reg) s[(r0 + 16 * a + (lane >> 4) + 4 * reg) * kLd + c0 + 16 * b + (lane & 15)] = acc[a][b][reg];
 }
 
-// ---- wide persistent schedule (schedule 4, up to one window per CU): k_cholesky with the step's
-// panel tiles in LDS. One workgroup per CU leaves LDS for two more tiles: the panel tiles A_ik of
-// step k are moved to LDS by DMA on wavefronts 1-3 during the diagonal factor, each panel's L_ik
-// replaces its A_ik there (and is stored for the backward substitution), and the band updates take
-// both operands from LDS: no global operand load on the step's chain except a third panel tile
-// (staged in sA) and the C tiles of the read-modify-writes (issued before the MFMAs as in
-// k_cholesky). The same operations in the same
-// order as k_cholesky: the same bits (test_cholesky_schedules_agree). Requires at most
-// kCholWidePanels non-zero tiles below every diagonal tile (host-checked, cholesky_wide_fits).
-#ifndef OKG_WIDE_OCC
-#define OKG_WIDE_OCC 1
-#endif
-__global__ __launch_bounds__(256, OKG_WIDE_OCC) void k_cholesky_wide(const DevProblem* __restrict__ Pp) {
-  const DevProblem& P = *Pp;
-  const int w = blockIdx.x;
-  if (!cholSelect(P, w)) return;
-  const int64_t ld = P.win_fpad[w];
-  const int T = (int)(ld / kTile);
-  double* S = P.S + P.win_soff[w];
-  double* Linv = P.Linv + P.win_linvoff[w];
-  const uint8_t* nz = P.tile_nz + P.win_tnzoff[w];
-  __shared__ double sA[kTile * kLd];
-  __shared__ double sX[kTile * kLd];
-  __shared__ double sP[2 * kTile * kLd];
-  __shared__ double sy[2 * kTile];
-  __shared__ double sRl[kTile];
-  __shared__ int sFl[4];
-  const int t = threadIdx.x;
-  const int fdim = P.win_fdim[w];
-  extern __shared__ double sxDyn[];
-  for (int e = t; e < ld; e += 256) sxDyn[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
-  __syncthreads();
-  bool haveDiag = false;
-  for (int k = 0; k < T; ++k) {
-    int pr[kCholWidePanels], np = 0;  // the step's panel rows, ascending
-    for (int i = k + 1; i < T && np < kCholWidePanels; ++i)
-      if (nz[i * T + k]) pr[np++] = i;
-    // panel b's tile: b < 2 in sP (moved there by DMA during the factor), b == 2 staged in sA
-    // (free after the factor; its L is last used by the updates of its own, the bottom, row, so
-    // the next diagonal tile can take sA afterwards)
-    auto pbuf = [&](int b) { return b < 2 ? sP + b * kTile * kLd : sA; };
-    if (t < kTile) sy[t] = sxDyn[k * kTile + t];
-    __syncthreads();  // full: the factor and the DMA read the tiles the last band update stored
-#ifdef OKG_WIDE_NODMA  // (development A/B: panel tiles loaded at panel time instead of during the factor)
-    constexpr bool kDma = false;
-#else
-    constexpr bool kDma = true;
-#endif
-    if (!potrfTile<3>(S + k * kTile * ld + k * kTile, ld, Linv + (int64_t)k * kTile * kTile, nullptr, sA, sX, sy, sRl,
-                      sFl, t, haveDiag, kDma && np > 0 ? S + pr[0] * kTile * ld + k * kTile : nullptr,
-                      kDma && np > 1 ? S + pr[1] * kTile * ld + k * kTile : nullptr, sP)) {
-      if (t == 0) P.st[w].gn_failed = 1;
-      return;
-    }
-    if (t < kTile) sxDyn[k * kTile + t] = sy[t];
-    // ---- panels from LDS: L_ik = A_ik X^T replaces A_ik in sP (and goes to S), rhs_i -= A_ik z
-    panelRhsVector(sX, sy, sy + kTile, sA, t);
-    for (int b = 0; b < np; ++b) {
-      double* sPb = pbuf(b);
-      if (b == 2 || !kDma) {
-        loadTile(S + pr[b] * kTile * ld + k * kTile, ld, 0, 0, sPb, t);
-        ldsBarrier();
-      }
-      dbl4 acc[2][2];
-      mfmaTileNT(sPb, sX, acc, t);
-      {
-        const int row = t >> 2, q = t & 3;
-        double a = 0.0;
-#pragma unroll
-        for (int c = 16 * q; c < 16 * q + 16; ++c) a += sPb[row * kLd + c] * sy[kTile + c];
-        a += __shfl_xor(a, 1, 64);
-        a += __shfl_xor(a, 2, 64);
-        if (q == 0) sxDyn[pr[b] * kTile + row] -= a;
-      }
-      ldsBarrier();  // every wavefront has read A_ik
-      accToLds(sPb, acc, t);
-      storeTile<false>(S + pr[b] * kTile * ld + k * kTile, ld, 0, 0, acc, t);
-    }
-    ldsBarrier();  // the L tiles in sP are complete
-    // ---- band update A_ij -= L_ik L_jk^T from the L tiles in LDS, block rows from the bottom
-    haveDiag = false;
-    for (int bi = np - 1; bi >= 0; --bi) {
-      const int i = pr[bi];
-      for (int bj = 0; bj <= bi; ++bj) {
-        const int j = pr[bj];
-        double* Cij = S + i * kTile * ld + j * kTile;
-        dbl4 c[2][2], acc[2][2];
-        loadC(Cij, ld, c, t);
-        mfmaTileNT(pbuf(bi), pbuf(bj), acc, t);
-        if (i == k + 1) {  // (then j == i) the next diagonal tile: c - acc straight into sA
-          ldsBarrier();    // every wavefront has read its operands (sA may hold panel 2's L)
-          accSubToLds(sA, c, acc, t);
-          haveDiag = true;
-        } else {
-          storeTileSub(Cij, ld, c, acc, t);
-        }
-      }
-    }
-  }
-  __syncthreads();  // the L stores of the last steps are read back by the backward substitution
-  backSubstitute(P, w, S, ld, T, Linv, nz, sxDyn, sA, sy, t);
-}
-
 __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restrict__ Pp, int k) {
   const DevProblem& P = *Pp;
   const int item = P.chol_upd_begin[k] + blockIdx.x;
@@ -1022,7 +877,8 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
   const int w = it.x, i = it.y, j = it.z, mode = it.w;
   if (!cholSelect(P, w)) return;
   const int64_t ld = P.win_fpad[w];
-  double* S = P.S + P.win_soff[w];
+  const TileSrc cur = tileSrc(P, w, ld);
+  double* W = P.W + P.win_soff[w];
   double* work = P.fwdF + P.win_fwdoff[w];
   __shared__ double sA[kTile * kLd];
   __shared__ double sX[kTile * kLd];
@@ -1034,8 +890,8 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
   if (mode & 1) {
     // panels of step k: L_ik (and L_jk) = A (X_k)^T, operands staged in LDS
     loadTile(P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile, kTile, 0, 0, sX, t);
-    loadTile(S + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
-    if (j != i) loadTile(S + j * kTile * ld + k * kTile, ld, 0, 0, sB, t);
+    loadTile(cur.at(i, k, k), ld, 0, 0, sA, t);
+    if (j != i) loadTile(cur.at(j, k, k), ld, 0, 0, sB, t);
     if (i == j && t < kTile) sy[t] = work[k * kTile + t];
     const int row = t >> 2, q = t & 3;
     const double rhsOld = (i == j && q == 0) ? work[i * kTile + row] : 0.0;
@@ -1061,10 +917,10 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
     ldsBarrier();  // every wavefront has read A_ik / A_jk (LDS-only: the rhs store stays in flight)
     accToLds(sA, li, t);
     if (j != i) accToLds(sB, lj, t);
-    double* Cij = S + i * kTile * ld + j * kTile;
+    double* Cij = W + i * kTile * ld + j * kTile;
     dbl4 c[2][2];
-    loadC(Cij, ld, c, t);  // read of the read-modify-write overlaps the barrier and the MFMAs
-    if (i == j) storeTile<false>(S + k * kTile * ld + i * kTile, ld, 0, 0, li, t);  // L_ik -> upper slot (k,i)
+    loadC(cur.at(i, j, k), ld, c, t);  // read of the read-modify-write overlaps the barrier and the MFMAs
+    if (i == j) storeTile<false>(W + k * kTile * ld + i * kTile, ld, 0, 0, li, t);  // L_ik -> upper slot (k,i)
     ldsBarrier();  // no reader of the upper slot in this launch
     dbl4 acc[2][2];
     mfmaTileNT(sA, j == i ? sA : sB, acc, t);
@@ -1094,7 +950,7 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
     if (t < kTile) sy[t] = work[d * kTile + t];
   }
   __syncthreads();
-  if (!potrfTile<2>(S + d * kTile * ld + d * kTile, ld, P.Linv + P.win_linvoff[w] + (int64_t)d * kTile * kTile,
+  if (!potrfTile<2>(cur.at(d, d, d), ld, P.Linv + P.win_linvoff[w] + (int64_t)d * kTile * kTile,
                     work + d * kTile, sA, sX, sy, sRl, sFl, t, (mode & 1) != 0))
     if (t == 0) P.st[w].gn_failed = 1;
 }
@@ -1112,7 +968,7 @@ __global__ __launch_bounds__(kBsReal) void k_chol_bsub(const DevProblem* __restr
   if (!cholSelect(P, w)) return;
   const int64_t ld = P.win_fpad[w];
   const int T = (int)(ld / kTile);
-  const double* S = P.S + P.win_soff[w];
+  const double* S = P.W + P.win_soff[w];  // L in the upper slots of the working copy
   const double* work = P.fwdF + P.win_fwdoff[w];
   const double* Linv = P.Linv + P.win_linvoff[w];
   __shared__ double sA[32 * kTile];
@@ -1162,478 +1018,6 @@ __global__ __launch_bounds__(kBsReal) void k_chol_bsub(const DevProblem* __restr
 #endif
 }
 
-// ---- wave-specialised persistent schedule. A workgroup of 8 wavefronts holds two window slots
-// when there are more windows than CUs (pairs mode), else one window. The factor wavefront of a
-// window (diagonal LLT, X = L^-1, y_k, all in LDS) is wavefront 4s of its slot; the MFMA
-// wavefronts (panels, band updates, forward-substitution updates) are 4s+1..4s+3 in pairs mode
-// and 1,2,3,5,6,7 with one window. Wavefronts are placed on the SIMDs round-robin (w and w+4
-// share one), so factor wavefronts never share a SIMD with MFMA wavefronts: a stream of FP64
-// MFMAs starves a readlane/VALU chain on the same SIMD ~40x. The LDS request keeps this to one
-// workgroup per CU. Within a window the wavefronts hand over through LDS flags, so the
-// factorisation of tile k+1 runs while the MFMA wavefronts finish the rest of step k:
-//   factor  k: wait diagReady > k (S_kk in sF, rhs_k final in work) -> LLT in sF
-//              -> wait xFree >= k -> X_k into sX, y_k, z_k = X_k^T y_k -> xReady = k+1
-//   MFMA    k: wait xReady > k -> panel (k+1,k) -> update (k+1,k+1) into sF -> diagReady = k+2
-//              -> X_k to global, other panels of step k -> xFree = k+1 -> other band updates
-// Panels: L_ik = A_ik X_k^T, and the forward substitution rhs_i -= L_ik y_k is formed as
-// A_ik z_k from the A_ik fragments already in registers. The 16x16 output blocks of a tile (only
-// the 10 lower ones of a diagonal tile: its upper triangle is never read) are dealt round-robin
-// to the MFMA wavefronts, two per round; operands come straight from global memory (or LDS) in
-// the 16x16x4 layout with the inner index permuted per lane (lane group lk owns k = 16 lk ..
-// 16 lk + 15): each lane reads 128 contiguous bytes; the sum is unchanged.
-constexpr int kSlotThreads = 256;
-constexpr int kWsThreads = 2 * kSlotThreads;
-constexpr int kMaxBlocksPerWave = 6;     // 16 blocks over >= 3 MFMA wavefronts
-
-// The n-th output block of MFMA wavefront g (of ng) in a full (16 blocks) or lower (10 blocks)
-// tile; -1 past the end. Block bi is (bi >> 2, bi & 3).
-__device__ __forceinline__ int blockOf(bool lower, int g, int ng, int n) {
-  const int idx = g + ng * n;
-  if (!lower) return idx < 16 ? idx : -1;
-  // lower blocks (a >= b) in order: 0 4 5 8 9 10 12 13 14 15
-  if (idx >= 10) return -1;
-  const int a = idx < 1 ? 0 : idx < 3 ? 1 : idx < 6 ? 2 : 3;
-  const int b = idx - a * (a + 1) / 2;
-  return 4 * a + b;
-}
-
-// Two 16x16 output blocks bi0, bi1 (bi1 < 0: one block) of a 64x64 tile product:
-// acc[m] = A[16a..][0..63] B[16b..][0..63]^T. Rows come from global memory (row stride ld) or LDS
-// (row stride kLd), inner index permuted per lane group; both blocks' operands are loaded before
-// the MFMAs. With sz != nullptr also pz[m] = A[16a + (lane & 15)][.] . sz for blocks of column 0
-// (complete in lanes 0..15).
-template <bool ALDS, bool BLDS>
-__device__ __forceinline__ void gemmPair(const double* A, int lda, const double* B, int ldb, int bi0, int bi1,
-                                         dbl4 acc[2], const double* sz, double pz[2], int lane) {
-  const int lr = lane & 15, lk = lane >> 4;
-  const int bis[2] = {bi0, bi1};
-  double fa[2][16], fb[2][16];
-#pragma unroll
-  for (int m = 0; m < 2; ++m) {
-    const int bi = bis[m];
-    if (bi < 0) break;
-    const double* pa = A + (16 * (bi >> 2) + lr) * (ALDS ? kLd : lda) + 16 * lk;
-    const double* pb = B + (16 * (bi & 3) + lr) * (BLDS ? kLd : ldb) + 16 * lk;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (ALDS) {
-        fa[m][2 * u] = pa[2 * u];
-        fa[m][2 * u + 1] = pa[2 * u + 1];
-      } else {
-        const double2 v = *gmem(reinterpret_cast<const double2*>(pa + 2 * u));
-        fa[m][2 * u] = v.x;
-        fa[m][2 * u + 1] = v.y;
-      }
-      if (BLDS) {
-        fb[m][2 * u] = pb[2 * u];
-        fb[m][2 * u + 1] = pb[2 * u + 1];
-      } else {
-        const double2 v = *gmem(reinterpret_cast<const double2*>(pb + 2 * u));
-        fb[m][2 * u] = v.x;
-        fb[m][2 * u + 1] = v.y;
-      }
-    }
-  }
-#pragma unroll
-  for (int m = 0; m < 2; ++m) {
-    const int bi = bis[m];
-    if (bi < 0) break;
-    acc[m] = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[m] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[m][q], fb[m][q], acc[m], 0, 0, 0);
-    if (sz && (bi & 3) == 0) {
-      double d0 = 0.0, d1 = 0.0;
-#pragma unroll
-      for (int q = 0; q < 16; q += 2) {
-        d0 += fa[m][q] * sz[16 * lk + q];
-        d1 += fa[m][q + 1] * sz[16 * lk + q + 1];
-      }
-      double d = d0 + d1;
-      d += __shfl_xor(d, 16);
-      d += __shfl_xor(d, 32);
-      pz[m] = d;
-    }
-  }
-}
-__device__ __forceinline__ void storeBlock(double* C, int ld, int bi, const dbl4& acc, int lane) {
-  double* dst = C + (16 * (bi >> 2) + (lane >> 4)) * ld + 16 * (bi & 3) + (lane & 15);
-#pragma unroll
-  for (int reg = 0; reg < 4; ++reg) dst[4 * reg * ld] = acc[reg];
-}
-__device__ __forceinline__ dbl4 subFromBlock(const double* C, int ld, int bi, const dbl4& acc, int lane) {
-  const auto src = gmem(C + (16 * (bi >> 2) + (lane >> 4)) * ld + 16 * (bi & 3) + (lane & 15));
-  dbl4 r;
-#pragma unroll
-  for (int reg = 0; reg < 4; ++reg) r[reg] = src[4 * reg * ld] - acc[reg];
-  return r;
-}
-
-// Panel tile, compute part: acc[n] = (A_ik X^T) blocks of wavefront g and the rhs correction
-// rhs_i -= A_ik z (blocks (a, 0) carry the row products). L_ik overwrites A_ik only after every
-// wavefront has read A_ik (blocksStore after a barrier).
-__device__ __forceinline__ void panelCompute(const double* Aik, int ld, const double* sX, const double* sZ,
-                                             double* worki, dbl4 acc[kMaxBlocksPerWave], int g, int ng, int lane) {
-#pragma unroll
-  for (int n0 = 0; n0 < kMaxBlocksPerWave; n0 += 2) {
-    const int bi0 = blockOf(false, g, ng, n0), bi1 = blockOf(false, g, ng, n0 + 1);
-    if (bi0 < 0) break;
-    double pz[2];
-    gemmPair<false, true>(Aik, ld, sX, 0, bi0, bi1, acc + n0, sZ, pz, lane);
-    if ((bi0 & 3) == 0 && lane < 16) worki[16 * (bi0 >> 2) + lane] -= pz[0];
-    if (bi1 >= 0 && (bi1 & 3) == 0 && lane < 16) worki[16 * (bi1 >> 2) + lane] -= pz[1];
-  }
-}
-__device__ __forceinline__ void blocksStore(double* C, int ld, const dbl4 acc[kMaxBlocksPerWave], bool lower, int g,
-                                            int ng, int lane) {
-#pragma unroll
-  for (int n = 0; n < kMaxBlocksPerWave; ++n) {
-    const int bi = blockOf(lower, g, ng, n);
-    if (bi < 0) break;
-    storeBlock(C, ld, bi, acc[n], lane);
-  }
-}
-// Band update tile C -= Li Lj^T (all global; lower blocks only for a diagonal tile).
-__device__ __forceinline__ void updateBlocks(double* C, const double* Li, const double* Lj, int ld, bool lower, int g,
-                                             int ng, int lane) {
-#pragma unroll 1
-  for (int n0 = 0; n0 < kMaxBlocksPerWave; n0 += 2) {
-    const int bi0 = blockOf(lower, g, ng, n0), bi1 = blockOf(lower, g, ng, n0 + 1);
-    if (bi0 < 0) break;
-    dbl4 acc[2];
-    double pz[2];
-    gemmPair<false, false>(Li, ld, Lj, ld, bi0, bi1, acc, nullptr, pz, lane);
-    storeBlock(C, ld, bi0, subFromBlock(C, ld, bi0, acc[0], lane), lane);
-    if (bi1 >= 0) storeBlock(C, ld, bi1, subFromBlock(C, ld, bi1, acc[1], lane), lane);
-  }
-}
-
-// Band update tile C -= A B^T with both operands in LDS (row stride kLd).
-__device__ __forceinline__ void updateBlocksLds(double* C, int ld, const double* sA, const double* sB, bool lower, int g,
-                                                int ng, int lane) {
-#pragma unroll 1
-  for (int n0 = 0; n0 < kMaxBlocksPerWave; n0 += 2) {
-    const int bi0 = blockOf(lower, g, ng, n0), bi1 = blockOf(lower, g, ng, n0 + 1);
-    if (bi0 < 0) break;
-    dbl4 acc[2];
-    double pz[2];
-    gemmPair<true, true>(sA, 0, sB, 0, bi0, bi1, acc, nullptr, pz, lane);
-    storeBlock(C, ld, bi0, subFromBlock(C, ld, bi0, acc[0], lane), lane);
-    if (bi1 >= 0) storeBlock(C, ld, bi1, subFromBlock(C, ld, bi1, acc[1], lane), lane);
-  }
-}
-// 64x64 global tile -> LDS (row stride kLd) by the nthr threads gt = 0.. of the MFMA wavefronts.
-__device__ __forceinline__ void stageTile(double* dst, const double* src, int ld, int gt, int nthr) {
-  for (int e = gt; e < kTile * kTile / 2; e += nthr) {
-    const int r = e >> 5, c = 2 * (e & 31);
-    const double2 v = *gmem(reinterpret_cast<const double2*>(src + r * ld + c));
-    dst[r * kLd + c] = v.x;
-    dst[r * kLd + c + 1] = v.y;
-  }
-}
-
-// Diagonal tile on the factor wavefront, all in LDS: sF holds S_kk on entry and L_kk on exit;
-// X = L_kk^-1 -> sX (after xFree >= xFreeNeed); y = X r (r: this lane's rhs row) -> sYk;
-// z = X^T y -> sZ. Blocked LLT with 16-column readlane panels and MFMA trailing updates;
-// blockwise inverse as in potrfTile. Returns false (uniformly) at a non-positive pivot.
-__device__ __forceinline__ bool potrfWave(double* sF, double* sX, double* sRl, double* sYk, double* sZ, double r,
-                                       int* xFree, int xFreeNeed, int* fail, int lane) {
-  CLK_INIT
-  const bool clk = lane == 0;
-  // sX is still read by the MFMA wavefronts (X_{k-1}) during the sweep: the 8x8 diagonal inverse
-  // blocks are stashed in the unused upper triangle of sF (block s at rows 8s.., columns 8s+8..;
-  // the last one at rows 40.., columns 56..) and moved to sX after xFree
-#pragma unroll 1
-  for (int s = 0; s < 8; ++s) {
-    double* xd = s < 7 ? sF + 8 * s * kLd + 8 * s + 8 : sF + 40 * kLd + 56;
-    if (!subPanel8(sF, xd, sRl, 8 * s, lane)) return false;
-    __builtin_amdgcn_wave_barrier();
-    CLKW(4, clk)
-    if (s < 7) trailing8(sF, 8 * s, 0, 1, lane);
-    __builtin_amdgcn_wave_barrier();
-    CLKW(5, clk)
-  }
-  if (!waitFlag(xFree, xFreeNeed, fail)) return false;  // X_{k-1}, z_{k-1} no longer read
-  CLKW(6, clk)
-#pragma unroll 8
-  for (int u = 0; u < 64; ++u) {
-    const int e = lane + 64 * u;
-    const int row = e >> 6, col = e & 63, sb = row >> 3;
-    // diagonal 8x8 blocks from the stash, zero elsewhere
-    const double* xd = sb < 7 ? sF + 8 * sb * kLd + 8 * sb + 8 : sF + 40 * kLd + 56;
-    sX[row * kLd + col] = (col >> 3) == sb ? xd[(row & 7) * kLd + (col & 7)] : 0.0;
-  }
-  __builtin_amdgcn_wave_barrier();
-  CLKW(7, clk)
-  for (int q = 0; q < 4; ++q) {  // X21 = -X22 (L21 X11) of diagonal block q; lane = (row m, column j)
-    const int m = lane >> 3, j = lane & 7, b = 16 * q;
-    double t = 0.0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) t += sF[(b + 8 + m) * kLd + b + k] * sX[(b + k) * kLd + b + j];
-    sX[(b + 8 + m) * kLd + b + j] = t;
-    __builtin_amdgcn_wave_barrier();
-    double tk[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) tk[k] = sX[(b + 8 + k) * kLd + b + j];
-    double v = 0.0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v += sX[(b + 8 + m) * kLd + b + 8 + k] * tk[k];
-    __builtin_amdgcn_wave_barrier();
-    sX[(b + 8 + m) * kLd + b + j] = -v;
-  }
-  __builtin_amdgcn_wave_barrier();
-  CLKW(8, clk)
-  for (int d = 1; d < 4; ++d)
-    for (int j = 0; j + d < 4; ++j) {
-      const int i = j + d;
-      dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
-      for (int m = j; m < i; ++m)
-        mfma16<1>(sF + 16 * i * kLd + 16 * m, kLd, sX + 16 * m * kLd + 16 * j, kLd, 1, 1.0, acc, lane);
-      double* Xij = sX + 16 * i * kLd + 16 * j;
-      storeC16(Xij, kLd, acc, lane);
-      __builtin_amdgcn_wave_barrier();
-      dbl4 x = dbl4{0.0, 0.0, 0.0, 0.0};
-      mfma16<1>(sX + 16 * i * kLd + 16 * i, kLd, Xij, kLd, 1, -1.0, x, lane);
-      __builtin_amdgcn_wave_barrier();
-      storeC16(Xij, kLd, x, lane);
-      __builtin_amdgcn_wave_barrier();
-    }
-  CLKW(9, clk)
-  // y = X r, z = X^T y (X is stored with its zero upper triangle: full-length unpredicated sums,
-  // so the LDS reads pipeline)
-  sYk[lane] = r;
-  __builtin_amdgcn_wave_barrier();
-  double y4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 16
-  for (int j = 0; j < kTile; ++j) y4[j & 3] += sX[lane * kLd + j] * sYk[j];
-  const double y = (y4[0] + y4[1]) + (y4[2] + y4[3]);
-  __builtin_amdgcn_wave_barrier();
-  sYk[lane] = y;
-  __builtin_amdgcn_wave_barrier();
-  double z4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 16
-  for (int i = 0; i < kTile; ++i) z4[i & 3] += sX[i * kLd + lane] * sYk[i];
-  const double z = (z4[0] + z4[1]) + (z4[2] + z4[3]);
-  sZ[lane] = z;
-  __builtin_amdgcn_wave_barrier();
-  CLKW(10, clk)
-  return true;
-}
-
-// Backward substitution on one slot (4 wavefronts, slot-local barriers): x = L^-T y with y in sx
-// (LDS) on entry and x there on exit; then x -> yF.
-__device__ void backSubstituteSlot(const DevProblem& P, int w, const double* S, int ld, int T, const double* Linv,
-                                   const uint8_t* nz, double* sx, double* sA, double* sy, int* bar, int& gen, int t) {
-  const int col = t & 63, q = t >> 6;
-  for (int I = T - 1; I >= 0; --I) {
-    double acc = 0.0;
-    for (int i = I + 1; i < T; ++i) {
-      if (!nz[i * T + I]) continue;
-      const double* Lt = S + i * kTile * ld + I * kTile + col;
-      double v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = Lt[(q + 4 * u) * ld];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) acc += v[u] * sx[i * kTile + q + 4 * u];
-    }
-    const double* Li = Linv + I * kTile * kTile + col;
-    double li[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) li[u] = Li[(q + 4 * u) * kTile];
-    sA[q * kTile + col] = acc;
-    waveBarrier(bar, gen, 4, t & 63);
-    if (t < kTile) sy[t] = sx[I * kTile + t] - ((sA[t] + sA[kTile + t]) + (sA[2 * kTile + t] + sA[3 * kTile + t]));
-    waveBarrier(bar, gen, 4, t & 63);
-    double a = 0.0;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) a += (q + 4 * u >= col) ? li[u] * sy[q + 4 * u] : 0.0;
-    sA[256 + q * kTile + col] = a;
-    waveBarrier(bar, gen, 4, t & 63);
-    if (t < kTile)
-      sx[I * kTile + t] = (sA[256 + t] + sA[256 + kTile + t]) + (sA[256 + 2 * kTile + t] + sA[256 + 3 * kTile + t]);
-    waveBarrier(bar, gen, 4, t & 63);
-  }
-  const int fdim = P.win_fdim[w];
-  for (int e = t; e < fdim; e += kSlotThreads) P.yF[(size_t)P.win_foff[w] + e] = sx[e];
-}
-
-__global__ __launch_bounds__(kWsThreads, 2) void k_cholesky_ws(const DevProblem* __restrict__ Pp, int pairs) {
-  const DevProblem& P = *Pp;
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-  // roles: slot, factor wavefront or MFMA wavefront g of ng
-  const int slot = pairs ? wid >> 2 : 0;
-  const bool isF = pairs ? (wid & 3) == 0 : wid == 0;
-  const int ng = pairs ? 3 : 6;
-  const int g = pairs ? (wid & 3) - 1 : (wid < 4 ? wid - 1 : wid - 2);
-  const int t = tid - slot * kSlotThreads;  // thread index within the slot (bsub: waves 0..3)
-  __shared__ double sFs[2][kTile * kLd];
-  __shared__ double sXs[2][kTile * kLd];
-  __shared__ double sRls[2][kTile];
-  __shared__ double sZs[2][kTile];
-  __shared__ WsFlags fls[2];
-  extern __shared__ double sxDyn[];  // per slot: y, then x (max_fpad doubles)
-  if (tid < 2) fls[tid] = WsFlags{0, 0, 0, 0, 0, 0};
-  __syncthreads();  // the only workgroup-wide barrier: from here on a slot never waits on the other
-  const int w = pairs ? 2 * blockIdx.x + slot : blockIdx.x;
-  if ((!pairs && wid == 4) || w >= P.n_win || !cholSelect(P, w)) return;
-  double* sF = sFs[slot];
-  double* sX = sXs[slot];
-  double* sRl = sRls[slot];
-  double* sZ = sZs[slot];
-  WsFlags& fl = fls[slot];
-  double* sy = sxDyn + slot * P.max_fpad;
-  const int ld = (int)P.win_fpad[w];
-  const int T = ld / kTile;
-  double* S = P.S + P.win_soff[w];
-  double* Linv = P.Linv + P.win_linvoff[w];
-  double* work = P.fwdF + P.win_fwdoff[w];
-  const uint8_t* nz = P.tile_nz + P.win_tnzoff[w];
-  int sgen = 0;
-  CLK_INIT
-  const bool fClk = blockIdx.x == 0 && slot == 0 && isF && lane == 0, gClk = slot == 0 && g == 0 && lane == 0;
-  if (isF) {
-    // ------------------------------------------------------------------ factor wavefront
-    for (int k = 0; k < T; ++k) {
-      CLKW(18, fClk)
-      if (!waitFlag(&fl.diagReady, k + 1, &fl.fail)) break;
-      CLKW(19, fClk)
-      const double r = work[k * kTile + lane];  // rhs_k, corrected by the MFMA wavefronts
-      if (!potrfWave(sF, sX, sRl, sy + k * kTile, sZ, r, &fl.xFree, k, &fl.fail, lane)) {
-        if (lane == 0) {
-          ldsRelease(&fl.fail, 1);
-          P.st[w].gn_failed = 1;
-        }
-        break;
-      }
-      CLKW(20, fClk)
-      if (lane == 0) ldsRelease(&fl.xReady, k + 1);
-    }
-  } else {
-    // ------------------------------------------------------------------ MFMA wavefronts
-    const int gt = 64 * g + lane;
-    int gen = 0;
-    {
-      const int fdim = P.win_fdim[w];
-      const double* rhs0 = P.rhsF + P.win_foff[w];
-      for (int e = gt; e < ld; e += 64 * ng) work[e] = e < fdim ? rhs0[e] : 0.0;
-    }
-    for (int e = gt; e < kTile * kTile; e += 64 * ng) sF[(e >> 6) * kLd + (e & 63)] = S[(e >> 6) * ld + (e & 63)];
-    waveBarrier(&fl.gbar, gen, ng, lane);
-    if (gt == 0) ldsRelease(&fl.diagReady, 1);
-    for (int k = 0; k < T; ++k) {
-      CLKW(21, gClk)
-      if (!waitFlag(&fl.xReady, k + 1, &fl.fail)) break;
-      CLKW(22, gClk)
-      const bool more = k + 1 < T;
-      const bool has1 = more && nz[(k + 1) * T + k];
-      double* Sd = S + (k + 1) * kTile * ld + (k + 1) * kTile;  // S_{k+1,k+1}
-      dbl4 acc[kMaxBlocksPerWave];
-      if (has1) {  // L_{k+1,k}: staged in sF now, over A_{k+1,k} once every wavefront has read it
-        panelCompute(S + (k + 1) * kTile * ld + k * kTile, ld, sX, sZ, work + (k + 1) * kTile, acc, g, ng, lane);
-        blocksStore(sF, kLd, acc, false, g, ng, lane);
-      }
-      CLKW(23, gClk)
-      waveBarrier(&fl.gbar, gen, ng, lane);
-      CLKW(24, gClk)
-      if (has1) {  // S_{k+1,k+1} - L L^T (lower blocks) -> sF (L staged in sF)
-        blocksStore(S + (k + 1) * kTile * ld + k * kTile, ld, acc, false, g, ng, lane);
-#pragma unroll
-        for (int n0 = 0; n0 < 4; n0 += 2) {  // <= 4 of the 10 lower blocks per wavefront
-          const int bi0 = blockOf(true, g, ng, n0), bi1 = blockOf(true, g, ng, n0 + 1);
-          if (bi0 < 0) break;
-          double pzd[2];
-          gemmPair<true, true>(sF, 0, sF, 0, bi0, bi1, acc + n0, nullptr, pzd, lane);
-          acc[n0] = subFromBlock(Sd, ld, bi0, acc[n0], lane);
-          if (bi1 >= 0) acc[n0 + 1] = subFromBlock(Sd, ld, bi1, acc[n0 + 1], lane);
-        }
-        waveBarrier(&fl.gbar, gen, ng, lane);  // every block has read L from sF
-        blocksStore(sF, kLd, acc, true, g, ng, lane);
-      } else if (more) {
-        for (int e = gt; e < kTile * kTile; e += 64 * ng) sF[(e >> 6) * kLd + (e & 63)] = Sd[(e >> 6) * ld + (e & 63)];
-      }
-      CLKW(25, gClk)
-      waveBarrier(&fl.gbar, gen, ng, lane);
-      CLKW(24, gClk)
-      if (gt == 0) ldsRelease(&fl.diagReady, k + 2);
-      // X_k -> global (backward substitution)
-      for (int e = gt; e < kTile * kTile / 2; e += 64 * ng) {
-        const int row = e >> 5, c = 2 * (e & 31);
-        *reinterpret_cast<double2*>(Linv + k * kTile * kTile + row * kTile + c) =
-            double2{sX[row * kLd + c], sX[row * kLd + c + 1]};
-      }
-      for (int i = k + 2; i < T; ++i) {
-        if (!nz[i * T + k]) continue;
-        panelCompute(S + i * kTile * ld + k * kTile, ld, sX, sZ, work + i * kTile, acc, g, ng, lane);
-        waveBarrier(&fl.gbar, gen, ng, lane);  // A_ik fully read
-        blocksStore(S + i * kTile * ld + k * kTile, ld, acc, false, g, ng, lane);
-      }
-      CLKW(26, gClk)
-      waveBarrier(&fl.gbar, gen, ng, lane);
-      CLKW(24, gClk)
-      if (gt == 0) ldsRelease(&fl.xFree, k + 1);
-      if (pairs) {
-        for (int i = k + 1; i < T; ++i) {
-          if (!nz[i * T + k]) continue;
-          for (int j = k + 1; j <= i; ++j) {
-            if (!nz[j * T + k] || (i == k + 1 && j == k + 1)) continue;
-            updateBlocks(S + i * kTile * ld + j * kTile, S + i * kTile * ld + k * kTile, S + j * kTile * ld + k * kTile,
-                         ld, i == j, g, ng, lane);
-          }
-        }
-      } else {
-        // one window per workgroup: the idle slot's LDS stages the operands (L_ik once per row)
-        double* stA = sFs[1];
-        double* stB = sXs[1];
-        for (int i = k + 1; i < T; ++i) {
-          if (!nz[i * T + k]) continue;
-          bool staged = false;
-          for (int j = k + 1; j <= i; ++j) {
-            if (!nz[j * T + k] || (i == k + 1 && j == k + 1)) continue;
-            if (!staged) {
-              stageTile(stA, S + i * kTile * ld + k * kTile, ld, gt, 64 * ng);
-              staged = true;
-            }
-            if (j != i) stageTile(stB, S + j * kTile * ld + k * kTile, ld, gt, 64 * ng);
-            waveBarrier(&fl.gbar, gen, ng, lane);
-            updateBlocksLds(S + i * kTile * ld + j * kTile, ld, stA, j == i ? stA : stB, i == j, g, ng, lane);
-            waveBarrier(&fl.gbar, gen, ng, lane);  // stB (and stA after the row) free again
-          }
-        }
-      }
-      CLKW(27, gClk)
-      waveBarrier(&fl.gbar, gen, ng, lane);
-      CLKW(24, gClk)
-    }
-  }
-  if (!pairs && wid > 4) return;  // MFMA wavefronts 5..7: done (the backward substitution uses 0..3)
-  CLKW(28, fClk || gClk)
-  waveBarrier(&fl.sbar, sgen, 4, lane);
-  CLKW(29, gClk)
-  if (ldsAcquire(&fl.fail)) return;
-  backSubstituteSlot(P, w, S, ld, T, Linv, nz, sy, sF, sX, &fl.sbar, sgen, t);  // sF / sX reused as scratch
-  CLKW(30, gClk)
-#ifdef OKG_CHOL_CLOCK
-  if (blockIdx.x == 0 && slot == 0 && t == 0)
-    printf("WSPOTRF pfac %llu ptrail %llu waitXFree %llu zeroX %llu dinv %llu subd %llu yz %llu\n", g_cholClk[4],
-           g_cholClk[5], g_cholClk[6], g_cholClk[7], g_cholClk[8], g_cholClk[9], g_cholClk[10]);
-  if (blockIdx.x == 0 && slot == 0 && t == 64)
-    printf("WSCLK T=%d F: waitDiag %llu potrf %llu | G: waitX %llu p1 %llu bar %llu upd1 %llu panels %llu upds %llu bsub %llu (x10ns)\n",
-           T, g_cholClk[19], g_cholClk[20], g_cholClk[22], g_cholClk[23], g_cholClk[24], g_cholClk[25], g_cholClk[26],
-           g_cholClk[27], g_cholClk[30]);
-#endif
-}
-
-bool cholesky_ws_fits(int max_fpad, size_t lds_per_block) {
-  hipFuncAttributes attr;
-  if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky_ws)) != hipSuccess) return false;
-  return attr.sharedSizeBytes + 2 * sizeof(double) * (size_t)max_fpad <= lds_per_block;
-}
-
-bool cholesky_wide_fits(int max_fpad, size_t lds_per_block) {
-  hipFuncAttributes attr;
-  if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky_wide)) != hipSuccess) return false;
-  return attr.sharedSizeBytes + sizeof(double) * (size_t)max_fpad <= lds_per_block;
-}
-
 bool cholesky_persistent_fits(int max_fpad, size_t lds_per_block) {
   hipFuncAttributes attr;
   if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky)) != hipSuccess) return false;
@@ -1644,17 +1028,6 @@ void launch_cholesky(const DevProblem& P, hipStream_t s) {
   if (P.n_win == 0) return;
   if (P.chol_schedule == 1) {
     hipLaunchKernelGGL(k_cholesky, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
-    return;
-  }
-  if (P.chol_schedule == 4) {
-    hipLaunchKernelGGL(k_cholesky_wide, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
-    return;
-  }
-  if (P.chol_schedule == 3) {
-    // two windows per workgroup once there are more windows than CUs (set by the runtime)
-    const int pairs = P.chol_pairs;
-    const int nb = pairs ? (P.n_win + 1) / 2 : P.n_win;
-    hipLaunchKernelGGL(k_cholesky_ws, dim3(nb), dim3(kWsThreads), 2 * sizeof(double) * P.max_fpad, s, P.self, pairs);
     return;
   }
   hipLaunchKernelGGL(k_chol_diag, dim3(P.n_win), dim3(256), 0, s, P.self, 0);

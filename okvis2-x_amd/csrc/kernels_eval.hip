@@ -228,13 +228,6 @@ __device__ __forceinline__ void applyF(const double* F, const double* v, double*
   for (int r = 9; r < 15; ++r) out[r] = v[r];
 }
 
-__device__ __forceinline__ double pick9(const double* v, int l) {  // v[l] for l < 9, register selects
-  double x = v[0];
-#pragma unroll
-  for (int e = 1; e < 9; ++e) x = (l == e) ? v[e] : x;
-  return x;
-}
-
 __device__ __forceinline__ double groupSum(double v) {  // sum over the 16 lanes of a group
   v += __shfl_xor(v, 8, 64);
   v += __shfl_xor(v, 4, 64);

@@ -11,7 +11,7 @@
 //   k_imu_hess    one wavefront per IMU factor: J^T J (packed) and J^T r of its 15x30 Jacobian.
 //   k_fgrad       one wavefront per f-block (pose / speed-bias): unscaled gradient and
 //                 diag(H_ff), and at iteration 0 the Jacobi scaling 1/(1+sqrt(diag)).
-//   k_zero_S      clears the structurally non-zero tiles of S (padded diagonal = 1).
+//   k_zero_S      clears the structurally non-zero tiles of S (padded diagonal = 1), once per build.
 //   k_assemble_pp one wavefront per pose-pose block pair (i >= j): 8 groups of 6 lanes (one per
 //                 row) sum fixed, interleaved subsets of the pair's contributions — visits,
 //                 landmark pairs (the Y_i U_j^T Schur terms), IMU / prior J^T J sub-blocks — and
@@ -758,13 +758,10 @@ __device__ __forceinline__ bool gnSelect(const DevProblem& P, int w) {
 }
 
 // Clears the structurally non-zero tiles of S (kZeroTiles consecutive tiles per workgroup; padded
-// diagonal = 1). Zero tiles are never written by the factorisation and stay zero from the initial
-// arena clear. Each tile's record and window are loaded before any test, 16-byte stores.
-//   tail = 0: the windows about to assemble (gnSelect; solve start and the eager paths);
-//   tail = 1: every window not done, launched after the candidate's cost reduction of the captured
-//             iteration, beside the linearisation: S is dead from there on (a rejected step reuses
-//             the stored GN step, a failed factorisation retries after a fresh assembly), so the
-//             next iteration's assembly finds it clear and the clear is off the critical path.
+// diagonal = 1). Since round 4 the factorisation works in W and never writes S, and the assembly
+// overwrites its blocks every iteration, so S is cleared once per build (mode 2: every window,
+// no state test) instead of every iteration. Modes 0 (windows about to assemble) and 1 (every
+// window not done) are kept for the eager entry points' semantics.
 constexpr int kZeroTiles = 4;  // (one per workgroup below kManyWindows windows: latency)
 __global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ Pp, int per, int tail) {
   const DevProblem& P = *Pp;
@@ -778,7 +775,7 @@ __global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ P
     const int fpad = gmem(P.win_fpad)[w], fdim = gmem(P.win_fdim)[w];
     const int64_t soff = gmem(P.win_soff)[w];
     asm volatile("" ::"v"(fpad), "v"(fdim), "v"(soff));
-    if ((sDone != 0) | (sNeed == 0) | (sFail != 0)) continue;  // uniform
+    if (tail != 2 && ((sDone != 0) | (sNeed == 0) | (sFail != 0))) continue;  // uniform
     double* S = P.S + soff;
     for (int e = threadIdx.x; e < kTile * kTile / 2; e += 256) {
       const int rl = e >> 5, cl = 2 * (e & 31);
@@ -1192,7 +1189,6 @@ void launch_assemble(const DevProblem& P, hipStream_t s) {
 }
 void launch_gn_reduce(const DevProblem& P, hipStream_t s) {
   launch_lm_prep(P, s);
-  launch_zero_S(P, s);
   launch_assemble(P, s);
 }
 void launch_gn_finalize(const DevProblem& P, hipStream_t s) {

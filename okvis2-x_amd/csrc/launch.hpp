@@ -41,11 +41,8 @@ void launch_gn_finalize(const DevProblem& P, hipStream_t s);
 
 // dense factorisation + both triangular solves, one persistent workgroup per window
 // (kernels_chol.hip)
-// wave-specialised Cholesky: does its LDS (static + 2 windows' solve vectors) fit a workgroup?
-bool cholesky_ws_fits(int max_fpad, size_t lds_per_block);
+// persistent Cholesky: does its LDS (static + the window's solve vector) fit a workgroup?
 bool cholesky_persistent_fits(int max_fpad, size_t lds_per_block);
-constexpr int kCholWidePanels = 3;  // panel tiles per step the wide persistent Cholesky handles (2 in LDS by DMA)
-bool cholesky_wide_fits(int max_fpad, size_t lds_per_block);
 void launch_cholesky(const DevProblem& P, hipStream_t s);
 
 // trust-region control (kernels_control.hip)

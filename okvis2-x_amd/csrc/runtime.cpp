@@ -150,6 +150,8 @@ struct HostBatch {
   int64_t s_total = 0, linv_total = 0, fwd_total = 0;
   std::vector<std::vector<uint8_t>> tileNz;
   std::vector<uint8_t> tile_nz;
+  std::vector<std::vector<int16_t>> tileFu;
+  std::vector<int16_t> tile_fu;
   std::vector<int64_t> win_tnzoff;
   std::vector<int> tileT;
   int f_total = 0;
@@ -905,6 +907,17 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
           if (nz[(size_t)i * T + k])
             for (int j = k + 1; j <= i; ++j)
               if (nz[(size_t)j * T + k]) nz[(size_t)i * T + j] = 1;
+      // first band update of every tile (a step k < j with L_ik and L_jk non-zero): until then the
+      // factorisation reads the tile from the assembled S, afterwards from its working copy W
+      std::vector<int16_t> fu((size_t)T * T, kNoUpdate);
+      for (int i = 0; i < T; ++i)
+        for (int j = 0; j <= i; ++j)
+          for (int k = 0; k < j; ++k)
+            if (nz[(size_t)i * T + k] && nz[(size_t)j * T + k]) {
+              fu[(size_t)i * T + j] = (int16_t)k;
+              break;
+            }
+      B.tileFu.push_back(fu);
       B.tileNz.push_back(nz);
       B.tileT.push_back(T);
     }
@@ -995,6 +1008,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
   for (int w = 0; w < B.n_win; ++w) {
     B.win_tnzoff.push_back((int64_t)B.tile_nz.size());
     B.tile_nz.insert(B.tile_nz.end(), B.tileNz[w].begin(), B.tileNz[w].end());
+    B.tile_fu.insert(B.tile_fu.end(), B.tileFu[w].begin(), B.tileFu[w].end());
     const int T = B.tileT[w];
     for (int k = 0; k < T; ++k) {
       int np = 0;
@@ -1143,10 +1157,16 @@ struct okvisgpu_ctx {
   hipGraphExec_t iterGraph = nullptr;
   int cuCount = 256;
   size_t ldsPerBlock = 65536;
-  bool wsFits() const { return cholesky_ws_fits(P.max_fpad, ldsPerBlock); }
   bool persistentFits() const { return cholesky_persistent_fits(P.max_fpad, ldsPerBlock); }
-  static constexpr bool kAutoWide = false;  // schedule 4 picked automatically (pending its A/B)
-  bool wideFits() const { return B.max_panels <= kCholWidePanels && cholesky_wide_fits(P.max_fpad, ldsPerBlock); }
+  // S is cleared by the build's arena memset; its padded diagonal (rows >= fdim) is set once per
+  // build before the first factorisation (k_zero_S setup mode). The factorisation works in W and
+  // the assembly overwrites its blocks, so S needs no clearing per iteration.
+  bool sNeedsInit = true;
+  void ensureS(hipStream_t s) {
+    if (!sNeedsInit) return;
+    launch_zero_S(P, s, 2);
+    sNeedsInit = false;
+  }
   bool haveProblem = false;
   // split-solve state
   bool inSolve = false;
@@ -1454,13 +1474,14 @@ struct okvisgpu_ctx {
     const size_t o_pw = upl(B.pair_win), o_pfi = upl(B.pair_fi), o_pfj = upl(B.pair_fj), o_pcb = upl(B.pair_cbegin),
                  o_pc = upl(B.pair_contrib);
     const size_t o_pruns = upl(B.pair_runs);
-    const size_t o_tnz = upl(B.tile_nz), o_tnzoff = upl(B.win_tnzoff);
+    const size_t o_tnz = upl(B.tile_nz), o_tnzoff = upl(B.win_tnzoff), o_tfu = upl(B.tile_fu);
     const size_t o_app = upl(B.asm_pp_items), o_asb = upl(B.asm_sb_items), o_appl = upl(B.asm_ppl_items);
     const size_t o_ti = upl(B.tile_items);
     const size_t o_cpi = upl(B.chol_panel_items), o_cpb = upl(B.chol_panel_begin), o_cui = upl(B.chol_upd_items),
                  o_cub = upl(B.chol_upd_begin);
     const size_t nf = std::max(1, B.f_total), nl3 = std::max<size_t>(1, (size_t)3 * D.n_lm);
     const size_t o_S = scratch(sizeof(double) * std::max<int64_t>(1, B.s_total));
+    const size_t o_W = scratch(sizeof(double) * std::max<int64_t>(1, B.s_total));
     const size_t o_Linv = scratch(sizeof(double) * std::max<int64_t>(1, B.linv_total));
     const size_t o_fwd = scratch(sizeof(double) * std::max<int64_t>(1, B.fwd_total));
     size_t of[10], ol[7];
@@ -1501,6 +1522,7 @@ struct okvisgpu_ctx {
     }
     if (A.size) HIPCHK(hipMemcpyAsync(base, hostStage, A.size, hipMemcpyHostToDevice, stream));
     HIPCHK(hipMemsetAsync(base + upSize, 0, AS.size, stream));
+    sNeedsInit = true;
     auto place = [&](size_t off) { return (off & kScratchTag) ? upSize + (off & ~kScratchTag) : off; };
     auto dp = [&](size_t off) { return reinterpret_cast<double*>(base + place(off)); };
     auto ip = [&](size_t off) { return reinterpret_cast<int32_t*>(base + place(off)); };
@@ -1554,19 +1576,20 @@ struct okvisgpu_ctx {
     D.pair_contrib = reinterpret_cast<const Contrib*>(base + place(o_pc));
     D.pair_runs = ip(o_pruns);
     D.tile_nz = reinterpret_cast<const uint8_t*>(base + place(o_tnz));
+    D.tile_fu = reinterpret_cast<const int16_t*>(base + place(o_tfu));
     D.win_tnzoff = reinterpret_cast<const int64_t*>(base + place(o_tnzoff));
     D.chol_panel_items = ip(o_cpi); D.chol_panel_begin = ip(o_cpb);
     D.chol_upd_items = ip(o_cui); D.chol_upd_begin = ip(o_cub);
     D.h_panel_begin = B.chol_panel_begin.data();
     D.h_upd_begin = B.chol_upd_begin.data();
     D.chol_schedule = 1;
-    D.chol_pairs = 0;
     D.asm_pp_items = ip(o_app); D.asm_sb_items = ip(o_asb);
     D.n_asm_pp = (int)B.asm_pp_items.size(); D.n_asm_sb = (int)B.asm_sb_items.size();
     D.asm_ppl_items = ip(o_appl); D.n_asm_ppl = (int)B.asm_ppl_items.size();
     D.tile_items = ip(o_ti);
     D.n_tiles = (int)(B.tile_items.size() / 3);
     D.S = dp(o_S);
+    D.W = dp(o_W);
     D.Linv = dp(o_Linv);
     D.win_linvoff = lp(o_wlinv);
     D.fwdF = dp(o_fwd);
@@ -1608,17 +1631,12 @@ struct okvisgpu_ctx {
     d.min_lm_diagonal = o.min_lm_diagonal;
     d.max_lm_diagonal = o.max_lm_diagonal;
     // Cholesky schedule (measured on MI355X, S50 windows, round 3: bench window-it/s of schedules
-    // 1 / 2 / 3 at 16: 20.3k / 24.6k / 18.6k, 64: 64.5k / 70.9k / 58.6k, 128: 102.2k / 92.8k / 92.6k,
-    // 192: 129.1k / 109.1k / 116.5k, 256: 155.6k / - / 140.4k, 2,048: 189.9k / - / 153.5k): below
-    // half a window per CU the tile-parallel launches spread each window over many CUs; from there
-    // the persistent kernel. The wave-specialised kernel no longer wins anywhere since the
-    // persistent kernel's sub-panel look-ahead; it stays selectable (cholesky_schedule = 3).
-    // Up to one window per CU the persistent kernel runs as the wide variant (schedule 4: one
-    // workgroup per CU anyway, so its extra LDS costs no occupancy; round 3, 256 S50 windows).
-    int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 4 ? o.cholesky_schedule : 0;
-    if (sched == 0) sched = 2 * P.n_win >= cuCount ? (kAutoWide && P.n_win <= cuCount && wideFits() ? 4 : 1) : 2;
-    if (sched == 4 && !wideFits()) sched = 1;
-    if (sched == 3 && !wsFits()) sched = 2;
+    // 1 / 2 at 16: 20.3k / 24.6k, 64: 64.5k / 70.9k, 128: 102.2k / 92.8k, 192: 129.1k / 109.1k):
+    // below half a window per CU the tile-parallel launches spread each window over many CUs; from
+    // there the persistent kernel. (A wave-specialised kernel and a persistent variant with the
+    // panel tiles in LDS were measured slower at every batch size and removed in round 4.)
+    int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 2 ? o.cholesky_schedule : 0;
+    if (sched == 0) sched = 2 * P.n_win >= cuCount ? 1 : 2;
     // the persistent kernel keeps the window's rhs / y in dynamic LDS next to its static tiles:
     // a reduced dimension beyond what fits falls back to the tile-parallel launches
     if (sched == 1 && !persistentFits()) sched = 2;
@@ -1627,7 +1645,6 @@ struct okvisgpu_ctx {
       iterGraph = nullptr;
     }
     P.chol_schedule = sched;
-    P.chol_pairs = P.n_win > cuCount ? 1 : 0;
     uploadDescriptor();
   }
 
@@ -1736,7 +1753,6 @@ struct okvisgpu_ctx {
 
   void launchIteration() {
     launch_lm_prep(P, stream);
-    launch_zero_S(P, stream, 0);
     launch_assemble(P, stream);
     launch_cholesky(P, stream);
     launch_gn_backsub(P, stream);
@@ -1798,10 +1814,6 @@ struct okvisgpu_ctx {
     join(side[0]);
     join(side[1]);
     launch_reduce(P, R_COST_CAND, stream);
-    // S is dead once the step is decided: cleared for the next iteration's assembly beside the
-    // linearisation (k_zero_S tail mode; solve_begin clears it for the first iteration)
-    fork(side[2]);
-    launch_zero_S(P, side[2], 1);
     // linearisation at the accepted point
     fork(side[0]);
     launch_imu_hess(P, 1, side[0]);
@@ -1809,7 +1821,6 @@ struct okvisgpu_ctx {
     join(side[0]);
     launch_fgrad(P, 1, stream);
     launch_gradnorm(P, 1, stream);
-    join(side[2]);
   }
 
   void ensureGraph() {
@@ -2005,7 +2016,7 @@ int okvisgpu_solve_begin(okvisgpu_ctx* c, const okvisgpu_options* o) {
     c->dropGraph();  // options are baked into the captured kernel arguments
     c->uploadParams();
     c->resetStates(1e-8);
-    launch_zero_S(c->P, c->stream, 0);  // the first iteration's S (the forked graph clears it at its end)
+    c->ensureS(c->stream);
     c->launchInit(2);
     c->failInitialHostEvaluations();
     c->ensureGraph();
@@ -2123,7 +2134,7 @@ int okvisgpu_profile_iteration(okvisgpu_ctx* c, double* ms) {
     };
     mark(-1);
     launch_lm_prep(P, s); mark(0);
-    launch_zero_S(P, s); mark(1);
+    mark(1);  // (S is no longer cleared per iteration: phase kept for the ABI's phase list)
     launch_assemble(P, s); mark(2);
     launch_cholesky(P, s); mark(3);
     launch_gn_finalize(P, s); mark(5);
@@ -2269,8 +2280,8 @@ int okvisgpu_time_kernel(okvisgpu_ctx* c, int32_t kernel, int32_t reps, double* 
         case K_JV: timed([&] { launch_jv(P, s); }); break;
         case K_LM_BACKSUB: timed([&] { launch_lm_backsub(P, s); }); break;
         case K_FGRAD: timed([&] { launch_fgrad(P, 1, s); }); break;
-        case K_CHOLESKY:  // needs a freshly assembled S each repetition
-          launch_zero_S(P, s);
+        case K_CHOLESKY:  // (the factorisation reads the assembled S and works in W: repeatable)
+          c->ensureS(s);
           launch_assemble(P, s);
           timed([&] { launch_cholesky(P, s); });
           break;

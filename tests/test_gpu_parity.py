@@ -365,12 +365,11 @@ def test_kernel_timing_hook(og, gpu_ctx):
 
 
 def test_cholesky_schedules_agree(og, oracle, gpu_ctx):
-    """The persistent per-window, the tile-parallel and the wide persistent (panel tiles in LDS)
-    Cholesky schedules run the same tile operations in the same order: bitwise-equal solves, all
-    matching the oracle."""
+    """The persistent per-window and the tile-parallel Cholesky schedules run the same tile
+    operations in the same order: bitwise-equal solves, both matching the oracle."""
     ws = [og.SynthWindow(10, 500, 4000, seed=s) for s in (31, 32)]
     res = []
-    for sched in (1, 2, 3, 4):
+    for sched in (1, 2):
         for w in ws:
             w.reset()
         opts = og.default_options(max_num_iterations=5, function_tolerance=0.0, gradient_tolerance=0.0,
@@ -379,18 +378,12 @@ def test_cholesky_schedules_agree(og, oracle, gpu_ctx):
         s = gpu_ctx.solve(opts, len(ws))
         res.append((s, [w.poses().copy() for w in ws]))
     for k in range(len(ws)):
-        for r in (1, 3):
-            assert res[0][0][k]["final_cost"] == res[r][0][k]["final_cost"]
-            assert np.array_equal(res[0][1][k], res[r][1][k])
+        assert res[0][0][k]["final_cost"] == res[1][0][k]["final_cost"]
+        assert np.array_equal(res[0][1][k], res[1][1][k])
     ws[0].reset()
     so = oracle.solve(ws[0].problem_ptr(), og.default_options(max_num_iterations=5, function_tolerance=0.0,
                                                               gradient_tolerance=0.0, parameter_tolerance=0.0))
     _close(res[1][0][0], so)
-    # wave-specialised schedule: same factorisation, different summation order inside the tiles
-    for k in range(len(ws)):
-        assert res[2][0][k]["final_cost"] == pytest.approx(res[0][0][k]["final_cost"], rel=1e-9)
-        np.testing.assert_allclose(res[2][1][k], res[0][1][k], rtol=0, atol=1e-7)
-    _close(res[2][0][0], so)
 
 
 def test_graph_file_solve_parity(og, oracle, gpu_ctx, tmp_path):
