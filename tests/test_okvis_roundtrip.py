@@ -63,7 +63,7 @@ def _zero_tol(og, iters):
                               parameter_tolerance=0.0)
 
 
-def _read_dump(path, p, n_solves):
+def _read_dump(og, path, p, n_solves):
     per = 4 + 7 * p.n_poses + 9 * p.n_speed_biases + 4 * p.n_landmarks + 526 * p.n_imu
     d = np.fromfile(path, dtype=np.float64)
     assert d.size == per * n_solves, (d.size, per)
@@ -71,7 +71,8 @@ def _read_dump(path, p, n_solves):
     for k in range(n_solves):
         x = d[k * per:(k + 1) * per]
         o = 4
-        rec = {"initial_cost": x[0], "final_cost": x[1], "num_iterations": int(x[2]), "termination": int(x[3])}
+        rec = {"initial_cost": x[0], "final_cost": x[1], "num_iterations": int(x[2]),
+               "termination": og.TERMINATION.get(int(x[3]), "?")}
         for name, n in (("poses", 7 * p.n_poses), ("sb", 9 * p.n_speed_biases), ("lm", 4 * p.n_landmarks),
                         ("states", 526 * p.n_imu)):
             rec[name] = x[o:o + n]
@@ -101,7 +102,7 @@ def test_okvis_objects_roundtrip_gpu(exe, og, oracle, tmp_path, parity):
     assert "okvis_roundtrip gpu ok" in r.stdout
     w = _window(og)
     p = w.problem
-    gpu = _read_dump(dump_path, p, len(ITERS))
+    gpu = _read_dump(og, dump_path, p, len(ITERS))
     sb_begin = np.ctypeslib.as_array(p.imu_sample_begin, shape=(p.n_imu + 1,))
     assert np.diff(sb_begin).min() >= 50  # every factor on the >= 50-sample arm
     imu_blocks = np.ctypeslib.as_array(p.imu_blocks, shape=(p.n_imu, 4))
