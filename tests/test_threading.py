@@ -51,7 +51,9 @@ def _bitwise(a, b, what):
 
 @pytest.mark.gpu
 def test_two_graphs_concurrently(og, oracle, parity):
-    rt = OwnedProblem.copy_of(og.SynthWindow(50, 2000, 16000, seed=20251015).problem)
+    sw = og.SynthWindow(50, 2000, 16000, seed=20251015)  # (kept alive while its arrays are copied)
+    rt = OwnedProblem.copy_of(sw.problem)
+    del sw
     fg, gps, _ = gps_window(seed=9, n_kf=200, n_lm=8000, n_obs=64000)
     graphs = {"realtime": Graph(og, rt, _opts(og, 10, num_threads=3)),
               "full": Graph(og, fg, _opts(og, 3, num_threads=3, linear_solver=og.SPARSE_NORMAL_CHOLESKY))}
