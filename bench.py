@@ -317,8 +317,10 @@ def single_window(og, cfg, opts, args, device):
     c1.synchronize()
     b = time.perf_counter()
     s1 = c1.solve_end()[0]
+    st1 = c1.stats()
     out = {"iters_per_s": args.steps / (b - a), "ms_per_iter": (b - a) / args.steps * 1e3,
-           "final_cost": s1["final_cost"]}
+           "final_cost": s1["final_cost"], "cholesky_launches": st1["cholesky_launches"],
+           "s_tiles_nonzero": st1["s_tiles_nonzero"]}
     gpu_pose = w1[0].poses().copy()
     gt_p, _, _ = w1[0].ground_truth()
     e2e = []

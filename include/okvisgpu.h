@@ -402,7 +402,7 @@ int okvisgpu_graph_save(const okvisgpu_problem* p, const int64_t* state_t_ns, co
  * layout figures bench.py's roofline work model needs). Sums over all windows. */
 typedef struct okvisgpu_problem_stats {
   int32_t n_windows;
-  int32_t reserved_;
+  int32_t cholesky_launches;        /* launches of the tile-parallel factorisation (roots + steps) */
   int64_t n_poses, n_speed_biases, n_landmarks, n_landmarks_free, n_extrinsics_free;
   int64_t n_observations, n_visits, n_imu, n_imu_samples, n_pose_priors, n_sb_priors, n_relpose;
   int64_t reduced_dim;              /* sum of the reduced (Schur) dimensions                      */

@@ -244,6 +244,8 @@ struct DevProblem {
   const int32_t* fb_kind;          // 0 pose / 1 sb
   const int32_t* fb_index;         // global pose / sb index
   const int32_t* fb_off;           // offset in the window's f-vector
+  const int32_t* win_sgap;         // [n_win][2] f offset and length of the gap rows of a nested-
+                                   // dissection order (identity rows of S, zero rhs; 0 0: none)
   const int32_t* fb_cbegin;        // [n_fblock+1] gradient / diagonal contributions (C_VISIT, C_IMU, priors)
   const Contrib* fb_contrib;
   const int32_t* asm_pp_items;      // pose-pose pairs, one per wavefront, XCD-grouped order (-1 = pad)
@@ -269,13 +271,14 @@ struct DevProblem {
   // window is block-banded and LLT creates no fill outside its envelope, so only structurally
   // non-zero 64x64 tiles are zeroed, factored and updated (bitwise identical to the dense LLT).
   const int32_t* tile_items;         // (w, i, j) every structurally non-zero tile (i >= j)
-  // tile-parallel schedule (few windows): per step k, the panel tiles (w, i) and the band updates
-  // (w, i, j) of all windows; begin offsets per k, host copies for the launch sizes
-  const int32_t* chol_panel_items;
-  const int32_t* chol_panel_begin;
+  // tile-parallel schedule (few windows; runtime.cpp cholSchedule): launch 0 factors the root tiles
+  // (w, d, first root of the window), launch l >= 1 runs the band-update items (w, i, j,
+  // mode | k << 8) scheduled there; begin offsets per launch, host copy for the launch sizes
+  const int32_t* chol_root_items;
+  int32_t n_chol_roots;
+  int32_t n_chol_launches;
   const int32_t* chol_upd_items;
   const int32_t* chol_upd_begin;
-  const int32_t* h_panel_begin;
   const int32_t* h_upd_begin;
   int32_t chol_schedule;             // 1 persistent per window, 2 tile-parallel (host-resolved)
   const uint8_t* tile_nz;            // per window T x T (row-major) structural non-zero flags of L

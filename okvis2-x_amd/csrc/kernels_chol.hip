@@ -454,13 +454,7 @@ __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li,
   // applies each sub-panel's rank-8 update to the next sub-panel's 8 columns itself (VALU, its own
   // row); wavefronts 1-3 apply it to the columns beyond (matrix cores) and form the 8x8 inverse
   // blocks, one sub-panel behind, handing over through LDS flags.
-#ifdef OKG_FACTOR_PRIO  // (A/B knob: the whole factoring workgroup ahead of the co-resident one)
-  __builtin_amdgcn_s_setprio(OKG_FACTOR_PRIO);
-#endif
   if (wave == 0) {
-#ifdef OKG_CHAIN_PRIO  // (A/B knob: issue priority of the sweep wavefront over co-resident waves)
-    __builtin_amdgcn_s_setprio(OKG_CHAIN_PRIO);
-#endif
     const int i = lane;
     double xp[8];
 #pragma unroll
@@ -526,9 +520,6 @@ __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li,
       }
     }
   }
-#if defined(OKG_CHAIN_PRIO) || defined(OKG_FACTOR_PRIO)
-  __builtin_amdgcn_s_setprio(0);
-#endif
   ldsBarrier();
   CLK(5)
   if (sFl[2]) return false;
@@ -824,37 +815,50 @@ __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem
 #endif
 }
 
-// ---- tile-parallel schedule (few windows: spreads each window over many CUs). One launch per
-// step k over all windows' band updates of that step; every workgroup forms the panels it needs
-// itself (L_ik = A_ik X_k^T from the final A_ik and the stored X_k), so no launch sits between the
-// diagonal factor and the updates. A_ik stays in place during the step (other workgroups of the
-// same launch still read it): the workgroup of the diagonal update (i,i) writes L_ik to the
-// unused upper slot (k,i) of S and applies rhs_i -= L_ik y_k; the backward substitution of this
-// schedule reads L there. The workgroup of tile (k+1,k+1) factors it right after its update.
-__global__ __launch_bounds__(256) void k_chol_diag(const DevProblem* __restrict__ Pp, int k) {
+// ---- tile-parallel schedule (few windows: spreads each window over many CUs; runtime.cpp
+// cholSchedule). Launch 0 factors the root tiles (no band update writes them: the first tile of
+// each independent part of a nested-dissection order); launch l >= 1 runs the band updates of the
+// steps scheduled there over all windows. Every workgroup forms the panels it needs itself
+// (L_ik = A_ik X_k^T from the final A_ik and the stored X_k), so no launch sits between a diagonal
+// factor and its updates. A_ik stays in place during the step (other workgroups of the same launch
+// still read it): the workgroup of the diagonal update (i,i) writes L_ik to the unused upper slot
+// (k,i) of W and applies rhs_i -= L_ik y_k; the backward substitution of this schedule reads L
+// there. The workgroup of a diagonal tile's last update factors it right after.
+__global__ __launch_bounds__(256) void k_chol_roots(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
-  const int w = blockIdx.x;
+  const int w = P.chol_root_items[3 * blockIdx.x], d = P.chol_root_items[3 * blockIdx.x + 1];
+  const bool first = P.chol_root_items[3 * blockIdx.x + 2] != 0;
   if (!cholSelect(P, w)) return;
   const int64_t ld = P.win_fpad[w];
   const int T = (int)(ld / kTile);
-  if (k >= T) return;
   const TileSrc cur = tileSrc(P, w, ld);
   double* work = P.fwdF + P.win_fwdoff[w];
+  const uint8_t* nz = P.tile_nz + P.win_tnzoff[w];
   __shared__ double sA[kTile * kLd];
   __shared__ double sX[kTile * kLd];
   __shared__ double sy[2 * kTile];
   __shared__ double sRl[kTile];
   __shared__ int sFl[4];
   const int t = threadIdx.x;
-  if (k == 0) {
-    const int fdim = P.win_fdim[w];
-    for (int e = t; e < ld; e += 256) work[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
-    __syncthreads();
+  // the window's rhs into its work vector: each root item its own block row, the first one also
+  // every block row that is not a root (read from launch 1 on)
+  const int fdim = P.win_fdim[w];
+  const double* rhs = P.rhsF + P.win_foff[w];
+  for (int e = t; e < ld; e += 256) {
+    const int b = e / kTile;
+    bool mine = b == d;
+    if (first && b != d) {
+      bool root = true;  // (a root is a diagonal tile with no non-zero tile left of it)
+      for (int q = 0; q < b && root; ++q) root = !nz[b * T + q];
+      mine = !root;
+    }
+    if (mine) work[e] = e < fdim ? rhs[e] : 0.0;
   }
-  if (t < kTile) sy[t] = work[k * kTile + t];
   __syncthreads();
-  if (!potrfTile<1>(cur.at(k, k, k), ld, P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile,
-                    work + k * kTile, sA, sX, sy, sRl, sFl, t, false))
+  if (t < kTile) sy[t] = work[d * kTile + t];
+  __syncthreads();
+  if (!potrfTile<1>(cur.at(d, d, d), ld, P.Linv + P.win_linvoff[w] + (int64_t)d * kTile * kTile,
+                    work + d * kTile, sA, sX, sy, sRl, sFl, t, false))
     if (t == 0) P.st[w].gn_failed = 1;
 }
 
@@ -870,11 +874,11 @@ __device__ __forceinline__ void accToLds(double* s, const dbl4 acc[2][2], int t)
       for (int reg = 0; reg < 4; ++reg) s[(r0 + 16 * a + (lane >> 4) + 4 * reg) * kLd + c0 + 16 * b + (lane & 15)] = acc[a][b][reg];
 }
 
-__global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restrict__ Pp, int k) {
+__global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restrict__ Pp, int launch) {
   const DevProblem& P = *Pp;
-  const int item = P.chol_upd_begin[k] + blockIdx.x;
+  const int item = P.chol_upd_begin[launch] + blockIdx.x;
   const int4 it = reinterpret_cast<const int4*>(P.chol_upd_items)[item];
-  const int w = it.x, i = it.y, j = it.z, mode = it.w;
+  const int w = it.x, i = it.y, j = it.z, mode = it.w & 0xff, k = it.w >> 8;
   if (!cholSelect(P, w)) return;
   const int64_t ld = P.win_fpad[w];
   const TileSrc cur = tileSrc(P, w, ld);
@@ -887,7 +891,8 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
   __shared__ double sRl[kTile];
   __shared__ int sFl[4];
   const int t = threadIdx.x;
-  if (mode & 1) {
+  // (every item updates; bit 1: tile (i,i)'s last update, which factors it afterwards)
+  {
     // panels of step k: L_ik (and L_jk) = A (X_k)^T, operands staged in LDS
     loadTile(P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile, kTile, 0, 0, sX, t);
     loadTile(cur.at(i, k, k), ld, 0, 0, sA, t);
@@ -925,8 +930,8 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
     dbl4 acc[2][2];
     mfmaTileNT(sA, j == i ? sA : sB, acc, t);
     if (mode & 2) {
-      // tile (k+1,k+1): the updated S_dd goes straight to LDS for the factor (its global copy is
-      // stale from here on and never read), and so does rhs_d
+      // tile (i,i) after its last update: straight to LDS for the factor (its global copy is stale
+      // from here on and never read), and so is rhs_i
       ldsBarrier();  // every wavefront has read L_ik from sA
       const int wave = t >> 6, lane = t & 63;
       const int r0 = 32 * (wave >> 1), cq = 32 * (wave & 1);
@@ -944,14 +949,10 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
     }
   }
   if (!(mode & 2)) return;
-  const int d = k + 1;
-  if (!(mode & 1)) {  // factor-only item: S_dd and rhs_d from global (written by earlier launches)
-    __syncthreads();
-    if (t < kTile) sy[t] = work[d * kTile + t];
-  }
+  const int d = i;
   __syncthreads();
   if (!potrfTile<2>(cur.at(d, d, d), ld, P.Linv + P.win_linvoff[w] + (int64_t)d * kTile * kTile,
-                    work + d * kTile, sA, sX, sy, sRl, sFl, t, (mode & 1) != 0))
+                    work + d * kTile, sA, sX, sy, sRl, sFl, t, true))
     if (t == 0) P.st[w].gn_failed = 1;
 }
 
@@ -1030,10 +1031,10 @@ void launch_cholesky(const DevProblem& P, hipStream_t s) {
     hipLaunchKernelGGL(k_cholesky, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
     return;
   }
-  hipLaunchKernelGGL(k_chol_diag, dim3(P.n_win), dim3(256), 0, s, P.self, 0);
-  for (int k = 0; k < P.max_tiles; ++k) {
-    const int nu = P.h_upd_begin[k + 1] - P.h_upd_begin[k];
-    if (nu > 0) hipLaunchKernelGGL(k_chol_update, dim3(nu), dim3(256), 0, s, P.self, k);
+  hipLaunchKernelGGL(k_chol_roots, dim3(P.n_chol_roots), dim3(256), 0, s, P.self);
+  for (int l = 1; l < P.n_chol_launches; ++l) {
+    const int nu = P.h_upd_begin[l + 1] - P.h_upd_begin[l];
+    if (nu > 0) hipLaunchKernelGGL(k_chol_update, dim3(nu), dim3(256), 0, s, P.self, l);
   }
   hipLaunchKernelGGL(k_chol_bsub, dim3(P.n_win), dim3(kBsReal),
                      sizeof(double) * P.max_fpad + sizeof(int) * (1 + kBsPre) * P.max_tiles + P.max_tiles * P.max_tiles, s,

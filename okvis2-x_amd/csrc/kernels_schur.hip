@@ -11,7 +11,7 @@
 //   k_imu_hess    one wavefront per IMU factor: J^T J (packed) and J^T r of its 15x30 Jacobian.
 //   k_fgrad       one wavefront per f-block (pose / speed-bias): unscaled gradient and
 //                 diag(H_ff), and at iteration 0 the Jacobi scaling 1/(1+sqrt(diag)).
-//   k_zero_S      clears the structurally non-zero tiles of S (padded diagonal = 1), once per build.
+//   k_zero_S      clears the structurally non-zero tiles of S (padding / gap diagonal = 1), once per build.
 //   k_assemble_pp one wavefront per pose-pose block pair (i >= j): 8 groups of 6 lanes (one per
 //                 row) sum fixed, interleaved subsets of the pair's contributions — visits,
 //                 landmark pairs (the Y_i U_j^T Schur terms), IMU / prior J^T J sub-blocks — and
@@ -773,14 +773,16 @@ __global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ P
     const auto gst = gmem(P.st + w);
     const int sDone = gst->done, sNeed = gst->need_gn | tail, sFail = gst->gn_failed & (tail ^ 1);
     const int fpad = gmem(P.win_fpad)[w], fdim = gmem(P.win_fdim)[w];
+    const int g0 = gmem(P.win_sgap)[2 * w], g1 = g0 + gmem(P.win_sgap)[2 * w + 1];
     const int64_t soff = gmem(P.win_soff)[w];
-    asm volatile("" ::"v"(fpad), "v"(fdim), "v"(soff));
+    asm volatile("" ::"v"(fpad), "v"(fdim), "v"(g0), "v"(g1), "v"(soff));
     if (tail != 2 && ((sDone != 0) | (sNeed == 0) | (sFail != 0))) continue;  // uniform
     double* S = P.S + soff;
     for (int e = threadIdx.x; e < kTile * kTile / 2; e += 256) {
       const int rl = e >> 5, cl = 2 * (e & 31);
       const int r = ti * kTile + rl, c = tj * kTile + cl;
-      const double2 v{(r == c && r >= fdim) ? 1.0 : 0.0, (r == c + 1 && r >= fdim) ? 1.0 : 0.0};
+      const bool unit = r >= fdim || (r >= g0 && r < g1);  // padding and gap rows: identity
+      const double2 v{(r == c && unit) ? 1.0 : 0.0, (r == c + 1 && unit) ? 1.0 : 0.0};
       *gmemw(reinterpret_cast<double2*>(S + (int64_t)r * fpad + c)) = v;
     }
   }

@@ -13,6 +13,7 @@
 #include <array>
 #include <cfloat>
 #include <chrono>
+#include <climits>
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
@@ -141,10 +142,18 @@ struct HostBatch {
   std::vector<int32_t> win_pose_range, win_sb_range, win_lm_range, win_obs_range, win_imu_range, win_pp_range,
       win_sbp_range, win_rp_range;
   std::vector<int32_t> fb_win, fb_kind, fb_index, fb_off, fb_cbegin;
+  // S offset of every f-block: fb_off, plus the window's gap rows after the left part of a
+  // nested-dissection order (win_sgap: f offset of the gap, gap length; 0 0 without one); natural
+  // index of every f entry (-1: gap row) and natural dimension per window
+  std::vector<int32_t> win_sgap, f_nat, win_fnat;
+  bool nd = false;  // order the windows' states for the tile-parallel schedule (nested dissection)
+  std::vector<int32_t> chol_root_items;  // (w, d, first-root-of-window flag): tiles no update writes
+  int n_chol_launches = 1;
   std::vector<Contrib> fb_contrib;
   std::vector<int32_t> pair_win, pair_fi, pair_fj, pair_cbegin, pair_runs;
   std::vector<int32_t> asm_pp_items, asm_sb_items, asm_ppl_items;
-  std::vector<int32_t> chol_panel_items, chol_panel_begin, chol_upd_items, chol_upd_begin, tile_items;
+  std::vector<int32_t> chol_upd_items, chol_upd_begin, tile_items;
+  int64_t n_panels = 0;  // structurally non-zero tiles below the diagonal (panel products)
   int64_t n_band_updates = 0;
   std::vector<Contrib> pair_contrib;
   int64_t s_total = 0, linv_total = 0, fwd_total = 0;
@@ -268,6 +277,105 @@ std::chrono::steady_clock::time_point g_alast;
 #endif
 
 // Build the batch. `constOverride` carries okvisgpu_set_block_constant() edits.
+// ---- tile-level symbolic factorisation and the tile-parallel launch schedule -------------------
+// Fill of LLT inside the envelope, on the tile pattern nz (T x T, lower triangle).
+void symbolicFill(std::vector<uint8_t>& nz, int T) {
+  for (int k = 0; k < T; ++k)
+    for (int i = k + 1; i < T; ++i)
+      if (nz[(size_t)i * T + k])
+        for (int j = k + 1; j <= i; ++j)
+          if (nz[(size_t)j * T + k]) nz[(size_t)i * T + j] = 1;
+}
+// Launch schedule of the tile-parallel factorisation for a window's (filled) tile pattern: step k's
+// band updates (tiles (i, j), k < j <= i, L_ik and L_jk non-zero) run in launch L[k] >= 1; launch 0
+// factors the root tiles (those no update writes); any other tile is factored by the workgroup of
+// its last update, so step k starts one launch after that; no tile is written by two updates of
+// one launch. last[] holds each tile's last update launch (-1: none). For a block-banded pattern
+// this is launch k + 1 for step k (the pre-round-4 schedule); for a nested-dissection order the
+// independent parts share launches. Returns the number of launches.
+int cholSchedule(const std::vector<uint8_t>& nz, int T, std::vector<int>& L, std::vector<int>& last) {
+  L.assign(T, 0);
+  last.assign((size_t)T * T, -1);
+  int n = 1;
+  for (int k = 0; k < T; ++k) {
+    int lk = std::max(1, last[(size_t)k * T + k] + 1);
+    bool any = false;
+    for (int i = k + 1; i < T; ++i)
+      if (nz[(size_t)i * T + k])
+        for (int j = k + 1; j <= i; ++j)
+          if (nz[(size_t)j * T + k]) {
+            lk = std::max(lk, last[(size_t)i * T + j] + 1);
+            any = true;
+          }
+    L[k] = lk;
+    if (!any) continue;
+    for (int i = k + 1; i < T; ++i)
+      if (nz[(size_t)i * T + k])
+        for (int j = k + 1; j <= i; ++j)
+          if (nz[(size_t)j * T + k]) last[(size_t)i * T + j] = lk;
+    n = std::max(n, lk + 1);
+  }
+  return n;
+}
+inline int pad64(int x) { return (x + kTile - 1) / kTile * kTile; }
+// One level of nested dissection of a window's state slots (few windows: the latency of a solve is
+// the chain of the tile-parallel launches). Slots [0, a) (left) and [b, n) (right) share no factor
+// once the separator [a, b) is eliminated last: order left | right | separator, left padded to a
+// tile boundary in S, so the two parts factor as independent chains. dim[u] = f scalars of slot u,
+// reach[u] = largest slot coupled to u (landmarks seen from both, IMU links, edges, host factors).
+// The split is chosen on the launch count of the estimated tile pattern (interval couplings);
+// returns {-1, -1} unless it saves two launches or more with at most one tile more.
+std::pair<int, int> chooseNd(const std::vector<int>& dim, const std::vector<int>& reach) {
+  const int n = (int)dim.size();
+  auto estimate = [&](int a, int b, int& tiles) {
+    std::vector<int> order;
+    for (int u = 0; u < a; ++u) order.push_back(u);
+    for (int u = b; u < n; ++u) order.push_back(u);
+    for (int u = a; u < b; ++u) order.push_back(u);
+    std::vector<int> off(n, 0);
+    int o = 0;
+    for (int t = 0; t < n; ++t) {
+      if (t == a && a > 0 && a < n) o = pad64(o);
+      off[order[t]] = o;
+      o += dim[order[t]];
+    }
+    const int T = std::max(1, pad64(o) / kTile);
+    tiles = T;
+    std::vector<uint8_t> nz((size_t)T * T, 0);
+    for (int i = 0; i < T; ++i) nz[(size_t)i * T + i] = 1;
+    for (int u = 0; u < n; ++u) {
+      if (!dim[u]) continue;
+      for (int v = u; v <= reach[u]; ++v) {
+        if (!dim[v]) continue;
+        for (int ti = off[u] / kTile; ti <= (off[u] + dim[u] - 1) / kTile; ++ti)
+          for (int tj = off[v] / kTile; tj <= (off[v] + dim[v] - 1) / kTile; ++tj)
+            nz[(size_t)std::max(ti, tj) * T + std::min(ti, tj)] = 1;
+      }
+    }
+    symbolicFill(nz, T);
+    std::vector<int> L, last;
+    return cholSchedule(nz, T, L, last);
+  };
+  int t0 = 0;
+  const int base = estimate(0, 0, t0);
+  std::vector<int> pm(n + 1, -1);
+  for (int u = 0; u < n; ++u) pm[u + 1] = std::max(pm[u], reach[u]);
+  int best = base, ba = -1, bb = -1;
+  const int stride = n > 64 ? n / 32 : 1;
+  for (int a = std::max(1, n > 64 ? n / 4 : 1); a < (n > 64 ? 3 * n / 4 : n - 1); a += stride) {
+    const int b = std::max(a, pm[a] + 1);
+    if (b >= n) continue;
+    int t = 0;
+    const int lv = estimate(a, b, t);
+    if (t <= t0 + 1 && lv < best) {
+      best = lv;
+      ba = a;
+      bb = b;
+    }
+  }
+  return best <= base - 2 ? std::make_pair(ba, bb) : std::make_pair(-1, -1);
+}
+
 void analyse(const std::vector<const okvisgpu_problem*>& probs,
              const std::map<std::tuple<int, int, int>, int>& constOverride, HostBatch& B) {
   B.seg_gbegin.push_back(0);
@@ -415,12 +523,78 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       hfix[h] = allConst;
       B.hf.push_back(F);
     }
-    // f-blocks in the reduced ordering: pose i, then speed/bias i
+    // f-blocks in the reduced ordering: pose i, then speed/bias i, state slot by slot; for the
+    // tile-parallel schedule (few windows) possibly in a nested-dissection order of the slots
     std::vector<int> posef(npx, -1), sbf(p->n_speed_biases, -1), poseFb(npx, -1), sbFb(p->n_speed_biases, -1);
     int fo = 0;
     const int nmax = std::max(p->n_poses, p->n_speed_biases);
     const int fbBase = (int)B.fb_win.size();
-    for (int i = 0; i < nmax; ++i) {
+    std::vector<int> slotOrder(nmax);
+    std::iota(slotOrder.begin(), slotOrder.end(), 0);
+    int ndLeft = 0;  // slots of the left part (0: natural order)
+    const bool extFree = std::any_of(pa.begin() + np, pa.end(), [](uint8_t a) { return a != 0; });
+    if (B.nd && !extFree && nmax >= 8) {  // (variable extrinsics couple every state: no split)
+      std::vector<int> dim(nmax, 0), reach(nmax);
+      for (int i = 0; i < nmax; ++i) {
+        dim[i] = (i < p->n_poses && pa[i] ? 6 : 0) + (i < p->n_speed_biases && sa[i] ? 9 : 0);
+        reach[i] = i;
+      }
+      auto couple = [&](int lo, int hi) {
+        if (lo >= 0 && hi > lo) reach[lo] = std::max(reach[lo], hi);
+      };
+      {  // landmarks: the free poses observing a free landmark are coupled by its elimination
+        std::vector<int> lo(p->n_landmarks, INT_MAX), hi(p->n_landmarks, -1);
+        for (int o = 0; o < p->n_observations; ++o) {
+          const int l = p->obs_landmark[o], ps = p->obs_pose[o];
+          if (!la[l] || !pa[ps]) continue;
+          lo[l] = std::min(lo[l], ps);
+          hi[l] = std::max(hi[l], ps);
+        }
+        for (int l = 0; l < p->n_landmarks; ++l)
+          if (hi[l] >= 0) couple(lo[l], hi[l]);
+      }
+      auto coupleSet = [&](std::initializer_list<int> slots) {
+        int lo = INT_MAX, hi = -1;
+        for (int u : slots)
+          if (u >= 0) { lo = std::min(lo, u); hi = std::max(hi, u); }
+        if (hi >= 0) couple(lo, hi);
+      };
+      for (int f = 0; f < p->n_imu; ++f) {
+        const int* b = &p->imu_blocks[4 * f];
+        coupleSet({pa[b[0]] ? b[0] : -1, sa[b[1]] ? b[1] : -1, pa[b[2]] ? b[2] : -1, sa[b[3]] ? b[3] : -1});
+      }
+      for (int i = 0; i < p->n_relpose; ++i) {
+        const int a = p->relpose_blocks[2 * i], b = p->relpose_blocks[2 * i + 1];
+        coupleSet({a < np && pa[a] ? a : -1, b < np && pa[b] ? b : -1});
+      }
+      for (int h = 0; h < p->n_host; ++h) {
+        int lo = INT_MAX, hi = -1;
+        for (int k = 0; k < 4 && p->host_param_kind[4 * h + k] >= 0; ++k) {
+          const int kind = p->host_param_kind[4 * h + k], idx = p->host_param_index[4 * h + k];
+          const bool act = kind == 0 ? (idx < np && pa[idx]) : sa[idx] != 0;
+          if (act) { lo = std::min(lo, idx); hi = std::max(hi, idx); }
+        }
+        if (hi >= 0) couple(lo, hi);
+      }
+      const auto ab = chooseNd(dim, reach);
+      if (ab.first > 0) {
+        slotOrder.clear();
+        for (int u = 0; u < ab.first; ++u) slotOrder.push_back(u);
+        for (int u = ab.second; u < nmax; ++u) slotOrder.push_back(u);
+        for (int u = ab.first; u < ab.second; ++u) slotOrder.push_back(u);
+        ndLeft = ab.first;
+      }
+    }
+    // (nested dissection: the left part ends on a tile boundary; the gap rows between are identity
+    // rows of S with zero rhs, so the f-vector and S share one index)
+    int gapAt = 0, gap = 0;
+    for (int t = 0; t < nmax; ++t) {
+      const int i = slotOrder[t];
+      if (ndLeft && t == ndLeft) {
+        gapAt = fo;
+        fo = pad64(fo);
+        gap = fo - gapAt;
+      }
       if (i < p->n_poses && pa[i]) {
         posef[i] = fo;
         poseFb[i] = (int)B.fb_win.size();
@@ -443,13 +617,32 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       B.fb_win.push_back(w); B.fb_kind.push_back(0); B.fb_index.push_back(pb + i); B.fb_off.push_back(fo);
       fo += 6;
     }
-    B.win_ext_free.push_back(fo > 0 && std::any_of(pa.begin() + np, pa.end(), [](uint8_t a) { return a != 0; }));
+    B.win_ext_free.push_back(fo > 0 && extFree);
+    B.win_sgap.push_back(gap ? gapAt : 0);
+    B.win_sgap.push_back(gap);
+    // natural order of the f entries (pose i, speed/bias i slot by slot, then extrinsics: the order
+    // of okvisgpu_linearize_reduce's export and of the oracle)
+    {
+      std::vector<int32_t> nat(fo, -1);
+      int no = 0;
+      auto put = [&](int f, int n) {
+        for (int c = 0; c < n; ++c) nat[f + c] = no++;
+      };
+      for (int i = 0; i < nmax; ++i) {
+        if (i < p->n_poses && posef[i] >= 0) put(posef[i], 6);
+        if (i < p->n_speed_biases && sbf[i] >= 0) put(sbf[i], 9);
+      }
+      for (int c = 0; c < ncam; ++c)
+        if (posef[np + c] >= 0) put(posef[np + c], 6);
+      B.f_nat.insert(B.f_nat.end(), nat.begin(), nat.end());
+      B.win_fnat.push_back(no);
+    }
     for (int i = 0; i < npx; ++i) { B.pose_f.push_back(posef[i]); B.pose_active.push_back(pa[i]); }
     for (int i = 0; i < p->n_speed_biases; ++i) { B.sb_f.push_back(sbf[i]); B.sb_active.push_back(sa[i]); }
     std::vector<uint8_t> laNew(p->n_landmarks);
     for (int k = 0; k < p->n_landmarks; ++k) laNew[k] = la[perm[k]];
     for (int k = 0; k < p->n_landmarks; ++k) B.lm_free.push_back(laNew[k]);
-    const int fpad = ((fo + kTile - 1) / kTile) * kTile;
+    const int fpad = pad64(fo);  // S dimension (leading dimension of the window's S)
     B.win_foff.push_back(B.f_total);
     B.win_fdim.push_back(fo);
     B.win_fpad.push_back(fpad);
@@ -902,11 +1095,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
           for (int tj = B.fb_off[fb2] / kTile; tj <= (B.fb_off[fb2] + nb - 1) / kTile; ++tj)
             nz[(size_t)std::max(ti, tj) * T + std::min(ti, tj)] = 1;
       }
-      for (int k = 0; k < T; ++k)
-        for (int i = k + 1; i < T; ++i)
-          if (nz[(size_t)i * T + k])
-            for (int j = k + 1; j <= i; ++j)
-              if (nz[(size_t)j * T + k]) nz[(size_t)i * T + j] = 1;
+      symbolicFill(nz, T);
       // first band update of every tile (a step k < j with L_ik and L_jk non-zero): until then the
       // factorisation reads the tile from the assembled S, afterwards from its working copy W
       std::vector<int16_t> fu((size_t)T * T, kNoUpdate);
@@ -943,32 +1132,46 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       B.pair_contrib.insert(B.pair_contrib.end(), kv.second.begin(), kv.second.end());
     }
   }
-  // per-panel work lists over the whole batch
-  const int maxT = B.max_fpad / kTile;
-  for (int k = 0; k <= maxT; ++k) {
-    B.chol_panel_begin.push_back((int)B.chol_panel_items.size() / 2);
-    B.chol_upd_begin.push_back((int)B.chol_upd_items.size() / 4);
-    if (k == maxT) break;
+  // tile-parallel schedule (cholSchedule): launch 0 factors every window's root tiles; launch
+  // l >= 1 runs the band updates of the steps scheduled there, each item (w, i, j, mode | k << 8):
+  // mode bit 0 = update of tile (i, j) by step k (panels formed from X_k), bit 1 = factor tile
+  // i (= j) afterwards (the item is its last update)
+  {
+    std::vector<std::vector<int32_t>> byLaunch(1);
     for (int w = 0; w < B.n_win; ++w) {
       const int T = B.tileT[w];
       const auto& nz = B.tileNz[w];
-      for (int i = k + 1; i < T; ++i)
-        if (nz[(size_t)i * T + k]) { B.chol_panel_items.push_back(w); B.chol_panel_items.push_back(i); }
-      // band updates of step k; the workgroup updating tile (k+1,k+1) then factors it (mode bit 1),
-      // or a factor-only item is added when step k does not touch that tile
-      auto push = [&](int i, int j, int mode) {
-        B.chol_upd_items.push_back(w); B.chol_upd_items.push_back(i);
-        B.chol_upd_items.push_back(j); B.chol_upd_items.push_back(mode);
-      };
-      if (k + 1 < T && !nz[(size_t)(k + 1) * T + k]) push(k + 1, k + 1, 2);
-      for (int i = k + 1; i < T; ++i)
-        if (nz[(size_t)i * T + k])
-          for (int j = k + 1; j <= i; ++j)
-            if (nz[(size_t)j * T + k]) {
-              push(i, j, (i == k + 1 && j == k + 1) ? 3 : 1);
-              ++B.n_band_updates;
-            }
+      std::vector<int> L, last;
+      const int nl = cholSchedule(nz, T, L, last);
+      B.n_chol_launches = std::max(B.n_chol_launches, nl);
+      if ((int)byLaunch.size() < nl) byLaunch.resize(nl);
+      bool first = true;
+      for (int d = 0; d < T; ++d)
+        if (last[(size_t)d * T + d] < 0) {
+          B.chol_root_items.push_back(w);
+          B.chol_root_items.push_back(d);
+          B.chol_root_items.push_back(first ? 1 : 0);
+          first = false;
+        }
+      for (int k = 0; k < T; ++k)
+        for (int i = k + 1; i < T; ++i)
+          if (nz[(size_t)i * T + k]) ++B.n_panels;
+      for (int k = 0; k < T; ++k)
+        for (int i = k + 1; i < T; ++i)
+          if (nz[(size_t)i * T + k])
+            for (int j = k + 1; j <= i; ++j)
+              if (nz[(size_t)j * T + k]) {
+                const bool fac = i == j && last[(size_t)i * T + i] == L[k];
+                auto& v = byLaunch[L[k]];
+                v.push_back(w); v.push_back(i); v.push_back(j); v.push_back((fac ? 3 : 1) | (k << 8));
+                ++B.n_band_updates;
+              }
     }
+    for (size_t l = 0; l < byLaunch.size(); ++l) {
+      B.chol_upd_begin.push_back((int)B.chol_upd_items.size() / 4);
+      B.chol_upd_items.insert(B.chol_upd_items.end(), byLaunch[l].begin(), byLaunch[l].end());
+    }
+    B.chol_upd_begin.push_back((int)B.chol_upd_items.size() / 4);
   }
   // assembly work lists: pose-pose pairs (one wavefront each, 4 per workgroup) are grouped so
   // that workgroups b, b+8, ... (one XCD under round-robin placement; speed only) walk the pairs of
@@ -1366,6 +1569,10 @@ struct okvisgpu_ctx {
     const auto tb0 = std::chrono::steady_clock::now();
     {
       HostBatch nb;
+      // nested-dissection order where the tile-parallel schedule will run (fewer windows than half
+      // the CUs, setOptions): its launch chain is the latency of a solve. The order is a function of
+      // the window and this flag only, so a window's bits depend on the batch just through it.
+      nb.nd = 2 * (int)probs.size() < cuCount;
       analyse(probs, constOverride, nb);  // may throw: B is untouched until it succeeds
       B = std::move(nb);
     }
@@ -1477,8 +1684,8 @@ struct okvisgpu_ctx {
     const size_t o_tnz = upl(B.tile_nz), o_tnzoff = upl(B.win_tnzoff), o_tfu = upl(B.tile_fu);
     const size_t o_app = upl(B.asm_pp_items), o_asb = upl(B.asm_sb_items), o_appl = upl(B.asm_ppl_items);
     const size_t o_ti = upl(B.tile_items);
-    const size_t o_cpi = upl(B.chol_panel_items), o_cpb = upl(B.chol_panel_begin), o_cui = upl(B.chol_upd_items),
-                 o_cub = upl(B.chol_upd_begin);
+    const size_t o_cri = upl(B.chol_root_items), o_cui = upl(B.chol_upd_items), o_cub = upl(B.chol_upd_begin);
+    const size_t o_wsgap = upl(B.win_sgap);
     const size_t nf = std::max(1, B.f_total), nl3 = std::max<size_t>(1, (size_t)3 * D.n_lm);
     const size_t o_S = scratch(sizeof(double) * std::max<int64_t>(1, B.s_total));
     const size_t o_W = scratch(sizeof(double) * std::max<int64_t>(1, B.s_total));
@@ -1578,10 +1785,12 @@ struct okvisgpu_ctx {
     D.tile_nz = reinterpret_cast<const uint8_t*>(base + place(o_tnz));
     D.tile_fu = reinterpret_cast<const int16_t*>(base + place(o_tfu));
     D.win_tnzoff = reinterpret_cast<const int64_t*>(base + place(o_tnzoff));
-    D.chol_panel_items = ip(o_cpi); D.chol_panel_begin = ip(o_cpb);
+    D.chol_root_items = ip(o_cri);
+    D.n_chol_roots = (int)B.chol_root_items.size() / 3;
+    D.n_chol_launches = B.n_chol_launches;
     D.chol_upd_items = ip(o_cui); D.chol_upd_begin = ip(o_cub);
-    D.h_panel_begin = B.chol_panel_begin.data();
     D.h_upd_begin = B.chol_upd_begin.data();
+    D.win_sgap = ip(o_wsgap);
     D.chol_schedule = 1;
     D.asm_pp_items = ip(o_app); D.asm_sb_items = ip(o_asb);
     D.n_asm_pp = (int)B.asm_pp_items.size(); D.n_asm_sb = (int)B.asm_sb_items.size();
@@ -2201,7 +2410,7 @@ double kernelWork(const HostBatch& B, const DevProblem& P, int k) {
     case K_CHOLESKY: {  // diagonal LLT + inverse + y_k, panels, band updates, backward solve
       double diag = 0;
       for (int w = 0; w < P.n_win; ++w) diag += B.tileT[w];
-      const double panels = (double)(B.chol_panel_items.size() / 2), upd = (double)B.n_band_updates;
+      const double panels = (double)B.n_panels, upd = (double)B.n_band_updates;
       return diag * (2.0 * tile3 / 3.0 + 4.0 * 64 * 64) + panels * (2.0 * tile3 + 4.0 * 64 * 64) + upd * 2.0 * tile3;
     }
     case K_LM_VISIT:  // obs linearisation + params in; segments, partial blocks, landmark blocks out
@@ -2325,7 +2534,9 @@ int okvisgpu_get_stats(okvisgpu_ctx* c, okvisgpu_problem_stats* st) {
   st->n_pose_priors = P.n_pprior;
   st->n_sb_priors = P.n_sbprior;
   st->n_relpose = P.n_relpose;
-  st->reduced_dim = B.f_total;
+  st->cholesky_launches = B.n_chol_launches;
+  st->reduced_dim = 0;
+  for (int d : B.win_fnat) st->reduced_dim += d;
   st->s_tiles_nonzero = (int64_t)B.tile_items.size() / 3;
   for (int T : B.tileT) st->s_tiles_dense += (int64_t)T * (T + 1) / 2;
   st->n_block_pairs = P.n_pair;
@@ -2375,20 +2586,29 @@ int okvisgpu_linearize_reduce(okvisgpu_ctx* c, int32_t window, int32_t jacobi_sc
     launch_gn_reduce(c->P, c->stream);
     HIPCHK(hipGetLastError());
     auto st = c->readStates();
-    const int fdim = c->B.win_fdim[window], fpad = c->B.win_fpad[window];
-    if (dim_out) *dim_out = fdim;
+    // exported in the natural order (pose i, speed/bias i, ..., extrinsics), whatever order the
+    // window's S is held in (nested dissection: permuted slots and gap rows)
+    const int fdim = c->B.win_fdim[window], fpad = c->B.win_fpad[window], dn = c->B.win_fnat[window];
+    const int32_t* nat = c->B.f_nat.data() + c->B.win_foff[window];
+    if (dim_out) *dim_out = dn;
     if (cost) *cost = st[window].x_cost + st[window].fixed_cost;
-    if (S && fdim) {
+    if (S && dn) {
       std::vector<double> full((size_t)fpad * fpad);
       HIPCHK(hipMemcpy(full.data(), c->P.S + c->B.win_soff[window], full.size() * 8, hipMemcpyDeviceToHost));
       for (int r = 0; r < fdim; ++r)
         for (int q = 0; q <= r; ++q) {
-          S[(size_t)r * fdim + q] = full[(size_t)r * fpad + q];
-          S[(size_t)q * fdim + r] = full[(size_t)r * fpad + q];
+          const int a = nat[r], b = nat[q];
+          if (a < 0 || b < 0) continue;
+          S[(size_t)a * dn + b] = full[(size_t)r * fpad + q];
+          S[(size_t)b * dn + a] = full[(size_t)r * fpad + q];
         }
     }
-    if (rhs && fdim)
-      HIPCHK(hipMemcpy(rhs, c->P.rhsF + c->B.win_foff[window], sizeof(double) * fdim, hipMemcpyDeviceToHost));
+    if (rhs && dn) {
+      std::vector<double> v(fdim);
+      HIPCHK(hipMemcpy(v.data(), c->P.rhsF + c->B.win_foff[window], sizeof(double) * fdim, hipMemcpyDeviceToHost));
+      for (int r = 0; r < fdim; ++r)
+        if (nat[r] >= 0) rhs[nat[r]] = v[r];
+    }
     if (st[window].gn_failed) return fail(c, OKVISGPU_ERR_NUMERICAL, "landmark block not positive definite");
     return (int)OKVISGPU_OK;
   });

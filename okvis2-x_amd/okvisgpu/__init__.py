@@ -135,14 +135,14 @@ class SynthConfig(C.Structure):
 
 
 class ProblemStats(C.Structure):
-    _fields_ = [("n_windows", C.c_int32), ("reserved_", C.c_int32)] + [(k, C.c_int64) for k in (
+    _fields_ = [("n_windows", C.c_int32), ("cholesky_launches", C.c_int32)] + [(k, C.c_int64) for k in (
         "n_poses", "n_speed_biases", "n_landmarks", "n_landmarks_free", "n_extrinsics_free", "n_observations",
         "n_visits", "n_imu", "n_imu_samples", "n_pose_priors", "n_sb_priors", "n_relpose", "reduced_dim",
         "s_tiles_nonzero", "s_tiles_dense", "n_block_pairs", "n_visit_segments", "n_partial_blocks",
         "arena_bytes")]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved_"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class ImuAppendBatch(C.Structure):

@@ -23,5 +23,7 @@ ctx.solve_iterate(n)
 ctx.synchronize()
 dt = time.perf_counter() - t0
 s = ctx.solve_end()[0]
-print(f"sched {sched}: {n / dt:.1f} it/s, {dt / n * 1e3:.3f} ms/it, final cost {s['final_cost']:.9g}")
+st = ctx.stats()
+print(f"sched {sched}: {n / dt:.1f} it/s, {dt / n * 1e3:.3f} ms/it, final cost {s['final_cost']:.9g}, "
+      f"{st['cholesky_launches']} cholesky launches, {st['s_tiles_nonzero']} tiles, dim {st['reduced_dim']}")
 ctx.close()
