@@ -320,18 +320,22 @@ int cholSchedule(const std::vector<uint8_t>& nz, int T, std::vector<int>& L, std
 inline int pad64(int x) { return (x + kTile - 1) / kTile * kTile; }
 // One level of nested dissection of a window's state slots (few windows: the latency of a solve is
 // the chain of the tile-parallel launches). Slots [0, a) (left) and [b, n) (right) share no factor
-// once the separator [a, b) is eliminated last: order left | right | separator, left padded to a
-// tile boundary in S, so the two parts factor as independent chains. dim[u] = f scalars of slot u,
+// once the separator [a, b) is eliminated last: order left | right reversed | separator, left padded
+// to a tile boundary in S, so the two parts factor as independent chains that each reach the
+// separator only at their ends (the right part in natural order would touch it from its first
+// tile on, and every step would write the separator's tiles). dim[u] = f scalars of slot u,
 // reach[u] = largest slot coupled to u (landmarks seen from both, IMU links, edges, host factors).
 // The split is chosen on the launch count of the estimated tile pattern (interval couplings);
 // returns {-1, -1} unless it saves two launches or more with at most one tile more.
 std::pair<int, int> chooseNd(const std::vector<int>& dim, const std::vector<int>& reach) {
   const int n = (int)dim.size();
   auto estimate = [&](int a, int b, int& tiles) {
-    std::vector<int> order;
-    for (int u = 0; u < a; ++u) order.push_back(u);
-    for (int u = b; u < n; ++u) order.push_back(u);
-    for (int u = a; u < b; ++u) order.push_back(u);
+    std::vector<int> order;  // (a = 0: the natural order)
+    for (int u = 0; u < (a > 0 ? a : n); ++u) order.push_back(u);
+    if (a > 0) {
+      for (int u = n - 1; u >= b; --u) order.push_back(u);
+      for (int u = a; u < b; ++u) order.push_back(u);
+    }
     std::vector<int> off(n, 0);
     int o = 0;
     for (int t = 0; t < n; ++t) {
@@ -580,7 +584,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
       if (ab.first > 0) {
         slotOrder.clear();
         for (int u = 0; u < ab.first; ++u) slotOrder.push_back(u);
-        for (int u = ab.second; u < nmax; ++u) slotOrder.push_back(u);
+        for (int u = nmax - 1; u >= ab.second; --u) slotOrder.push_back(u);
         for (int u = ab.first; u < ab.second; ++u) slotOrder.push_back(u);
         ndLeft = ab.first;
       }
