@@ -1577,6 +1577,7 @@ struct okvisgpu_ctx {
       // the CUs, setOptions): its launch chain is the latency of a solve. The order is a function of
       // the window and this flag only, so a window's bits depend on the batch just through it.
       nb.nd = 2 * (int)probs.size() < cuCount;
+      if (const char* e = std::getenv("OKVISGPU_ND")) nb.nd = e[0] == '1';  // (development A/B)
       analyse(probs, constOverride, nb);  // may throw: B is untouched until it succeeds
       B = std::move(nb);
     }
