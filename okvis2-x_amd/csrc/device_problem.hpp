@@ -246,6 +246,8 @@ struct DevProblem {
   const int32_t* fb_off;           // offset in the window's f-vector
   const int32_t* win_sgap;         // [n_win][2] f offset and length of the gap rows of a nested-
                                    // dissection order (identity rows of S, zero rhs; 0 0: none)
+  const int32_t* win_bsplit;       // [n_win][2] tiles tL, tS: left part [0, tL), right part [tL, tS),
+                                   // separator [tS, T) of the backward substitution (0 0: no split)
   const int32_t* fb_cbegin;        // [n_fblock+1] gradient / diagonal contributions (C_VISIT, C_IMU, priors)
   const Contrib* fb_contrib;
   const int32_t* asm_pp_items;      // pose-pose pairs, one per wavefront, XCD-grouped order (-1 = pad)

@@ -960,15 +960,27 @@ __global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restric
 // pipelined. Step I-1's operands do not depend on x, so their loads are issued before step I's
 // reductions (a single window is a chain of T steps that would otherwise each wait a full memory
 // latency); two register sets, no copies; barriers order LDS only, so the loads stay in flight
-// across them. Same operations in the same order as backSubstitute.
+// across them. Same operations in the same order as backSubstitute. A nested-dissection window
+// (win_bsplit) is solved by two workgroups: both solve the separator's block rows, then workgroup
+// 0 the left part and workgroup 1 the right part (independent: no non-zero tile between them);
+// each step's operations are those of the one-workgroup order, so the bits are the same.
 constexpr int kBsReal = 512;
 __global__ __launch_bounds__(kBsReal) void k_chol_bsub(const DevProblem* __restrict__ Pp) {
   constexpr int kV = kBsThreads / kBsReal;
   const DevProblem& P = *Pp;
-  const int w = blockIdx.x;
+  const int w = blockIdx.x, h = blockIdx.y;
   if (!cholSelect(P, w)) return;
   const int64_t ld = P.win_fpad[w];
   const int T = (int)(ld / kTile);
+  const int tL = P.win_bsplit[2 * w], tS = P.win_bsplit[2 * w + 1];
+  const bool split = tS > 0;
+  if (h == 1 && !split) return;
+  // step n -> block row: the separator [tS, T) (whole window without a split), then this
+  // workgroup's part, descending
+  const int nSep = split ? T - tS : T;
+  const int nSteps = nSep + (split ? (h == 0 ? tL : tS - tL) : 0);
+  const int partTop = h == 0 ? tL - 1 : tS - 1;
+  auto rowAt = [&](int n) { return n < nSep ? T - 1 - n : partTop - (n - nSep); };
   const double* S = P.W + P.win_soff[w];  // L in the upper slots of the working copy
   const double* work = P.fwdF + P.win_fwdoff[w];
   const double* Linv = P.Linv + P.win_linvoff[w];
@@ -1002,18 +1014,21 @@ __global__ __launch_bounds__(kBsReal) void k_chol_bsub(const DevProblem* __restr
     if (t < kTile) sx[I * kTile + t] = sum32(sA + t);
     ldsBarrier();
   };
-  load(T - 1, ping);
+  load(rowAt(0), ping);
   CLK(12)
-  for (int I = T - 1; I >= 0; I -= 2) {  // (loads clamped, not skipped: no loads under a branch)
-    load(I > 0 ? I - 1 : 0, pong);
-    step(I, ping);
-    if (I == 0) break;
-    load(I > 1 ? I - 2 : 0, ping);
-    step(I - 1, pong);
+  for (int n = 0; n < nSteps; n += 2) {  // (loads clamped, not skipped: no loads under a branch)
+    load(rowAt(min(n + 1, nSteps - 1)), pong);
+    step(rowAt(n), ping);
+    if (n + 1 == nSteps) break;
+    load(rowAt(min(n + 2, nSteps - 1)), ping);
+    step(rowAt(n + 1), pong);
   }
   CLK(13)
+  // x of the rows this workgroup owns (the separator's by workgroup 0)
   const int fdim = P.win_fdim[w];
-  for (int e = t; e < fdim; e += kBsReal) P.yF[(size_t)P.win_foff[w] + e] = sx[e];
+  const int e0 = !split ? 0 : (h == 0 ? 0 : tL * kTile), e1 = !split ? fdim : (h == 0 ? fdim : tS * kTile);
+  for (int e = e0 + t; e < e1; e += kBsReal)
+    if (!split || h == 1 || e < tL * kTile || e >= tS * kTile) P.yF[(size_t)P.win_foff[w] + e] = sx[e];
 #ifdef OKG_CHOL_CLOCK
   if (blockIdx.x == 0 && t == 0) printf("BSUBCLK T=%d init %llu steps %llu (x10ns)\n", T, g_cholClk[12], g_cholClk[13]);
 #endif
@@ -1036,7 +1051,7 @@ void launch_cholesky(const DevProblem& P, hipStream_t s) {
     const int nu = P.h_upd_begin[l + 1] - P.h_upd_begin[l];
     if (nu > 0) hipLaunchKernelGGL(k_chol_update, dim3(nu), dim3(256), 0, s, P.self, l);
   }
-  hipLaunchKernelGGL(k_chol_bsub, dim3(P.n_win), dim3(kBsReal),
+  hipLaunchKernelGGL(k_chol_bsub, dim3(P.n_win, 2), dim3(kBsReal),
                      sizeof(double) * P.max_fpad + sizeof(int) * (1 + kBsPre) * P.max_tiles + P.max_tiles * P.max_tiles, s,
                      P.self);
 }

@@ -145,7 +145,7 @@ struct HostBatch {
   // S offset of every f-block: fb_off, plus the window's gap rows after the left part of a
   // nested-dissection order (win_sgap: f offset of the gap, gap length; 0 0 without one); natural
   // index of every f entry (-1: gap row) and natural dimension per window
-  std::vector<int32_t> win_sgap, f_nat, win_fnat;
+  std::vector<int32_t> win_sgap, f_nat, win_fnat, win_bsplit;
   bool nd = false;  // order the windows' states for the tile-parallel schedule (nested dissection)
   std::vector<int32_t> chol_root_items;  // (w, d, first-root-of-window flag): tiles no update writes
   int n_chol_launches = 1;
@@ -535,7 +535,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
     const int fbBase = (int)B.fb_win.size();
     std::vector<int> slotOrder(nmax);
     std::iota(slotOrder.begin(), slotOrder.end(), 0);
-    int ndLeft = 0;  // slots of the left part (0: natural order)
+    int ndLeft = 0, ndSep = 0;  // slots of the left part (0: natural order); order index of the separator
     const bool extFree = std::any_of(pa.begin() + np, pa.end(), [](uint8_t a) { return a != 0; });
     if (B.nd && !extFree && nmax >= 8) {  // (variable extrinsics couple every state: no split)
       std::vector<int> dim(nmax, 0), reach(nmax);
@@ -587,18 +587,21 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
         for (int u = nmax - 1; u >= ab.second; --u) slotOrder.push_back(u);
         for (int u = ab.first; u < ab.second; ++u) slotOrder.push_back(u);
         ndLeft = ab.first;
+        ndSep = ab.first + (nmax - ab.second);
       }
     }
     // (nested dissection: the left part ends on a tile boundary; the gap rows between are identity
     // rows of S with zero rhs, so the f-vector and S share one index)
-    int gapAt = 0, gap = 0;
+    int gapAt = 0, gap = 0, rightAt = 0, sepAt = 0;
     for (int t = 0; t < nmax; ++t) {
       const int i = slotOrder[t];
       if (ndLeft && t == ndLeft) {
         gapAt = fo;
         fo = pad64(fo);
         gap = fo - gapAt;
+        rightAt = fo;
       }
+      if (ndLeft && t == ndSep) sepAt = fo;
       if (i < p->n_poses && pa[i]) {
         posef[i] = fo;
         poseFb[i] = (int)B.fb_win.size();
@@ -1110,6 +1113,16 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
               fu[(size_t)i * T + j] = (int16_t)k;
               break;
             }
+      // backward substitution split (nested dissection): the tiles of the left part [0, tL) and of
+      // the right part [tL, tS) share no non-zero tile, so once the separator's tiles [tS, T) are
+      // solved the two parts are independent (k_chol_bsub: one workgroup each)
+      int tL = rightAt / kTile, tS = sepAt / kTile;
+      bool split = ndLeft > 0 && tL > 0 && tS > tL;
+      for (int i = tL; split && i < tS; ++i)
+        for (int j = 0; j < tL; ++j)
+          if (nz[(size_t)i * T + j]) split = false;
+      B.win_bsplit.push_back(split ? tL : 0);
+      B.win_bsplit.push_back(split ? tS : 0);
       B.tileFu.push_back(fu);
       B.tileNz.push_back(nz);
       B.tileT.push_back(T);
@@ -1690,7 +1703,7 @@ struct okvisgpu_ctx {
     const size_t o_app = upl(B.asm_pp_items), o_asb = upl(B.asm_sb_items), o_appl = upl(B.asm_ppl_items);
     const size_t o_ti = upl(B.tile_items);
     const size_t o_cri = upl(B.chol_root_items), o_cui = upl(B.chol_upd_items), o_cub = upl(B.chol_upd_begin);
-    const size_t o_wsgap = upl(B.win_sgap);
+    const size_t o_wsgap = upl(B.win_sgap), o_wbsp = upl(B.win_bsplit);
     const size_t nf = std::max(1, B.f_total), nl3 = std::max<size_t>(1, (size_t)3 * D.n_lm);
     const size_t o_S = scratch(sizeof(double) * std::max<int64_t>(1, B.s_total));
     const size_t o_W = scratch(sizeof(double) * std::max<int64_t>(1, B.s_total));
@@ -1796,6 +1809,7 @@ struct okvisgpu_ctx {
     D.chol_upd_items = ip(o_cui); D.chol_upd_begin = ip(o_cub);
     D.h_upd_begin = B.chol_upd_begin.data();
     D.win_sgap = ip(o_wsgap);
+    D.win_bsplit = ip(o_wbsp);
     D.chol_schedule = 1;
     D.asm_pp_items = ip(o_app); D.asm_sb_items = ip(o_asb);
     D.n_asm_pp = (int)B.asm_pp_items.size(); D.n_asm_sb = (int)B.asm_sb_items.size();
