@@ -468,6 +468,10 @@ __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li,
       double r[8], x[8], rl[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) r[k] = sA[i * kLd + c0 + k];
+      // Scheduling fences (scripts/ubench_ptile.hip): the row's loads retire here, and the look-ahead
+      // result and the factor's x are complete before their stores are issued; left to itself the
+      // compiler interleaves those stores and loads with the FP64 chain (22.4 -> 16.4 us per tile)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (s >= 1) {  // look-ahead update by sub-panel s-1: r -= L_i,s-1 L_(c0..c0+7),s-1^T
         // (c outer: the 8 independent chains r[m] interleave, so no FMA waits on the previous one's
         // result; every r[m] still sums over c in order, the same bits)
@@ -475,6 +479,7 @@ __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li,
         for (int c = 0; c < 8; ++c)
 #pragma unroll
           for (int m = 0; m < 8; ++m) r[m] -= xp[c] * sA[(c0 + m) * kLd + c0 - 8 + c];
+        asm volatile("" ::"v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]));
         if (i >= c0) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) sA[i * kLd + c0 + k] = r[k];
@@ -486,6 +491,7 @@ __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li,
         if (lane == 0) ldsReleaseL(&sFl[2], 1);
         break;
       }
+      asm volatile("" ::"v"(x[7]));
       CLK(23)
       storeRow8(sA, c0, x, i);
       if (lane == 0) {

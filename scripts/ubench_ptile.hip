@@ -2,22 +2,22 @@
 // y = X rhs) on one 256-thread workgroup, isolated (1 workgroup) and under load (2 per CU), plus a
 // stamped copy of the sweep's chain wavefront (variant V, -DOKG_V=n) whose per-sub-panel phase
 // times (s_memtime, shader clock) show where the chain spends its cycles.
-// hipcc --offload-arch=gfx950 -O3 -I include -DOKG_V=0 scripts/ubench_ptile.hip -o scripts/ubench_ptile
+// hipcc --offload-arch=gfx950 -O3 -I include scripts/ubench_ptile.hip -o scripts/ubench_ptile
 #include "../okvis2-x_amd/csrc/kernels_chol.hip"
 
 #include <cmath>
 #include <cstdio>
 #include <vector>
 
-#ifndef OKG_V
-#define OKG_V 0
-#endif
 
 namespace okg {
 __device__ unsigned long long g_tr[8][8];
 
 // The chain wavefront's loop of potrfTile with stamps (lane 0 of wavefront 0, workgroup 0):
 // [0] start [1] waited [2] r loaded [3] look-ahead FMAs [4] r stored [5] chol8 [6] stored
+// Variants: 0 stamps + scheduling fences (lgkmcnt wait after the r loads, r / x consumed before the
+// stores), 2 fences without stamps, 3 the consumption fences only, 4 stamps only.
+#define STAMP(s, k) if (V == 0 || V == 4) st[s][k] = __builtin_amdgcn_s_memtime();
 template <int V>
 __device__ __noinline__ bool potrfExp(const double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX,
                                       double* sy, double* sRl, int* sFl, int t) {
@@ -40,47 +40,47 @@ __device__ __noinline__ bool potrfExp(const double* Sg, int64_t ld, double* Li, 
 #pragma unroll 1
     for (int s = 0; s < 8; ++s) {
       const int c0 = 8 * s;
-      st[s][0] = __builtin_amdgcn_s_memtime();
+      STAMP(s, 0)
       if (s >= 2 && !waitFlag<true>(&sFl[1], s - 1, &sFl[2])) break;
-      st[s][1] = __builtin_amdgcn_s_memtime();
+      STAMP(s, 1)
       double r[8], x[8], rl[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) r[k] = sA[i * kLd + c0 + k];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      st[s][2] = __builtin_amdgcn_s_memtime();
+      if (V == 0 || V == 2) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      STAMP(s, 2)
       if (s >= 1) {
 #pragma unroll
         for (int c = 0; c < 8; ++c)
 #pragma unroll
           for (int m = 0; m < 8; ++m) r[m] -= xp[c] * sA[(c0 + m) * kLd + c0 - 8 + c];
-        asm volatile("" ::"v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]));
-        st[s][3] = __builtin_amdgcn_s_memtime();
+        if (V != 4) asm volatile("" ::"v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]));
+        STAMP(s, 3)
         if (V == 1 ? (i >= c0 && i < c0 + 8) : i >= c0) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) sA[i * kLd + c0 + k] = r[k];
         }
         __builtin_amdgcn_wave_barrier();
       } else {
-        st[s][3] = st[s][2];
+        if (V == 0 || V == 4) st[s][3] = st[s][2];
       }
-      st[s][4] = __builtin_amdgcn_s_memtime();
+      STAMP(s, 4)
       if (!chol8Row(sA, c0, r, x, rl)) {
         if (lane == 0) ldsReleaseL(&sFl[2], 1);
         break;
       }
-      asm volatile("" ::"v"(x[7]));
-      st[s][5] = __builtin_amdgcn_s_memtime();
+      if (V != 4) asm volatile("" ::"v"(x[7]));
+      STAMP(s, 5)
       storeRow8(sA, c0, x, i);
       if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) sRl[c0 + k] = rl[k];
         ldsReleaseL(&sFl[0], s + 1);
       }
-      st[s][6] = __builtin_amdgcn_s_memtime();
+      STAMP(s, 6)
 #pragma unroll
       for (int k = 0; k < 8; ++k) xp[k] = x[k];
     }
-    if (tr)
+    if ((V == 0 || V == 4) && tr)
       for (int s = 0; s < 8; ++s)
         for (int k = 0; k < 7; ++k) g_tr[s][k] = st[s][k];
   } else {
@@ -116,7 +116,7 @@ __device__ __noinline__ bool potrfExp(const double* Sg, int64_t ld, double* Li, 
 }
 }  // namespace okg
 
-template <int EXP>
+template <int EXP>  // -1: the product's potrfTile, else potrfExp<EXP>
 __global__ __launch_bounds__(256, 2) void kptile(const double* A, double* Li, double* work, int reps,
                                                  unsigned long long* ticks) {
   __shared__ double sA[okg::kTile * okg::kLd];
@@ -130,8 +130,8 @@ __global__ __launch_bounds__(256, 2) void kptile(const double* A, double* Li, do
     if (t < 64) sy[t] = 1.0 + t;
     __syncthreads();
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    if (EXP)
-      okg::potrfExp<OKG_V>(A, 64, Li + (size_t)blockIdx.x * 4096, work + (size_t)blockIdx.x * 64, sA, sX, sy, sRl, sFl, t);
+    if (EXP >= 0)
+      okg::potrfExp<(EXP < 0 ? 0 : EXP)>(A, 64, Li + (size_t)blockIdx.x * 4096, work + (size_t)blockIdx.x * 64, sA, sX, sy, sRl, sFl, t);
     else
       okg::potrfTile<1>(A, 64, Li + (size_t)blockIdx.x * 4096, work + (size_t)blockIdx.x * 64, sA, sX, sy, sRl, sFl, t,
                         false);
@@ -191,9 +191,12 @@ int main() {
   (void)hipMalloc(&dW, 8 * 64 * (size_t)nb);
   (void)hipMalloc(&dT, 8 * nb);
   (void)hipMemcpy(dA, A.data(), 8 * 4096, hipMemcpyHostToDevice);
-  run<0>("product", dA, dL, dW, dT, A);
-  run<1>("stamped", dA, dL, dW, dT, A);
-  hipLaunchKernelGGL(kptile<1>, 1, 256, 0, 0, dA, dL, dW, 1, dT);
+  run<-1>("product", dA, dL, dW, dT, A);
+  run<2>("fences", dA, dL, dW, dT, A);
+  run<3>("consume-only", dA, dL, dW, dT, A);
+  run<4>("stamps-only", dA, dL, dW, dT, A);
+  run<0>("stamped", dA, dL, dW, dT, A);
+  hipLaunchKernelGGL(kptile<0>, 1, 256, 0, 0, dA, dL, dW, 1, dT);
   (void)hipDeviceSynchronize();
   unsigned long long T[8][8];
   (void)hipMemcpyFromSymbol(T, HIP_SYMBOL(okg::g_tr), sizeof(T));
