@@ -238,9 +238,11 @@ typedef struct okvisgpu_options {   /* ::ceres::Solver::Options fields okvis set
   int32_t redo_propagation_always;  /* ImuError::redoPropagationAlways (ViSlamBackend.cpp:2036)  */
   int32_t num_threads;              /* host threads (reference path / host evaluation)          */
   int32_t verbose;
-  int32_t cholesky_schedule;        /* 0 auto, 1 one persistent workgroup per window (from half a */
-                                    /* window per CU), 2 tile-parallel launches per step (fewer   */
-                                    /* windows); both give the same bits. Other values: auto.     */
+  int32_t cholesky_schedule;        /* 0 auto, 1 one persistent workgroup per window (batches of */
+                                    /* more windows than CUs), 2 tile-parallel launches (fewer    */
+                                    /* than half as many), 3 persistent, split over the two parts */
+                                    /* of a nested-dissection window (in between); all give the  */
+                                    /* same bits for one batch. Other values: auto.               */
 } okvisgpu_options;
 
 typedef struct okvisgpu_summary {   /* ::ceres::Solver::Summary subset */
@@ -410,6 +412,7 @@ typedef struct okvisgpu_problem_stats {
   int64_t s_tiles_dense;            /* lower-triangle tiles of the dense reduced matrices          */
   int64_t n_block_pairs, n_visit_segments, n_partial_blocks;
   int64_t arena_bytes;              /* device memory held by the context                           */
+  int64_t cholesky_split_windows;   /* windows whose nested-dissection parts factor independently */
 } okvisgpu_problem_stats;
 int okvisgpu_get_stats(okvisgpu_ctx* ctx, okvisgpu_problem_stats* stats);
 

@@ -288,6 +288,8 @@ struct DevProblem {
                                      // writes tile (i, j) (kNoUpdate if none): before it the tile is read from S
   const int64_t* win_tnzoff;         // [n_win] offset of the window's flags in tile_nz
   int32_t n_tiles;
+  double* chol_defer;              // split persistent schedule: the right part's rhs contributions
+  const int64_t* win_defoff;       //   to the separator's rows, [T - tS][tS - tL][64] per window
   double* fwdF;                    // per window fpad: forward-substitution work vector
   const int64_t* win_fwdoff;       // [n_win] offset into fwdF
   double* sF;   double* sL;        // Jacobi scaling (fixed at iteration 0)

@@ -406,6 +406,9 @@ __device__ __forceinline__ void yBlock16(const double* sX, double* sy, int q, in
 // The 16 rows of block q of X to Li (row-major 64 x 64) by three wavefronts (g < 3). The persistent
 // schedule's backward substitution masks the upper triangle of X (bsDiag), so it stores the lower
 // one only; the tile-parallel update kernels stage X whole for the MFMAs (zeros stored).
+// kCaller: 1 k_chol_roots, 2 k_chol_update, 10 + MODE the persistent k_cholesky<MODE> (which keeps
+// y in LDS and stores X lower-triangular)
+__host__ __device__ constexpr bool persistentCaller(int kCaller) { return kCaller >= 10; }
 template <int kCaller>
 __device__ __forceinline__ void xStoreRows16(const double* sX, double* Li, int q, int g, int lane) {
   double2 v[3];
@@ -417,7 +420,7 @@ __device__ __forceinline__ void xStoreRows16(const double* sX, double* Li, int q
 #pragma unroll
   for (int it = 0; it < 3; ++it) {
     const int e = 64 * g + lane + 192 * it, r = 16 * q + (e >> 5), c = 2 * (e & 31);
-    if (e < 512 && (kCaller != 0 || c <= r)) *reinterpret_cast<double2*>(Li + r * kTile + c) = v[it];
+    if (e < 512 && (!persistentCaller(kCaller) || c <= r)) *reinterpret_cast<double2*>(Li + r * kTile + c) = v[it];
   }
 }
 
@@ -534,7 +537,7 @@ __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li,
   if (t < kTile) {
     const double y = sy[kTile + t];
     sy[t] = y;
-    if (kCaller != 0) workk[t] = y;
+    if (!persistentCaller(kCaller)) workk[t] = y;
   }
   ldsBarrier();
   CLK(10)
@@ -570,7 +573,7 @@ __device__ __forceinline__ void panelRhsVector(const double* sX, const double* s
 // L_ik = A_ik X^T (X = L_kk^-1 in sX) stored over A_ik, and rhs_i -= A_ik z (z = X^T y_k in sz),
 // the row products formed from the A_ik tile in LDS while the MFMAs run.
 __device__ __forceinline__ void panelTile(const double* Aik, double* Lik, int64_t ld, double* worki, double* sA, const double* sX, const double* sz,
-                          int t) {
+                          int t, double* defer = nullptr) {
   loadTile(Aik, ld, 0, 0, sA, t);
   ldsBarrier();  // LDS-only: the previous panel's L / rhs stores stay in flight
   dbl4 acc[2][2];
@@ -582,7 +585,10 @@ __device__ __forceinline__ void panelTile(const double* Aik, double* Lik, int64_
     for (int c = 16 * q; c < 16 * q + 16; ++c) a += sA[row * kLd + c] * sz[c];
     a += __shfl_xor(a, 1, 64);
     a += __shfl_xor(a, 2, 64);
-    if (q == 0) worki[row] -= a;  // rhs_i in LDS
+    if (q == 0) {
+      if (defer) defer[row] = a;  // (split schedule: subtracted by the separator's launch, in step order)
+      else worki[row] -= a;       // rhs_i in LDS
+    }
   }
   ldsBarrier();  // sA is free for the next panel
   storeTile<false>(Lik, ld, 0, 0, acc, t);
@@ -724,16 +730,39 @@ __device__ __forceinline__ void backSubstitute(const DevProblem& P, int w, const
 #ifndef OKG_CHOL_OCC
 #define OKG_CHOL_OCC 2
 #endif
+// Persistent schedule, one workgroup per window (MODE 0), or split over a nested-dissection
+// window's two independent parts (win_bsplit; schedule 3, runtime.cpp setOptions):
+//   MODE 1 (launch A, workgroups 2w and 2w+1): part 0 runs the left part's steps [0, tL) with all
+//          their updates; part 1 the right part's steps [tL, tS) with the updates of targets left
+//          of the separator, and for the separator's tiles it stores only L (the panels) and each
+//          panel's rhs contribution (chol_defer); both write their y / rhs rows to fwdF.
+//   MODE 2 (launch B, one workgroup per window): the right steps' updates of the separator's
+//          tiles and their rhs contributions, step by step, then the separator's steps [tS, T)
+//          and the backward substitution.
+// Every tile receives its updates in step order in all modes (the left part's steps precede the
+// right part's), each with the same operations, so the split gives the bits of MODE 0 on the same
+// order. A window without a split runs MODE 0 in part 0 of launch A (MODE 2 skips it).
+template <int MODE>
 __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
-  const int w = blockIdx.x;
+  const int w = MODE == 1 ? (int)(blockIdx.x >> 1) : (int)blockIdx.x, part = MODE == 1 ? (int)(blockIdx.x & 1) : 0;
   if (!cholSelect(P, w)) return;
   const int64_t ld = P.win_fpad[w];
   const int T = (int)(ld / kTile);
+  const int tL = MODE == 0 ? 0 : P.win_bsplit[2 * w], tS = MODE == 0 ? 0 : P.win_bsplit[2 * w + 1];
+  const bool split = MODE != 0 && tS > 0;
+  if ((MODE == 1 && part == 1 && !split) || (MODE == 2 && !split)) return;
+  // this workgroup's steps [k0, k1), targets (i, j) with j < jEnd, and whether it ends the window
+  const int k0 = !split ? 0 : (MODE == 2 ? tS : (part == 0 ? 0 : tL));
+  const int k1 = !split ? T : (MODE == 2 ? T : (part == 0 ? tL : tS));
+  const int jEnd = split && MODE == 1 && part == 1 ? tS : T;
+  const bool finish = !split || MODE == 2;
   const TileSrc cur = tileSrc(P, w, ld);
   double* W = P.W + P.win_soff[w];
   double* Linv = P.Linv + P.win_linvoff[w];
   const uint8_t* nz = P.tile_nz + P.win_tnzoff[w];
+  double* work = P.fwdF + P.win_fwdoff[w];
+  double* defer = split ? P.chol_defer + P.win_defoff[w] : nullptr;
   __shared__ double sA[kTile * kLd];
   __shared__ double sX[kTile * kLd];
   __shared__ double sy[2 * kTile];  // y_k | panel column scratch
@@ -745,42 +774,33 @@ __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem
   // rhs / y of the whole window in LDS (sxDyn, ld doubles) for the forward substitution, the
   // panels' rhs updates and the backward substitution (no global round trip per step)
   extern __shared__ double sxDyn[];
-  for (int e = t; e < ld; e += 256) sxDyn[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
+  if (MODE == 2) {
+    for (int e = t; e < ld; e += 256) sxDyn[e] = work[e];
+  } else {
+    for (int e = t; e < ld; e += 256) sxDyn[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
+  }
   __syncthreads();
-  bool haveDiag = false;  // S_kk (updated by the previous step) already in sA
-  for (int k = 0; k < T; ++k) {
-    CLK(11)
-    if (t < kTile) sy[t] = sxDyn[k * kTile + t];
-    __syncthreads();  // full: the factor and the panels read the tiles the last band update stored
-    if (!potrfTile<0>(cur.at(k, k, k), ld, Linv + (int64_t)k * kTile * kTile, nullptr, sA, sX,
-                   sy, sRl, sFl, t, haveDiag)) {
-      if (t == 0) P.st[w].gn_failed = 1;
-      return;
-    }
-    if (t < kTile) sxDyn[k * kTile + t] = sy[t];  // y_k (ordered before its readers by the barriers below)
-    CLK(0)
-    // ---- panel: L_ik = A_ik X^T, rhs_i -= L_ik y_k = A_ik X^T y_k
-    panelRhsVector(sX, sy, sy + kTile, sA, t);
-    for (int i = k + 1; i < T; ++i)
-      if (nz[i * T + k])
-        panelTile(cur.at(i, k, k), W + i * kTile * ld + k * kTile, ld, sxDyn + i * kTile, sA, sX, sy + kTile, t);
-    __syncthreads();  // full barrier: the band update reads the L_ik just stored
-    CLK(1)
-    // ---- trailing band update: A_ij -= L_ik L_jk^T, k < j <= i, both tiles non-zero. The A_ij
-    // read of the read-modify-write is issued before the MFMAs, so its latency overlaps them.
-    // Block rows from the bottom: the L_jk staged in sX for a lower row is reused as the row
-    // operand when its own row comes (one staging per L tile on a 2-tile band instead of 3), and
-    // the last update, S_(k+1)(k+1), goes to sA for the next factor instead of through global
-    // memory. Independent tiles, the same operations: the same bits in any order.
+  // ---- trailing band update of step k: A_ij -= L_ik L_jk^T, k < j <= i, jLo <= j < jEnd, both
+  // tiles non-zero. The A_ij read of the read-modify-write is issued before the MFMAs, so its
+  // latency overlaps them. Block rows from the bottom: the L_jk staged in sX for a lower row is
+  // reused as the row operand when its own row comes (one staging per L tile on a 2-tile band
+  // instead of 3), and the last update, S_(k+1)(k+1), goes to sA for the next factor instead of
+  // through global memory (toLds). Independent tiles, the same operations: the same bits in any
+  // order. Returns whether S_(k+1)(k+1) was left in sA.
+  auto bandUpdate = [&](int k, int jLo, bool toLds) {
     int xHeld = -1;  // block row of the L tile in sX
-    haveDiag = false;
-    for (int i = T - 1; i > k; --i) {
+    bool inLds = false;
+    for (int i = T - 1; i > k && i >= jLo; --i) {
       if (!nz[i * T + k]) continue;
       const bool aInX = xHeld == i;
       const double* aBuf = aInX ? sX : sA;
-      if (!aInX) loadTile(W + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
-      for (int j = k + 1; j <= i; ++j) {
+      bool aLoaded = aInX;
+      for (int j = max(k + 1, jLo); j <= i && j < jEnd; ++j) {
         if (!nz[j * T + k]) continue;
+        if (!aLoaded) {
+          loadTile(W + i * kTile * ld + k * kTile, ld, 0, 0, sA, t);
+          aLoaded = true;
+        }
         const double* bBuf = aBuf;
         if (j != i) {
           if (aInX) {
@@ -797,23 +817,63 @@ __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem
         dbl4 c[2][2], acc[2][2];
         loadC(cur.at(i, j, k), ld, c, t);
         mfmaTileNT(aBuf, bBuf, acc, t);
-        if (i == k + 1) {  // (then j == i) the next diagonal tile: c - acc straight into sA
-          ldsBarrier();    // every wavefront has read its operands
+        if (toLds && i == k + 1) {  // (then j == i) the next diagonal tile: c - acc straight into sA
+          ldsBarrier();             // every wavefront has read its operands
           accSubToLds(sA, c, acc, t);
-          haveDiag = true;  // its global copy is stale from here on and never read
+          inLds = true;  // its global copy is stale from here on and never read
         } else {
           storeTileSub(Cij, ld, c, acc, t);
         }
         ldsBarrier();  // LDS-only: the updated tiles are read from the next step on, after full barriers
       }
     }
+    return inLds;
+  };
+  if (MODE == 2) {
+    // the right part's contributions to the separator, in step order: each step's panel rhs terms,
+    // then its updates of the separator's tiles (L from W, written by launch A)
+    for (int k = tL; k < tS; ++k) {
+      for (int i = tS; i < T; ++i)
+        if (nz[i * T + k] && t < kTile)
+          sxDyn[i * kTile + t] -= defer[((size_t)(i - tS) * (tS - tL) + (k - tL)) * kTile + t];
+      __syncthreads();
+      bandUpdate(k, tS, false);
+      __syncthreads();
+    }
+  }
+  bool haveDiag = false;  // S_kk (updated by the previous step) already in sA
+  for (int k = k0; k < k1; ++k) {
+    CLK(11)
+    if (t < kTile) sy[t] = sxDyn[k * kTile + t];
+    __syncthreads();  // full: the factor and the panels read the tiles the last band update stored
+    if (!potrfTile<10 + MODE>(cur.at(k, k, k), ld, Linv + (int64_t)k * kTile * kTile, nullptr, sA, sX,
+                   sy, sRl, sFl, t, haveDiag)) {
+      if (t == 0) P.st[w].gn_failed = 1;
+      return;
+    }
+    if (t < kTile) sxDyn[k * kTile + t] = sy[t];  // y_k (ordered before its readers by the barriers below)
+    CLK(0)
+    // ---- panel: L_ik = A_ik X^T, rhs_i -= L_ik y_k = A_ik X^T y_k (the separator's rows deferred
+    // by part 1 of the split)
+    panelRhsVector(sX, sy, sy + kTile, sA, t);
+    for (int i = k + 1; i < T; ++i)
+      if (nz[i * T + k])
+        panelTile(cur.at(i, k, k), W + i * kTile * ld + k * kTile, ld, sxDyn + i * kTile, sA, sX, sy + kTile, t,
+                  i >= jEnd ? defer + ((size_t)(i - tS) * (tS - tL) + (k - tL)) * kTile : nullptr);
+    __syncthreads();  // full barrier: the band update reads the L_ik just stored
+    CLK(1)
+    haveDiag = bandUpdate(k, 0, true);
   }
   CLK(2)
+  if (!finish) {  // launch A: this part's rows of y (part 0 also the separator's rhs) for launch B
+    const int e0 = part == 0 ? 0 : tL * kTile, e1 = part == 0 ? tL * kTile : tS * kTile;
+    for (int e = t; e < ld; e += 256)
+      if ((e >= e0 && e < e1) || (part == 0 && e >= tS * kTile)) work[e] = sxDyn[e];
+    return;
+  }
   backSubstitute(P, w, W, ld, T, Linv, nz, sxDyn, sA, sy, t);
   CLK(3)
 #ifdef OKG_CHOL_CLOCK
-  if (blockIdx.x == 0 && t == 0)
-    printf("SWEEP wait %llu look %llu chol %llu store %llu\n", g_cholClk[21], g_cholClk[22], g_cholClk[23], g_cholClk[24]);
   if (blockIdx.x == 0 && t == 0)
     printf("CHOLCLK T=%d potrf %llu panel %llu update %llu bsub %llu | load %llu pfac %llu ptrail %llu dinv %llu subd %llu store %llu y %llu (x10ns)\n",
            T, g_cholClk[0], g_cholClk[1], g_cholClk[2] + g_cholClk[11], g_cholClk[3], g_cholClk[4], g_cholClk[5], g_cholClk[6],
@@ -1042,14 +1102,19 @@ __global__ __launch_bounds__(kBsReal) void k_chol_bsub(const DevProblem* __restr
 
 bool cholesky_persistent_fits(int max_fpad, size_t lds_per_block) {
   hipFuncAttributes attr;
-  if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky)) != hipSuccess) return false;
+  if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky<0>)) != hipSuccess) return false;
   return attr.sharedSizeBytes + sizeof(double) * (size_t)max_fpad <= lds_per_block;
 }
 
 void launch_cholesky(const DevProblem& P, hipStream_t s) {
   if (P.n_win == 0) return;
   if (P.chol_schedule == 1) {
-    hipLaunchKernelGGL(k_cholesky, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
+    hipLaunchKernelGGL(k_cholesky<0>, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
+    return;
+  }
+  if (P.chol_schedule == 3) {
+    hipLaunchKernelGGL(k_cholesky<1>, dim3(2 * P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
+    hipLaunchKernelGGL(k_cholesky<2>, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
     return;
   }
   hipLaunchKernelGGL(k_chol_roots, dim3(P.n_chol_roots), dim3(256), 0, s, P.self);

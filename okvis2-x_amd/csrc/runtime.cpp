@@ -146,6 +146,9 @@ struct HostBatch {
   // nested-dissection order (win_sgap: f offset of the gap, gap length; 0 0 without one); natural
   // index of every f entry (-1: gap row) and natural dimension per window
   std::vector<int32_t> win_sgap, f_nat, win_fnat, win_bsplit;
+  std::vector<int64_t> win_defoff;
+  int64_t defer_total = 0;
+  bool any_split = false;
   bool nd = false;  // order the windows' states for the tile-parallel schedule (nested dissection)
   std::vector<int32_t> chol_root_items;  // (w, d, first-root-of-window flag): tiles no update writes
   int n_chol_launches = 1;
@@ -1123,6 +1126,9 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
           if (nz[(size_t)i * T + j]) split = false;
       B.win_bsplit.push_back(split ? tL : 0);
       B.win_bsplit.push_back(split ? tS : 0);
+      B.win_defoff.push_back(B.defer_total);
+      if (split) B.defer_total += (int64_t)(T - tS) * (tS - tL) * kTile;
+      B.any_split = B.any_split || split;
       B.tileFu.push_back(fu);
       B.tileNz.push_back(nz);
       B.tileT.push_back(T);
@@ -1586,10 +1592,11 @@ struct okvisgpu_ctx {
     const auto tb0 = std::chrono::steady_clock::now();
     {
       HostBatch nb;
-      // nested-dissection order where the tile-parallel schedule will run (fewer windows than half
-      // the CUs, setOptions): its launch chain is the latency of a solve. The order is a function of
-      // the window and this flag only, so a window's bits depend on the batch just through it.
-      nb.nd = 2 * (int)probs.size() < cuCount;
+      // nested-dissection order where the tile-parallel or the split persistent schedule will run
+      // (at most one window per CU, setOptions): the chain of a window's factorisation is the
+      // latency there. The order is a function of the window and this flag only, so a window's
+      // bits depend on the batch just through it.
+      nb.nd = (int)probs.size() <= cuCount;
       if (const char* e = std::getenv("OKVISGPU_ND")) nb.nd = e[0] == '1';  // (development A/B)
       analyse(probs, constOverride, nb);  // may throw: B is untouched until it succeeds
       B = std::move(nb);
@@ -1703,12 +1710,13 @@ struct okvisgpu_ctx {
     const size_t o_app = upl(B.asm_pp_items), o_asb = upl(B.asm_sb_items), o_appl = upl(B.asm_ppl_items);
     const size_t o_ti = upl(B.tile_items);
     const size_t o_cri = upl(B.chol_root_items), o_cui = upl(B.chol_upd_items), o_cub = upl(B.chol_upd_begin);
-    const size_t o_wsgap = upl(B.win_sgap), o_wbsp = upl(B.win_bsplit);
+    const size_t o_wsgap = upl(B.win_sgap), o_wbsp = upl(B.win_bsplit), o_wdef = upl(B.win_defoff);
     const size_t nf = std::max(1, B.f_total), nl3 = std::max<size_t>(1, (size_t)3 * D.n_lm);
     const size_t o_S = scratch(sizeof(double) * std::max<int64_t>(1, B.s_total));
     const size_t o_W = scratch(sizeof(double) * std::max<int64_t>(1, B.s_total));
     const size_t o_Linv = scratch(sizeof(double) * std::max<int64_t>(1, B.linv_total));
     const size_t o_fwd = scratch(sizeof(double) * std::max<int64_t>(1, B.fwd_total));
+    const size_t o_defer = scratch(sizeof(double) * std::max<int64_t>(1, B.defer_total));
     size_t of[10], ol[7];
     for (int i = 0; i < 10; ++i) of[i] = scratch(sizeof(double) * nf);
     for (int i = 0; i < 7; ++i) ol[i] = scratch(sizeof(double) * nl3);
@@ -1821,6 +1829,8 @@ struct okvisgpu_ctx {
     D.Linv = dp(o_Linv);
     D.win_linvoff = lp(o_wlinv);
     D.fwdF = dp(o_fwd);
+    D.chol_defer = dp(o_defer);
+    D.win_defoff = lp(o_wdef);
     D.win_fwdoff = lp(o_wfwd);
     double** fv[10] = {&D.sF, &D.diagF, &D.hdF, &D.gF, &D.rhsF, &D.yF, &D.gnF, &D.dgF, &D.vF, &D.stepF};
     for (int i = 0; i < 10; ++i) *fv[i] = dp(of[i]);
@@ -1863,11 +1873,12 @@ struct okvisgpu_ctx {
     // below half a window per CU the tile-parallel launches spread each window over many CUs; from
     // there the persistent kernel. (A wave-specialised kernel and a persistent variant with the
     // panel tiles in LDS were measured slower at every batch size and removed in round 4.)
-    int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 2 ? o.cholesky_schedule : 0;
-    if (sched == 0) sched = 2 * P.n_win >= cuCount ? 1 : 2;
+    int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 3 ? o.cholesky_schedule : 0;
+    if (sched == 0) sched = 2 * P.n_win < cuCount ? 2 : (B.any_split && P.n_win <= cuCount ? 3 : 1);
+    if (sched == 3 && !B.any_split) sched = 1;  // (no window with a nested-dissection split)
     // the persistent kernel keeps the window's rhs / y in dynamic LDS next to its static tiles:
     // a reduced dimension beyond what fits falls back to the tile-parallel launches
-    if (sched == 1 && !persistentFits()) sched = 2;
+    if ((sched == 1 || sched == 3) && !persistentFits()) sched = 2;
     if (sched != P.chol_schedule && iterGraph) {
       (void)hipGraphExecDestroy(iterGraph);
       iterGraph = nullptr;
@@ -2562,6 +2573,8 @@ int okvisgpu_get_stats(okvisgpu_ctx* c, okvisgpu_problem_stats* st) {
   st->n_visit_segments = P.n_seg;
   st->n_partial_blocks = P.n_part;
   st->arena_bytes = (int64_t)c->arenaBytes;
+  st->cholesky_split_windows = 0;
+  for (size_t w = 0; w + 1 < c->B.win_bsplit.size(); w += 2) st->cholesky_split_windows += c->B.win_bsplit[w + 1] > 0;
   return OKVISGPU_OK;
 }
 

@@ -139,7 +139,7 @@ class ProblemStats(C.Structure):
         "n_poses", "n_speed_biases", "n_landmarks", "n_landmarks_free", "n_extrinsics_free", "n_observations",
         "n_visits", "n_imu", "n_imu_samples", "n_pose_priors", "n_sb_priors", "n_relpose", "reduced_dim",
         "s_tiles_nonzero", "s_tiles_dense", "n_block_pairs", "n_visit_segments", "n_partial_blocks",
-        "arena_bytes")]
+        "arena_bytes", "cholesky_split_windows")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -386,6 +386,34 @@ def test_cholesky_schedules_agree(og, oracle, gpu_ctx):
     _close(res[1][0][0], so)
 
 
+def test_cholesky_schedules_agree_nested_dissection(og, oracle, gpu_ctx):
+    """S50 windows in a small batch are held in a nested-dissection order (runtime.cpp chooseNd):
+    the tile-parallel launches, the persistent kernel and the persistent kernel split over the two
+    parts (launch A per part, launch B for the separator) give bitwise-equal solves; the oracle
+    (natural order) agrees to the usual tolerance."""
+    ws = [og.SynthWindow(50, 2000, 16000, seed=s) for s in (33, 34)]
+    res = []
+    for sched in (1, 2, 3):
+        for w in ws:
+            w.reset()
+        opts = og.default_options(max_num_iterations=4, function_tolerance=0.0, gradient_tolerance=0.0,
+                                  parameter_tolerance=0.0, cholesky_schedule=sched)
+        gpu_ctx.set_problems([w.problem for w in ws])
+        st = gpu_ctx.stats()
+        assert st["cholesky_split_windows"] == len(ws) and st["cholesky_launches"] < 12, st
+        s = gpu_ctx.solve(opts, len(ws))
+        res.append((s, [w.poses().copy() for w in ws], [w.landmarks().copy() for w in ws]))
+    for r in res[1:]:
+        for k in range(len(ws)):
+            assert r[0][k]["final_cost"] == res[0][0][k]["final_cost"]
+            assert np.array_equal(r[1][k], res[0][1][k]) and np.array_equal(r[2][k], res[0][2][k])
+    ws[0].reset()
+    so = oracle.solve(ws[0].problem_ptr(), og.default_options(max_num_iterations=4, function_tolerance=0.0,
+                                                              gradient_tolerance=0.0, parameter_tolerance=0.0))
+    _close(res[0][0][0], so)
+    assert np.abs(res[0][1][0][:, :3] - ws[0].poses()[:, :3]).max() <= 1e-6
+
+
 def test_graph_file_solve_parity(og, oracle, gpu_ctx, tmp_path):
     """A window written as an okvis Component graph and loaded back (okvisgpu_graph_save / _load)
     solves on the GPU like the oracle on the same loaded arrays."""
