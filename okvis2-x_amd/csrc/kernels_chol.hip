@@ -471,10 +471,6 @@ __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li,
       double r[8], x[8], rl[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) r[k] = sA[i * kLd + c0 + k];
-      // Scheduling fences (scripts/ubench_ptile.hip): the row's loads retire here, and the look-ahead
-      // result and the factor's x are complete before their stores are issued; left to itself the
-      // compiler interleaves those stores and loads with the FP64 chain (22.4 -> 16.4 us per tile)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (s >= 1) {  // look-ahead update by sub-panel s-1: r -= L_i,s-1 L_(c0..c0+7),s-1^T
         // (c outer: the 8 independent chains r[m] interleave, so no FMA waits on the previous one's
         // result; every r[m] still sums over c in order, the same bits)
@@ -482,7 +478,6 @@ __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li,
         for (int c = 0; c < 8; ++c)
 #pragma unroll
           for (int m = 0; m < 8; ++m) r[m] -= xp[c] * sA[(c0 + m) * kLd + c0 - 8 + c];
-        asm volatile("" ::"v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]));
         if (i >= c0) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) sA[i * kLd + c0 + k] = r[k];
@@ -494,7 +489,6 @@ __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li,
         if (lane == 0) ldsReleaseL(&sFl[2], 1);
         break;
       }
-      asm volatile("" ::"v"(x[7]));
       CLK(23)
       storeRow8(sA, c0, x, i);
       if (lane == 0) {
@@ -890,7 +884,10 @@ __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem
 // still read it): the workgroup of the diagonal update (i,i) writes L_ik to the unused upper slot
 // (k,i) of W and applies rhs_i -= L_ik y_k; the backward substitution of this schedule reads L
 // there. The workgroup of a diagonal tile's last update factors it right after.
-__global__ __launch_bounds__(256) void k_chol_roots(const DevProblem* __restrict__ Pp) {
+// (launch bounds of two workgroups per CU: without them the compiler gives potrfTile<1> the
+// one-wave-per-SIMD register budget and emits a longer chain, 22.3 against 16.3 us per tile in
+// scripts/ubench_ptile.hip)
+__global__ __launch_bounds__(256, 2) void k_chol_roots(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int w = P.chol_root_items[3 * blockIdx.x], d = P.chol_root_items[3 * blockIdx.x + 1];
   const bool first = P.chol_root_items[3 * blockIdx.x + 2] != 0;
@@ -940,7 +937,7 @@ __device__ __forceinline__ void accToLds(double* s, const dbl4 acc[2][2], int t)
       for (int reg = 0; reg < 4; ++reg) s[(r0 + 16 * a + (lane >> 4) + 4 * reg) * kLd + c0 + 16 * b + (lane & 15)] = acc[a][b][reg];
 }
 
-__global__ __launch_bounds__(256) void k_chol_update(const DevProblem* __restrict__ Pp, int launch) {
+__global__ __launch_bounds__(256, 2) void k_chol_update(const DevProblem* __restrict__ Pp, int launch) {
   const DevProblem& P = *Pp;
   const int item = P.chol_upd_begin[launch] + blockIdx.x;
   const int4 it = reinterpret_cast<const int4*>(P.chol_upd_items)[item];

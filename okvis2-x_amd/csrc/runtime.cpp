@@ -1596,7 +1596,7 @@ struct okvisgpu_ctx {
       // (at most one window per CU, setOptions): the chain of a window's factorisation is the
       // latency there. The order is a function of the window and this flag only, so a window's
       // bits depend on the batch just through it.
-      nb.nd = (int)probs.size() <= cuCount;
+      nb.nd = (int)probs.size() < cuCount;
       if (const char* e = std::getenv("OKVISGPU_ND")) nb.nd = e[0] == '1';  // (development A/B)
       analyse(probs, constOverride, nb);  // may throw: B is untouched until it succeeds
       B = std::move(nb);
@@ -1868,13 +1868,16 @@ struct okvisgpu_ctx {
     d.min_relative_decrease = o.min_relative_decrease;
     d.min_lm_diagonal = o.min_lm_diagonal;
     d.max_lm_diagonal = o.max_lm_diagonal;
-    // Cholesky schedule (measured on MI355X, S50 windows, round 3: bench window-it/s of schedules
-    // 1 / 2 at 16: 20.3k / 24.6k, 64: 64.5k / 70.9k, 128: 102.2k / 92.8k, 192: 129.1k / 109.1k):
-    // below half a window per CU the tile-parallel launches spread each window over many CUs; from
-    // there the persistent kernel. (A wave-specialised kernel and a persistent variant with the
-    // panel tiles in LDS were measured slower at every batch size and removed in round 4.)
+    // Cholesky schedule (measured on MI355X, S50 windows, bench window-it/s, round 4 with the
+    // nested-dissection order (nd) below one window per CU: 64 windows: schedule 1 65.2k, 2 (nd)
+    // 72.2k; 128: 1 103.6k, 3 (nd) 107.9k, 2 (nd) 98.2k; 256: 1 159.7k, 3 (nd) 152.8k; 512: 1
+    // 186.5k, 3 (nd) 166.0k; gpurun_out r04g / r04h nd_probe): below half a window per CU the
+    // tile-parallel launches spread each window over many CUs; up to one window per CU the
+    // persistent kernel split over the two parts of the order; from there one persistent
+    // workgroup per window. (A wave-specialised kernel and a persistent variant with the panel
+    // tiles in LDS were measured slower at every batch size and removed in round 4.)
     int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 3 ? o.cholesky_schedule : 0;
-    if (sched == 0) sched = 2 * P.n_win < cuCount ? 2 : (B.any_split && P.n_win <= cuCount ? 3 : 1);
+    if (sched == 0) sched = 2 * P.n_win < cuCount ? 2 : (B.any_split && P.n_win < cuCount ? 3 : 1);
     if (sched == 3 && !B.any_split) sched = 1;  // (no window with a nested-dissection split)
     // the persistent kernel keeps the window's rhs / y in dynamic LDS next to its static tiles:
     // a reduced dimension beyond what fits falls back to the tile-parallel launches
