@@ -416,6 +416,19 @@ typedef struct okvisgpu_problem_stats {
 } okvisgpu_problem_stats;
 int okvisgpu_get_stats(okvisgpu_ctx* ctx, okvisgpu_problem_stats* stats);
 
+/* Host-only plan of one window's reduced system (no device, no context; for tests and tools): the
+ * state order a batch below one window per CU gives it (nested_dissection = 1) or the natural one
+ * (0), its tile pattern and the tile-parallel factorisation schedule. Any output may be NULL.
+ *   info[8]:        natural reduced dimension, S dimension (64-padded), tiles T, structurally
+ *                   non-zero tiles (after fill), launches (roots + updates), split tL, split tS
+ *                   (0 0: none), gap rows
+ *   tile_nz[T*T]:   the filled lower-triangular tile pattern (row-major, 1 = non-zero)
+ *   step_launch[T]: launch of step k's band updates (0: the step has none)
+ *   natural[dim]:   natural index of each row of S (-1: gap or padding row), dim = info[1]
+ * Pass tile_nz / step_launch / natural sized from a first call with them NULL. */
+int okvisgpu_plan_window(const okvisgpu_problem* problem, int32_t nested_dissection, int64_t* info,
+                         uint8_t* tile_nz, int32_t* step_launch, int32_t* natural);
+
 /* Copy device parameter values back into the caller's host arrays without solving. */
 int okvisgpu_get_params(okvisgpu_ctx* ctx);
 

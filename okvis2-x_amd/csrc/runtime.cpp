@@ -2581,6 +2581,38 @@ int okvisgpu_get_stats(okvisgpu_ctx* c, okvisgpu_problem_stats* st) {
   return OKVISGPU_OK;
 }
 
+int okvisgpu_plan_window(const okvisgpu_problem* p, int32_t nested_dissection, int64_t* info, uint8_t* tile_nz,
+                         int32_t* step_launch, int32_t* natural) {
+  if (!p) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  try {
+    HostBatch B;
+    B.nd = nested_dissection != 0;
+    analyse({p}, {}, B);
+    const int T = B.tileT[0], fpad = B.win_fpad[0];
+    const auto& nz = B.tileNz[0];
+    std::vector<int> L, last;
+    const int nl = cholSchedule(nz, T, L, last);
+    if (info) {
+      int64_t nnz = 0;
+      for (uint8_t v : nz) nnz += v;
+      const int64_t v[8] = {B.win_fnat[0], fpad, T, nnz, nl, B.win_bsplit[0], B.win_bsplit[1], B.win_sgap[1]};
+      std::copy(v, v + 8, info);
+    }
+    if (tile_nz) std::copy(nz.begin(), nz.end(), tile_nz);
+    if (step_launch)
+      for (int k = 0; k < T; ++k) {
+        bool any = false;
+        for (int i = k + 1; i < T && !any; ++i) any = nz[(size_t)i * T + k] != 0;
+        step_launch[k] = any ? L[k] : 0;
+      }
+    if (natural)
+      for (int r = 0; r < fpad; ++r) natural[r] = r < B.win_fdim[0] ? B.f_nat[r] : -1;
+    return OKVISGPU_OK;
+  } catch (const std::exception&) {
+    return OKVISGPU_ERR_INVALID_ARGUMENT;
+  }
+}
+
 int okvisgpu_evaluate(okvisgpu_ctx* c, int32_t window, double* cost) {
   if (!c) return OKVISGPU_ERR_INVALID_ARGUMENT;
   if (!c->haveProblem) return fail(c, OKVISGPU_ERR_NO_PROBLEM, "no problem set");

@@ -170,7 +170,7 @@ EXPORTED_SYMBOLS = [
     "okvisgpu_time_kernel", "okvisgpu_eval_relpose", "okvisgpu_twopose_compute",
     "okvisgpu_graph_load", "okvisgpu_graph_problem", "okvisgpu_graph_ids", "okvisgpu_graph_destroy",
     "okvisgpu_graph_save", "okvisgpu_get_stats", "okvisgpu_synth_true_extrinsics", "okvisgpu_imu_append",
-    "okvisgpu_eval_host",
+    "okvisgpu_eval_host", "okvisgpu_plan_window",
 ]
 N_PHASES = 15
 
@@ -229,10 +229,36 @@ def lib():
         L.okvisgpu_graph_destroy.argtypes = [C.c_void_p]
         L.okvisgpu_graph_save.argtypes = [C.POINTER(Problem), _lp, C.c_char_p]
         L.okvisgpu_get_stats.argtypes = [C.c_void_p, C.POINTER(ProblemStats)]
+        L.okvisgpu_plan_window.argtypes = [C.POINTER(Problem), C.c_int32, _lp, C.POINTER(C.c_uint8), _ip, _ip]
         L.okvisgpu_imu_append.argtypes = [C.c_void_p, C.POINTER(ImuAppendBatch), _ip]
         L.okvisgpu_twopose_compute.argtypes = [C.c_void_p, C.POINTER(TwoPoseEdges), _dp, _dp, _dp, _dp, _dp]
         _lib = L
     return _lib
+
+
+def plan_window(problem, nested_dissection):
+    """okvisgpu_plan_window (host only): the window's state order, filled tile pattern and
+    tile-parallel factorisation schedule."""
+    L = lib()
+    info = (C.c_int64 * 8)()
+    pp = C.byref(problem) if isinstance(problem, Problem) else problem
+    rc = L.okvisgpu_plan_window(pp, int(nested_dissection), info, None, None, None)
+    if rc != 0:
+        raise RuntimeError(f"okvisgpu_plan_window failed ({rc})")
+    keys = ("reduced_dim", "s_dim", "tiles", "nonzero_tiles", "launches", "split_tL", "split_tS", "gap_rows")
+    out = {k: int(v) for k, v in zip(keys, info)}
+    T, D = out["tiles"], out["s_dim"]
+    nz = np.zeros(T * T, dtype=np.uint8)
+    launch = np.zeros(T, dtype=np.int32)
+    nat = np.zeros(D, dtype=np.int32)
+    rc = L.okvisgpu_plan_window(pp, int(nested_dissection), info, nz.ctypes.data_as(C.POINTER(C.c_uint8)),
+                                launch.ctypes.data_as(_ip), nat.ctypes.data_as(_ip))
+    if rc != 0:
+        raise RuntimeError(f"okvisgpu_plan_window failed ({rc})")
+    out["tile_nz"] = nz.reshape(T, T)
+    out["step_launch"] = launch
+    out["natural"] = nat
+    return out
 
 
 def default_options(**kw) -> Options:
