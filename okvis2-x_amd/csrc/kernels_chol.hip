@@ -478,6 +478,11 @@ __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li,
         for (int c = 0; c < 8; ++c)
 #pragma unroll
           for (int m = 0; m < 8; ++m) r[m] -= xp[c] * sA[(c0 + m) * kLd + c0 - 8 + c];
+        // Scheduling fence: the look-ahead result is complete before its stores are issued (and,
+        // below, x before the row stores). Without these the compiler interleaves the stores and
+        // the next loads with the FP64 chain: 22.6 against 15.9 us per tile
+        // (scripts/ubench_ptile.hip, "product" vs "consume-only")
+        asm volatile("" ::"v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]));
         if (i >= c0) {
 #pragma unroll
           for (int k = 0; k < 8; ++k) sA[i * kLd + c0 + k] = r[k];
@@ -489,6 +494,7 @@ __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li,
         if (lane == 0) ldsReleaseL(&sFl[2], 1);
         break;
       }
+      asm volatile("" ::"v"(x[7]));
       CLK(23)
       storeRow8(sA, c0, x, i);
       if (lane == 0) {
