@@ -118,7 +118,10 @@ __device__ __noinline__ bool potrfExp(const double* Sg, int64_t ld, double* Li, 
 }
 }  // namespace okg
 
-template <int EXP>  // -1: the product's potrfTile, else potrfExp<EXP>
+// -1: the product's potrfTile as the tile-parallel kernels instantiate it, -2: as the persistent
+// kernel does; each through an instantiation of its own (3, 19: one caller, like the product's, so
+// that the register budget and the code match the product build), else potrfExp<EXP>
+template <int EXP>
 __global__ __launch_bounds__(256, 2) void kptile(const double* A, double* Li, double* work, int reps,
                                                  unsigned long long* ticks) {
   __shared__ double sA[okg::kTile * okg::kLd];
@@ -134,9 +137,11 @@ __global__ __launch_bounds__(256, 2) void kptile(const double* A, double* Li, do
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     if (EXP >= 0)
       okg::potrfExp<(EXP < 0 ? 0 : EXP)>(A, 64, Li + (size_t)blockIdx.x * 4096, work + (size_t)blockIdx.x * 64, sA, sX, sy, sRl, sFl, t);
-    else
-      okg::potrfTile<1>(A, 64, Li + (size_t)blockIdx.x * 4096, work + (size_t)blockIdx.x * 64, sA, sX, sy, sRl, sFl, t,
+    else if (EXP == -1)
+      okg::potrfTile<3>(A, 64, Li + (size_t)blockIdx.x * 4096, work + (size_t)blockIdx.x * 64, sA, sX, sy, sRl, sFl, t,
                         false);
+    else
+      okg::potrfTile<19>(A, 64, Li + (size_t)blockIdx.x * 4096, nullptr, sA, sX, sy, sRl, sFl, t, false);
     __syncthreads();
     tot += __builtin_amdgcn_s_memrealtime() - t0;
   }
@@ -193,7 +198,8 @@ int main() {
   (void)hipMalloc(&dW, 8 * 64 * (size_t)nb);
   (void)hipMalloc(&dT, 8 * nb);
   (void)hipMemcpy(dA, A.data(), 8 * 4096, hipMemcpyHostToDevice);
-  run<-1>("product", dA, dL, dW, dT, A);
+  run<-1>("product (tile-parallel)", dA, dL, dW, dT, A);
+  run<-2>("product (persistent)", dA, dL, dW, dT, A);
   run<2>("fences", dA, dL, dW, dT, A);
   run<3>("consume-only", dA, dL, dW, dT, A);
   run<4>("stamps-only", dA, dL, dW, dT, A);
