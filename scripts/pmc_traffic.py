@@ -21,7 +21,7 @@ for path in sys.argv[3:]:
         name = name.replace(", false>", ">").replace(", true>", ">").replace("<false>", "").replace("<true>", "")
         # the specialised k_lm_visit<mode> kernels under bench.py's table names
         name = {"k_lm_visit<1>": "k_lm_visit", "k_lm_visit<2>": "k_lm_visit_prep", "k_lm_visit<0>": "k_lm_visit_init",
-                "k_lm_prep_windows": "k_lm_visit_prep"}.get(name, name)
+                "k_lm_prep_windows": "k_lm_visit_prep", "k_cholesky<0>": "k_cholesky"}.get(name, name)
         vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 kern = {}
 for k, d in vals.items():
