@@ -21,61 +21,64 @@
 
 namespace okg {
 
-#ifndef OKG_RB
-#define OKG_RB 256
-#endif
-constexpr int kRB = OKG_RB;  // per-window workgroup size (k_reduce, k_gradnorm, k_dogleg)
-static_assert((kRB & (kRB - 1)) == 0 && kRB >= 64 && kRB <= 1024,
-              "OKG_RB must be a power of two in [64, 1024] (blockSum / blockMax tree reductions)");
+// Per-window workgroup size of k_reduce, k_gradnorm and k_dogleg: 256 threads for batches, 1,024
+// when the batch has at most a quarter window per CU (a single window's reductions are chains of
+// dependent loads per thread: four times the threads, a quarter of the chain). A power of two in
+// [64, 1024] (the tree reductions); the reduction order follows it, so a window's bits depend on
+// the batch size only through this choice (and the Cholesky order, runtime.cpp build).
+constexpr int kRBBatch = 256, kRBFew = 1024;
+__host__ __device__ constexpr bool fewWindows(int nWin, int cuCount) { return 4 * nWin <= cuCount; }
 
 // Fixed-order tree reductions over the workgroup. The barriers order LDS only (ldsBarrier): a
 // __syncthreads() also waited for every global store still in flight (k_dogleg's Plus pass leaves
 // thousands), and N values reduced together share one tree's barriers: per value the same
 // additions in the same order as a separate tree, so the same bits.
-template <int N>
-__device__ __forceinline__ void blockSumN(double (&v)[N], double* sh) {  // sh: N * kRB doubles
+template <int RB, int N>
+__device__ __forceinline__ void blockSumN(double (&v)[N], double* sh) {  // sh: N * RB doubles
   const int t = threadIdx.x;
 #pragma unroll
-  for (int n = 0; n < N; ++n) sh[n * kRB + t] = v[n];
+  for (int n = 0; n < N; ++n) sh[n * RB + t] = v[n];
   ldsBarrier();
-  for (int s = kRB / 2; s > 0; s >>= 1) {
+  for (int s = RB / 2; s > 0; s >>= 1) {
     if (t < s) {
 #pragma unroll
-      for (int n = 0; n < N; ++n) sh[n * kRB + t] += sh[n * kRB + t + s];
+      for (int n = 0; n < N; ++n) sh[n * RB + t] += sh[n * RB + t + s];
     }
     ldsBarrier();
   }
 #pragma unroll
-  for (int n = 0; n < N; ++n) v[n] = sh[n * kRB];
+  for (int n = 0; n < N; ++n) v[n] = sh[n * RB];
   ldsBarrier();
 }
+template <int RB>
 __device__ __forceinline__ double blockSum(double v, double* sh) {
   double a[1] = {v};
-  blockSumN<1>(a, sh);
+  blockSumN<RB, 1>(a, sh);
   return a[0];
 }
-// Strided per-thread loop over i = b + t, b + t + kRB, ... < e with the loads of U consecutive
+// Strided per-thread loop over i = b + t, b + t + RB, ... < e with the loads of U consecutive
 // iterations issued before any of them is consumed. A window's reductions run in one workgroup, so a
 // single window is a chain of dependent loads per thread; batching shortens it U-fold. use() sees the
 // elements in the order of the plain loop, so every sum is bitwise the same.
-template <int U, class Load, class Use>
+template <int RB, int U, class Load, class Use>
 __device__ __forceinline__ void stridedBatched(int b, int e, Load load, Use use) {
   int i = b + (int)threadIdx.x;
-  for (; i + (U - 1) * kRB < e; i += U * kRB) {
+  for (; i + (U - 1) * RB < e; i += U * RB) {
     decltype(load(i)) v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = load(i + u * kRB);
+    for (int u = 0; u < U; ++u) v[u] = load(i + u * RB);
 #pragma unroll
-    for (int u = 0; u < U; ++u) use(i + u * kRB, v[u]);
+    for (int u = 0; u < U; ++u) use(i + u * RB, v[u]);
   }
-  for (; i < e; i += kRB) use(i, load(i));
+  for (; i < e; i += RB) use(i, load(i));
 }
 
+template <int RB>
 __device__ __forceinline__ double blockMax(double v, double* sh) {
   const int t = threadIdx.x;
   sh[t] = v;
   ldsBarrier();
-  for (int s = kRB / 2; s > 0; s >>= 1) {
+  for (int s = RB / 2; s > 0; s >>= 1) {
     if (t < s) sh[t] = fmax(sh[t], sh[t + s]);
     ldsBarrier();
   }
@@ -251,6 +254,7 @@ __device__ void finalizeIteration(const DevProblem& P, WinState& s) {
 // J*v reductions of window w (once per GN step): jcc, jgg, jcg and the Cauchy alpha =
 // |gradient_|^2 / jcc, stored by thread 0 in the window state; every thread gets alpha.
 // Reprojection rows and landmark gradients come as the landmark groups' sums (k_lm_backsub_jv).
+template <int RB>
 __device__ double reduceJv(const DevProblem& P, int w, WinState& s, double* sh) {
   const int t = threadIdx.x;
   const int ib = P.win_imu_range[2 * w], ie = P.win_imu_range[2 * w + 1];
@@ -263,21 +267,21 @@ __device__ double reduceJv(const DevProblem& P, int w, WinState& s, double* sh) 
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     double acc = 0.0;
-    for (int g = gb + t; g < ge; g += kRB) acc += P.grp_red[(size_t)g * kGrpRed + k];
-    for (int f = ib + t; f < ie; f += kRB) acc += P.imu_jv[(size_t)k * P.n_fac + f];
-    for (int f = hb + t; f < he; f += kRB) acc += P.imu_jv[(size_t)k * P.n_fac + f];
-    for (int i = pb + t; i < pe; i += kRB) acc += P.pp_jv[(size_t)k * P.n_pprior + i];
-    for (int i = sbb + t; i < sbe; i += kRB) acc += P.sbp_jv[(size_t)k * P.n_sbprior + i];
-    for (int i = rpb + t; i < rpe; i += kRB) acc += P.rp_jv[(size_t)k * P.n_relpose + i];
+    for (int g = gb + t; g < ge; g += RB) acc += P.grp_red[(size_t)g * kGrpRed + k];
+    for (int f = ib + t; f < ie; f += RB) acc += P.imu_jv[(size_t)k * P.n_fac + f];
+    for (int f = hb + t; f < he; f += RB) acc += P.imu_jv[(size_t)k * P.n_fac + f];
+    for (int i = pb + t; i < pe; i += RB) acc += P.pp_jv[(size_t)k * P.n_pprior + i];
+    for (int i = sbb + t; i < sbe; i += RB) acc += P.sbp_jv[(size_t)k * P.n_sbprior + i];
+    for (int i = rpb + t; i < rpe; i += RB) acc += P.rp_jv[(size_t)k * P.n_relpose + i];
     a[k] = acc;
   }
-  blockSumN<3>(a, sh);
+  blockSumN<RB, 3>(a, sh);
   // |gradient_|^2 over the window (f-vector + free landmarks)
   double g2 = 0.0;
   const int fo = P.win_foff[w], fd = P.win_fdim[w];
-  for (int e = t; e < fd; e += kRB) g2 += P.dgF[fo + e] * P.dgF[fo + e];
-  for (int g = gb + t; g < ge; g += kRB) g2 += P.grp_red[(size_t)g * kGrpRed + 3];
-  g2 = blockSum(g2, sh);
+  for (int e = t; e < fd; e += RB) g2 += P.dgF[fo + e] * P.dgF[fo + e];
+  for (int g = gb + t; g < ge; g += RB) g2 += P.grp_red[(size_t)g * kGrpRed + 3];
+  g2 = blockSum<RB>(g2, sh);
   const double alpha = g2 / a[0];
   if (t == 0) {
     s.jcc = a[0];
@@ -288,12 +292,13 @@ __device__ double reduceJv(const DevProblem& P, int w, WinState& s, double* sh) 
   return alpha;
 }
 
-__global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ Pp, int mode) {
+template <int RB>
+__global__ __launch_bounds__(RB) void k_reduce(const DevProblem* __restrict__ Pp, int mode) {
   const DevProblem& P = *Pp;
   const int w = blockIdx.x;
   WinState& s = P.st[w];
   if (s.done) return;
-  __shared__ double sh[3 * kRB];
+  __shared__ double sh[3 * RB];
   const int t = threadIdx.x;
   const int ob = P.win_obs_range[2 * w], oe = P.win_obs_range[2 * w + 1];
   const int ib = P.win_imu_range[2 * w], ie = P.win_imu_range[2 * w + 1];
@@ -307,35 +312,35 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
     double c = 0.0, cf = 0.0;
     struct OC { double c; uint8_t f; };
     const double* oc = P.obs_cost[lb];
-    stridedBatched<8>(ob, oe, [&](int o) { return OC{oc[o], P.obs_flags[o]}; },
+    stridedBatched<RB, 8>(ob, oe, [&](int o) { return OC{oc[o], P.obs_flags[o]}; },
                       [&](int, const OC& v) {
                         if (v.f & 2) cf += v.c;
                         else c += v.c;
                       });
-    for (int f = ib + t; f < ie; f += kRB) {
+    for (int f = ib + t; f < ie; f += RB) {
       if (P.imu_flags[f] & 2) cf += P.imu_cost[lb][f];
       else c += P.imu_cost[lb][f];
     }
     const int hb = P.win_host_range[2 * w], he = P.win_host_range[2 * w + 1];
-    for (int f = hb + t; f < he; f += kRB) {
+    for (int f = hb + t; f < he; f += RB) {
       if (P.imu_flags[f] & 2) cf += P.imu_cost[lb][f];
       else c += P.imu_cost[lb][f];
     }
-    for (int i = pb + t; i < pe; i += kRB) {
+    for (int i = pb + t; i < pe; i += RB) {
       if (P.pose_f[P.pp_block[i]] < 0) cf += P.pp_cost[lb][i];
       else c += P.pp_cost[lb][i];
     }
-    for (int i = sbb + t; i < sbe; i += kRB) {
+    for (int i = sbb + t; i < sbe; i += RB) {
       if (P.sb_f[P.sbp_block[i]] < 0) cf += P.sbp_cost[lb][i];
       else c += P.sbp_cost[lb][i];
     }
-    for (int i = rpb + t; i < rpe; i += kRB) {
+    for (int i = rpb + t; i < rpe; i += RB) {
       if (P.rp_flags[i] & 2) cf += P.rp_cost[lb][i];
       else c += P.rp_cost[lb][i];
     }
     {
       double r2[2] = {c, cf};
-      blockSumN<2>(r2, sh);
+      blockSumN<RB, 2>(r2, sh);
       c = r2[0];
       cf = r2[1];
     }
@@ -393,23 +398,24 @@ __global__ __launch_bounds__(kRB) void k_reduce(const DevProblem* __restrict__ P
 
   // J*v reductions (once per GN step)
   if (!(s.need_gn && !s.gn_failed)) return;
-  reduceJv(P, w, s, sh);
+  reduceJv<RB>(P, w, s, sh);
 }
 
 // |x - Plus(x, -g)| and |x| over the window's active blocks; gradient tolerance test.
-__global__ __launch_bounds__(kRB) void k_gradnorm(const DevProblem* __restrict__ Pp, int lin_mode) {
+template <int RB>
+__global__ __launch_bounds__(RB) void k_gradnorm(const DevProblem* __restrict__ Pp, int lin_mode) {
   const DevProblem& P = *Pp;
   const int w = blockIdx.x;
   WinState& s = P.st[w];
   if (s.done) return;
   if (lin_mode == 1 && !s.accepted) return;
-  __shared__ double sh[3 * kRB];
+  __shared__ double sh[3 * RB];
   const int t = threadIdx.x;
   const int xs = s.xcur;
   const int foff = P.win_foff[w];
   double mx = 0.0, g2 = 0.0, x2 = 0.0;
   const int p0 = P.win_pose_range[2 * w], p1 = P.win_pose_range[2 * w + 1];
-  for (int p = p0 + t; p < p1; p += kRB) {
+  for (int p = p0 + t; p < p1; p += RB) {
     if (!P.pose_active[p]) continue;
     const double* x = P.pose[xs] + 7 * (size_t)p;
     for (int k = 0; k < 7; ++k) x2 += x[k] * x[k];
@@ -427,7 +433,7 @@ __global__ __launch_bounds__(kRB) void k_gradnorm(const DevProblem* __restrict__
     }
   }
   const int s0 = P.win_sb_range[2 * w], s1 = P.win_sb_range[2 * w + 1];
-  for (int b = s0 + t; b < s1; b += kRB) {
+  for (int b = s0 + t; b < s1; b += RB) {
     if (!P.sb_active[b]) continue;
     const double* x = P.sb[xs] + 9 * (size_t)b;
     const double* g = P.gF + foff + P.sb_f[b];
@@ -440,7 +446,7 @@ __global__ __launch_bounds__(kRB) void k_gradnorm(const DevProblem* __restrict__
   }
   const int l0 = P.win_lm_range[2 * w], l1 = P.win_lm_range[2 * w + 1];
   struct LX { double x[4], g[3]; uint8_t f; };
-  stridedBatched<4>(l0, l1,
+  stridedBatched<RB, 4>(l0, l1,
                     [&](int l) {
                       LX v;
                       v.f = P.lm_free[l];
@@ -457,10 +463,10 @@ __global__ __launch_bounds__(kRB) void k_gradnorm(const DevProblem* __restrict__
                         g2 += d * d;
                       }
                     });
-  mx = blockMax(mx, sh);
+  mx = blockMax<RB>(mx, sh);
   {
     double r2[2] = {g2, x2};
-    blockSumN<2>(r2, sh);
+    blockSumN<RB, 2>(r2, sh);
     g2 = r2[0];
     x2 = r2[1];
   }
@@ -485,12 +491,13 @@ __global__ __launch_bounds__(kRB) void k_gradnorm(const DevProblem* __restrict__
 }
 
 // One workgroup per window: GN failure handling, traditional dogleg step, Plus into X[1-xcur].
-__global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ Pp) {
+template <int RB>
+__global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
   const int w = blockIdx.x;
   WinState& s = P.st[w];
   if (s.done) return;
-  __shared__ double sh[3 * kRB];
+  __shared__ double sh[3 * RB];
   __shared__ int sflag;
   const int t = threadIdx.x;
   const bool sflagGn = s.need_gn && !s.gn_failed;  // (read before thread 0 updates the state)
@@ -530,19 +537,19 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
   // a new GN step: its J*v reduction first (formerly k_reduce R_JV, one launch fewer per
   // iteration; the same workgroup per window, so a barrier orders it)
   double alpha = s.alpha;
-  if (sflagGn) alpha = reduceJv(P, w, s, sh);
+  if (sflagGn) alpha = reduceJv<RB>(P, w, s, sh);
   const int foff = P.win_foff[w], fd = P.win_fdim[w];
   const int l0 = P.win_lm_range[2 * w], l1 = P.win_lm_range[2 * w + 1];
   // pass 1: norms (f-blocks here, landmarks as the landmark groups' sums of k_lm_backsub_jv)
   double gg = 0.0, nn = 0.0, gn = 0.0;
-  for (int e = t; e < fd; e += kRB) {
+  for (int e = t; e < fd; e += RB) {
     const double a = P.dgF[foff + e], b = P.gnF[foff + e];
     gg += a * a;
     nn += b * b;
     gn += a * b;
   }
   const int gb = P.win_lmg_range[2 * w], ge = P.win_lmg_range[2 * w + 1];
-  for (int g = gb + t; g < ge; g += kRB) {
+  for (int g = gb + t; g < ge; g += RB) {
     const double* r = P.grp_red + (size_t)g * kGrpRed;
     gg += r[3];
     nn += r[4];
@@ -550,7 +557,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
   }
   {
     double r3[3] = {gg, nn, gn};
-    blockSumN<3>(r3, sh);
+    blockSumN<RB, 3>(r3, sh);
     gg = r3[0];
     nn = r3[1];
     gn = r3[2];
@@ -581,7 +588,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
   const int p0 = P.win_pose_range[2 * w], p1 = P.win_pose_range[2 * w + 1];
   // (every operand of a block is loaded before its first store: the stores may alias the
   // f-vectors for the compiler, and a single window is a chain of such rounds)
-  for (int p = p0 + t; p < p1; p += kRB) {
+  for (int p = p0 + t; p < p1; p += RB) {
     const int pf = P.pose_f[p];
     if (pf < 0) continue;
     double dg[6], gn[6], dia[6], sc[6], g[6], x[7];
@@ -613,7 +620,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
     }
   }
   const int b0 = P.win_sb_range[2 * w], b1 = P.win_sb_range[2 * w + 1];
-  for (int b = b0 + t; b < b1; b += kRB) {
+  for (int b = b0 + t; b < b1; b += RB) {
     const int sf = P.sb_f[b];
     if (sf < 0) continue;
     double* y = P.sb[xd] + 9 * (size_t)b;
@@ -639,7 +646,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
     }
   }
   struct LS { double x[4], dg[3], gn[3], dia[3], sl[3], g[3]; uint8_t f; };
-  stridedBatched<4>(l0, l1,
+  stridedBatched<RB, (RB >= 1024 ? 1 : 4)>(l0, l1,
                     [&](int l) {
                       LS v;
                       v.f = P.lm_free[l];
@@ -671,7 +678,7 @@ __global__ __launch_bounds__(kRB) void k_dogleg(const DevProblem* __restrict__ P
                     });
   {
     double r3[3] = {sn2, dn2, jr};
-    blockSumN<3>(r3, sh);
+    blockSumN<RB, 3>(r3, sh);
     sn2 = r3[0];
     dn2 = r3[1];
     jr = r3[2];
@@ -707,13 +714,17 @@ void launch_jv(const DevProblem& P, hipStream_t s) {
   if (n > 0) hipLaunchKernelGGL(k_jv, dim3((n + 15) / 16), dim3(256), 0, s, P.self);
 }
 void launch_reduce(const DevProblem& P, int mode, hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce, dim3(P.n_win), dim3(kRB), 0, s, P.self, mode);
+  if (fewWindows(P.n_win, P.cu_count)) hipLaunchKernelGGL(k_reduce<kRBFew>, dim3(P.n_win), dim3(kRBFew), 0, s, P.self, mode);
+  else hipLaunchKernelGGL(k_reduce<kRBBatch>, dim3(P.n_win), dim3(kRBBatch), 0, s, P.self, mode);
 }
 void launch_gradnorm(const DevProblem& P, int lin_mode, hipStream_t s) {
-  hipLaunchKernelGGL(k_gradnorm, dim3(P.n_win), dim3(kRB), 0, s, P.self, lin_mode);
+  if (fewWindows(P.n_win, P.cu_count))
+    hipLaunchKernelGGL(k_gradnorm<kRBFew>, dim3(P.n_win), dim3(kRBFew), 0, s, P.self, lin_mode);
+  else hipLaunchKernelGGL(k_gradnorm<kRBBatch>, dim3(P.n_win), dim3(kRBBatch), 0, s, P.self, lin_mode);
 }
 void launch_dogleg(const DevProblem& P, hipStream_t s) {
-  hipLaunchKernelGGL(k_dogleg, dim3(P.n_win), dim3(kRB), 0, s, P.self);
+  if (fewWindows(P.n_win, P.cu_count)) hipLaunchKernelGGL(k_dogleg<kRBFew>, dim3(P.n_win), dim3(kRBFew), 0, s, P.self);
+  else hipLaunchKernelGGL(k_dogleg<kRBBatch>, dim3(P.n_win), dim3(kRBBatch), 0, s, P.self);
 }
 
 // Write-back staging: a window whose current parameters are set 1 gets them copied into set 0, so
