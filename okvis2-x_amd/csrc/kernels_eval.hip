@@ -580,35 +580,39 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
       }
       __syncthreads();
       ICLK(6)
-      // ---- Q: the two product chains (every lane computes them; lane 0 stores)
+      // ---- Q: the two product chains. Delta_q on every lane (lane 0 stores it); cross_ distributed,
+      // lane e < 9 owning entry e = (r, c): each step needs column c of the previous cross_ (three
+      // shuffles inside the group) instead of the whole 3x3 product on every lane. Same expressions
+      // per entry as mm3, so the same bits.
       {
       Q cdq{carry[0], carry[1], carry[2], carry[3]};
-      double cross[9];
-      for (int i = 0; i < 9; ++i) cross[i] = carry[4 + i];
+      const int er = min(l, 8) / 3, ec = min(l, 8) % 3, gbase = threadIdx.x & ~(kImuGroup - 1);
+      double crs = carry[4 + min(l, 8)];
       if (l == 0) {
         q1[0] = cdq.x; q1[1] = cdq.y; q1[2] = cdq.z; q1[3] = cdq.w;
-        for (int i = 0; i < 9; ++i) cr[i] = cross[i];
       }
+      if (l < 9) cr[l] = crs;
       for (int k = 0; k < nk; ++k) {
         const double* R = rec + k * kStepRec;
         const double dt = R[0];
         if (dt > 0.0) {  // uniform over the group
           cdq = qmul(cdq, Q{R[1], R[2], R[3], R[4]});
-          double Rdqi[9], tmp[9];
-          for (int i = 0; i < 9; ++i) Rdqi[i] = R[17 + i];
-          mm3(Rdqi, cross, tmp);
-          for (int i = 0; i < 9; ++i) cross[i] = tmp[i] + R[8 + i] * dt;
+          const double b0 = __shfl(crs, gbase + ec, 64), b1 = __shfl(crs, gbase + 3 + ec, 64),
+                       b2 = __shfl(crs, gbase + 6 + ec, 64);
+          const double* a = R + 17 + 3 * er;
+          const double tmp = a[0] * b0 + a[1] * b1 + a[2] * b2;
+          crs = tmp + R[8 + 3 * er + ec] * dt;
         }
         if (l == 0) {
           double* qo = q1 + 4 * (k + 1);
           qo[0] = cdq.x; qo[1] = cdq.y; qo[2] = cdq.z; qo[3] = cdq.w;
-          for (int i = 0; i < 9; ++i) cr[9 * (k + 1) + i] = cross[i];
         }
+        if (l < 9) cr[9 * (k + 1) + l] = crs;
       }
       if (l == 0) {
         carry[0] = cdq.x; carry[1] = cdq.y; carry[2] = cdq.z; carry[3] = cdq.w;
-        for (int i = 0; i < 9; ++i) carry[4 + i] = cross[i];
       }
+      if (l < 9) carry[4 + l] = crs;
       }
       __syncthreads();
       ICLK(7)
