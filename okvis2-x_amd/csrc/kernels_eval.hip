@@ -390,6 +390,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   }
   const auto parp = gmem(P.imu_par + 7 * wR);  // (read where needed: nothing held across the chain)
   const int64_t tsLast = gmem(P.imu_ts)[max(send - 1, 0)];
+  const int nTot = gmem(P.imu_sbegin)[P.n_imu];  // samples of the batch (bounds of the cache warm-up)
   asm volatile("" ::"v"(flR), "v"(blkR.y), "v"(t0), "v"(t1), "v"(st0), "v"(st1), "v"(bref[0]), "v"(bref[5]),
                "v"(sDone), "v"(sCand), "v"(sX), "v"(sL), "v"(tsLast));
   const bool live = inR && (APPEND || ((sDone == 0) & (mode != 1 || sCand != 0) & !((flR & 2) && mode < 2)));
@@ -580,6 +581,18 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
       }
       __syncthreads();
       ICLK(6)
+      // Warm the caches with the next chunk's samples (5 samples of 48 B and their time stamps per
+      // group): an LDS-DMA touch per 64-byte line, issued now so that its memory latency overlaps
+      // this chunk's phases instead of heading the next step-record phase (which read them from
+      // HBM with 4 of 16 lanes active). The DMA's data lands in group 0's F_delta block, dead until
+      // the I phase writes it (the barrier after the Q phase waits for the DMA); never read.
+      if (c0 + kImuK < Nmax) {
+        const int nb = min(sbeg + c0 + kImuK, nTot - 1);
+        const void* src = l < 4 ? (const void*)(P.imu_ga + min(6 * (int64_t)nb + 8 * l, 6 * (int64_t)nTot - 1))
+                                : (const void*)(P.imu_ts + min(nb + 8 * (l & 1), nTot - 1));
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(sAll[0] + kLF), 4, 0, 0);
+      }
       // ---- Q: the two product chains. Delta_q on every lane (lane 0 stores it); cross_ distributed,
       // lane e < 9 owning entry e = (r, c): each step needs column c of the previous cross_ (three
       // shuffles inside the group) instead of the whole 3x3 product on every lane. Same expressions
