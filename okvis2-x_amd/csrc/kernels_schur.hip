@@ -1154,17 +1154,11 @@ void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s) {
     else hipLaunchKernelGGL((k_lm_visit<2, false>), g, b, 0, s, P.self);
   }
 }
-void launch_assemble_pp_heavy(const DevProblem& P, hipStream_t s) {
+void launch_assemble_pp(const DevProblem& P, hipStream_t s) {
   if (P.n_asm_pp > 0) hipLaunchKernelGGL(k_assemble_pp, dim3((P.n_asm_pp + 3) / 4), dim3(256), 0, s, P.self);
-}
-void launch_assemble_pp_light(const DevProblem& P, hipStream_t s) {
   if (P.n_asm_ppl > 0)
     hipLaunchKernelGGL(k_assemble_pp_light, dim3((P.n_asm_ppl + 256 / kPplLanes - 1) / (256 / kPplLanes)), dim3(256), 0,
                        s, P.self);
-}
-void launch_assemble_pp(const DevProblem& P, hipStream_t s) {
-  launch_assemble_pp_heavy(P, s);
-  launch_assemble_pp_light(P, s);
 }
 void launch_assemble_sb(const DevProblem& P, hipStream_t s) {
   if (P.n_asm_sb > 0) hipLaunchKernelGGL(k_assemble_sb, dim3((P.n_asm_sb + 3) / 4), dim3(256), 0, s, P.self);

@@ -35,8 +35,6 @@ void launch_zero_S(const DevProblem& P, hipStream_t s, int tail = 0);
 void launch_assemble(const DevProblem& P, hipStream_t s);
 void launch_lm_backsub(const DevProblem& P, hipStream_t s);  // kernels_backsub.hip: + landmark dogleg vectors, J*v
 void launch_assemble_pp(const DevProblem& P, hipStream_t s);
-void launch_assemble_pp_heavy(const DevProblem& P, hipStream_t s);  // (the two halves of launch_assemble_pp:
-void launch_assemble_pp_light(const DevProblem& P, hipStream_t s);  //  disjoint pairs, any order)
 void launch_assemble_sb(const DevProblem& P, hipStream_t s);
 void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s);  // 0/1: linearisation, 2: GN prep
 void launch_gn_finalize(const DevProblem& P, hipStream_t s);

@@ -2032,15 +2032,13 @@ struct okvisgpu_ctx {
       HIPCHK(hipStreamWaitEvent(stream, e, 0));
     };
     // Gauss-Newton system: the stale Z rebuilt (few windows after the first iteration), then the
-    // three assembly kernels on three streams (disjoint pairs of S)
+    // assembly kernels and the clearing of the tile entries they do not write, on four streams
+    // (disjoint entries of S)
     launch_lm_prep(P, stream);
     fork(side[0]);
-    fork(side[1]);
     launch_assemble_sb(P, side[0]);
-    launch_assemble_pp_light(P, side[1]);
-    launch_assemble_pp_heavy(P, stream);
+    launch_assemble_pp(P, stream);
     join(side[0]);
-    join(side[1]);
     launch_cholesky(P, stream);
     launch_gn_finalize(P, stream);
     fork(side[0]);
