@@ -15,7 +15,7 @@
 //   landmark y_l from the q_v of its visits (visit order), its dogleg vectors, and s v_c, -s y_l
 //            to LDS for the visits
 //   visit    J_s v_c and J_s v_g of its 1-2 residuals (A re-read from L1/L2)
-// The f-block half of k_gn_finalize runs before (v_c of the poses); the IMU factors', priors' and
+// The f-blocks' GN vectors come from the Cholesky's back substitution (v_c of the poses); the IMU factors', priors' and
 // edges' J*v stay in k_jv. The group's J*v forms and landmark norms leave as one fixed-order sum per
 // group (grp_red), so the per-window reductions read ~36 records instead of every visit and landmark.
 #include "device_problem.hpp"

@@ -699,6 +699,23 @@ __device__ __forceinline__ void bsList(const uint8_t* nz, int T, int I, int* lst
     if (nz[i * T + I]) lst[1 + n++] = i;
   lst[0] = n;
 }
+// The GN step's f-vectors from the solution x of row e (DoglegStrategy::ComputeGaussNewtonStep /
+// ComputeGradient; formerly k_gn_finalize, one launch fewer per iteration): gauss_newton_step_ =
+// -diagonal_ .* x, gradient_ = s .* g / diagonal_, v = gradient_ / diagonal_. Gap rows of a
+// nested-dissection order (no f-block) are skipped.
+__device__ __forceinline__ void gnFinalizeRow(const DevProblem& P, size_t i, double x) {
+  const double dg = gmem(P.diagF)[i], sc = gmem(P.sF)[i], g = gmem(P.gF)[i];
+  P.yF[i] = x;
+  P.gnF[i] = -dg * x;
+  const double gr = sc * g / dg;
+  P.dgF[i] = gr;
+  P.vF[i] = gr / dg;
+}
+__device__ __forceinline__ bool gapRow(const DevProblem& P, int w, int e) {
+  const int g0 = P.win_sgap[2 * w];
+  return e >= g0 && e < g0 + P.win_sgap[2 * w + 1];
+}
+
 // Persistent schedule (256 threads, 4 virtual threads each): y already in sx (LDS), then
 // the steps with operands loaded in-step. sA: >= 32 x 64 doubles.
 __device__ __forceinline__ void backSubstitute(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* Linv,
@@ -724,7 +741,8 @@ __device__ __forceinline__ void backSubstitute(const DevProblem& P, int w, const
     __syncthreads();
   }
   const int fdim = P.win_fdim[w];
-  for (int e = t; e < fdim; e += blockDim.x) P.yF[(size_t)P.win_foff[w] + e] = sx[e];
+  for (int e = t; e < fdim; e += blockDim.x)
+    if (!gapRow(P, w, e)) gnFinalizeRow(P, (size_t)P.win_foff[w] + e, sx[e]);
 }
 
 #ifndef OKG_CHOL_OCC
@@ -1097,7 +1115,8 @@ __global__ __launch_bounds__(kBsReal) void k_chol_bsub(const DevProblem* __restr
   const int fdim = P.win_fdim[w];
   const int e0 = !split ? 0 : (h == 0 ? 0 : tL * kTile), e1 = !split ? fdim : (h == 0 ? fdim : tS * kTile);
   for (int e = e0 + t; e < e1; e += kBsReal)
-    if (!split || h == 1 || e < tL * kTile || e >= tS * kTile) P.yF[(size_t)P.win_foff[w] + e] = sx[e];
+    if ((!split || h == 1 || e < tL * kTile || e >= tS * kTile) && !gapRow(P, w, e))
+      gnFinalizeRow(P, (size_t)P.win_foff[w] + e, sx[e]);
 #ifdef OKG_CHOL_CLOCK
   if (blockIdx.x == 0 && t == 0) printf("BSUBCLK T=%d init %llu steps %llu (x10ns)\n", T, g_cholClk[12], g_cholClk[13]);
 #endif

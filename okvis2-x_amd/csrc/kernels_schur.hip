@@ -18,7 +18,7 @@
 //                 a fixed tree combines the groups, so the sum is deterministic without atomics;
 //                 diagonal pairs also emit the Schur rhs and the dogleg diagonal.
 //   k_assemble_sb one wavefront per block pair involving a speed/bias block (one entry per lane).
-//   k_gn_finalize Gauss-Newton step / dogleg gradient of the f-blocks in the dogleg-scaled space
+//   (the f-blocks' Gauss-Newton step / dogleg gradient: the Cholesky's back substitution, gnFinalizeRow)
 //                 (the landmarks' back substitution and vectors: k_lm_backsub_jv, kernels_backsub.hip).
 #include <algorithm>
 #include <cfloat>
@@ -1097,43 +1097,6 @@ __global__ __launch_bounds__(256) void k_assemble_sb(const DevProblem* __restric
   }
 }
 
-// gauss_newton_step_ = -diagonal_ .* y ; gradient_ = s .* g / diagonal_ ; v = gradient_ / diagonal_
-// (DoglegStrategy::ComputeGradient / ComputeCauchyPoint / ComputeGaussNewtonStep) of the f-blocks;
-// the landmarks' share is formed with their back substitution (k_lm_backsub_jv).
-__global__ __launch_bounds__(256) void k_gn_finalize(const DevProblem* __restrict__ Pp) {
-  const DevProblem& P = *Pp;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= P.n_fblock) return;
-  // the block record and window state, then all of the block's operands (loads before the stores:
-  // the output vectors may alias the inputs as far as the compiler knows)
-  const int w = gmem(P.fb_win)[t], kind = gmem(P.fb_kind)[t], fo = gmem(P.fb_off)[t];
-  const auto gst = gmem(P.st + w);
-  const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed;
-  const int foff = gmem(P.win_foff)[w];
-  asm volatile("" ::"v"(kind), "v"(fo), "v"(foff));
-  if ((sDone != 0) | (sNeed == 0) | (sFail != 0)) return;  // gnSelect
-  const int n = kind == 0 ? 6 : 9;
-  const size_t base = (size_t)foff + fo;
-  double dg[9], y[9], sc[9], g[9];
-#pragma unroll
-  for (int c = 0; c < 9; ++c) {
-    const size_t i = base + (c < n ? c : 0);
-    dg[c] = gmem(P.diagF)[i];
-    y[c] = gmem(P.yF)[i];
-    sc[c] = gmem(P.sF)[i];
-    g[c] = gmem(P.gF)[i];
-  }
-#pragma unroll
-  for (int c = 0; c < 9; ++c) {
-    if (c >= n) break;
-    const size_t i = base + c;
-    P.gnF[i] = -dg[c] * y[c];
-    const double gr = sc[c] * g[c] / dg[c];
-    P.dgF[i] = gr;
-    P.vF[i] = gr / dg[c];
-  }
-}
-
 // ------------------------------------------------------------------------------------ launchers
 void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s) {
   if (P.n_lmg <= 0) return;
@@ -1193,12 +1156,8 @@ void launch_gn_reduce(const DevProblem& P, hipStream_t s) {
   launch_lm_prep(P, s);
   launch_assemble(P, s);
 }
-void launch_gn_finalize(const DevProblem& P, hipStream_t s) {
-  if (P.n_fblock > 0) hipLaunchKernelGGL(k_gn_finalize, dim3((P.n_fblock + 255) / 256), dim3(256), 0, s, P.self);
-}
 void launch_gn_backsub(const DevProblem& P, hipStream_t s) {
-  launch_gn_finalize(P, s);  // v_c of the f-blocks: read by the landmark pass
-  launch_lm_backsub(P, s);
+  launch_lm_backsub(P, s);  // (the f-blocks' GN vectors are written by the Cholesky's back substitution)
 }
 
 }  // namespace okg

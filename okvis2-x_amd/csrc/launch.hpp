@@ -37,7 +37,6 @@ void launch_lm_backsub(const DevProblem& P, hipStream_t s);  // kernels_backsub.
 void launch_assemble_pp(const DevProblem& P, hipStream_t s);
 void launch_assemble_sb(const DevProblem& P, hipStream_t s);
 void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s);  // 0/1: linearisation, 2: GN prep
-void launch_gn_finalize(const DevProblem& P, hipStream_t s);
 
 // dense factorisation + both triangular solves, one persistent workgroup per window
 // (kernels_chol.hip)

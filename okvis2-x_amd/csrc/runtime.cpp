@@ -2039,8 +2039,7 @@ struct okvisgpu_ctx {
     launch_assemble_sb(P, side[0]);
     launch_assemble_pp(P, stream);
     join(side[0]);
-    launch_cholesky(P, stream);
-    launch_gn_finalize(P, stream);
+    launch_cholesky(P, stream);  // (with the f-blocks' GN vectors, formerly k_gn_finalize)
     fork(side[0]);
     launch_jv(P, side[0]);
     launch_lm_backsub(P, stream);
@@ -2379,7 +2378,7 @@ int okvisgpu_profile_iteration(okvisgpu_ctx* c, double* ms) {
     mark(1);  // (S is no longer cleared per iteration: phase kept for the ABI's phase list)
     launch_assemble(P, s); mark(2);
     launch_cholesky(P, s); mark(3);
-    launch_gn_finalize(P, s); mark(5);
+    mark(5);  // (gn_finalize: fused into the Cholesky's back substitution; phase kept for the ABI list)
     launch_lm_backsub(P, s); mark(4);
     launch_jv(P, s); mark(6);
     mark(7);  // (the J*v reduction runs inside k_dogleg)

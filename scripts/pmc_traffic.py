@@ -19,6 +19,7 @@ for path in sys.argv[3:]:
         name = r["Kernel_Name"].split("(")[0].replace("okg::", "").replace("void ", "")
         # template arguments: the extrinsics flag (<..., false|true>) and bool-only specialisations
         name = name.replace(", false>", ">").replace(", true>", ">").replace("<false>", "").replace("<true>", "")
+        name = name.replace("<256>", "").replace("<1024>", "")  # per-window reduction workgroup sizes
         # the specialised k_lm_visit<mode> kernels under bench.py's table names
         name = {"k_lm_visit<1>": "k_lm_visit", "k_lm_visit<2>": "k_lm_visit_prep", "k_lm_visit<0>": "k_lm_visit_init",
                 "k_lm_prep_windows": "k_lm_visit_prep", "k_cholesky<0>": "k_cholesky"}.get(name, name)
@@ -31,7 +32,7 @@ for k, d in vals.items():
     w = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"]) * 1024
     kern[k] = {"fetch_bytes_per_dispatch": f, "write_bytes_per_dispatch": w, "bytes_per_dispatch": f + w}
     if k in ("k_assemble_pp", "k_assemble_sb", "k_eval_imu", "k_eval_obs", "k_fgrad", "k_cholesky", "k_lm_backsub", "k_lm_backsub_jv",
-             "k_zero_S", "k_jv", "k_gn_finalize", "k_dogleg"):
+             "k_zero_S", "k_jv", "k_dogleg", "k_reduce", "k_gradnorm"):
         kern[k]["bytes_per_iteration"] = f + w  # one dispatch per iteration
     elif k in ("k_lm_visit", "k_lm_visit_prep"):
         # one dispatch each per iteration; the solve's dispatches only touch the windows that need
