@@ -352,9 +352,17 @@ __device__ unsigned int g_imuDone;
 // chain starts from the stored state (Delta_q, integrals, cross_, dv_db_g, P) at imu_t0 (= the old
 // t1), integrates the appended samples with the eliminated state's bias (sb[0] row blk[1]) up to
 // imu_t1, and writes the state and the new square-root information; no residual.
+__device__ __noinline__ void evalPriorsThread(const DevProblem& P, int t, int mode);
 template <bool APPEND>
 __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* __restrict__ Pp, int mode) {
   const DevProblem& P = *Pp;
+  if (!APPEND) {  // the trailing workgroups: priors and pose-graph edges (uniform per workgroup)
+    const int nImuWG = (P.n_imu + kImuPerWG - 1) / kImuPerWG;
+    if ((int)blockIdx.x >= nImuWG) {
+      evalPriorsThread(P, ((int)blockIdx.x - nImuWG) * 64 + (int)threadIdx.x, mode);
+      return;
+    }
+  }
   const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
   const int f = blockIdx.x * kImuPerWG + g;
   ICLK_INIT
@@ -1002,9 +1010,9 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
 }
 
 // ------------------------------------------------------------------------------------ priors
-__global__ __launch_bounds__(64) void k_eval_priors(const DevProblem* __restrict__ Pp, int mode) {
-  const DevProblem& P = *Pp;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+// Pose priors, speed/bias priors and relative-pose edges, one thread each (t = their index in that
+// order). Runs as the trailing workgroups of k_eval_imu (evalPriorsThread; one launch fewer).
+__device__ __noinline__ void evalPriorsThread(const DevProblem& P, int t, int mode) {
   if (t < P.n_pprior) {
     const int i = t;
     const int w = P.pp_win[i];
@@ -1203,14 +1211,13 @@ void launch_host_scatter(const DevProblem& P, hipStream_t s) {
 void launch_eval_obs(const DevProblem& P, int mode, hipStream_t s) {
   if (P.n_obs > 0) hipLaunchKernelGGL(k_eval_obs, dim3((P.n_obs + 255) / 256), dim3(256), 0, s, P.self, mode);
 }
+// k_eval_imu's grid: the IMU factors (4 per workgroup), then the priors and edges (64 per workgroup)
 void launch_eval_imu(const DevProblem& P, int mode, hipStream_t s) {
-  if (P.n_imu > 0)
-    hipLaunchKernelGGL(k_eval_imu<false>, dim3((P.n_imu + kImuPerWG - 1) / kImuPerWG), dim3(64), 0, s, P.self, mode);
-}
-void launch_eval_priors(const DevProblem& P, int mode, hipStream_t s) {
   const int np = P.n_pprior + P.n_sbprior + P.n_relpose;
-  if (np > 0) hipLaunchKernelGGL(k_eval_priors, dim3((np + 63) / 64), dim3(64), 0, s, P.self, mode);
+  const int nb = (P.n_imu + kImuPerWG - 1) / kImuPerWG + (np + 63) / 64;
+  if (nb > 0) hipLaunchKernelGGL(k_eval_imu<false>, dim3(nb), dim3(64), 0, s, P.self, mode);
 }
+void launch_eval_priors(const DevProblem& P, int mode, hipStream_t s) {}  // (in launch_eval_imu)
 void launch_eval(const DevProblem& P, int mode, hipStream_t s) {
   launch_eval_obs(P, mode, s);
   launch_eval_imu(P, mode, s);
