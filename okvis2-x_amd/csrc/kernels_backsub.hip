@@ -19,6 +19,7 @@
 // edges' J*v stay in k_jv. The group's J*v forms and landmark norms leave as one fixed-order sum per
 // group (grp_red), so the per-window reductions read ~36 records instead of every visit and landmark.
 #include "device_problem.hpp"
+#include "jv_groups.hpp"
 #include "launch.hpp"
 #include "okvisgpu_math.hpp"
 
@@ -47,6 +48,10 @@ __device__ __forceinline__ bool loadExtTerm(const DevProblem& P, int o, int w, i
 template <bool EXT>
 __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
+  if ((int)blockIdx.x >= P.n_lmg) {  // trailing workgroups: the factors' J*v (uniform per workgroup)
+    jvGroups(P, (int)blockIdx.x - P.n_lmg);
+    return;
+  }
   const int t = threadIdx.x;
   const auto gi = gmem(reinterpret_cast<const int4*>(P.lmg_info + kLmgInfo * blockIdx.x));
   const int4 gi0 = gi[0], gi1 = gi[kLmgInfo / 4];
@@ -268,10 +273,12 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
   }
 }
 
+// grid: the landmark groups, then the factors' J*v workgroups (jvGroups)
 void launch_lm_backsub(const DevProblem& P, hipStream_t s) {
-  if (P.n_lmg <= 0) return;
-  if (P.n_xvisit > 0) hipLaunchKernelGGL(k_lm_backsub_jv<true>, dim3(P.n_lmg), dim3(kLmGroupVisits), 0, s, P.self);
-  else hipLaunchKernelGGL(k_lm_backsub_jv<false>, dim3(P.n_lmg), dim3(kLmGroupVisits), 0, s, P.self);
+  const int nb = P.n_lmg + jvBlocks(P);
+  if (nb <= 0) return;
+  if (P.n_xvisit > 0) hipLaunchKernelGGL(k_lm_backsub_jv<true>, dim3(nb), dim3(kLmGroupVisits), 0, s, P.self);
+  else hipLaunchKernelGGL(k_lm_backsub_jv<false>, dim3(nb), dim3(kLmGroupVisits), 0, s, P.self);
 }
 
 }  // namespace okg

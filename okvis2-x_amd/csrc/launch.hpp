@@ -47,7 +47,7 @@ void launch_cholesky(const DevProblem& P, hipStream_t s);
 // trust-region control (kernels_control.hip)
 enum ReduceMode { R_COST_INIT = 0, R_COST_CAND = 1, R_JV = 2 };
 void launch_reduce(const DevProblem& P, int mode, hipStream_t s);
-void launch_jv(const DevProblem& P, hipStream_t s);
+void launch_jv(const DevProblem& P, hipStream_t s);  // (standalone, for okvisgpu_time_kernel; launch_lm_backsub includes it)
 void launch_gradnorm(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_dogleg(const DevProblem& P, hipStream_t s);
 void launch_select_current(const DevProblem& P, hipStream_t s);  // set 1 -> set 0 where xcur == 1

@@ -1997,8 +1997,7 @@ struct okvisgpu_ctx {
     launch_lm_prep(P, stream);
     launch_assemble(P, stream);
     launch_cholesky(P, stream);
-    launch_gn_backsub(P, stream);
-    launch_jv(P, stream);
+    launch_gn_backsub(P, stream);  // (with the factors' J*v)
     launch_dogleg(P, stream);
     evalAll(1, stream);
     launch_reduce(P, R_COST_CAND, stream);
@@ -2040,10 +2039,7 @@ struct okvisgpu_ctx {
     launch_assemble_pp(P, stream);
     join(side[0]);
     launch_cholesky(P, stream);  // (with the f-blocks' GN vectors, formerly k_gn_finalize)
-    fork(side[0]);
-    launch_jv(P, side[0]);
-    launch_lm_backsub(P, stream);
-    join(side[0]);
+    launch_lm_backsub(P, stream);  // (with the factors' J*v)
     launch_dogleg(P, stream);
     // candidate evaluation
     fork(side[0]);
@@ -2380,7 +2376,7 @@ int okvisgpu_profile_iteration(okvisgpu_ctx* c, double* ms) {
     launch_cholesky(P, s); mark(3);
     mark(5);  // (gn_finalize: fused into the Cholesky's back substitution; phase kept for the ABI list)
     launch_lm_backsub(P, s); mark(4);
-    launch_jv(P, s); mark(6);
+    mark(6);  // (jv: the trailing workgroups of lm_backsub; phase kept for the ABI list)
     mark(7);  // (the J*v reduction runs inside k_dogleg)
     launch_dogleg(P, s); mark(8);
     launch_eval_obs(P, 1, s); mark(9);
