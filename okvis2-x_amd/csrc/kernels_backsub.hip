@@ -48,7 +48,8 @@ __device__ __forceinline__ bool loadExtTerm(const DevProblem& P, int o, int w, i
 template <bool EXT>
 __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
-  if ((int)blockIdx.x >= P.n_lmg) {  // trailing workgroups: the factors' J*v (uniform per workgroup)
+  if (!EXT && (int)blockIdx.x >= P.n_lmg) {  // trailing workgroups: the factors' J*v (uniform per workgroup;
+                                             // the extrinsics variant launches k_jv beside it instead)
     jvGroups(P, (int)blockIdx.x - P.n_lmg);
     return;
   }
@@ -275,10 +276,13 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
 
 // grid: the landmark groups, then the factors' J*v workgroups (jvGroups)
 void launch_lm_backsub(const DevProblem& P, hipStream_t s) {
+  if (P.n_xvisit > 0) {  // (the J*v path would raise the extrinsics variant's registers: a launch of its own)
+    if (P.n_lmg > 0) hipLaunchKernelGGL(k_lm_backsub_jv<true>, dim3(P.n_lmg), dim3(kLmGroupVisits), 0, s, P.self);
+    launch_jv(P, s);
+    return;
+  }
   const int nb = P.n_lmg + jvBlocks(P);
-  if (nb <= 0) return;
-  if (P.n_xvisit > 0) hipLaunchKernelGGL(k_lm_backsub_jv<true>, dim3(nb), dim3(kLmGroupVisits), 0, s, P.self);
-  else hipLaunchKernelGGL(k_lm_backsub_jv<false>, dim3(nb), dim3(kLmGroupVisits), 0, s, P.self);
+  if (nb > 0) hipLaunchKernelGGL(k_lm_backsub_jv<false>, dim3(nb), dim3(kLmGroupVisits), 0, s, P.self);
 }
 
 }  // namespace okg
