@@ -33,6 +33,9 @@ constexpr int kObsLin = 8;   // r (2) | A = L Jh C_CW (2x3), Cauchy-scaled
 constexpr int kSegHG = 28;   // per visit segment: H = sum J_p^T J_p (21, sym packed) | g = sum J_p^T r (6) | pad
 constexpr int kSegUz = 8;    // per visit segment: sum U z (6) | pad
 constexpr int kLmGroupVisits = 256;  // k_lm_visit: visits of one landmark group (one workgroup)
+// A batch of at most a quarter window per CU: the latency regime (per-window reductions at 1,024
+// threads, fused launches of the iteration's independent small kernels).
+__host__ __device__ constexpr bool fewWindows(int nWin, int cuCount) { return 4 * nWin <= cuCount; }
 constexpr int kLmGroupMax = 64;      // landmarks per group
 constexpr int kLmPartStage = 2048;   // landmark-pair products per group (staged in LDS)
 constexpr int kAsmLightMax = 24;     // contributions of a pose-pose pair assembled by a 16-lane quarter

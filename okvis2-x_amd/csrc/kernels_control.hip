@@ -28,7 +28,6 @@ namespace okg {
 // [64, 1024] (the tree reductions); the reduction order follows it, so a window's bits depend on
 // the batch size only through this choice (and the Cholesky order, runtime.cpp build).
 constexpr int kRBBatch = 256, kRBFew = 1024;
-__host__ __device__ constexpr bool fewWindows(int nWin, int cuCount) { return 4 * nWin <= cuCount; }
 
 // Fixed-order tree reductions over the workgroup. The barriers order LDS only (ldsBarrier): a
 // __syncthreads() also waited for every global store still in flight (k_dogleg's Plus pass leaves

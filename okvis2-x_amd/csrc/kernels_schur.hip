@@ -799,10 +799,9 @@ __global__ __launch_bounds__(256) void k_zero_S(const DevProblem* __restrict__ P
 // its own Y row, and two steps of descriptors/operands are in flight per lane.
 constexpr int kGroups = 8;
 
-__global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __restrict__ Pp) {
-  const DevProblem& P = *Pp;
+__device__ __forceinline__ void asmPairsHeavy(const DevProblem& P, int bid) {
   const int lane = threadIdx.x & 63;
-  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int item = bid * 4 + (threadIdx.x >> 6);
   if (item >= P.n_asm_pp) return;
   const int k = gmem(P.asm_pp_items)[item];
   if (k < 0) return;
@@ -938,16 +937,16 @@ __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __rest
     P.rhsF[idx] = P.sF[idx] * P.gF[idx] - uz;
   }
 }
+__global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __restrict__ Pp) { asmPairsHeavy(*Pp, (int)blockIdx.x); }
 
 // k_assemble_pp_light: off-diagonal pose-pose pairs with few contributions (no visits; partial
 // blocks, then factor blocks; <= kAsmLightMax). A 16-lane quarter of a wavefront per pair: 2 groups
 // of 6 lanes (one per row) take alternate contributions, one fixed combining step. Same sums as
 // k_assemble_pp with kGroups = 2.
 constexpr int kPplLanes = 16, kPplGroups = 2;
-__global__ __launch_bounds__(256) void k_assemble_pp_light(const DevProblem* __restrict__ Pp) {
-  const DevProblem& P = *Pp;
+__device__ __forceinline__ void asmPairsLight(const DevProblem& P, int bid) {
   const int lane = threadIdx.x & 63, sub = threadIdx.x & (kPplLanes - 1);
-  const int item = (blockIdx.x * 256 + threadIdx.x) / kPplLanes;
+  const int item = (bid * 256 + threadIdx.x) / kPplLanes;
   const int kRaw = item < P.n_asm_ppl ? gmem(P.asm_ppl_items)[item] : -1;
   const bool has = kRaw >= 0;
   const int k = has ? kRaw : 0;
@@ -1034,13 +1033,13 @@ __global__ __launch_bounds__(256) void k_assemble_pp_light(const DevProblem* __r
 #pragma unroll
   for (int q = 0; q < 6; ++q) Srow[q] = si * P.sF[(size_t)foff + offj + q] * H[q] - Sc[q];
 }
+__global__ __launch_bounds__(256) void k_assemble_pp_light(const DevProblem* __restrict__ Pp) { asmPairsLight(*Pp, (int)blockIdx.x); }
 
 // k_assemble_sb: pairs with a speed/bias block (6x9, 9x9): few contributions (IMU factors,
 // speed/bias priors), one entry per lane.
-__global__ __launch_bounds__(256) void k_assemble_sb(const DevProblem* __restrict__ Pp) {
-  const DevProblem& P = *Pp;
+__device__ __forceinline__ void asmPairsSb(const DevProblem& P, int bid) {
   const int lane = threadIdx.x & 63;
-  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int item = bid * 4 + (threadIdx.x >> 6);
   if (item >= P.n_asm_sb) return;
   const int k = gmem(P.asm_sb_items)[item];
   // the pair record, then the window state and the block offsets, consumed (empty asm) before the
@@ -1096,6 +1095,7 @@ __global__ __launch_bounds__(256) void k_assemble_sb(const DevProblem* __restric
     P.rhsF[idx] = P.sF[idx] * P.gF[idx];
   }
 }
+__global__ __launch_bounds__(256) void k_assemble_sb(const DevProblem* __restrict__ Pp) { asmPairsSb(*Pp, (int)blockIdx.x); }
 
 // ------------------------------------------------------------------------------------ launchers
 void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s) {
@@ -1148,7 +1148,22 @@ void launch_zero_S(const DevProblem& P, hipStream_t s, int tail) {
   const int per = P.n_win >= kManyWindows ? kZeroTiles : 1;
   if (P.n_tiles > 0) hipLaunchKernelGGL(k_zero_S, dim3((P.n_tiles + per - 1) / per), dim3(256), 0, s, P.self, per, tail);
 }
+// Few windows: the three assembly kernels as one launch (block ranges; the kernels are independent:
+// disjoint pairs of S), two graph nodes fewer on a single window's latency chain.
+__global__ __launch_bounds__(256) void k_assemble_few(const DevProblem* __restrict__ Pp, int nHeavy, int nLight) {
+  const DevProblem& P = *Pp;
+  const int b = blockIdx.x;
+  if (b < nHeavy) asmPairsHeavy(P, b);
+  else if (b < nHeavy + nLight) asmPairsLight(P, b - nHeavy);
+  else asmPairsSb(P, b - nHeavy - nLight);
+}
 void launch_assemble(const DevProblem& P, hipStream_t s) {
+  if (fewWindows(P.n_win, P.cu_count)) {
+    const int nH = (P.n_asm_pp + 3) / 4, nL = (P.n_asm_ppl + 256 / kPplLanes - 1) / (256 / kPplLanes),
+              nS = (P.n_asm_sb + 3) / 4;
+    if (nH + nL + nS > 0) hipLaunchKernelGGL(k_assemble_few, dim3(nH + nL + nS), dim3(256), 0, s, P.self, nH, nL);
+    return;
+  }
   launch_assemble_pp(P, s);
   launch_assemble_sb(P, s);
 }
