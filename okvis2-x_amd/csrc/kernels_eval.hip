@@ -41,9 +41,7 @@ __device__ __forceinline__ bool evalSelect(const DevProblem& P, int w, int mode,
   return true;
 }
 
-__global__ __launch_bounds__(256) void k_eval_obs(const DevProblem* __restrict__ Pp, int mode) {
-  const DevProblem& P = *Pp;
-  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void evalObsThread(const DevProblem& P, int o, int mode) {
   if (o >= P.n_obs) return;
   // The observation's record (indices, flags, keypoint, information) is loaded together with no
   // branch in between; the window test (evalSelect) reads the WinState fields at once and consumes
@@ -134,6 +132,10 @@ __global__ __launch_bounds__(256) void k_eval_obs(const DevProblem* __restrict__
 #pragma unroll
   for (int k = 0; k < 6; ++k) lin[(2 + k) * S + o] = A[k] * sc;
   pick2(lb, P.obs_cost[0], P.obs_cost[1])[o] = cost;
+}
+
+__global__ __launch_bounds__(256) void k_eval_obs(const DevProblem* __restrict__ Pp, int mode) {
+  evalObsThread(*Pp, (int)(blockIdx.x * blockDim.x + threadIdx.x), mode);
 }
 
 // ------------------------------------------------------------------------------------ IMU
@@ -354,17 +356,16 @@ __device__ unsigned int g_imuDone;
 // imu_t1, and writes the state and the new square-root information; no residual.
 __device__ __noinline__ void evalPriorsThread(const DevProblem& P, int t, int mode);
 template <bool APPEND>
-__global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* __restrict__ Pp, int mode) {
-  const DevProblem& P = *Pp;
+__device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int bid) {
   if (!APPEND) {  // the trailing workgroups: priors and pose-graph edges (uniform per workgroup)
     const int nImuWG = (P.n_imu + kImuPerWG - 1) / kImuPerWG;
-    if ((int)blockIdx.x >= nImuWG) {
-      evalPriorsThread(P, ((int)blockIdx.x - nImuWG) * 64 + (int)threadIdx.x, mode);
+    if (bid >= nImuWG) {
+      evalPriorsThread(P, (bid - nImuWG) * 64 + (int)threadIdx.x, mode);
       return;
     }
   }
   const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
-  const int f = blockIdx.x * kImuPerWG + g;
+  const int f = bid * kImuPerWG + g;
   ICLK_INIT
 
   // per-group LDS: the chain's records (layout at kLRec..kLNz above), then symmetric P / Jacobi
@@ -1009,6 +1010,21 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
 #endif
 }
 
+template <bool APPEND>
+__global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* __restrict__ Pp, int mode) {
+  evalImuBlock<APPEND>(*Pp, mode, (int)blockIdx.x);
+}
+// Few windows: the observations (64 per workgroup), then the IMU factors, priors and edges, as one
+// launch (one graph node fewer on a single window's latency chain).
+__global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_few(const DevProblem* __restrict__ Pp, int mode, int nObsWG) {
+  const DevProblem& P = *Pp;
+  if ((int)blockIdx.x < nObsWG) {
+    evalObsThread(P, (int)blockIdx.x * 64 + (int)threadIdx.x, mode);
+    return;
+  }
+  evalImuBlock<false>(P, mode, (int)blockIdx.x - nObsWG);
+}
+
 // ------------------------------------------------------------------------------------ priors
 // Pose priors, speed/bias priors and relative-pose edges, one thread each (t = their index in that
 // order). Runs as the trailing workgroups of k_eval_imu (evalPriorsThread; one launch fewer).
@@ -1219,6 +1235,12 @@ void launch_eval_imu(const DevProblem& P, int mode, hipStream_t s) {
 }
 void launch_eval_priors(const DevProblem& P, int mode, hipStream_t s) {}  // (in launch_eval_imu)
 void launch_eval(const DevProblem& P, int mode, hipStream_t s) {
+  if (fewWindows(P.n_win, P.cu_count)) {
+    const int np = P.n_pprior + P.n_sbprior + P.n_relpose;
+    const int nObs = (P.n_obs + 63) / 64, nb = nObs + (P.n_imu + kImuPerWG - 1) / kImuPerWG + (np + 63) / 64;
+    if (nb > 0) hipLaunchKernelGGL(k_eval_few, dim3(nb), dim3(64), 0, s, P.self, mode, nObs);
+    return;
+  }
   launch_eval_obs(P, mode, s);
   launch_eval_imu(P, mode, s);
   launch_eval_priors(P, mode, s);
