@@ -630,10 +630,9 @@ __device__ __forceinline__ int sym30(int a, int b) {  // packed upper triangle o
 
 // J^T J (30x30, packed) and J^T r of every IMU factor of the windows being linearised, one
 // wavefront per factor with J staged in LDS; consumed by k_fgrad and both assembly kernels.
-__global__ __launch_bounds__(256) void k_imu_hess(const DevProblem* __restrict__ Pp, int lin_mode) {
-  const DevProblem& P = *Pp;
+__device__ __forceinline__ void imuHessBlock(const DevProblem& P, int bid, int lin_mode) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int f = blockIdx.x * 4 + wv;
+  const int f = bid * 4 + wv;
   __shared__ double sJ[4][kImuLin];
   if (f >= P.n_fac) return;
   const int w = P.imu_win[f];
@@ -658,6 +657,17 @@ __global__ __launch_bounds__(256) void k_imu_hess(const DevProblem* __restrict__
     }
     H[e] = acc;
   }
+}
+__global__ __launch_bounds__(256) void k_imu_hess(const DevProblem* __restrict__ Pp, int lin_mode) {
+  imuHessBlock(*Pp, (int)blockIdx.x, lin_mode);
+}
+// Few windows: the landmark groups' linearisation (k_lm_visit<1>) and the IMU factors' J^T J as one
+// launch (trailing workgroups), one graph node fewer on a single window's latency chain.
+template <bool EXT>
+__global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lin_few(const DevProblem* __restrict__ Pp, int lin_mode) {
+  const DevProblem& P = *Pp;
+  if ((int)blockIdx.x < P.n_lmg) lmVisitGroup<1, EXT>(P, blockIdx.x);
+  else imuHessBlock(P, (int)blockIdx.x - P.n_lmg, lin_mode);
 }
 
 // A 16-lane group per f-block (16 per 256-thread workgroup; a pose has ~10 contributions): lanes
@@ -1139,8 +1149,17 @@ void launch_imu_hess(const DevProblem& P, int lin_mode, hipStream_t s) {
   if (P.n_fac > 0) hipLaunchKernelGGL(k_imu_hess, dim3((P.n_fac + 3) / 4), dim3(256), 0, s, P.self, lin_mode);
 }
 void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
-  launch_lm_blocks(P, lin_mode, s);
-  launch_imu_hess(P, lin_mode, s);
+  if (lin_mode == 1 && fewWindows(P.n_win, P.cu_count)) {
+    const int nb = P.n_lmg + (P.n_fac + 3) / 4;
+    if (nb > 0) {
+      if (P.n_xvisit > 0) hipLaunchKernelGGL(k_lin_few<true>, dim3(nb), dim3(kLmGroupVisits), 0, s, P.self, lin_mode);
+      else hipLaunchKernelGGL(k_lin_few<false>, dim3(nb), dim3(kLmGroupVisits), 0, s, P.self, lin_mode);
+    }
+    if (P.n_pe > 0) hipLaunchKernelGGL(k_pose_extr, dim3((P.n_pe + 255) / 256), dim3(256), 0, s, P.self, lin_mode);
+  } else {
+    launch_lm_blocks(P, lin_mode, s);
+    launch_imu_hess(P, lin_mode, s);
+  }
   launch_fgrad(P, lin_mode, s);
 }
 void launch_lm_prep(const DevProblem& P, hipStream_t s) { launch_lm_visit(P, 2, s); }
