@@ -358,9 +358,10 @@ __device__ unsigned int g_imuDone;
 // PART (candidate / linearisation evaluations of a full batch): 0 = every factor; 1 = the lean
 // launch, every factor that does not re-integrate this evaluation (the common case once the biases
 // have settled), compiled without the chain, the square root and their LDS, so its waves co-reside
-// with k_eval_obs; 2 = the re-integrating factors, whose workgroups return at once when none of
-// their four factors re-integrates, and the priors and edges (their noinline callee would give the
-// lean launch its register budget). 1 then 2 writes what 0 writes (the same code per factor).
+// with k_eval_obs; 2 = the re-integrating factors, whose workgroups return at once when PART 1
+// found none of their four factors re-integrating (imu_redo_wg), and the priors and edges (their
+// noinline callee would give the lean launch its register budget). 1 then 2 writes what 0 writes
+// (the same code per factor).
 __device__ __noinline__ void evalPriorsThread(const DevProblem& P, int t, int mode);
 template <bool APPEND, int PART = 0>
 __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int bid) {
@@ -372,6 +373,7 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
       return;
     }
   }
+  if (PART == 2 && gmem(P.imu_redo_wg)[bid] == 0) return;  // (written by PART 1 for every workgroup)
   const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
   const int f = bid * kImuPerWG + g;
   ICLK_INIT
@@ -433,7 +435,10 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
   const bool doRedo =
       APPEND || (redo && ((send - sbeg) < 50 || P.opt.redo_propagation_always)) || redoCounter == 0;
   const bool live = PART == 1 ? live0 && !doRedo : (PART == 2 ? live0 && doRedo : live0);
-  if (PART == 2 && !__any(live)) return;  // (the workgroup is one wavefront: uniform)
+  if (PART == 1) {  // (the workgroup is one wavefront: uniform)
+    const bool anyRedo = __any(live0 && doRedo);
+    if (threadIdx.x == 0) P.imu_redo_wg[bid] = anyRedo ? 1 : 0;
+  }
   // redoPreintegration returns -1 before touching any state when the samples do not cover t1
   // (ImuError.cpp:270-273): the old preintegration is kept.
   const bool covered = (send > sbeg) && tsLast >= t1;
