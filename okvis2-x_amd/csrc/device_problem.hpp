@@ -194,7 +194,6 @@ struct DevProblem {
   double* imu_state;               // [n_imu][kImuState]
   double* imu_lin[2];              // [n_fac][kImuLin]
   double* imu_cost[2];             // [n_fac]
-  int32_t* imu_redo_wg;            // [IMU workgroups] k_eval_imu_lean -> k_eval_imu_redo: any factor re-integrates
   double* imu_H;                   // [n_fac][kImuHess] of the linearisation lin[lcur] (k_imu_hess)
   double* imu_jv;                  // [3][n_fac]
   const int32_t* win_host_range;   // [n_win][2] host factors of the window (global factor indices)

@@ -20,7 +20,6 @@
 // flagged eval_cand); 2 = initial evaluation (also residuals whose blocks are all constant, which
 // Ceres evaluates once for fixed_cost); 3 = like 2 without the robust loss (parity hook).
 #include <cfloat>
-#include <cstdlib>
 
 #include "device_problem.hpp"
 #include "launch.hpp"
@@ -142,22 +141,24 @@ __global__ __launch_bounds__(256) void k_eval_obs(const DevProblem* __restrict__
 // ------------------------------------------------------------------------------------ IMU
 namespace {
 
-// preintegrated quantities (ImuError.hpp:273-304) of the stored state: Delta_q in registers, the
-// matrices read where they are used (the residual phase then holds ~60 doubles fewer per lane)
-struct ImuPre {
+struct ImuPre {  // preintegrated quantities (ImuError.hpp:273-304), register resident per lane
   Q dq;
-  const double *Ci, *Cdi, *ai, *adi, *dadbg, *dvdbg, *dpdbg;
+  double Ci[9], Cdi[9], ai[3], adi[3], dadbg[9], dvdbg[9], dpdbg[9];
 };
 
 __device__ void loadPre(const double* s, ImuPre& p) {
   p.dq = Q{s[2], s[3], s[4], s[5]};
-  p.Ci = s + 6;
-  p.Cdi = s + 15;
-  p.ai = s + 24;
-  p.adi = s + 27;
-  p.dadbg = s + 30;
-  p.dvdbg = s + 39;
-  p.dpdbg = s + 48;
+  for (int i = 0; i < 9; ++i) {
+    p.Ci[i] = s[6 + i];
+    p.Cdi[i] = s[15 + i];
+    p.dadbg[i] = s[30 + i];
+    p.dvdbg[i] = s[39 + i];
+    p.dpdbg[i] = s[48 + i];
+  }
+  for (int i = 0; i < 3; ++i) {
+    p.ai[i] = s[24 + i];
+    p.adi[i] = s[27 + i];
+  }
 }
 
 // ---- k_eval_imu: one 16-lane group per ImuError, four factors per wavefront
@@ -196,7 +197,6 @@ constexpr int kLRec = 0, kLQ1 = kLRec + kImuK * kStepRec, kLCr = kLQ1 + 4 * (kIm
 static_assert(kLCj + 9 * kImuK <= kLCc && 15 * kS <= kLCc, "chain records / P exchange overlap the sums");
 static_assert(kImuLds >= 32 * kS + 32, "the square-root phase needs sA, sB and sR");
 static_assert(kImuLds * 8 * 4 <= 20480, "LDS for eight workgroups (two waves per SIMD) per CU");
-constexpr int kImuLdsLean = 16 * kS + 90;  // the lean launch (PART 1): U (sA) and the residual's 3x3 blocks (sB)
 
 // F_delta (ImuError.cpp:395-410) of one step in LDS: non-identity 3x3 blocks
 constexpr int kF03 = 0, kF09 = 9, kF012 = 18, kF39 = 27, kF63 = 36, kF69 = 45, kF612 = 54, kFdt = 63;
@@ -354,26 +354,16 @@ __device__ unsigned int g_imuDone;
 // chain starts from the stored state (Delta_q, integrals, cross_, dv_db_g, P) at imu_t0 (= the old
 // t1), integrates the appended samples with the eliminated state's bias (sb[0] row blk[1]) up to
 // imu_t1, and writes the state and the new square-root information; no residual.
-//
-// PART (candidate / linearisation evaluations of a full batch): 0 = every factor; 1 = the lean
-// launch, every factor that does not re-integrate this evaluation (the common case once the biases
-// have settled), compiled without the chain, the square root and their LDS, so its waves co-reside
-// with k_eval_obs; 2 = the re-integrating factors, whose workgroups return at once when PART 1
-// found none of their four factors re-integrating (imu_redo_wg), and the priors and edges (their
-// noinline callee would give the lean launch its register budget). 1 then 2 writes what 0 writes
-// (the same code per factor).
 __device__ __noinline__ void evalPriorsThread(const DevProblem& P, int t, int mode);
-template <bool APPEND, int PART = 0>
+template <bool APPEND>
 __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int bid) {
-  static_assert(PART == 0 || !APPEND, "the split is for evaluations");
-  if (!APPEND && PART != 1) {  // the trailing workgroups: priors and pose-graph edges (uniform per workgroup)
+  if (!APPEND) {  // the trailing workgroups: priors and pose-graph edges (uniform per workgroup)
     const int nImuWG = (P.n_imu + kImuPerWG - 1) / kImuPerWG;
     if (bid >= nImuWG) {
       evalPriorsThread(P, (bid - nImuWG) * 64 + (int)threadIdx.x, mode);
       return;
     }
   }
-  if (PART == 2 && gmem(P.imu_redo_wg)[bid] == 0) return;  // (written by PART 1 for every workgroup)
   const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
   const int f = bid * kImuPerWG + g;
   ICLK_INIT
@@ -381,7 +371,7 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
   // per-group LDS: the chain's records (layout at kLRec..kLNz above), then symmetric P / Jacobi
   // matrix / U (sA, row-major 16x16); L (column-major) / Jacobi eigenvectors (sB); Jacobi rotations
   // (sR). 19 KB per workgroup: two workgroups (waves) per SIMD.
-  __shared__ double sAll[kImuPerWG][PART == 1 ? kImuLdsLean : kImuLds];
+  __shared__ double sAll[kImuPerWG][kImuLds];
   double* sG = sAll[g];
   double* sA = sG;
   double* sB = sG + 16 * kS;
@@ -416,10 +406,10 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
   const int nTot = gmem(P.imu_sbegin)[P.n_imu];  // samples of the batch (bounds of the cache warm-up)
   asm volatile("" ::"v"(flR), "v"(blkR.y), "v"(t0), "v"(t1), "v"(st0), "v"(st1), "v"(bref[0]), "v"(bref[5]),
                "v"(sDone), "v"(sCand), "v"(sX), "v"(sL), "v"(tsLast));
-  const bool live0 = inR && (APPEND || ((sDone == 0) & (mode != 1 || sCand != 0) & !((flR & 2) && mode < 2)));
+  const bool live = inR && (APPEND || ((sDone == 0) & (mode != 1 || sCand != 0) & !((flR & 2) && mode < 2)));
   const int w = APPEND ? 0 : wR;
   const int xs = APPEND ? 0 : (mode == 1 ? 1 - sX : sX), lb = APPEND ? 0 : (mode == 1 ? 1 - sL : sL);
-  const int fs = live0 ? f : 0;  // safe index for idle groups (writes are all under live)
+  const int fs = live ? f : 0;  // safe index for idle groups (writes are all under live)
 
   const int* blk = P.imu_blocks + 4 * fs;
   const auto sb0 = gmem(pick2(xs, P.sb[0], P.sb[1]) + 9 * (size_t)blkR.y);
@@ -434,16 +424,11 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
   }
   const bool doRedo =
       APPEND || (redo && ((send - sbeg) < 50 || P.opt.redo_propagation_always)) || redoCounter == 0;
-  const bool live = PART == 1 ? live0 && !doRedo : (PART == 2 ? live0 && doRedo : live0);
-  if (PART == 1) {  // (the workgroup is one wavefront: uniform)
-    const bool anyRedo = __any(live0 && doRedo);
-    if (threadIdx.x == 0) P.imu_redo_wg[bid] = anyRedo ? 1 : 0;
-  }
   // redoPreintegration returns -1 before touching any state when the samples do not cover t1
   // (ImuError.cpp:270-273): the old preintegration is kept.
   const bool covered = (send > sbeg) && tsLast >= t1;
-  const bool integrate = PART != 1 && live && doRedo && covered;
-  const bool resetDb = PART != 1 && live && doRedo && !APPEND;  // Delta_b is zero after a redo (ImuError.cpp:855)
+  const bool integrate = live && doRedo && covered;
+  const bool resetDb = live && doRedo && !APPEND;  // Delta_b is zero after a redo (ImuError.cpp:855)
   if (resetDb) {
     redoCounter++;
     redo = false;
@@ -459,7 +444,7 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
   for (int i = 0; i < 15; ++i) Pc[i] = 0.0;
   int steps = 0;
   double* const carry = sG + kLCarry;  // Delta_q (4) | cross_ (9) between chunks
-  if (PART != 1 && l == 0) {
+  if (l == 0) {
     carry[0] = 0.0; carry[1] = 0.0; carry[2] = 0.0; carry[3] = 1.0;
     for (int i = 0; i < 9; ++i) carry[4 + i] = 0.0;
   }
@@ -498,7 +483,7 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
   //  S  (lane = component)  the running sums (C_integral, acc_integral, their double integrals,
   //                         dalpha/dv/dp_db_g) and the F_delta blocks that read them (:395-410);
   //  P  (lane = column)     P <- F P F^T + Q (ImuError.cpp:412-426).
-  if (PART != 1) {
+  {
     const int N = integrate ? send - sbeg : 0;
     int Nmax = N;
     Nmax = max(Nmax, __shfl_xor(Nmax, 16, 64));
@@ -775,7 +760,7 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
   ICLK(2)
   // (skipped by a workgroup none of whose factors re-integrated: the common case once the biases
   // have settled; the workgroup is one wavefront, so the test is uniform)
-  if (PART != 1 && __any(integrate)) {
+  if (__any(integrate)) {
     // ---- square-root information of P (PseudoInverse.hpp:132-158)
     // symmetrise (ImuError.cpp:441): sB holds P column-major; the symmetric P is kept row-major
     // (16x16 with a decoupled zero pad) in sA for the eigen fallback
@@ -1029,14 +1014,6 @@ template <bool APPEND>
 __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* __restrict__ Pp, int mode) {
   evalImuBlock<APPEND>(*Pp, mode, (int)blockIdx.x);
 }
-// A full batch: the factors that keep their preintegration in a launch with the register and LDS
-// budget of the residual alone, then the re-integrating ones, the priors and the edges.
-__global__ __launch_bounds__(64, 3) void k_eval_imu_lean(const DevProblem* __restrict__ Pp, int mode) {
-  evalImuBlock<false, 1>(*Pp, mode, (int)blockIdx.x);
-}
-__global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu_redo(const DevProblem* __restrict__ Pp, int mode) {
-  evalImuBlock<false, 2>(*Pp, mode, (int)blockIdx.x);
-}
 // Few windows: the observations (64 per workgroup), then the IMU factors, priors and edges, as one
 // launch (one graph node fewer on a single window's latency chain).
 __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_few(const DevProblem* __restrict__ Pp, int mode, int nObsWG) {
@@ -1250,22 +1227,11 @@ void launch_host_scatter(const DevProblem& P, hipStream_t s) {
 void launch_eval_obs(const DevProblem& P, int mode, hipStream_t s) {
   if (P.n_obs > 0) hipLaunchKernelGGL(k_eval_obs, dim3((P.n_obs + 255) / 256), dim3(256), 0, s, P.self, mode);
 }
-// OKVISGPU_IMU_SPLIT=0 keeps the single launch (development A/B, tests; read when a graph is built)
-static bool imuSplit() {
-  const char* e = std::getenv("OKVISGPU_IMU_SPLIT");
-  return !(e && e[0] == '0');
-}
 // k_eval_imu's grid: the IMU factors (4 per workgroup), then the priors and edges (64 per workgroup)
 void launch_eval_imu(const DevProblem& P, int mode, hipStream_t s) {
   const int np = P.n_pprior + P.n_sbprior + P.n_relpose;
-  const int nImuWG = (P.n_imu + kImuPerWG - 1) / kImuPerWG, nb = nImuWG + (np + 63) / 64;
-  if (nb == 0) return;
-  if (imuSplit()) {
-    if (nImuWG > 0) hipLaunchKernelGGL(k_eval_imu_lean, dim3(nImuWG), dim3(64), 0, s, P.self, mode);
-    hipLaunchKernelGGL(k_eval_imu_redo, dim3(nb), dim3(64), 0, s, P.self, mode);
-  } else {
-    hipLaunchKernelGGL(k_eval_imu<false>, dim3(nb), dim3(64), 0, s, P.self, mode);
-  }
+  const int nb = (P.n_imu + kImuPerWG - 1) / kImuPerWG + (np + 63) / 64;
+  if (nb > 0) hipLaunchKernelGGL(k_eval_imu<false>, dim3(nb), dim3(64), 0, s, P.self, mode);
 }
 void launch_eval_priors(const DevProblem& P, int mode, hipStream_t s) {}  // (in launch_eval_imu)
 void launch_eval(const DevProblem& P, int mode, hipStream_t s) {

@@ -1676,7 +1676,6 @@ struct okvisgpu_ctx {
                  o_imu_lin1 = scratch(sizeof(double) * kImuLin * D.n_fac);
     const size_t o_imu_cost0 = scratch(sizeof(double) * D.n_fac), o_imu_cost1 = scratch(sizeof(double) * D.n_fac),
                  o_imu_jv = scratch(sizeof(double) * 3 * D.n_fac),
-                 o_imu_redo = scratch(sizeof(int32_t) * (D.n_fac / 4 + 1)),
                  o_imu_H = scratch(sizeof(double) * kImuHess * D.n_fac);
     const size_t o_whr = upl(B.win_host_range), o_host_in = scratch(sizeof(double) * kHostIn * D.n_host),
                  o_host_out = scratch(sizeof(double) * kHostOut * D.n_host);
@@ -1787,7 +1786,6 @@ struct okvisgpu_ctx {
     D.imu_ga = dp(o_imu_ga); D.imu_par = dp(o_imu_par); D.imu_state = dp(o_imu_state);
     D.imu_lin[0] = dp(o_imu_lin0); D.imu_lin[1] = dp(o_imu_lin1);
     D.imu_cost[0] = dp(o_imu_cost0); D.imu_cost[1] = dp(o_imu_cost1); D.imu_jv = dp(o_imu_jv);
-    D.imu_redo_wg = ip(o_imu_redo);
     D.imu_H = dp(o_imu_H);
     D.win_host_range = ip(o_whr); D.host_in = dp(o_host_in); D.host_out = dp(o_host_out);
     D.pp_block = ip(o_pp_block); D.pp_win = ip(o_pp_win); D.pp_meas = dp(o_pp_meas); D.pp_L = dp(o_pp_L);
@@ -2043,21 +2041,14 @@ struct okvisgpu_ctx {
     launch_cholesky(P, stream);  // (with the f-blocks' GN vectors, formerly k_gn_finalize)
     launch_lm_backsub(P, stream);  // (with the factors' J*v)
     launch_dogleg(P, stream);
-    // candidate evaluation (OKVISGPU_EVAL_ORDER, development A/B: 0 the IMU factors beside the
-    // observations, 1 after them, 2 before them on the same stream)
-    const char* eo = std::getenv("OKVISGPU_EVAL_ORDER");
-    const int evalOrder = eo ? std::atoi(eo) : 0;
+    // candidate evaluation
+    fork(side[0]);
     fork(side[1]);
-    if (evalOrder == 0) {
-      fork(side[0]);
-      launch_eval_imu(P, 1, side[0]);
-    }
+    launch_eval_imu(P, 1, side[0]);
     launch_eval_priors(P, 1, side[1]);
     evalHost(1, side[1]);
-    if (evalOrder == 2) launch_eval_imu(P, 1, stream);
     launch_eval_obs(P, 1, stream);
-    if (evalOrder == 1) launch_eval_imu(P, 1, stream);
-    if (evalOrder == 0) join(side[0]);
+    join(side[0]);
     join(side[1]);
     launch_reduce(P, R_COST_CAND, stream);
     // linearisation at the accepted point

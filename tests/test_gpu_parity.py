@@ -237,36 +237,6 @@ def test_forked_and_serial_graphs_agree(og, gpu_ctx, monkeypatch):
         assert np.array_equal(res[0][2][k], res[1][2][k])
 
 
-def test_imu_split_launches_agree(og, oracle, gpu_ctx, monkeypatch):
-    """Above one window per four CUs the IMU evaluation runs as two launches (kernels_eval.hip
-    evalImuBlock PART 1 / 2: the factors that keep their preintegration, then the re-integrating
-    ones, the priors and the edges): bitwise the single launch's solve on both graph shapes, over
-    iterations where every factor, some factors and no factor re-integrates; window 0 against the
-    oracle."""
-    ws = [_window(og, kf=8, lm=300, obs=2400, seed=900 + s) for s in range(72)]
-    opts = og.default_options(max_num_iterations=8, function_tolerance=0.0, gradient_tolerance=0.0,
-                              parameter_tolerance=0.0)
-    res = {}
-    for ser in ("1", "0"):
-        for split in ("1", "0"):
-            monkeypatch.setenv("OKVISGPU_SERIAL_GRAPH", ser)
-            monkeypatch.setenv("OKVISGPU_IMU_SPLIT", split)
-            for w in ws:
-                w.reset()
-            gpu_ctx.set_problems([w.problem for w in ws])  # (a new graph reads both variables)
-            s = gpu_ctx.solve(opts, len(ws))
-            res[ser, split] = ([r["final_cost"] for r in s], np.concatenate([w.poses() for w in ws]),
-                               np.concatenate([w.speed_biases() for w in ws]))
-    ref = res["1", "0"]
-    for key, r in res.items():
-        assert r[0] == ref[0], key
-        assert np.array_equal(r[1], ref[1]) and np.array_equal(r[2], ref[2]), key
-    w = ws[0]
-    w.reset()
-    so = oracle.solve(w.problem_ptr(), opts)
-    assert abs(ref[0][0] - so["final_cost"]) <= 1e-7 * so["final_cost"]
-
-
 def _close(sg, so, rel=1e-7):
     assert sg["num_iterations"] == so["num_iterations"], (sg, so)
     assert sg["termination"] == so["termination"], (sg, so)
