@@ -127,6 +127,8 @@ struct DevProblem {
   const uint8_t* obs_flags;        // bit0 cauchy, bit1 fixed (all blocks constant)
   const double* obs_kp;            // [n_obs][2]
   const double* obs_L;             // [n_obs][4]
+  const double* obs_Ls;            // [n_obs] s of L = diag(s, s) when obs_iso
+  int32_t obs_iso;                 // every observation's L is diag(s, s) (runtime.cpp build)
   double* obs_lin[2];              // [kObsLin][obs_stride]; lin[lcur] belongs to params X[xcur]
   double* obs_cost[2];             // [n_obs]
   double* grp_red;                 // [n_lmg][kGrpRed]: per landmark group (k_lm_backsub_jv), fixed-order

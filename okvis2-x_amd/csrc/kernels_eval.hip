@@ -41,6 +41,8 @@ __device__ __forceinline__ bool evalSelect(const DevProblem& P, int w, int mode,
   return true;
 }
 
+// ISO (DevProblem::obs_iso): L = diag(s, s) read as s alone; the zeros enter the same products
+template <bool ISO>
 __device__ __forceinline__ void evalObsThread(const DevProblem& P, int o, int mode) {
   if (o >= P.n_obs) return;
   // The observation's record (indices, flags, keypoint, information) is loaded together with no
@@ -48,9 +50,16 @@ __device__ __forceinline__ void evalObsThread(const DevProblem& P, int o, int mo
   // the record (o >> 31 is 0), so none of these loads is sunk behind it.
   const int w = gmem(P.obs_win)[o], op = gmem(P.obs_pose)[o], ol = gmem(P.obs_lm)[o], ci = gmem(P.obs_cam)[o];
   uint8_t flags = gmem(P.obs_flags)[o];
-  const auto Lp = gmem(P.obs_L + 4 * (size_t)o);
+  double L[4];
+  if (ISO) {
+    const double sL = gmem(P.obs_Ls)[o];
+    L[0] = sL; L[1] = 0.0; L[2] = 0.0; L[3] = sL;
+  } else {
+    const auto Lp = gmem(P.obs_L + 4 * (size_t)o);
+    L[0] = Lp[0]; L[1] = Lp[1]; L[2] = Lp[2]; L[3] = Lp[3];
+  }
   const auto mp = gmem(P.obs_kp + 2 * (size_t)o);
-  const double L[4] = {Lp[0], Lp[1], Lp[2], Lp[3]}, m[2] = {mp[0], mp[1]};
+  const double m[2] = {mp[0], mp[1]};
   const auto gst = gmem(P.st + w);
   const int sDone = gst->done, sCand = gst->eval_cand, sX = gst->xcur, sL = gst->lcur;
   const bool sel = (sDone == 0) & (mode != 1 || sCand != 0) & !((flags & 2) && mode < 2);
@@ -134,8 +143,9 @@ __device__ __forceinline__ void evalObsThread(const DevProblem& P, int o, int mo
   pick2(lb, P.obs_cost[0], P.obs_cost[1])[o] = cost;
 }
 
+template <bool ISO>
 __global__ __launch_bounds__(256) void k_eval_obs(const DevProblem* __restrict__ Pp, int mode) {
-  evalObsThread(*Pp, (int)(blockIdx.x * blockDim.x + threadIdx.x), mode);
+  evalObsThread<ISO>(*Pp, (int)(blockIdx.x * blockDim.x + threadIdx.x), mode);
 }
 
 // ------------------------------------------------------------------------------------ IMU
@@ -1019,7 +1029,8 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
 __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_few(const DevProblem* __restrict__ Pp, int mode, int nObsWG) {
   const DevProblem& P = *Pp;
   if ((int)blockIdx.x < nObsWG) {
-    evalObsThread(P, (int)blockIdx.x * 64 + (int)threadIdx.x, mode);
+    if (P.obs_iso) evalObsThread<true>(P, (int)blockIdx.x * 64 + (int)threadIdx.x, mode);
+    else evalObsThread<false>(P, (int)blockIdx.x * 64 + (int)threadIdx.x, mode);
     return;
   }
   evalImuBlock<false>(P, mode, (int)blockIdx.x - nObsWG);
@@ -1225,7 +1236,9 @@ void launch_host_scatter(const DevProblem& P, hipStream_t s) {
 
 // ------------------------------------------------------------------------------------ launchers
 void launch_eval_obs(const DevProblem& P, int mode, hipStream_t s) {
-  if (P.n_obs > 0) hipLaunchKernelGGL(k_eval_obs, dim3((P.n_obs + 255) / 256), dim3(256), 0, s, P.self, mode);
+  if (P.n_obs == 0) return;
+  if (P.obs_iso) hipLaunchKernelGGL(k_eval_obs<true>, dim3((P.n_obs + 255) / 256), dim3(256), 0, s, P.self, mode);
+  else hipLaunchKernelGGL(k_eval_obs<false>, dim3((P.n_obs + 255) / 256), dim3(256), 0, s, P.self, mode);
 }
 // k_eval_imu's grid: the IMU factors (4 per workgroup), then the priors and edges (64 per workgroup)
 void launch_eval_imu(const DevProblem& P, int mode, hipStream_t s) {

@@ -108,6 +108,8 @@ struct HostBatch {
   std::vector<int32_t> obs_pose, obs_lm, obs_cam, obs_win, obs_orig;
   std::vector<uint8_t> obs_flags;
   std::vector<double> obs_kp, obs_L;
+  std::vector<double> obs_Ls;  // isotropic batches: L = diag(s, s) per observation, s only (obs_iso)
+  bool obs_iso = false;
   // visits
   std::vector<int32_t> lm_visit_begin, visit_pose, visit_obs_begin, visit_lm, lmg_begin;
   std::vector<int32_t> lmg_info;  // [n_lmg+1][kLmgInfo]: first landmark, first visit, window, first segment,
@@ -1647,6 +1649,18 @@ struct okvisgpu_ctx {
     const size_t o_obs_pose = upl(B.obs_pose), o_obs_lm = upl(B.obs_lm), o_obs_cam = upl(B.obs_cam),
                  o_obs_win = upl(B.obs_win), o_obs_flags = upl(B.obs_flags), o_obs_kp = upl(B.obs_kp),
                  o_obs_L = upl(B.obs_L);
+    // every reprojection's square-root information diag(s, s) (okvis' keypoint-size information;
+    // +0.0 off the diagonal): k_eval_obs then reads s alone (8 instead of 32 bytes per observation)
+    // and forms the same products with the constant zeros, so the same bits
+    B.obs_iso = D.n_obs > 0;
+    B.obs_Ls.assign(std::max(1, D.n_obs), 0.0);
+    for (int o = 0; o < D.n_obs && B.obs_iso; ++o) {
+      const double* L = B.obs_L.data() + 4 * (size_t)o;
+      B.obs_iso = L[1] == 0.0 && !std::signbit(L[1]) && L[2] == 0.0 && !std::signbit(L[2]) && L[0] == L[3] &&
+                  std::signbit(L[0]) == std::signbit(L[3]);
+      B.obs_Ls[o] = L[0];
+    }
+    const size_t o_obs_Ls = upl(B.obs_Ls);
     const size_t o_obs_lin0 = scratch(sizeof(double) * kObsLin * D.obs_stride);
     const size_t o_obs_lin1 = scratch(sizeof(double) * kObsLin * D.obs_stride);
     const size_t o_obs_cost0 = scratch(sizeof(double) * D.n_obs), o_obs_cost1 = scratch(sizeof(double) * D.n_obs);
@@ -1768,6 +1782,7 @@ struct okvisgpu_ctx {
     D.pose_active = up(o_pose_act); D.sb_active = up(o_sb_act);
     D.obs_pose = ip(o_obs_pose); D.obs_lm = ip(o_obs_lm); D.obs_cam = ip(o_obs_cam); D.obs_win = ip(o_obs_win);
     D.obs_flags = up(o_obs_flags); D.obs_kp = dp(o_obs_kp); D.obs_L = dp(o_obs_L);
+    D.obs_Ls = dp(o_obs_Ls); D.obs_iso = B.obs_iso;
     D.obs_lin[0] = dp(o_obs_lin0); D.obs_lin[1] = dp(o_obs_lin1);
     D.obs_cost[0] = dp(o_obs_cost0); D.obs_cost[1] = dp(o_obs_cost1); D.grp_red = dp(o_grp_red);
     D.lm_visit_begin = ip(o_lmvb); D.visit_pose = ip(o_vpose); D.visit_obs_begin = ip(o_vob); D.visit_lm = ip(o_vlm);
@@ -2448,7 +2463,7 @@ double kernelWork(const HostBatch& B, const DevProblem& P, int k) {
       return nObs * (kObsLin * d8 + 1) + nVis * (7 * d8 + 16) + (double)P.n_seg * 6 * d8 +
              (double)B.part_contrib.size() * 4 + (double)P.n_part * 36 * d8 + nLm * 34 * d8;
     case K_EVAL_IMU: return nImu * (2.0 * kImuState + kImuLin + 2 * 16) * d8 + (double)B.imu_ts.size() * 7 * d8;
-    case K_EVAL_OBS: return nObs * (16 + 32 + 13 + kObsLin * d8 + 8) + nLm * 4 * d8 + (double)B.pose_f.size() * 7 * d8;
+    case K_EVAL_OBS: return nObs * (16 + (P.obs_iso ? 8 : 32) + 13 + kObsLin * d8 + 8) + nLm * 4 * d8 + (double)B.pose_f.size() * 7 * d8;
     case K_JV:  // factors: IMU linearisation, prior / edge Jacobians in, their J*v forms out
       return nImu * (kImuLin + 3) * d8 + (double)P.n_pprior * (42 + 3) * d8 + (double)P.n_sbprior * (90 + 3) * d8 +
              (double)P.n_relpose * (kRelPoseLin + 3) * d8;

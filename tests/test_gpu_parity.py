@@ -96,6 +96,29 @@ def test_distortion_models_parity(og, oracle, gpu_ctx, distortion, parity):
     parity(f"{distortion} 4-iteration solve poses (m)", np.abs(P[:, :3] - w.poses()[:, :3]).max(), 1e-6)
 
 
+def test_anisotropic_information_parity(og, oracle, gpu_ctx, parity):
+    """Reprojection square-root information other than diag(s, s): the general 2x2 read of
+    k_eval_obs (okvis' keypoint-size information is isotropic, and such batches read s alone,
+    runtime.cpp obs_iso). Functor outputs and a short solve against the oracle."""
+    w = _window(og, seed=31)
+    p = w.problem
+    n = p.n_observations
+    L = np.ctypeslib.as_array(p.obs_sqrt_info, shape=(n, 2, 2))
+    rng = np.random.default_rng(5)
+    L[:, 1, 0] = 0.1 * L[:, 0, 0] * rng.standard_normal(n)  # sheared, lower triangular
+    L[:, 1, 1] *= 1.0 + 0.2 * rng.random(n)
+    _reprojection_parity(gpu_ctx, oracle, w, parity, "anisotropic")
+    opts = og.default_options(max_num_iterations=4, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    sg = gpu_ctx.solve(opts, 1)[0]
+    P = w.poses().copy()
+    w.reset()
+    so = oracle.solve(w.problem_ptr(), opts)
+    assert sg["num_iterations"] == so["num_iterations"]
+    parity("anisotropic 4-iteration solve final cost (rel)", abs(sg["final_cost"] - so["final_cost"]) / so["final_cost"], 1e-7)
+    parity("anisotropic 4-iteration solve poses (m)", np.abs(P[:, :3] - w.poses()[:, :3]).max(), 1e-6)
+
+
 def test_imu_functor_invariants(og, oracle, gpu_ctx, parity):
     w = _window(og)
     p = w.problem
