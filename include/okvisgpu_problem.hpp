@@ -312,9 +312,13 @@ struct ImuErrorMembers : E {
   // The members are `mutable` in okvis, but a pointer to member cannot modify a const object
   // ([expr.mptr.oper]), hence E&. information_ = U^T U as redoPreintegration / append set it
   // (ImuError.cpp:463,252). dPdsigma_ (the four covariance derivatives ImuError::append continues
-  // from, ImuError.cpp:220-223,242-248) is written as P_delta_ / sigma_k^2 in the slot of the first
-  // non-zero noise density and zero in the others: append's recursion is linear in them, so it then
-  // continues P_delta_ exactly as from the four separate matrices.
+  // from, ImuError.cpp:220-223,242-248) is touched only when the GPU changed P_delta_ (it redid or
+  // appended the preintegration): it is then written as P_delta_ / sigma_k^2 in the slot of the
+  // first non-zero noise density and zero in the others. append's recursion is linear in them, so it
+  // continues P_delta_ exactly as from the four separate matrices. Limitation: the four per-sigma
+  // matrices themselves are not reproduced after a GPU re-integration (the device carries their
+  // sigma^2-weighted sum only), so ImuError::EvaluateWithSigmaGradientAndHessian (not called by
+  // okvis' solve) would see the folded slot; a factor the GPU did not re-integrate keeps its own.
   static void write(const double* s, E& e) {
     e.*(&ImuErrorMembers::redoCounter_) = (int)s[0];
     e.*(&ImuErrorMembers::redo_) = s[1] != 0.0;
@@ -332,6 +336,12 @@ struct ImuErrorMembers : E {
     for (int i = 0; i < 9; ++i) sb(i) = s[57 + i];
     matOut(s + 66, 15, 15, e.*(&ImuErrorMembers::squareRootInformation_));
     matOut(s + 292, 3, 3, e.*(&ImuErrorMembers::cross_));
+    bool pChanged = false;
+    {
+      const auto& P0 = e.*(&ImuErrorMembers::P_delta_);
+      for (int r = 0; r < 15; ++r)
+        for (int c = 0; c < 15; ++c) pChanged = pChanged || (double)P0(r, c) != s[301 + 15 * r + c];
+    }
     matOut(s + 301, 15, 15, e.*(&ImuErrorMembers::P_delta_));
     const double* U = s + 66;
     auto& info = e.*(&ImuErrorMembers::information_);
@@ -341,6 +351,7 @@ struct ImuErrorMembers : E {
         for (int k = 0; k < 15; ++k) v += U[k * 15 + r] * U[k * 15 + c];
         info(r, c) = v;
       }
+    if (!pChanged) return;  // the okvis object's own dPdsigma_ stays (it produced this P_delta_)
     const auto& p = e.imuParameters();
     const double sig[4] = {(double)p.sigma_g_c, (double)p.sigma_a_c, (double)p.sigma_gw_c, (double)p.sigma_aw_c};
     int k0 = -1;

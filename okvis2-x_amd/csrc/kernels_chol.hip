@@ -19,6 +19,7 @@
 // MFMA tile: each of the 4 wavefronts owns a 32x32 quarter of the 64x64 output (2x2 16x16 MFMA
 // tiles), K = 64 in steps of 4. v_mfma_f64_16x16x4_f64 operand map: lane l supplies A[l&15][l>>4]
 // and B[l>>4][l&15]; result reg r of lane l is C[(l>>4) + 4r][l&15] (cdna_hip_programming.md §3).
+#include "dev_clock.hpp"
 #include "device_problem.hpp"
 #include "launch.hpp"
 #include "okvisgpu_math.hpp"
@@ -27,28 +28,7 @@ namespace okg {
 
 constexpr int kLd = kTile + 1;  // padded LDS row (65 doubles)
 
-// Development-only phase clock (make OPT="-O3 -DOKG_CHOL_CLOCK"): workgroup 0 of k_cholesky
-// accumulates s_memrealtime ticks (100 MHz) per phase and prints them.
-#ifdef OKG_CHOL_CLOCK
-__device__ unsigned long long g_cholClk[32];
-#define CLK_INIT unsigned long long clkLast = __builtin_amdgcn_s_memrealtime();
-#define CLK(i)                                                                  \
-  if (blockIdx.x == 0 && threadIdx.x == 0) {                                    \
-    const unsigned long long now = __builtin_amdgcn_s_memrealtime();            \
-    g_cholClk[i] += now - clkLast;                                              \
-    clkLast = now;                                                              \
-  }
-#define CLKW(i, cond)                                                           \
-  if (blockIdx.x == 0 && (cond)) {                                              \
-    const unsigned long long now = __builtin_amdgcn_s_memrealtime();            \
-    g_cholClk[i] += now - clkLast;                                              \
-    clkLast = now;                                                              \
-  }
-#else
-#define CLK_INIT
-#define CLK(i)
-#define CLKW(i, cond)
-#endif
+// (development-only phase clocks: CLK_INIT / CLK / CLKW, dev_clock.hpp; empty in product builds)
 
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
@@ -891,12 +871,7 @@ __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem
   }
   backSubstitute(P, w, W, ld, T, Linv, nz, sxDyn, sA, sy, t);
   CLK(3)
-#ifdef OKG_CHOL_CLOCK
-  if (blockIdx.x == 0 && t == 0)
-    printf("CHOLCLK T=%d potrf %llu panel %llu update %llu bsub %llu | load %llu pfac %llu ptrail %llu dinv %llu subd %llu store %llu y %llu (x10ns)\n",
-           T, g_cholClk[0], g_cholClk[1], g_cholClk[2] + g_cholClk[11], g_cholClk[3], g_cholClk[4], g_cholClk[5], g_cholClk[6],
-           g_cholClk[7], g_cholClk[8], g_cholClk[9], g_cholClk[10]);
-#endif
+  CHOL_CLK_REPORT(T)
 }
 
 // ---- tile-parallel schedule (few windows: spreads each window over many CUs; runtime.cpp
@@ -1117,9 +1092,7 @@ __global__ __launch_bounds__(kBsReal) void k_chol_bsub(const DevProblem* __restr
   for (int e = e0 + t; e < e1; e += kBsReal)
     if ((!split || h == 1 || e < tL * kTile || e >= tS * kTile) && !gapRow(P, w, e))
       gnFinalizeRow(P, (size_t)P.win_foff[w] + e, sx[e]);
-#ifdef OKG_CHOL_CLOCK
-  if (blockIdx.x == 0 && t == 0) printf("BSUBCLK T=%d init %llu steps %llu (x10ns)\n", T, g_cholClk[12], g_cholClk[13]);
-#endif
+  BSUB_CLK_REPORT(T)
 }
 
 bool cholesky_persistent_fits(int max_fpad, size_t lds_per_block) {

@@ -21,6 +21,7 @@
 // Ceres evaluates once for fixed_cost); 3 = like 2 without the robust loss (parity hook).
 #include <cfloat>
 
+#include "dev_clock.hpp"
 #include "device_problem.hpp"
 #include "launch.hpp"
 #include "okvisgpu_math.hpp"
@@ -327,39 +328,7 @@ __device__ void groupJacobi(double* A, double* V, double* rot, int l, bool need)
 #ifndef OKG_IMU_OCC
 #define OKG_IMU_OCC 2
 #endif
-// Development-only phase clock of k_eval_imu (make OPT="-O3 -DOKG_IMU_CLOCK"): every wavefront
-// accumulates its s_memrealtime ticks (100 MHz) per phase in wave-uniform (scalar) registers and
-// adds them to the totals once, at its end (per-phase atomics contended and inflated the phases
-// they fell into); the last workgroup prints the totals.
-#ifdef OKG_IMU_CLOCK
-__device__ unsigned long long g_imuClk[12];
-__device__ unsigned int g_imuDone;
-#define ICLK_INIT                                                                       \
-  unsigned long long iclk = __builtin_amdgcn_s_memrealtime(), iacc[12];                 \
-  for (int i_ = 0; i_ < 12; ++i_) iacc[i_] = 0;
-#define ICLK(i)                                                                         \
-  {                                                                                     \
-    const unsigned long long now = __builtin_amdgcn_s_memrealtime();                    \
-    iacc[i] += now - iclk;                                                              \
-    iclk = now;                                                                         \
-  }
-#define ICLK_END                                                                        \
-  if (!APPEND && threadIdx.x == 0) {                                                    \
-    for (int i_ = 0; i_ < 12; ++i_) atomicAdd(&g_imuClk[i_], iacc[i_]);                 \
-    __threadfence();                                                                    \
-    if (atomicAdd(&g_imuDone, 1u) == gridDim.x - 1) {                                   \
-      printf("IMUCLK pro %llu chain %llu state %llu sqrt %llu resid %llu jac %llu | R %llu Q %llu I %llu S %llu " \
-             "P %llu (x10ns)\n", g_imuClk[0], g_imuClk[1], g_imuClk[2], g_imuClk[3], g_imuClk[4], g_imuClk[5], \
-             g_imuClk[6], g_imuClk[7], g_imuClk[8], g_imuClk[9], g_imuClk[10]);                               \
-      for (int i_ = 0; i_ < 12; ++i_) g_imuClk[i_] = 0;                                 \
-      g_imuDone = 0;                                                                    \
-    }                                                                                   \
-  }
-#else
-#define ICLK_INIT
-#define ICLK(i)
-#define ICLK_END
-#endif
+// (development-only phase clock of k_eval_imu: ICLK_INIT / ICLK / ICLK_END, dev_clock.hpp)
 // APPEND: ImuError::append (ImuError.cpp:63-255) for a batch of factors (okvisgpu_imu_append): the
 // chain starts from the stored state (Delta_q, integrals, cross_, dv_db_g, P) at imu_t0 (= the old
 // t1), integrates the appended samples with the eliminated state's bias (sb[0] row blk[1]) up to
@@ -1014,10 +983,8 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
       }
     }
   }
-#ifdef OKG_IMU_CLOCK
   ICLK(5)
   ICLK_END
-#endif
 }
 
 template <bool APPEND>

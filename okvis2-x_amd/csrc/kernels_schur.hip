@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cfloat>
 
+#include "dev_clock.hpp"
 #include "device_problem.hpp"
 #include "launch.hpp"
 #include "okvisgpu_math.hpp"
@@ -93,34 +94,7 @@ __device__ __forceinline__ bool lmVisitSelect(const DevProblem& P, int w, int mo
 #endif
 constexpr int kPartRows = OKG_PART_ROWS, kPartThreads = 6 / kPartRows;  // partial-block rows per thread
 static_assert(kPartRows == 2 || kPartRows == 3, "OKG_PART_ROWS must be 2 or 3");
-// Development-only phase clock of k_lm_visit<1> (make OPT="-O3 -DOKG_LMV_CLOCK"): thread 0 of every
-// workgroup adds its s_memrealtime ticks (100 MHz) per phase with vector atomics; the last workgroup
-// prints the totals.
-#ifdef OKG_LMV_CLOCK
-__device__ unsigned long long g_lmvClk[8];
-__device__ unsigned int g_lmvDone;
-#define LCLK_INIT unsigned long long lclk = __builtin_amdgcn_s_memrealtime();
-#define LCLK(i)                                                                         \
-  if (mode == 1 && threadIdx.x == 0) {                                                  \
-    const unsigned long long now = __builtin_amdgcn_s_memrealtime();                    \
-    atomicAdd(&g_lmvClk[i], now - lclk);                                                \
-    lclk = now;                                                                         \
-  }
-#define LCLK_END                                                                        \
-  if (mode == 1 && threadIdx.x == 0) {                                                  \
-    __threadfence();                                                                    \
-    if (atomicAdd(&g_lmvDone, 1u) == gridDim.x - 1) {                                   \
-      printf("LMVCLK visit %llu lm %llu seg %llu z %llu stage %llu part %llu (x10ns, summed)\n", \
-             g_lmvClk[0], g_lmvClk[1], g_lmvClk[2], g_lmvClk[3], g_lmvClk[4], g_lmvClk[5]);       \
-      for (int i = 0; i < 8; ++i) g_lmvClk[i] = 0;                                      \
-      g_lmvDone = 0;                                                                    \
-    }                                                                                   \
-  }
-#else
-#define LCLK_INIT
-#define LCLK(i)
-#define LCLK_END
-#endif
+// (development-only phase clock of k_lm_visit<1>: LCLK_INIT / LCLK / LCLK_END, dev_clock.hpp)
 // (mode is a template parameter: each mode is its own specialised kernel, and rocprof reports them
 // apart — k_lm_visit<1> is the per-iteration linearisation, k_lm_visit<2> the GN prep)
 // EXT (batches with variable extrinsics): threads nvg.. of a group are its extrinsic visits — per
@@ -160,11 +134,7 @@ __device__ __forceinline__ void lmVisitGroup(const DevProblem& P, const int grp)
   // (the visit record is folded into the test, so the compiler issues its loads before the branch
   // instead of after it: vc >> 31 is 0, so the second term is always false)
   const bool skip = !selW | (((vLm ^ vPose ^ vSlot ^ obBeg ^ obEnd) & (vc >> 31)) != 0);
-#ifdef OKG_LMV_CLOCK
-  if (skip) { LCLK_END return; }
-#else
-  if (skip) return;    // uniform
-#endif
+  if (skip) { LCLK_END return; }  // uniform
   LCLK_INIT
   // the group's landmark-pair products go to LDS by DMA now (no registers held; they land with the
   // visit loads below and are read in the last phase)
@@ -546,11 +516,7 @@ __device__ __forceinline__ void lmVisitGroup(const DevProblem& P, const int grp)
 #pragma unroll
     for (int q = 0; q < 3 * kPartRows; ++q) out[q] = double2{acc[2 * q], acc[2 * q + 1]};
   }
-#ifdef OKG_LMV_CLOCK
-  __syncthreads();
-  LCLK(5)
-  LCLK_END
-#endif
+  LCLK_TAIL(5)
 }
 
 template <int mode, bool EXT>

@@ -23,7 +23,7 @@ void launch_host_scatter(const DevProblem& P, hipStream_t s);
 
 // landmark / reduced-system kernels (kernels_schur.hip); lin_mode 0 = init, 1 = accepted only
 void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t s);
-void launch_gn_reduce(const DevProblem& P, hipStream_t s);    // lm_prep + zero S + assemble
+void launch_gn_reduce(const DevProblem& P, hipStream_t s);    // lm_prep + assemble (S is initialised once per build, ensureS)
 void launch_gn_backsub(const DevProblem& P, hipStream_t s);   // landmark back substitution + gn vectors
 void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_imu_hess(const DevProblem& P, int lin_mode, hipStream_t s);

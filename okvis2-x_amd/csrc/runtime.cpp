@@ -267,7 +267,7 @@ void validate(const okvisgpu_problem* p, int w) {
   }
 }
 
-// Development: host-time split of analyse() (OKG_ANALYSE_TIMING, scripts/analyse_bench.cpp).
+// Development: host-time split of analyse() (build with -DOKG_ANALYSE_TIMING; printed per build).
 #ifdef OKG_ANALYSE_TIMING
 double g_atime[16];
 std::chrono::steady_clock::time_point g_alast;
@@ -1599,7 +1599,9 @@ struct okvisgpu_ctx {
       // latency there. The order is a function of the window and this flag only, so a window's
       // bits depend on the batch just through it.
       nb.nd = (int)probs.size() < cuCount;
-      if (const char* e = std::getenv("OKVISGPU_ND")) nb.nd = e[0] == '1';  // (development A/B)
+#ifdef OKG_ND_OVERRIDE
+      if (const char* e = std::getenv("OKVISGPU_ND")) nb.nd = e[0] == '1';  // (development A/B builds only)
+#endif
       analyse(probs, constOverride, nb);  // may throw: B is untouched until it succeeds
       B = std::move(nb);
     }

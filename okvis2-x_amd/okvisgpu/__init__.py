@@ -278,6 +278,30 @@ class OkvisGpuError(RuntimeError):
     pass
 
 
+class _OwnedBuffer:
+    """numpy base object of a view into library-owned memory: holds a reference to the Python
+    object that owns the memory, so the view keeps it (and its C allocation) alive."""
+
+    def __init__(self, ptr, shape, owner):
+        addr = C.cast(ptr, C.c_void_p).value
+        if not addr and int(np.prod(shape)) > 0:
+            raise OkvisGpuError("null array in problem")
+        self.__array_interface__ = {"data": (addr or 0, False), "shape": tuple(int(n) for n in shape),
+                                    "typestr": "<f8", "version": 3}
+        self._owner = owner
+
+
+def _owned_view(ptr, shape, owner) -> np.ndarray:
+    return np.asarray(_OwnedBuffer(ptr, shape, owner))
+
+
+def _owned_problem(ptr, owner):
+    """POINTER(Problem) / Problem from the library, each holding a reference to its owner (the
+    SynthWindow / Graph whose allocation the arrays point into)."""
+    ptr._owner = owner
+    return ptr
+
+
 class SynthWindow:
     """A synthetic sliding window (owned by the C library)."""
 
@@ -295,10 +319,12 @@ class SynthWindow:
 
     @property
     def problem(self) -> Problem:
-        return lib().okvisgpu_synth_problem(self.handle).contents
+        pr = self.problem_ptr().contents
+        pr._owner = self  # the struct's arrays live in this window's allocation
+        return pr
 
     def problem_ptr(self):
-        return lib().okvisgpu_synth_problem(self.handle)
+        return _owned_problem(lib().okvisgpu_synth_problem(self.handle), self)
 
     def reset(self):
         lib().okvisgpu_synth_reset(self.handle)
@@ -318,24 +344,24 @@ class SynthWindow:
 
     def extrinsics(self):
         p = self.problem
-        return np.ctypeslib.as_array(p.extrinsics, shape=(p.n_cameras, 7))
+        return _owned_view(p.extrinsics, (p.n_cameras, 7), self)
 
-    # views into the (mutable) parameter arrays
+    # views into the (mutable) parameter arrays; each view keeps this window alive
     def poses(self):
         p = self.problem
-        return np.ctypeslib.as_array(p.poses, shape=(p.n_poses, 7))
+        return _owned_view(p.poses, (p.n_poses, 7), self)
 
     def speed_biases(self):
         p = self.problem
-        return np.ctypeslib.as_array(p.speed_biases, shape=(p.n_speed_biases, 9))
+        return _owned_view(p.speed_biases, (p.n_speed_biases, 9), self)
 
     def landmarks(self):
         p = self.problem
-        return np.ctypeslib.as_array(p.landmarks, shape=(p.n_landmarks, 4))
+        return _owned_view(p.landmarks, (p.n_landmarks, 4), self)
 
     def imu_state(self):
         p = self.problem
-        return np.ctypeslib.as_array(p.imu_state, shape=(p.n_imu, IMU_STATE_DOUBLES))
+        return _owned_view(p.imu_state, (p.n_imu, IMU_STATE_DOUBLES), self)
 
     def __del__(self):
         try:
@@ -429,10 +455,12 @@ class Graph:
 
     @property
     def problem(self) -> Problem:
-        return lib().okvisgpu_graph_problem(self.handle).contents
+        pr = self.problem_ptr().contents
+        pr._owner = self
+        return pr
 
     def problem_ptr(self):
-        return lib().okvisgpu_graph_problem(self.handle)
+        return _owned_problem(lib().okvisgpu_graph_problem(self.handle), self)
 
     def ids(self):
         p = self.problem
@@ -444,11 +472,11 @@ class Graph:
 
     def poses(self):
         p = self.problem
-        return np.ctypeslib.as_array(p.poses, shape=(p.n_poses, 7))
+        return _owned_view(p.poses, (p.n_poses, 7), self)
 
     def landmarks(self):
         p = self.problem
-        return np.ctypeslib.as_array(p.landmarks, shape=(p.n_landmarks, 4))
+        return _owned_view(p.landmarks, (p.n_landmarks, 4), self)
 
     def __del__(self):
         try:

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (OKVISGPU_ND is read only by a library built with -DOKG_ND_OVERRIDE: make OPT="-O3 -DOKG_ND_OVERRIDE")
 # Kernel-trace stats of the Cholesky launches per schedule at a batch size (via gpurun): TAG WINDOWS "SCHEDULES"
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (OKVISGPU_ND is read only by a library built with -DOKG_ND_OVERRIDE: make OPT="-O3 -DOKG_ND_OVERRIDE")
 # Batch rate vs windows per GPU for the Cholesky schedule x state order (nested dissection on/off):
 # which one the automatic choice should take at each batch size. Usage (via gpurun): nd_probe.sh TAG
 set -o pipefail

@@ -66,6 +66,13 @@ struct ImuErrorFiller : ImuError {
   }
   const mini::Matrix<15, 15>& info() const { return information_; }
   const mini::AlignedVector<mini::Matrix<15, 15>>& dP() const { return dPdsigma_; }
+  // four distinct per-sigma derivatives (what okvis' own integration leaves)
+  void setDistinctDp() {
+    dPdsigma_.resize(4);
+    for (int k = 0; k < 4; ++k)
+      for (int r = 0; r < 15; ++r)
+        for (int c = 0; c < 15; ++c) dPdsigma_[k](r, c) = 0.5 * k + 0.01 * r - 0.002 * c;
+  }
 };
 
 int cpuTests() {
@@ -133,9 +140,11 @@ int cpuTests() {
   CHECK(std::memcmp(view.state.data(), u.data(), sizeof(double) * OKVISGPU_IMU_STATE_DOUBLES) == 0);
   view.state[0] = 11;  // what a solve's write-back leaves in the term
   view.state[57 + 3] = 0.123;
+  f.setDistinctDp();  // P_delta_ unchanged by the "solve": the object's own dPdsigma_ stays
   view.pushState();
   Members::read(f, u.data());
   CHECK(u[0] == 11 && u[60] == 0.123);
+  CHECK(f.dP().size() == 4 && f.dP()[2](3, 5) == 0.5 * 2 + 0.01 * 3 - 0.002 * 5 && f.dP()[0](1, 1) == 0.01 - 0.002);
   e.fill(0.75);  // the object changed between solves (ImuError::append): the view re-reads it
   okvisgpu::OkvisImuError<ImuError> view2(&e);
   e.fill(0.25);
