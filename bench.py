@@ -261,6 +261,33 @@ def run_cpu_baseline(cfg, iters, threads, n_windows, reps):
     return ws[0], s0, float(np.median(times))
 
 
+def run_cpu_baseline_batch(cfg, iters, host_threads, n_windows, reps):
+    """Like-for-like CPU batch: `host_threads` workers each solve their own windows with one solver
+    thread (num_threads = 1), all in flight together, like the GPU's batch of independent windows.
+    The oracle's C solve runs without the GIL (ctypes), so the workers run in parallel. Returns the
+    median wall time of `reps` passes over `n_windows` windows after one warm-up pass."""
+    from concurrent.futures import ThreadPoolExecutor
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import _oracle  # noqa: E402  (bench.py's cpu_baseline leg is an allowed oracle user)
+    ws = make_windows(cfg, range(n_windows))
+    opts = bench_options(iters)
+    opts.num_threads = 1
+
+    def one(w):
+        w.reset()
+        return _oracle.solve(w.problem_ptr(), opts)["num_iterations"]
+
+    times = []
+    with ThreadPoolExecutor(max_workers=host_threads) as ex:
+        for r in range(reps + 1):
+            t0 = time.perf_counter()
+            its = list(ex.map(one, ws))
+            if r > 0:
+                times.append(time.perf_counter() - t0)
+            assert all(i == iters for i in its), its
+    return float(np.median(times))
+
+
 def free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -291,7 +318,9 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=3, help="realtime_num_threads (okvis2.yaml:93)")
     ap.add_argument("--cpu-iters", type=int, default=None, help="default: warmup + steps")
     ap.add_argument("--cpu-reps", type=int, default=5, help="median of this many timed passes after 1 warm-up")
-    ap.add_argument("--cpu-windows", type=int, default=24, help="windows in the CPU baseline sample")
+    ap.add_argument("--cpu-windows", type=int, default=24, help="windows in the realtime (one at a time) CPU sample")
+    ap.add_argument("--cpu-batch-windows", type=int, default=None,
+                    help="windows in the batch CPU sample (default: 3 per host thread)")
     ap.add_argument("--kernel-reps", type=int, default=5, help="repetitions per kernel in the roofline table")
     ap.add_argument("--e2e-reps", type=int, default=5, help="single-window set_problems + solve repetitions")
     ap.add_argument("--cholesky-schedule", type=int, default=0, help="0 auto, 1 persistent per window, 2 tile-parallel, 3 persistent split over a nested-dissection window")
@@ -539,15 +568,20 @@ def main(argv=None):
                 if th == args.cpu_threads:
                     wc, sc = wct, sct
             best = variants[f"{allc}_threads"]
+            nb = args.cpu_batch_windows if args.cpu_batch_windows is not None else 3 * allc
+            dtb = run_cpu_baseline_batch(cfg, args.cpu_iters, allc, nb, args.cpu_reps)
+            variants[f"batch_{allc}x1_threads"] = {"value": nb * args.cpu_iters / dtb, "wall_s": dtb, "windows": nb}
+            batch = variants[f"batch_{allc}x1_threads"]
             result["cpu_baseline"] = {
-                "value": best["value"],
+                "value": batch["value"],
                 "unit": "window-iterations/s",
                 "cores": allc,
                 "kind": "port",
-                "sample": f"{args.cpu_windows} {args.config.upper()} windows x {args.cpu_iters} iterations each, "
-                          f"median of {args.cpu_reps} passes after 1 warm-up (oracle/liboracle.so, same options); "
-                          f"value at all {allc} host threads given to the job, also at "
-                          f"{args.cpu_threads} = realtime_num_threads",
+                "sample": f"batch: {nb} {args.config.upper()} windows x {args.cpu_iters} iterations each, "
+                          f"{allc} host threads each solving its own windows with one solver thread (all in flight "
+                          f"together, like the GPU batch), median of {args.cpu_reps} passes after 1 warm-up "
+                          f"(oracle/liboracle.so, same options). Realtime variants: {args.cpu_windows} windows one at "
+                          f"a time at {args.cpu_threads} = realtime_num_threads and at {allc} threads per solve",
                 "host": {"cpu_model": cpu_model(), "host_threads": allc, "nproc": os.cpu_count()},
                 "variants": variants,
             }

@@ -225,6 +225,36 @@ def test_batched_windows_match_single(og, gpu_ctx):
         assert np.array_equal(w.poses(), Pb[k])
 
 
+@pytest.mark.parametrize("n_batch", [100, 300])
+def test_window_alone_vs_large_batch(og, gpu_ctx, parity, n_batch):
+    """A window's operation order depends on the batch only through the batch size against the
+    device's CU count (runtime.cpp: the nested-dissection state order below one window per CU;
+    device_problem.hpp fewWindows: 1,024-thread per-window reductions and fused launches at or
+    below a quarter window per CU). On MI355X (256 CUs) a window alone runs with both, in a batch of
+    100 with the order but not the reductions, in a batch of 300 with neither. Bitwise equality
+    holds inside one regime (test_batched_windows_match_single); across regimes the solves agree to
+    rounding: same iterations, termination and successful steps, cost and poses to the solve
+    tolerances."""
+    seeds = [900 + k for k in range(n_batch)]
+    ws = [_window(og, seed=s) for s in seeds]
+    opts = og.default_options(max_num_iterations=5)
+    gpu_ctx.set_problems([w.problem for w in ws])
+    sb = gpu_ctx.solve(opts, n_batch)
+    picks = (0, n_batch // 2, n_batch - 1)
+    Pb = {k: ws[k].poses().copy() for k in picks}
+    for k in picks:
+        w = ws[k]
+        w.reset()
+        gpu_ctx.set_problems([w.problem])
+        s1 = gpu_ctx.solve(opts, 1)[0]
+        for f in ("num_iterations", "termination_type", "num_successful_steps"):
+            assert s1[f] == sb[k][f], (f, k)
+        parity(f"window alone vs in a batch of {n_batch}: cost (rel)",
+               abs(s1["final_cost"] - sb[k]["final_cost"]) / sb[k]["final_cost"], 1e-9)
+        parity(f"window alone vs in a batch of {n_batch}: positions (m)",
+               float(np.abs(w.poses()[:, :3] - Pb[k][:, :3]).max()), 1e-8)
+
+
 def test_solve_is_deterministic(og, gpu_ctx):
     w = _window(og)
     opts = og.default_options(max_num_iterations=5)
