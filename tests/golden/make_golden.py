@@ -36,13 +36,19 @@ DIGEST_FIELDS = ("poses", "pose_constant", "speed_biases", "speed_bias_constant"
                  "relpose_sqrt_info", "relpose_lin_point", "relpose_kind")
 
 
-def input_digest(problem):
-    """SHA-256 over the input arrays of a problem (DIGEST_FIELDS, then samples, cameras, IMU params)."""
+def input_digest(problem, variable_extrinsics=False):
+    """SHA-256 over the input arrays of a problem (DIGEST_FIELDS, then samples, cameras, IMU params;
+    with variable_extrinsics also the extrinsics flags and priors)."""
     p = OwnedProblem.copy_of(problem)
     assert not np.any(p.imu_state), "a golden window starts from fresh IMU states"
-    assert np.all(p.extrinsics_constant == 1), "golden windows have constant extrinsics"
+    fields = DIGEST_FIELDS
+    if variable_extrinsics:
+        fields = fields + ("extrinsics_constant", "extrinsics_prior_camera", "extrinsics_prior_meas",
+                           "extrinsics_prior_sqrt_info")
+    else:
+        assert np.all(p.extrinsics_constant == 1), "golden windows have constant extrinsics"
     h = hashlib.sha256()
-    for k in DIGEST_FIELDS:
+    for k in fields:
         h.update(k.encode())
         h.update(np.ascontiguousarray(getattr(p, k)).tobytes())
     for a in (p.imu_sample_begin, p.imu_sample_t_ns, p.imu_sample_gyr_acc):

@@ -148,7 +148,8 @@ class _PairedBackend:
         for k, a in v.items():
             a[:] = snap[k]
         sc = self.oracle.solve(C.pointer(P), options)
-        self.records.append({"gpu": sg, "cpu": sc, "perturbed": sp, "dpose": float(np.abs(gpu_poses[:, :3] - v["poses"][:, :3]).max())})
+        self.records.append({"gpu": sg, "cpu": sc, "perturbed": sp, "dpose": float(np.abs(gpu_poses[:, :3] - v["poses"][:, :3]).max()),
+                             "drel": _relative_pose_dev(gpu_poses, v["poses"])})
         return sc
 
     def imu_append(self, *args):
@@ -159,6 +160,24 @@ class _PairedBackend:
 
     def close(self):
         self.ctx.close()
+
+
+def _rot(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def _relative_pose_dev(Pa, Pb):
+    """max over consecutive states of the difference of the relative translations R_i^T (p_i+1 - p_i)
+    (metres): invariant under a common rigid motion of all states, the gauge freedom of a window
+    whose first-state prior carries no information in some directions (ViGraph.cpp:348-361)."""
+    if len(Pa) < 2:
+        return 0.0
+    def rel(P):
+        return np.array([_rot(P[i, 3:]).T @ (P[i + 1, :3] - P[i, :3]) for i in range(len(P) - 1)])
+    return float(np.abs(rel(Pa) - rel(Pb)).max())
 
 
 @pytest.mark.gpu
@@ -184,6 +203,7 @@ def test_gpu_vigraph2(og, oracle, case, parity):
     finally:
         paired.close()
     worst_tight, worst_pose = 0.0, 0.0
+    worst_free, worst_free_ratio, worst_free_rel, n_free = 0.0, 0.0, 0.0, 0
     for k, r in enumerate(paired.records):
         g, c, p = r["gpu"], r["cpu"], r["perturbed"]
         assert (g["num_iterations"], g["termination"], g["num_successful_steps"]) == \
@@ -194,5 +214,16 @@ def test_gpu_vigraph2(og, oracle, case, parity):
         if sens < 1e-9:  # well-conditioned solves: the usual bounds
             worst_tight = max(worst_tight, rel)
             worst_pose = max(worst_pose, r["dpose"])
+        else:  # gauge-free solves: cost against the oracle's own sensitivity, gauge-invariant poses
+            n_free += 1
+            worst_free = max(worst_free, rel)
+            worst_free_ratio = max(worst_free_ratio, rel / max(10.0 * sens, 1e-7))
+            worst_free_rel = max(worst_free_rel, r["drel"])
     parity(f"TestViGraph2 case {case}: cost, well-conditioned solves (rel)", worst_tight, 1e-7)
     parity(f"TestViGraph2 case {case}: poses, well-conditioned solves (m)", worst_pose, 1e-6)
+    print(f"TestViGraph2 case {case}: {n_free} gauge-free solves of {len(paired.records)}")
+    parity(f"TestViGraph2 case {case}: cost, gauge-free solves (rel)", worst_free, 1e-3)
+    parity(f"TestViGraph2 case {case}: cost, gauge-free solves (rel / max(10 x oracle sensitivity, 1e-7))",
+           worst_free_ratio, 1.0)
+    parity(f"TestViGraph2 case {case}: relative poses of consecutive states, gauge-free solves (m)",
+           worst_free_rel, 1e-3)
