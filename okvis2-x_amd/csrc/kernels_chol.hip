@@ -419,10 +419,22 @@ __device__ __forceinline__ void xStoreRows16(const double* sX, double* Li, int q
 // Returns false (uniformly) at a non-positive pivot.
 // (one non-inlined instantiation per calling kernel: a shared callee gets a generic register
 // budget that halves the persistent kernel's occupancy)
+// Team callers (kCaller >= 20: the pipelined persistent kernel, whose workgroup holds two teams of
+// four wavefronts) run it on one team: t is the team's thread index, and the three workgroup
+// barriers become barriers of the team's four wavefronts on the counter sFl[4], whose arrival
+// count before the call is 4 * tgen0 (the caller adds kPotrfBarriers to its count afterwards).
+__host__ __device__ constexpr bool teamCaller(int kCaller) { return kCaller >= 20; }
+constexpr int kPotrfBarriers = 3;
+template <int kCaller>
+__device__ __forceinline__ void potrfSync(int* sFl, int& tgen, int lane) {
+  if (teamCaller(kCaller)) waveBarrier<true>(&sFl[4], tgen, 4, lane);
+  else ldsBarrier();
+}
 template <int kCaller>
 __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX, double* sy,
-                                      double* sRl, int* sFl, int t, bool haveTile) {
+                                      double* sRl, int* sFl, int t, bool haveTile, int tgen0 = 0) {
   const int wave = t >> 6, lane = t & 63;
+  int tgen = tgen0;
   CLK_INIT
   if (!haveTile) loadTile(Sg, ld, 0, 0, sA, t);  // (else the caller left S_kk in sA)
 #pragma unroll
@@ -431,7 +443,7 @@ __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li,
     sX[(e >> 6) * kLd + (e & 63)] = 0.0;
   }
   if (t < 4) sFl[t] = 0;  // sub-panels factored, trailing updates done, fail, barrier counter
-  ldsBarrier();
+  potrfSync<kCaller>(sFl, tgen, lane);
   CLK(4)
   // Sweep with look-ahead: wavefront 0 runs the chain of the 8 sub-panel factorisations and
   // applies each sub-panel's rank-8 update to the next sub-panel's 8 columns itself (VALU, its own
@@ -509,7 +521,7 @@ __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li,
       }
     }
   }
-  ldsBarrier();
+  potrfSync<kCaller>(sFl, tgen, lane);
   CLK(5)
   if (sFl[2]) return false;
   // LDS-only barriers from here: the X / y stores stay in flight (no reader in this
@@ -519,7 +531,7 @@ __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li,
     sy[t] = y;
     if (!persistentCaller(kCaller)) workk[t] = y;
   }
-  ldsBarrier();
+  potrfSync<kCaller>(sFl, tgen, lane);
   CLK(10)
   return true;
 }

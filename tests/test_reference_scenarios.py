@@ -226,4 +226,4 @@ def test_gpu_vigraph2(og, oracle, case, parity):
     parity(f"TestViGraph2 case {case}: cost, gauge-free solves (rel / max(10 x oracle sensitivity, 1e-7))",
            worst_free_ratio, 1.0)
     parity(f"TestViGraph2 case {case}: relative poses of consecutive states, gauge-free solves (m)",
-           worst_free_rel, 1e-3)
+           worst_free_rel, 1e-5)
