@@ -1,0 +1,756 @@
+// chol_tiles.hpp — the tile routines of the dense LLT of the reduced camera matrix (kernels_chol.hip,
+// kernels_chol_pipe.hip): 64x64 FP64 tiles staged in LDS, products on the FP64 matrix cores, the
+// diagonal-tile factor (potrfTile), panels, the backward substitution. Every schedule builds on
+// these, so the schedules perform the same tile operations and give the same bits.
+//
+// MFMA tile: each of the 4 wavefronts owns a 32x32 quarter of the 64x64 output (2x2 16x16 MFMA
+// tiles), K = 64 in steps of 4. v_mfma_f64_16x16x4_f64 operand map: lane l supplies A[l&15][l>>4]
+// and B[l>>4][l&15]; result reg r of lane l is C[(l>>4) + 4r][l&15] (cdna_hip_programming.md §3).
+#pragma once
+#include "dev_clock.hpp"
+#include "device_problem.hpp"
+#include "okvisgpu_math.hpp"
+
+namespace okg {
+
+constexpr int kLd = kTile + 1;  // padded LDS row (65 doubles)
+
+// (development-only phase clocks: CLK_INIT / CLK / CLKW, dev_clock.hpp; empty in product builds)
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bool cholSelect(const DevProblem& P, int w) {
+  const WinState& s = P.st[w];
+  return !s.done && s.need_gn && !s.gn_failed;
+}
+
+// Tile (i, j) as the factorisation sees it at step k: the assembled S until the first band update
+// has written it (step tile_fu), the working copy W from then on. Every factorisation write (band
+// updates, panels L_ik, the tile-parallel schedule's upper-slot L) goes to W, so S keeps the
+// assembled blocks and zeros and is never cleared per iteration.
+struct TileSrc {
+  const double* S;
+  const double* W;
+  const int16_t* fu;
+  int T;
+  int64_t ld;
+  __device__ __forceinline__ const double* at(int i, int j, int k) const {
+    return (fu[i * T + j] < k ? W : S) + (int64_t)i * kTile * ld + j * kTile;
+  }
+};
+__device__ __forceinline__ TileSrc tileSrc(const DevProblem& P, int w, int64_t ld) {
+  return TileSrc{P.S + P.win_soff[w], P.W + P.win_soff[w], P.tile_fu + P.win_tnzoff[w], (int)(ld / kTile), ld};
+}
+
+// 64x64 global tile (row stride ld) -> LDS [64][kLd]: all 8 16-byte loads of a thread are issued
+// before the LDS stores.
+__device__ __forceinline__ void loadTile(const double* A, int64_t ld, int r0, int c0, double* s, int t) {
+  double2 v[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = t + 256 * u, r = e >> 5, c = 2 * (e & 31);
+    v[u] = *gmem(reinterpret_cast<const double2*>(A + (int64_t)(r0 + r) * ld + c0 + c));
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int e = t + 256 * u, r = e >> 5, c = 2 * (e & 31);
+    s[r * kLd + c] = v[u].x;
+    s[r * kLd + c + 1] = v[u].y;
+  }
+}
+
+// acc = sA * sB^T over the 64-deep inner dimension (both tiles row-major [64][kLd] in LDS).
+__device__ __forceinline__ void mfmaTileNT(const double* sA, const double* sB, dbl4 acc[2][2], int t) {
+  const int wave = t >> 6, lane = t & 63;
+  const int r0 = 32 * (wave >> 1), c0 = 32 * (wave & 1);
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int kk = 0; kk < kTile; kk += 4) {
+    double av[2], bv[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) av[a] = sA[(r0 + 16 * a + lr) * kLd + kk + lk];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) bv[b] = sB[(c0 + 16 * b + lr) * kLd + kk + lk];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], bv[b], acc[a][b], 0, 0, 0);
+  }
+}
+
+template <bool SUB>
+__device__ __forceinline__ void storeTile(double* A, int64_t ld, int r0g, int c0g, const dbl4 acc[2][2], int t) {
+  const int wave = t >> 6, lane = t & 63;
+  const int r0 = 32 * (wave >> 1), c0 = 32 * (wave & 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int rr = r0 + 16 * a + (lane >> 4) + 4 * reg;
+        const int cc = c0 + 16 * b + (lane & 15);
+        auto dst = gmemw(A + (int64_t)(r0g + rr) * ld + c0g + cc);
+        if (SUB) *dst -= acc[a][b][reg];
+        else *dst = acc[a][b][reg];
+      }
+}
+
+// The C-layout values of a 64x64 global tile (as storeTile writes them), and C - acc stored back.
+__device__ __forceinline__ void loadC(const double* A, int64_t ld, dbl4 c[2][2], int t) {
+  const int wave = t >> 6, lane = t & 63;
+  const int r0 = 32 * (wave >> 1), c0 = 32 * (wave & 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg)
+        c[a][b][reg] = gmem(A)[(int64_t)(r0 + 16 * a + (lane >> 4) + 4 * reg) * ld + c0 + 16 * b + (lane & 15)];
+}
+__device__ __forceinline__ void storeTileSub(double* A, int64_t ld, const dbl4 c[2][2], const dbl4 acc[2][2], int t) {
+  const int wave = t >> 6, lane = t & 63;
+  const int r0 = 32 * (wave >> 1), c0 = 32 * (wave & 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg)
+        gmemw(A)[(int64_t)(r0 + 16 * a + (lane >> 4) + 4 * reg) * ld + c0 + 16 * b + (lane & 15)] = c[a][b][reg] - acc[a][b][reg];
+}
+
+// 1/sqrt(d) to ~1 ulp: v_rsq_f64 (~5e-8 relative) refined by two Newton steps (measured on
+// gfx950: 2.3e-16 max relative error over d in [e^-40, e^40]).
+__device__ __forceinline__ double rsqrtRefined(double d) {
+  double r = __builtin_amdgcn_rsq(d);
+  const double h = 0.5 * d;
+  r = r * (1.5 - h * r * r);
+  r = r * (1.5 - h * r * r);
+  return r;
+}
+
+// 16x16 block product on one wavefront: acc += sign * A(16 x 16K) B(16K x 16) with
+// A[m][k] = a[m * lda + k], B[k][n] = b[k * ldbk + n * ldbn] (LDS), result in the MFMA C layout.
+template <int KB>
+__device__ __forceinline__ void mfma16(const double* a, int lda, const double* b, int ldbk, int ldbn, double sign,
+                                       dbl4& acc, int lane) {
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < 4 * KB; ++q) {
+    const double av = sign * a[lr * lda + 4 * q + lk];
+    const double bv = b[(4 * q + lk) * ldbk + lr * ldbn];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+  }
+}
+__device__ __forceinline__ dbl4 loadC16(const double* c, int ldc, int lane) {
+  dbl4 v;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = c[((lane >> 4) + 4 * r) * ldc + (lane & 15)];
+  return v;
+}
+__device__ __forceinline__ void storeC16(double* c, int ldc, const dbl4& v, int lane) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) c[((lane >> 4) + 4 * r) * ldc + (lane & 15)] = v[r];
+}
+
+__device__ __forceinline__ int ldsAcquire(int* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void ldsRelease(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// LDS flags with LDS-only ordering (the diagonal tile's hand-overs, where only LDS data is passed
+// between wavefronts): the fences are restricted to the local address space. A release at
+// workgroup scope also waits for every outstanding global store of the wavefront (vmcnt(0)),
+// which stalled the X-storing wavefronts by ~2k cycles per hand-over.
+__device__ __forceinline__ int ldsAcquireL(int* p) {
+  const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  return v;
+}
+__device__ __forceinline__ void ldsReleaseL(int* p, int v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Poll interval of the LDS flag waits (s_sleep units of 64 clocks; build knob: 0, 1 and 2 measured
+// within noise of each other at 2,048 windows and on one window).
+#ifndef OKG_WAIT_SLEEP
+#define OKG_WAIT_SLEEP 1
+#endif
+// Wave-uniform wait for *p >= v; false once the factor wavefront reported a failed pivot.
+template <bool LOCAL = false>
+__device__ __forceinline__ bool waitFlag(int* p, int v, int* fail) {
+  for (;;) {
+    if ((LOCAL ? ldsAcquireL(p) : ldsAcquire(p)) >= v) return true;
+    if (LOCAL ? ldsAcquireL(fail) : ldsAcquire(fail)) return false;
+    __builtin_amdgcn_s_sleep(OKG_WAIT_SLEEP);
+  }
+}
+// Barrier of n wavefronts on a monotonic arrival counter (gen counts this wavefront's barriers).
+template <bool LOCAL = false>
+__device__ __forceinline__ void waveBarrier(int* ctr, int& gen, int n, int lane) {
+  ++gen;
+  if (LOCAL) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (ldsAcquireL(ctr) < gen * n) __builtin_amdgcn_s_sleep(OKG_WAIT_SLEEP);
+  } else {
+    if (lane == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (ldsAcquire(ctr) < gen * n) __builtin_amdgcn_s_sleep(OKG_WAIT_SLEEP);
+  }
+}
+
+// One 8-column sub-panel of the in-LDS 64x64 LLT on one wavefront (lane = row i of the tile; the
+// rows of the sub-panel's 8x8 diagonal block D are rows c0..c0+7). No cross-lane traffic in the
+// column chain: every lane loads D (LDS broadcast reads) and factors it redundantly in registers,
+// then solves its own row r (the row's 8 entries of the sub-panel, updated) against it (row
+// TRSM), so the 8 dependent pivots cost only the FP64 latency of rsqrt + scaling + the next pivot
+// update. x: row i of L in the sub-panel (x[i - c0] = r * rl = d * rl = L_ii, bit-identical to the
+// redundant factor's L_ii). Returns false (wave-uniform) at a non-positive pivot.
+__device__ __forceinline__ bool chol8Row(const double* sA, int c0, double (&r)[8], double (&x)[8], double (&rl)[8]) {
+  double D[8][8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int k = 0; k <= m; ++k) D[m][k] = sA[(c0 + m) * kLd + c0 + k];
+  bool bad = false;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const double d = D[c][c];
+    if (!(d > 0.0)) bad = true;  // wave-uniform (every lane holds the same D)
+    rl[c] = rsqrtRefined(d);
+#pragma unroll
+    for (int m = c + 1; m < 8; ++m) D[m][c] *= rl[c];
+    x[c] = r[c] * rl[c];
+#pragma unroll
+    for (int m = c + 1; m < 8; ++m) {
+      D[m][m] -= D[m][c] * D[m][c];  // next pivots first: they carry the chain
+      r[m] -= x[c] * D[m][c];
+    }
+#pragma unroll
+    for (int m = c + 2; m < 8; ++m)
+#pragma unroll
+      for (int k = c + 1; k < m; ++k) D[m][k] -= D[m][c] * D[k][c];
+  }
+  return !bad;
+}
+// Row i of L for the sub-panel into the tile: all 8 entries below the diagonal block, entries
+// k <= i - c0 inside it.
+__device__ __forceinline__ void storeRow8(double* sA, int c0, const double (&x)[8], int i) {
+  if (i >= c0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (i >= c0 + 8 || k <= i - c0) sA[i * kLd + c0 + k] = x[k];
+  }
+}
+// 8x8 diagonal block of X = L^-1 from the final L_D in the tile and 1/L_cc (sRl): lanes 0..7, one
+// column j = lane each, y_m = (delta_mj - sum_{k<m} L_mk y_k) / L_mm, to xd (row stride kLd).
+__device__ __forceinline__ void inv8(const double* sA, const double* sRl, double* xd, int c0, int lane) {
+  if (lane >= 8) return;
+  // every operand into registers before the first store (xd may alias sA for the compiler, so a
+  // load after a store would wait for it: one LDS round trip per row)
+  double L[8][8], rl[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    rl[m] = sRl[c0 + m];
+#pragma unroll
+    for (int k = 0; k < m; ++k) L[m][k] = sA[(c0 + m) * kLd + c0 + k];
+  }
+  double y[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    double v = (m == lane) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < m; ++k) v -= L[m][k] * y[k];
+    y[m] = v * rl[m];
+  }
+#pragma unroll
+  for (int m = 0; m < 8; ++m) xd[m * kLd + lane] = y[m];
+}
+// The whole sub-panel on one wavefront: factor, L into the tile, 1/L_cc to sRl and the 8x8
+// diagonal inverse block to xd. Returns false (wave-uniform) at a non-positive pivot.
+__device__ __forceinline__ bool subPanel8(double* sA, double* xd, double* sRl, int c0, int lane) {
+  double r[8], x[8], rl[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = sA[lane * kLd + c0 + k];
+  if (!chol8Row(sA, c0, r, x, rl)) return false;
+  storeRow8(sA, c0, x, lane);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sRl[c0 + k] = rl[k];
+  }
+  __builtin_amdgcn_wave_barrier();
+  inv8(sA, sRl, xd, c0, lane);
+  return true;
+}
+
+// Rank-8 trailing update of the in-LDS tile by sub-panel c0: A_ij -= sum_k L_ik L_jk (k in the
+// sub-panel) for the 16x16 output blocks of rows and columns >= cs (cs >= c0 + 8, a multiple of 8),
+// lower block triangle, dealt to nw wavefronts (this one is wg of nw). A block column that starts
+// before cs keeps its left 8 columns (already final L, or the next sub-panel's columns, which the
+// look-ahead wavefront may be updating: not written at all), and the block row that starts there
+// keeps its top 8 rows (the upper triangle, where potrfWave stashes inverse blocks).
+__device__ __forceinline__ void trailingFrom(double* sA, int c0, int cs, int wg, int nw, int lane) {
+  const int cb0 = cs >> 4;
+  const bool part = (cs & 15) != 0;
+  const int lr = lane & 15, lk = lane >> 4;
+  int idx = 0;
+  for (int rb = cb0; rb < 4; ++rb)
+    for (int cb = cb0; cb <= rb; ++cb, ++idx) {
+      if (idx % nw != wg) continue;
+      double* C = sA + 16 * rb * kLd + 16 * cb;
+      dbl4 acc = loadC16(C, kLd, lane);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const double av = -sA[(16 * rb + lr) * kLd + c0 + 4 * q + lk];
+        const double bv = sA[(16 * cb + lr) * kLd + c0 + 4 * q + lk];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+      // masked entries are not written back at all: another wavefront may be updating them
+      if (part && cb == cb0 && lr < 8) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (!(part && rb == cb0 && r < 2)) C[(lk + 4 * r) * kLd + lr] = acc[r];  // rows lk + 4 r
+    }
+}
+__device__ __forceinline__ void trailing8(double* sA, int c0, int wg, int nw, int lane) {
+  trailingFrom(sA, c0, c0 + 8, wg, nw, lane);
+}
+
+// X = L^-1 of the in-LDS diagonal tile by 16-row block rows (sX holds X, sA the final L):
+// X21 = -X22 (L21 X11) of the diagonal 16x16 block q, whose 8x8 diagonal inverses are in sX
+// (one wavefront; lane = (row m, column j)).
+__device__ __forceinline__ void xDiag16(const double* sA, double* sX, int q, int lane) {
+  const int m = lane >> 3, j = lane & 7;
+  const int b = 16 * q;
+  double t = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t += sA[(b + 8 + m) * kLd + b + k] * sX[(b + k) * kLd + b + j];
+  sX[(b + 8 + m) * kLd + b + j] = t;  // T = L21 X11 staged in place (this wavefront only)
+  __builtin_amdgcn_wave_barrier();
+  double tk[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) tk[k] = sX[(b + 8 + k) * kLd + b + j];
+  double v = 0.0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v += sX[(b + 8 + m) * kLd + b + 8 + k] * tk[k];
+  __builtin_amdgcn_wave_barrier();
+  sX[(b + 8 + m) * kLd + b + j] = -v;
+}
+// X_qj = -X_qq (sum_{m=j}^{q-1} L_qm X_mj), j < q, on the matrix cores (one wavefront).
+__device__ __forceinline__ void xOffDiag16(const double* sA, double* sX, int q, int j, int lane) {
+  dbl4 acc = dbl4{0.0, 0.0, 0.0, 0.0};
+  for (int m = j; m < q; ++m)  // T = sum L_qm X_mj   (B[k][n] = X[16m + k][16j + n])
+    mfma16<1>(sA + 16 * q * kLd + 16 * m, kLd, sX + 16 * m * kLd + 16 * j, kLd, 1, 1.0, acc, lane);
+  double* Xqj = sX + 16 * q * kLd + 16 * j;
+  storeC16(Xqj, kLd, acc, lane);  // T staged in the (q, j) block (this wavefront only)
+  dbl4 x = dbl4{0.0, 0.0, 0.0, 0.0};
+  mfma16<1>(sX + 16 * q * kLd + 16 * q, kLd, Xqj, kLd, 1, -1.0, x, lane);
+  storeC16(Xqj, kLd, x, lane);
+}
+// y_r = sum_{j <= r} X_rj rhs_j for the 16 rows of block q (rhs in sy[0..63], y to sy[64 + r]):
+// lane = (row r, quarter p of the columns j = p mod 4), fixed butterfly over the quarters.
+__device__ __forceinline__ void yBlock16(const double* sX, double* sy, int q, int lane) {
+  const int r = 16 * q + (lane & 15), p = lane >> 4;
+  double xv[16], rv[16];
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {  // all operands first (columns beyond r are masked)
+    xv[it] = sX[r * kLd + p + 4 * it];
+    rv[it] = sy[p + 4 * it];
+  }
+  double a = 0.0;
+#pragma unroll
+  for (int it = 0; it < 16; ++it) a += (p + 4 * it <= r) ? xv[it] * rv[it] : 0.0;
+  a += __shfl_xor(a, 16, 64);
+  a += __shfl_xor(a, 32, 64);
+  if (p == 0) sy[kTile + r] = a;
+}
+// The 16 rows of block q of X to Li (row-major 64 x 64) by three wavefronts (g < 3). The persistent
+// schedule's backward substitution masks the upper triangle of X (bsDiag), so it stores the lower
+// one only; the tile-parallel update kernels stage X whole for the MFMAs (zeros stored).
+// kCaller: 1 k_chol_roots, 2 k_chol_update, 10 + MODE the persistent k_cholesky<MODE> (which keeps
+// y in LDS and stores X lower-triangular)
+__host__ __device__ constexpr bool persistentCaller(int kCaller) { return kCaller >= 10; }
+template <int kCaller>
+__device__ __forceinline__ void xStoreRows16(const double* sX, double* Li, int q, int g, int lane) {
+  double2 v[3];
+#pragma unroll
+  for (int it = 0; it < 3; ++it) {  // loads first, then the stores
+    const int e = min(64 * g + lane + 192 * it, 511), r = 16 * q + (e >> 5), c = 2 * (e & 31);
+    v[it] = double2{(c <= r) ? sX[r * kLd + c] : 0.0, (c + 1 <= r) ? sX[r * kLd + c + 1] : 0.0};
+  }
+#pragma unroll
+  for (int it = 0; it < 3; ++it) {
+    const int e = 64 * g + lane + 192 * it, r = 16 * q + (e >> 5), c = 2 * (e & 31);
+    if (e < 512 && (!persistentCaller(kCaller) || c <= r)) *reinterpret_cast<double2*>(Li + r * kTile + c) = v[it];
+  }
+}
+
+// Diagonal tile: L_kk (in sA only: every later use of the diagonal goes through X, so L_kk is
+// never stored), X = L_kk^-1 (into sX and the Linv store) and y_k = X rhs_k
+// (sy holds rhs_k on entry, y_k on exit; the tile-parallel callers also write it to workk, the
+// forward-substitution vector in global memory; the persistent kernel keeps y in LDS and passes
+// no workk). Right-looking LLT in 8-column
+// sub-panels (the chain on wavefront 0, the rank-8 trailing updates on the matrix cores of
+// wavefronts 1-3), and X by 16-row block rows as soon as the sweep has passed them, on wavefronts
+// 1-3 while wavefront 0 factors the next sub-panels: the 8x8 diagonal inverses come out of the
+// sub-panels, X21 = -X22 L21 X11 completes the 16x16 diagonal block (xDiag16) and
+// X_qj = -X_qq (sum_{m=j}^{q-1} L_qm X_mj) the rest of the block row on the matrix cores
+// (xOffDiag16); y_q and the Linv store of the block row follow. Only block row 3 remains after
+// the sweep (one isolated tile, scripts/ubench_ptile.hip: 24.0 -> 22.6 us).
+// Returns false (uniformly) at a non-positive pivot.
+// (one non-inlined instantiation per calling kernel: a shared callee gets a generic register
+// budget that halves the persistent kernel's occupancy)
+// Team callers (kCaller >= 20: the pipelined persistent kernel, whose workgroup holds two teams of
+// four wavefronts) run it on one team: t is the team's thread index, and the three workgroup
+// barriers become barriers of the team's four wavefronts on the counter sFl[4], whose arrival
+// count before the call is 4 * tgen0 (the caller adds kPotrfBarriers to its count afterwards).
+__host__ __device__ constexpr bool teamCaller(int kCaller) { return kCaller >= 20; }
+constexpr int kPotrfBarriers = 3;
+template <int kCaller>
+__device__ __forceinline__ void potrfSync(int* sFl, int& tgen, int lane) {
+  if (teamCaller(kCaller)) waveBarrier<true>(&sFl[4], tgen, 4, lane);
+  else ldsBarrier();
+}
+template <int kCaller>
+__device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX, double* sy,
+                                      double* sRl, int* sFl, int t, bool haveTile, int tgen0 = 0) {
+  const int wave = t >> 6, lane = t & 63;
+  int tgen = tgen0;
+  CLK_INIT
+  if (!haveTile) loadTile(Sg, ld, 0, 0, sA, t);  // (else the caller left S_kk in sA)
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = t + 256 * u;
+    sX[(e >> 6) * kLd + (e & 63)] = 0.0;
+  }
+  if (t < 4) sFl[t] = 0;  // sub-panels factored, trailing updates done, fail, barrier counter
+  potrfSync<kCaller>(sFl, tgen, lane);
+  CLK(4)
+  // Sweep with look-ahead: wavefront 0 runs the chain of the 8 sub-panel factorisations and
+  // applies each sub-panel's rank-8 update to the next sub-panel's 8 columns itself (VALU, its own
+  // row); wavefronts 1-3 apply it to the columns beyond (matrix cores) and form the 8x8 inverse
+  // blocks, one sub-panel behind, handing over through LDS flags.
+  if (wave == 0) {
+    const int i = lane;
+    double xp[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) xp[k] = 0.0;
+#pragma unroll 1
+    for (int s = 0; s < 8; ++s) {
+      const int c0 = 8 * s;
+      CLK(25)
+      if (s >= 2 && !waitFlag<true>(&sFl[1], s - 1, &sFl[2])) break;  // trailing update of sub-panel s-2
+      CLK(21)
+      double r[8], x[8], rl[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) r[k] = sA[i * kLd + c0 + k];
+      if (s >= 1) {  // look-ahead update by sub-panel s-1: r -= L_i,s-1 L_(c0..c0+7),s-1^T
+        // (c outer: the 8 independent chains r[m] interleave, so no FMA waits on the previous one's
+        // result; every r[m] still sums over c in order, the same bits)
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+#pragma unroll
+          for (int m = 0; m < 8; ++m) r[m] -= xp[c] * sA[(c0 + m) * kLd + c0 - 8 + c];
+        // Scheduling fence: the look-ahead result is complete before its stores are issued (and,
+        // below, x before the row stores). Without these the compiler interleaves the stores and
+        // the next loads with the FP64 chain: 22.6 against 15.9 us per tile
+        // (scripts/ubench_ptile.hip, "product" vs "consume-only")
+        asm volatile("" ::"v"(r[0]), "v"(r[1]), "v"(r[2]), "v"(r[3]), "v"(r[4]), "v"(r[5]), "v"(r[6]), "v"(r[7]));
+        if (i >= c0) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) sA[i * kLd + c0 + k] = r[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+      CLK(22)
+      if (!chol8Row(sA, c0, r, x, rl)) {
+        if (lane == 0) ldsReleaseL(&sFl[2], 1);
+        break;
+      }
+      asm volatile("" ::"v"(x[7]));
+      CLK(23)
+      storeRow8(sA, c0, x, i);
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sRl[c0 + k] = rl[k];
+        ldsReleaseL(&sFl[0], s + 1);
+      }
+      CLK(24)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) xp[k] = x[k];
+    }
+  } else {
+    const int g = wave - 1;
+    int gen = 0;
+#pragma unroll 1
+    for (int s = 0; s < 8; ++s) {
+      if (!waitFlag<true>(&sFl[0], s + 1, &sFl[2])) break;
+      if (g == 0) inv8(sA, sRl, sX + 8 * s * kLd + 8 * s, 8 * s, lane);
+      if (s < 6) trailingFrom(sA, 8 * s, 8 * s + 16, g, 3, lane);
+      waveBarrier<true>(&sFl[3], gen, 3, lane);
+      if (g == 0 && lane == 0) ldsReleaseL(&sFl[1], s + 1);
+      if (s & 1) {
+        // the 16 columns of block q are factored: block row q of X, y_q and the X store of those
+        // rows, in the shadow of wavefront 0's next sub-panels (only block row 3 follows the sweep)
+        const int q = s >> 1;
+        if (g == 0) xDiag16(sA, sX, q, lane);
+        waveBarrier<true>(&sFl[3], gen, 3, lane);
+        if (g < q) xOffDiag16(sA, sX, q, g, lane);
+        waveBarrier<true>(&sFl[3], gen, 3, lane);
+        if (g == 0) yBlock16(sX, sy, q, lane);
+        xStoreRows16<kCaller>(sX, Li, q, g, lane);
+      }
+    }
+  }
+  potrfSync<kCaller>(sFl, tgen, lane);
+  CLK(5)
+  if (sFl[2]) return false;
+  // LDS-only barriers from here: the X / y stores stay in flight (no reader in this
+  // workgroup before a later full barrier or the end of the launch)
+  if (t < kTile) {
+    const double y = sy[kTile + t];
+    sy[t] = y;
+    if (!persistentCaller(kCaller)) workk[t] = y;
+  }
+  potrfSync<kCaller>(sFl, tgen, lane);
+  CLK(10)
+  return true;
+}
+
+// acc (C layout) -> LDS tile [64][kLd]
+__device__ __forceinline__ void accToLds(double* s, const dbl4 acc[2][2], int t) {
+  const int wave = t >> 6, lane = t & 63;
+  const int r0 = 32 * (wave >> 1), c0 = 32 * (wave & 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) s[(r0 + 16 * a + (lane >> 4) + 4 * reg) * kLd + c0 + 16 * b + (lane & 15)] = acc[a][b][reg];
+}
+// c - acc (C layout) -> LDS tile [64][kLd]
+__device__ __forceinline__ void accSubToLds(double* s, const dbl4 c[2][2], const dbl4 acc[2][2], int t) {
+  const int wave = t >> 6, lane = t & 63;
+  const int r0 = 32 * (wave >> 1), c0 = 32 * (wave & 1);
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg)
+        s[(r0 + 16 * a + (lane >> 4) + 4 * reg) * kLd + c0 + 16 * b + (lane & 15)] = c[a][b][reg] - acc[a][b][reg];
+}
+
+// z = X^T y_k (X = L_kk^-1 lower in sX, y_k in sy), so that the forward substitution update of
+// every panel is rhs_i -= L_ik y_k = A_ik z. Partials of four row quarters via sP (4 x 64).
+// (Sync: the barrier that orders LDS among the threads running the routine — the workgroup's
+// s_barrier (WgSync), or a team barrier of the pipelined persistent kernel)
+struct WgSync {
+  __device__ __forceinline__ void operator()() const { ldsBarrier(); }
+};
+template <class Sync = WgSync>
+__device__ __forceinline__ void panelRhsVector(const double* sX, const double* sy, double* sz, double* sP, int t,
+                                               Sync sync = Sync()) {
+  const int c = t & 63, q = t >> 6;
+  double a = 0.0;
+#pragma unroll
+  for (int r = 16 * q; r < 16 * q + 16; ++r) a += (r >= c) ? sX[r * kLd + c] * sy[r] : 0.0;
+  sP[q * kTile + c] = a;
+  sync();
+  if (t < kTile) sz[t] = (sP[t] + sP[kTile + t]) + (sP[2 * kTile + t] + sP[3 * kTile + t]);
+  sync();
+}
+
+// (A_ik z)_row of the panel's forward-substitution update: row t >> 2, quarter t & 3 of the
+// columns, summed over the quarters by two shuffles (the result on every lane of the quad).
+__device__ __forceinline__ double panelRhsRow(const double* sA, const double* sz, int t) {
+  const int row = t >> 2, q = t & 3;
+  double a = 0.0;
+#pragma unroll
+  for (int c = 16 * q; c < 16 * q + 16; ++c) a += sA[row * kLd + c] * sz[c];
+  a += __shfl_xor(a, 1, 64);
+  a += __shfl_xor(a, 2, 64);
+  return a;
+}
+
+// L_ik = A_ik X^T (X = L_kk^-1 in sX) stored over A_ik, and rhs_i -= A_ik z (z = X^T y_k in sz),
+// the row products formed from the A_ik tile in LDS while the MFMAs run.
+template <class Sync = WgSync>
+__device__ __forceinline__ void panelTile(const double* Aik, double* Lik, int64_t ld, double* worki, double* sA, const double* sX, const double* sz,
+                          int t, double* defer = nullptr, Sync sync = Sync()) {
+  loadTile(Aik, ld, 0, 0, sA, t);
+  sync();  // LDS-only: the previous panel's L / rhs stores stay in flight
+  dbl4 acc[2][2];
+  mfmaTileNT(sA, sX, acc, t);
+  {
+    const int row = t >> 2, q = t & 3;
+    const double a = panelRhsRow(sA, sz, t);
+    if (q == 0) {
+      if (defer) defer[row] = a;  // (split schedule: subtracted by the separator's launch, in step order)
+      else worki[row] -= a;       // rhs_i in LDS
+    }
+  }
+  sync();  // sA is free for the next panel
+  storeTile<false>(Lik, ld, 0, 0, acc, t);
+}
+
+
+// Backward substitution x = L^-T y, x := y_F, with the stored diagonal inverses: per block row I
+// (from the last), x_I = X_II^T (y_I - sum_i L_iI^T x_i) over the non-zero tiles below. The work
+// of a step is laid out over 1024 virtual threads vt: column pair (2 cp, 2 cp + 1), cp = vt & 31,
+// rows rg + 32u (rg = vt >> 5, u < 2) of every operand tile (2 16-byte loads per tile), partials
+// summed over the 32 row groups in a fixed tree. The tile-parallel kernel runs them as real
+// threads (few registers per thread, so the next step's loads fit in flight); the persistent
+// kernel runs 4 per thread in the same order, so both give the same bits. UPPER: L_iI is stored
+// in the upper slot (I,i) (tile-parallel schedule), else at (i,I).
+constexpr int kBsThreads = 1024;
+constexpr int kBsPre = 3;  // operand tiles per step from the list (further ones are loaded in the step)
+struct BsOps {
+  double2 v[kBsPre][2];
+  double2 li[2];
+};
+template <bool UPPER>
+__device__ __forceinline__ const double* bsTile(const double* S, int64_t ld, int I, int i) {
+  return UPPER ? S + (int64_t)I * kTile * ld + i * kTile : S + (int64_t)i * kTile * ld + I * kTile;
+}
+// lst: count of non-zero tiles below I (capped at kBsPre), then their block rows ascending.
+// Loads are unconditional (an absent tile reads the diagonal one and is masked): loads under a
+// branch make the wait-count insertion fall back to vmcnt(0).
+template <bool UPPER>
+__device__ __forceinline__ void bsLoad(const double* S, int64_t ld, const double* Linv, const int* lst, int I, int vt,
+                                       BsOps& o) {
+  const int c2 = 2 * (vt & 31), rg = vt >> 5;
+#pragma unroll
+  for (int m = 0; m < kBsPre; ++m) {
+    const double* Lt = bsTile<UPPER>(S, ld, I, m < lst[0] ? lst[1 + m] : I) + c2;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) o.v[m][u] = *gmem(reinterpret_cast<const double2*>(Lt + (int64_t)(rg + 32 * u) * ld));
+  }
+  const double* Li = Linv + (int64_t)I * kTile * kTile + c2;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) o.li[u] = *gmem(reinterpret_cast<const double2*>(Li + (rg + 32 * u) * kTile));
+}
+__device__ __forceinline__ double sum32(const double* p) {  // p[64 k], k < 32, fixed tree
+  double a[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] = (p[kTile * k] + p[kTile * (k + 8)]) + (p[kTile * (k + 16)] + p[kTile * (k + 24)]);
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+}
+// Non-zero tiles below I beyond the listed ones (rare; out of line, so the wait counts of the
+// pipelined loads around the call site stay exact).
+template <bool UPPER>
+__device__ __noinline__ double2 bsExtra(const double* S, int64_t ld, int T, const uint8_t* nz, int last, int I,
+                                        const double* sx, int vt, double ax, double ay) {
+  const int c2 = 2 * (vt & 31), rg = vt >> 5;
+  for (int i = last + 1; i < T; ++i) {
+    if (!nz[i * T + I]) continue;
+    const double* Lt = bsTile<UPPER>(S, ld, I, i) + c2;
+    const double* xi = sx + i * kTile + rg;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const double2 v = *gmem(reinterpret_cast<const double2*>(Lt + (int64_t)(rg + 32 * u) * ld));
+      ax += v.x * xi[32 * u];
+      ay += v.y * xi[32 * u];
+    }
+  }
+  return double2{ax, ay};
+}
+// Partial (L^T x) of virtual thread vt for step I -> sA[rg][c2..c2+1] (sx: y of unsolved rows, x of solved).
+template <bool UPPER>
+__device__ __forceinline__ void bsPartial(const double* S, int64_t ld, int T, const uint8_t* nz, const int* lst, int I,
+                                          const BsOps& c, const double* sx, double* sA, int vt) {
+  const int c2 = 2 * (vt & 31), rg = vt >> 5;
+  double ax = 0.0, ay = 0.0;
+#pragma unroll
+  for (int m = 0; m < kBsPre; ++m) {
+    const bool on = m < lst[0];
+    const double* xi = sx + (on ? lst[1 + m] : I) * kTile + rg;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {  // a masked tile adds exact zeros
+      ax += (on ? c.v[m][u].x : 0.0) * xi[32 * u];
+      ay += (on ? c.v[m][u].y : 0.0) * xi[32 * u];
+    }
+  }
+  if (lst[0] == kBsPre) {
+    const double2 e = bsExtra<UPPER>(S, ld, T, nz, lst[kBsPre], I, sx, vt, ax, ay);
+    ax = e.x;
+    ay = e.y;
+  }
+  sA[rg * kTile + c2] = ax;
+  sA[rg * kTile + c2 + 1] = ay;
+}
+// Partial (X_II^T y_I) of virtual thread vt -> sA (sy: y_I corrected).
+__device__ __forceinline__ void bsDiag(const BsOps& c, const double* sy, double* sA, int vt) {
+  const int c2 = 2 * (vt & 31), rg = vt >> 5;
+  double bx = 0.0, by = 0.0;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int r = rg + 32 * u;
+    bx += (r >= c2) ? c.li[u].x * sy[r] : 0.0;
+    by += (r >= c2 + 1) ? c.li[u].y * sy[r] : 0.0;
+  }
+  sA[rg * kTile + c2] = bx;
+  sA[rg * kTile + c2 + 1] = by;
+}
+// The non-zero tiles below block row I (bitmap nz), in the lst format of bsLoad.
+__device__ __forceinline__ void bsList(const uint8_t* nz, int T, int I, int* lst) {
+  int n = 0;
+  for (int i = I + 1; i < T && n < kBsPre; ++i)
+    if (nz[i * T + I]) lst[1 + n++] = i;
+  lst[0] = n;
+}
+// The GN step's f-vectors from the solution x of row e (DoglegStrategy::ComputeGaussNewtonStep /
+// ComputeGradient; formerly k_gn_finalize, one launch fewer per iteration): gauss_newton_step_ =
+// -diagonal_ .* x, gradient_ = s .* g / diagonal_, v = gradient_ / diagonal_. Gap rows of a
+// nested-dissection order (no f-block) are skipped.
+__device__ __forceinline__ void gnFinalizeRow(const DevProblem& P, size_t i, double x) {
+  const double dg = gmem(P.diagF)[i], sc = gmem(P.sF)[i], g = gmem(P.gF)[i];
+  P.yF[i] = x;
+  P.gnF[i] = -dg * x;
+  const double gr = sc * g / dg;
+  P.dgF[i] = gr;
+  P.vF[i] = gr / dg;
+}
+__device__ __forceinline__ bool gapRow(const DevProblem& P, int w, int e) {
+  const int g0 = P.win_sgap[2 * w];
+  return e >= g0 && e < g0 + P.win_sgap[2 * w + 1];
+}
+
+// Persistent schedules (NT = 256 threads, 4 virtual threads each, or the pipelined kernel's 512
+// threads, 2 each): y already in sx (LDS), then the steps with operands loaded in-step. sA: >= 32 x
+// 64 doubles.
+template <int NT = 256>
+__device__ __forceinline__ void backSubstitute(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* Linv,
+                               const uint8_t* nz, double* sx, double* sA, double* sy, int t) {
+  // sx already holds y (the persistent kernel keeps the whole forward substitution in LDS)
+  __syncthreads();
+  constexpr int kV = kBsThreads / NT;
+  for (int I = T - 1; I >= 0; --I) {
+    int lst[1 + kBsPre];
+    bsList(nz, T, I, lst);
+    BsOps c[kV];
+#pragma unroll
+    for (int k = 0; k < kV; ++k) bsLoad<false>(S, ld, Linv, lst, I, t + NT * k, c[k]);
+#pragma unroll
+    for (int k = 0; k < kV; ++k) bsPartial<false>(S, ld, T, nz, lst, I, c[k], sx, sA, t + NT * k);
+    __syncthreads();
+    if (t < kTile) sy[t] = sx[I * kTile + t] - sum32(sA + t);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kV; ++k) bsDiag(c[k], sy, sA, t + NT * k);
+    __syncthreads();
+    if (t < kTile) sx[I * kTile + t] = sum32(sA + t);
+    __syncthreads();
+  }
+  const int fdim = P.win_fdim[w];
+  for (int e = t; e < fdim; e += blockDim.x)
+    if (!gapRow(P, w, e)) gnFinalizeRow(P, (size_t)P.win_foff[w] + e, sx[e]);
+}
+
+}  // namespace okg

@@ -8,7 +8,7 @@
 // ---- k_cholesky / k_chol_bsub (-DOKG_CHOL_CLOCK): workgroup 0 accumulates s_memrealtime ticks
 // (100 MHz) per phase and prints them at its end.
 #ifdef OKG_CHOL_CLOCK
-__device__ unsigned long long g_cholClk[32];
+static __device__ unsigned long long g_cholClk[32];
 #define CLK_INIT unsigned long long clkLast = __builtin_amdgcn_s_memrealtime();
 #define CLK(i)                                                                  \
   if (blockIdx.x == 0 && threadIdx.x == 0) {                                    \
@@ -44,8 +44,8 @@ __device__ unsigned long long g_cholClk[32];
 // contended and inflated the phases they fell into); the last workgroup prints the totals. Uses the
 // kernel's APPEND template parameter.
 #ifdef OKG_IMU_CLOCK
-__device__ unsigned long long g_imuClk[12];
-__device__ unsigned int g_imuDone;
+static __device__ unsigned long long g_imuClk[12];
+static __device__ unsigned int g_imuDone;
 #define ICLK_INIT                                                                       \
   unsigned long long iclk = __builtin_amdgcn_s_memrealtime(), iacc[12];                 \
   for (int i_ = 0; i_ < 12; ++i_) iacc[i_] = 0;
@@ -76,8 +76,8 @@ __device__ unsigned int g_imuDone;
 // ---- k_lm_visit<1> (-DOKG_LMV_CLOCK): thread 0 of every workgroup adds its s_memrealtime ticks per
 // phase with vector atomics; the last workgroup prints the totals. Uses the kernel's `mode`.
 #ifdef OKG_LMV_CLOCK
-__device__ unsigned long long g_lmvClk[8];
-__device__ unsigned int g_lmvDone;
+static __device__ unsigned long long g_lmvClk[8];
+static __device__ unsigned int g_lmvDone;
 #define LCLK_INIT unsigned long long lclk = __builtin_amdgcn_s_memrealtime();
 #define LCLK(i)                                                                         \
   if (mode == 1 && threadIdx.x == 0) {                                                  \

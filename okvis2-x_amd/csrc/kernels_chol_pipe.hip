@@ -1,0 +1,234 @@
+// kernels_chol_pipe.hip — the pipelined persistent schedule of the reduced camera matrix's LLT
+// (Cholesky schedule 4, runtime.cpp setOptions): one 512-thread workgroup per window, split into two
+// teams of four wavefronts that work on consecutive steps of the right-looking factorisation.
+//
+//   team F (wavefronts 0-3): the diagonal tiles, potrfTile (L_kk, X_k = L_kk^-1, y_k = X_k rhs_k),
+//            one after the other;
+//   team B (wavefronts 4-7): step k's panels L_ik = A_ik X_k^T with rhs_i -= A_ik X_k^T y_k and band
+//            updates A_ij -= L_ik L_jk^T, on the FP64 matrix cores.
+//
+// The persistent kernel (k_cholesky<0>) runs the three phases of a step one after the other with
+// the whole workgroup, so while wavefront 0 walks the diagonal tile's latency chain the matrix cores
+// wait. Here team B takes X_k (into registers, in MFMA fragment order) as soon as team F has it and
+// first runs the two products on the critical path — the panel L_(k+1)k and its update of the next
+// diagonal tile, which it writes straight into team F's LDS tile — then hands tile k+1 to team F
+// and runs the step's other panels and updates while team F factors it. The step time becomes
+// factor + one panel + one update instead of factor + every panel and update of the step.
+//
+// The tile operations are those of the other schedules (chol_tiles.hpp: the same routines, the same
+// operands, each tile's updates in step order), so the factorisation gives their bits. The teams
+// synchronise through LDS flags (workgroup-scope release / acquire, which also order the global W
+// tiles one team writes and the other reads) and barriers of their own four wavefronts; the
+// backward substitution runs on all 512 threads once both teams are done.
+#include "chol_tiles.hpp"
+#include "launch.hpp"
+
+namespace okg {
+
+// Barrier of one team's four wavefronts on an LDS arrival counter (LOCAL: orders LDS only; else
+// also the global stores of the team, e.g. W tiles another wavefront of the team reads next).
+template <bool LOCAL>
+struct TeamSync {
+  int* ctr;
+  int* gen;
+  int lane;
+  __device__ __forceinline__ void operator()() const { waveBarrier<LOCAL>(ctr, *gen, 4, lane); }
+};
+
+// X^T's B-operand fragments of mfmaTileNT(sA, sX) for this wavefront (columns c0 + 16 b + lr,
+// k = 4 q + lk), so that the panels of a step no longer need X in LDS.
+__device__ __forceinline__ void loadXFrag(const double* sX, double (&xf)[16][2], int t) {
+  const int wave = t >> 6, lane = t & 63;
+  const int c0 = 32 * (wave & 1), lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int q = 0; q < 16; ++q)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) xf[q][b] = sX[(c0 + 16 * b + lr) * kLd + 4 * q + lk];
+}
+// acc = sA X^T with X^T's fragments in registers: the MFMA sequence of mfmaTileNT(sA, sX), so the
+// same bits.
+__device__ __forceinline__ void mfmaTileNTX(const double* sA, const double (&xf)[16][2], dbl4 acc[2][2], int t) {
+  const int wave = t >> 6, lane = t & 63;
+  const int r0 = 32 * (wave >> 1);
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    double av[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) av[a] = sA[(r0 + 16 * a + lr) * kLd + 4 * q + lk];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], xf[q][b], acc[a][b], 0, 0, 0);
+  }
+}
+
+// Panel of team B: L_ik = A_ik X^T (A_ik staged in sBuf), rhs_i -= A_ik z (panelTile's
+// operations), L_ik stored to W and left in sBuf for the step's band updates.
+template <class Sync>
+__device__ __forceinline__ void pipePanel(const double* Aik, double* Lik, int64_t ld, double* worki, double* sBuf,
+                                          const double (&xf)[16][2], const double* sz, int t, Sync sync) {
+  loadTile(Aik, ld, 0, 0, sBuf, t);
+  sync();
+  dbl4 acc[2][2];
+  mfmaTileNTX(sBuf, xf, acc, t);
+  const double a = panelRhsRow(sBuf, sz, t);
+  if ((t & 3) == 0) worki[t >> 2] -= a;  // rhs_i in LDS
+  sync();  // every wavefront has read A_ik
+  accToLds(sBuf, acc, t);
+  storeTile<false>(Lik, ld, 0, 0, acc, t);
+  sync();  // L_ik in sBuf for every wavefront of the team
+}
+
+// LDS of the pipelined kernel besides the window's rhs / y (dynamic, ld doubles)
+struct PipeLds {
+  double sA[kTile * kLd];     // F: the diagonal tile being factored (team B writes the next one here)
+  double sX[kTile * kLd];     // F: X_k
+  double sB[2][kTile * kLd];  // B: A_ik staging / the step's L tiles
+  double sy[2 * kTile];       // F: rhs_k -> y_k | scratch (backward substitution: y_I)
+  double sz[2 * kTile];       // B: y_k | z_k = X_k^T y_k
+  double sRl[kTile];          // F: 1 / L_cc
+  int sFl[8];                 // potrfTile's flags [0..3], team F's barrier [4], team B's barrier [5]
+  int pipe[4];                // [0] steps factored (F), [1] diagonal tiles handed over (B),
+                              // [2] the handed-over tile is in sA, [3] failed pivot
+};
+
+__global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __restrict__ Pp) {
+  const DevProblem& P = *Pp;
+  const int w = blockIdx.x;
+  if (!cholSelect(P, w)) return;  // (uniform over the workgroup)
+  const int64_t ld = P.win_fpad[w];
+  const int T = (int)(ld / kTile);
+  const TileSrc cur = tileSrc(P, w, ld);
+  double* W = P.W + P.win_soff[w];
+  double* Linv = P.Linv + P.win_linvoff[w];
+  const uint8_t* nz = P.tile_nz + P.win_tnzoff[w];
+  __shared__ PipeLds L;
+  extern __shared__ double sxDyn[];  // rhs / y of the whole window
+  const int t = threadIdx.x, team = t >> 8, tt = t & 255, lane = t & 63;
+  const int fdim = P.win_fdim[w];
+  for (int e = t; e < ld; e += 512) sxDyn[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
+  if (t < 8) L.sFl[t] = 0;
+  if (t < 4) L.pipe[t] = 0;
+  __syncthreads();
+  if (team == 0) {
+    // ---- team F: the diagonal tiles in order
+    int fgen = 0;
+    for (int k = 0; k < T; ++k) {
+      bool inLds = false;
+      if (k > 0) {  // tile k has all its updates (and rhs_k its panel terms); X_(k-1) was taken
+        if (!waitFlag<false>(&L.pipe[1], k, &L.pipe[3])) break;
+        inLds = L.pipe[2] != 0;
+      }
+      if (tt < kTile) L.sy[tt] = sxDyn[k * kTile + tt];
+      if (!potrfTile<20>(cur.at(k, k, k), ld, Linv + (int64_t)k * kTile * kTile, nullptr, L.sA, L.sX, L.sy, L.sRl,
+                         L.sFl, tt, inLds, fgen)) {
+        if (tt == 0) ldsRelease(&L.pipe[3], 1);
+        break;
+      }
+      fgen += kPotrfBarriers;
+      if (tt < kTile) sxDyn[k * kTile + tt] = L.sy[tt];  // y_k
+      if (tt == 0) ldsRelease(&L.pipe[0], k + 1);         // X_k in sX, y_k in sxDyn
+    }
+  } else {
+    // ---- team B: the panels and band updates of step k once X_k is there
+    const int tt0 = tt;
+    int bgen = 0;
+    const TeamSync<false> bsync{&L.sFl[5], &bgen, lane};
+    const TeamSync<true> bsyncL{&L.sFl[5], &bgen, lane};
+    double xf[16][2];
+    for (int k = 0; k + 1 < T; ++k) {
+      if (!waitFlag<false>(&L.pipe[0], k + 1, &L.pipe[3])) break;
+      // the thread index, opaque per step: the step's LDS / global addresses are formed in the step
+      // instead of being hoisted out of the loop (and spilled: the kernel is at 256 VGPRs)
+      int tt = tt0;
+      asm volatile("" : "+v"(tt));
+      // z_k = X_k^T y_k and X_k into registers from team F's sX (untouched until tile k+1 is
+      // handed over below)
+      if (tt < kTile) L.sz[tt] = sxDyn[k * kTile + tt];
+      bsyncL();
+      panelRhsVector(L.sX, L.sz, L.sz + kTile, L.sB[0], tt, bsyncL);
+      loadXFrag(L.sX, xf, tt);
+      int held[2] = {-1, -1};  // block row i of the L_ik in sB[0] / sB[1]
+      const bool crit = nz[(k + 1) * T + k] != 0;
+      if (crit) {
+        // the critical path: panel (k+1, k), then its update of tile (k+1, k+1) into team F's sA
+        pipePanel(cur.at(k + 1, k, k), W + (int64_t)(k + 1) * kTile * ld + k * kTile, ld, sxDyn + (k + 1) * kTile,
+                  L.sB[0], xf, L.sz + kTile, tt, bsyncL);
+        held[0] = k + 1;
+        dbl4 c[2][2], acc[2][2];
+        loadC(cur.at(k + 1, k + 1, k), ld, c, tt);
+        mfmaTileNT(L.sB[0], L.sB[0], acc, tt);
+        accSubToLds(L.sA, c, acc, tt);
+        bsyncL();
+      }
+      if (tt == 0) {
+        L.pipe[2] = crit ? 1 : 0;
+        ldsRelease(&L.pipe[1], k + 1);
+      }
+      // the step's other panels (the last ones stay in LDS for the updates)
+      int hb = crit ? 1 : 0;
+      for (int i = k + 2; i < T; ++i) {
+        if (!nz[i * T + k]) continue;
+        pipePanel(cur.at(i, k, k), W + (int64_t)i * kTile * ld + k * kTile, ld, sxDyn + i * kTile, L.sB[hb], xf,
+                  L.sz + kTile, tt, bsyncL);
+        held[hb] = i;
+        if (!crit) hb ^= 1;
+      }
+      bsync();  // the L tiles in W for reloads by other wavefronts of the team
+      // band updates A_ij -= L_ik L_jk^T of step k but (k+1, k+1), bottom-up
+      for (int i = T - 1; i > k; --i) {
+        if (!nz[i * T + k]) continue;
+        for (int j = k + 1; j <= i; ++j) {
+          if (!nz[j * T + k] || i == k + 1) continue;  // (row k+1: only (k+1, k+1), done above)
+          int bi = held[0] == i ? 0 : (held[1] == i ? 1 : -1);
+          int bj = j == i ? bi : (held[0] == j ? 0 : (held[1] == j ? 1 : -1));
+          bool loaded = false;
+          if (bi < 0) {
+            bi = bj >= 0 ? bj ^ 1 : 0;
+            loadTile(W + (int64_t)i * kTile * ld + k * kTile, ld, 0, 0, L.sB[bi], tt);
+            held[bi] = i;
+            if (j == i) bj = bi;
+            loaded = true;
+          }
+          if (bj < 0) {
+            bj = bi ^ 1;
+            loadTile(W + (int64_t)j * kTile * ld + k * kTile, ld, 0, 0, L.sB[bj], tt);
+            held[bj] = j;
+            loaded = true;
+          }
+          if (loaded) bsyncL();
+          dbl4 c[2][2], acc[2][2];
+          loadC(cur.at(i, j, k), ld, c, tt);
+          mfmaTileNT(L.sB[bi], L.sB[bj], acc, tt);
+          storeTileSub(W + (int64_t)i * kTile * ld + j * kTile, ld, c, acc, tt);
+          bsyncL();  // the operands may be replaced next
+        }
+      }
+      bsync();  // the updated tiles in W for the next step's panels
+    }
+  }
+  __syncthreads();
+  if (L.pipe[3]) {
+    if (t == 0) P.st[w].gn_failed = 1;
+    return;
+  }
+  backSubstitute<512>(P, w, W, ld, T, Linv, nz, sxDyn, L.sB[0], L.sy, t);
+}
+
+bool cholesky_pipe_fits(int max_fpad, size_t lds_per_block) {
+  hipFuncAttributes attr;
+  if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky_pipe)) != hipSuccess) return false;
+  return attr.sharedSizeBytes + sizeof(double) * (size_t)max_fpad <= lds_per_block;
+}
+
+void launch_cholesky_pipe(const DevProblem& P, hipStream_t s) {
+  if (P.n_win == 0) return;
+  hipLaunchKernelGGL(k_cholesky_pipe, dim3(P.n_win), dim3(512), sizeof(double) * P.max_fpad, s, P.self);
+}
+
+}  // namespace okg

@@ -422,7 +422,7 @@ def test_cholesky_schedules_agree(og, oracle, gpu_ctx):
     operations in the same order: bitwise-equal solves, both matching the oracle."""
     ws = [og.SynthWindow(10, 500, 4000, seed=s) for s in (31, 32)]
     res = []
-    for sched in (1, 2):
+    for sched in (1, 2, 4):
         for w in ws:
             w.reset()
         opts = og.default_options(max_num_iterations=5, function_tolerance=0.0, gradient_tolerance=0.0,
@@ -446,7 +446,7 @@ def test_cholesky_schedules_agree_nested_dissection(og, oracle, gpu_ctx):
     (natural order) agrees to the usual tolerance."""
     ws = [og.SynthWindow(50, 2000, 16000, seed=s) for s in (33, 34)]
     res = []
-    for sched in (1, 2, 3):
+    for sched in (1, 2, 3, 4):
         for w in ws:
             w.reset()
         opts = og.default_options(max_num_iterations=4, function_tolerance=0.0, gradient_tolerance=0.0,
