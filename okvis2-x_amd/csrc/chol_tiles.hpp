@@ -418,8 +418,8 @@ __device__ __forceinline__ void potrfSync(int* sFl, int& tgen, int lane) {
   else ldsBarrier();
 }
 template <int kCaller>
-__device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX, double* sy,
-                                      double* sRl, int* sFl, int t, bool haveTile, int tgen0 = 0) {
+__device__ __forceinline__ bool potrfTileBody(const double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX,
+                                              double* sy, double* sRl, int* sFl, int t, bool haveTile, int tgen0) {
   const int wave = t >> 6, lane = t & 63;
   int tgen = tgen0;
   CLK_INIT
@@ -521,6 +521,14 @@ __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li,
   potrfSync<kCaller>(sFl, tgen, lane);
   CLK(10)
   return true;
+}
+// The non-inlined form (one instantiation per calling kernel); the pipelined kernel's team F
+// inlines the body instead (a call there saved and restored ~33 callee-saved VGPRs through scratch
+// around every tile: 22.6 against 16.1 us per tile in scripts/ubench_team.hip).
+template <int kCaller>
+__device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX, double* sy,
+                                      double* sRl, int* sFl, int t, bool haveTile, int tgen0 = 0) {
+  return potrfTileBody<kCaller>(Sg, ld, Li, workk, sA, sX, sy, sRl, sFl, t, haveTile, tgen0);
 }
 
 // acc (C layout) -> LDS tile [64][kLd]
@@ -725,11 +733,16 @@ __device__ __forceinline__ bool gapRow(const DevProblem& P, int w, int e) {
 // Persistent schedules (NT = 256 threads, 4 virtual threads each, or the pipelined kernel's 512
 // threads, 2 each): y already in sx (LDS), then the steps with operands loaded in-step. sA: >= 32 x
 // 64 doubles.
-template <int NT = 256>
+// (Sync: the workgroup's __syncthreads (FullSync), or a team barrier when each team of the
+// two-window pipelined kernel solves its own window)
+struct FullSync {
+  __device__ __forceinline__ void operator()() const { __syncthreads(); }
+};
+template <int NT = 256, class Sync = FullSync>
 __device__ __forceinline__ void backSubstitute(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* Linv,
-                               const uint8_t* nz, double* sx, double* sA, double* sy, int t) {
+                               const uint8_t* nz, double* sx, double* sA, double* sy, int t, Sync sync = Sync()) {
   // sx already holds y (the persistent kernel keeps the whole forward substitution in LDS)
-  __syncthreads();
+  sync();
   constexpr int kV = kBsThreads / NT;
   for (int I = T - 1; I >= 0; --I) {
     int lst[1 + kBsPre];
@@ -739,17 +752,17 @@ __device__ __forceinline__ void backSubstitute(const DevProblem& P, int w, const
     for (int k = 0; k < kV; ++k) bsLoad<false>(S, ld, Linv, lst, I, t + NT * k, c[k]);
 #pragma unroll
     for (int k = 0; k < kV; ++k) bsPartial<false>(S, ld, T, nz, lst, I, c[k], sx, sA, t + NT * k);
-    __syncthreads();
+    sync();
     if (t < kTile) sy[t] = sx[I * kTile + t] - sum32(sA + t);
-    __syncthreads();
+    sync();
 #pragma unroll
     for (int k = 0; k < kV; ++k) bsDiag(c[k], sy, sA, t + NT * k);
-    __syncthreads();
+    sync();
     if (t < kTile) sx[I * kTile + t] = sum32(sA + t);
-    __syncthreads();
+    sync();
   }
   const int fdim = P.win_fdim[w];
-  for (int e = t; e < fdim; e += blockDim.x)
+  for (int e = t; e < fdim; e += NT)
     if (!gapRow(P, w, e)) gnFinalizeRow(P, (size_t)P.win_foff[w] + e, sx[e]);
 }
 

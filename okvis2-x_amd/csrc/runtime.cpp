@@ -1387,6 +1387,7 @@ struct okvisgpu_ctx {
   size_t ldsPerBlock = 65536;
   bool persistentFits() const { return cholesky_persistent_fits(P.max_fpad, ldsPerBlock); }
   bool pipeFits() const { return cholesky_pipe_fits(P.max_fpad, ldsPerBlock); }
+  bool pipe2Fits() const { return cholesky_pipe2_fits(P.max_fpad, ldsPerBlock); }
   // S is cleared by the build's arena memset; its padded diagonal (rows >= fdim) is set once per
   // build before the first factorisation (k_zero_S setup mode). The factorisation works in W and
   // the assembly overwrites its blocks, so S needs no clearing per iteration.
@@ -1894,11 +1895,12 @@ struct okvisgpu_ctx {
     // persistent kernel split over the two parts of the order; from there one persistent
     // workgroup per window. (A wave-specialised kernel and a persistent variant with the panel
     // tiles in LDS were measured slower at every batch size and removed in round 4.)
-    int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 4 ? o.cholesky_schedule : 0;
+    int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 5 ? o.cholesky_schedule : 0;
     if (sched == 0) sched = 2 * P.n_win < cuCount ? 2 : (B.any_split && P.n_win < cuCount ? 3 : 1);
     if (sched == 3 && !B.any_split) sched = 1;  // (no window with a nested-dissection split)
     // the persistent kernel keeps the window's rhs / y in dynamic LDS next to its static tiles:
     // a reduced dimension beyond what fits falls back to the tile-parallel launches
+    if (sched == 5 && !pipe2Fits()) sched = 4;
     if (sched == 4 && !pipeFits()) sched = 1;
     if ((sched == 1 || sched == 3) && !persistentFits()) sched = 2;
     if (sched != P.chol_schedule && iterGraph) {

@@ -3,7 +3,7 @@
 // stamped copy of the sweep's chain wavefront (variant V, -DOKG_V=n) whose per-sub-panel phase
 // times (s_memtime, shader clock) show where the chain spends its cycles.
 // hipcc --offload-arch=gfx950 -O3 -I include scripts/ubench_ptile.hip -o scripts/ubench_ptile
-#include "../okvis2-x_amd/csrc/kernels_chol.hip"
+#include "../okvis2-x_amd/csrc/chol_tiles.hpp"
 
 #include <cmath>
 #include <cstdio>

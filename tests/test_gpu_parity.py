@@ -422,7 +422,7 @@ def test_cholesky_schedules_agree(og, oracle, gpu_ctx):
     operations in the same order: bitwise-equal solves, both matching the oracle."""
     ws = [og.SynthWindow(10, 500, 4000, seed=s) for s in (31, 32)]
     res = []
-    for sched in (1, 2, 4):
+    for sched in (1, 2, 4, 5):
         for w in ws:
             w.reset()
         opts = og.default_options(max_num_iterations=5, function_tolerance=0.0, gradient_tolerance=0.0,
@@ -446,7 +446,7 @@ def test_cholesky_schedules_agree_nested_dissection(og, oracle, gpu_ctx):
     (natural order) agrees to the usual tolerance."""
     ws = [og.SynthWindow(50, 2000, 16000, seed=s) for s in (33, 34)]
     res = []
-    for sched in (1, 2, 3, 4):
+    for sched in (1, 2, 3, 4, 5):
         for w in ws:
             w.reset()
         opts = og.default_options(max_num_iterations=4, function_tolerance=0.0, gradient_tolerance=0.0,
@@ -465,6 +465,28 @@ def test_cholesky_schedules_agree_nested_dissection(og, oracle, gpu_ctx):
                                                               gradient_tolerance=0.0, parameter_tolerance=0.0))
     _close(res[0][0][0], so)
     assert np.abs(res[0][1][0][:, :3] - ws[0].poses()[:, :3]).max() <= 1e-6
+
+
+def test_cholesky_schedules_ragged_batch(og, gpu_ctx):
+    """Windows of different sizes, an odd count (the two-window pipelined schedule pairs windows
+    0-1 and 2-3 and leaves window 4 alone) and a window that terminates early (done windows are
+    skipped inside a pair): the persistent, tile-parallel and both pipelined schedules give the same
+    bits."""
+    shapes = [(10, 500, 4000), (30, 1200, 9000), (12, 600, 5000), (50, 2000, 16000), (20, 900, 7000)]
+    ws = [og.SynthWindow(kf, lm, obs, seed=60 + k) for k, (kf, lm, obs) in enumerate(shapes)]
+    res = []
+    for sched in (1, 2, 4, 5):
+        for w in ws:
+            w.reset()
+        opts = og.default_options(max_num_iterations=5, cholesky_schedule=sched)
+        gpu_ctx.set_problems([w.problem for w in ws])
+        s = gpu_ctx.solve(opts, len(ws))
+        res.append((s, [w.poses().copy() for w in ws]))
+    for r in res[1:]:
+        for k in range(len(ws)):
+            assert r[0][k]["num_iterations"] == res[0][0][k]["num_iterations"]
+            assert r[0][k]["final_cost"] == res[0][0][k]["final_cost"], k
+            assert np.array_equal(r[1][k], res[0][1][k]), k
 
 
 def test_graph_file_solve_parity(og, oracle, gpu_ctx, tmp_path):
