@@ -389,10 +389,6 @@ void launch_cholesky(const DevProblem& P, hipStream_t s) {
     launch_cholesky_pipe(P, s);
     return;
   }
-  if (P.chol_schedule == 5) {
-    launch_cholesky_pipe2(P, s);
-    return;
-  }
   if (P.chol_schedule == 1) {
     hipLaunchKernelGGL(k_cholesky<0>, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
     return;

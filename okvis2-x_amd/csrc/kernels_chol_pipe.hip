@@ -234,221 +234,6 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
   backSubstitute<512>(P, w, W, ld, T, Linv, nz, sxDyn, L.sB[0], L.sy, t);
 }
 
-// ---- Two windows per workgroup (Cholesky schedule 5, batches of two or more windows per CU). The
-// persistent kernel keeps two 256-thread workgroups per CU; on the same SIMDs, one window's
-// panels and band updates stall the other's diagonal chain (FP64 MFMAs beside the FP64 VALU
-// chain, above). Here one 512-thread workgroup takes two windows and keeps the chain off team B's
-// SIMDs (team F = the even wavefronts, SIMDs 3 and 2; team B = the odd ones, SIMDs 0 and 1): team F
-// factors the diagonal tiles of both windows in the fixed order (w0, 0), (w1, 0), (w0, 1), ...,
-// team B runs the steps in the same order, so while team F factors one window's tile, team B
-// works on the other window's step. Hand-overs go through global memory: X_k from the stored
-// Linv tile (lower triangle; the upper entries masked to the zeros sX holds), the next diagonal
-// tile from W. Each window's operations are those of the other schedules: the same bits.
-struct Pipe2Lds {
-  double sA[kTile * kLd];     // F: the diagonal tile being factored
-  double sX[kTile * kLd];     // F: potrfTile's X workspace
-  double sB[2][kTile * kLd];  // B: A_ik staging / the step's L tiles
-  double sy[2 * kTile];       // F: rhs_k -> y_k
-  double sz[2 * kTile];       // B: y_k | z_k = X_k^T y_k
-  double sRl[kTile];          // F: 1 / L_cc
-  int sFl[8];                 // potrfTile's flags [0..3], team F's barrier [4], team B's barrier [5]
-  int fact[2], diag[2], fail[2];  // per window: steps factored, diagonal tiles handed over, failed pivot
-};
-
-// X_k^T's B-operand fragments from the stored lower triangle of X_k (Linv tile, row-major 64 x 64).
-__device__ __forceinline__ void loadXFragG(const double* Xg, double (&xf)[16][2], int t) {
-  const int wave = t >> 6, lane = t & 63;
-  const int c0 = 32 * (wave & 1), lr = lane & 15, lk = lane >> 4;
-  const auto X = gmem(Xg);
-#pragma unroll
-  for (int q = 0; q < 16; ++q)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int r = c0 + 16 * b + lr, c = 4 * q + lk;
-      const double v = X[r * kTile + c];
-      xf[q][b] = c <= r ? v : 0.0;
-    }
-}
-// z = X^T y from the stored lower triangle of X (panelRhsVector's operations, the same bits).
-template <class Sync>
-__device__ __forceinline__ void panelRhsVectorG(const double* Xg, const double* sy, double* sz, double* sP, int t, Sync sync) {
-  const int c = t & 63, q = t >> 6;
-  const auto X = gmem(Xg);
-  double a = 0.0;
-#pragma unroll
-  for (int r = 16 * q; r < 16 * q + 16; ++r) {
-    const double v = X[r * kTile + c];
-    a += (r >= c) ? v * sy[r] : 0.0;
-  }
-  sP[q * kTile + c] = a;
-  sync();
-  if (t < kTile) sz[t] = (sP[t] + sP[kTile + t]) + (sP[2 * kTile + t] + sP[3 * kTile + t]);
-  sync();
-}
-
-__global__ __launch_bounds__(512, 1) void k_cholesky_pipe2(const DevProblem* __restrict__ Pp) {
-  const DevProblem& P = *Pp;
-  int wv[2], Tv[2];
-  int64_t ldv[2];
-  bool any = false;
-#pragma unroll
-  for (int v = 0; v < 2; ++v) {
-    wv[v] = 2 * (int)blockIdx.x + v;
-    const bool sel = wv[v] < P.n_win && cholSelect(P, wv[v]);
-    ldv[v] = sel ? P.win_fpad[wv[v]] : 0;
-    Tv[v] = (int)(ldv[v] / kTile);
-    any = any || sel;
-  }
-  if (!any) return;  // (uniform over the workgroup)
-  __shared__ Pipe2Lds L;
-  extern __shared__ double sxDyn[];  // rhs / y of the two windows, max_fpad doubles each
-  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  const int team = wave & 1, tt = (wave >> 1) * 64 + lane;
-#pragma unroll
-  for (int v = 0; v < 2; ++v) {
-    if (Tv[v] == 0) continue;
-    const int fdim = P.win_fdim[wv[v]];
-    const double* rhs = P.rhsF + P.win_foff[wv[v]];
-    for (int e = t; e < ldv[v]; e += 512) sxDyn[v * P.max_fpad + e] = (e < fdim) ? rhs[e] : 0.0;
-  }
-  if (t < 8) L.sFl[t] = 0;
-  if (t < 2) { L.fact[t] = 0; L.diag[t] = 0; L.fail[t] = 0; }
-  __syncthreads();
-  const int Tmax = max(Tv[0], Tv[1]);
-  if (team == 0) {
-    // ---- team F: (w0, 0), (w1, 0), (w0, 1), (w1, 1), ...
-    int fgen = 0;
-    int failed = 0;  // bit v: window v's factorisation failed
-    for (int k = 0; k < Tmax; ++k)
-      for (int v = 0; v < 2; ++v) {
-        // (the pair's values picked by select: an indexed read of the arrays would go to scratch)
-        const int w = v ? wv[1] : wv[0], Tw = v ? Tv[1] : Tv[0];
-        const int64_t ld = v ? ldv[1] : ldv[0];
-        if (k >= Tw || ((failed >> v) & 1)) continue;
-        double* sx = sxDyn + v * P.max_fpad;
-        if (k > 0) waitFlag<false>(&L.diag[v], k, &L.fail[v]);  // (team B never sets fail)
-        if (tt < kTile) L.sy[tt] = sx[k * kTile + tt];
-        if (!potrfTileBody<22>(tileSrc(P, w, ld).at(k, k, k), ld, P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile,
-                               nullptr, L.sA, L.sX, L.sy, L.sRl, L.sFl, tt, false, fgen)) {
-          fgen += kPotrfBarriers - 1;  // (a failed factor passes two of its three barriers)
-          failed |= 1 << v;
-          if (tt == 0) {
-            P.st[w].gn_failed = 1;
-            ldsRelease(&L.fail[v], 1);
-          }
-          continue;
-        }
-        fgen += kPotrfBarriers;
-        if (tt < kTile) sx[k * kTile + tt] = L.sy[tt];  // y_k
-        waveBarrier<false>(&L.sFl[4], fgen, 4, lane);      // every X_k row stored to Linv
-        if (tt == 0) ldsRelease(&L.fact[v], k + 1);
-      }
-  } else {
-    // ---- team B: step (w, k) once X_k is stored, in team F's order
-    const int tt0 = tt;
-    int bgen = 0;
-    const TeamSync<false> bsync{&L.sFl[5], &bgen, lane};
-    const TeamSync<true> bsyncL{&L.sFl[5], &bgen, lane};
-    int failed = 0;
-    double xf[16][2];
-    for (int k = 0; k + 1 < Tmax; ++k)
-      for (int v = 0; v < 2; ++v) {
-        const int w = v ? wv[1] : wv[0], T = v ? Tv[1] : Tv[0];
-        const int64_t ld = v ? ldv[1] : ldv[0];
-        if (k + 1 >= T || ((failed >> v) & 1)) continue;
-        if (!waitFlag<false>(&L.fact[v], k + 1, &L.fail[v])) {
-          failed |= 1 << v;
-          continue;
-        }
-        int tt = tt0;
-        asm volatile("" : "+v"(tt));
-        const TileSrc cur = tileSrc(P, w, ld);
-        double* W = P.W + P.win_soff[w];
-        const uint8_t* nz = P.tile_nz + P.win_tnzoff[w];
-        double* sx = sxDyn + v * P.max_fpad;
-        const double* Xg = P.Linv + P.win_linvoff[w] + (int64_t)k * kTile * kTile;
-        if (tt < kTile) L.sz[tt] = sx[k * kTile + tt];
-        bsyncL();
-        panelRhsVectorG(Xg, L.sz, L.sz + kTile, L.sB[0], tt, bsyncL);
-        loadXFragG(Xg, xf, tt);
-        int held[2] = {-1, -1};
-        const bool crit = nz[(k + 1) * T + k] != 0;
-        if (crit) {
-          // the critical path: panel (k+1, k), then its update of tile (k+1, k+1) (to W)
-          pipePanel(cur.at(k + 1, k, k), W + (int64_t)(k + 1) * kTile * ld + k * kTile, ld, sx + (k + 1) * kTile, L.sB[0],
-                    xf, L.sz + kTile, tt, bsyncL);
-          held[0] = k + 1;
-          dbl4 c[2][2], acc[2][2];
-          loadC(cur.at(k + 1, k + 1, k), ld, c, tt);
-          mfmaTileNT(L.sB[0], L.sB[0], acc, tt);
-          storeTileSub(W + (int64_t)(k + 1) * kTile * ld + (k + 1) * kTile, ld, c, acc, tt);
-        }
-        bsync();  // tile (k+1, k+1) in W and rhs_(k+1) for team F
-        if (tt == 0) ldsRelease(&L.diag[v], k + 1);
-        int hb = crit ? 1 : 0;
-        for (int i = k + 2; i < T; ++i) {
-          if (!nz[i * T + k]) continue;
-          pipePanel(cur.at(i, k, k), W + (int64_t)i * kTile * ld + k * kTile, ld, sx + i * kTile, L.sB[hb], xf,
-                    L.sz + kTile, tt, bsyncL);
-          held[hb] = i;
-          if (!crit) hb ^= 1;
-        }
-        bsync();
-        for (int i = T - 1; i > k; --i) {
-          if (!nz[i * T + k]) continue;
-          for (int j = k + 1; j <= i; ++j) {
-            if (!nz[j * T + k] || i == k + 1) continue;
-            int bi = held[0] == i ? 0 : (held[1] == i ? 1 : -1);
-            int bj = j == i ? bi : (held[0] == j ? 0 : (held[1] == j ? 1 : -1));
-            bool loaded = false;
-            if (bi < 0) {
-              bi = bj >= 0 ? bj ^ 1 : 0;
-              loadTile(W + (int64_t)i * kTile * ld + k * kTile, ld, 0, 0, L.sB[bi], tt);
-              held[bi] = i;
-              if (j == i) bj = bi;
-              loaded = true;
-            }
-            if (bj < 0) {
-              bj = bi ^ 1;
-              loadTile(W + (int64_t)j * kTile * ld + k * kTile, ld, 0, 0, L.sB[bj], tt);
-              held[bj] = j;
-              loaded = true;
-            }
-            if (loaded) bsyncL();
-            dbl4 c[2][2], acc[2][2];
-            loadC(cur.at(i, j, k), ld, c, tt);
-            mfmaTileNT(L.sB[bi], L.sB[bj], acc, tt);
-            storeTileSub(W + (int64_t)i * kTile * ld + j * kTile, ld, c, acc, tt);
-            bsyncL();
-          }
-        }
-        bsync();
-      }
-  }
-  __syncthreads();
-  // backward substitutions: team F solves the first window, team B the second (team barriers)
-  const int v = team;
-  const int w = v ? wv[1] : wv[0], Tw = v ? Tv[1] : Tv[0];
-  const int64_t ldw = v ? ldv[1] : ldv[0];
-  if (Tw == 0 || L.fail[v]) return;
-  int sgen = 0;
-  int* ctr = &L.sFl[6 + team];
-  const TeamSync<false> ssync{ctr, &sgen, lane};
-  backSubstitute<256>(P, w, P.W + P.win_soff[w], ldw, Tw, P.Linv + P.win_linvoff[w], P.tile_nz + P.win_tnzoff[w],
-                      sxDyn + v * P.max_fpad, team == 0 ? L.sA : L.sB[0], team == 0 ? L.sy : L.sz, tt, ssync);
-}
-
-bool cholesky_pipe2_fits(int max_fpad, size_t lds_per_block) {
-  hipFuncAttributes attr;
-  if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky_pipe2)) != hipSuccess) return false;
-  return attr.sharedSizeBytes + 2 * sizeof(double) * (size_t)max_fpad <= lds_per_block;
-}
-
-void launch_cholesky_pipe2(const DevProblem& P, hipStream_t s) {
-  if (P.n_win == 0) return;
-  hipLaunchKernelGGL(k_cholesky_pipe2, dim3((P.n_win + 1) / 2), dim3(512), 2 * sizeof(double) * P.max_fpad, s, P.self);
-}
-
 bool cholesky_pipe_fits(int max_fpad, size_t lds_per_block) {
   hipFuncAttributes attr;
   if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky_pipe)) != hipSuccess) return false;

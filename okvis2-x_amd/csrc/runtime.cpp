@@ -1387,7 +1387,6 @@ struct okvisgpu_ctx {
   size_t ldsPerBlock = 65536;
   bool persistentFits() const { return cholesky_persistent_fits(P.max_fpad, ldsPerBlock); }
   bool pipeFits() const { return cholesky_pipe_fits(P.max_fpad, ldsPerBlock); }
-  bool pipe2Fits() const { return cholesky_pipe2_fits(P.max_fpad, ldsPerBlock); }
   // S is cleared by the build's arena memset; its padded diagonal (rows >= fdim) is set once per
   // build before the first factorisation (k_zero_S setup mode). The factorisation works in W and
   // the assembly overwrites its blocks, so S needs no clearing per iteration.
@@ -1890,17 +1889,21 @@ struct okvisgpu_ctx {
     // Cholesky schedule (measured on MI355X, S50 windows, bench window-it/s, round 4 with the
     // nested-dissection order (nd) below one window per CU: 64 windows: schedule 1 65.2k, 2 (nd)
     // 72.2k; 128: 1 103.6k, 3 (nd) 107.9k, 2 (nd) 98.2k; 256: 1 159.7k, 3 (nd) 152.8k; 512: 1
-    // 186.5k, 3 (nd) 166.0k; gpurun_out r04g / r04h nd_probe): below half a window per CU the
-    // tile-parallel launches spread each window over many CUs; up to one window per CU the
-    // persistent kernel split over the two parts of the order; from there one persistent
-    // workgroup per window. (A wave-specialised kernel and a persistent variant with the panel
-    // tiles in LDS were measured slower at every batch size and removed in round 4.)
-    int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 5 ? o.cholesky_schedule : 0;
-    if (sched == 0) sched = 2 * P.n_win < cuCount ? 2 : (B.any_split && P.n_win < cuCount ? 3 : 1);
+    // 186.5k, 3 (nd) 166.0k; gpurun_out r04g / r04h nd_probe; round 5, the pipelined two-team
+    // kernel (4), gpurun_out r05g: 64: 2 74.1k, 4 67.0k; 128: 3 110.1k, 4 105.7k; 256: 1 161.0k,
+    // 4 170.1k; 512: 1 186.7k, 4 178.7k): below half a window per CU the tile-parallel launches
+    // spread each window over many CUs; up to half a window per CU the persistent kernel split over
+    // the two parts of the order; up to one window per CU the pipelined kernel (its step is the
+    // factor plus one panel and one update); from there one persistent workgroup per window, two
+    // per CU. (A wave-specialised kernel and a persistent variant with the panel tiles in LDS were
+    // measured slower at every batch size and removed in round 4; a two-window pipelined
+    // workgroup, round 5, ran 166.8k against 199.4k at 2,048 windows and was removed.)
+    int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 4 ? o.cholesky_schedule : 0;
+    if (sched == 0)
+      sched = 2 * P.n_win < cuCount ? 2 : (2 * P.n_win <= cuCount && B.any_split ? 3 : (P.n_win <= cuCount ? 4 : 1));
     if (sched == 3 && !B.any_split) sched = 1;  // (no window with a nested-dissection split)
     // the persistent kernel keeps the window's rhs / y in dynamic LDS next to its static tiles:
     // a reduced dimension beyond what fits falls back to the tile-parallel launches
-    if (sched == 5 && !pipe2Fits()) sched = 4;
     if (sched == 4 && !pipeFits()) sched = 1;
     if ((sched == 1 || sched == 3) && !persistentFits()) sched = 2;
     if (sched != P.chol_schedule && iterGraph) {
