@@ -381,6 +381,24 @@ def single_window(og, cfg, opts, args, device):
         w1[0].reset()
         c1.update_params()
         out["eval_imu_forced_reintegration_ms"] = round(c1.time_kernel("k_eval_imu", 5)[0], 4)
+        # which iterations of window 0 re-integrated IMU factors (ImuError::redoPreintegration,
+        # counted by redoCounter_ = imu_state[:, 0]): solves of 0..K iterations from the same start
+        # (the same bits up to their last iteration), the counters written back after each; entry n
+        # is the number of factors re-integrated during iteration n (entry 0: the initial evaluation)
+        o2 = bench_options(total_iters)
+        o2.cholesky_schedule = opts.cholesky_schedule
+        counts = []
+        for n in range(total_iters + 1):
+            w1[0].reset()
+            c1.update_params()
+            o2.max_num_iterations = n
+            c1.solve(o2)
+            counts.append(float(w1[0].imu_state()[:, 0].sum()))
+        per = [int(round(counts[0]))] + [int(round(counts[n] - counts[n - 1])) for n in range(1, len(counts))]
+        out["imu_reintegrated_factors_per_iteration"] = per
+        later = [n for n in range(1, len(per)) if per[n] > 0]
+        out["imu_last_reintegrating_iteration"] = later[-1] if later else 0
+        out["imu_factors"] = int(w1[0].problem.n_imu)
     c1.close()
     return out, gpu_pose, gt_p
 
