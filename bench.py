@@ -117,18 +117,18 @@ def ate(P, gt):
 
 
 PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
-PMC_CALIB = os.path.join(REPO, "profiles", "r03_pmc_calib.json")
+PMC_CALIB = os.path.join(REPO, "profiles", "r05_pmc_calib.json")
 
 
 def pmc_mfma():
     """MFMA counters of k_cholesky on this workload (scripts/gpu_pmc_calib.sh ->
-    profiles/r03_pmc_calib.json): the busy fraction of the matrix cores and the FLOPs the counted
+    profiles/r05_pmc_calib.json, collected on the round-5 code): the busy fraction of the matrix cores and the FLOPs the counted
     v_mfma_f64_16x16x4f64 instructions perform, or None."""
     try:
         with open(PMC_CALIB) as f:
             d = json.load(f)["k_cholesky_mfma"]
         return {"mfma_busy_frac": d["mfma_busy_frac"], "mfma_flops_per_dispatch": d["mfma_flops"],
-                "source": "profiles/r03_pmc_calib.json (SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_F64, "
+                "source": "profiles/r05_pmc_calib.json (SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_F64, "
                           "GRBM_GUI_ACTIVE; 2,048 S50 windows)"}
     except (OSError, KeyError, ValueError, TypeError):
         return None
