@@ -86,61 +86,22 @@ __device__ __forceinline__ void evalObsThread(const DevProblem& P, int o, int mo
 #pragma unroll
   for (int k = 0; k < 4; ++k) hp[k] = hpp[k];
 
-  double C_WS[9], C_SC[9];
+  double C_WS[9];
   qrot(qnormalize(Q{pose[3], pose[4], pose[5], pose[6]}), C_WS);
-  qrot(qnormalize(Q{ex[3], ex[4], ex[5], ex[6]}), C_SC);
-  const double w4 = hp[3];
-  // p = hp_W.xyz - t_WS w ; hp_S = C_SW p ; hp_C = C_CS (hp_S - t_SC w)
-  const double p[3] = {hp[0] - pose[0] * w4, hp[1] - pose[1] * w4, hp[2] - pose[2] * w4};
-  double hS[3];
-  mtv3(C_WS, p, hS);
-  const double q3[3] = {hS[0] - ex[0] * w4, hS[1] - ex[1] * w4, hS[2] - ex[2] * w4};
-  double hC[3];
-  mtv3(C_SC, q3, hC);
-
-  double kp[2], Jh[6];
-  projectHomogeneous(cam, hC[0], hC[1], hC[2], w4, kp, Jh, true);
-  const double e0 = m[0] - kp[0], e1 = m[1] - kp[1];
-  double r0 = L[0] * e0 + L[1] * e1;
-  double r1 = L[2] * e0 + L[3] * e1;
-  // Jh_w = L Jh (2x3); C_CW = C_SC^T C_WS^T ; A = Jh_w C_CW
-  double Jw[6];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    Jw[c] = L[0] * Jh[c] + L[1] * Jh[3 + c];
-    Jw[3 + c] = L[2] * Jh[c] + L[3] * Jh[3 + c];
-  }
-  double B[6];  // Jh_w C_CS = Jh_w C_SC^T : B[r][k] = sum_j Jw[r][j] C_SC[k][j]
-#pragma unroll
-  for (int r = 0; r < 2; ++r)
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-      B[r * 3 + k] = Jw[r * 3 + 0] * C_SC[k * 3 + 0] + Jw[r * 3 + 1] * C_SC[k * 3 + 1] + Jw[r * 3 + 2] * C_SC[k * 3 + 2];
-  double A[6];  // B C_SW = B C_WS^T : A[r][c] = sum_k B[r][k] C_WS[c][k]
-#pragma unroll
-  for (int r = 0; r < 2; ++r)
-#pragma unroll
-    for (int c = 0; c < 3; ++c)
-      A[r * 3 + c] = B[r * 3 + 0] * C_WS[c * 3 + 0] + B[r * 3 + 1] * C_WS[c * 3 + 1] + B[r * 3 + 2] * C_WS[c * 3 + 2];
-
-  // Cauchy(1) corrector (rho'' < 0 branch: scale residual and Jacobian by sqrt(rho'))
-  const double sq = r0 * r0 + r1 * r1;
-  double cost, sc = 1.0;
-  if (flags & 1) {
-    const double sum = 1.0 + sq;
-    cost = 0.5 * log(sum);
-    sc = sqrt(fmax(DBL_MIN, 1.0 / sum));
-  } else {
-    cost = 0.5 * sq;
-  }
+  double r[2], A[6], cost;
+  obsCore(cam, L, m, pose, C_WS, hp, ex, (flags & 1) != 0, true, r, A, cost);
   // stored: r and A (both Cauchy-scaled); the pose/landmark Jacobians follow from A and the
-  // linearisation point (obsJacobians)
+  // linearisation point (obsJacobians). (Also at a candidate: measured in round 5, storing only the
+  // candidate's cost and forming r and A in k_lm_visit<1> after an accepted step took k_eval_obs
+  // 0.98 -> 0.63 ms but k_lm_visit<1> 2.84 -> 3.70 ms at 2,048 S50 windows, 195.7k -> 188.0k
+  // window-it/s with the same bits: the eval kernel's thread per residual hides the loads' latency
+  // that a landmark group's threads do not.)
   double* lin = pick2(lb, P.obs_lin[0], P.obs_lin[1]);
   const int64_t S = P.obs_stride;
-  lin[0 * S + o] = r0 * sc;
-  lin[1 * S + o] = r1 * sc;
+  lin[0 * S + o] = r[0];
+  lin[1 * S + o] = r[1];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) lin[(2 + k) * S + o] = A[k] * sc;
+  for (int k = 0; k < 6; ++k) lin[(2 + k) * S + o] = A[k];
   pick2(lb, P.obs_cost[0], P.obs_cost[1])[o] = cost;
 }
 

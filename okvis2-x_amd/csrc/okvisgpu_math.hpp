@@ -4,6 +4,7 @@
 // Conventions follow the reference's Eigen usage: quaternion coefficients (x, y, z, w), Hamilton
 // product, Eigen::QuaternionBase::toRotationMatrix(). Formulas cite the okvis source they restate.
 #pragma once
+#include <cfloat>
 
 #include <hip/hip_runtime.h>
 #include <cmath>
@@ -372,6 +373,62 @@ OKG_HD void reprojectA(const Cam& cam, const double* pose, const double* hp, con
   for (int rr = 0; rr < 2; ++rr)
     for (int c = 0; c < 3; ++c)
       A[rr * 3 + c] = B[rr * 3 + 0] * C_WS[c * 3 + 0] + B[rr * 3 + 1] * C_WS[c * 3 + 1] + B[rr * 3 + 2] * C_WS[c * 3 + 2];
+}
+
+// ReprojectionError<G>::EvaluateWithMinimalJacobians + the Cauchy(1) corrector in the fused form of
+// the device (implementation/ReprojectionError.hpp:71-220, ViGraph.cpp:235,338): residual r = L (m -
+// kp) and, with wantA, A = L Jh C_CS C_SW (2x3), both scaled by the corrector's sqrt(rho'), and the
+// robustified cost. C_WS = R(q_WS) of the pose (formed once per pose by the callers), ex = T_SC.
+// (k_eval_obs; without wantA only r and the cost.)
+OKG_HD void obsCore(const Cam& cam, const double L[4], const double m[2], const double* pose, const double C_WS[9],
+                    const double hp[4], const double ex[7], bool loss, bool wantA, double r[2], double A[6],
+                    double& cost) {
+  double C_SC[9];
+  qrot(qnormalize(Q{ex[3], ex[4], ex[5], ex[6]}), C_SC);
+  const double w4 = hp[3];
+  // p = hp_W.xyz - t_WS w ; hp_S = C_SW p ; hp_C = C_CS (hp_S - t_SC w)
+  const double p[3] = {hp[0] - pose[0] * w4, hp[1] - pose[1] * w4, hp[2] - pose[2] * w4};
+  double hS[3];
+  mtv3(C_WS, p, hS);
+  const double q3[3] = {hS[0] - ex[0] * w4, hS[1] - ex[1] * w4, hS[2] - ex[2] * w4};
+  double hC[3];
+  mtv3(C_SC, q3, hC);
+  double kp[2], Jh[6];
+  projectHomogeneous(cam, hC[0], hC[1], hC[2], w4, kp, Jh, wantA);
+  const double e0 = m[0] - kp[0], e1 = m[1] - kp[1];
+  const double r0 = L[0] * e0 + L[1] * e1;
+  const double r1 = L[2] * e0 + L[3] * e1;
+  // Cauchy(1) corrector (rho'' < 0 branch: scale residual and Jacobian by sqrt(rho'))
+  const double sq = r0 * r0 + r1 * r1;
+  double sc = 1.0;
+  if (loss) {
+    const double sum = 1.0 + sq;
+    cost = 0.5 * log(sum);
+    sc = sqrt(fmax(DBL_MIN, 1.0 / sum));
+  } else {
+    cost = 0.5 * sq;
+  }
+  r[0] = r0 * sc;
+  r[1] = r1 * sc;
+  if (!wantA) return;
+  // Jh_w = L Jh (2x3); C_CW = C_SC^T C_WS^T ; A = Jh_w C_CW
+  double Jw[6];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    Jw[c] = L[0] * Jh[c] + L[1] * Jh[3 + c];
+    Jw[3 + c] = L[2] * Jh[c] + L[3] * Jh[3 + c];
+  }
+  double B[6];  // Jh_w C_CS = Jh_w C_SC^T : B[r][k] = sum_j Jw[r][j] C_SC[k][j]
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      B[rr * 3 + k] = Jw[rr * 3 + 0] * C_SC[k * 3 + 0] + Jw[rr * 3 + 1] * C_SC[k * 3 + 1] + Jw[rr * 3 + 2] * C_SC[k * 3 + 2];
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr)  // B C_SW = B C_WS^T : A[r][c] = sum_k B[r][k] C_WS[c][k]
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      A[rr * 3 + c] = (B[rr * 3 + 0] * C_WS[c * 3 + 0] + B[rr * 3 + 1] * C_WS[c * 3 + 1] + B[rr * 3 + 2] * C_WS[c * 3 + 2]) * sc;
 }
 
 // Symmetric eigen-decomposition A = V diag(lam) V^T by cyclic Jacobi (Eigen's
