@@ -323,7 +323,7 @@ def parse_args(argv=None):
                     help="windows in the batch CPU sample (default: 3 per host thread)")
     ap.add_argument("--kernel-reps", type=int, default=5, help="repetitions per kernel in the roofline table")
     ap.add_argument("--e2e-reps", type=int, default=5, help="single-window set_problems + solve repetitions")
-    ap.add_argument("--cholesky-schedule", type=int, default=0, help="0 auto, 1 persistent per window, 2 tile-parallel, 3 persistent split over a nested-dissection window, 4 pipelined persistent (two teams per window)")
+    ap.add_argument("--cholesky-schedule", type=int, default=0, help="0 auto, 1 persistent per window, 2 tile-parallel, 3 persistent split over a nested-dissection window, 4 pipelined persistent (two teams per window), 5 split with each part pipelined")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-profile", action="store_true")

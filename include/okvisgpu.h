@@ -242,8 +242,9 @@ typedef struct okvisgpu_options {   /* ::ceres::Solver::Options fields okvis set
                                     /* more windows than CUs), 2 tile-parallel launches (fewer    */
                                     /* than half as many), 3 persistent, split over the two parts */
                                     /* of a nested-dissection window (half as many), 4 pipelined  */
-                                    /* persistent, two teams per window (up to one per CU); all   */
-                                    /* give the same bits for one batch. Other values: auto.      */
+                                    /* persistent, two teams per window (up to one per CU), 5 the */
+                                    /* split schedule with each part pipelined; all give the same */
+                                    /* bits for one batch. Other values: auto.                    */
 } okvisgpu_options;
 
 typedef struct okvisgpu_summary {   /* ::ceres::Solver::Summary subset */

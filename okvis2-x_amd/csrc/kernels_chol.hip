@@ -377,6 +377,10 @@ __global__ __launch_bounds__(kBsReal) void k_chol_bsub(const DevProblem* __restr
   BSUB_CLK_REPORT(T)
 }
 
+void launch_cholesky_split_b(const DevProblem& P, hipStream_t s) {
+  hipLaunchKernelGGL(k_cholesky<2>, dim3(P.n_win), dim3(256), sizeof(double) * P.max_fpad, s, P.self);
+}
+
 bool cholesky_persistent_fits(int max_fpad, size_t lds_per_block) {
   hipFuncAttributes attr;
   if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky<0>)) != hipSuccess) return false;
@@ -385,8 +389,8 @@ bool cholesky_persistent_fits(int max_fpad, size_t lds_per_block) {
 
 void launch_cholesky(const DevProblem& P, hipStream_t s) {
   if (P.n_win == 0) return;
-  if (P.chol_schedule == 4) {
-    launch_cholesky_pipe(P, s);
+  if (P.chol_schedule == 4 || P.chol_schedule == 5) {
+    launch_cholesky_pipe(P, s, P.chol_schedule == 5);
     return;
   }
   if (P.chol_schedule == 1) {

@@ -69,15 +69,21 @@ __device__ __forceinline__ void mfmaTileNTX(const double* sA, const double (&xf)
 
 // Panel of team B: L_ik = A_ik X^T (A_ik staged in sBuf), rhs_i -= A_ik z (panelTile's
 // operations), L_ik stored to W and left in sBuf for the step's band updates.
+// (defer: the split schedule's right part stores the rhs term of a separator row instead, for the
+// separator's launch to subtract in step order)
 template <class Sync>
 __device__ __forceinline__ void pipePanel(const double* Aik, double* Lik, int64_t ld, double* worki, double* sBuf,
-                                          const double (&xf)[16][2], const double* sz, int t, Sync sync) {
+                                          const double (&xf)[16][2], const double* sz, int t, Sync sync,
+                                          double* defer = nullptr) {
   loadTile(Aik, ld, 0, 0, sBuf, t);
   sync();
   dbl4 acc[2][2];
   mfmaTileNTX(sBuf, xf, acc, t);
   const double a = panelRhsRow(sBuf, sz, t);
-  if ((t & 3) == 0) worki[t >> 2] -= a;  // rhs_i in LDS
+  if ((t & 3) == 0) {
+    if (defer) defer[t >> 2] = a;
+    else worki[t >> 2] -= a;  // rhs_i in LDS
+  }
   sync();  // every wavefront has read A_ik
   accToLds(sBuf, acc, t);
   storeTile<false>(Lik, ld, 0, 0, acc, t);
@@ -109,12 +115,27 @@ struct PipeLds {
                               // [2] the handed-over tile is in sA, [3] failed pivot
 };
 
+// MODE 0: the whole window (schedule 4). MODE 1: launch A of the split schedule over a nested-
+// dissection window's two independent parts (schedule 5; k_cholesky<1>'s roles, pipelined):
+// workgroup 2w + part runs the part's steps [k0, k1); the right part (part 1) updates only targets
+// left of the separator and, for the separator's rows, stores L and each panel's rhs term
+// (chol_defer); both leave their y / rhs rows in fwdF for launch B (k_cholesky<2>: the separator's
+// contributions in step order, its factorisation and the backward substitution). A window without
+// a split runs MODE 0's work in part 0.
+template <int MODE>
 __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
-  const int w = blockIdx.x;
+  const int w = MODE == 1 ? (int)(blockIdx.x >> 1) : (int)blockIdx.x, part = MODE == 1 ? (int)(blockIdx.x & 1) : 0;
   if (!cholSelect(P, w)) return;  // (uniform over the workgroup)
   const int64_t ld = P.win_fpad[w];
   const int T = (int)(ld / kTile);
+  const int tL = MODE == 0 ? 0 : P.win_bsplit[2 * w], tS = MODE == 0 ? 0 : P.win_bsplit[2 * w + 1];
+  const bool split = MODE != 0 && tS > 0;
+  if (MODE == 1 && part == 1 && !split) return;
+  const int k0 = !split ? 0 : (part == 0 ? 0 : tL), k1 = !split ? T : (part == 0 ? tL : tS);
+  const int jEnd = split && part == 1 ? tS : T;  // targets (i, j) with j < jEnd
+  double* defer = split && part == 1 ? P.chol_defer + P.win_defoff[w] : nullptr;
+  auto deferAt = [&](int i, int k) { return defer + ((size_t)(i - tS) * (tS - tL) + (k - tL)) * kTile; };
   const TileSrc cur = tileSrc(P, w, ld);
   double* W = P.W + P.win_soff[w];
   double* Linv = P.Linv + P.win_linvoff[w];
@@ -132,9 +153,9 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
   if (team == 0) {
     // ---- team F: the diagonal tiles in order
     int fgen = 0;
-    for (int k = 0; k < T; ++k) {
+    for (int k = k0; k < k1; ++k) {
       bool inLds = false;
-      if (k > 0) {  // tile k has all its updates (and rhs_k its panel terms); X_(k-1) was taken
+      if (k > k0) {  // tile k has all its updates (and rhs_k its panel terms); X_(k-1) was taken
         if (!waitFlag<false>(&L.pipe[1], k, &L.pipe[3])) break;
         inLds = L.pipe[2] != 0;
       }
@@ -155,8 +176,17 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
     const TeamSync<false> bsync{&L.sFl[5], &bgen, lane};
     const TeamSync<true> bsyncL{&L.sFl[5], &bgen, lane};
     double xf[16][2];
-    for (int k = 0; k + 1 < T; ++k) {
+    for (int k = k0; k < k1; ++k) {
       if (!waitFlag<false>(&L.pipe[0], k + 1, &L.pipe[3])) break;
+      bool below = false;  // (a step without tiles below only hands the next tile over)
+      for (int i = k + 1; i < T; ++i) below = below || nz[i * T + k];
+      if (!below) {
+        if (tt0 == 0) {
+          L.pipe[2] = 0;
+          ldsRelease(&L.pipe[1], k + 1);
+        }
+        continue;
+      }
       // the thread index, opaque per step: the step's LDS / global addresses are formed in the step
       // instead of being hoisted out of the loop (and spilled: the kernel is at 256 VGPRs)
       int tt = tt0;
@@ -168,7 +198,7 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
       panelRhsVector(L.sX, L.sz, L.sz + kTile, L.sB[0], tt, bsyncL);
       loadXFrag(L.sX, xf, tt);
       int held[2] = {-1, -1};  // block row i of the L_ik in sB[0] / sB[1]
-      const bool crit = nz[(k + 1) * T + k] != 0;
+      const bool crit = k + 1 < k1 && nz[(k + 1) * T + k] != 0;
       if (crit) {
         // the critical path: panel (k+1, k), then its update of tile (k+1, k+1) into team F's sA
         pipePanel(cur.at(k + 1, k, k), W + (int64_t)(k + 1) * kTile * ld + k * kTile, ld, sxDyn + (k + 1) * kTile,
@@ -189,7 +219,7 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
       for (int i = k + 2; i < T; ++i) {
         if (!nz[i * T + k]) continue;
         pipePanel(cur.at(i, k, k), W + (int64_t)i * kTile * ld + k * kTile, ld, sxDyn + i * kTile, L.sB[hb], xf,
-                  L.sz + kTile, tt, bsyncL);
+                  L.sz + kTile, tt, bsyncL, i >= jEnd ? deferAt(i, k) : nullptr);
         held[hb] = i;
         if (!crit) hb ^= 1;
       }
@@ -198,7 +228,9 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
       for (int i = T - 1; i > k; --i) {
         if (!nz[i * T + k]) continue;
         for (int j = k + 1; j <= i; ++j) {
-          if (!nz[j * T + k] || i == k + 1) continue;  // (row k+1: only (k+1, k+1), done above)
+          // (row k+1: only (k+1, k+1), done above when critical; the right part of a split
+          // window leaves the separator's tiles to launch B)
+          if (!nz[j * T + k] || (i == k + 1 && crit) || j >= jEnd) continue;
           int bi = held[0] == i ? 0 : (held[1] == i ? 1 : -1);
           int bj = j == i ? bi : (held[0] == j ? 0 : (held[1] == j ? 1 : -1));
           bool loaded = false;
@@ -231,18 +263,31 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
     if (t == 0) P.st[w].gn_failed = 1;
     return;
   }
+  if (split) {  // launch A: this part's rows of y (part 0 also the separator's rhs) for launch B
+    double* work = P.fwdF + P.win_fwdoff[w];
+    const int e0 = part == 0 ? 0 : tL * kTile, e1 = part == 0 ? tL * kTile : tS * kTile;
+    for (int e = t; e < ld; e += 512)
+      if ((e >= e0 && e < e1) || (part == 0 && e >= tS * kTile)) work[e] = sxDyn[e];
+    return;
+  }
   backSubstitute<512>(P, w, W, ld, T, Linv, nz, sxDyn, L.sB[0], L.sy, t);
 }
 
 bool cholesky_pipe_fits(int max_fpad, size_t lds_per_block) {
   hipFuncAttributes attr;
-  if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky_pipe)) != hipSuccess) return false;
+  if (hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(k_cholesky_pipe<1>)) != hipSuccess) return false;
   return attr.sharedSizeBytes + sizeof(double) * (size_t)max_fpad <= lds_per_block;
 }
 
-void launch_cholesky_pipe(const DevProblem& P, hipStream_t s) {
+// split: schedule 5 (launch A pipelined per nested-dissection part, launch B = k_cholesky<2>)
+void launch_cholesky_pipe(const DevProblem& P, hipStream_t s, bool split) {
   if (P.n_win == 0) return;
-  hipLaunchKernelGGL(k_cholesky_pipe, dim3(P.n_win), dim3(512), sizeof(double) * P.max_fpad, s, P.self);
+  if (!split) {
+    hipLaunchKernelGGL(k_cholesky_pipe<0>, dim3(P.n_win), dim3(512), sizeof(double) * P.max_fpad, s, P.self);
+    return;
+  }
+  hipLaunchKernelGGL(k_cholesky_pipe<1>, dim3(2 * P.n_win), dim3(512), sizeof(double) * P.max_fpad, s, P.self);
+  launch_cholesky_split_b(P, s);
 }
 
 }  // namespace okg

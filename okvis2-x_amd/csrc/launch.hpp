@@ -44,7 +44,8 @@ void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s);  // 0/1: lin
 bool cholesky_persistent_fits(int max_fpad, size_t lds_per_block);
 bool cholesky_pipe_fits(int max_fpad, size_t lds_per_block);  // (kernels_chol_pipe.hip)
 void launch_cholesky(const DevProblem& P, hipStream_t s);
-void launch_cholesky_pipe(const DevProblem& P, hipStream_t s);
+void launch_cholesky_pipe(const DevProblem& P, hipStream_t s, bool split);
+void launch_cholesky_split_b(const DevProblem& P, hipStream_t s);  // k_cholesky<2> (kernels_chol.hip)
 
 // trust-region control (kernels_control.hip)
 enum ReduceMode { R_COST_INIT = 0, R_COST_CAND = 1, R_JV = 2 };

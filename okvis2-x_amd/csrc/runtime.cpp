@@ -1898,12 +1898,14 @@ struct okvisgpu_ctx {
     // per CU. (A wave-specialised kernel and a persistent variant with the panel tiles in LDS were
     // measured slower at every batch size and removed in round 4; a two-window pipelined
     // workgroup, round 5, ran 166.8k against 199.4k at 2,048 windows and was removed.)
-    int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 4 ? o.cholesky_schedule : 0;
+    int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 5 ? o.cholesky_schedule : 0;
     if (sched == 0)
       sched = 2 * P.n_win < cuCount ? 2 : (2 * P.n_win <= cuCount && B.any_split ? 3 : (P.n_win <= cuCount ? 4 : 1));
     if (sched == 3 && !B.any_split) sched = 1;  // (no window with a nested-dissection split)
+    if (sched == 5 && !B.any_split) sched = 4;
     // the persistent kernel keeps the window's rhs / y in dynamic LDS next to its static tiles:
     // a reduced dimension beyond what fits falls back to the tile-parallel launches
+    if (sched == 5 && !(pipeFits() && persistentFits())) sched = 3;
     if (sched == 4 && !pipeFits()) sched = 1;
     if ((sched == 1 || sched == 3) && !persistentFits()) sched = 2;
     if (sched != P.chol_schedule && iterGraph) {

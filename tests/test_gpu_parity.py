@@ -446,7 +446,7 @@ def test_cholesky_schedules_agree_nested_dissection(og, oracle, gpu_ctx):
     (natural order) agrees to the usual tolerance."""
     ws = [og.SynthWindow(50, 2000, 16000, seed=s) for s in (33, 34)]
     res = []
-    for sched in (1, 2, 3, 4):
+    for sched in (1, 2, 3, 4, 5):
         for w in ws:
             w.reset()
         opts = og.default_options(max_num_iterations=4, function_tolerance=0.0, gradient_tolerance=0.0,
@@ -473,7 +473,7 @@ def test_cholesky_schedules_ragged_batch(og, gpu_ctx):
     shapes = [(10, 500, 4000), (30, 1200, 9000), (12, 600, 5000), (50, 2000, 16000), (20, 900, 7000)]
     ws = [og.SynthWindow(kf, lm, obs, seed=60 + k) for k, (kf, lm, obs) in enumerate(shapes)]
     res = []
-    for sched in (1, 2, 4):
+    for sched in (1, 2, 4, 5):
         for w in ws:
             w.reset()
         opts = og.default_options(max_num_iterations=5, cholesky_schedule=sched)

@@ -123,7 +123,7 @@ def test_relpose_cholesky_schedules(og, oracle, gpu_ctx):
     """Non-adjacent keyframe pairs widen the band of S: every schedule must follow the fill."""
     w = _relpose_window(og, 20, 800, 6000, n_relpose=6, stride=9, seed=44)
     so = None
-    for sched in (1, 2, 3, 4):
+    for sched in (1, 2, 3, 4, 5):
         w.reset()
         gpu_ctx.set_problems([w.problem])
         sg = gpu_ctx.solve(_opts(og, 4, cholesky_schedule=sched), 1)[0]
@@ -142,7 +142,7 @@ def test_wide_band_schedules_bitwise(og, oracle, gpu_ctx):
     schedules must still agree bitwise, and both with the oracle."""
     w = _relpose_window(og, 40, 1600, 12000, n_relpose=4, stride=30, seed=45)
     res = []
-    for sched in (1, 2, 3, 4):
+    for sched in (1, 2, 3, 4, 5):
         w.reset()
         gpu_ctx.set_problems([w.problem])
         sg = gpu_ctx.solve(_opts(og, 4, cholesky_schedule=sched), 1)[0]
