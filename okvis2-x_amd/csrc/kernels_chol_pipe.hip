@@ -216,7 +216,9 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
       }
       // the step's other panels (the last ones stay in LDS for the updates)
       int hb = crit ? 1 : 0;
-      for (int i = k + 2; i < T; ++i) {
+      // (without the critical pair this includes row k+1: at the end of a part of a split window,
+      // where tile k+1 is the separator's)
+      for (int i = crit ? k + 2 : k + 1; i < T; ++i) {
         if (!nz[i * T + k]) continue;
         pipePanel(cur.at(i, k, k), W + (int64_t)i * kTile * ld + k * kTile, ld, sxDyn + i * kTile, L.sB[hb], xf,
                   L.sz + kTile, tt, bsyncL, i >= jEnd ? deferAt(i, k) : nullptr);
