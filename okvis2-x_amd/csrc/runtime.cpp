@@ -1891,16 +1891,18 @@ struct okvisgpu_ctx {
     // 72.2k; 128: 1 103.6k, 3 (nd) 107.9k, 2 (nd) 98.2k; 256: 1 159.7k, 3 (nd) 152.8k; 512: 1
     // 186.5k, 3 (nd) 166.0k; gpurun_out r04g / r04h nd_probe; round 5, the pipelined two-team
     // kernel (4), gpurun_out r05g: 64: 2 74.1k, 4 67.0k; 128: 3 110.1k, 4 105.7k; 256: 1 161.0k,
-    // 4 170.1k; 512: 1 186.7k, 4 178.7k): below half a window per CU the tile-parallel launches
-    // spread each window over many CUs; up to half a window per CU the persistent kernel split over
-    // the two parts of the order; up to one window per CU the pipelined kernel (its step is the
-    // factor plus one panel and one update); from there one persistent workgroup per window, two
-    // per CU. (A wave-specialised kernel and a persistent variant with the panel tiles in LDS were
+    // 4 170.1k; 512: 1 186.7k, 4 178.7k; the split schedule with pipelined parts (5), r05s: 64: 2
+    // 73.9k, 3 70.4k, 5 73.7k; 128: 3 109.8k, 5 114.5k; 192: 4 133.6k, 3 127.3k, 5 120.7k; one S50
+    // window: 2 2,765, 5 2,336, 3 2,233, 4 1,858 it/s): below half a window per CU the
+    // tile-parallel launches spread each window over many CUs; at half a window per CU the split
+    // schedule with each part pipelined; up to one window per CU the pipelined kernel (its step is
+    // the factor plus one panel and one update); from there one persistent workgroup per window,
+    // two per CU. (A wave-specialised kernel and a persistent variant with the panel tiles in LDS were
     // measured slower at every batch size and removed in round 4; a two-window pipelined
     // workgroup, round 5, ran 166.8k against 199.4k at 2,048 windows and was removed.)
     int sched = o.cholesky_schedule >= 1 && o.cholesky_schedule <= 5 ? o.cholesky_schedule : 0;
     if (sched == 0)
-      sched = 2 * P.n_win < cuCount ? 2 : (2 * P.n_win <= cuCount && B.any_split ? 3 : (P.n_win <= cuCount ? 4 : 1));
+      sched = 2 * P.n_win < cuCount ? 2 : (2 * P.n_win <= cuCount && B.any_split ? 5 : (P.n_win <= cuCount ? 4 : 1));
     if (sched == 3 && !B.any_split) sched = 1;  // (no window with a nested-dissection split)
     if (sched == 5 && !B.any_split) sched = 4;
     // the persistent kernel keeps the window's rhs / y in dynamic LDS next to its static tiles:
