@@ -453,10 +453,20 @@ __device__ __forceinline__ bool potrfTileBody(const double* Sg, int64_t ld, doub
       if (s >= 1) {  // look-ahead update by sub-panel s-1: r -= L_i,s-1 L_(c0..c0+7),s-1^T
         // (c outer: the 8 independent chains r[m] interleave, so no FMA waits on the previous one's
         // result; every r[m] still sums over c in order, the same bits)
+        // operands in two batches of 32, each loaded before its FMAs (one LDS wait per batch;
+        // every r[m] still sums over c in order)
 #pragma unroll
-        for (int c = 0; c < 8; ++c)
+        for (int hb = 0; hb < 2; ++hb) {
+          double Lq[4][8];
 #pragma unroll
-          for (int m = 0; m < 8; ++m) r[m] -= xp[c] * sA[(c0 + m) * kLd + c0 - 8 + c];
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int m = 0; m < 8; ++m) Lq[c][m] = sA[(c0 + m) * kLd + c0 - 8 + 4 * hb + c];
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int m = 0; m < 8; ++m) r[m] -= xp[4 * hb + c] * Lq[c][m];
+        }
         // Scheduling fence: the look-ahead result is complete before its stores are issued (and,
         // below, x before the row stores). Without these the compiler interleaves the stores and
         // the next loads with the FP64 chain: 22.6 against 15.9 us per tile
@@ -475,7 +485,13 @@ __device__ __forceinline__ bool potrfTileBody(const double* Sg, int64_t ld, doub
       }
       asm volatile("" ::"v"(x[7]));
       CLK(23)
-      storeRow8(sA, c0, x, i);
+      // row i of L in the sub-panel, all 8 entries for the rows of the diagonal block too (those
+      // above its diagonal land in the tile's upper triangle, which nothing reads): one store
+      // predicate instead of one per entry (tile 16.07 -> 15.62 us, scripts/ubench_ptile.hip)
+      if (i >= c0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sA[i * kLd + c0 + k] = x[k];
+      }
       if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) sRl[c0 + k] = rl[k];
