@@ -554,7 +554,7 @@ def main(argv=None):
                 "unit": "GB/s" if d["bound"] == "hbm" else "TFLOP/s", "frac": d["frac"],
                 "traffic": traffic,
                 "traffic_calibration": "FETCH_SIZE x2, WRITE_SIZE x1: measured for this code's 16-B, 8-B and "
-                                       "tile-row access shapes (scripts/pmc_calib.hip, profiles/r03_pmc_calib.json)",
+                                       "tile-row access shapes (scripts/pmc_calib.hip, profiles/r05_pmc_calib.json)",
                 "counters": pmc_mfma() if dominant == "k_cholesky" else None,
                 "work_per_iteration": d["work"], "ms_per_iteration": d["ms"],
                 "frac_survey_8d": survey.get(dominant, {}).get("frac") if d["bound"] == "hbm" else None,

@@ -24,6 +24,17 @@ __device__ __forceinline__ bool cholSelect(const DevProblem& P, int w) {
   return !s.done && s.need_gn && !s.gn_failed;
 }
 
+// 16-column blocks of diagonal tile k before its identity tail: the rows after the last f entry
+// (padding to whole tiles) and the nested-dissection gap that ends the left part on a tile boundary
+// (runtime.cpp) are identity rows of S, uncoupled and with zero rhs, so X = I and y = rhs there;
+// potrfTile factors only the blocks before them (S10: 22 of the last tile's 64 columns hold entries).
+__device__ __forceinline__ int tileBlocks(const DevProblem& P, int w, int k) {
+  const int fdim = P.win_fdim[w], g0 = P.win_sgap[2 * w], gl = P.win_sgap[2 * w + 1];
+  int end = min(fdim - kTile * k, kTile);
+  if (gl > 0 && g0 >= kTile * k && g0 < kTile * (k + 1)) end = min(end, g0 - kTile * k);
+  return max(1, (end + 15) >> 4);
+}
+
 // Tile (i, j) as the factorisation sees it at step k: the assembled S until the first band update
 // has written it (step tile_fu), the working copy W from then on. Every factorisation write (band
 // updates, panels L_ik, the tile-parallel schedule's upper-slot L) goes to W, so S keeps the
@@ -419,11 +430,15 @@ __device__ __forceinline__ void potrfSync(int* sFl, int& tgen, int lane) {
 }
 template <int kCaller>
 __device__ __forceinline__ bool potrfTileBody(const double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX,
-                                              double* sy, double* sRl, int* sFl, int t, bool haveTile, int tgen0) {
+                                              double* sy, double* sRl, int* sFl, int t, bool haveTile, int tgen0, int nq) {
   const int wave = t >> 6, lane = t & 63;
   int tgen = tgen0;
   CLK_INIT
   if (!haveTile) loadTile(Sg, ld, 0, 0, sA, t);  // (else the caller left S_kk in sA)
+  // rows / columns from 16 nq on are an identity tail (tileBlocks): the sweep stops before them,
+  // and X = I, y = rhs there (written by wavefront 0 before its sweep, so its sub-panel flags
+  // publish them to the X stores of wavefronts 1-3)
+  nq = __builtin_amdgcn_readfirstlane(nq);
 #pragma unroll
   for (int u = 0; u < 16; ++u) {
     const int e = t + 256 * u;
@@ -438,11 +453,15 @@ __device__ __forceinline__ bool potrfTileBody(const double* Sg, int64_t ld, doub
   // blocks, one sub-panel behind, handing over through LDS flags.
   if (wave == 0) {
     const int i = lane;
+    if (i >= 16 * nq) {
+      sX[i * kLd + i] = 1.0;
+      sy[kTile + i] = sy[i];
+    }
     double xp[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) xp[k] = 0.0;
 #pragma unroll 1
-    for (int s = 0; s < 8; ++s) {
+    for (int s = 0; s < 2 * nq; ++s) {
       const int c0 = 8 * s;
       CLK(25)
       if (s >= 2 && !waitFlag<true>(&sFl[1], s - 1, &sFl[2])) break;  // trailing update of sub-panel s-2
@@ -505,7 +524,7 @@ __device__ __forceinline__ bool potrfTileBody(const double* Sg, int64_t ld, doub
     const int g = wave - 1;
     int gen = 0;
 #pragma unroll 1
-    for (int s = 0; s < 8; ++s) {
+    for (int s = 0; s < 2 * nq; ++s) {
       if (!waitFlag<true>(&sFl[0], s + 1, &sFl[2])) break;
       if (g == 0) inv8(sA, sRl, sX + 8 * s * kLd + 8 * s, 8 * s, lane);
       if (s < 6) trailingFrom(sA, 8 * s, 8 * s + 16, g, 3, lane);
@@ -520,7 +539,8 @@ __device__ __forceinline__ bool potrfTileBody(const double* Sg, int64_t ld, doub
         if (g < q) xOffDiag16(sA, sX, q, g, lane);
         waveBarrier<true>(&sFl[3], gen, 3, lane);
         if (g == 0) yBlock16(sX, sy, q, lane);
-        xStoreRows16<kCaller>(sX, Li, q, g, lane);
+        // (after the last factored block row, the identity tail's rows too)
+        for (int qs = q, qe = q + 1 < nq ? q + 1 : 4; qs < qe; ++qs) xStoreRows16<kCaller>(sX, Li, qs, g, lane);
       }
     }
   }
@@ -543,8 +563,8 @@ __device__ __forceinline__ bool potrfTileBody(const double* Sg, int64_t ld, doub
 // around every tile: 22.6 against 16.1 us per tile in scripts/ubench_team.hip).
 template <int kCaller>
 __device__ __noinline__ bool potrfTile(const double* Sg, int64_t ld, double* Li, double* workk, double* sA, double* sX, double* sy,
-                                      double* sRl, int* sFl, int t, bool haveTile, int tgen0 = 0) {
-  return potrfTileBody<kCaller>(Sg, ld, Li, workk, sA, sX, sy, sRl, sFl, t, haveTile, tgen0);
+                                      double* sRl, int* sFl, int t, bool haveTile, int tgen0 = 0, int nq = 4) {
+  return potrfTileBody<kCaller>(Sg, ld, Li, workk, sA, sX, sy, sRl, sFl, t, haveTile, tgen0, nq);
 }
 
 // acc (C layout) -> LDS tile [64][kLd]

@@ -142,7 +142,7 @@ __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem
     if (t < kTile) sy[t] = sxDyn[k * kTile + t];
     __syncthreads();  // full: the factor and the panels read the tiles the last band update stored
     if (!potrfTile<10 + MODE>(cur.at(k, k, k), ld, Linv + (int64_t)k * kTile * kTile, nullptr, sA, sX,
-                   sy, sRl, sFl, t, haveDiag)) {
+                   sy, sRl, sFl, t, haveDiag, 0, tileBlocks(P, w, k))) {
       if (t == 0) P.st[w].gn_failed = 1;
       return;
     }
@@ -217,7 +217,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_roots(const DevProblem* __restr
   if (t < kTile) sy[t] = work[d * kTile + t];
   __syncthreads();
   if (!potrfTile<1>(cur.at(d, d, d), ld, P.Linv + P.win_linvoff[w] + (int64_t)d * kTile * kTile,
-                    work + d * kTile, sA, sX, sy, sRl, sFl, t, false))
+                    work + d * kTile, sA, sX, sy, sRl, sFl, t, false, 0, tileBlocks(P, w, d)))
     if (t == 0) P.st[w].gn_failed = 1;
 }
 
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(const DevProblem* __rest
   const int d = i;
   __syncthreads();
   if (!potrfTile<2>(cur.at(d, d, d), ld, P.Linv + P.win_linvoff[w] + (int64_t)d * kTile * kTile,
-                    work + d * kTile, sA, sX, sy, sRl, sFl, t, true))
+                    work + d * kTile, sA, sX, sy, sRl, sFl, t, true, 0, tileBlocks(P, w, d)))
     if (t == 0) P.st[w].gn_failed = 1;
 }
 

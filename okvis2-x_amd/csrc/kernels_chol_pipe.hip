@@ -98,8 +98,10 @@ __device__ __forceinline__ void pipePanel(const double* Aik, double* Lik, int64_
 // instead of ~2.9 on half the matrix cores; MAP 0 (default): F = wavefronts 0-3, B = 4-7, one of
 // each team per SIMD. One window per CU (256 S50 windows): MAP 0 168.0k against MAP 1 161.6k
 // window-it/s (gpurun_out r05f): team B's step work outweighs the chain's slowdown.
-// MAP 2: team F = the chain, its SIMD's other wavefront and one wavefront on each of two further
-// SIMDs; team B = the rest (three SIMDs, none shared with the chain).
+// A third mapping from the SIMD each wavefront landed on (HW_ID), team F = the chain, its SIMD's
+// other wavefront and one wavefront on each of two further SIMDs, team B = the rest (three SIMDs,
+// none shared with the chain), ran 163.0k against 169.5k window-it/s (k_cholesky 0.578 against
+// 0.515 ms, gpurun_out r05m) and was removed.
 #ifndef OKG_PIPE_MAP
 #define OKG_PIPE_MAP 0
 #endif
@@ -113,7 +115,6 @@ struct PipeLds {
   double sz[2 * kTile];       // B: y_k | z_k = X_k^T y_k
   double sRl[kTile];          // F: 1 / L_cc
   int sFl[8];                 // potrfTile's flags [0..3], team F's barrier [4], team B's barrier [5]
-  int simd[8];                // the SIMD of each wavefront (OKG_PIPE_MAP 2)
   int pipe[4];                // [0] steps factored (F), [1] diagonal tiles handed over (B),
                               // [2] the handed-over tile is in sA, [3] failed pivot
 };
@@ -146,54 +147,8 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
   __shared__ PipeLds L;
   extern __shared__ double sxDyn[];  // rhs / y of the whole window
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-#if OKG_PIPE_MAP == 2
-  // roles from the SIMD each wavefront landed on (HW_ID [5:4]): team F = the chain (wavefront 0),
-  // the other wavefront on the chain's SIMD (helper role 3, the lightest) and one wavefront on each
-  // of two further SIMDs (roles 1, 2); team B = the remaining four, so no wavefront of team B shares
-  // the chain's SIMD (one SIMD then hosts two of team B's quarters)
-  if (lane == 0) L.simd[wave] = (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3;
-  __syncthreads();
-  int team = 1, role = 0;
-  {
-    int sid[8];
-#pragma unroll
-    for (int v = 0; v < 8; ++v) sid[v] = __builtin_amdgcn_readfirstlane(L.simd[v]);  // (uniform: scalar)
-    int fRole[8], bRole[8], used = 0, nb = 0;
-#pragma unroll
-    for (int v = 0; v < 8; ++v) fRole[v] = -1;
-    fRole[0] = 0;
-    int mate = -1;  // the other wavefront on the chain's SIMD
-#pragma unroll
-    for (int v = 1; v < 8; ++v)
-      if (mate < 0 && sid[v] == sid[0]) mate = v;
-    if (mate >= 0) fRole[mate] = 3;
-    int nextRole = 1;
-#pragma unroll
-    for (int v = 1; v < 8; ++v) {
-      if (fRole[v] >= 0 || nextRole > (mate >= 0 ? 2 : 3)) continue;
-      if (sid[v] == sid[0] || ((used >> sid[v]) & 1)) continue;  // one helper per further SIMD
-      fRole[v] = nextRole++;
-      used |= 1 << sid[v];
-    }
-#pragma unroll
-    for (int v = 1; v < 8; ++v)  // (a pattern with too few SIMDs: fill team F in wavefront order)
-      if (fRole[v] < 0 && nextRole <= (mate >= 0 ? 2 : 3)) fRole[v] = nextRole++;
-#pragma unroll
-    for (int v = 0; v < 8; ++v) bRole[v] = fRole[v] < 0 ? nb++ : -1;
-#pragma unroll
-    for (int v = 0; v < 8; ++v)
-      if (v == wave) {
-        team = fRole[v] >= 0 ? 0 : 1;
-        role = fRole[v] >= 0 ? fRole[v] : bRole[v];
-      }
-    team = __builtin_amdgcn_readfirstlane(team);
-    role = __builtin_amdgcn_readfirstlane(role);
-  }
-  const int tt = role * 64 + lane;
-#else
   const int team = OKG_PIPE_MAP == 0 ? wave >> 2 : wave & 1;
   const int tt = (OKG_PIPE_MAP == 0 ? (wave & 3) : (wave >> 1)) * 64 + lane;
-#endif
   const int fdim = P.win_fdim[w];
   for (int e = t; e < ld; e += 512) sxDyn[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
   if (t < 8) L.sFl[t] = 0;
@@ -210,7 +165,7 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
       }
       if (tt < kTile) L.sy[tt] = sxDyn[k * kTile + tt];
       if (!potrfTileBody<20>(cur.at(k, k, k), ld, Linv + (int64_t)k * kTile * kTile, nullptr, L.sA, L.sX, L.sy, L.sRl,
-                             L.sFl, tt, inLds, fgen)) {
+                             L.sFl, tt, inLds, fgen, tileBlocks(P, w, k))) {
         if (tt == 0) ldsRelease(&L.pipe[3], 1);
         break;
       }

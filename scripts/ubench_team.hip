@@ -38,7 +38,7 @@ __global__ __launch_bounds__(512, 1) void kteam(const double* A, double* Li, dou
       if (tt < 64) sy[tt] = 1.0 + tt;
       okg::waveBarrier<true>(&sFl[4], gen, 4, lane);
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      okg::potrfTileBody<21>(A, 64, Li + (size_t)blockIdx.x * 4096, nullptr, sA, sX, sy, sRl, sFl, tt, false, gen);
+      okg::potrfTileBody<21>(A, 64, Li + (size_t)blockIdx.x * 4096, nullptr, sA, sX, sy, sRl, sFl, tt, false, gen, 4);
       gen += okg::kPotrfBarriers;
       tot += __builtin_amdgcn_s_memrealtime() - t0;
     }
