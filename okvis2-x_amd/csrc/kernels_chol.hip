@@ -8,8 +8,9 @@
 // tiles (the host's tile-level symbolic factorisation, DevProblem::tile_nz: the reduced camera
 // matrix of a sliding window is block-banded and LLT creates no fill outside its envelope, so
 // skipping zero tiles is exact). Per step k, inside one workgroup:
-//   diagonal  L_kk and X = L_kk^-1 (16-column register panels with v_readlane broadcasts, MFMA
-//             trailing updates, blockwise inverse), fused forward substitution y_k = X rhs_k
+//   diagonal  L_kk and X = L_kk^-1 (8-column sub-panels on one wavefront with a look-ahead, MFMA
+//             trailing updates and X by 16-row block rows on the other three; potrfTile), fused
+//             forward substitution y_k = X rhs_k
 //   panel     L_ik = A_ik X^T for every non-zero tile below (64x64x64 on the FP64 matrix cores)
 //             and rhs_i -= L_ik y_k
 //   update    A_ij -= L_ik L_jk^T for the non-zero tiles of the trailing band (matrix cores;
@@ -37,6 +38,7 @@ namespace okg {
 // Every tile receives its updates in step order in all modes (the left part's steps precede the
 // right part's), each with the same operations, so the split gives the bits of MODE 0 on the same
 // order. A window without a split runs MODE 0 in part 0 of launch A (MODE 2 skips it).
+
 template <int MODE>
 __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem* __restrict__ Pp) {
   const DevProblem& P = *Pp;
