@@ -591,6 +591,96 @@ __device__ __forceinline__ void accSubToLds(double* s, const dbl4 c[2][2], const
         s[(r0 + 16 * a + (lane >> 4) + 4 * reg) * kLd + c0 + 16 * b + (lane & 15)] = c[a][b][reg] - acc[a][b][reg];
 }
 
+// ---- products with structure. Every 16x16 output block below is the MFMA chain of mfmaTileNT
+// (k ascending from acc = +0), cut short only where the remaining steps add exact zeros, so the
+// results are the same bits as the full 64x64x64 product:
+// Panels L_ik = A_ik X^T with X = L_kk^-1 lower triangular (its upper part is exact zeros in sX):
+// block column cb needs k < 16 (cb + 1) only. Wavefront w computes block row w over all four block
+// columns, 4 + 8 + 12 + 16 = 40 MFMAs per wavefront instead of 64 for a 32x32 quarter.
+__device__ __forceinline__ void mfmaPanelRows(const double* sA, const double* sX, dbl4 acc[4], int t) {
+  const int wave = t >> 6, lane = t & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) acc[cb] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kk = 0; kk < kTile; kk += 4) {
+    const double av = sA[(16 * wave + lr) * kLd + kk + lk];
+#pragma unroll
+    for (int cb = kk >> 4; cb < 4; ++cb)
+      acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, sX[(16 * cb + lr) * kLd + kk + lk], acc[cb], 0, 0, 0);
+  }
+}
+// element reg of block cb of mfmaPanelRows' output: row 16 w + (lane >> 4) + 4 reg, column 16 cb + (lane & 15)
+__device__ __forceinline__ void storePanelRows(double* A, int64_t ld, const dbl4 acc[4], int t) {
+  const int wave = t >> 6, lane = t & 63;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg)
+      gmemw(A)[(int64_t)(16 * wave + (lane >> 4) + 4 * reg) * ld + 16 * cb + (lane & 15)] = acc[cb][reg];
+}
+__device__ __forceinline__ void panelRowsToLds(double* s, const dbl4 acc[4], int t) {
+  const int wave = t >> 6, lane = t & 63;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) s[(16 * wave + (lane >> 4) + 4 * reg) * kLd + 16 * cb + (lane & 15)] = acc[cb][reg];
+}
+// Diagonal-tile updates A_ii -= L_ik L_ik^T: symmetric, and only the lower triangle of a diagonal
+// tile is ever read (the factor's sweep, inverse and products read L below the diagonal; what the
+// sweep's lanes above a sub-panel compute from the upper triangle is never stored below it), so only
+// the 10 blocks rb >= cb are formed, dealt 3 / 3 / 2 / 2 over the wavefronts: wavefront 0 (0,0)
+// (1,0) (1,1), 1 (2,0) (2,1) (2,2), 2 (3,0) (3,1), 3 (3,2) (3,3). The upper triangle keeps stale
+// values.
+__device__ __forceinline__ int diagRb(int wave, int e) { return wave == 0 ? (e == 0 ? 0 : 1) : (wave == 1 ? 2 : 3); }
+__device__ __forceinline__ int diagCb(int wave, int e) { return wave == 0 ? (e == 0 ? 0 : e - 1) : (wave == 3 ? 2 + e : e); }
+__device__ __forceinline__ int diagN(int wave) { return wave < 2 ? 3 : 2; }
+__device__ __forceinline__ void mfmaDiagNT(const double* sL, dbl4 acc[3], int t) {
+  const int wave = t >> 6, lane = t & 63;
+  const int lr = lane & 15, lk = lane >> 4;
+  const int n = diagN(wave);
+  int ra[3], rb[3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    ra[e] = (16 * diagRb(wave, e) + lr) * kLd + lk;
+    rb[e] = (16 * diagCb(wave, e) + lr) * kLd + lk;
+    acc[e] = dbl4{0.0, 0.0, 0.0, 0.0};
+  }
+#pragma unroll 4
+  for (int kk = 0; kk < kTile; kk += 4) {
+#pragma unroll
+    for (int e = 0; e < 3; ++e)
+      if (e < n) acc[e] = __builtin_amdgcn_mfma_f64_16x16x4f64(sL[ra[e] + kk], sL[rb[e] + kk], acc[e], 0, 0, 0);
+  }
+}
+__device__ __forceinline__ int64_t diagAt(int wave, int e, int reg, int lane, int64_t ld) {
+  return (int64_t)(16 * diagRb(wave, e) + (lane >> 4) + 4 * reg) * ld + 16 * diagCb(wave, e) + (lane & 15);
+}
+__device__ __forceinline__ void loadCDiag(const double* A, int64_t ld, dbl4 c[3], int t) {
+  const int wave = t >> 6, lane = t & 63, n = diagN(wave);
+#pragma unroll
+  for (int e = 0; e < 3; ++e)
+    if (e < n)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) c[e][reg] = gmem(A)[diagAt(wave, e, reg, lane, ld)];
+}
+__device__ __forceinline__ void storeDiagSub(double* A, int64_t ld, const dbl4 c[3], const dbl4 acc[3], int t) {
+  const int wave = t >> 6, lane = t & 63, n = diagN(wave);
+#pragma unroll
+  for (int e = 0; e < 3; ++e)
+    if (e < n)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) gmemw(A)[diagAt(wave, e, reg, lane, ld)] = c[e][reg] - acc[e][reg];
+}
+__device__ __forceinline__ void diagSubToLds(double* s, const dbl4 c[3], const dbl4 acc[3], int t) {
+  const int wave = t >> 6, lane = t & 63, n = diagN(wave);
+#pragma unroll
+  for (int e = 0; e < 3; ++e)
+    if (e < n)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) s[diagAt(wave, e, reg, lane, kLd)] = c[e][reg] - acc[e][reg];
+}
+
 // z = X^T y_k (X = L_kk^-1 lower in sX, y_k in sy), so that the forward substitution update of
 // every panel is rhs_i -= L_ik y_k = A_ik z. Partials of four row quarters via sP (4 x 64).
 // (Sync: the barrier that orders LDS among the threads running the routine — the workgroup's
@@ -630,8 +720,8 @@ __device__ __forceinline__ void panelTile(const double* Aik, double* Lik, int64_
                           int t, double* defer = nullptr, Sync sync = Sync()) {
   loadTile(Aik, ld, 0, 0, sA, t);
   sync();  // LDS-only: the previous panel's L / rhs stores stay in flight
-  dbl4 acc[2][2];
-  mfmaTileNT(sA, sX, acc, t);
+  dbl4 acc[4];
+  mfmaPanelRows(sA, sX, acc, t);
   {
     const int row = t >> 2, q = t & 3;
     const double a = panelRhsRow(sA, sz, t);
@@ -641,7 +731,7 @@ __device__ __forceinline__ void panelTile(const double* Aik, double* Lik, int64_
     }
   }
   sync();  // sA is free for the next panel
-  storeTile<false>(Lik, ld, 0, 0, acc, t);
+  storePanelRows(Lik, ld, acc, t);
 }
 
 

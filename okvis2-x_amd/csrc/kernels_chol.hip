@@ -84,7 +84,11 @@ __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem
   // instead of 3), and the last update, S_(k+1)(k+1), goes to sA for the next factor instead of
   // through global memory (toLds). Independent tiles, the same operations: the same bits in any
   // order. Returns whether S_(k+1)(k+1) was left in sA.
+  // the thread index, opaque per step (set in the step loop): the step's LDS / global addresses
+  // are formed in the step instead of being hoisted out of the loop and spilled
+  int tStep = t;
   auto bandUpdate = [&](int k, int jLo, bool toLds) {
+    const int t = tStep;
     int xHeld = -1;  // block row of the L tile in sX
     bool inLds = false;
     for (int i = T - 1; i > k && i >= jLo; --i) {
@@ -111,14 +115,21 @@ __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem
         }
         ldsBarrier();
         double* Cij = W + i * kTile * ld + j * kTile;
-        dbl4 c[2][2], acc[2][2];
-        loadC(cur.at(i, j, k), ld, c, t);
-        mfmaTileNT(aBuf, bBuf, acc, t);
-        if (toLds && i == k + 1) {  // (then j == i) the next diagonal tile: c - acc straight into sA
-          ldsBarrier();             // every wavefront has read its operands
-          accSubToLds(sA, c, acc, t);
-          inLds = true;  // its global copy is stale from here on and never read
+        if (j == i) {  // diagonal tile: its lower block triangle only (chol_tiles.hpp)
+          dbl4 c[3], acc[3];
+          loadCDiag(cur.at(i, j, k), ld, c, t);
+          mfmaDiagNT(aBuf, acc, t);
+          if (toLds && i == k + 1) {  // the next diagonal tile: c - acc straight into sA
+            ldsBarrier();             // every wavefront has read its operands
+            diagSubToLds(sA, c, acc, t);
+            inLds = true;  // its global copy is stale from here on and never read
+          } else {
+            storeDiagSub(Cij, ld, c, acc, t);
+          }
         } else {
+          dbl4 c[2][2], acc[2][2];
+          loadC(cur.at(i, j, k), ld, c, t);
+          mfmaTileNT(aBuf, bBuf, acc, t);
           storeTileSub(Cij, ld, c, acc, t);
         }
         ldsBarrier();  // LDS-only: the updated tiles are read from the next step on, after full barriers
@@ -150,12 +161,14 @@ __global__ __launch_bounds__(256, OKG_CHOL_OCC) void k_cholesky(const DevProblem
     }
     if (t < kTile) sxDyn[k * kTile + t] = sy[t];  // y_k (ordered before its readers by the barriers below)
     CLK(0)
+    tStep = t;
+    asm volatile("" : "+v"(tStep));
     // ---- panel: L_ik = A_ik X^T, rhs_i -= L_ik y_k = A_ik X^T y_k (the separator's rows deferred
     // by part 1 of the split)
     panelRhsVector(sX, sy, sy + kTile, sA, t);
     for (int i = k + 1; i < T; ++i)
       if (nz[i * T + k])
-        panelTile(cur.at(i, k, k), W + i * kTile * ld + k * kTile, ld, sxDyn + i * kTile, sA, sX, sy + kTile, t,
+        panelTile(cur.at(i, k, k), W + i * kTile * ld + k * kTile, ld, sxDyn + i * kTile, sA, sX, sy + kTile, tStep,
                   i >= jEnd ? defer + ((size_t)(i - tS) * (tS - tL) + (k - tL)) * kTile : nullptr);
     __syncthreads();  // full barrier: the band update reads the L_ik just stored
     CLK(1)
@@ -254,9 +267,9 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(const DevProblem* __rest
     // rhs_i -= L_ik y_k, formed as A_ik z with z = X_k^T y_k from the A_ik tile in LDS (the same
     // operations as panelTile, so all schedules give the same bits)
     if (i == j) panelRhsVector(sX, sy, sy + kTile, sB, t);
-    dbl4 li[2][2], lj[2][2];
-    mfmaTileNT(sA, sX, li, t);
-    if (j != i) mfmaTileNT(sB, sX, lj, t);
+    dbl4 li[4], lj[4];
+    mfmaPanelRows(sA, sX, li, t);
+    if (j != i) mfmaPanelRows(sB, sX, lj, t);
     if (i == j) {
       const double a = panelRhsRow(sA, sy + kTile, t);
       if (q == 0) {
@@ -266,31 +279,32 @@ __global__ __launch_bounds__(256, 2) void k_chol_update(const DevProblem* __rest
       }
     }
     ldsBarrier();  // every wavefront has read A_ik / A_jk (LDS-only: the rhs store stays in flight)
-    accToLds(sA, li, t);
-    if (j != i) accToLds(sB, lj, t);
+    panelRowsToLds(sA, li, t);
+    if (j != i) panelRowsToLds(sB, lj, t);
     double* Cij = W + i * kTile * ld + j * kTile;
-    dbl4 c[2][2];
-    loadC(cur.at(i, j, k), ld, c, t);  // read of the read-modify-write overlaps the barrier and the MFMAs
-    if (i == j) storeTile<false>(W + k * kTile * ld + i * kTile, ld, 0, 0, li, t);  // L_ik -> upper slot (k,i)
-    ldsBarrier();  // no reader of the upper slot in this launch
-    dbl4 acc[2][2];
-    mfmaTileNT(sA, j == i ? sA : sB, acc, t);
-    if (mode & 2) {
-      // tile (i,i) after its last update: straight to LDS for the factor (its global copy is stale
-      // from here on and never read), and so is rhs_i
-      ldsBarrier();  // every wavefront has read L_ik from sA
-      const int wave = t >> 6, lane = t & 63;
-      const int r0 = 32 * (wave >> 1), cq = 32 * (wave & 1);
-#pragma unroll
-      for (int a2 = 0; a2 < 2; ++a2)
-#pragma unroll
-        for (int b2 = 0; b2 < 2; ++b2)
-#pragma unroll
-          for (int reg = 0; reg < 4; ++reg)
-            sA[(r0 + 16 * a2 + (lane >> 4) + 4 * reg) * kLd + cq + 16 * b2 + (lane & 15)] = c[a2][b2][reg] - acc[a2][b2][reg];
-      __syncthreads();
-      if (t < kTile) sy[t] = sRl[t];
+    if (i == j) {  // diagonal tile: its lower block triangle only (chol_tiles.hpp)
+      dbl4 c[3];
+      loadCDiag(cur.at(i, j, k), ld, c, t);  // read of the read-modify-write overlaps the barrier and the MFMAs
+      storePanelRows(W + k * kTile * ld + i * kTile, ld, li, t);  // L_ik -> upper slot (k,i)
+      ldsBarrier();  // no reader of the upper slot in this launch
+      dbl4 acc[3];
+      mfmaDiagNT(sA, acc, t);
+      if (mode & 2) {
+        // tile (i,i) after its last update: straight to LDS for the factor (its global copy is stale
+        // from here on and never read), and so is rhs_i
+        ldsBarrier();  // every wavefront has read L_ik from sA
+        diagSubToLds(sA, c, acc, t);
+        __syncthreads();
+        if (t < kTile) sy[t] = sRl[t];
+      } else {
+        storeDiagSub(Cij, ld, c, acc, t);
+      }
     } else {
+      dbl4 c[2][2];
+      loadC(cur.at(i, j, k), ld, c, t);
+      ldsBarrier();
+      dbl4 acc[2][2];
+      mfmaTileNT(sA, sB, acc, t);
       storeTileSub(Cij, ld, c, acc, t);
     }
   }

@@ -45,8 +45,26 @@ __device__ __forceinline__ void loadXFrag(const double* sX, double (&xf)[16][2],
 #pragma unroll
     for (int b = 0; b < 2; ++b) xf[q][b] = sX[(c0 + 16 * b + lr) * kLd + 4 * q + lk];
 }
-// acc = sA X^T with X^T's fragments in registers: the MFMA sequence of mfmaTileNT(sA, sX), so the
-// same bits.
+// acc = sA X^T with X^T's fragments in registers: the MFMA sequence of mfmaTileNT(sA, sX), cut
+// where X's upper triangle (exact zeros) would only add zeros (block column cb needs k < 16 (cb + 1):
+// mfmaPanelRows in chol_tiles.hpp), so the same bits: 24 MFMAs on the wavefronts of block columns
+// 0-1, 56 on those of 2-3, instead of 64.
+template <int HALF>
+__device__ __forceinline__ void mfmaTileNTXHalf(const double* sA, const double (&xf)[16][2], dbl4 acc[2][2], int r0,
+                                                int lr, int lk) {
+#pragma unroll
+  for (int q = 0; q < 8 + 8 * HALF; ++q) {
+    double av[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) av[a] = sA[(r0 + 16 * a + lr) * kLd + 4 * q + lk];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        if (q < 4 * (2 * HALF + b + 1))  // (block column 2 HALF + b)
+          acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], xf[q][b], acc[a][b], 0, 0, 0);
+  }
+}
 __device__ __forceinline__ void mfmaTileNTX(const double* sA, const double (&xf)[16][2], dbl4 acc[2][2], int t) {
   const int wave = t >> 6, lane = t & 63;
   const int r0 = 32 * (wave >> 1);
@@ -55,16 +73,8 @@ __device__ __forceinline__ void mfmaTileNTX(const double* sA, const double (&xf)
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    double av[2];
-#pragma unroll
-    for (int a = 0; a < 2; ++a) av[a] = sA[(r0 + 16 * a + lr) * kLd + 4 * q + lk];
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[a], xf[q][b], acc[a][b], 0, 0, 0);
-  }
+  if (wave & 1) mfmaTileNTXHalf<1>(sA, xf, acc, r0, lr, lk);
+  else mfmaTileNTXHalf<0>(sA, xf, acc, r0, lr, lk);
 }
 
 // Panel of team B: L_ik = A_ik X^T (A_ik staged in sBuf), rhs_i -= A_ik z (panelTile's
@@ -208,10 +218,10 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
         pipePanel(cur.at(k + 1, k, k), W + (int64_t)(k + 1) * kTile * ld + k * kTile, ld, sxDyn + (k + 1) * kTile,
                   L.sB[0], xf, L.sz + kTile, tt, bsyncL);
         held[0] = k + 1;
-        dbl4 c[2][2], acc[2][2];
-        loadC(cur.at(k + 1, k + 1, k), ld, c, tt);
-        mfmaTileNT(L.sB[0], L.sB[0], acc, tt);
-        accSubToLds(L.sA, c, acc, tt);
+        dbl4 c[3], acc[3];  // (a diagonal tile: its lower block triangle, chol_tiles.hpp)
+        loadCDiag(cur.at(k + 1, k + 1, k), ld, c, tt);
+        mfmaDiagNT(L.sB[0], acc, tt);
+        diagSubToLds(L.sA, c, acc, tt);
         bsyncL();
       }
       if (tt == 0) {
@@ -254,10 +264,17 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
             loaded = true;
           }
           if (loaded) bsyncL();
-          dbl4 c[2][2], acc[2][2];
-          loadC(cur.at(i, j, k), ld, c, tt);
-          mfmaTileNT(L.sB[bi], L.sB[bj], acc, tt);
-          storeTileSub(W + (int64_t)i * kTile * ld + j * kTile, ld, c, acc, tt);
+          if (j == i) {
+            dbl4 c[3], acc[3];
+            loadCDiag(cur.at(i, j, k), ld, c, tt);
+            mfmaDiagNT(L.sB[bi], acc, tt);
+            storeDiagSub(W + (int64_t)i * kTile * ld + j * kTile, ld, c, acc, tt);
+          } else {
+            dbl4 c[2][2], acc[2][2];
+            loadC(cur.at(i, j, k), ld, c, tt);
+            mfmaTileNT(L.sB[bi], L.sB[bj], acc, tt);
+            storeTileSub(W + (int64_t)i * kTile * ld + j * kTile, ld, c, acc, tt);
+          }
           bsyncL();  // the operands may be replaced next
         }
       }
