@@ -779,7 +779,7 @@ __device__ __forceinline__ void asmPairsHeavy(const DevProblem& P, int bid) {
   const int lane = threadIdx.x & 63;
   const int item = bid * 4 + (threadIdx.x >> 6);
   if (item >= P.n_asm_pp) return;
-  const int k = gmem(P.asm_pp_items)[item];
+  const int k = __builtin_amdgcn_readfirstlane(gmem(P.asm_pp_items)[item]);  // (wave-uniform: scalar loads)
   if (k < 0) return;
   // the pair record in one round of loads; then the window state, the first round of descriptors
   // and the block offsets in the next, all consumed (empty asm) before the window test, so no load
@@ -1012,14 +1012,31 @@ __device__ __forceinline__ void asmPairsLight(const DevProblem& P, int bid) {
 __global__ __launch_bounds__(256) void k_assemble_pp_light(const DevProblem* __restrict__ Pp) { asmPairsLight(*Pp, (int)blockIdx.x); }
 
 // k_assemble_sb: pairs with a speed/bias block (6x9, 9x9): few contributions (IMU factors,
-// speed/bias priors), one entry per lane.
+// speed/bias priors), one entry per lane. The first kSbPre contribution descriptors are loaded with
+// the pair record (before the window test), and the IMU entries of a pair's contributions are
+// loaded together before they are summed in contribution order (the same sums): a pair costs one
+// dependent global load per level instead of two per contribution.
+constexpr int kSbPre = 4;
+__device__ __forceinline__ double sbPriorTerm(const DevProblem& P, const Contrib& C, int lb, int r, int q) {
+  if (C.type == C_SBPRIOR) {
+    const double* L = P.sbp_lin[lb] + 90 * (size_t)C.a + 9;
+    double s2 = 0;
+    for (int k2 = 0; k2 < 9; ++k2) s2 += L[k2 * 9 + r] * L[k2 * 9 + q];
+    return s2;
+  }
+  const double* L = P.pp_lin[lb] + 42 * (size_t)C.a + 6;  // C_PPRIOR
+  double s2 = 0;
+  for (int k2 = 0; k2 < 6; ++k2) s2 += L[k2 * 6 + r] * L[k2 * 6 + q];
+  return s2;
+}
 __device__ __forceinline__ void asmPairsSb(const DevProblem& P, int bid) {
   const int lane = threadIdx.x & 63;
   const int item = bid * 4 + (threadIdx.x >> 6);
   if (item >= P.n_asm_sb) return;
-  const int k = gmem(P.asm_sb_items)[item];
-  // the pair record, then the window state and the block offsets, consumed (empty asm) before the
-  // window test so that no load is sunk behind it
+  // (wave-uniform from here: the pair record and its descriptors go to scalar registers)
+  const int k = __builtin_amdgcn_readfirstlane(gmem(P.asm_sb_items)[item]);
+  // the pair record, then the window state, the block offsets and the first contribution
+  // descriptors, consumed (empty asm) before the window test so that no load is sunk behind it
   const int w = gmem(P.pair_win)[k], fi = gmem(P.pair_fi)[k], fj = gmem(P.pair_fj)[k];
   const int cb = gmem(P.pair_cbegin)[k], ce = gmem(P.pair_cbegin)[k + 1];
   const auto gst = gmem(P.st + w);
@@ -1029,33 +1046,38 @@ __device__ __forceinline__ void asmPairsSb(const DevProblem& P, int bid) {
   const int offi = gmem(P.fb_off)[fi], offj = gmem(P.fb_off)[fj];
   const int foff = gmem(P.win_foff)[w], ld = gmem(P.win_fpad)[w];
   const int64_t soff = gmem(P.win_soff)[w];
+  const int nc = ce - cb;
+  Contrib Cs[kSbPre];
+#pragma unroll
+  for (int u = 0; u < kSbPre; ++u) Cs[u] = gmem(P.pair_contrib)[cb + min(u, max(nc - 1, 0))];
   asm volatile("" ::"v"(ki), "v"(kj), "v"(offi), "v"(offj), "v"(foff), "v"(ld), "v"(soff), "v"(cb), "v"(ce),
-               "v"(lb), "v"(sMu));
+               "v"(lb), "v"(sMu), "v"(Cs[0].a), "v"(Cs[kSbPre - 1].a));
   if ((sDone != 0) | (sNeed == 0) | (sFail != 0)) return;  // gnSelect
   const int ni = ki == 0 ? 6 : 9, nj = kj == 0 ? 6 : 9;
   const bool diag = fi == fj;
   double* S = P.S + soff;
   const double smu = sqrt(sMu);
+  const auto imuH = gmem(P.imu_H);
   for (int e = lane; e < ni * nj; e += 64) {
     const int r = e / nj, q = e - r * nj;
+    const double si = P.sF[(size_t)foff + offi + r], sj = P.sF[(size_t)foff + offj + q];
     double H = 0.0;
-    for (int c = cb; c < ce; ++c) {
-      const Contrib C = P.pair_contrib[c];
-      if (C.type == C_IMU) {
-        H += P.imu_H[(size_t)C.a * kImuHess + sym30(C.b + r, C.c + q)];
-      } else if (C.type == C_SBPRIOR) {
-        const double* L = P.sbp_lin[lb] + 90 * (size_t)C.a + 9;
-        double s2 = 0;
-        for (int k2 = 0; k2 < 9; ++k2) s2 += L[k2 * 9 + r] * L[k2 * 9 + q];
-        H += s2;
-      } else if (C.type == C_PPRIOR) {
-        const double* L = P.pp_lin[lb] + 42 * (size_t)C.a + 6;
-        double s2 = 0;
-        for (int k2 = 0; k2 < 6; ++k2) s2 += L[k2 * 6 + r] * L[k2 * 6 + q];
-        H += s2;
+    if (nc <= kSbPre) {
+      double v[kSbPre];
+#pragma unroll
+      for (int u = 0; u < kSbPre; ++u) {
+        const Contrib& C = Cs[u];
+        v[u] = C.type == C_IMU ? imuH[(size_t)C.a * kImuHess + sym30(C.b + r, C.c + q)] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < kSbPre; ++u)
+        if (u < nc) H += Cs[u].type == C_IMU ? v[u] : sbPriorTerm(P, Cs[u], lb, r, q);
+    } else {
+      for (int c = cb; c < ce; ++c) {
+        const Contrib C = P.pair_contrib[c];
+        H += C.type == C_IMU ? P.imu_H[(size_t)C.a * kImuHess + sym30(C.b + r, C.c + q)] : sbPriorTerm(P, C, lb, r, q);
       }
     }
-    const double si = P.sF[(size_t)foff + offi + r], sj = P.sF[(size_t)foff + offj + q];
     double val = si * sj * H;
     if (diag && r == q) {
       const size_t idx = (size_t)foff + offi + r;
