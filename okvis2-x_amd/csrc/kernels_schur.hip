@@ -936,10 +936,16 @@ __device__ __forceinline__ void asmPairsLight(const DevProblem& P, int bid) {
   const auto gst = gmem(P.st + w);
   const int sDone = gst->done, sNeed = gst->need_gn, sFail = gst->gn_failed, lb = gst->lcur;
   const int g = sub / 6, r = sub - 6 * (sub / 6);
-  const int cFirst = min(pb + g, max(ce - 1, pb));
+  // the group's first factor-block descriptor and its first round of partial-block descriptors,
+  // loaded with the window state (before the test: one level of dependent loads fewer per pair)
+  const int cFirst = min(ob + g, max(ce - 1, pb));
   const Contrib C0 = pc[cFirst];
+  int ai0[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) ai0[u] = pc[max(min(pb + g + u * kPplGroups, ob - 1), 0)].a;
   const int foff = gmem(P.win_foff)[w], offi = gmem(P.fb_off)[fi], offj = gmem(P.fb_off)[fj];
-  asm volatile("" ::"v"(C0.type), "v"(C0.a), "v"(C0.b), "v"(C0.c), "v"(foff), "v"(offi), "v"(offj), "v"(lb));
+  asm volatile("" ::"v"(C0.type), "v"(C0.a), "v"(C0.b), "v"(C0.c), "v"(foff), "v"(offi), "v"(offj), "v"(lb),
+               "v"(ai0[0]), "v"(ai0[1]), "v"(ai0[2]), "v"(ai0[3]));
   const bool live = has & (sDone == 0) & (sNeed != 0) & (sFail == 0);  // gnSelect
   if (!__any(live)) return;
   const int g0 = (live && g < kPplGroups) ? g : 1 << 29;  // lanes 12..15 of a quarter idle
@@ -952,7 +958,7 @@ __device__ __forceinline__ void asmPairsLight(const DevProblem& P, int bid) {
   for (int c = pb + g0; c < ob; c += 4 * kPplGroups) {
     int ai[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) ai[u] = pc[min(c + u * kPplGroups, ob - 1)].a;
+    for (int u = 0; u < 4; ++u) ai[u] = c == pb + g ? ai0[u] : pc[min(c + u * kPplGroups, ob - 1)].a;
     double2 v[4][3];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
