@@ -613,9 +613,14 @@ __device__ __forceinline__ void imuHessBlock(const DevProblem& P, int bid, int l
   for (int e = lane; e < kImuHess; e += 64) {
     double acc = 0.0;
     if (e < 465) {
-      int a = 0, rem = e;
-      while (rem >= 30 - a) { rem -= 30 - a; ++a; }
-      const int b = a + rem;
+      // row a of the packed upper triangle: start(a) = 30 a - a (a - 1) / 2 <= e < start(a + 1),
+      // from the root of the quadratic and one exact integer correction each way (no per-lane
+      // loop: lanes with different rows diverged over up to 30 iterations)
+      int a = (int)((61.0f - sqrtf(3721.0f - 8.0f * (float)e)) * 0.5f);
+      a = max(0, min(a, 29));
+      if (30 * a - (a * (a - 1)) / 2 > e) --a;
+      if (30 * (a + 1) - ((a + 1) * a) / 2 <= e) ++a;
+      const int b = a + (e - (30 * a - (a * (a - 1)) / 2));
       for (int k = 0; k < 15; ++k) acc += J[15 + k * 30 + a] * J[15 + k * 30 + b];
     } else {
       const int a = e - 465;
