@@ -106,16 +106,14 @@ __device__ void finalizeIteration(const DevProblem& P, WinState& s) {
 // J*v reductions of window w (once per GN step): jcc, jgg, jcg and the Cauchy alpha =
 // |gradient_|^2 / jcc, stored by thread 0 in the window state; every thread gets alpha.
 // Reprojection rows and landmark gradients come as the landmark groups' sums (k_lm_backsub_jv).
-template <int RB>
-__device__ double reduceJv(const DevProblem& P, int w, WinState& s, double* sh) {
-  const int t = threadIdx.x;
+// (this thread's partial sums of jcc, jgg, jcg: reduceJv and the merged reduction of k_dogleg)
+__device__ __forceinline__ void jvPartials(const DevProblem& P, int w, int t, int RB, double (&a)[3]) {
   const int ib = P.win_imu_range[2 * w], ie = P.win_imu_range[2 * w + 1];
   const int hb = P.win_host_range[2 * w], he = P.win_host_range[2 * w + 1];
   const int pb = P.win_pp_range[2 * w], pe = P.win_pp_range[2 * w + 1];
   const int sbb = P.win_sbp_range[2 * w], sbe = P.win_sbp_range[2 * w + 1];
   const int rpb = P.win_rp_range[2 * w], rpe = P.win_rp_range[2 * w + 1];
   const int gb = P.win_lmg_range[2 * w], ge = P.win_lmg_range[2 * w + 1];
-  double a[3];
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     double acc = 0.0;
@@ -127,6 +125,14 @@ __device__ double reduceJv(const DevProblem& P, int w, WinState& s, double* sh) 
     for (int i = rpb + t; i < rpe; i += RB) acc += P.rp_jv[(size_t)k * P.n_relpose + i];
     a[k] = acc;
   }
+}
+
+template <int RB>
+__device__ double reduceJv(const DevProblem& P, int w, WinState& s, double* sh) {
+  const int t = threadIdx.x;
+  const int gb = P.win_lmg_range[2 * w], ge = P.win_lmg_range[2 * w + 1];
+  double a[3];
+  jvPartials(P, w, t, RB, a);
   blockSumN<RB, 3>(a, sh);
   // |gradient_|^2 over the window (f-vector + free landmarks)
   double g2 = 0.0;
@@ -349,7 +355,7 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
   const int w = blockIdx.x;
   WinState& s = P.st[w];
   if (s.done) return;
-  __shared__ double sh[3 * RB];
+  __shared__ double sh[6 * RB];
   __shared__ int sflag;
   const int t = threadIdx.x;
   const bool sflagGn = s.need_gn && !s.gn_failed;  // (read before thread 0 updates the state)
@@ -386,10 +392,6 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
   }
   __syncthreads();
   if (sflag) return;
-  // a new GN step: its J*v reduction first (formerly k_reduce R_JV, one launch fewer per
-  // iteration; the same workgroup per window, so a barrier orders it)
-  double alpha = s.alpha;
-  if (sflagGn) alpha = reduceJv<RB>(P, w, s, sh);
   const int foff = P.win_foff[w], fd = P.win_fdim[w];
   const int l0 = P.win_lm_range[2 * w], l1 = P.win_lm_range[2 * w + 1];
   // pass 1: norms (f-blocks here, landmarks as the landmark groups' sums of k_lm_backsub_jv)
@@ -407,7 +409,27 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
     nn += r[4];
     gn += r[5];
   }
-  {
+  // a new GN step also needs its J*v forms (formerly k_reduce R_JV) and alpha = |gradient_|^2 /
+  // jcc: reduced in the same tree as the norms (|gradient_|^2 is gg, the same per-thread order as
+  // reduceJv's), one tree instead of three, each value with the same additions (same bits)
+  double alpha = s.alpha;
+  if (sflagGn) {
+    double r6[6];
+    double a3[3];
+    jvPartials(P, w, t, RB, a3);
+    r6[0] = a3[0]; r6[1] = a3[1]; r6[2] = a3[2]; r6[3] = gg; r6[4] = nn; r6[5] = gn;
+    blockSumN<RB, 6>(r6, sh);
+    gg = r6[3];
+    nn = r6[4];
+    gn = r6[5];
+    alpha = gg / r6[0];
+    if (t == 0) {
+      s.jcc = r6[0];
+      s.jgg = r6[1];
+      s.jcg = r6[2];
+      s.alpha = alpha;
+    }
+  } else {
     double r3[3] = {gg, nn, gn};
     blockSumN<RB, 3>(r3, sh);
     gg = r3[0];
