@@ -81,11 +81,12 @@ __device__ __forceinline__ void mfmaTileNTX(const double* sA, const double (&xf)
 // operations), L_ik stored to W and left in sBuf for the step's band updates.
 // (defer: the split schedule's right part stores the rhs term of a separator row instead, for the
 // separator's launch to subtract in step order)
+// (staged: A_ik is in sBuf already, prefetched by the previous step)
 template <class Sync>
 __device__ __forceinline__ void pipePanel(const double* Aik, double* Lik, int64_t ld, double* worki, double* sBuf,
                                           const double (&xf)[16][2], const double* sz, int t, Sync sync,
-                                          double* defer = nullptr) {
-  loadTile(Aik, ld, 0, 0, sBuf, t);
+                                          double* defer = nullptr, bool staged = false) {
+  if (!staged) loadTile(Aik, ld, 0, 0, sBuf, t);
   sync();
   dbl4 acc[2][2];
   mfmaTileNTX(sBuf, xf, acc, t);
@@ -190,6 +191,7 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
     const TeamSync<false> bsync{&L.sFl[5], &bgen, lane};
     const TeamSync<true> bsyncL{&L.sFl[5], &bgen, lane};
     double xf[16][2];
+    int staged = -1;  // the step whose critical A_(k+1)k is in sB[0] (prefetched at the previous step's end)
     for (int k = k0; k < k1; ++k) {
       if (!waitFlag<false>(&L.pipe[0], k + 1, &L.pipe[3])) break;
       bool below = false;  // (a step without tiles below only hands the next tile over)
@@ -209,14 +211,14 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
       // handed over below)
       if (tt < kTile) L.sz[tt] = sxDyn[k * kTile + tt];
       bsyncL();
-      panelRhsVector(L.sX, L.sz, L.sz + kTile, L.sB[0], tt, bsyncL);
+      panelRhsVector(L.sX, L.sz, L.sz + kTile, L.sB[1], tt, bsyncL);  // (scratch: sB[0] may hold A staged)
       loadXFrag(L.sX, xf, tt);
       int held[2] = {-1, -1};  // block row i of the L_ik in sB[0] / sB[1]
       const bool crit = k + 1 < k1 && nz[(k + 1) * T + k] != 0;
       if (crit) {
         // the critical path: panel (k+1, k), then its update of tile (k+1, k+1) into team F's sA
         pipePanel(cur.at(k + 1, k, k), W + (int64_t)(k + 1) * kTile * ld + k * kTile, ld, sxDyn + (k + 1) * kTile,
-                  L.sB[0], xf, L.sz + kTile, tt, bsyncL);
+                  L.sB[0], xf, L.sz + kTile, tt, bsyncL, nullptr, staged == k);
         held[0] = k + 1;
         dbl4 c[3], acc[3];  // (a diagonal tile: its lower block triangle, chol_tiles.hpp)
         loadCDiag(cur.at(k + 1, k + 1, k), ld, c, tt);
@@ -279,6 +281,13 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
         }
       }
       bsync();  // the updated tiles in W for the next step's panels
+      // the next step's critical A_(k+2)(k+1) has all its updates now: into sB[0] while team F
+      // factors tile k+1 (one global round trip off the next step's critical path; the panel's
+      // first team barrier orders these LDS writes before its reads)
+      if (k + 2 < k1 && nz[(k + 2) * T + k + 1]) {
+        loadTile(cur.at(k + 2, k + 1, k + 1), ld, 0, 0, L.sB[0], tt);
+        staged = k + 1;
+      }
     }
   }
   __syncthreads();
