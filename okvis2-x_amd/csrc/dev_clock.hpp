@@ -105,3 +105,26 @@ static __device__ unsigned int g_lmvDone;
 #define LCLK_END
 #define LCLK_TAIL(i)
 #endif
+
+// ---- k_cholesky_pipe (-DOKG_PIPE_CLOCK): workgroup 0, one thread per team (t 0: team F, t 256:
+// team B) accumulates s_memrealtime ticks (100 MHz) per phase; printed at the kernel's end.
+#ifdef OKG_PIPE_CLOCK
+static __device__ unsigned long long g_pipeClk[16];
+#define PCLK_INIT unsigned long long pclk = __builtin_amdgcn_s_memrealtime();
+#define PCLK(i, tid)                                                            \
+  if (blockIdx.x == 0 && threadIdx.x == (tid)) {                                \
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();            \
+    g_pipeClk[i] += now - pclk;                                                 \
+    pclk = now;                                                                 \
+  }
+#define PCLK_REPORT(T)                                                                                   \
+  if (blockIdx.x == 0 && threadIdx.x == 0)                                                               \
+    printf("PIPECLK T=%d F: wait %llu potrf %llu | B: waitX %llu prep %llu crit %llu panels %llu "       \
+           "updates %llu prefetch %llu | F tail %llu bsub %llu (x10ns)\n",                              \
+           (T), g_pipeClk[0], g_pipeClk[1], g_pipeClk[2], g_pipeClk[3], g_pipeClk[4], g_pipeClk[5],       \
+           g_pipeClk[6], g_pipeClk[7], g_pipeClk[9], g_pipeClk[8]);
+#else
+#define PCLK_INIT
+#define PCLK(i, tid)
+#define PCLK_REPORT(T)
+#endif

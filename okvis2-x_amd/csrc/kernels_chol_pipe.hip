@@ -165,6 +165,7 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
   if (t < 8) L.sFl[t] = 0;
   if (t < 4) L.pipe[t] = 0;
   __syncthreads();
+  PCLK_INIT
   if (team == 0) {
     // ---- team F: the diagonal tiles in order
     int fgen = 0;
@@ -174,6 +175,7 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
         if (!waitFlag<false>(&L.pipe[1], k, &L.pipe[3])) break;
         inLds = L.pipe[2] != 0;
       }
+      PCLK(0, 0)
       if (tt < kTile) L.sy[tt] = sxDyn[k * kTile + tt];
       if (!potrfTileBody<20>(cur.at(k, k, k), ld, Linv + (int64_t)k * kTile * kTile, nullptr, L.sA, L.sX, L.sy, L.sRl,
                              L.sFl, tt, inLds, fgen, tileBlocks(P, w, k))) {
@@ -183,6 +185,7 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
       fgen += kPotrfBarriers;
       if (tt < kTile) sxDyn[k * kTile + tt] = L.sy[tt];  // y_k
       if (tt == 0) ldsRelease(&L.pipe[0], k + 1);         // X_k in sX, y_k in sxDyn
+      PCLK(1, 0)
     }
   } else {
     // ---- team B: the panels and band updates of step k once X_k is there
@@ -193,7 +196,9 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
     double xf[16][2];
     int staged = -1;  // the step whose critical A_(k+1)k is in sB[0] (prefetched at the previous step's end)
     for (int k = k0; k < k1; ++k) {
+      PCLK(6, 256)
       if (!waitFlag<false>(&L.pipe[0], k + 1, &L.pipe[3])) break;
+      PCLK(2, 256)
       bool below = false;  // (a step without tiles below only hands the next tile over)
       for (int i = k + 1; i < T; ++i) below = below || nz[i * T + k];
       if (!below) {
@@ -213,6 +218,7 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
       bsyncL();
       panelRhsVector(L.sX, L.sz, L.sz + kTile, L.sB[1], tt, bsyncL);  // (scratch: sB[0] may hold A staged)
       loadXFrag(L.sX, xf, tt);
+      PCLK(3, 256)
       int held[2] = {-1, -1};  // block row i of the L_ik in sB[0] / sB[1]
       const bool crit = k + 1 < k1 && nz[(k + 1) * T + k] != 0;
       if (crit) {
@@ -230,6 +236,7 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
         L.pipe[2] = crit ? 1 : 0;
         ldsRelease(&L.pipe[1], k + 1);
       }
+      PCLK(4, 256)
       // the step's other panels (the last ones stay in LDS for the updates)
       int hb = crit ? 1 : 0;
       // (without the critical pair this includes row k+1: at the end of a part of a split window,
@@ -242,6 +249,7 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
         if (!crit) hb ^= 1;
       }
       bsync();  // the L tiles in W for reloads by other wavefronts of the team
+      PCLK(5, 256)
       // band updates A_ij -= L_ik L_jk^T of step k but (k+1, k+1), bottom-up
       for (int i = T - 1; i > k; --i) {
         if (!nz[i * T + k]) continue;
@@ -288,6 +296,7 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
         loadTile(cur.at(k + 2, k + 1, k + 1), ld, 0, 0, L.sB[0], tt);
         staged = k + 1;
       }
+      PCLK(7, 256)
     }
   }
   __syncthreads();
@@ -302,7 +311,10 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
       if ((e >= e0 && e < e1) || (part == 0 && e >= tS * kTile)) work[e] = sxDyn[e];
     return;
   }
+  PCLK(9, 0)
   backSubstitute<512>(P, w, W, ld, T, Linv, nz, sxDyn, L.sB[0], L.sy, t);
+  PCLK(8, 0)
+  PCLK_REPORT(T)
 }
 
 bool cholesky_pipe_fits(int max_fpad, size_t lds_per_block) {
