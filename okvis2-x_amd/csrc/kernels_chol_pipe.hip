@@ -3,17 +3,20 @@
 // teams of four wavefronts that work on consecutive steps of the right-looking factorisation.
 //
 //   team F (wavefronts 0-3): the diagonal tiles, potrfTile (L_kk, X_k = L_kk^-1, y_k = X_k rhs_k),
-//            one after the other;
-//   team B (wavefronts 4-7): step k's panels L_ik = A_ik X_k^T with rhs_i -= A_ik X_k^T y_k and band
-//            updates A_ij -= L_ik L_jk^T, on the FP64 matrix cores.
+//            one after the other, each followed by the step's critical pair: the panel L_(k+1)k
+//            (X_k still in LDS) and its update of tile (k+1, k+1), which stays in LDS for the next
+//            factor;
+//   team B (wavefronts 4-7): step k's other panels L_ik = A_ik X_k^T with rhs_i -= A_ik X_k^T y_k
+//            and band updates A_ij -= L_ik L_jk^T, on the FP64 matrix cores.
 //
 // The persistent kernel (k_cholesky<0>) runs the three phases of a step one after the other with
 // the whole workgroup, so while wavefront 0 walks the diagonal tile's latency chain the matrix cores
 // wait. Here team B takes X_k (into registers, in MFMA fragment order) as soon as team F has it and
-// first runs the two products on the critical path — the panel L_(k+1)k and its update of the next
-// diagonal tile, which it writes straight into team F's LDS tile — then hands tile k+1 to team F
-// and runs the step's other panels and updates while team F factors it. The step time becomes
-// factor + one panel + one update instead of factor + every panel and update of the step.
+// runs the step's other panels and updates (row k+2 first: the next critical pair reads it) while
+// team F forms the critical pair and factors tile k+1. The step time becomes factor + one panel +
+// one update instead of factor + every panel and update of the step. (Until round 5 team B formed
+// the critical pair and handed the tile over; the team-F form is 3 % faster at one window per CU,
+// gpurun_out r05ag: team B no longer waits with its own step's work queued behind the pair.)
 //
 // The tile operations are those of the other schedules (chol_tiles.hpp: the same routines, the same
 // operands, each tile's updates in step order), so the factorisation gives their bits. The teams
@@ -81,12 +84,11 @@ __device__ __forceinline__ void mfmaTileNTX(const double* sA, const double (&xf)
 // operations), L_ik stored to W and left in sBuf for the step's band updates.
 // (defer: the split schedule's right part stores the rhs term of a separator row instead, for the
 // separator's launch to subtract in step order)
-// (staged: A_ik is in sBuf already, prefetched by the previous step)
 template <class Sync>
 __device__ __forceinline__ void pipePanel(const double* Aik, double* Lik, int64_t ld, double* worki, double* sBuf,
                                           const double (&xf)[16][2], const double* sz, int t, Sync sync,
-                                          double* defer = nullptr, bool staged = false) {
-  if (!staged) loadTile(Aik, ld, 0, 0, sBuf, t);
+                                          double* defer = nullptr) {
+  loadTile(Aik, ld, 0, 0, sBuf, t);
   sync();
   dbl4 acc[2][2];
   mfmaTileNTX(sBuf, xf, acc, t);
@@ -116,18 +118,31 @@ __device__ __forceinline__ void pipePanel(const double* Aik, double* Lik, int64_
 #ifndef OKG_PIPE_MAP
 #define OKG_PIPE_MAP 0
 #endif
+// The teams' waits on each other, with a spin limit no correct run reaches (~1 s): a wait that
+// never ends reports a failed factorisation (the window's GN step is retried) instead of hanging
+// the device.
+__device__ __forceinline__ bool pipeWait(int* p, int v, int* fail) {
+  for (int it = 0; it < (1 << 24); ++it) {
+    if (ldsAcquire(p) >= v) return true;
+    if (ldsAcquire(fail)) return false;
+    __builtin_amdgcn_s_sleep(OKG_WAIT_SLEEP);
+  }
+  if ((threadIdx.x & 63) == 0) ldsRelease(fail, 1);
+  return false;
+}
 
 // LDS of the pipelined kernel besides the window's rhs / y (dynamic, ld doubles)
 struct PipeLds {
-  double sA[kTile * kLd];     // F: the diagonal tile being factored (team B writes the next one here)
+  double sA[kTile * kLd];     // F: the diagonal tile being factored, then the critical pair's operands
   double sX[kTile * kLd];     // F: X_k
   double sB[2][kTile * kLd];  // B: A_ik staging / the step's L tiles
   double sy[2 * kTile];       // F: rhs_k -> y_k | scratch (backward substitution: y_I)
   double sz[2 * kTile];       // B: y_k | z_k = X_k^T y_k
   double sRl[kTile];          // F: 1 / L_cc
   int sFl[8];                 // potrfTile's flags [0..3], team F's barrier [4], team B's barrier [5]
-  int pipe[4];                // [0] steps factored (F), [1] diagonal tiles handed over (B),
-                              // [2] the handed-over tile is in sA, [3] failed pivot
+  int pipe[8];                // [0] steps factored (F), [1] X_k taken (B), [3] failed pivot, [4]
+                              // critical panels stored (F), [5] rows whose earlier updates are
+                              // applied (B)
 };
 
 // MODE 0: the whole window (schedule 4). MODE 1: launch A of the split schedule over a nested-
@@ -163,17 +178,23 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
   const int fdim = P.win_fdim[w];
   for (int e = t; e < ld; e += 512) sxDyn[e] = (e < fdim) ? P.rhsF[(size_t)P.win_foff[w] + e] : 0.0;
   if (t < 8) L.sFl[t] = 0;
-  if (t < 4) L.pipe[t] = 0;
+  if (t < 8) L.pipe[t] = t == 5 ? k0 + 1 : 0;  // (row k0+1 has no updates of earlier steps in this part)
   __syncthreads();
   PCLK_INIT
   if (team == 0) {
-    // ---- team F: the diagonal tiles in order
+    // ---- team F: the diagonal tiles in order, and after each the critical pair of the step: panel
+    // L_(k+1)k = A_(k+1)k X_k^T (X_k still in sX) and its update of tile (k+1, k+1), which stays in
+    // sA for the next factor. Team B takes the rest of the step.
     int fgen = 0;
+    const TeamSync<false> fsync{&L.sFl[4], &fgen, lane};
+    const TeamSync<true> fsyncL{&L.sFl[4], &fgen, lane};
+    bool inLds = false;  // tile k already in sA (the previous step's critical update)
     for (int k = k0; k < k1; ++k) {
-      bool inLds = false;
-      if (k > k0) {  // tile k has all its updates (and rhs_k its panel terms); X_(k-1) was taken
-        if (!waitFlag<false>(&L.pipe[1], k, &L.pipe[3])) break;
-        inLds = L.pipe[2] != 0;
+      if (k > k0) {
+        // X_(k-1) taken by team B (sX is overwritten next); without the critical update in sA the
+        // tile comes from W once team B has applied its updates
+        if (!pipeWait(&L.pipe[1], k, &L.pipe[3])) break;
+        if (!inLds && !pipeWait(&L.pipe[5], k, &L.pipe[3])) break;
       }
       PCLK(0, 0)
       if (tt < kTile) L.sy[tt] = sxDyn[k * kTile + tt];
@@ -186,25 +207,53 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
       if (tt < kTile) sxDyn[k * kTile + tt] = L.sy[tt];  // y_k
       if (tt == 0) ldsRelease(&L.pipe[0], k + 1);         // X_k in sX, y_k in sxDyn
       PCLK(1, 0)
+      inLds = false;
+      if (k + 1 < k1 && nz[(k + 1) * T + k]) {
+        // tiles (k+1, k) and (k+1, k+1) have team B's updates of the earlier steps
+        int tc = tt;  // (opaque: the section's addresses are formed here, not held across the loop)
+        asm volatile("" : "+v"(tc));
+        if (!pipeWait(&L.pipe[5], k + 1, &L.pipe[3])) break;
+        panelRhsVector(L.sX, L.sy, L.sy + kTile, L.sA, tc, fsyncL);  // z_k (sA: scratch, L_kk is not needed)
+        loadTile(cur.at(k + 1, k, k), ld, 0, 0, L.sA, tc);
+        dbl4 c[3];
+        loadCDiag(cur.at(k + 1, k + 1, k), ld, c, tc);  // (in flight during the panel)
+        fsyncL();
+        dbl4 acc[4];
+        mfmaPanelRows(L.sA, L.sX, acc, tc);
+        {
+          const double a = panelRhsRow(L.sA, L.sy + kTile, tc);
+          if ((tc & 3) == 0) sxDyn[(k + 1) * kTile + (tc >> 2)] -= a;  // rhs_(k+1) in LDS
+        }
+        fsyncL();  // every wavefront has read A_(k+1)k
+        panelRowsToLds(L.sA, acc, tc);
+        storePanelRows(W + (int64_t)(k + 1) * kTile * ld + k * kTile, ld, acc, tc);
+        fsyncL();
+        dbl4 acc3[3];
+        mfmaDiagNT(L.sA, acc3, tc);
+        fsyncL();  // every wavefront has read L_(k+1)k
+        diagSubToLds(L.sA, c, acc3, tc);
+        fsync();  // (orders the L_(k+1)k stores before the flag)
+        if (tc == 0) ldsRelease(&L.pipe[4], k + 1);  // L_(k+1)k in W
+        inLds = true;
+        PCLK(2, 0)
+      }
     }
   } else {
-    // ---- team B: the panels and band updates of step k once X_k is there
+    // ---- team B: the step's other panels and band updates once X_k is there
     const int tt0 = tt;
     int bgen = 0;
     const TeamSync<false> bsync{&L.sFl[5], &bgen, lane};
     const TeamSync<true> bsyncL{&L.sFl[5], &bgen, lane};
     double xf[16][2];
-    int staged = -1;  // the step whose critical A_(k+1)k is in sB[0] (prefetched at the previous step's end)
     for (int k = k0; k < k1; ++k) {
-      PCLK(6, 256)
-      if (!waitFlag<false>(&L.pipe[0], k + 1, &L.pipe[3])) break;
-      PCLK(2, 256)
-      bool below = false;  // (a step without tiles below only hands the next tile over)
+      if (!pipeWait(&L.pipe[0], k + 1, &L.pipe[3])) break;
+      PCLK(3, 256)
+      bool below = false;  // (a step without tiles below has nothing for team B)
       for (int i = k + 1; i < T; ++i) below = below || nz[i * T + k];
       if (!below) {
         if (tt0 == 0) {
-          L.pipe[2] = 0;
           ldsRelease(&L.pipe[1], k + 1);
+          ldsRelease(&L.pipe[5], k + 2);
         }
         continue;
       }
@@ -212,50 +261,42 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
       // instead of being hoisted out of the loop (and spilled: the kernel is at 256 VGPRs)
       int tt = tt0;
       asm volatile("" : "+v"(tt));
-      // z_k = X_k^T y_k and X_k into registers from team F's sX (untouched until tile k+1 is
-      // handed over below)
+      // z_k = X_k^T y_k and X_k into registers from team F's sX, then sX is released
       if (tt < kTile) L.sz[tt] = sxDyn[k * kTile + tt];
       bsyncL();
-      panelRhsVector(L.sX, L.sz, L.sz + kTile, L.sB[1], tt, bsyncL);  // (scratch: sB[0] may hold A staged)
+      panelRhsVector(L.sX, L.sz, L.sz + kTile, L.sB[1], tt, bsyncL);
       loadXFrag(L.sX, xf, tt);
-      PCLK(3, 256)
-      int held[2] = {-1, -1};  // block row i of the L_ik in sB[0] / sB[1]
+      bsyncL();
+      if (tt == 0) ldsRelease(&L.pipe[1], k + 1);
       const bool crit = k + 1 < k1 && nz[(k + 1) * T + k] != 0;
-      if (crit) {
-        // the critical path: panel (k+1, k), then its update of tile (k+1, k+1) into team F's sA
-        pipePanel(cur.at(k + 1, k, k), W + (int64_t)(k + 1) * kTile * ld + k * kTile, ld, sxDyn + (k + 1) * kTile,
-                  L.sB[0], xf, L.sz + kTile, tt, bsyncL, nullptr, staged == k);
-        held[0] = k + 1;
-        dbl4 c[3], acc[3];  // (a diagonal tile: its lower block triangle, chol_tiles.hpp)
-        loadCDiag(cur.at(k + 1, k + 1, k), ld, c, tt);
-        mfmaDiagNT(L.sB[0], acc, tt);
-        diagSubToLds(L.sA, c, acc, tt);
-        bsyncL();
-      }
-      if (tt == 0) {
-        L.pipe[2] = crit ? 1 : 0;
-        ldsRelease(&L.pipe[1], k + 1);
-      }
-      PCLK(4, 256)
-      // the step's other panels (the last ones stay in LDS for the updates)
-      int hb = crit ? 1 : 0;
-      // (without the critical pair this includes row k+1: at the end of a part of a split window,
-      // where tile k+1 is the separator's)
+      int held[2] = {-1, -1};  // block row i of the L_ik in sB[0] / sB[1]
+      int hb = 0;
+      // the step's other panels (the last two stay in LDS for the updates); without the critical
+      // pair this includes row k+1: at the end of a part of a split window, where tile k+1 is the
+      // separator's
       for (int i = crit ? k + 2 : k + 1; i < T; ++i) {
         if (!nz[i * T + k]) continue;
         pipePanel(cur.at(i, k, k), W + (int64_t)i * kTile * ld + k * kTile, ld, sxDyn + i * kTile, L.sB[hb], xf,
                   L.sz + kTile, tt, bsyncL, i >= jEnd ? deferAt(i, k) : nullptr);
         held[hb] = i;
-        if (!crit) hb ^= 1;
+        hb ^= 1;
       }
       bsync();  // the L tiles in W for reloads by other wavefronts of the team
-      PCLK(5, 256)
-      // band updates A_ij -= L_ik L_jk^T of step k but (k+1, k+1), bottom-up
-      for (int i = T - 1; i > k; --i) {
-        if (!nz[i * T + k]) continue;
+      if (crit && !pipeWait(&L.pipe[4], k + 1, &L.pipe[3])) break;  // L_(k+1)k from team F
+      PCLK(4, 256)
+      // band updates A_ij -= L_ik L_jk^T of step k but (k+1, k+1) (team F's): row k+2 first (team
+      // F's next critical pair reads it), then the rest bottom-up; each tile once per step, so the
+      // order across tiles does not change the bits
+      for (int r = 0; r < T; ++r) {
+        const int i = r == 0 ? k + 2 : (r == 1 ? k + 1 : T + 1 - r);  // k+2, k+1, T-1, ..., k+3
+        if (i <= k || i >= T || (r >= 2 && i <= k + 2) || !nz[i * T + k]) {
+          if (r == 0) {
+            bsync();
+            if (tt == 0) ldsRelease(&L.pipe[5], k + 2);
+          }
+          continue;
+        }
         for (int j = k + 1; j <= i; ++j) {
-          // (row k+1: only (k+1, k+1), done above when critical; the right part of a split
-          // window leaves the separator's tiles to launch B)
           if (!nz[j * T + k] || (i == k + 1 && crit) || j >= jEnd) continue;
           int bi = held[0] == i ? 0 : (held[1] == i ? 1 : -1);
           int bj = j == i ? bi : (held[0] == j ? 0 : (held[1] == j ? 1 : -1));
@@ -287,15 +328,12 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
           }
           bsyncL();  // the operands may be replaced next
         }
+        if (r == 0) {  // row k+2 done: team F's next critical pair may read its tiles
+          bsync();
+          if (tt == 0) ldsRelease(&L.pipe[5], k + 2);
+        }
       }
       bsync();  // the updated tiles in W for the next step's panels
-      // the next step's critical A_(k+2)(k+1) has all its updates now: into sB[0] while team F
-      // factors tile k+1 (one global round trip off the next step's critical path; the panel's
-      // first team barrier orders these LDS writes before its reads)
-      if (k + 2 < k1 && nz[(k + 2) * T + k + 1]) {
-        loadTile(cur.at(k + 2, k + 1, k + 1), ld, 0, 0, L.sB[0], tt);
-        staged = k + 1;
-      }
       PCLK(7, 256)
     }
   }
