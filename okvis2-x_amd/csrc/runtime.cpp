@@ -1383,6 +1383,12 @@ struct okvisgpu_ctx {
   void* arena = nullptr;
   size_t arenaBytes = 0;
   hipGraphExec_t iterGraph = nullptr;
+  // Few windows: kGraphIters iterations captured as one graph as well (iterGraphK): consecutive
+  // launches of one graph are ~8 us apart on the device (the S10 iteration is ~180 us), so
+  // solve_iterate runs n iterations as n / K launches of it and n mod K of the single one.
+  static constexpr int kGraphIters = 4;
+  hipGraphExec_t iterGraphK = nullptr;
+  int graphIters = 1;
   int cuCount = 256;
   size_t ldsPerBlock = 65536;
   bool persistentFits() const { return cholesky_persistent_fits(P.max_fpad, ldsPerBlock); }
@@ -1430,7 +1436,7 @@ struct okvisgpu_ctx {
   }
 
   ~okvisgpu_ctx() {
-    if (iterGraph) (void)hipGraphExecDestroy(iterGraph);
+    dropGraph();
     if (arena) (void)hipFree(arena);
     if (hostStage) (void)hipHostFree(hostStage);
     if (hostIn) (void)hipHostFree(hostIn);
@@ -1446,6 +1452,18 @@ struct okvisgpu_ctx {
       (void)hipGraphExecDestroy(iterGraph);
       iterGraph = nullptr;
     }
+    if (iterGraphK) {
+      (void)hipGraphExecDestroy(iterGraphK);
+      iterGraphK = nullptr;
+    }
+    graphIters = 1;
+  }
+  // n iterations of the captured graph(s), in stream order
+  void launchIterations(int n) {
+    int k = 0;
+    if (iterGraphK)
+      for (; k + graphIters <= n; k += graphIters) HIPCHK(hipGraphLaunch(iterGraphK, stream));
+    for (; k < n; ++k) HIPCHK(hipGraphLaunch(iterGraph, stream));
   }
 
   // ---- host-evaluated factors (SURVEY.md §8b fallback) ------------------------------------------
@@ -1910,10 +1928,7 @@ struct okvisgpu_ctx {
     if (sched == 5 && !(pipeFits() && persistentFits())) sched = 3;
     if (sched == 4 && !pipeFits()) sched = 1;
     if ((sched == 1 || sched == 3) && !persistentFits()) sched = 2;
-    if (sched != P.chol_schedule && iterGraph) {
-      (void)hipGraphExecDestroy(iterGraph);
-      iterGraph = nullptr;
-    }
+    if (sched != P.chol_schedule) dropGraph();
     P.chol_schedule = sched;
     uploadDescriptor();
   }
@@ -2103,6 +2118,20 @@ struct okvisgpu_ctx {
     HIPCHK(hipStreamEndCapture(stream, &g));
     HIPCHK(hipGraphInstantiate(&iterGraph, g, nullptr, nullptr, 0));
     HIPCHK(hipGraphDestroy(g));
+    // Env override OKVISGPU_GRAPH_ITERS=<K> (measurements; 1 = single-iteration graph only).
+    const char* gi = std::getenv("OKVISGPU_GRAPH_ITERS");
+    const int K = gi && *gi ? std::max(1, std::min(std::atoi(gi), 64)) : (serial ? kGraphIters : 1);
+    if (K > 1) {
+      HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+      for (int k = 0; k < K; ++k) {
+        if (serial) launchIteration();
+        else launchIterationForked();
+      }
+      HIPCHK(hipStreamEndCapture(stream, &g));
+      HIPCHK(hipGraphInstantiate(&iterGraphK, g, nullptr, nullptr, 0));
+      HIPCHK(hipGraphDestroy(g));
+      graphIters = K;
+    }
   }
 };
 
@@ -2294,7 +2323,7 @@ int okvisgpu_solve_iterate(okvisgpu_ctx* c, int32_t n) {
   if (!c || n < 0) return OKVISGPU_ERR_INVALID_ARGUMENT;
   if (!c->inSolve) return fail(c, OKVISGPU_ERR_INVALID_ARGUMENT, "solve_iterate without solve_begin");
   return guarded(c, [&]() {
-    for (int k = 0; k < n; ++k) HIPCHK(hipGraphLaunch(c->iterGraph, c->stream));
+    c->launchIterations(n);
     c->replays += n;
     return (int)OKVISGPU_OK;
   });

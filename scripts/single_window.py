@@ -24,6 +24,6 @@ ctx.synchronize()
 dt = time.perf_counter() - t0
 s = ctx.solve_end()[0]
 st = ctx.stats()
-print(f"sched {sched}: {n / dt:.1f} it/s, {dt / n * 1e3:.3f} ms/it, final cost {s['final_cost']:.9g}, "
+print(f"sched {sched}: {n / dt:.1f} it/s, {dt / n * 1e3:.3f} ms/it, final cost {s['final_cost']!r}, "
       f"{st['cholesky_launches']} cholesky launches, {st['s_tiles_nonzero']} tiles, dim {st['reduced_dim']}")
 ctx.close()
