@@ -22,6 +22,7 @@
 //                 (the landmarks' back substitution and vectors: k_lm_backsub_jv, kernels_backsub.hip).
 #include <algorithm>
 #include <cfloat>
+#include <cstdlib>
 
 #include "dev_clock.hpp"
 #include "device_problem.hpp"
@@ -102,17 +103,23 @@ static_assert(kPartRows == 2 || kPartRows == 3, "OKG_PART_ROWS must be 2 or 3");
 // (implementation/ReprojectionError.hpp:186-214, extrJacobian), giving W_e, H_ee, g_e, and so Z_e and
 // the products with the pose visits' Z exactly like a pose visit; V / g_l come from the pose visits.
 // (the body of one landmark group grp; the kernels below run it per workgroup or per window loop)
+// LDS of lmVisitGroup at namespace scope: one allocation per kernel whatever modes it runs
+// (k_lin_few<.., true> runs modes 1 and 2). gLmvBuf rows 0..8: visit shares of V (6) | g_l (3);
+// rows 9..17: visit values being summed into segments; finally rows 0..17: the visits' Z for the
+// partial Schur blocks. gLmvLz per landmark: L^-1 (9) | zz (3) | s_l (3). gLmvPC: the group's
+// landmark-pair products (a | b << 16).
+__shared__ double gLmvBuf[18][kLmGroupVisits];
+__shared__ double gLmvLz[15][kLmGroupMax];
+__shared__ int gLmvPC[kLmPartStage];
 template <int mode, bool EXT>
 __device__ __forceinline__ void lmVisitGroup(const DevProblem& P, const int grp) {
   const int t = threadIdx.x;
   const auto gi = gmem(reinterpret_cast<const int4*>(P.lmg_info + kLmgInfo * grp));
   const int4 gi0 = gi[0], gi1 = gi[kLmgInfo / 4];
   const int l0 = gi0.x, l1 = gi1.x, v0 = gi0.y, v1 = gi1.y;
-  // sBuf rows 0..8: visit shares of V (6) | g_l (3); rows 9..17: visit values being summed into
-  // segments; finally rows 0..17: the visits' Z for the partial Schur blocks
-  __shared__ double sBuf[18][kLmGroupVisits];
-  __shared__ double sLz[15][kLmGroupMax];    // per landmark: L^-1 (9) | zz (3) | s_l (3)
-  __shared__ int sPC[kLmPartStage];          // the group's landmark-pair products (a | b << 16)
+  double (*sBuf)[kLmGroupVisits] = gLmvBuf;
+  double (*sLz)[kLmGroupMax] = gLmvLz;
+  int* sPC = gLmvPC;
   double (*sVg)[kLmGroupVisits] = sBuf;
   double (*sR)[kLmGroupVisits] = sBuf + 9;
   const int w = gi0.z;                       // a group never spans windows
@@ -634,11 +641,25 @@ __global__ __launch_bounds__(256) void k_imu_hess(const DevProblem* __restrict__
 }
 // Few windows: the landmark groups' linearisation (k_lm_visit<1>) and the IMU factors' J^T J as one
 // launch (trailing workgroups), one graph node fewer on a single window's latency chain.
-template <bool EXT>
+// PREP: a group of a window whose step was not accepted runs the GN prep (k_lm_visit<2>) instead,
+// which the next iteration would otherwise start with (one launch fewer per iteration). The prep
+// selects exactly such windows (an accepted one gets Z for its new mu here), and nothing between
+// this launch and the next assembly changes what it reads: the gradient test (k_gradnorm) passes
+// over windows that were not accepted.
+template <bool EXT, bool PREP>
 __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lin_few(const DevProblem* __restrict__ Pp, int lin_mode) {
   const DevProblem& P = *Pp;
-  if ((int)blockIdx.x < P.n_lmg) lmVisitGroup<1, EXT>(P, blockIdx.x);
-  else imuHessBlock(P, (int)blockIdx.x - P.n_lmg, lin_mode);
+  const int b = blockIdx.x;
+  if (b >= P.n_lmg) return imuHessBlock(P, b - P.n_lmg, lin_mode);
+  if (PREP && !gmem(P.st + gmem(P.lmg_info)[kLmgInfo * b + 2])->accepted) lmVisitGroup<2, EXT>(P, b);
+  else lmVisitGroup<1, EXT>(P, b);
+}
+// Few windows run the GN prep inside the linearisation launch (k_lin_few<.., true>); env override
+// OKVISGPU_LIN_PREP=0 (measurements).
+bool lin_runs_prep(const DevProblem& P) {
+  if (!fewWindows(P.n_win, P.cu_count)) return false;
+  const char* e = std::getenv("OKVISGPU_LIN_PREP");
+  return !(e && e[0] == '0');
 }
 
 // A 16-lane group per f-block (16 per 256-thread workgroup; a pose has ~10 contributions): lanes
@@ -1151,8 +1172,14 @@ void launch_linearization_blocks(const DevProblem& P, int lin_mode, hipStream_t 
   if (lin_mode == 1 && fewWindows(P.n_win, P.cu_count)) {
     const int nb = P.n_lmg + (P.n_fac + 3) / 4;
     if (nb > 0) {
-      if (P.n_xvisit > 0) hipLaunchKernelGGL(k_lin_few<true>, dim3(nb), dim3(kLmGroupVisits), 0, s, P.self, lin_mode);
-      else hipLaunchKernelGGL(k_lin_few<false>, dim3(nb), dim3(kLmGroupVisits), 0, s, P.self, lin_mode);
+      const bool prep = lin_runs_prep(P);
+      if (P.n_xvisit > 0) {
+        if (prep) hipLaunchKernelGGL((k_lin_few<true, true>), dim3(nb), dim3(kLmGroupVisits), 0, s, P.self, lin_mode);
+        else hipLaunchKernelGGL((k_lin_few<true, false>), dim3(nb), dim3(kLmGroupVisits), 0, s, P.self, lin_mode);
+      } else {
+        if (prep) hipLaunchKernelGGL((k_lin_few<false, true>), dim3(nb), dim3(kLmGroupVisits), 0, s, P.self, lin_mode);
+        else hipLaunchKernelGGL((k_lin_few<false, false>), dim3(nb), dim3(kLmGroupVisits), 0, s, P.self, lin_mode);
+      }
     }
     if (P.n_pe > 0) hipLaunchKernelGGL(k_pose_extr, dim3((P.n_pe + 255) / 256), dim3(256), 0, s, P.self, lin_mode);
   } else {

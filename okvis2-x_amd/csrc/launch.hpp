@@ -29,6 +29,9 @@ void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_imu_hess(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_lm_prep(const DevProblem& P, hipStream_t s);
+// few windows: the GN prep runs inside the linearisation after a step (launch_linearization_blocks),
+// so the captured iteration does not start with it and the initial linearisation ends with it
+bool lin_runs_prep(const DevProblem& P);
 // the non-zero tiles of S: tail = 0 of the windows about to assemble; tail = 1 of every window not
 // done (end of the captured iteration, S dead)
 void launch_zero_S(const DevProblem& P, hipStream_t s, int tail = 0);

@@ -1371,6 +1371,7 @@ struct okvisgpu_ctx {
   hipStream_t stream = nullptr;
   hipStream_t side[3] = {nullptr, nullptr, nullptr};  // fork streams of the captured iteration graph
   std::vector<hipEvent_t> forkEv;
+  size_t forkEvUsed = 0;  // events of forkEv taken by the capture in progress
   std::string last_error;
   HostBatch B;
   std::vector<const okvisgpu_problem*> probs;
@@ -1383,9 +1384,9 @@ struct okvisgpu_ctx {
   void* arena = nullptr;
   size_t arenaBytes = 0;
   hipGraphExec_t iterGraph = nullptr;
-  // Few windows: kGraphIters iterations captured as one graph as well (iterGraphK): consecutive
-  // launches of one graph are ~8 us apart on the device (the S10 iteration is ~180 us), so
-  // solve_iterate runs n iterations as n / K launches of it and n mod K of the single one.
+  // kGraphIters iterations captured as one graph as well (iterGraphK): consecutive launches of one
+  // graph are ~8 us apart on the device (4.5 % of the S10 single-window iteration; batches +0.2-0.3 %,
+  // r05bk), so solve_iterate runs n iterations as n / K launches of it and n mod K of the single one.
   static constexpr int kGraphIters = 4;
   hipGraphExec_t iterGraphK = nullptr;
   int graphIters = 1;
@@ -2033,11 +2034,12 @@ struct okvisgpu_ctx {
     launch_reduce(P, R_COST_INIT, stream);
     launch_linearization_blocks(P, 0, stream);
     launch_gradnorm(P, 0, stream);
+    if (lin_runs_prep(P)) launch_lm_prep(P, stream);  // (the first iteration's; later ones: k_lin_few)
     HIPCHK(hipGetLastError());
   }
 
   void launchIteration() {
-    launch_lm_prep(P, stream);
+    if (!lin_runs_prep(P)) launch_lm_prep(P, stream);
     launch_assemble(P, stream);
     launch_cholesky(P, stream);
     launch_gn_backsub(P, stream);  // (with the factors' J*v)
@@ -2054,7 +2056,7 @@ struct okvisgpu_ctx {
   // Hessians; J*v: reprojection rows / factor rows; S tiles zeroed vs. landmark-group records;
   // pose-pose vs. speed/bias blocks of S).
   void launchIterationForked() {
-    size_t ne = 0;
+    size_t& ne = forkEvUsed;  // (distinct events for every fork / join of one capture)
     auto ev = [&]() {
       if (ne == forkEv.size()) {
         hipEvent_t e;
@@ -2113,6 +2115,7 @@ struct okvisgpu_ctx {
     // OKVISGPU_SERIAL_GRAPH=0|1 (measurements).
     const char* ser = std::getenv("OKVISGPU_SERIAL_GRAPH");
     const bool serial = ser && (ser[0] == '0' || ser[0] == '1') ? ser[0] == '1' : P.n_win < cuCount;
+    forkEvUsed = 0;
     if (serial) launchIteration();
     else launchIterationForked();
     HIPCHK(hipStreamEndCapture(stream, &g));
@@ -2120,9 +2123,10 @@ struct okvisgpu_ctx {
     HIPCHK(hipGraphDestroy(g));
     // Env override OKVISGPU_GRAPH_ITERS=<K> (measurements; 1 = single-iteration graph only).
     const char* gi = std::getenv("OKVISGPU_GRAPH_ITERS");
-    const int K = gi && *gi ? std::max(1, std::min(std::atoi(gi), 64)) : (serial ? kGraphIters : 1);
+    const int K = gi && *gi ? std::max(1, std::min(std::atoi(gi), 64)) : kGraphIters;
     if (K > 1) {
       HIPCHK(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+      forkEvUsed = 0;
       for (int k = 0; k < K; ++k) {
         if (serial) launchIteration();
         else launchIterationForked();
