@@ -665,6 +665,7 @@ bool lin_runs_prep(const DevProblem& P) {
 // A 16-lane group per f-block (16 per 256-thread workgroup; a pose has ~10 contributions): lanes
 // stride over the contribution list, then a fixed xor-tree reduction over the group (deterministic).
 constexpr int kFgLanes = 16;
+template <int PRE>
 __global__ __launch_bounds__(256) void k_fgrad(const DevProblem* __restrict__ Pp, int lin_mode) {
   const DevProblem& P = *Pp;
   const int fbRaw = blockIdx.x * (256 / kFgLanes) + (threadIdx.x / kFgLanes);
@@ -687,19 +688,36 @@ __global__ __launch_bounds__(256) void k_fgrad(const DevProblem* __restrict__ Pp
   double g[9], hd[9];
 #pragma unroll
   for (int c = 0; c < 9; ++c) { g[c] = 0.0; hd[c] = 0.0; }
-  for (int k = c0 + lane; live && k < c1; k += kFgLanes) {
-    const Contrib cb = k == c0 + lane ? cFirst : P.fb_contrib[k];
-    if (cb.type == C_VISIT) {
-      const double* H = P.seg_hg + (size_t)cb.a * kSegHG;
-      const double* gp = H + 21;
+  // Contributions in rounds of PRE per lane (k = c0 + lane + 16 j): the round's descriptors, then
+  // the directly stored values (visit segments, IMU J^T J), then their sums in k order (the same
+  // additions in the same order as one at a time, so the same bits). Few windows take two per round
+  // (one dependent load round per two contributions on a single window's latency chain), batches
+  // one (the registers of a second would halve the occupancy). Priors and edges form their
+  // products where they are summed.
+  auto loadDirect = [&](const Contrib& cb, double (&vg)[9], double (&vh)[9]) {
+    const bool visit = cb.type == C_VISIT, imu = cb.type == C_IMU;
+    const double* base = visit ? P.seg_hg + (size_t)cb.a * kSegHG : P.imu_H + (size_t)(imu ? cb.a : 0) * kImuHess;
 #pragma unroll
-      for (int c = 0; c < 6; ++c) { g[c] += gp[c]; hd[c] += H[sym6(c, c)]; }
-    } else if (cb.type == C_IMU) {
-      const double* Hf = P.imu_H + (size_t)cb.a * kImuHess;
-      for (int c = 0; c < n; ++c) {
-        g[c] += Hf[465 + cb.b + c];
-        hd[c] += Hf[sym30(cb.b + c, cb.b + c)];
+    for (int c = 0; c < 9; ++c) {
+      vg[c] = 0.0;
+      vh[c] = 0.0;
+      if (visit ? c < 6 : (imu && c < n)) {
+        vg[c] = visit ? base[21 + c] : base[465 + cb.b + c];
+        vh[c] = visit ? base[sym6(c, c)] : base[sym30(cb.b + c, cb.b + c)];
       }
+    }
+  };
+  auto accumulate = [&](const Contrib& cb, const double (&vg)[9], const double (&vh)[9]) {
+    if (cb.type == C_VISIT) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) { g[c] += vg[c]; hd[c] += vh[c]; }
+    } else if (cb.type == C_IMU) {
+#pragma unroll
+      for (int c = 0; c < 9; ++c)
+        if (c < n) {
+          g[c] += vg[c];
+          hd[c] += vh[c];
+        }
     } else if (cb.type == C_PPRIOR) {
       const double* L = P.pp_lin[lb] + 42 * (size_t)cb.a;
       for (int c = 0; c < 6; ++c) {
@@ -737,6 +755,41 @@ __global__ __launch_bounds__(256) void k_fgrad(const DevProblem* __restrict__ Pp
         hd[c] += sh;
       }
     }
+  };
+  if constexpr (PRE == 1) {
+    for (int k = c0 + lane; live && k < c1; k += kFgLanes) {
+      const Contrib cb = k == c0 + lane ? cFirst : P.fb_contrib[k];
+      if (cb.type == C_VISIT) {
+        const double* H = P.seg_hg + (size_t)cb.a * kSegHG;
+        const double* gp = H + 21;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) { g[c] += gp[c]; hd[c] += H[sym6(c, c)]; }
+      } else if (cb.type == C_IMU) {
+        const double* Hf = P.imu_H + (size_t)cb.a * kImuHess;
+        for (int c = 0; c < n; ++c) {
+          g[c] += Hf[465 + cb.b + c];
+          hd[c] += Hf[sym30(cb.b + c, cb.b + c)];
+        }
+      } else {
+        const double z[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        accumulate(cb, z, z);  // (priors and edges)
+      }
+    }
+  } else
+  for (int k = c0 + lane; live && k < c1; k += PRE * kFgLanes) {
+    Contrib cb[PRE];
+    double vg[PRE][9], vh[PRE][9];
+#pragma unroll
+    for (int j = 0; j < PRE; ++j) {
+      const int kj = k + j * kFgLanes;
+      cb[j] = j == 0 && k == c0 + lane ? cFirst : P.fb_contrib[kj < c1 ? kj : k];
+      if (kj >= c1) cb[j].type = -1;
+    }
+#pragma unroll
+    for (int j = 0; j < PRE; ++j) loadDirect(cb[j], vg[j], vh[j]);
+#pragma unroll
+    for (int j = 0; j < PRE; ++j)
+      if (k + j * kFgLanes < c1) accumulate(cb[j], vg[j], vh[j]);
   }
 #pragma unroll
   for (int c = 0; c < 9; ++c)
@@ -1161,9 +1214,10 @@ void launch_lm_blocks(const DevProblem& P, int lin_mode, hipStream_t s) {
   if (P.n_pe > 0) hipLaunchKernelGGL(k_pose_extr, dim3((P.n_pe + 255) / 256), dim3(256), 0, s, P.self, lin_mode);
 }
 void launch_fgrad(const DevProblem& P, int lin_mode, hipStream_t s) {
-  if (P.n_fblock > 0)
-    hipLaunchKernelGGL(k_fgrad, dim3((P.n_fblock + 256 / kFgLanes - 1) / (256 / kFgLanes)), dim3(256), 0, s, P.self,
-                       lin_mode);
+  if (P.n_fblock <= 0) return;
+  const dim3 g((P.n_fblock + 256 / kFgLanes - 1) / (256 / kFgLanes));
+  if (fewWindows(P.n_win, P.cu_count)) hipLaunchKernelGGL(k_fgrad<2>, g, dim3(256), 0, s, P.self, lin_mode);
+  else hipLaunchKernelGGL(k_fgrad<1>, g, dim3(256), 0, s, P.self, lin_mode);
 }
 void launch_imu_hess(const DevProblem& P, int lin_mode, hipStream_t s) {
   if (P.n_fac > 0) hipLaunchKernelGGL(k_imu_hess, dim3((P.n_fac + 3) / 4), dim3(256), 0, s, P.self, lin_mode);
