@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of k_fgrad's two-contribution rounds for few windows (via gpurun): the -m gpu suite, then
+# A/B of a few-window change against lib_base1.so = the previous commit (via gpurun; k_fgrad rounds, r05fg; batched strided tails, r05sb): the -m gpu suite, then
 # single-window rates (100 iterations) with final costs and batch lines with final cost sums for
 # lib_base1.so (before) and the current library.
 set -o pipefail
