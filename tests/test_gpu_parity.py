@@ -290,6 +290,31 @@ def test_forked_and_serial_graphs_agree(og, gpu_ctx, monkeypatch):
         assert np.array_equal(res[0][2][k], res[1][2][k])
 
 
+def test_graph_iterations_and_prep_placement_agree(og, gpu_ctx, monkeypatch):
+    """Iterations per captured graph (runtime.cpp iterGraphK: solve_iterate runs n / K launches of
+    the K-iteration graph and n mod K of the single one) and the few-window GN prep inside the
+    linearisation launch (k_lin_few<.., true>) change the launch structure only: bitwise-equal
+    solves, with the prep as its own launch and one iteration per graph as the reference."""
+    ws = [_window(og, seed=s) for s in (51, 52)]
+    opts = og.default_options(max_num_iterations=7, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    res = []
+    for iters, prep in (("1", "0"), ("4", "1"), ("3", "1"), ("8", "0")):
+        monkeypatch.setenv("OKVISGPU_GRAPH_ITERS", iters)
+        monkeypatch.setenv("OKVISGPU_LIN_PREP", prep)
+        for w in ws:
+            w.reset()
+        gpu_ctx.set_problems([w.problem for w in ws])  # drops the captured graphs
+        s = gpu_ctx.solve(opts, len(ws))
+        res.append((s, [w.poses().copy() for w in ws], [w.landmarks().copy() for w in ws]))
+    for r in res[1:]:
+        for k in range(len(ws)):
+            assert r[0][k]["final_cost"] == res[0][0][k]["final_cost"]
+            assert r[0][k]["num_iterations"] == res[0][0][k]["num_iterations"] == 7
+            assert np.array_equal(r[1][k], res[0][1][k])
+            assert np.array_equal(r[2][k], res[0][2][k])
+
+
 def _close(sg, so, rel=1e-7):
     assert sg["num_iterations"] == so["num_iterations"], (sg, so)
     assert sg["termination"] == so["termination"], (sg, so)
