@@ -117,21 +117,36 @@ def ate(P, gt):
 
 
 PMC_TRAFFIC = os.path.join(REPO, "profiles", "pmc_traffic.json")
-PMC_CALIB = os.path.join(REPO, "profiles", "r05_pmc_calib.json")
+# MFMA counters of the newest round that collected them (scripts/gpu_pmc_calib.sh)
+PMC_CALIBS = [os.path.join(REPO, "profiles", f) for f in ("r06_pmc_calib.json", "r05_pmc_calib.json")]
 
 
 def pmc_mfma():
     """MFMA counters of k_cholesky on this workload (scripts/gpu_pmc_calib.sh ->
-    profiles/r05_pmc_calib.json, collected on the round-5 code): the busy fraction of the matrix cores and the FLOPs the counted
+    profiles/rNN_pmc_calib.json, the newest round's): the busy fraction of the matrix cores and the FLOPs the counted
     v_mfma_f64_16x16x4f64 instructions perform, or None."""
-    try:
-        with open(PMC_CALIB) as f:
-            d = json.load(f)["k_cholesky_mfma"]
-        return {"mfma_busy_frac": d["mfma_busy_frac"], "mfma_flops_per_dispatch": d["mfma_flops"],
-                "source": "profiles/r05_pmc_calib.json (SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_F64, "
-                          "GRBM_GUI_ACTIVE; 2,048 S50 windows)"}
-    except (OSError, KeyError, ValueError, TypeError):
+    for path in PMC_CALIBS:
+        try:
+            with open(path) as f:
+                d = json.load(f)["k_cholesky_mfma"]
+            return {"mfma_busy_frac": d["mfma_busy_frac"], "mfma_flops_per_dispatch": d["mfma_flops"],
+                    "windows": 2048,
+                    "source": f"profiles/{os.path.basename(path)} (SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_F64, "
+                              "GRBM_GUI_ACTIVE; 2,048 S50 windows)"}
+        except (OSError, KeyError, ValueError, TypeError):
+            continue
+    return None
+
+
+def issued_frac(d, windows, n_windows):
+    """k_cholesky's FP64 matrix-core rate on the FLOPs its MFMA instructions perform (counted by
+    SQ_INSTS_VALU_MFMA_F64 on 2,048 S50 windows, scaled per window) over the event-timed launch,
+    beside the algorithmic `frac`; None without the counter file."""
+    m = pmc_mfma()
+    if not m or d["ms"] <= 0 or not n_windows:
         return None
+    flops = m["mfma_flops_per_dispatch"] / m.get("windows", 2048) * windows
+    return flops / (d["ms"] * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS
 
 
 def rank_windows(total, world, rank):
@@ -365,23 +380,7 @@ def single_window(og, cfg, opts, args, device):
     out["e2e_iterations"] = total_iters
     out["e2e_iters_per_s"] = total_iters / e2e
     if not args.no_profile:
-        # per-phase device times of one real iteration: after the warm-up (the steady state: the
-        # biases have settled, the candidate evaluations keep the IMU preintegration) and the first
-        # iteration of the solve (the biases still move: ImuError re-integrates, ImuError.cpp:834-858),
-        # plus the forced re-integration of every factor of the window (okvisgpu_time_kernel)
-        for key, it in (("kernel_ms_per_iteration", args.warmup), ("kernel_ms_first_iteration", 0)):
-            w1[0].reset()
-            c1.update_params()
-            c1.solve_begin(opts)
-            c1.solve_iterate(it)
-            ph1 = c1.profile_iteration()
-            c1.solve_end()
-            out[key] = {k: round(v, 4) for k, v in ph1.items()}
-            out[key.replace("kernel_ms", "ms")] = round(sum(ph1.values()), 4)
-        w1[0].reset()
-        c1.update_params()
-        out["eval_imu_forced_reintegration_ms"] = round(c1.time_kernel("k_eval_imu", 5)[0], 4)
-        # which iterations of window 0 re-integrated IMU factors (ImuError::redoPreintegration,
+        # which iterations of window 0 re-integrate IMU factors (ImuError::redoPreintegration,
         # counted by redoCounter_ = imu_state[:, 0]): solves of 0..K iterations from the same start
         # (the same bits up to their last iteration), the counters written back after each; entry n
         # is the number of factors re-integrated during iteration n (entry 0: the initial evaluation)
@@ -397,8 +396,41 @@ def single_window(og, cfg, opts, args, device):
         per = [int(round(counts[0]))] + [int(round(counts[n] - counts[n - 1])) for n in range(1, len(counts))]
         out["imu_reintegrated_factors_per_iteration"] = per
         later = [n for n in range(1, len(per)) if per[n] > 0]
-        out["imu_last_reintegrating_iteration"] = later[-1] if later else 0
+        last = later[-1] if later else 0
+        out["imu_last_reintegrating_iteration"] = last
         out["imu_factors"] = int(w1[0].problem.n_imu)
+        # per-phase device times of one real iteration (eager launches between HIP events): the
+        # steady state = the first iteration after the last one that re-integrates (the biases have
+        # settled, the candidate evaluations keep the IMU preintegration), and the first iteration of
+        # the solve (the biases still move: ImuError re-integrates, ImuError.cpp:834-858); plus the
+        # forced re-integration of every factor of the window (okvisgpu_time_kernel)
+        steady = min(last, total_iters - 1)
+        out["steady_state_iteration"] = steady + 1
+        for key, it in (("kernel_ms_per_iteration", steady), ("kernel_ms_first_iteration", 0)):
+            w1[0].reset()
+            c1.update_params()
+            c1.solve_begin(opts)
+            c1.solve_iterate(it)
+            ph1 = c1.profile_iteration()
+            c1.solve_end()
+            out[key] = {k: round(v, 4) for k, v in ph1.items()}
+            out[key.replace("kernel_ms", "ms")] = round(sum(ph1.values()), 4)
+        # the steady state as the solve runs it (graph launches, wall time like iters_per_s): the
+        # iterations after the last re-integrating one
+        n_steady = total_iters - steady
+        w1[0].reset()
+        c1.update_params()
+        c1.solve_begin(opts)
+        c1.solve_iterate(steady)
+        c1.synchronize()
+        a = time.perf_counter()
+        c1.solve_iterate(n_steady)
+        c1.synchronize()
+        out["ms_per_iter_steady_state"] = (time.perf_counter() - a) / n_steady * 1e3
+        c1.solve_end()
+        w1[0].reset()
+        c1.update_params()
+        out["eval_imu_forced_reintegration_ms"] = round(c1.time_kernel("k_eval_imu", 5)[0], 4)
     c1.close()
     return out, gpu_pose, gt_p
 
@@ -554,13 +586,18 @@ def main(argv=None):
                 "unit": "GB/s" if d["bound"] == "hbm" else "TFLOP/s", "frac": d["frac"],
                 "traffic": traffic,
                 "traffic_calibration": "FETCH_SIZE x2, WRITE_SIZE x1: measured for this code's 16-B, 8-B and "
-                                       "tile-row access shapes (scripts/pmc_calib.hip, profiles/r05_pmc_calib.json)",
+                                       "tile-row access shapes (scripts/pmc_calib.hip, profiles/rNN_pmc_calib.json)",
                 "counters": pmc_mfma() if dominant == "k_cholesky" else None,
+                "frac_issued": issued_frac(d, len(mine), stats["n_windows"]) if dominant == "k_cholesky" else None,
                 "work_per_iteration": d["work"], "ms_per_iteration": d["ms"],
                 "frac_survey_8d": survey.get(dominant, {}).get("frac") if d["bound"] == "hbm" else None,
                 "method": f"HIP events on the context stream, {args.kernel_reps} launches of one iteration's "
                           "worth on the resident batch; work = algorithmic bytes/FLOPs of the builder's model "
-                          "(DESIGN.md §4; FP64 flops of the tile-sparse LLT for k_cholesky); frac_survey_8d = "
+                          "(DESIGN.md §4; for k_cholesky the FP64 flops of the tile-sparse LLT: n^3/3 per "
+                          "diagonal potrf, n^3 per panel TRSM, n^2(n+1) per diagonal SYRK, 2n^3 per GEMM "
+                          "update, 2n^2 / 4n^2 per diagonal / panel tile for the two solves, n = 64); "
+                          "frac_issued = the FLOPs of the v_mfma_f64 instructions the kernel issues "
+                          "(SQ_INSTS_VALU_MFMA_F64, counters.source) / the same time; frac_survey_8d = "
                           "SURVEY.md §8(d) compulsory bytes (S tile-sparse) / the same time; traffic = "
                           "rocprofv3 --pmc HBM bytes per iteration from profiles/pmc_traffic.json",
             }

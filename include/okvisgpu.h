@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define OKVISGPU_ABI_VERSION 5
+#define OKVISGPU_ABI_VERSION 6
 
 /* ---------------------------------------------------------------- status codes */
 typedef enum okvisgpu_status {
@@ -86,6 +86,42 @@ typedef struct okvisgpu_imu_params { /* okvis::ImuParameters subset, okvis_commo
   double sigma_g_c, sigma_a_c, sigma_gw_c, sigma_aw_c;
   double g;
 } okvisgpu_imu_params;
+
+/* ---------------------------------------------------------------- robust losses (ABI 6)
+ * The ::ceres::LossFunction family (ceres-solver >= 2.1 loss_function.h; un-vendored submodule,
+ * SURVEY.md §8c). okvis builds four losses in ViGraph's constructor (ViGraph.cpp:235-238):
+ * CauchyLoss(1.0) for reprojections (:338) and Cauchy-robustified submap alignment (:1505),
+ * CauchyLoss(3.0) for GPS (:88,:999,:1408), TukeyLoss(2.0) / TukeyLoss(0.1) for LiDAR / depth submap
+ * alignment (:1510,:1513). rho(s) of the squared residual norm s, with rho[1] = rho', rho[2] = rho'':
+ *   CAUCHY(a)      b = a^2:  b log(1 + s/b)
+ *   TUKEY(a)       s <= a^2: a^2/3 (1 - (1 - s/a^2)^3), else a^2/3
+ *   HUBER(a)       s <= a^2: s, else 2 a sqrt(s) - a^2
+ *   SOFTLONE(a)    2 a^2 (sqrt(1 + s/a^2) - 1)
+ *   ARCTAN(a)      a atan2(s, a)
+ *   TOLERANT(a, b) b log(1 + exp((s - a)/b)) - b log(1 + exp(-a/b))
+ * The backend applies Ceres' Corrector (restated by okvis at TwoPoseGraphError.cpp:292-337): cost
+ * 1/2 rho(s); for rho'' <= 0 (or s = 0) r and J scaled by sqrt(rho'); for rho'' > 0 (TOLERANT) the
+ * second-order correction alpha = 1 - sqrt(1 + 2 s rho''/rho'), r scaled by sqrt(rho')/(1 - alpha),
+ * J <- sqrt(rho') (I - alpha/s r r^T) J. */
+typedef enum okvisgpu_loss_kind {
+  OKVISGPU_LOSS_NONE = 0,           /* nullptr loss (TrivialLoss)                                */
+  OKVISGPU_LOSS_CAUCHY = 1,
+  OKVISGPU_LOSS_TUKEY = 2,
+  OKVISGPU_LOSS_HUBER = 3,
+  OKVISGPU_LOSS_SOFTLONE = 4,
+  OKVISGPU_LOSS_ARCTAN = 5,
+  OKVISGPU_LOSS_TOLERANT = 6
+} okvisgpu_loss_kind;
+
+typedef struct okvisgpu_loss {
+  int32_t kind;                     /* okvisgpu_loss_kind                                        */
+  int32_t reserved;                 /* 0                                                          */
+  double a, b;                      /* scale a (> 0); b: TOLERANT's width (> 0), else unused      */
+} okvisgpu_loss;
+
+/* rho[3] = (rho(s), rho'(s), rho''(s)) of a loss, as ::ceres::LossFunction::Evaluate (host only).
+ * OKVISGPU_ERR_INVALID_ARGUMENT for an unknown kind or a non-positive scale. */
+int okvisgpu_loss_evaluate(const okvisgpu_loss* loss, double s, double* rho);
 
 /* Size (doubles) of one ImuError's persistent preintegration state (in/out, see imu_state). Layout:
  *  [0]       redo counter (0 => never integrated; first Evaluate integrates, ImuError.cpp:837)
@@ -212,9 +248,15 @@ typedef struct okvisgpu_problem {
                                        (index < n_poses: a state's pose; n_poses + c: camera c's
                                        extrinsics), 1 speed/bias, -1 none (trailing)             */
   const int32_t* host_param_index;  /* [n][4]                                                      */
-  const uint8_t* host_cauchy;       /* [n] 1 = CauchyLoss(1.0) (may be NULL = no loss)            */
+  const uint8_t* host_cauchy;       /* [n] 1 = CauchyLoss(1.0) (may be NULL = no loss); ignored
+                                       when host_loss is set                                    */
   okvisgpu_host_evaluate_fn host_evaluate;
   void* host_user;
+
+  /* --- ABI 6: the loss function of each host-evaluated factor (any okvisgpu_loss_kind, e.g.
+   * CauchyLoss(3.0) on GPS factors, ViGraph.cpp:999; TukeyLoss(2.0) on LiDAR submap alignment,
+   * :1510). NULL = host_cauchy. */
+  const okvisgpu_loss* host_loss;   /* [n_host]                                                     */
 } okvisgpu_problem;
 
 /* ---------------------------------------------------------------- solver options / summary */
@@ -257,6 +299,23 @@ typedef struct okvisgpu_summary {   /* ::ceres::Solver::Summary subset */
   double total_time_s;              /* wall time of okvisgpu_solve for this batch               */
   double final_radius;
   double final_mu;
+  /* ABI 6: the ::ceres::Solver::Summary timing fields (seconds; one batch, the same in every
+   * window's summary). Wall clock of okvisgpu_solve's parts: preprocessor (parameter upload,
+   * structure rebuild after freeze / unfreeze, iteration 0, graph instantiation), minimizer (the
+   * trust-region iterations), postprocessor (write-back). Device time of the iterations' phases
+   * from HIP events on the context's stream, only when options.verbose is set (the iterations then
+   * run as eager launches instead of the captured graph: the same kernels in the same order, the
+   * same bits), else -1: linear solver (GN prep, Schur assembly, LLT + back substitution, J*v),
+   * residual evaluation (candidate evaluation and its cost reduction), Jacobian evaluation
+   * (linearisation at the accepted point and the gradient norms), step (the dogleg step, Plus and
+   * the accept / reject decision; no Ceres field: part of its minimizer time). */
+  double preprocessor_time_s;
+  double minimizer_time_s;
+  double postprocessor_time_s;
+  double linear_solver_time_s;
+  double residual_evaluation_time_s;
+  double jacobian_evaluation_time_s;
+  double step_time_s;
 } okvisgpu_summary;
 
 /* ---------------------------------------------------------------- context */

@@ -79,21 +79,68 @@ class HomogeneousPointManifold final : public Manifold {
 };
 
 // ---------------------------------------------------------------- losses (ceres::LossFunction)
+// The Ceres loss family with ::ceres::LossFunction::Evaluate(s, rho) (evaluated by the library,
+// okvisgpu_loss_evaluate: the same restatement the backend applies). okvis builds four of them in
+// ViGraph's constructor (ViGraph.cpp:235-238): CauchyLoss(1.0) (every reprojection, :338; Cauchy
+// submap alignment, :1505), CauchyLoss(3.0) (GPS, :88,:999,:1408), TukeyLoss(0.1) / TukeyLoss(2.0)
+// (depth / LiDAR submap alignment, :1513 / :1510). The GPU evaluates reprojections with
+// CauchyLoss(1) only; host-evaluated factors take any of these.
 class LossFunction {
  public:
   virtual ~LossFunction() = default;
   virtual const char* name() const = 0;
-};
-// CauchyLoss(1.0) on every reprojection (ViGraph.cpp:235,338); other scales are not on the path
-class CauchyLoss final : public LossFunction {
- public:
-  explicit CauchyLoss(double a = 1.0) : a_(a) {
-    if (a != 1.0) throw Unsupported("CauchyLoss scale other than 1 (okvis uses CauchyLoss(1.0))");
+  virtual okvisgpu_loss descriptor() const = 0;
+  // rho[0..2] = rho(s), rho'(s), rho''(s) of the squared residual norm s
+  void Evaluate(double s, double rho[3]) const {
+    const okvisgpu_loss d = descriptor();
+    if (okvisgpu_loss_evaluate(&d, s, rho) != OKVISGPU_OK) throw Error(std::string(name()) + ": invalid scale");
   }
-  const char* name() const override { return "CauchyLoss"; }
+};
+namespace detail {
+template <int Kind>
+class ScaledLoss : public LossFunction {
+ public:
+  explicit ScaledLoss(double a, double b = 0.0) : a_(a), b_(b) {
+    const okvisgpu_loss d = descriptor();
+    double rho[3];
+    if (okvisgpu_loss_evaluate(&d, 0.0, rho) != OKVISGPU_OK) throw Error("loss function with an invalid scale");
+  }
+  okvisgpu_loss descriptor() const override { return okvisgpu_loss{Kind, 0, a_, b_}; }
+  double a() const { return a_; }
 
- private:
-  double a_;
+ protected:
+  double a_, b_;
+};
+}  // namespace detail
+class CauchyLoss final : public detail::ScaledLoss<OKVISGPU_LOSS_CAUCHY> {
+ public:
+  explicit CauchyLoss(double a = 1.0) : ScaledLoss(a) {}
+  const char* name() const override { return "CauchyLoss"; }
+};
+class TukeyLoss final : public detail::ScaledLoss<OKVISGPU_LOSS_TUKEY> {
+ public:
+  explicit TukeyLoss(double a) : ScaledLoss(a) {}
+  const char* name() const override { return "TukeyLoss"; }
+};
+class HuberLoss final : public detail::ScaledLoss<OKVISGPU_LOSS_HUBER> {
+ public:
+  explicit HuberLoss(double a) : ScaledLoss(a) {}
+  const char* name() const override { return "HuberLoss"; }
+};
+class SoftLOneLoss final : public detail::ScaledLoss<OKVISGPU_LOSS_SOFTLONE> {
+ public:
+  explicit SoftLOneLoss(double a) : ScaledLoss(a) {}
+  const char* name() const override { return "SoftLOneLoss"; }
+};
+class ArctanLoss final : public detail::ScaledLoss<OKVISGPU_LOSS_ARCTAN> {
+ public:
+  explicit ArctanLoss(double a) : ScaledLoss(a) {}
+  const char* name() const override { return "ArctanLoss"; }
+};
+class TolerantLoss final : public detail::ScaledLoss<OKVISGPU_LOSS_TOLERANT> {
+ public:
+  TolerantLoss(double a, double b) : ScaledLoss(a, b) {}
+  const char* name() const override { return "TolerantLoss"; }
 };
 
 // ---------------------------------------------------------------- cost functions
@@ -214,7 +261,8 @@ class RelativePoseError final : public CostFunction {
 // or extrinsics) and speed/bias (9) blocks, at most 2 of each, <= 15 residuals. Evaluate has the
 // ::ceres::CostFunction::Evaluate contract: ambient Jacobians (the backend applies the blocks'
 // PoseManifold), return false on failure. It is called from up to options.num_threads host threads
-// at every point the solver evaluates; CauchyLoss(1) may be attached at AddResidualBlock.
+// at every point the solver evaluates; any loss of the family above may be attached at
+// AddResidualBlock (CauchyLoss(3.0) for GPS, TukeyLoss for submap alignment: ViGraph.cpp:999,1510).
 class HostCostFunction : public CostFunction {
  public:
   std::string typeInfo() const override { return "HostCostFunction"; }
@@ -571,8 +619,11 @@ class Problem {
     if (!host && !known.count(t))
       throw Unsupported("cost function \"" + t + "\" has no GPU evaluation (wrap it in a HostCostFunction)");
     if (loss && !host && t != "ReprojectionError") throw Unsupported(t + " with a loss function (okvis adds none)");
-    if (loss && !dynamic_cast<const CauchyLoss*>(loss))  // the device applies CauchyLoss(1) only
-      throw Unsupported(t + " with loss \"" + loss->name() + "\" (only CauchyLoss(1) is evaluated)");
+    if (loss && t == "ReprojectionError") {  // the device applies CauchyLoss(1) to reprojections
+      const okvisgpu_loss d = loss->descriptor();
+      if (d.kind != OKVISGPU_LOSS_CAUCHY || d.a != 1.0)
+        throw Unsupported(t + " with loss \"" + loss->name() + "\" (reprojections take CauchyLoss(1.0), ViGraph.cpp:338)");
+    }
     const std::vector<int> sizes = cost->parameterBlockSizes();
     if (host) {  // the §8b fallback's limits (okvisgpu.h host_*)
       int np = 0, ns = 0;
@@ -899,7 +950,7 @@ class Problem {
       A_.host_kind.insert(A_.host_kind.end(), kind, kind + 4);
       A_.host_index.insert(A_.host_index.end(), idx, idx + 4);
       A_.host_dim.push_back(h->residualDim());
-      A_.host_cauchy.push_back(r->loss != nullptr);
+      A_.host_loss.push_back(r->loss ? r->loss->descriptor() : okvisgpu_loss{OKVISGPU_LOSS_NONE, 0, 1.0, 0.0});
       hostTerms_.push_back(h);
     }
     gatherValues();
@@ -956,7 +1007,8 @@ class Problem {
     P.host_dim = A_.host_dim.data();
     P.host_param_kind = A_.host_kind.data();
     P.host_param_index = A_.host_index.data();
-    P.host_cauchy = A_.host_cauchy.data();
+    P.host_cauchy = nullptr;
+    P.host_loss = A_.host_loss.data();
     P.host_evaluate = &Problem::hostTrampoline;
     P.host_user = this;
     built_ = true;
@@ -1001,7 +1053,8 @@ class Problem {
   struct Arrays {
     std::vector<double> pose, sb, lm, extr, obs_kp, obs_L, imu_ga, imu_state, pp_meas, pp_L, sbp_meas, sbp_L, rp_dx,
         rp_J, rp_lp, ep_meas, ep_L;
-    std::vector<uint8_t> pose_c, sb_c, lm_c, extr_c, obs_cauchy, rp_kind, host_cauchy;
+    std::vector<uint8_t> pose_c, sb_c, lm_c, extr_c, obs_cauchy, rp_kind;
+    std::vector<okvisgpu_loss> host_loss;
     std::vector<int32_t> obs_pose, obs_lm, obs_cam, imu_blocks, imu_begin, pp_block, sbp_block, rp_blocks, ep_cam,
         host_kind, host_index, host_dim;
     std::vector<int64_t> imu_t0, imu_t1, imu_ts;
@@ -1068,6 +1121,14 @@ void toSummary(const okvisgpu_summary& s, SolverSummary* out) {
   out->num_unsuccessful_steps = s.num_unsuccessful_steps;
   out->termination_type = static_cast<decltype(out->termination_type)>(s.termination_type);
   out->total_time_in_seconds = s.total_time_s;
+  // the Summary timing fields FullReport prints (ViGraph.cpp:1887-1889); the device phase times
+  // are filled when the solve ran with options.verbose (minimizer_progress_to_stdout), else -1
+  out->preprocessor_time_in_seconds = s.preprocessor_time_s;
+  out->minimizer_time_in_seconds = s.minimizer_time_s;
+  out->postprocessor_time_in_seconds = s.postprocessor_time_s;
+  out->linear_solver_time_in_seconds = s.linear_solver_time_s;
+  out->residual_evaluation_time_in_seconds = s.residual_evaluation_time_s;
+  out->jacobian_evaluation_time_in_seconds = s.jacobian_evaluation_time_s;
 }
 template <class SolverOptions, class SolverSummary>
 int Solve(const SolverOptions& options, Problem* problem, SolverSummary* summary, bool denseSchur = true,

@@ -857,16 +857,12 @@ __device__ __forceinline__ bool gapRow(const DevProblem& P, int w, int e) {
 }
 
 // Persistent schedules (NT = 256 threads, 4 virtual threads each, or the pipelined kernel's 512
-// threads, 2 each): y already in sx (LDS), then the steps with operands loaded in-step. sA: >= 32 x
-// 64 doubles.
-// (Sync: the workgroup's __syncthreads (FullSync), or a team barrier when each team of the
-// two-window pipelined kernel solves its own window)
-struct FullSync {
-  __device__ __forceinline__ void operator()() const { __syncthreads(); }
-};
-template <int NT = 256, class Sync = FullSync>
+// threads, 2 each): y already in sx (LDS), then the steps with operands loaded in-step; every
+// thread of the workgroup takes part (__syncthreads between the phases). sA: >= 32 x 64 doubles.
+template <int NT = 256>
 __device__ __forceinline__ void backSubstitute(const DevProblem& P, int w, const double* S, int64_t ld, int T, const double* Linv,
-                               const uint8_t* nz, double* sx, double* sA, double* sy, int t, Sync sync = Sync()) {
+                               const uint8_t* nz, double* sx, double* sA, double* sy, int t) {
+  const auto sync = [] { __syncthreads(); };
   // sx already holds y (the persistent kernel keeps the whole forward substitution in LDS)
   sync();
   constexpr int kV = kBsThreads / NT;

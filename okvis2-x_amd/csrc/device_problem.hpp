@@ -79,7 +79,9 @@ struct WinState {
   int32_t eval_cand;               // candidate must be evaluated this iteration
   int32_t step_valid;
   int32_t accepted;
-  int32_t pad_[3];
+  int32_t dev_error;               // a kernel gave up on this window (pipelined Cholesky wait limit):
+                                   // the host reports OKVISGPU_ERR_DEVICE, not a failed GN step
+  int32_t pad_[2];
 };
 
 // Options mirrored on the device (okvisgpu_options subset used inside kernels).
@@ -97,6 +99,8 @@ struct DevProblem {
   const DevProblem* self;          // device-resident copy of this descriptor (what kernels receive)
   int32_t n_win, n_pose, n_sb, n_lm, n_obs, n_visit, n_imu, n_pprior, n_sbprior, n_cam;
   int32_t cu_count;                // compute units of the device (persistent-style grids)
+  int32_t lin_prep;                // host only: GN prep inside the linearisation launch (1 / 0),
+                                   // fixed per solve (lin_runs_prep); -1 = not yet decided
   int32_t n_fblock, n_pair;
   int32_t max_fpad, max_tiles;     // largest padded reduced dimension / its 64-tile count
   int64_t obs_stride;              // plane stride of the obs linearisation SoA (>= n_obs)

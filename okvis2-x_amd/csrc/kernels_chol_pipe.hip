@@ -118,17 +118,21 @@ __device__ __forceinline__ void pipePanel(const double* Aik, double* Lik, int64_
 #ifndef OKG_PIPE_MAP
 #define OKG_PIPE_MAP 0
 #endif
-// The teams' waits on each other, with a spin limit no correct run reaches (~1 s): a wait that
-// never ends reports a failed factorisation (the window's GN step is retried) instead of hanging
-// the device.
+// The teams' waits on each other. fail (pipe[3]) = 1: team F met a non-positive pivot and stopped;
+// it set no flag after that, so once fail is seen the flag has its final value and is re-read:
+// every wavefront of a team returns the same outcome (a wavefront that saw the flag earlier saw a
+// value the re-read also sees), and the team barriers that follow stay matched. A spin limit no
+// correct run reaches (~1 s) ends a wait that never completes with fail = 2 (atomic max, so a pivot
+// failure is not overwritten): the window is reported as a device error (WinState::dev_error ->
+// OKVISGPU_ERR_DEVICE), not as a failed GN step, instead of hanging the device.
 __device__ __forceinline__ bool pipeWait(int* p, int v, int* fail) {
   for (int it = 0; it < (1 << 24); ++it) {
     if (ldsAcquire(p) >= v) return true;
-    if (ldsAcquire(fail)) return false;
+    if (ldsAcquire(fail)) return ldsAcquire(p) >= v;
     __builtin_amdgcn_s_sleep(OKG_WAIT_SLEEP);
   }
-  if ((threadIdx.x & 63) == 0) ldsRelease(fail, 1);
-  return false;
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_max(fail, 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return ldsAcquire(p) >= v;
 }
 
 // LDS of the pipelined kernel besides the window's rhs / y (dynamic, ld doubles)
@@ -339,7 +343,10 @@ __global__ __launch_bounds__(512, 1) void k_cholesky_pipe(const DevProblem* __re
   }
   __syncthreads();
   if (L.pipe[3]) {
-    if (t == 0) P.st[w].gn_failed = 1;
+    if (t == 0) {
+      if (L.pipe[3] == 1) P.st[w].gn_failed = 1;  // non-positive pivot: the GN step is retried
+      else P.st[w].dev_error = 1;                 // wait limit
+    }
     return;
   }
   if (split) {  // launch A: this part's rows of y (part 0 also the separator's rhs) for launch B

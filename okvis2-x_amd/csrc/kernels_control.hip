@@ -401,13 +401,16 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
         if (s.mu < 1.0) {
           sflag = 1;  // retry next pass, iteration not consumed
         } else {
-          // LINEAR_SOLVER_FAILURE -> invalid step (HandleInvalidStep, StepIsInvalid)
-          s.iteration += 1;
-          s.num_unsucc += 1;
+          // LINEAR_SOLVER_FAILURE -> invalid step (HandleInvalidStep, StepIsInvalid). The step that
+          // reaches max_num_consecutive_invalid_steps ends the solve before Ceres'
+          // FinalizeIteration records it (TrustRegionMinimizer: `if (!HandleInvalidStep()) return;`):
+          // neither the iteration nor the unsuccessful step is counted
           if (++s.consecutive_invalid >= P.opt.max_num_consecutive_invalid_steps) {
             s.done = 1;
             s.termination = 2;
           } else {
+            s.iteration += 1;
+            s.num_unsucc += 1;
             s.mu *= 10.0;
             s.need_gn = 1;
             finalizeIteration(P, s);
@@ -598,19 +601,30 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
     s.consecutive_invalid = 0;
     s.eval_cand = 1;
   } else {
-    // HandleInvalidStep + DoglegStrategy::StepIsInvalid
+    // HandleInvalidStep + DoglegStrategy::StepIsInvalid; the step that reaches
+    // max_num_consecutive_invalid_steps ends the solve unrecorded (iteration and unsuccessful step
+    // not counted, as Ceres returns before FinalizeIteration)
     s.step_valid = 0;
     s.eval_cand = 0;
-    s.num_unsucc += 1;
     if (++s.consecutive_invalid >= P.opt.max_num_consecutive_invalid_steps) {
       s.done = 1;
       s.termination = 2;  // FAILURE
+      s.iteration -= 1;
       return;
     }
+    s.num_unsucc += 1;
     s.mu *= 10.0;
     s.need_gn = 1;
     finalizeIteration(P, s);
   }
+}
+
+__global__ __launch_bounds__(64) void k_hold(int rounds) {
+  for (int r = 0; r < rounds; ++r) __builtin_amdgcn_s_sleep(127);  // ~127 x 64 clocks each
+}
+void launch_hold(hipStream_t s, int us) {
+  const int rounds = us * 2400 / (127 * 64) + 1;  // 2.4 GHz shader clock (calibrated)
+  hipLaunchKernelGGL(k_hold, dim3(1), dim3(64), 0, s, rounds);
 }
 
 // The factors' J*v on their own: in the iteration they are the trailing workgroups of

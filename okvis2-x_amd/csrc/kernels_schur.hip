@@ -655,8 +655,11 @@ __global__ __launch_bounds__(kLmGroupVisits, OKG_LMV_OCC) void k_lin_few(const D
   else lmVisitGroup<1, EXT>(P, b);
 }
 // Few windows run the GN prep inside the linearisation launch (k_lin_few<.., true>); env override
-// OKVISGPU_LIN_PREP=0 (measurements).
+// OKVISGPU_LIN_PREP=0 (measurements). The runtime decides once per solve (P.lin_prep, set in
+// okvisgpu_solve_begin before the initial launches and the graph capture), so the initial
+// linearisation and the captured iterations always agree on where the prep runs.
 bool lin_runs_prep(const DevProblem& P) {
+  if (P.lin_prep >= 0) return P.lin_prep != 0;
   if (!fewWindows(P.n_win, P.cu_count)) return false;
   const char* e = std::getenv("OKVISGPU_LIN_PREP");
   return !(e && e[0] == '0');

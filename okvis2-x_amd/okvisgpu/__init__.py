@@ -42,6 +42,39 @@ class ImuParams(C.Structure):
                 ("g", C.c_double)]
 
 
+# robust losses (ABI 6; okvisgpu_loss_kind): ::ceres::LossFunction family
+LOSS_NONE, LOSS_CAUCHY, LOSS_TUKEY, LOSS_HUBER, LOSS_SOFTLONE, LOSS_ARCTAN, LOSS_TOLERANT = range(7)
+LOSS_KINDS = {"none": LOSS_NONE, "cauchy": LOSS_CAUCHY, "tukey": LOSS_TUKEY, "huber": LOSS_HUBER,
+              "softlone": LOSS_SOFTLONE, "arctan": LOSS_ARCTAN, "tolerant": LOSS_TOLERANT}
+
+
+class Loss(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("reserved", C.c_int32), ("a", C.c_double), ("b", C.c_double)]
+
+
+# numpy record layout of okvisgpu_loss (arrays of per-factor losses: host_loss)
+LOSS_DTYPE = np.dtype([("kind", "<i4"), ("reserved", "<i4"), ("a", "<f8"), ("b", "<f8")])
+
+
+def loss_array(specs):
+    """[(kind name or id, a[, b]), ...] -> LOSS_DTYPE array for okvisgpu_problem.host_loss."""
+    out = np.zeros(len(specs), dtype=LOSS_DTYPE)
+    for i, sp in enumerate(specs):
+        k = LOSS_KINDS[sp[0]] if isinstance(sp[0], str) else int(sp[0])
+        out[i] = (k, 0, float(sp[1]) if len(sp) > 1 else 1.0, float(sp[2]) if len(sp) > 2 else 0.0)
+    return out
+
+
+def loss_evaluate(kind, a=1.0, b=0.0, s=0.0):
+    """okvisgpu_loss_evaluate: (rho, rho', rho'') of a loss at the squared norm s (host only)."""
+    L = Loss(LOSS_KINDS[kind] if isinstance(kind, str) else int(kind), 0, a, b)
+    rho = (C.c_double * 3)()
+    rc = lib().okvisgpu_loss_evaluate(C.byref(L), float(s), rho)
+    if rc != 0:
+        raise OkvisGpuError(f"okvisgpu_loss_evaluate failed ({rc})")
+    return tuple(rho)
+
+
 # okvisgpu_host_evaluate_fn (ABI 5): (user, factor, parameters, residuals, jacobians) -> nonzero = ok
 HOST_EVALUATE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int32, C.POINTER(_dp), _dp, C.POINTER(_dp))
 HOST_MAX_RESIDUALS = 15
@@ -68,6 +101,7 @@ class Problem(C.Structure):
         ("extrinsics_prior_meas", _dp), ("extrinsics_prior_sqrt_info", _dp),
         ("n_host", C.c_int32), ("host_dim", _ip), ("host_param_kind", _ip), ("host_param_index", _ip),
         ("host_cauchy", _up), ("host_evaluate", HOST_EVALUATE_FN), ("host_user", C.c_void_p),
+        ("host_loss", C.c_void_p),
     ]
 
 
@@ -117,7 +151,11 @@ class Summary(C.Structure):
     _fields_ = [("initial_cost", C.c_double), ("final_cost", C.c_double),
                 ("num_iterations", C.c_int32), ("num_successful_steps", C.c_int32),
                 ("num_unsuccessful_steps", C.c_int32), ("termination_type", C.c_int32),
-                ("total_time_s", C.c_double), ("final_radius", C.c_double), ("final_mu", C.c_double)]
+                ("total_time_s", C.c_double), ("final_radius", C.c_double), ("final_mu", C.c_double),
+                ("preprocessor_time_s", C.c_double), ("minimizer_time_s", C.c_double),
+                ("postprocessor_time_s", C.c_double), ("linear_solver_time_s", C.c_double),
+                ("residual_evaluation_time_s", C.c_double), ("jacobian_evaluation_time_s", C.c_double),
+                ("step_time_s", C.c_double)]
 
     def as_dict(self):
         d = {k: getattr(self, k) for k, _ in self._fields_}
@@ -170,7 +208,7 @@ EXPORTED_SYMBOLS = [
     "okvisgpu_time_kernel", "okvisgpu_eval_relpose", "okvisgpu_twopose_compute",
     "okvisgpu_graph_load", "okvisgpu_graph_problem", "okvisgpu_graph_ids", "okvisgpu_graph_destroy",
     "okvisgpu_graph_save", "okvisgpu_get_stats", "okvisgpu_synth_true_extrinsics", "okvisgpu_imu_append",
-    "okvisgpu_eval_host", "okvisgpu_plan_window",
+    "okvisgpu_eval_host", "okvisgpu_plan_window", "okvisgpu_loss_evaluate",
 ]
 N_PHASES = 15
 
@@ -232,6 +270,7 @@ def lib():
         L.okvisgpu_plan_window.argtypes = [C.POINTER(Problem), C.c_int32, _lp, C.POINTER(C.c_uint8), _ip, _ip]
         L.okvisgpu_imu_append.argtypes = [C.c_void_p, C.POINTER(ImuAppendBatch), _ip]
         L.okvisgpu_twopose_compute.argtypes = [C.c_void_p, C.POINTER(TwoPoseEdges), _dp, _dp, _dp, _dp, _dp]
+        L.okvisgpu_loss_evaluate.argtypes = [C.POINTER(Loss), C.c_double, _dp]
         _lib = L
     return _lib
 

@@ -144,4 +144,9 @@ void oracle_pose_plus(const double* x, const double* delta, double* out);
 void oracle_pose_plus_jacobian(const double* x, double* J76);
 void oracle_pose_minus_jacobian(const double* x, double* J67);
 int oracle_dense_cholesky(int32_t n, double* A, int32_t num_threads); /* lower, in place; 0 = ok */
+/* ::ceres::LossFunction::Evaluate restated (rho, rho', rho''), okvisgpu_loss_kind */
+int oracle_loss_evaluate(const okvisgpu_loss* loss, double s, double* rho);
+/* Ceres' Corrector on one residual block: r [nres] and J [nres][ncols] (may be NULL) corrected in
+ * place, cost = rho(|r|^2)/2 */
+int oracle_loss_correct(const okvisgpu_loss* loss, int32_t nres, int32_t ncols, double* r, double* J, double* cost);
 }

@@ -349,6 +349,117 @@ void parallelFor(int n, int nthreads, F f) {
   Pool::get().run(nt, job);
 }
 
+// ::ceres::LossFunction::Evaluate of the loss family a problem can attach to host-evaluated
+// factors (okvisgpu.h "robust losses"): rho = (rho(s), rho'(s), rho''(s)) as published in
+// ceres-solver >= 2.1 internal/ceres/loss_function.cc (un-vendored submodule);
+// okvis constructs CauchyLoss(1.0), CauchyLoss(3.0), TukeyLoss(0.1), TukeyLoss(2.0)
+// (okvis_ceres/src/ViGraph.cpp:235-238).
+void lossEvaluate(const okvisgpu_loss& L, double s, double rho[3]) {
+  const double a = L.a, dmin = std::numeric_limits<double>::min();
+  switch (L.kind) {
+    case OKVISGPU_LOSS_CAUCHY: {  // b = a^2, c = 1/b: b log(1 + s c)
+      const double b = a * a, c = 1.0 / b, sum = 1.0 + s * c, inv = 1.0 / sum;
+      rho[0] = b * std::log(sum);
+      rho[1] = std::max(dmin, inv);
+      rho[2] = -c * (inv * inv);
+      break;
+    }
+    case OKVISGPU_LOSS_TUKEY: {  // a^2/3 (1 - (1 - s/a^2)^3) inside, a^2/3 outside
+      const double a2 = a * a;
+      if (s <= a2) {
+        const double v = 1.0 - s / a2, v2 = v * v;
+        rho[0] = a2 / 3.0 * (1.0 - v2 * v);
+        rho[1] = v2;
+        rho[2] = -2.0 / a2 * v;
+      } else {
+        rho[0] = a2 / 3.0;
+        rho[1] = 0.0;
+        rho[2] = 0.0;
+      }
+      break;
+    }
+    case OKVISGPU_LOSS_HUBER: {
+      const double b = a * a;
+      if (s > b) {
+        const double r = std::sqrt(s);
+        rho[0] = 2.0 * a * r - b;
+        rho[1] = std::max(dmin, a / r);
+        rho[2] = -rho[1] / (2.0 * s);
+      } else {
+        rho[0] = s;
+        rho[1] = 1.0;
+        rho[2] = 0.0;
+      }
+      break;
+    }
+    case OKVISGPU_LOSS_SOFTLONE: {
+      const double b = a * a, c = 1.0 / b, sum = 1.0 + s * c, t = std::sqrt(sum);
+      rho[0] = 2.0 * b * (t - 1.0);
+      rho[1] = std::max(dmin, 1.0 / t);
+      rho[2] = -(c * rho[1]) / (2.0 * sum);
+      break;
+    }
+    case OKVISGPU_LOSS_ARCTAN: {
+      const double b = 1.0 / (a * a), sum = 1.0 + s * s * b, inv = 1.0 / sum;
+      rho[0] = a * std::atan2(s, a);
+      rho[1] = std::max(dmin, inv);
+      rho[2] = -2.0 * s * b * (inv * inv);
+      break;
+    }
+    case OKVISGPU_LOSS_TOLERANT: {  // b log(1 + e^((s-a)/b)) - b log(1 + e^(-a/b))
+      const double b = L.b, c = b * std::log(1.0 + std::exp(-a / b)), x = (s - a) / b;
+      if (x > 36.7) {  // ln(2^53): 1 + e^x == e^x
+        rho[0] = s - a - c;
+        rho[1] = 1.0;
+        rho[2] = 0.0;
+      } else {
+        const double e = std::exp(x);
+        rho[0] = b * std::log(1.0 + e) - c;
+        rho[1] = std::max(dmin, e / (1.0 + e));
+        rho[2] = 0.5 / (b * (1.0 + std::cosh(x)));
+      }
+      break;
+    }
+    default:
+      rho[0] = s;
+      rho[1] = 1.0;
+      rho[2] = 0.0;
+  }
+}
+
+// Ceres' Corrector (internal/ceres/corrector.cc; okvis restates it at TwoPoseGraphError.cpp:292-337)
+// on the raw residual rr (squared norm sq) and the minimal (tangent-space) Jacobian, as Ceres'
+// ResidualBlock applies it after the manifold: returns the cost rho(sq)/2; res (may be NULL) =
+// corrected residual; jac (may be NULL; row-major nres x ncols) corrected in place. rho'' <= 0 or
+// sq = 0: r and J scaled by sqrt(rho'); rho'' > 0: alpha = 1 - sqrt(1 + 2 sq rho''/rho'), r scaled by
+// sqrt(rho')/(1 - alpha), J <- sqrt(rho') (J - alpha/sq r (r^T J)), column by column.
+double applyCorrector(const okvisgpu_loss& loss, int nres, int ncols, const double* rr, double sq, double* res,
+                      double* jac) {
+  double rho[3];
+  lossEvaluate(loss, sq, rho);
+  const double sqrtRho1 = std::sqrt(rho[1]);
+  double scale = sqrtRho1, alphaSq = 0.0;
+  if (sq != 0.0 && rho[2] > 0.0) {
+    const double D = 1.0 + 2.0 * sq * rho[2] / rho[1];
+    const double alpha = 1.0 - std::sqrt(D);
+    scale = sqrtRho1 / (1.0 - alpha);
+    alphaSq = alpha / sq;
+  }
+  if (res)
+    for (int i = 0; i < nres; ++i) res[i] = rr[i] * scale;
+  if (jac)
+    for (int c = 0; c < ncols; ++c) {
+      if (alphaSq == 0.0) {
+        for (int i = 0; i < nres; ++i) jac[i * ncols + c] *= sqrtRho1;
+        continue;
+      }
+      double rtj = 0.0;
+      for (int i = 0; i < nres; ++i) rtj += jac[i * ncols + c] * rr[i];
+      for (int i = 0; i < nres; ++i) jac[i * ncols + c] = sqrtRho1 * (jac[i * ncols + c] - alphaSq * rr[i] * rtj);
+    }
+  return 0.5 * rho[0];
+}
+
 // Evaluate one residual block: residuals (corrected), local Jacobian (corrected, row-major
 // nres x jcols over the ACTIVE blocks in parameter order), cost contribution.
 double evalResidual(Program& P, const std::vector<double>& x, int ri, double* res, double* jac,
@@ -364,6 +475,7 @@ double evalResidual(Program& P, const std::vector<double>& x, int ri, double* re
       if (P.pbs[r.pb[k]].active) ja[k] = ambJ[k];
   double rr[15];
   bool useLoss = false;
+  okvisgpu_loss loss{OKVISGPU_LOSS_CAUCHY, 0, 1.0, 0.0};  // CauchyLoss(1) unless a host factor says otherwise
   switch (r.kind) {
     case rReproj: {
       const int o = r.index;
@@ -402,24 +514,20 @@ double evalResidual(Program& P, const std::vector<double>& x, int ri, double* re
         if (jac) for (int i = 0; i < r.nres * r.jcols; ++i) jac[i] = 0.0;
         return HUGE_VAL;
       }
-      useLoss = p->host_cauchy ? p->host_cauchy[r.index] != 0 : false;
+      if (p->host_loss) {  // ABI 6: the factor's own loss
+        loss = p->host_loss[r.index];
+        useLoss = loss.kind != OKVISGPU_LOSS_NONE;
+      } else {
+        useLoss = p->host_cauchy ? p->host_cauchy[r.index] != 0 : false;
+      }
       break;
     }
   }
   double sq = 0;
   for (int i = 0; i < r.nres; ++i) sq += rr[i] * rr[i];
-  double cost, scale = 1.0;
-  if (useLoss) {  // CauchyLoss(1): rho = [log(1+s), max(DBL_MIN, 1/(1+s)), -1/(1+s)^2]
-    const double sum = 1.0 + sq;
-    const double inv = 1.0 / sum;
-    cost = 0.5 * std::log(sum);
-    // Corrector (rho'' < 0 branch): residual and Jacobian scaled by sqrt(rho')
-    scale = std::sqrt(std::max(DBL_MIN, inv));
-  } else {
-    cost = 0.5 * sq;
-  }
+  double cost = 0.5 * sq;
   if (res)
-    for (int i = 0; i < r.nres; ++i) res[i] = rr[i] * scale;
+    for (int i = 0; i < r.nres; ++i) res[i] = rr[i];
   if (jac) {
     // local Jacobian = ambient * PlusJacobian (Ceres ResidualBlock with manifold)
     int col = 0;
@@ -433,18 +541,19 @@ double evalResidual(Program& P, const std::vector<double>& x, int ri, double* re
           for (int c = 0; c < 6; ++c) {
             double s = 0;
             for (int a = 0; a < 7; ++a) s += ambJ[k][i * 7 + a] * Jp[a * 6 + c];
-            jac[i * r.jcols + col + c] = s * scale;
+            jac[i * r.jcols + col + c] = s;
           }
       } else if (b.kind == kLm) {
         for (int i = 0; i < r.nres; ++i)
-          for (int c = 0; c < 3; ++c) jac[i * r.jcols + col + c] = ambJ[k][i * 4 + c] * scale;
+          for (int c = 0; c < 3; ++c) jac[i * r.jcols + col + c] = ambJ[k][i * 4 + c];
       } else {
         for (int i = 0; i < r.nres; ++i)
-          for (int c = 0; c < 9; ++c) jac[i * r.jcols + col + c] = ambJ[k][i * 9 + c] * scale;
+          for (int c = 0; c < 9; ++c) jac[i * r.jcols + col + c] = ambJ[k][i * 9 + c];
       }
       col += b.loc;
     }
   }
+  if (useLoss) cost = applyCorrector(loss, r.nres, r.jcols, rr, sq, res, jac);
   return cost;
 }
 
@@ -1089,10 +1198,12 @@ struct Minimizer {
           consecutive_invalid = 0;
         }
       }
-      if (!valid) {  // HandleInvalidStep (the iteration counts as an unsuccessful one)
-        ++num_unsucc;
+      if (!valid) {  // HandleInvalidStep: the next FinalizeIteration counts it as unsuccessful
         if (++consecutive_invalid >= o.max_num_consecutive_invalid_steps) {
+          // Ceres returns before FinalizeIteration records this iteration: not counted
+          // (TrustRegionMinimizer::Minimize, `if (!HandleInvalidStep()) return;`)
           termination = OKVISGPU_FAILURE;
+          --iteration;
           break;
         }
         mu *= 10.0;  // StepIsInvalid
@@ -1473,5 +1584,23 @@ void oracle_pose_plus(const double* x, const double* delta, double* out) { poseP
 void oracle_pose_plus_jacobian(const double* x, double* J) { posePlusJacobian(x, J); }
 void oracle_pose_minus_jacobian(const double* x, double* J) { poseMinusJacobian(x, J); }
 int oracle_dense_cholesky(int32_t n, double* A, int32_t num_threads) { return denseCholesky(n, A, num_threads); }
+
+int oracle_loss_evaluate(const okvisgpu_loss* loss, double s, double* rho) {
+  if (!loss || !rho) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  lossEvaluate(*loss, s, rho);
+  return OKVISGPU_OK;
+}
+
+int oracle_loss_correct(const okvisgpu_loss* loss, int32_t nres, int32_t ncols, double* r, double* J, double* cost) {
+  if (!loss || !r || nres < 1 || nres > 15) return OKVISGPU_ERR_INVALID_ARGUMENT;
+  double rr[15], sq = 0.0;
+  for (int i = 0; i < nres; ++i) {
+    rr[i] = r[i];
+    sq += r[i] * r[i];
+  }
+  const double c = applyCorrector(*loss, nres, ncols, rr, sq, r, J);
+  if (cost) *cost = c;
+  return OKVISGPU_OK;
+}
 
 }  // extern "C"

@@ -40,6 +40,8 @@ def lib():
         L.oracle_imu_merge.argtypes = [P, C.c_int32, _dp, _dp]
         L.oracle_twopose_compute.argtypes = [C.POINTER(og.TwoPoseEdges), _dp, _dp, _dp, _dp, _dp]
         L.oracle_imu_append.argtypes = [C.POINTER(og.ImuAppendBatch), _ip]
+        L.oracle_loss_evaluate.argtypes = [C.POINTER(og.Loss), C.c_double, _dp]
+        L.oracle_loss_correct.argtypes = [C.POINTER(og.Loss), C.c_int32, C.c_int32, _dp, _dp, _dp]
         _lib = L
     return _lib
 
@@ -49,6 +51,14 @@ def solve(problem_ptr, options):
     rc = lib().oracle_solve(problem_ptr, C.byref(options), C.byref(s))
     assert rc == 0
     return s.as_dict()
+
+
+def loss_evaluate(kind, a=1.0, b=0.0, s=0.0):
+    """The oracle's ::ceres::LossFunction::Evaluate restatement: (rho, rho', rho'')."""
+    L = og.Loss(og.LOSS_KINDS[kind] if isinstance(kind, str) else int(kind), 0, a, b)
+    rho = (C.c_double * 3)()
+    assert lib().oracle_loss_evaluate(C.byref(L), float(s), rho) == 0
+    return tuple(rho)
 
 
 def evaluate(problem_ptr):

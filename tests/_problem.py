@@ -56,6 +56,7 @@ class OwnedProblem:
         self.imu_sample_gyr_acc = np.zeros((0, 6))
         self.imu_params = og.ImuParams()
         self.host_fn = None  # og.host_evaluate(...) callback of the host factors (ABI 5)
+        self.host_loss = None  # og.loss_array(...) per host factor (ABI 6), None = host_cauchy
         self.struct = og.Problem()
         self.bind()
 
@@ -105,6 +106,12 @@ class OwnedProblem:
         s.n_extrinsics_priors = len(self.extrinsics_prior_camera)
         s.n_host = len(self.host_dim)
         s.host_evaluate = self.host_fn if self.host_fn is not None else og.HOST_EVALUATE_FN()
+        if self.host_loss is not None:
+            self.host_loss = np.ascontiguousarray(self.host_loss, dtype=og.LOSS_DTYPE)
+            assert len(self.host_loss) == s.n_host
+            s.host_loss = self.host_loss.ctypes.data
+        else:
+            s.host_loss = None
         if len(self.extrinsics_constant) != len(self.cameras):  # default: constant extrinsics
             self.extrinsics_constant = np.ones(len(self.cameras), np.uint8)
             s.extrinsics_constant = self.extrinsics_constant.ctypes.data_as(_up) if len(self.cameras) else None

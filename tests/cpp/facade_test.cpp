@@ -82,6 +82,9 @@ struct CeresLikeOptions {
 };
 struct CeresLikeSummary {
   double initial_cost = -1, final_cost = -1, total_time_in_seconds = -1;
+  double preprocessor_time_in_seconds = -2, minimizer_time_in_seconds = -2, postprocessor_time_in_seconds = -2;
+  double linear_solver_time_in_seconds = -2, residual_evaluation_time_in_seconds = -2,
+         jacobian_evaluation_time_in_seconds = -2;
   int num_successful_steps = -1, num_unsuccessful_steps = -1;
   CeresLikeTermination termination_type = CeresLikeTermination::FAILURE;
 };
@@ -296,7 +299,7 @@ int cpuTests() {
     CHECK(hf.typeInfo() == "GpsErrorAsynchronous" && hf.residualDim() == 3 && hf.parameterBlockSizes().size() == 3);
     auto rg = P.AddResidualBlock(&hf, nullptr, T0, sb0, Tsc);
     const okvisgpu_problem& w = P.view();
-    CHECK(w.n_host == 1 && w.host_dim[0] == 3 && w.host_cauchy[0] == 0);
+    CHECK(w.n_host == 1 && w.host_dim[0] == 3 && w.host_cauchy == nullptr && w.host_loss[0].kind == OKVISGPU_LOSS_NONE);
     CHECK(w.host_param_kind[0] == 0 && w.host_param_kind[1] == 1 && w.host_param_kind[2] == 0 && w.host_param_kind[3] == -1);
     CHECK(w.host_param_index[0] == 0 && w.host_param_index[1] == 0 && w.host_param_index[2] == w.n_poses);
     const double* prm[3] = {T0, sb0, Tsc};
@@ -350,9 +353,54 @@ int cpuTests() {
   threw = false;
   try { P.AddResidualBlock(&prior, nullptr, sb0); } catch (const okvisgpu::Error&) { threw = true; }
   CHECK(threw);
-  threw = false;
-  try { okvisgpu::CauchyLoss c2(2.0); (void)c2; } catch (const okvisgpu::Unsupported&) { threw = true; }
-  CHECK(threw);
+  // the four losses ViGraph's constructor builds (ViGraph.cpp:235-238), ::ceres::LossFunction::Evaluate
+  {
+    okvisgpu::CauchyLoss cauchyLoss(1.0), cauchyGpsLoss(3.0);
+    okvisgpu::TukeyLoss tukeyDepthLoss(0.1), tukeyLidarLoss(2.0);
+    double rho[3];
+    cauchyGpsLoss.Evaluate(9.0, rho);  // b log(1 + s/b), b = 9
+    CHECK(std::fabs(rho[0] - 9.0 * std::log(2.0)) < 1e-14 && std::fabs(rho[1] - 0.5) < 1e-15 &&
+          std::fabs(rho[2] + 1.0 / 36.0) < 1e-15);
+    cauchyLoss.Evaluate(3.0, rho);
+    CHECK(std::fabs(rho[0] - std::log(4.0)) < 1e-15 && rho[1] == 0.25);
+    tukeyLidarLoss.Evaluate(1.0, rho);  // a^2/3 (1 - (1 - s/a^2)^3), rho' = (1 - s/a^2)^2
+    CHECK(std::fabs(rho[0] - 4.0 / 3.0 * (1.0 - 27.0 / 64.0)) < 1e-15 && rho[1] == 0.5625 && rho[2] == -0.375);
+    tukeyLidarLoss.Evaluate(5.0, rho);  // outlier: constant cost, no gradient
+    CHECK(std::fabs(rho[0] - 4.0 / 3.0) < 1e-15 && rho[1] == 0.0 && rho[2] == 0.0);
+    tukeyDepthLoss.Evaluate(0.02, rho);
+    CHECK(rho[1] == 0.0 && std::fabs(rho[0] - 0.01 / 3.0) < 1e-17);
+    CHECK(std::string(tukeyLidarLoss.name()) == "TukeyLoss" && cauchyGpsLoss.a() == 3.0);
+    // reprojections take CauchyLoss(1.0) only (the device's); host factors take any of them
+    okvisgpu::Problem Q;
+    double Ta[7] = {0, 0, 0, 0, 0, 0, 1}, Tb[7] = {1, 0, 0, 0, 0, 0, 1}, Ex[7] = {0, 0, 0, 0, 0, 0, 1};
+    double La[4] = {0, 0, 5, 1}, sa[9] = {};
+    Q.AddParameterBlock(Ta, 7, &pm);
+    Q.AddParameterBlock(Tb, 7, &pm);
+    Q.AddParameterBlock(Ex, 7, &pm);
+    Q.AddParameterBlock(La, 4, &hm);
+    okvisgpu::ReprojectionError ea(cam, kp, Li);
+    threw = false;
+    try { Q.AddResidualBlock(&ea, &cauchyGpsLoss, Ta, La, Ex); } catch (const okvisgpu::Unsupported&) { threw = true; }
+    CHECK(threw);
+    Q.AddResidualBlock(&ea, &cauchyLoss, Ta, La, Ex);
+    GpsFunctor g;
+    okvisgpu::HostFunctor<GpsFunctor> hg(&g);
+    struct SubmapLike final : okvisgpu::HostCostFunction {  // SubmapIcpError's blocks: (pose A, pose B)
+      int residualDim() const override { return 1; }
+      std::vector<int> parameterBlockSizes() const override { return {7, 7}; }
+      bool Evaluate(double const* const*, double* r, double**) const override { r[0] = 0.0; return true; }
+    } sm;
+    Q.AddResidualBlock(&hg, &cauchyGpsLoss, Ta, sa, Ex);
+    Q.AddResidualBlock(&sm, &tukeyLidarLoss, Ta, Tb);
+    Q.AddResidualBlock(&sm, &tukeyDepthLoss, Ta, Tb);
+    const okvisgpu_problem& v = Q.view();
+    CHECK(v.n_host == 3 && v.host_loss[0].kind == OKVISGPU_LOSS_CAUCHY && v.host_loss[0].a == 3.0);
+    CHECK(v.host_loss[1].kind == OKVISGPU_LOSS_TUKEY && v.host_loss[1].a == 2.0 && v.host_loss[2].a == 0.1);
+    CHECK(v.obs_cauchy[0] == 1);
+    threw = false;
+    try { okvisgpu::TukeyLoss bad(-1.0); (void)bad; } catch (const okvisgpu::Error&) { threw = true; }
+    CHECK(threw);
+  }
   // one VARIABLE extrinsics block seen with two different intrinsics would become two independent
   // ABI blocks: rejected (a constant one is fine: two ABI cameras sharing the same constant T_SC)
   {
@@ -397,11 +445,16 @@ int cpuTests() {
     okvisgpu_summary s{};
     s.initial_cost = 3.0; s.final_cost = 1.0; s.num_successful_steps = 4; s.num_unsuccessful_steps = 2;
     s.termination_type = OKVISGPU_USER_SUCCESS; s.total_time_s = 0.5;
+    s.preprocessor_time_s = 0.1; s.minimizer_time_s = 0.3; s.postprocessor_time_s = 0.1;
+    s.linear_solver_time_s = 0.2; s.residual_evaluation_time_s = 0.04; s.jacobian_evaluation_time_s = 0.05;
     CeresLikeSummary cs;
     okvisgpu::toSummary(s, &cs);
     CHECK(cs.initial_cost == 3.0 && cs.final_cost == 1.0 && cs.num_successful_steps == 4 &&
           cs.num_unsuccessful_steps == 2 && cs.termination_type == CeresLikeTermination::USER_SUCCESS &&
           cs.total_time_in_seconds == 0.5);
+    CHECK(cs.preprocessor_time_in_seconds == 0.1 && cs.minimizer_time_in_seconds == 0.3 &&
+          cs.postprocessor_time_in_seconds == 0.1 && cs.linear_solver_time_in_seconds == 0.2 &&
+          cs.residual_evaluation_time_in_seconds == 0.04 && cs.jacobian_evaluation_time_in_seconds == 0.05);
   }
   // no device in this container: Solve reports the C ABI's status instead of crashing
   int32_t ndev = 0;

@@ -27,7 +27,7 @@ def _run(consumers, exe, mode):
 def test_c_consumer_cpu(consumers):
     r = _run(consumers, "abi_consumer", "cpu")
     assert r.returncode == 0, r.stderr
-    assert "abi_consumer cpu ok: ABI 5, 10 poses / 500 landmarks / 4000 observations" in r.stdout
+    assert "abi_consumer cpu ok: ABI 6, 10 poses / 500 landmarks / 4000 observations" in r.stdout
 
 
 def test_facade_cpu(consumers):

@@ -550,3 +550,74 @@ def test_large_window_parity(og, oracle, gpu_ctx):
     so = oracle.solve(w.problem_ptr(), opts)
     _close(sg, so, rel=1e-6)
     assert np.abs(P[:, :3] - w.poses()[:, :3]).max() <= 1e-6
+
+
+def _window_with_degenerate_state(og, seed, j=25):
+    """An S50 window with an extra state (pose + speed/bias, index j) whose only residual is a
+    host-evaluated constant factor: its 15 columns of J are exactly zero. With min_lm_diagonal = 0
+    the LM diagonal adds nothing there, so the diagonal tile holding them has a zero pivot and every
+    Gauss-Newton attempt of this window fails (mu retries, then invalid steps, then FAILURE after
+    max_num_consecutive_invalid_steps), in the middle of the factorisation's chain."""
+    from _problem import OwnedProblem
+    sw = og.SynthWindow(50, 2000, 16000, seed=seed)
+    P = OwnedProblem.copy_of(sw.problem)
+    del sw
+    P.poses = np.insert(P.poses, j, P.poses[j], axis=0)
+    P.speed_biases = np.insert(P.speed_biases, j, P.speed_biases[j], axis=0)
+    P.pose_constant = np.insert(P.pose_constant, j, 0)
+    P.speed_bias_constant = np.insert(P.speed_bias_constant, j, 0)
+    P.obs_pose = np.where(P.obs_pose >= j, P.obs_pose + 1, P.obs_pose)
+    P.imu_blocks = np.where(P.imu_blocks >= j, P.imu_blocks + 1, P.imu_blocks)
+    P.pose_prior_block = np.where(P.pose_prior_block >= j, P.pose_prior_block + 1, P.pose_prior_block)
+    P.sb_prior_block = np.where(P.sb_prior_block >= j, P.sb_prior_block + 1, P.sb_prior_block)
+    P.host_dim = np.array([1], np.int32)
+    P.host_param_kind = np.array([[0, 1, -1, -1]], np.int32)
+    P.host_param_index = np.array([[j, j, -1, -1]], np.int32)
+    P.host_cauchy = np.zeros(1, np.uint8)
+    P.host_fn = og.host_evaluate(lambda h, prm: (np.array([0.1]), [np.zeros((1, 7)), np.zeros((1, 9))]), [[7, 9]])
+    P.bind()
+    return P
+
+
+def test_cholesky_failure_path_all_schedules(og, oracle, gpu_ctx):
+    """A failed factorisation (zero pivot in the middle of one window's chain) in a batch of three
+    S50 windows: the persistent (1), pipelined (4: team F stops, team B sees the failure through
+    pipe[3]) and split pipelined (5) schedules give the same iterations, unsuccessful steps,
+    termination and bits; the failing window's summary is the oracle's; the two healthy windows
+    get the bits they get in a batch without the failing one (same size regime)."""
+    from _problem import OwnedProblem
+    bad = _window_with_degenerate_state(og, seed=71)
+    good = [OwnedProblem.copy_of(og.SynthWindow(50, 2000, 16000, seed=s).problem) for s in (72, 73)]
+    probs = [good[0], bad, good[1]]
+    snaps = [p.snapshot() for p in probs]
+    opts = dict(max_num_iterations=8, function_tolerance=0.0, gradient_tolerance=0.0, parameter_tolerance=0.0,
+                min_lm_diagonal=0.0)
+    res = []
+    for sched in (1, 4, 5):
+        for p, s in zip(probs, snaps):
+            p.restore(s)
+        gpu_ctx.set_problems([p.struct for p in probs])
+        if sched == 5:
+            assert gpu_ctx.stats()["cholesky_split_windows"] >= 2
+        s = gpu_ctx.solve(og.default_options(cholesky_schedule=sched, **opts), len(probs))
+        res.append((s, [p.poses.copy() for p in probs]))
+    key = lambda s: (s["num_iterations"], s["num_successful_steps"], s["num_unsuccessful_steps"], s["termination"])  # noqa: E731
+    for r in res[1:]:
+        for k in range(len(probs)):
+            assert key(r[0][k]) == key(res[0][0][k]), (k, r[0][k], res[0][0][k])
+            assert r[0][k]["final_cost"] == res[0][0][k]["final_cost"], k
+            assert np.array_equal(r[1][k], res[0][1][k]), k
+    sb = res[0][0][1]
+    assert sb["termination"] == "FAILURE" and sb["num_successful_steps"] == 1, sb
+    bad.restore(snaps[1])
+    so = oracle.solve(bad.ptr(), og.default_options(**opts))
+    assert key(so) == key(sb), (so, sb)
+    assert abs(so["final_cost"] - sb["final_cost"]) <= 1e-9 * so["final_cost"]
+    # the healthy windows: as in a batch of their own
+    for p, s in zip(good, (snaps[0], snaps[2])):
+        p.restore(s)
+    gpu_ctx.set_problems([p.struct for p in good])
+    sg = gpu_ctx.solve(og.default_options(cholesky_schedule=1, **opts), len(good))
+    for k, i in ((0, 0), (1, 2)):
+        assert key(sg[k]) == key(res[0][0][i]) and sg[k]["final_cost"] == res[0][0][i]["final_cost"], (k, sg[k])
+        assert np.array_equal(good[k].poses, res[0][1][i])
