@@ -619,14 +619,6 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
   }
 }
 
-__global__ __launch_bounds__(64) void k_hold(int rounds) {
-  for (int r = 0; r < rounds; ++r) __builtin_amdgcn_s_sleep(127);  // ~127 x 64 clocks each
-}
-void launch_hold(hipStream_t s, int us) {
-  const int rounds = us * 2400 / (127 * 64) + 1;  // 2.4 GHz shader clock (calibrated)
-  hipLaunchKernelGGL(k_hold, dim3(1), dim3(64), 0, s, rounds);
-}
-
 // The factors' J*v on their own: in the iteration they are the trailing workgroups of
 // k_lm_backsub_jv (launch_lm_backsub); this launch serves okvisgpu_time_kernel's table.
 __global__ __launch_bounds__(256) void k_jv(const DevProblem* __restrict__ Pp) { jvGroups(*Pp, (int)blockIdx.x); }

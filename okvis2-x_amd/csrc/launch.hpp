@@ -57,10 +57,6 @@ void launch_jv(const DevProblem& P, hipStream_t s);  // (standalone, for okvisgp
 void launch_gradnorm(const DevProblem& P, int lin_mode, hipStream_t s);
 void launch_dogleg(const DevProblem& P, hipStream_t s);
 void launch_select_current(const DevProblem& P, hipStream_t s);  // set 1 -> set 0 where xcur == 1
-// A one-wavefront kernel that idles ~`us` microseconds (s_sleep, no memory traffic): launched ahead
-// of an eagerly timed sequence, it holds the stream while the host enqueues the rest, so the HIP
-// events between the following kernels measure device time, not host launch gaps.
-void launch_hold(hipStream_t s, int us);
 
 // pose-graph edges (kernels_twopose.hip): TwoPoseStandardGraphError::compute, one wavefront per edge
 void launch_twopose_compute(const TwoPoseDev& T, hipStream_t s);

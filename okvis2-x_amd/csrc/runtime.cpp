@@ -1587,9 +1587,6 @@ struct okvisgpu_ctx {
       ev.push_back(e);
       phaseOf.push_back(phase);
     };
-    // the stream is held while the rest is enqueued: the events then bracket back-to-back device
-    // work as in the captured graph, not the host's launch rate
-    launch_hold(s, 400);
     mark(-1);
     launch_lm_prep(P, s); mark(0);
     mark(1);  // (S is no longer cleared per iteration: phase kept for the ABI's phase list)

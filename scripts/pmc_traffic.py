@@ -1,6 +1,6 @@
 """Turn rocprofv3 --pmc passes (scripts/gpu_pmc.sh) into profiles/pmc_traffic.json: HBM bytes per
 dispatch of each kernel. FETCH_SIZE / WRITE_SIZE are in KiB; FETCH_SIZE is doubled, WRITE_SIZE taken
-as is: the calibration of scripts/pmc_calib.hip (profiles/r03_pmc_calib.json) measured exactly these
+as is: the calibration of scripts/pmc_calib.hip (profiles/rNN_pmc_calib.json, re-measured each round) measured exactly these
 factors for every access shape these kernels use (16 B and 8 B per lane, the Cholesky's tile rows),
 on a buffer four times the Infinity Cache.
 
@@ -9,6 +9,7 @@ batch; bench.py scales bytes_per_window_iteration by its own windows per GPU).""
 import collections
 import csv
 import json
+import os
 import sys
 
 out = sys.argv[1]
@@ -42,6 +43,6 @@ for k, d in vals.items():
     if "bytes_per_iteration" in kern[k]:
         kern[k]["bytes_per_window_iteration"] = kern[k]["bytes_per_iteration"] / windows
 json.dump({"source": sys.argv[3:], "windows": windows,
-           "correction": "FETCH_SIZE x2, WRITE_SIZE x1 (calibrated: profiles/r03_pmc_calib.json), KiB -> bytes",
+           "correction": "FETCH_SIZE x2, WRITE_SIZE x1 (calibrated: " + os.environ.get("PMC_CALIB_FILE", "profiles/r06_pmc_calib.json") + "), KiB -> bytes",
            "kernels": kern}, open(out, "w"), indent=1, sort_keys=True)
 print(json.dumps({k: round(v["bytes_per_dispatch"] / 1e9, 3) for k, v in kern.items()}, indent=0))
