@@ -723,6 +723,71 @@ class Problem {
     return okvisgpu_evaluate(ctx_, 0, cost);
   }
 
+  // ::ceres::Problem::EvaluateResidualBlock(id, apply_loss_function, &cost, residuals, jacobians) at the
+  // caller's current parameter values (okvis: the GPS residual dump, ViGraph.hpp:553, which passes no
+  // Jacobians). Host cost functions are evaluated on the host through their Evaluate; the GPU terms
+  // (ReprojectionError, ImuError, TwoPose / RelativePose edges) through the C ABI's evaluation hooks
+  // (the problem is uploaded or its values refreshed first). With apply_loss_function the cost is
+  // rho(|r|^2)/2 and r is corrected as Ceres' Corrector does; else cost = |r|^2/2 and the raw r. An
+  // ImuError residual is U e with the device's square-root information U (any U with U^T U = the
+  // reference's information, DESIGN.md §5: |r| and the cost are the reference's, the components may
+  // differ by an orthogonal factor), and the evaluation may re-integrate on the device as
+  // ImuError::Evaluate would (not written back into the term). Returns false if a host term's
+  // Evaluate fails; Jacobians and the prior terms (PoseError, SpeedAndBiasError) throw Unsupported.
+  bool EvaluateResidualBlock(ResidualBlockId id, bool apply_loss_function, double* cost, double* residuals,
+                             double** jacobians) {
+    const ResidualBlock* rb = find(id);
+    if (jacobians) throw Unsupported("EvaluateResidualBlock with Jacobians (okvis requests none, ViGraph.hpp:553)");
+    const int dim = rb->cost->residualDim();
+    double r[OKVISGPU_HOST_MAX_RESIDUALS];
+    if (const auto* h = dynamic_cast<const HostCostFunction*>(rb->cost)) {
+      std::vector<const double*> prm(rb->blocks.begin(), rb->blocks.end());
+      if (!h->Evaluate(prm.data(), r, nullptr)) return false;
+    } else {
+      const std::string t = rb->cost->typeInfo();
+      const bool rp = t == "TwoPoseStandardGraphError" || t == "TwoPoseStandardGraphErrorConst" || t == "RelativePoseError";
+      if (t != "ReprojectionError" && t != "ImuError" && !rp)
+        throw Unsupported("EvaluateResidualBlock of " + t + " (no device evaluation hook)");
+      if (!refreshDevice()) throw Error(std::string("EvaluateResidualBlock: ") + last_error());
+      int idx = 0;  // position among the residuals of the same ABI kind (the order build() emits them)
+      for (const auto& o : residuals_) {
+        if (o.get() == id) break;
+        const std::string u = o->cost->typeInfo();
+        const bool urp = u == "TwoPoseStandardGraphError" || u == "TwoPoseStandardGraphErrorConst" || u == "RelativePoseError";
+        if (rp ? urp : u == t) ++idx;
+      }
+      int rc;
+      if (t == "ReprojectionError") {
+        std::vector<double> all(2 * (size_t)view_.n_observations);
+        rc = okvisgpu_eval_reprojection(ctx_, 0, all.data(), nullptr, nullptr);
+        if (rc == OKVISGPU_OK) std::copy(all.begin() + 2 * idx, all.begin() + 2 * idx + 2, r);
+      } else if (t == "ImuError") {
+        std::vector<double> all(15 * (size_t)view_.n_imu);
+        rc = okvisgpu_eval_imu(ctx_, 0, 0, all.data(), nullptr);
+        if (rc == OKVISGPU_OK) std::copy(all.begin() + 15 * idx, all.begin() + 15 * idx + 15, r);
+      } else {
+        std::vector<double> all(6 * (size_t)view_.n_relpose);
+        rc = okvisgpu_eval_relpose(ctx_, 0, all.data(), nullptr);
+        if (rc == OKVISGPU_OK) std::copy(all.begin() + 6 * idx, all.begin() + 6 * idx + 6, r);
+      }
+      if (rc != OKVISGPU_OK) throw Error(std::string("EvaluateResidualBlock: ") + last_error());
+    }
+    double sq = 0.0;
+    for (int i = 0; i < dim; ++i) sq += r[i] * r[i];
+    double c = 0.5 * sq, scale = 1.0;
+    if (apply_loss_function && rb->loss) {  // Ceres' Corrector on the residual (corrector.cc)
+      double rho[3];
+      rb->loss->Evaluate(sq, rho);
+      c = 0.5 * rho[0];
+      scale = std::sqrt(rho[1]);
+      if (sq != 0.0 && rho[2] > 0.0) scale /= std::sqrt(1.0 + 2.0 * sq * rho[2] / rho[1]);  // / (1 - alpha)
+    }
+    if (cost) *cost = c;
+    if (residuals)
+      for (int i = 0; i < dim; ++i) residuals[i] = r[i] * scale;
+    return true;
+  }
+
   const char* last_error() const { return ctx_ ? okvisgpu_last_error(ctx_) : okvisgpu_last_error(nullptr); }
 
   // The C-ABI problem the facade hands to okvisgpu_set_problems (rebuilt from the recorded graph;
@@ -802,6 +867,23 @@ class Problem {
   int ensureContext() {
     if (ctx_) return OKVISGPU_OK;
     return okvisgpu_ctx_create(device_, &ctx_);
+  }
+  // the device holds the recorded graph with the caller's current values (as Solve prepares it)
+  bool refreshDevice() {
+    if (ensureContext() != OKVISGPU_OK) return false;
+    if (dirty_ || !uploaded_) {
+      build();
+      if (okvisgpu_set_problems(ctx_, &view_, 1) != OKVISGPU_OK) return false;
+      uploaded_ = true;
+      dirty_ = false;
+      constDirty_.clear();
+      return true;
+    }
+    gatherValues();
+    for (const auto& kv : constDirty_)
+      if (okvisgpu_set_block_constant(ctx_, 0, kv.first.first, kv.first.second, kv.second) != OKVISGPU_OK) return false;
+    constDirty_.clear();
+    return okvisgpu_update_params(ctx_) == OKVISGPU_OK;
   }
 
   // Flatten the recorded graph into the SoA arrays of okvisgpu_problem. Blocks are ordered by

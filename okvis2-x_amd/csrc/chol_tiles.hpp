@@ -754,15 +754,23 @@ __device__ __forceinline__ const double* bsTile(const double* S, int64_t ld, int
   return UPPER ? S + (int64_t)I * kTile * ld + i * kTile : S + (int64_t)i * kTile * ld + I * kTile;
 }
 // lst: count of non-zero tiles below I (capped at kBsPre), then their block rows ascending.
-// Loads are unconditional (an absent tile reads the diagonal one and is masked): loads under a
-// branch make the wait-count insertion fall back to vmcnt(0).
+// Loads are unconditional (an absent tile is masked in bsPartial): loads under a branch make the
+// wait-count insertion fall back to vmcnt(0). An absent slot re-reads the first listed tile, the same
+// addresses this thread has just requested (served by the caches; it used to read the diagonal tile
+// (I, I), a third of the step's tile traffic on a two-tile band that nothing else reads there), and
+// the diagonal tile only on the last block row, which has none below.
 template <bool UPPER>
 __device__ __forceinline__ void bsLoad(const double* S, int64_t ld, const double* Linv, const int* lst, int I, int vt,
                                        BsOps& o) {
   const int c2 = 2 * (vt & 31), rg = vt >> 5;
+#ifdef OKG_BS_DUMMY_DIAG  // (A/B build knob: the round-5 dummy, the diagonal tile)
+  const int dummy = I;
+#else
+  const int dummy = lst[0] > 0 ? lst[1] : I;
+#endif
 #pragma unroll
   for (int m = 0; m < kBsPre; ++m) {
-    const double* Lt = bsTile<UPPER>(S, ld, I, m < lst[0] ? lst[1 + m] : I) + c2;
+    const double* Lt = bsTile<UPPER>(S, ld, I, m < lst[0] ? lst[1 + m] : dummy) + c2;
 #pragma unroll
     for (int u = 0; u < 2; ++u) o.v[m][u] = *gmem(reinterpret_cast<const double2*>(Lt + (int64_t)(rg + 32 * u) * ld));
   }

@@ -59,7 +59,7 @@ static __device__ unsigned int g_imuDone;
   if (!APPEND && threadIdx.x == 0) {                                                    \
     for (int i_ = 0; i_ < 12; ++i_) atomicAdd(&g_imuClk[i_], iacc[i_]);                 \
     __threadfence();                                                                    \
-    if (atomicAdd(&g_imuDone, 1u) == gridDim.x - 1) {                                   \
+    if (atomicAdd(&g_imuDone, 1u) == (unsigned)((P.n_imu + kImuPerWG - 1) / kImuPerWG) - 1) { \
       printf("IMUCLK pro %llu chain %llu state %llu sqrt %llu resid %llu jac %llu | R %llu Q %llu I %llu S %llu " \
              "P %llu (x10ns)\n", g_imuClk[0], g_imuClk[1], g_imuClk[2], g_imuClk[3], g_imuClk[4], g_imuClk[5], \
              g_imuClk[6], g_imuClk[7], g_imuClk[8], g_imuClk[9], g_imuClk[10]);                               \

@@ -153,7 +153,14 @@ __device__ void loadPre(const double* s, ImuPre& p) {
 constexpr int kImuGroup = 16;
 constexpr int kImuPerWG = 4;
 constexpr int kStepRec = 26;  // dt | dq (4) | a_true (3) | Jr (9) | R(dq)^T (9)
-constexpr int kImuK = 4;      // integration steps per chunk
+constexpr int kImuK = 4;      // integration steps per chunk (batches)
+constexpr int kImuFewChunkWindows = 2;
+#ifndef OKG_IMU_FEW_K
+#define OKG_IMU_FEW_K 16  // (build knob for A/B measurements)
+#endif
+constexpr int kImuKFew = OKG_IMU_FEW_K;  // one or two windows: a chunk covers a 0.1 s keyframe interval's 20 samples
+                              // in two rounds (the step records and products are lane-parallel over a
+                              // chunk, so fewer chunks shorten a single factor's latency chain)
 constexpr int kFStride = 66;  // F_delta blocks of one step (offsets below) | dt | pad (lanes writing
                               // consecutive steps fall on different LDS banks)
 constexpr int kS = 17;        // row stride of the 16x16 LDS matrices: lanes walking a column hit
@@ -161,14 +168,17 @@ constexpr int kS = 17;        // row stride of the 16x16 LDS matrices: lanes wal
 // per-group LDS (doubles) during the chain: step records, Delta_q and cross_ after each step (slot
 // 0 = before the chunk), C_1 Jr, C + C_1, (C + C_1) a, X, F_delta, noise; the P exchange (15 x kS)
 // reuses the first 255. After the chain: P / U (sA, 16 x kS), L / eigenvectors (sB, 16 x kS),
-// Jacobi rotations (sR, 32).
-constexpr int kLRec = 0, kLQ1 = kLRec + kImuK * kStepRec, kLCr = kLQ1 + 4 * (kImuK + 1),
-              kLCj = kLCr + 9 * (kImuK + 1), kLM = 0, kLCc = 256, kLCa = kLCc + 9 * kImuK, kLXx = kLCa + 3 * kImuK,
-              kLF = kLXx + 9 * kImuK, kLNz = kLF + kFStride * kImuK, kLCarry = kLNz + 5 * kImuK,
-              kImuLds = kLCarry + 13;
-static_assert(kLCj + 9 * kImuK <= kLCc && 15 * kS <= kLCc, "chain records / P exchange overlap the sums");
-static_assert(kImuLds >= 32 * kS + 32, "the square-root phase needs sA, sB and sR");
-static_assert(kImuLds * 8 * 4 <= 20480, "LDS for eight workgroups (two waves per SIMD) per CU");
+// Jacobi rotations (sR, 32). K = steps per chunk.
+template <int K>
+struct ImuLds {
+  static constexpr int rec = 0, q1 = rec + K * 26 /* kStepRec */, cr = q1 + 4 * (K + 1), cj = cr + 9 * (K + 1),
+                       m = 0, cc = (cj + 9 * K > 256 ? cj + 9 * K : 256), ca = cc + 9 * K, xx = ca + 3 * K,
+                       f = xx + 9 * K, nz = f + kFStride * K, carry = nz + 5 * K, total = carry + 13;
+  static_assert(cj + 9 * K <= cc && 15 * kS <= cc, "chain records / P exchange overlap the sums");
+  static_assert(total >= 32 * kS + 32, "the square-root phase needs sA, sB and sR");
+};
+static_assert(ImuLds<kImuK>::total * 8 * 4 <= 20480, "LDS for eight workgroups (two waves per SIMD) per CU");
+static_assert(ImuLds<kImuKFew>::total * 8 * 4 <= 80 * 1024, "two few-window workgroups per CU");
 
 // F_delta (ImuError.cpp:395-410) of one step in LDS: non-identity 3x3 blocks
 constexpr int kF03 = 0, kF09 = 9, kF012 = 18, kF39 = 27, kF63 = 36, kF69 = 45, kF612 = 54, kFdt = 63;
@@ -295,8 +305,9 @@ __device__ void groupJacobi(double* A, double* V, double* rot, int l, bool need)
 // t1), integrates the appended samples with the eliminated state's bias (sb[0] row blk[1]) up to
 // imu_t1, and writes the state and the new square-root information; no residual.
 __device__ __noinline__ void evalPriorsThread(const DevProblem& P, int t, int mode);
-template <bool APPEND>
+template <bool APPEND, int K = kImuK>
 __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int bid) {
+  using LY = ImuLds<K>;
   if (!APPEND) {  // the trailing workgroups: priors and pose-graph edges (uniform per workgroup)
     const int nImuWG = (P.n_imu + kImuPerWG - 1) / kImuPerWG;
     if (bid >= nImuWG) {
@@ -308,10 +319,10 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
   const int f = bid * kImuPerWG + g;
   ICLK_INIT
 
-  // per-group LDS: the chain's records (layout at kLRec..kLNz above), then symmetric P / Jacobi
+  // per-group LDS: the chain's records (layout ImuLds<K> above), then symmetric P / Jacobi
   // matrix / U (sA, row-major 16x16); L (column-major) / Jacobi eigenvectors (sB); Jacobi rotations
   // (sR). 19 KB per workgroup: two workgroups (waves) per SIMD.
-  __shared__ double sAll[kImuPerWG][kImuLds];
+  __shared__ double sAll[kImuPerWG][LY::total];
   double* sG = sAll[g];
   double* sA = sG;
   double* sB = sG + 16 * kS;
@@ -383,7 +394,7 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
   double Pc[15];  // column l of P
   for (int i = 0; i < 15; ++i) Pc[i] = 0.0;
   int steps = 0;
-  double* const carry = sG + kLCarry;  // Delta_q (4) | cross_ (9) between chunks
+  double* const carry = sG + LY::carry;  // Delta_q (4) | cross_ (9) between chunks
   if (l == 0) {
     carry[0] = 0.0; carry[1] = 0.0; carry[2] = 0.0; carry[3] = 1.0;
     for (int i = 0; i < 9; ++i) carry[4 + i] = 0.0;
@@ -409,7 +420,7 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
 
   ICLK(0)
   // ---- redoPreintegration (ImuError.cpp:258-466), uniform trip count over the wavefront, in
-  // chunks of kImuK steps and five phases per chunk, so that no phase holds more than its own
+  // chunks of K steps and five phases per chunk, so that no phase holds more than its own
   // working set in registers (the single-pass form carried ~140 live doubles per lane and spilled):
   //  R  (lane k, parallel)  step record: dt, interpolated samples, dq = exp(w dt), Jr(w dt),
   //                         R(dq)^T, the noise of the step. The integration time before step `it`
@@ -429,18 +440,18 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
     Nmax = max(Nmax, __shfl_xor(Nmax, 16, 64));
     Nmax = max(Nmax, __shfl_xor(Nmax, 32, 64));
     bool started = false;  // hasStarted: an earlier step was integrated
-    double* const rec = sG + kLRec;
-    double* const q1 = sG + kLQ1;
-    double* const cr = sG + kLCr;
-    double* const cj = sG + kLCj;
-    double* const cc = sG + kLCc;
-    double* const ca = sG + kLCa;
-    double* const xx = sG + kLXx;
-    double* const Fs = sG + kLF;
-    double* const nz = sG + kLNz;
-    double* const M = sG + kLM;      // (phase P; aliases the records, q1, cr and cj)
-    for (int c0 = 0; c0 < Nmax; c0 += kImuK) {
-      const int nk = min(kImuK, Nmax - c0);
+    double* const rec = sG + LY::rec;
+    double* const q1 = sG + LY::q1;
+    double* const cr = sG + LY::cr;
+    double* const cj = sG + LY::cj;
+    double* const cc = sG + LY::cc;
+    double* const ca = sG + LY::ca;
+    double* const xx = sG + LY::xx;
+    double* const Fs = sG + LY::f;
+    double* const nz = sG + LY::nz;
+    double* const M = sG + LY::m;      // (phase P; aliases the records, q1, cr and cj)
+    for (int c0 = 0; c0 < Nmax; c0 += K) {
+      const int nk = min(K, Nmax - c0);
       // ---- R
       {
         const double bg[3] = {sb0[3], sb0[4], sb0[5]}, ba[3] = {sb0[6], sb0[7], sb0[8]};
@@ -451,7 +462,7 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
         double dt = 0.0, om0[3] = {0, 0, 0}, ac0[3] = {0, 0, 0}, om1[3] = {0, 0, 0}, ac1[3] = {0, 0, 0};
         int64_t nexttime = 0;
         int s0 = sbeg;
-        if (l < kImuK && it < N) {
+        if (l < K && it < N) {
           s0 = sbeg + it;
           const int s1 = (it + 1 < N) ? s0 + 1 : s0;
           for (int k = 0; k < 3; ++k) {
@@ -485,8 +496,8 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
         }
         started = started || gm != 0;
         steps += __popc(gm);
-        double* R = rec + min(l, kImuK - 1) * kStepRec;
-        if (l < kImuK) {
+        double* R = rec + min(l, K - 1) * kStepRec;
+        if (l < K) {
           R[0] = ok ? dt : 0.0;
           Fs[l * kFStride + kFdt] = ok ? dt : 0.0;
         }
@@ -539,12 +550,12 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
       // this chunk's phases instead of heading the next step-record phase (which read them from
       // HBM with 4 of 16 lanes active). The DMA's data lands in group 0's F_delta block, dead until
       // the I phase writes it (the barrier after the Q phase waits for the DMA); never read.
-      if (c0 + kImuK < Nmax) {
-        const int nb = min(sbeg + c0 + kImuK, nTot - 1);
+      if (c0 + K < Nmax) {
+        const int nb = min(sbeg + c0 + K, nTot - 1);
         const void* src = l < 4 ? (const void*)(P.imu_ga + min(6 * (int64_t)nb + 8 * l, 6 * (int64_t)nTot - 1))
                                 : (const void*)(P.imu_ts + min(nb + 8 * (l & 1), nTot - 1));
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)(sAll[0] + kLF), 4, 0, 0);
+                                         (__attribute__((address_space(3))) void*)(sAll[0] + LY::f), 4, 0, 0);
       }
       // ---- Q: the two product chains. Delta_q on every lane (lane 0 stores it); cross_ distributed,
       // lane e < 9 owning entry e = (r, c): each step needs column c of the previous cross_ (three
@@ -953,7 +964,10 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_imu(const DevProblem* 
   evalImuBlock<APPEND>(*Pp, mode, (int)blockIdx.x);
 }
 // Few windows: the observations (64 per workgroup), then the IMU factors, priors and edges, as one
-// launch (one graph node fewer on a single window's latency chain).
+// launch (one graph node fewer on a single window's latency chain). K: steps per IMU chunk
+// (kImuKFew for one or two windows, whose IMU factors are a latency chain; its LDS, ~72 KB per
+// workgroup, would hold the observation workgroups of larger batches to two per CU).
+template <int K>
 __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_few(const DevProblem* __restrict__ Pp, int mode, int nObsWG) {
   const DevProblem& P = *Pp;
   if ((int)blockIdx.x < nObsWG) {
@@ -961,7 +975,7 @@ __global__ __launch_bounds__(64, OKG_IMU_OCC) void k_eval_few(const DevProblem* 
     else evalObsThread<false>(P, (int)blockIdx.x * 64 + (int)threadIdx.x, mode);
     return;
   }
-  evalImuBlock<false>(P, mode, (int)blockIdx.x - nObsWG);
+  evalImuBlock<false, K>(P, mode, (int)blockIdx.x - nObsWG);
 }
 
 // ------------------------------------------------------------------------------------ priors
@@ -1175,11 +1189,24 @@ void launch_eval_imu(const DevProblem& P, int mode, hipStream_t s) {
   if (nb > 0) hipLaunchKernelGGL(k_eval_imu<false>, dim3(nb), dim3(64), 0, s, P.self, mode);
 }
 void launch_eval_priors(const DevProblem& P, int mode, hipStream_t s) {}  // (in launch_eval_imu)
+// The IMU factors (and priors / edges) as the solve's evaluation runs them: one or two windows
+// through k_eval_few's IMU chunking (no observation workgroups), else k_eval_imu (okvisgpu_time_kernel).
+void launch_eval_imu_as_solved(const DevProblem& P, int mode, hipStream_t s) {
+  if (fewWindows(P.n_win, P.cu_count) && P.n_win <= kImuFewChunkWindows) {
+    const int np = P.n_pprior + P.n_sbprior + P.n_relpose;
+    const int nb = (P.n_imu + kImuPerWG - 1) / kImuPerWG + (np + 63) / 64;
+    if (nb > 0) hipLaunchKernelGGL(k_eval_few<kImuKFew>, dim3(nb), dim3(64), 0, s, P.self, mode, 0);
+    return;
+  }
+  launch_eval_imu(P, mode, s);
+}
 void launch_eval(const DevProblem& P, int mode, hipStream_t s) {
   if (fewWindows(P.n_win, P.cu_count)) {
     const int np = P.n_pprior + P.n_sbprior + P.n_relpose;
     const int nObs = (P.n_obs + 63) / 64, nb = nObs + (P.n_imu + kImuPerWG - 1) / kImuPerWG + (np + 63) / 64;
-    if (nb > 0) hipLaunchKernelGGL(k_eval_few, dim3(nb), dim3(64), 0, s, P.self, mode, nObs);
+    if (nb <= 0) return;
+    if (P.n_win <= kImuFewChunkWindows) hipLaunchKernelGGL(k_eval_few<kImuKFew>, dim3(nb), dim3(64), 0, s, P.self, mode, nObs);
+    else hipLaunchKernelGGL(k_eval_few<kImuK>, dim3(nb), dim3(64), 0, s, P.self, mode, nObs);
     return;
   }
   launch_eval_obs(P, mode, s);

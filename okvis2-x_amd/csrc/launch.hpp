@@ -13,6 +13,7 @@ void launch_eval(const DevProblem& P, int mode, hipStream_t s);
 void launch_eval_obs(const DevProblem& P, int mode, hipStream_t s);
 void launch_eval_imu(const DevProblem& P, int mode, hipStream_t s);
 void launch_eval_priors(const DevProblem& P, int mode, hipStream_t s);
+void launch_eval_imu_as_solved(const DevProblem& P, int mode, hipStream_t s);  // (okvisgpu_time_kernel)
 // ImuError::append for a batch (P: n_imu, imu_blocks {0, f, 0, f}, imu_t0 = old t1, imu_t1 = new t1,
 // imu_sbegin / imu_ts / imu_ga = appended samples, imu_par (one row), imu_state, sb[0] = biases)
 void launch_imu_append(const DevProblem& P, hipStream_t s);

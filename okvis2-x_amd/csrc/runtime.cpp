@@ -2763,7 +2763,7 @@ int okvisgpu_time_kernel(okvisgpu_ctx* c, int32_t kernel, int32_t reps, double* 
           // mostly perform (the device-side IMU state is scratch afterwards)
           if (P.n_imu > 0)
             HIPCHK(hipMemset2DAsync(P.imu_state, sizeof(double) * kImuState, 0, sizeof(double), P.n_imu, s));
-          timed([&] { launch_eval_imu(P, 1, s); });
+          timed([&] { launch_eval_imu_as_solved(P, 1, s); });
           break;
         case K_EVAL_OBS: timed([&] { launch_eval_obs(P, 1, s); }); break;
         case K_JV: timed([&] { launch_jv(P, s); }); break;

@@ -191,6 +191,7 @@ struct Recorded {
   okvisgpu::HomogeneousPointManifold pointManifold;
   okvisgpu::CauchyLoss cauchy{1.0};
   std::vector<std::unique_ptr<okvisgpu::CostFunction>> costs;
+  std::vector<okvisgpu::ResidualBlockId> ids;  // in the order recorded: observations, IMU, priors
 };
 
 void record(okvisgpu::Problem& P, const okvisgpu_problem* p, Recorded& R) {
@@ -213,8 +214,9 @@ void record(okvisgpu::Problem& P, const okvisgpu_problem* p, Recorded& R) {
   for (int o = 0; o < p->n_observations; ++o) {
     const int c = p->obs_camera[o];
     R.costs.emplace_back(new okvisgpu::ReprojectionError(p->cameras[c], &p->obs_keypoint[2 * o], &p->obs_sqrt_info[4 * o]));
-    P.AddResidualBlock(R.costs.back().get(), (!p->obs_cauchy || p->obs_cauchy[o]) ? &R.cauchy : nullptr,
-                       &p->poses[7 * p->obs_pose[o]], &p->landmarks[4 * p->obs_landmark[o]], &p->extrinsics[7 * c]);
+    R.ids.push_back(P.AddResidualBlock(R.costs.back().get(), (!p->obs_cauchy || p->obs_cauchy[o]) ? &R.cauchy : nullptr,
+                                       &p->poses[7 * p->obs_pose[o]], &p->landmarks[4 * p->obs_landmark[o]],
+                                       &p->extrinsics[7 * c]));
   }
   for (int f = 0; f < p->n_imu; ++f) {
     const int s0 = p->imu_sample_begin[f], s1 = p->imu_sample_begin[f + 1];
@@ -223,8 +225,8 @@ void record(okvisgpu::Problem& P, const okvisgpu_problem* p, Recorded& R) {
     auto* e = new okvisgpu::ImuError(ts, ga, p->imu_params, p->imu_t0_ns[f], p->imu_t1_ns[f]);
     R.costs.emplace_back(e);
     const int* b = &p->imu_blocks[4 * f];
-    P.AddResidualBlock(e, nullptr, &p->poses[7 * b[0]], &p->speed_biases[9 * b[1]], &p->poses[7 * b[2]],
-                       &p->speed_biases[9 * b[3]]);
+    R.ids.push_back(P.AddResidualBlock(e, nullptr, &p->poses[7 * b[0]], &p->speed_biases[9 * b[1]],
+                                       &p->poses[7 * b[2]], &p->speed_biases[9 * b[3]]));
   }
   for (int i = 0; i < p->n_pose_priors; ++i) {
     R.costs.emplace_back(new okvisgpu::PoseError(&p->pose_prior_meas[7 * i], &p->pose_prior_sqrt_info[36 * i]));
@@ -308,6 +310,11 @@ int cpuTests() {
     CHECK(w.host_evaluate(w.host_user, 0, prm, r1, jac) == 1);
     f.Evaluate(prm, r2, nullptr);
     CHECK(r1[0] == r2[0] && r1[1] == r2[1] && r1[2] == r2[2]);
+    // EvaluateResidualBlock (ViGraph.hpp:553) of a host term: on the host, raw without a loss
+    double ec = -1, er[3];
+    CHECK(P.EvaluateResidualBlock(rg, true, &ec, er, nullptr));
+    CHECK(er[0] == r2[0] && er[1] == r2[1] && er[2] == r2[2]);
+    CHECK(std::fabs(ec - 0.5 * (r2[0] * r2[0] + r2[1] * r2[1] + r2[2] * r2[2])) <= 1e-15 * ec);
     P.RemoveResidualBlock(rg);
     CHECK(P.view().n_host == 0);
     // the fallback's limits: no landmark block, at most 2 pose-kind blocks
@@ -400,6 +407,25 @@ int cpuTests() {
     threw = false;
     try { okvisgpu::TukeyLoss bad(-1.0); (void)bad; } catch (const okvisgpu::Error&) { threw = true; }
     CHECK(threw);
+    // EvaluateResidualBlock with the loss applied (Ceres' Corrector on r): CauchyLoss(3) on the GPS
+    // term, cost b log(1 + s/b), r scaled by sqrt(rho')
+    {
+      const double* prm[3] = {Ta, sa, Ex};
+      double raw[3], ec = -1, er[3];
+      g.Evaluate(prm, raw, nullptr);
+      const double sq = raw[0] * raw[0] + raw[1] * raw[1] + raw[2] * raw[2];
+      std::vector<okvisgpu::ResidualBlockId> ids;
+      Q.GetResidualBlocksForParameterBlock(sa, &ids);
+      CHECK(ids.size() == 1 && Q.EvaluateResidualBlock(ids[0], true, &ec, er, nullptr));
+      CHECK(std::fabs(ec - 0.5 * 9.0 * std::log1p(sq / 9.0)) <= 1e-14 * ec);
+      const double sc = 1.0 / std::sqrt(1.0 + sq / 9.0);
+      CHECK(std::fabs(er[0] - raw[0] * sc) <= 1e-15 * std::fabs(raw[0]) + 1e-300);
+      CHECK(Q.EvaluateResidualBlock(ids[0], false, &ec, er, nullptr) && er[1] == raw[1] && ec == 0.5 * sq);
+      threw = false;
+      double* jac[3] = {nullptr, nullptr, nullptr};
+      try { Q.EvaluateResidualBlock(ids[0], false, &ec, er, jac); } catch (const okvisgpu::Unsupported&) { threw = true; }
+      CHECK(threw);
+    }
   }
   // one VARIABLE extrinsics block seen with two different intrinsics would become two independent
   // ABI blocks: rejected (a constant one is fine: two ABI cameras sharing the same constant T_SC)
@@ -536,6 +562,35 @@ int windowVsDirect() {
   okvisgpu::Problem P;
   Recorded R;
   record(P, pa, R);
+  // EvaluateResidualBlock (ViGraph.hpp:553) of GPU terms against the C ABI's evaluation hooks on the
+  // same values: reprojections bit for bit (raw, and with the CauchyLoss(1) Corrector), IMU |r|^2
+  {
+    okvisgpu_ctx* ec = nullptr;
+    CHECK(okvisgpu_ctx_create(0, &ec) == OKVISGPU_OK && okvisgpu_set_problems(ec, pb, 1) == OKVISGPU_OK);
+    const int no = pb->n_observations, ni = pb->n_imu;
+    std::vector<double> ro(2 * (size_t)no), ri(15 * (size_t)ni);
+    CHECK(okvisgpu_eval_reprojection(ec, 0, ro.data(), nullptr, nullptr) == OKVISGPU_OK);
+    CHECK(okvisgpu_eval_imu(ec, 0, 0, ri.data(), nullptr) == OKVISGPU_OK);
+    double worst = 0.0;
+    for (int o : {0, 1234, no - 1}) {
+      double c = -1, r[2];
+      CHECK(P.EvaluateResidualBlock(R.ids[o], false, &c, r, nullptr));
+      CHECK(r[0] == ro[2 * o] && r[1] == ro[2 * o + 1]);
+      const double sq = r[0] * r[0] + r[1] * r[1];
+      CHECK(P.EvaluateResidualBlock(R.ids[o], true, &c, r, nullptr));
+      CHECK(std::fabs(c - 0.5 * std::log1p(sq)) <= 1e-15 * c + 1e-300);
+      worst = std::max(worst, std::fabs(r[0] - ro[2 * o] / std::sqrt(1.0 + sq)));
+    }
+    CHECK(worst <= 1e-12);
+    for (int f : {0, ni - 1}) {
+      double c = -1, r[15], s2 = 0.0;
+      CHECK(P.EvaluateResidualBlock(R.ids[no + f], true, &c, r, nullptr));
+      for (int i = 0; i < 15; ++i) s2 += ri[15 * f + i] * ri[15 * f + i];
+      CHECK(std::fabs(c - 0.5 * s2) <= 1e-12 * c);
+    }
+    std::printf("EvaluateResidualBlock: reprojections equal to the C ABI hooks, IMU cost to 1e-12\n");
+    okvisgpu_ctx_destroy(ec);
+  }
   okvisgpu_summary sa, sb;
   CHECK(P.Solve(zeroTol(5), &sa) == OKVISGPU_OK);
   okvisgpu_ctx* ctx = nullptr;
@@ -587,8 +642,9 @@ int windowVsDirect() {
 }
 
 // §8b fallback end to end: an S10 window plus one GpsFunctor per keyframe on (pose k, speed/bias k,
-// camera 0's constant T_SC as the alignment block), through the facade (HostFunctor<GpsFunctor>) and
-// through the C ABI directly (host_* arrays + a C callback): same solve.
+// camera 0's constant T_SC as the alignment block) under CauchyLoss(3.0), through the facade
+// (HostFunctor<GpsFunctor>, okvisgpu::CauchyLoss) and through the C ABI directly (host_* arrays,
+// host_loss, a C callback): same solve.
 int gpsHostFallback() {
   okvisgpu_synth_config cfg;
   okvisgpu_synth_default_config(&cfg, 10, 500, 4000, 20251016u);
@@ -609,10 +665,14 @@ int gpsHostFallback() {
   okvisgpu::Problem P;
   Recorded R;
   record(P, pa, R);
+  // GPS factors as ViGraph adds them: with cauchyGpsLossFunctionPtr_ = CauchyLoss(3.0)
+  // (ViGraph.cpp:236,999); keyframe 4's measurement carries a gross error
+  gps[4].meas[0] += 1.5;
+  okvisgpu::CauchyLoss cauchyGpsLoss(3.0);
   std::vector<std::unique_ptr<okvisgpu::HostFunctor<GpsFunctor>>> hf;
   for (int k = 0; k < n; ++k) {
     hf.emplace_back(new okvisgpu::HostFunctor<GpsFunctor>(&gps[k]));
-    P.AddResidualBlock(hf.back().get(), nullptr, &pa->poses[7 * k], &pa->speed_biases[9 * k], &pa->extrinsics[0]);
+    P.AddResidualBlock(hf.back().get(), &cauchyGpsLoss, &pa->poses[7 * k], &pa->speed_biases[9 * k], &pa->extrinsics[0]);
   }
   okvisgpu_options o = zeroTol(8);
   o.num_threads = 2;
@@ -630,6 +690,8 @@ int gpsHostFallback() {
   q.host_param_kind = kind.data();
   q.host_param_index = idx.data();
   q.host_cauchy = nullptr;
+  const std::vector<okvisgpu_loss> losses(n, okvisgpu_loss{OKVISGPU_LOSS_CAUCHY, 0, 3.0, 0.0});
+  q.host_loss = losses.data();
   q.host_user = &gps;
   q.host_evaluate = [](void* user, int32_t f, const double* const* prm, double* r, double** J) -> int {
     return (*static_cast<std::vector<GpsFunctor>*>(user))[f].Evaluate(prm, r, J) ? 1 : 0;
