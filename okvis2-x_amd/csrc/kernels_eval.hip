@@ -728,37 +728,53 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
     }
     trace = groupSum(trace);
     __syncthreads();
-    // right-looking Cholesky P = L L^T in LDS: sB (column-major) starts as P, lane j owns column j
+    // right-looking Cholesky P = L L^T with lane l holding row l (j <= l) in registers: per pivot k
+    // the pivot comes by shuffle from lane k, each lane scales its L(l,k) and publishes it into column
+    // k of sB (column-major), one barrier, then updates its row with column k. Same products and the
+    // same ascending-k order per element as a column-oriented LDS factorisation.
     bool ok = true;
-    if (integrate)
-      for (int i = 0; i < 16; ++i) sB[l * kS + i] = (l < 15 && i < 15) ? Pc[i] : 0.0;
-    __syncthreads();
+    const int gbase = threadIdx.x & ~(kImuGroup - 1);
+    double rw[15];
+#pragma unroll
+    for (int j = 0; j < 15; ++j) rw[j] = Pc[j];
+#pragma unroll
     for (int k = 0; k < 15; ++k) {
+      const double dk = __shfl(rw[k], gbase + k, 64);
       if (integrate && l >= k && l < 15) {
-        const double d = sB[k * kS + k];
-        if (!(d > 0.0)) ok = false;
-        const double v = sB[k * kS + l] / sqrt(d);
-        sB[k * kS + l] = v;
+        if (!(dk > 0.0)) ok = false;
+        rw[k] = rw[k] / sqrt(dk);
+        sB[k * kS + l] = rw[k];
       }
       __syncthreads();
       if (integrate && l > k && l < 15) {
-        const double ljk = sB[k * kS + l];
-        for (int i = l; i < 15; ++i) sB[l * kS + i] -= sB[k * kS + i] * ljk;
+#pragma unroll
+        for (int j = k + 1; j < 15; ++j)
+          if (j <= l) rw[j] -= sB[k * kS + j] * rw[k];
       }
-      __syncthreads();
     }
-    // U = L^-1 in place (column-major, backward over columns):
-    //   U(j,j) = 1/L(j,j),  U(i,j) = -U(j,j) sum_{m=j+1..i} U(i,m) L(m,j)   (i > j)
+    // U = L^-1 per lane (row l of U from L in sB, no barriers):
+    //   U(l,l) = 1/L(l,l),  U(l,j) = -(1/L(j,j)) sum_{m=j+1..l} U(l,m) L(m,j)   (j < l)
+    double ur[15];
+#pragma unroll
     for (int j = 14; j >= 0; --j) {
-      double acc = 0.0, ujj = 0.0;
+      ur[j] = 0.0;
       if (integrate && l >= j && l < 15) {
-        ujj = 1.0 / sB[j * kS + j];
-        for (int m = j + 1; m <= l; ++m) acc += sB[m * kS + l] * sB[j * kS + m];
+        const double ujj = 1.0 / sB[j * kS + j];
+        double acc = 0.0;
+#pragma unroll
+        for (int m = j + 1; m < 15; ++m)
+          if (m <= l) acc += ur[m] * sB[j * kS + m];
+        ur[j] = (l == j) ? ujj : -ujj * acc;
       }
-      __syncthreads();
-      if (integrate && l >= j && l < 15) sB[j * kS + l] = (l == j) ? ujj : -ujj * acc;
-      __syncthreads();
     }
+    __syncthreads();
+    // U column-major into sB (lower triangle) for the norm test, the transpose and the append
+    if (integrate && l < 15) {
+#pragma unroll
+      for (int j = 0; j < 15; ++j)
+        if (j <= l) sB[j * kS + l] = ur[j];
+    }
+    __syncthreads();
     double fro = 0.0;
     if (integrate && l < 15)
       for (int i = l; i < 15; ++i) fro += sB[l * kS + i] * sB[l * kS + i];

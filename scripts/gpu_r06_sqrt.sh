@@ -1,0 +1,12 @@
+#!/bin/bash
+# A/B of the IMU square-root phase (register rows vs column-oriented LDS Cholesky), its phase clock,
+# then the IMU-touching GPU tests.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+OUT=gpurun_out/${1:-r06sqrt}; mkdir -p $OUT
+for rep in 1 2; do for lib in libokvisgpu.so lib_sqrtold.so; do for shape in "50 2000 16000" "10 500 4000"; do
+  OKVISGPU_LIB=okvis2-x_amd/$lib timeout -k 10 120 python scripts/imu_probe.py $shape | sed "s/^/$lib /" | tee -a $OUT/imu_probe.txt || exit 1
+done; done; done
+OKVISGPU_LIB=okvis2-x_amd/lib_iclk.so timeout -k 10 120 python scripts/imu_clock.py 50 2000 16000 1 > $OUT/iclk.txt 2>&1 || exit 1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_shapes.py tests/test_imu_append.py tests/test_reference_scenarios.py tests/test_losses.py -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.txt 2>&1 || { echo "pytest rc=$?"; tail -20 $OUT/pytest.txt; exit 1; }
+tail -1 $OUT/pytest.txt
