@@ -158,6 +158,9 @@ constexpr int kImuFewChunkWindows = 2;
 #ifndef OKG_IMU_FEW_K
 #define OKG_IMU_FEW_K 16  // (build knob for A/B measurements)
 #endif
+#ifndef OKG_IMU_FREG
+#define OKG_IMU_FREG 1  // (build knob: 0 reads F_delta from LDS in both products of a step)
+#endif
 constexpr int kImuKFew = OKG_IMU_FEW_K;  // one or two windows: a chunk covers a 0.1 s keyframe interval's 20 samples
                               // in two rounds (the step records and products are lane-parallel over a
                               // chunk, so fewer chunks shorten a single factor's latency chain)
@@ -661,7 +664,18 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
       ICLK(9)
       // ---- P <- F P F^T + Q : M = F P (column l), exchange rows, P' = F M^T (column l)
       for (int k = 0; k < nk; ++k) {
+#if OKG_IMU_FREG
+        // the step's F_delta blocks read once into registers for both products (the barrier
+        // between them would force a second LDS read)
+        double F[kFdt + 1];
+        {
+          const double* Fl = Fs + k * kFStride;
+#pragma unroll
+          for (int i = 0; i <= kFdt; ++i) F[i] = Fl[i];
+        }
+#else
         const double* F = Fs + k * kFStride;
+#endif
         const bool doStep = F[kFdt] > 0.0;  // uniform over the group
         if (doStep && l < 15) {
           double Mc[15];
