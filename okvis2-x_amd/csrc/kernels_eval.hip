@@ -118,7 +118,8 @@ struct ImuPre {  // preintegrated quantities (ImuError.hpp:273-304), register re
   double Ci[9], Cdi[9], ai[3], adi[3], dadbg[9], dvdbg[9], dpdbg[9];
 };
 
-__device__ void loadPre(const double* s, ImuPre& p) {
+template <typename Ptr>
+__device__ __forceinline__ void loadPre(Ptr s, ImuPre& p) {
   p.dq = Q{s[2], s[3], s[4], s[5]};
   for (int i = 0; i < 9; ++i) {
     p.Ci[i] = s[6 + i];
@@ -365,9 +366,9 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
   const int xs = APPEND ? 0 : (mode == 1 ? 1 - sX : sX), lb = APPEND ? 0 : (mode == 1 ? 1 - sL : sL);
   const int fs = live ? f : 0;  // safe index for idle groups (writes are all under live)
 
-  const int* blk = P.imu_blocks + 4 * fs;
+  const auto blk = gmem(P.imu_blocks + 4 * fs);
   const auto sb0 = gmem(pick2(xs, P.sb[0], P.sb[1]) + 9 * (size_t)blkR.y);
-  double* state = P.imu_state + (size_t)fs * kImuState;
+  const auto state = gmemw(P.imu_state + (size_t)fs * kImuState);
 
   // ---- re-preintegration decision (ImuError.cpp:833-859)
   int redoCounter = (int)st0;
@@ -469,16 +470,16 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
           s0 = sbeg + it;
           const int s1 = (it + 1 < N) ? s0 + 1 : s0;
           for (int k = 0; k < 3; ++k) {
-            om0[k] = P.imu_ga[6 * (size_t)s0 + k];
-            ac0[k] = P.imu_ga[6 * (size_t)s0 + 3 + k];
-            om1[k] = P.imu_ga[6 * (size_t)s1 + k];
-            ac1[k] = P.imu_ga[6 * (size_t)s1 + 3 + k];
+            om0[k] = gmem(P.imu_ga)[6 * (size_t)s0 + k];
+            ac0[k] = gmem(P.imu_ga)[6 * (size_t)s0 + 3 + k];
+            om1[k] = gmem(P.imu_ga)[6 * (size_t)s1 + k];
+            ac1[k] = gmem(P.imu_ga)[6 * (size_t)s1 + 3 + k];
           }
-          nexttime = (it + 1 == N) ? t1 : P.imu_ts[s0 + 1];
-          const int64_t tb = (it == 0) ? t0 : max(t0, min(P.imu_ts[s0], t1));
+          nexttime = (it + 1 == N) ? t1 : gmem(P.imu_ts)[s0 + 1];
+          const int64_t tb = (it == 0) ? t0 : max(t0, min(gmem(P.imu_ts)[s0], t1));
           dt = durToSec(nexttime - tb);
           if (t1 < nexttime) {
-            const double interval = durToSec(nexttime - P.imu_ts[s0]);
+            const double interval = durToSec(nexttime - gmem(P.imu_ts)[s0]);
             nexttime = t1;
             dt = durToSec(nexttime - tb);
             const double r = dt / interval;
@@ -491,7 +492,7 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
         }
         const unsigned gm = (unsigned)((__ballot(ok) >> (16 * g)) & 0xFFFFull);
         if (ok && !started && l == __ffs(gm) - 1) {  // the first integrated step starts at t0
-          const double r = dt / durToSec(nexttime - P.imu_ts[s0]);
+          const double r = dt / durToSec(nexttime - gmem(P.imu_ts)[s0]);
           for (int k = 0; k < 3; ++k) {
             om0[k] = r * om0[k] + (1.0 - r) * om1[k];
             ac0[k] = r * ac0[k] + (1.0 - r) * ac1[k];
@@ -742,6 +743,7 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
     }
     trace = groupSum(trace);
     __syncthreads();
+    ICLK(11)
     // right-looking Cholesky P = L L^T with lane l holding row l (j <= l) in registers: per pivot k
     // the pivot comes by shuffle from lane k, each lane scales its L(l,k) and publishes it into column
     // k of sB (column-major), one barrier, then updates its row with column k. Same products and the
@@ -789,6 +791,7 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
         if (j <= l) sB[j * kS + l] = ur[j];
     }
     __syncthreads();
+    ICLK(12)
     double fro = 0.0;
     if (integrate && l < 15)
       for (int i = l; i < 15; ++i) fro += sB[l * kS + i] * sB[l * kS + i];
@@ -797,6 +800,7 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
     const double eps = DBL_EPSILON;
     const bool needEig = integrate && !(ok && fro > 0.0 && 1.0 / fro > 4.0 * fmax(eps, eps * 15.0 * trace));
     __syncthreads();
+    ICLK_COUNT(13, needEig && l == 0)
     if (__any(needEig)) {
       // clamped eigenvalues possible: the reference's eigen-decomposition (cyclic Jacobi) of the
       // symmetric P kept in sA; eigenvectors into sB, then U = diag(clamped lambda^-1/2) V^T
@@ -827,9 +831,9 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
   __syncthreads();  // state writes of the group visible to all its lanes
   ICLK(3)
   if (APPEND) return;  // uniform over the workgroup
-  const double* p0 = pick2(xs, P.pose[0], P.pose[1]) + 7 * (size_t)blk[0];
-  const double* p1 = pick2(xs, P.pose[0], P.pose[1]) + 7 * (size_t)blk[2];
-  const double* sb1 = pick2(xs, P.sb[0], P.sb[1]) + 9 * (size_t)blk[3];
+  const auto p0 = gmem(pick2(xs, P.pose[0], P.pose[1]) + 7 * (size_t)blk[0]);
+  const auto p1 = gmem(pick2(xs, P.pose[0], P.pose[1]) + 7 * (size_t)blk[2]);
+  const auto sb1 = gmem(pick2(xs, P.sb[0], P.sb[1]) + 9 * (size_t)blk[3]);
   ImuPre pre;
   loadPre(state, pre);
   const bool success = live && (!integrate || steps > 0);
@@ -936,14 +940,14 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
       }
   }
   const size_t fl = live ? (size_t)f : 0;
-  double* lin = P.imu_lin[lb] + fl * kImuLin;
+  const auto lin = gmemw(P.imu_lin[lb] + fl * kImuLin);
   double rr = 0.0;
   if (live && l < 15) {
     for (int k = 0; k < 15; ++k) rr += sA[l * kS + k] * err[k];
     lin[l] = rr;
   }
   const double c2 = groupSum(l < 15 ? rr * rr : 0.0);
-  if (live && l == 0) P.imu_cost[lb][f] = 0.5 * c2;
+  if (live && l == 0) gmemw(P.imu_cost[lb])[f] = 0.5 * c2;
   __syncthreads();
   ICLK(4)
   // J = U [F0 | F1]; lane l computes columns l and l + 16 of the 15 x 30 Jacobian. Column j of
