@@ -44,11 +44,11 @@ static __device__ unsigned long long g_cholClk[32];
 // contended and inflated the phases they fell into); the last workgroup prints the totals. Uses the
 // kernel's APPEND template parameter.
 #ifdef OKG_IMU_CLOCK
-static __device__ unsigned long long g_imuClk[14];
+static __device__ unsigned long long g_imuClk[16];
 static __device__ unsigned int g_imuDone;
 #define ICLK_INIT                                                                       \
-  unsigned long long iclk = __builtin_amdgcn_s_memrealtime(), iacc[14];                 \
-  for (int i_ = 0; i_ < 14; ++i_) iacc[i_] = 0;
+  unsigned long long iclk = __builtin_amdgcn_s_memrealtime(), iacc[16];                 \
+  for (int i_ = 0; i_ < 16; ++i_) iacc[i_] = 0;
 #define ICLK(i)                                                                         \
   {                                                                                     \
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();                    \
@@ -57,13 +57,13 @@ static __device__ unsigned int g_imuDone;
   }
 #define ICLK_END                                                                        \
   if (!APPEND && threadIdx.x == 0) {                                                    \
-    for (int i_ = 0; i_ < 14; ++i_) atomicAdd(&g_imuClk[i_], iacc[i_]);                 \
+    for (int i_ = 0; i_ < 16; ++i_) atomicAdd(&g_imuClk[i_], iacc[i_]);                 \
     __threadfence();                                                                    \
     if (atomicAdd(&g_imuDone, 1u) == (unsigned)((P.n_imu + kImuPerWG - 1) / kImuPerWG) - 1) { \
       printf("IMUCLK pro %llu chain %llu state %llu sqrt %llu resid %llu jac %llu | R %llu Q %llu I %llu S %llu " \
-             "P %llu | sqrt: sym %llu chol %llu (x10ns) | eigen groups %llu\n", g_imuClk[0], g_imuClk[1], g_imuClk[2], g_imuClk[3], g_imuClk[4], g_imuClk[5], \
-             g_imuClk[6], g_imuClk[7], g_imuClk[8], g_imuClk[9], g_imuClk[10], g_imuClk[11], g_imuClk[12], g_imuClk[13]);                               \
-      for (int i_ = 0; i_ < 14; ++i_) g_imuClk[i_] = 0;                                 \
+             "P %llu | sqrt: sym %llu chol %llu (x10ns) | eigen groups %llu | tail: stores %llu wait %llu\n", g_imuClk[0], g_imuClk[1], g_imuClk[2], g_imuClk[3], g_imuClk[4], g_imuClk[5], \
+             g_imuClk[6], g_imuClk[7], g_imuClk[8], g_imuClk[9], g_imuClk[10], g_imuClk[11], g_imuClk[12], g_imuClk[13], g_imuClk[14], g_imuClk[15]);                               \
+      for (int i_ = 0; i_ < 16; ++i_) g_imuClk[i_] = 0;                                 \
       g_imuDone = 0;                                                                    \
     }                                                                                   \
   }

@@ -823,13 +823,15 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
       for (int i = 0; i < 15; ++i) sA[i * kS + l] = (i >= l) ? sB[l * kS + i] : 0.0;
     __syncthreads();
   }
+  ICLK(3)
   if (integrate) {
     for (int e = l; e < 225; e += kImuGroup) state[66 + e] = sA[(e / 15) * kS + e % 15];
   } else if (live) {
     for (int e = l; e < 225; e += kImuGroup) sA[(e / 15) * kS + e % 15] = state[66 + e];
   }
+  ICLK(14)
   __syncthreads();  // state writes of the group visible to all its lanes
-  ICLK(3)
+  ICLK(15)
   if (APPEND) return;  // uniform over the workgroup
   const auto p0 = gmem(pick2(xs, P.pose[0], P.pose[1]) + 7 * (size_t)blk[0]);
   const auto p1 = gmem(pick2(xs, P.pose[0], P.pose[1]) + 7 * (size_t)blk[2]);
