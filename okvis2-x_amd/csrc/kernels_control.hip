@@ -147,12 +147,12 @@ __device__ __forceinline__ void jvPartials(const DevProblem& P, int w, int t, in
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     double acc = 0.0;
-    for (int g = gb + t; g < ge; g += RB) acc += P.grp_red[(size_t)g * kGrpRed + k];
-    for (int f = ib + t; f < ie; f += RB) acc += P.imu_jv[(size_t)k * P.n_fac + f];
-    for (int f = hb + t; f < he; f += RB) acc += P.imu_jv[(size_t)k * P.n_fac + f];
-    for (int i = pb + t; i < pe; i += RB) acc += P.pp_jv[(size_t)k * P.n_pprior + i];
-    for (int i = sbb + t; i < sbe; i += RB) acc += P.sbp_jv[(size_t)k * P.n_sbprior + i];
-    for (int i = rpb + t; i < rpe; i += RB) acc += P.rp_jv[(size_t)k * P.n_relpose + i];
+    for (int g = gb + t; g < ge; g += RB) acc += gmem(P.grp_red)[(size_t)g * kGrpRed + k];
+    for (int f = ib + t; f < ie; f += RB) acc += gmem(P.imu_jv)[(size_t)k * P.n_fac + f];
+    for (int f = hb + t; f < he; f += RB) acc += gmem(P.imu_jv)[(size_t)k * P.n_fac + f];
+    for (int i = pb + t; i < pe; i += RB) acc += gmem(P.pp_jv)[(size_t)k * P.n_pprior + i];
+    for (int i = sbb + t; i < sbe; i += RB) acc += gmem(P.sbp_jv)[(size_t)k * P.n_sbprior + i];
+    for (int i = rpb + t; i < rpe; i += RB) acc += gmem(P.rp_jv)[(size_t)k * P.n_relpose + i];
     a[k] = acc;
   }
 }
@@ -167,8 +167,8 @@ __device__ double reduceJv(const DevProblem& P, int w, WinState& s, double* sh) 
   // |gradient_|^2 over the window (f-vector + free landmarks)
   double g2 = 0.0;
   const int fo = P.win_foff[w], fd = P.win_fdim[w];
-  for (int e = t; e < fd; e += RB) g2 += P.dgF[fo + e] * P.dgF[fo + e];
-  for (int g = gb + t; g < ge; g += RB) g2 += P.grp_red[(size_t)g * kGrpRed + 3];
+  for (int e = t; e < fd; e += RB) g2 += gmem(P.dgF)[fo + e] * gmem(P.dgF)[fo + e];
+  for (int g = gb + t; g < ge; g += RB) g2 += gmem(P.grp_red)[(size_t)g * kGrpRed + 3];
   g2 = blockSum<RB>(g2, sh);
   const double alpha = g2 / a[0];
   if (t == 0) {
@@ -199,32 +199,35 @@ __global__ __launch_bounds__(RB) void k_reduce(const DevProblem* __restrict__ Pp
     const int lb = (mode == R_COST_CAND) ? 1 - s.lcur : s.lcur;
     double c = 0.0, cf = 0.0;
     struct OC { double c; uint8_t f; };
-    const double* oc = P.obs_cost[lb];
-    stridedBatched<RB, 8>(ob, oe, [&](int o) { return OC{oc[o], P.obs_flags[o]}; },
+    const auto oc = gmem(P.obs_cost[lb]);
+    const auto ofl = gmem(P.obs_flags);
+    stridedBatched<RB, 8>(ob, oe, [&](int o) { return OC{oc[o], ofl[o]}; },
                       [&](int, const OC& v) {
                         if (v.f & 2) cf += v.c;
                         else c += v.c;
                       });
+    const auto ifl = gmem(P.imu_flags);
+    const auto icost = gmem(P.imu_cost[lb]);
     for (int f = ib + t; f < ie; f += RB) {
-      if (P.imu_flags[f] & 2) cf += P.imu_cost[lb][f];
-      else c += P.imu_cost[lb][f];
+      if (ifl[f] & 2) cf += icost[f];
+      else c += icost[f];
     }
     const int hb = P.win_host_range[2 * w], he = P.win_host_range[2 * w + 1];
     for (int f = hb + t; f < he; f += RB) {
-      if (P.imu_flags[f] & 2) cf += P.imu_cost[lb][f];
-      else c += P.imu_cost[lb][f];
+      if (ifl[f] & 2) cf += icost[f];
+      else c += icost[f];
     }
     for (int i = pb + t; i < pe; i += RB) {
-      if (P.pose_f[P.pp_block[i]] < 0) cf += P.pp_cost[lb][i];
-      else c += P.pp_cost[lb][i];
+      if (gmem(P.pose_f)[gmem(P.pp_block)[i]] < 0) cf += gmem(P.pp_cost[lb])[i];
+      else c += gmem(P.pp_cost[lb])[i];
     }
     for (int i = sbb + t; i < sbe; i += RB) {
-      if (P.sb_f[P.sbp_block[i]] < 0) cf += P.sbp_cost[lb][i];
-      else c += P.sbp_cost[lb][i];
+      if (gmem(P.sb_f)[gmem(P.sbp_block)[i]] < 0) cf += gmem(P.sbp_cost[lb])[i];
+      else c += gmem(P.sbp_cost[lb])[i];
     }
     for (int i = rpb + t; i < rpe; i += RB) {
-      if (P.rp_flags[i] & 2) cf += P.rp_cost[lb][i];
-      else c += P.rp_cost[lb][i];
+      if (gmem(P.rp_flags)[i] & 2) cf += gmem(P.rp_cost[lb])[i];
+      else c += gmem(P.rp_cost[lb])[i];
     }
     {
       double r2[2] = {c, cf};
@@ -304,11 +307,11 @@ __global__ __launch_bounds__(RB) void k_gradnorm(const DevProblem* __restrict__ 
   double mx = 0.0, g2 = 0.0, x2 = 0.0;
   const int p0 = P.win_pose_range[2 * w], p1 = P.win_pose_range[2 * w + 1];
   for (int p = p0 + t; p < p1; p += RB) {
-    if (!P.pose_active[p]) continue;
-    const double* x = P.pose[xs] + 7 * (size_t)p;
+    if (!gmem(P.pose_active)[p]) continue;
+    const auto x = gmem(P.pose[xs] + 7 * (size_t)p);
     for (int k = 0; k < 7; ++k) x2 += x[k] * x[k];
-    const int pf = P.pose_f[p];
-    const double* g = P.gF + foff + pf;
+    const int pf = gmem(P.pose_f)[p];
+    const auto g = gmem(P.gF + foff + pf);
     double xp[7];
     for (int k = 0; k < 3; ++k) xp[k] = x[k] + (-g[k]);
     const Q dq = deltaQ(-g[3], -g[4], -g[5]);
@@ -322,9 +325,9 @@ __global__ __launch_bounds__(RB) void k_gradnorm(const DevProblem* __restrict__ 
   }
   const int s0 = P.win_sb_range[2 * w], s1 = P.win_sb_range[2 * w + 1];
   for (int b = s0 + t; b < s1; b += RB) {
-    if (!P.sb_active[b]) continue;
-    const double* x = P.sb[xs] + 9 * (size_t)b;
-    const double* g = P.gF + foff + P.sb_f[b];
+    if (!gmem(P.sb_active)[b]) continue;
+    const auto x = gmem(P.sb[xs] + 9 * (size_t)b);
+    const auto g = gmem(P.gF + foff + gmem(P.sb_f)[b]);
     for (int k = 0; k < 9; ++k) {
       x2 += x[k] * x[k];
       const double d = x[k] - (x[k] + (-g[k]));
@@ -337,9 +340,9 @@ __global__ __launch_bounds__(RB) void k_gradnorm(const DevProblem* __restrict__ 
   stridedBatched<RB, 4>(l0, l1,
                     [&](int l) {
                       LX v;
-                      v.f = P.lm_free[l];
-                      for (int k = 0; k < 4; ++k) v.x[k] = P.lm[xs][4 * (size_t)l + k];
-                      for (int k = 0; k < 3; ++k) v.g[k] = P.lm_g[3 * (size_t)l + k];
+                      v.f = gmem(P.lm_free)[l];
+                      for (int k = 0; k < 4; ++k) v.x[k] = gmem(P.lm[xs])[4 * (size_t)l + k];
+                      for (int k = 0; k < 3; ++k) v.g[k] = gmem(P.lm_g)[3 * (size_t)l + k];
                       return v;
                     },
                     [&](int, const LX& v) {
@@ -430,14 +433,14 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
   // pass 1: norms (f-blocks here, landmarks as the landmark groups' sums of k_lm_backsub_jv)
   double gg = 0.0, nn = 0.0, gn = 0.0;
   for (int e = t; e < fd; e += RB) {
-    const double a = P.dgF[foff + e], b = P.gnF[foff + e];
+    const double a = gmem(P.dgF)[foff + e], b = gmem(P.gnF)[foff + e];
     gg += a * a;
     nn += b * b;
     gn += a * b;
   }
   const int gb = P.win_lmg_range[2 * w], ge = P.win_lmg_range[2 * w + 1];
   for (int g = gb + t; g < ge; g += RB) {
-    const double* r = P.grp_red + (size_t)g * kGrpRed;
+    const auto r = gmem(P.grp_red + (size_t)g * kGrpRed);
     gg += r[3];
     nn += r[4];
     gn += r[5];
@@ -496,28 +499,28 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
   // (every operand of a block is loaded before its first store: the stores may alias the
   // f-vectors for the compiler, and a single window is a chain of such rounds)
   for (int p = p0 + t; p < p1; p += RB) {
-    const int pf = P.pose_f[p];
+    const int pf = gmem(P.pose_f)[p];
     if (pf < 0) continue;
     double dg[6], gn[6], dia[6], sc[6], g[6], x[7];
     for (int c = 0; c < 6; ++c) {
       const size_t i = (size_t)foff + pf + c;
-      dg[c] = P.dgF[i];
-      gn[c] = P.gnF[i];
-      dia[c] = P.diagF[i];
-      sc[c] = P.sF[i];
-      g[c] = P.gF[i];
+      dg[c] = gmem(P.dgF)[i];
+      gn[c] = gmem(P.gnF)[i];
+      dia[c] = gmem(P.diagF)[i];
+      sc[c] = gmem(P.sF)[i];
+      g[c] = gmem(P.gF)[i];
     }
-    for (int k = 0; k < 7; ++k) x[k] = P.pose[xs][7 * (size_t)p + k];
+    for (int k = 0; k < 7; ++k) x[k] = gmem(P.pose[xs])[7 * (size_t)p + k];
     double delta[6];
     for (int c = 0; c < 6; ++c) {
       const double v = ca * dg[c] + cb * gn[c];
       dn2 += v * v;
       const double st = v / dia[c];
-      P.stepF[(size_t)foff + pf + c] = st;
+      gmemw(P.stepF)[(size_t)foff + pf + c] = st;
       delta[c] = st * sc[c];
       jr += delta[c] * g[c];
     }
-    double* y = P.pose[xd] + 7 * (size_t)p;
+    const auto y = gmemw(P.pose[xd] + 7 * (size_t)p);
     const Q dq = deltaQ(delta[3], delta[4], delta[5]);
     const Q q = qnormalize(qmul(dq, qnormalize(Q{x[3], x[4], x[5], x[6]})));
     double yv[7] = {x[0] + delta[0], x[1] + delta[1], x[2] + delta[2], q.x, q.y, q.z, q.w};
@@ -528,24 +531,24 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
   }
   const int b0 = P.win_sb_range[2 * w], b1 = P.win_sb_range[2 * w + 1];
   for (int b = b0 + t; b < b1; b += RB) {
-    const int sf = P.sb_f[b];
+    const int sf = gmem(P.sb_f)[b];
     if (sf < 0) continue;
-    double* y = P.sb[xd] + 9 * (size_t)b;
+    const auto y = gmemw(P.sb[xd] + 9 * (size_t)b);
     double dg[9], gn[9], dia[9], sc[9], g[9], x[9];
     for (int c = 0; c < 9; ++c) {
       const size_t i = (size_t)foff + sf + c;
-      dg[c] = P.dgF[i];
-      gn[c] = P.gnF[i];
-      dia[c] = P.diagF[i];
-      sc[c] = P.sF[i];
-      g[c] = P.gF[i];
-      x[c] = P.sb[xs][9 * (size_t)b + c];
+      dg[c] = gmem(P.dgF)[i];
+      gn[c] = gmem(P.gnF)[i];
+      dia[c] = gmem(P.diagF)[i];
+      sc[c] = gmem(P.sF)[i];
+      g[c] = gmem(P.gF)[i];
+      x[c] = gmem(P.sb[xs])[9 * (size_t)b + c];
     }
     for (int c = 0; c < 9; ++c) {
       const double v = ca * dg[c] + cb * gn[c];
       dn2 += v * v;
       const double st = v / dia[c];
-      P.stepF[(size_t)foff + sf + c] = st;
+      gmemw(P.stepF)[(size_t)foff + sf + c] = st;
       jr += (st * sc[c]) * g[c];
       const double yv = x[c] + st * sc[c];
       y[c] = yv;
@@ -556,26 +559,26 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
   stridedBatched<RB, (RB >= 1024 ? 1 : 4)>(l0, l1,
                     [&](int l) {
                       LS v;
-                      v.f = P.lm_free[l];
-                      for (int k = 0; k < 4; ++k) v.x[k] = P.lm[xs][4 * (size_t)l + k];
+                      v.f = gmem(P.lm_free)[l];
+                      for (int k = 0; k < 4; ++k) v.x[k] = gmem(P.lm[xs])[4 * (size_t)l + k];
                       for (int c = 0; c < 3; ++c) {
                         const size_t i = 3 * (size_t)l + c;
-                        v.dg[c] = P.dgL[i];
-                        v.gn[c] = P.gnL[i];
-                        v.dia[c] = P.diagL[i];
-                        v.sl[c] = P.sL[i];
-                        v.g[c] = P.gL[i];
+                        v.dg[c] = gmem(P.dgL)[i];
+                        v.gn[c] = gmem(P.gnL)[i];
+                        v.dia[c] = gmem(P.diagL)[i];
+                        v.sl[c] = gmem(P.sL)[i];
+                        v.g[c] = gmem(P.gL)[i];
                       }
                       return v;
                     },
                     [&](int l, const LS& v) {
                       if (!v.f) return;
-                      double* y = P.lm[xd] + 4 * (size_t)l;
+                      const auto y = gmemw(P.lm[xd] + 4 * (size_t)l);
                       for (int c = 0; c < 3; ++c) {
                         const double vv = ca * v.dg[c] + cb * v.gn[c];
                         dn2 += vv * vv;
                         const double st = vv / v.dia[c];
-                        P.stepL[3 * (size_t)l + c] = st;
+                        gmemw(P.stepL)[3 * (size_t)l + c] = st;
                         jr += (st * v.sl[c]) * v.g[c];
                         const double yv = v.x[c] + st * v.sl[c];
                         y[c] = yv;
