@@ -398,7 +398,7 @@ __device__ __forceinline__ void xStoreRows16(const double* sX, double* Li, int q
 #pragma unroll
   for (int it = 0; it < 3; ++it) {
     const int e = 64 * g + lane + 192 * it, r = 16 * q + (e >> 5), c = 2 * (e & 31);
-    if (e < 512 && (!persistentCaller(kCaller) || c <= r)) *reinterpret_cast<double2*>(Li + r * kTile + c) = v[it];
+    if (e < 512 && (!persistentCaller(kCaller) || c <= r)) *gmemw(reinterpret_cast<double2*>(Li + r * kTile + c)) = v[it];
   }
 }
 
@@ -552,7 +552,7 @@ __device__ __forceinline__ bool potrfTileBody(const double* Sg, int64_t ld, doub
   if (t < kTile) {
     const double y = sy[kTile + t];
     sy[t] = y;
-    if (!persistentCaller(kCaller)) workk[t] = y;
+    if (!persistentCaller(kCaller)) gmemw(workk)[t] = y;
   }
   potrfSync<kCaller>(sFl, tgen, lane);
   CLK(10)
