@@ -191,13 +191,13 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
         for (int c = a; c < 3; ++c) y += li[c * 3 + a] * u[c];
         const size_t i = 3 * (size_t)L + a;
         const double dg = dgv[a];
-        P.yL[i] = y;
+        gmemw(P.yL)[i] = y;
         const double gn = -dg * y;
-        P.gnL[i] = gn;
+        gmemw(P.gnL)[i] = gn;
         const double gr = s3[a] * lg[a] / dg;
         const double vc = gr / dg;
-        P.dgL[i] = gr;
-        P.vL[i] = vc;
+        gmemw(P.dgL)[i] = gr;
+        gmemw(P.vL)[i] = vc;
         // this landmark's share of |gradient_|^2, |gauss_newton_step_|^2, gradient_ . gn (k_dogleg,
         // k_reduce), summed per group below
         lred[0] += gr * gr;
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(kLmGroupVisits) void k_lm_backsub_jv(const DevProbl
     double a = sW[0][t];
 #pragma unroll
     for (int wv = 1; wv < kLmGroupVisits / 64; ++wv) a += sW[wv][t];
-    P.grp_red[(size_t)blockIdx.x * kGrpRed + t] = a;
+    gmemw(P.grp_red)[(size_t)blockIdx.x * kGrpRed + t] = a;
   }
 }
 

@@ -316,9 +316,9 @@ __device__ __forceinline__ void lmVisitGroup(const DevProblem& P, const int grp)
         double V[6] = {0, 0, 0, 0, 0, 0}, g[3] = {0, 0, 0};
         if (mode == 2) {
 #pragma unroll
-          for (int i = 0; i < 6; ++i) V[i] = P.lm_V[6 * (size_t)L + i];
+          for (int i = 0; i < 6; ++i) V[i] = gmem(P.lm_V)[6 * (size_t)L + i];
 #pragma unroll
-          for (int i = 0; i < 3; ++i) g[i] = P.lm_g[3 * (size_t)L + i];
+          for (int i = 0; i < 3; ++i) g[i] = gmem(P.lm_g)[3 * (size_t)L + i];
         } else {
           for (int u = ub; u < ue; ++u) {
 #pragma unroll
@@ -327,12 +327,12 @@ __device__ __forceinline__ void lmVisitGroup(const DevProblem& P, const int grp)
             for (int i = 0; i < 3; ++i) g[i] += sVg[6 + i][u];
           }
 #pragma unroll
-          for (int i = 0; i < 6; ++i) P.lm_V[6 * (size_t)L + i] = V[i];
+          for (int i = 0; i < 6; ++i) gmemw(P.lm_V)[6 * (size_t)L + i] = V[i];
 #pragma unroll
-          for (int i = 0; i < 3; ++i) P.lm_g[3 * (size_t)L + i] = g[i];
+          for (int i = 0; i < 3; ++i) gmemw(P.lm_g)[3 * (size_t)L + i] = g[i];
           if (mode == 0)  // Jacobi scaling fixed at iteration 0 (TrustRegionMinimizer)
             for (int a = 0; a < 3; ++a)
-              P.sL[3 * (size_t)L + a] = P.opt.jacobi_scaling ? 1.0 / (1.0 + sqrt(V[sym3(a, a)])) : 1.0;
+              gmemw(P.sL)[3 * (size_t)L + a] = P.opt.jacobi_scaling ? 1.0 / (1.0 + sqrt(V[sym3(a, a)])) : 1.0;
         }
         if (mode != 0) {
           const double mu = sMu;
@@ -342,7 +342,7 @@ __device__ __forceinline__ void lmVisitGroup(const DevProblem& P, const int grp)
           const double smu = sqrt(mu);
           for (int a = 0; a < 3; ++a) {
             const double dg = sqrt(fmin(fmax(A[a * 3 + a], P.opt.min_lm_diagonal), P.opt.max_lm_diagonal));
-            P.diagL[3 * (size_t)L + a] = dg;
+            gmemw(P.diagL)[3 * (size_t)L + a] = dg;
             const double d = dg * smu;
             A[a * 3 + a] += d * d;
           }
@@ -384,9 +384,9 @@ __device__ __forceinline__ void lmVisitGroup(const DevProblem& P, const int grp)
             const double sg[3] = {s[0] * g[0], s[1] * g[1], s[2] * g[2]};
             for (int a = 0; a < 3; ++a) zz[a] = Li[a * 3 + 0] * sg[0] + Li[a * 3 + 1] * sg[1] + Li[a * 3 + 2] * sg[2];
           }
-          double* Lo = P.lm_Linv + 9 * (size_t)L;
+          const auto Lo = gmemw(P.lm_Linv + 9 * (size_t)L);
           for (int i = 0; i < 9; ++i) Lo[i] = Li[i];
-          for (int a = 0; a < 3; ++a) P.lm_zz[3 * (size_t)L + a] = zz[a];
+          for (int a = 0; a < 3; ++a) gmemw(P.lm_zz)[3 * (size_t)L + a] = zz[a];
 #pragma unroll
           for (int i = 0; i < 9; ++i) sLz[i][t] = Li[i];
 #pragma unroll
@@ -419,12 +419,12 @@ __device__ __forceinline__ void lmVisitGroup(const DevProblem& P, const int grp)
       if (t < nseg * nval) {  // first pass: the prefetched range
         const int sgi = t / nval, i = t - sgi * nval;
         const int2 r = chunk == 0 ? rA : rB;
-        P.seg_hg[(size_t)(sg0 + sgi) * kSegHG + 18 * chunk + i] = rangeSum(sBuf[i], r.x, r.y);
+        gmemw(P.seg_hg)[(size_t)(sg0 + sgi) * kSegHG + 18 * chunk + i] = rangeSum(sBuf[i], r.x, r.y);
       }
       for (int e = t + kLmGroupVisits; e < nseg * nval; e += kLmGroupVisits) {
         const int sgi = e / nval, i = e - sgi * nval;
-        const int m0 = P.seg_range[2 * (sg0 + sgi)], m1 = P.seg_range[2 * (sg0 + sgi) + 1];
-        P.seg_hg[(size_t)(sg0 + sgi) * kSegHG + 18 * chunk + i] = rangeSum(sBuf[i], m0, m1);
+        const int m0 = gmem(P.seg_range)[2 * (sg0 + sgi)], m1 = gmem(P.seg_range)[2 * (sg0 + sgi) + 1];
+        gmemw(P.seg_hg)[(size_t)(sg0 + sgi) * kSegHG + 18 * chunk + i] = rangeSum(sBuf[i], m0, m1);
       }
       ldsBarrier();
     }
@@ -463,12 +463,12 @@ __device__ __forceinline__ void lmVisitGroup(const DevProblem& P, const int grp)
   ldsBarrier();
   if (t < nseg * 6) {  // first pass: the prefetched range
     const int sgi = t / 6, i = t - sgi * 6;
-    P.seg_uz[(size_t)(sg0 + sgi) * kSegUz + i] = rangeSum(sR[i], rC.x, rC.y);
+    gmemw(P.seg_uz)[(size_t)(sg0 + sgi) * kSegUz + i] = rangeSum(sR[i], rC.x, rC.y);
   }
   for (int e = t + kLmGroupVisits; e < nseg * 6; e += kLmGroupVisits) {
     const int sgi = e / 6, i = e - sgi * 6;
-    const int m0 = P.seg_range[2 * (sg0 + sgi)], m1 = P.seg_range[2 * (sg0 + sgi) + 1];
-    P.seg_uz[(size_t)(sg0 + sgi) * kSegUz + i] = rangeSum(sR[i], m0, m1);
+    const int m0 = gmem(P.seg_range)[2 * (sg0 + sgi)], m1 = gmem(P.seg_range)[2 * (sg0 + sgi) + 1];
+    gmemw(P.seg_uz)[(size_t)(sg0 + sgi) * kSegUz + i] = rangeSum(sR[i], m0, m1);
   }
   // ---- partial Schur blocks: for each pose pair of the group, rows 2h, 2h+1 of sum Z_a Z_b^T over
   // the group's landmark-pair products (fixed order), from Z staged visit-major in LDS (144-byte
@@ -488,7 +488,7 @@ __device__ __forceinline__ void lmVisitGroup(const DevProblem& P, const int grp)
   // kPartRows rows of the 6x6 block per thread (kPartThreads = 6 / kPartRows threads per block)
   for (int e = t; e < npart * kPartThreads; e += kLmGroupVisits) {
     const int pi = e / kPartThreads, h = e - pi * kPartThreads;
-    const int c0 = (e == t ? pcA : P.part_cbegin[pg0 + pi]) - pc0, c1 = (e == t ? pcB : P.part_cbegin[pg0 + pi + 1]) - pc0;
+    const int c0 = (e == t ? pcA : gmem(P.part_cbegin)[pg0 + pi]) - pc0, c1 = (e == t ? pcB : gmem(P.part_cbegin)[pg0 + pi + 1]) - pc0;
     double acc[6 * kPartRows];
 #pragma unroll
     for (int i = 0; i < 6 * kPartRows; ++i) acc[i] = 0.0;
@@ -519,7 +519,7 @@ __device__ __forceinline__ void lmVisitGroup(const DevProblem& P, const int grp)
         for (int q = 0; q < 6; ++q)
           acc[rr * 6 + q] += za[3 * rr] * zb[3 * q] + za[3 * rr + 1] * zb[3 * q + 1] + za[3 * rr + 2] * zb[3 * q + 2];
     }
-    double2* out = reinterpret_cast<double2*>(P.part_S + (size_t)(pg0 + pi) * 36 + 6 * kPartRows * h);
+    const auto out = gmemw(reinterpret_cast<double2*>(P.part_S + (size_t)(pg0 + pi) * 36 + 6 * kPartRows * h));
 #pragma unroll
     for (int q = 0; q < 3 * kPartRows; ++q) out[q] = double2{acc[2 * q], acc[2 * q + 1]};
   }
@@ -974,16 +974,16 @@ __device__ __forceinline__ void asmPairsHeavy(const DevProblem& P, int bid) {
   }
   if (lane >= 6) return;
   const bool diag = fi == fj;
-  const double si = P.sF[(size_t)foff + offi + r];
-  double* Srow = P.S + P.win_soff[w] + (int64_t)(offi + r) * P.win_fpad[w] + offj;
+  const double si = gmem(P.sF)[(size_t)foff + offi + r];
+  const auto Srow = gmemw(P.S + gmem(P.win_soff)[w] + (int64_t)(offi + r) * gmem(P.win_fpad)[w] + offj);
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
-    const double sj = P.sF[(size_t)foff + offj + q];
+    const double sj = gmem(P.sF)[(size_t)foff + offj + q];
     double val = si * sj * H[q] - Sc[q];
     if (diag && r == q) {
       const size_t idx = (size_t)foff + offi + r;
-      const double dg = sqrt(fmin(fmax(si * si * P.hdF[idx], P.opt.min_lm_diagonal), P.opt.max_lm_diagonal));
-      P.diagF[idx] = dg;
+      const double dg = sqrt(fmin(fmax(si * si * gmem(P.hdF)[idx], P.opt.min_lm_diagonal), P.opt.max_lm_diagonal));
+      gmemw(P.diagF)[idx] = dg;
       const double d = dg * sqrt(sMu);
       val += d * d;
     }
@@ -992,7 +992,7 @@ __device__ __forceinline__ void asmPairsHeavy(const DevProblem& P, int bid) {
   if (diag) {
     // Schur rhs: s_i g_i - sum_visits U_v z_l
     const size_t idx = (size_t)foff + offi + r;
-    P.rhsF[idx] = P.sF[idx] * P.gF[idx] - uz;
+    gmemw(P.rhsF)[idx] = gmem(P.sF)[idx] * gmem(P.gF)[idx] - uz;
   }
 }
 __global__ __launch_bounds__(256, 6) void k_assemble_pp(const DevProblem* __restrict__ Pp) { asmPairsHeavy(*Pp, (int)blockIdx.x); }
@@ -1092,10 +1092,10 @@ __device__ __forceinline__ void asmPairsLight(const DevProblem& P, int bid) {
     Sc[q] += __shfl(Sc[q], src, 64);
   }
   if (sub >= 6 || !live) return;
-  const double si = P.sF[(size_t)foff + offi + r];
-  double* Srow = P.S + P.win_soff[w] + (int64_t)(offi + r) * P.win_fpad[w] + offj;
+  const double si = gmem(P.sF)[(size_t)foff + offi + r];
+  const auto Srow = gmemw(P.S + gmem(P.win_soff)[w] + (int64_t)(offi + r) * gmem(P.win_fpad)[w] + offj);
 #pragma unroll
-  for (int q = 0; q < 6; ++q) Srow[q] = si * P.sF[(size_t)foff + offj + q] * H[q] - Sc[q];
+  for (int q = 0; q < 6; ++q) Srow[q] = si * gmem(P.sF)[(size_t)foff + offj + q] * H[q] - Sc[q];
 }
 __global__ __launch_bounds__(256) void k_assemble_pp_light(const DevProblem* __restrict__ Pp) { asmPairsLight(*Pp, (int)blockIdx.x); }
 
@@ -1143,12 +1143,12 @@ __device__ __forceinline__ void asmPairsSb(const DevProblem& P, int bid) {
   if ((sDone != 0) | (sNeed == 0) | (sFail != 0)) return;  // gnSelect
   const int ni = ki == 0 ? 6 : 9, nj = kj == 0 ? 6 : 9;
   const bool diag = fi == fj;
-  double* S = P.S + soff;
+  const auto S = gmemw(P.S + soff);
   const double smu = sqrt(sMu);
   const auto imuH = gmem(P.imu_H);
   for (int e = lane; e < ni * nj; e += 64) {
     const int r = e / nj, q = e - r * nj;
-    const double si = P.sF[(size_t)foff + offi + r], sj = P.sF[(size_t)foff + offj + q];
+    const double si = gmem(P.sF)[(size_t)foff + offi + r], sj = gmem(P.sF)[(size_t)foff + offj + q];
     double H = 0.0;
     if (nc <= kSbPre) {
       double v[kSbPre];
@@ -1169,8 +1169,8 @@ __device__ __forceinline__ void asmPairsSb(const DevProblem& P, int bid) {
     double val = si * sj * H;
     if (diag && r == q) {
       const size_t idx = (size_t)foff + offi + r;
-      const double dg = sqrt(fmin(fmax(si * si * P.hdF[idx], P.opt.min_lm_diagonal), P.opt.max_lm_diagonal));
-      P.diagF[idx] = dg;
+      const double dg = sqrt(fmin(fmax(si * si * gmem(P.hdF)[idx], P.opt.min_lm_diagonal), P.opt.max_lm_diagonal));
+      gmemw(P.diagF)[idx] = dg;
       const double d = dg * smu;
       val += d * d;
     }
@@ -1178,7 +1178,7 @@ __device__ __forceinline__ void asmPairsSb(const DevProblem& P, int bid) {
   }
   if (diag && lane < ni) {
     const size_t idx = (size_t)foff + offi + lane;
-    P.rhsF[idx] = P.sF[idx] * P.gF[idx];
+    gmemw(P.rhsF)[idx] = gmem(P.sF)[idx] * gmem(P.gF)[idx];
   }
 }
 __global__ __launch_bounds__(256) void k_assemble_sb(const DevProblem* __restrict__ Pp) { asmPairsSb(*Pp, (int)blockIdx.x); }
