@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B of the batch graph's assembly on three streams (libokvisgpu.so) against two (lib_asm2.so):
 # the default batched bench line twice each, then 256 windows per GPU.
+# (the OKG_ASM_STREAMS switch lived in runtime.cpp for this A/B only; result: profiles/r06_asm_streams_ab.txt)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
