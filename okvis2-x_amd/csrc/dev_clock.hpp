@@ -77,7 +77,8 @@ static __device__ unsigned int g_imuDone;
 #endif
 
 // ---- k_lm_visit<1> (-DOKG_LMV_CLOCK): thread 0 of every workgroup adds its s_memrealtime ticks per
-// phase with vector atomics; the last workgroup prints the totals. Uses the kernel's `mode`.
+// phase with vector atomics; the last landmark group prints the totals (also inside k_lin_few, whose
+// grid has further blocks). Uses the kernel's `mode` and `P`.
 #ifdef OKG_LMV_CLOCK
 static __device__ unsigned long long g_lmvClk[8];
 static __device__ unsigned int g_lmvDone;
@@ -91,7 +92,7 @@ static __device__ unsigned int g_lmvDone;
 #define LCLK_END                                                                        \
   if (mode == 1 && threadIdx.x == 0) {                                                  \
     __threadfence();                                                                    \
-    if (atomicAdd(&g_lmvDone, 1u) == gridDim.x - 1) {                                   \
+    if (atomicAdd(&g_lmvDone, 1u) == (unsigned)P.n_lmg - 1) {                          \
       printf("LMVCLK visit %llu lm %llu seg %llu z %llu stage %llu part %llu (x10ns, summed)\n", \
              g_lmvClk[0], g_lmvClk[1], g_lmvClk[2], g_lmvClk[3], g_lmvClk[4], g_lmvClk[5]);       \
       for (int i = 0; i < 8; ++i) g_lmvClk[i] = 0;                                      \

@@ -152,6 +152,7 @@ struct HostBatch {
   int64_t defer_total = 0;
   bool any_split = false;
   bool nd = false;  // order the windows' states for the tile-parallel schedule (nested dissection)
+  int lmg_visits = kLmGroupVisits, lmg_lms = kLmGroupMax;  // landmark-group bounds (k_lm_visit workgroups)
   std::vector<int32_t> chol_root_items;  // (w, d, first-root-of-window flag): tiles no update writes
   int n_chol_launches = 1;
   std::vector<Contrib> fb_contrib;
@@ -988,7 +989,7 @@ void analyse(const std::vector<const okvisgpu_problem*>& probs,
           throw ArgError{"landmark with more than " + std::to_string(kLmGroupVisits) + " observing poses"};
         const int gv = lmVisitBegin[l] - lmVisitBegin[g0] + lmXBegin[l] - lmXBegin[g0];
         const int pcl = pairCount(l);
-        if (l > g0 && (gv + nv > kLmGroupVisits || gl == kLmGroupMax || gpc + pcl > kLmPartStage)) {
+        if (l > g0 && (gv + nv > B.lmg_visits || gl == B.lmg_lms || gpc + pcl > kLmPartStage)) {
           closeGroup(g0, l);
           g0 = l;
           gl = 0;
@@ -1825,6 +1826,23 @@ struct okvisgpu_ctx {
       nb.nd = (int)probs.size() < cuCount;
 #ifdef OKG_ND_OVERRIDE
       if (const char* e = std::getenv("OKVISGPU_ND")) nb.nd = e[0] == '1';  // (development A/B builds only)
+#endif
+      // smaller landmark groups where a window's linearisation is a latency chain (fewWindows: one
+      // workgroup per group, ~16 us of phases for a 256-visit group): 64 visits / 16 landmarks
+      // (one S50 window: 36 -> 144 groups; steady iteration 0.3144 -> 0.3121 ms, S10 0.1580 ->
+      // 0.1541 ms, profiles/r06_lmg_ab.txt). Like the state order, a function of the batch size only.
+      if (fewWindows((int)probs.size(), cuCount)) {
+        nb.lmg_visits = 64;
+        nb.lmg_lms = 16;
+      }
+#ifdef OKG_LMG_OVERRIDE  // (development A/B builds only: OKVISGPU_LMG=visits,landmarks)
+      if (const char* e = std::getenv("OKVISGPU_LMG")) {
+        int v = 0, m = 0;
+        if (std::sscanf(e, "%d,%d", &v, &m) == 2 && v >= 1 && v <= kLmGroupVisits && m >= 1 && m <= kLmGroupMax) {
+          nb.lmg_visits = v;
+          nb.lmg_lms = m;
+        }
+      }
 #endif
       analyse(probs, constOverride, nb);  // may throw: B is untouched until it succeeds
       B = std::move(nb);
