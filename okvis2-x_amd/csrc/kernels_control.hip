@@ -15,107 +15,21 @@
 //               the candidate parameter set, model_cost_change and the step-validity bookkeeping.
 #include <cfloat>
 
+#include "block_reduce.hpp"
 #include "device_problem.hpp"
+#include "gradnorm.hpp"
 #include "jv_groups.hpp"
 #include "launch.hpp"
 #include "okvisgpu_math.hpp"
 
 namespace okg {
 
-// Per-window workgroup size of k_reduce, k_gradnorm and k_dogleg: 256 threads for batches, 1,024
+// Per-window workgroup size of k_reduce and k_dogleg (k_gradnorm: always 256): 256 threads for batches, 1,024
 // when the batch has at most a quarter window per CU (a single window's reductions are chains of
 // dependent loads per thread: four times the threads, a quarter of the chain). A power of two in
 // [64, 1024] (the tree reductions); the reduction order follows it, so a window's bits depend on
 // the batch size only through this choice (and the Cholesky order, runtime.cpp build).
 constexpr int kRBBatch = 256, kRBFew = 1024;
-
-// Fixed-order tree reductions over the workgroup. The barriers order LDS only (ldsBarrier): a
-// __syncthreads() also waited for every global store still in flight (k_dogleg's Plus pass leaves
-// thousands), and N values reduced together share one tree's barriers: per value the same
-// additions in the same order as a separate tree, so the same bits.
-// The levels that pair entries of different wavefronts (s >= 128) go through LDS with a barrier
-// each; the last seven (s = 64 .. 1) run in wavefront 0, lane t holding entry t, each level adding
-// lane t + s to lane t as the LDS level did (same pairs, same operand order, so the same bits):
-// 6 barriers per tree instead of 12 at 1,024 threads (a single window's reductions), 4 instead of
-// 10 at 256.
-template <int RB, class Op>
-__device__ __forceinline__ double treeTail(const double* sh, int t, Op op) {  // (t < 64; entry 0's total in lane 0)
-  double a = RB >= 128 ? op(sh[t], sh[t + 64]) : sh[t];
-#pragma unroll
-  for (int s = 32; s > 0; s >>= 1) a = op(a, __shfl_down(a, s, 64));
-  return a;
-}
-template <int RB, int N>
-__device__ __forceinline__ void blockSumN(double (&v)[N], double* sh) {  // sh: N * RB doubles
-  static_assert(RB >= 64 && (RB & (RB - 1)) == 0, "a power of two from 64");
-  const int t = threadIdx.x;
-#pragma unroll
-  for (int n = 0; n < N; ++n) sh[n * RB + t] = v[n];
-  ldsBarrier();
-  for (int s = RB / 2; s >= 128; s >>= 1) {
-    if (t < s) {
-#pragma unroll
-      for (int n = 0; n < N; ++n) sh[n * RB + t] += sh[n * RB + t + s];
-    }
-    ldsBarrier();
-  }
-  if (t < 64) {
-    double r[N];
-#pragma unroll
-    for (int n = 0; n < N; ++n) r[n] = treeTail<RB>(sh + n * RB, t, [](double x, double y) { return x + y; });
-    __builtin_amdgcn_wave_barrier();  // (every lane's reads of sh before lane 0's writes)
-    if (t == 0) {
-#pragma unroll
-      for (int n = 0; n < N; ++n) sh[n * RB] = r[n];
-    }
-  }
-  ldsBarrier();
-#pragma unroll
-  for (int n = 0; n < N; ++n) v[n] = sh[n * RB];
-  ldsBarrier();
-}
-template <int RB>
-__device__ __forceinline__ double blockSum(double v, double* sh) {
-  double a[1] = {v};
-  blockSumN<RB, 1>(a, sh);
-  return a[0];
-}
-// Strided per-thread loop over i = b + t, b + t + RB, ... < e with the loads of U consecutive
-// iterations issued before any of them is consumed. A window's reductions run in one workgroup, so a
-// single window is a chain of dependent loads per thread; batching shortens it U-fold. use() sees the
-// elements in the order of the plain loop, so every sum is bitwise the same.
-template <int RB, int U, class Load, class Use>
-__device__ __forceinline__ void stridedBatched(int b, int e, Load load, Use use) {
-  int i = b + (int)threadIdx.x;
-  for (; i + (U - 1) * RB < e; i += U * RB) {
-    decltype(load(i)) v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = load(i + u * RB);
-#pragma unroll
-    for (int u = 0; u < U; ++u) use(i + u * RB, v[u]);
-  }
-  for (; i < e; i += RB) use(i, load(i));
-}
-
-template <int RB>
-__device__ __forceinline__ double blockMax(double v, double* sh) {
-  const int t = threadIdx.x;
-  sh[t] = v;
-  ldsBarrier();
-  for (int s = RB / 2; s >= 128; s >>= 1) {
-    if (t < s) sh[t] = fmax(sh[t], sh[t + s]);
-    ldsBarrier();
-  }
-  if (t < 64) {
-    const double m = treeTail<RB>(sh, t, [](double x, double y) { return fmax(x, y); });
-    __builtin_amdgcn_wave_barrier();
-    if (t == 0) sh[0] = m;
-  }
-  ldsBarrier();
-  const double r = sh[0];
-  ldsBarrier();
-  return r;
-}
 
 // Bookkeeping common to every iteration end (FinalizeIterationAndCheckIfMinimizerCanContinue):
 // iteration cap, then the trust-region radius floor. (The gradient test follows the next
@@ -292,93 +206,10 @@ __global__ __launch_bounds__(RB) void k_reduce(const DevProblem* __restrict__ Pp
   reduceJv<RB>(P, w, s, sh);
 }
 
-// |x - Plus(x, -g)| and |x| over the window's active blocks; gradient tolerance test.
+// |x - Plus(x, -g)| and |x| over the window's active blocks; gradient tolerance test (gradnorm.hpp).
 template <int RB>
 __global__ __launch_bounds__(RB) void k_gradnorm(const DevProblem* __restrict__ Pp, int lin_mode) {
-  const DevProblem& P = *Pp;
-  const int w = blockIdx.x;
-  WinState& s = P.st[w];
-  if (s.done) return;
-  if (lin_mode == 1 && !s.accepted) return;
-  __shared__ double sh[3 * RB];
-  const int t = threadIdx.x;
-  const int xs = s.xcur;
-  const int foff = P.win_foff[w];
-  double mx = 0.0, g2 = 0.0, x2 = 0.0;
-  const int p0 = P.win_pose_range[2 * w], p1 = P.win_pose_range[2 * w + 1];
-  for (int p = p0 + t; p < p1; p += RB) {
-    if (!gmem(P.pose_active)[p]) continue;
-    const auto x = gmem(P.pose[xs] + 7 * (size_t)p);
-    for (int k = 0; k < 7; ++k) x2 += x[k] * x[k];
-    const int pf = gmem(P.pose_f)[p];
-    const auto g = gmem(P.gF + foff + pf);
-    double xp[7];
-    for (int k = 0; k < 3; ++k) xp[k] = x[k] + (-g[k]);
-    const Q dq = deltaQ(-g[3], -g[4], -g[5]);
-    const Q q = qnormalize(qmul(dq, qnormalize(Q{x[3], x[4], x[5], x[6]})));
-    xp[3] = q.x; xp[4] = q.y; xp[5] = q.z; xp[6] = q.w;
-    for (int k = 0; k < 7; ++k) {
-      const double d = x[k] - xp[k];
-      mx = fmax(mx, fabs(d));
-      g2 += d * d;
-    }
-  }
-  const int s0 = P.win_sb_range[2 * w], s1 = P.win_sb_range[2 * w + 1];
-  for (int b = s0 + t; b < s1; b += RB) {
-    if (!gmem(P.sb_active)[b]) continue;
-    const auto x = gmem(P.sb[xs] + 9 * (size_t)b);
-    const auto g = gmem(P.gF + foff + gmem(P.sb_f)[b]);
-    for (int k = 0; k < 9; ++k) {
-      x2 += x[k] * x[k];
-      const double d = x[k] - (x[k] + (-g[k]));
-      mx = fmax(mx, fabs(d));
-      g2 += d * d;
-    }
-  }
-  const int l0 = P.win_lm_range[2 * w], l1 = P.win_lm_range[2 * w + 1];
-  struct LX { double x[4], g[3]; uint8_t f; };
-  stridedBatched<RB, 4>(l0, l1,
-                    [&](int l) {
-                      LX v;
-                      v.f = gmem(P.lm_free)[l];
-                      for (int k = 0; k < 4; ++k) v.x[k] = gmem(P.lm[xs])[4 * (size_t)l + k];
-                      for (int k = 0; k < 3; ++k) v.g[k] = gmem(P.lm_g)[3 * (size_t)l + k];
-                      return v;
-                    },
-                    [&](int, const LX& v) {
-                      if (!v.f) return;
-                      for (int k = 0; k < 4; ++k) x2 += v.x[k] * v.x[k];
-                      for (int k = 0; k < 3; ++k) {
-                        const double d = v.x[k] - (v.x[k] + (-v.g[k]));
-                        mx = fmax(mx, fabs(d));
-                        g2 += d * d;
-                      }
-                    });
-  mx = blockMax<RB>(mx, sh);
-  {
-    double r2[2] = {g2, x2};
-    blockSumN<RB, 2>(r2, sh);
-    g2 = r2[0];
-    x2 = r2[1];
-  }
-  if (t != 0) return;
-  s.grad_max_norm = mx;
-  s.grad_norm = sqrt(g2);
-  s.x_norm = sqrt(x2);
-  if (lin_mode == 0 && s.iteration >= P.opt.max_num_iterations) {
-    s.done = 1;
-    s.termination = 1;
-    return;
-  }
-  if (mx <= P.opt.gradient_tolerance) {
-    s.done = 1;
-    s.termination = 0;
-    return;
-  }
-  if (lin_mode == 0 && s.radius <= P.opt.min_radius) {
-    s.done = 1;
-    s.termination = 0;
-  }
+  gradnormWindow<RB>(*Pp, (int)blockIdx.x, lin_mode);
 }
 
 // One workgroup per window: GN failure handling, traditional dogleg step, Plus into X[1-xcur].
@@ -632,10 +463,10 @@ void launch_reduce(const DevProblem& P, int mode, hipStream_t s) {
   if (fewWindows(P.n_win, P.cu_count)) hipLaunchKernelGGL(k_reduce<kRBFew>, dim3(P.n_win), dim3(kRBFew), 0, s, P.self, mode);
   else hipLaunchKernelGGL(k_reduce<kRBBatch>, dim3(P.n_win), dim3(kRBBatch), 0, s, P.self, mode);
 }
+// (256 threads for every batch size: the few-window iteration runs the same test inside the
+// assembly launch, k_assemble_few, and both forms must give the same bits)
 void launch_gradnorm(const DevProblem& P, int lin_mode, hipStream_t s) {
-  if (fewWindows(P.n_win, P.cu_count))
-    hipLaunchKernelGGL(k_gradnorm<kRBFew>, dim3(P.n_win), dim3(kRBFew), 0, s, P.self, lin_mode);
-  else hipLaunchKernelGGL(k_gradnorm<kRBBatch>, dim3(P.n_win), dim3(kRBBatch), 0, s, P.self, lin_mode);
+  hipLaunchKernelGGL(k_gradnorm<kRBBatch>, dim3(P.n_win), dim3(kRBBatch), 0, s, P.self, lin_mode);
 }
 void launch_dogleg(const DevProblem& P, hipStream_t s) {
   if (fewWindows(P.n_win, P.cu_count)) hipLaunchKernelGGL(k_dogleg<kRBFew>, dim3(P.n_win), dim3(kRBFew), 0, s, P.self);

@@ -26,6 +26,7 @@
 
 #include "dev_clock.hpp"
 #include "device_problem.hpp"
+#include "gradnorm.hpp"
 #include "launch.hpp"
 #include "okvisgpu_math.hpp"
 
@@ -1252,23 +1253,33 @@ void launch_zero_S(const DevProblem& P, hipStream_t s, int tail) {
 }
 // Few windows: the three assembly kernels as one launch (block ranges; the kernels are independent:
 // disjoint pairs of S), two graph nodes fewer on a single window's latency chain.
-__global__ __launch_bounds__(256) void k_assemble_few(const DevProblem* __restrict__ Pp, int nHeavy, int nLight) {
+// With grad (the captured few-window iteration, runtime.cpp launchIteration): one more block per
+// window runs the gradient tolerance test of the previous iteration's linearisation (gradnorm.hpp,
+// 256 threads as everywhere): it reads the parameters, the gradient and the window state, which
+// the assembly does not write, and the assembly needs no result of it (a window it ends is
+// skipped from the Cholesky on), so the two share a launch instead of following each other.
+__global__ __launch_bounds__(256) void k_assemble_few(const DevProblem* __restrict__ Pp, int nHeavy, int nLight, int nAsm) {
   const DevProblem& P = *Pp;
   const int b = blockIdx.x;
   if (b < nHeavy) asmPairsHeavy(P, b);
   else if (b < nHeavy + nLight) asmPairsLight(P, b - nHeavy);
-  else asmPairsSb(P, b - nHeavy - nLight);
+  else if (b < nAsm) asmPairsSb(P, b - nHeavy - nLight);
+  else gradnormWindow<256>(P, b - nAsm, 1);
+}
+static void launchAssembleFew(const DevProblem& P, hipStream_t s, bool grad) {
+  const int nH = (P.n_asm_pp + 3) / 4, nL = (P.n_asm_ppl + 256 / kPplLanes - 1) / (256 / kPplLanes),
+            nS = (P.n_asm_sb + 3) / 4, nA = nH + nL + nS, nG = grad ? P.n_win : 0;
+  if (nA + nG > 0) hipLaunchKernelGGL(k_assemble_few, dim3(nA + nG), dim3(256), 0, s, P.self, nH, nL, nA);
 }
 void launch_assemble(const DevProblem& P, hipStream_t s) {
   if (fewWindows(P.n_win, P.cu_count)) {
-    const int nH = (P.n_asm_pp + 3) / 4, nL = (P.n_asm_ppl + 256 / kPplLanes - 1) / (256 / kPplLanes),
-              nS = (P.n_asm_sb + 3) / 4;
-    if (nH + nL + nS > 0) hipLaunchKernelGGL(k_assemble_few, dim3(nH + nL + nS), dim3(256), 0, s, P.self, nH, nL);
+    launchAssembleFew(P, s, false);
     return;
   }
   launch_assemble_pp(P, s);
   launch_assemble_sb(P, s);
 }
+void launch_assemble_gradnorm_few(const DevProblem& P, hipStream_t s) { launchAssembleFew(P, s, true); }
 void launch_gn_reduce(const DevProblem& P, hipStream_t s) {
   launch_lm_prep(P, s);
   launch_assemble(P, s);

@@ -38,6 +38,7 @@ bool lin_runs_prep(const DevProblem& P);
 void launch_zero_S(const DevProblem& P, hipStream_t s, int tail = 0);
 void launch_assemble(const DevProblem& P, hipStream_t s);
 void launch_lm_backsub(const DevProblem& P, hipStream_t s);  // kernels_backsub.hip: + landmark dogleg vectors, J*v
+void launch_assemble_gradnorm_few(const DevProblem& P, hipStream_t s);  // few windows: + the gradient test
 void launch_assemble_pp(const DevProblem& P, hipStream_t s);
 void launch_assemble_sb(const DevProblem& P, hipStream_t s);
 void launch_lm_visit(const DevProblem& P, int mode, hipStream_t s);  // 0/1: linearisation, 2: GN prep

@@ -2261,16 +2261,27 @@ struct okvisgpu_ctx {
     HIPCHK(hipGetLastError());
   }
 
+  // One iteration. Few windows (a latency chain of small launches): the gradient test of an
+  // iteration runs inside the next iteration's assembly launch (k_assemble_few; it reads nothing the
+  // assembly writes, and a window it ends is skipped from the Cholesky on), and the captured
+  // graph ends with one standalone test (graphTail), so that every graph launch leaves complete
+  // window states. The test is idempotent (the same state gives the same norms and decision), so
+  // the repeat at the start of the next graph launch is harmless.
+  bool fusedGradnorm() const { return fewWindows(P.n_win, P.cu_count); }
   void launchIteration() {
     if (!lin_runs_prep(P)) launch_lm_prep(P, stream);
-    launch_assemble(P, stream);
+    if (fusedGradnorm()) launch_assemble_gradnorm_few(P, stream);
+    else launch_assemble(P, stream);
     launch_cholesky(P, stream);
     launch_gn_backsub(P, stream);  // (with the factors' J*v)
     launch_dogleg(P, stream);
     evalAll(1, stream);
     launch_reduce(P, R_COST_CAND, stream);
     launch_linearization_blocks(P, 1, stream);
-    launch_gradnorm(P, 1, stream);
+    if (!fusedGradnorm()) launch_gradnorm(P, 1, stream);
+  }
+  void graphTail(bool serial) {
+    if (serial && fusedGradnorm()) launch_gradnorm(P, 1, stream);
   }
 
   // The captured iteration with the independent kernels of a phase on fork streams, so the graph
@@ -2341,6 +2352,7 @@ struct okvisgpu_ctx {
     forkEvUsed = 0;
     if (serial) launchIteration();
     else launchIterationForked();
+    graphTail(serial);
     HIPCHK(hipStreamEndCapture(stream, &g));
     HIPCHK(hipGraphInstantiate(&iterGraph, g, nullptr, nullptr, 0));
     HIPCHK(hipGraphDestroy(g));
@@ -2354,6 +2366,7 @@ struct okvisgpu_ctx {
         if (serial) launchIteration();
         else launchIterationForked();
       }
+      graphTail(serial);
       HIPCHK(hipStreamEndCapture(stream, &g));
       HIPCHK(hipGraphInstantiate(&iterGraphK, g, nullptr, nullptr, 0));
       HIPCHK(hipGraphDestroy(g));
