@@ -255,6 +255,39 @@ def test_window_alone_vs_large_batch(og, gpu_ctx, parity, n_batch):
                float(np.abs(w.poses()[:, :3] - Pb[k][:, :3]).max()), 1e-8)
 
 
+@pytest.mark.parametrize("n_batch", [1, 80], ids=["alone", "batch80"])
+def test_gradient_tolerance_termination(og, oracle, gpu_ctx, parity, n_batch):
+    """The gradient test ends the solve at the oracle's iteration (TrustRegionMinimizer: max-norm of
+    x - Plus(x, -g) <= gradient_tolerance after an accepted step). Alone (a quarter window per CU or
+    less) the test runs inside the next iteration's assembly launch with one standalone test closing
+    each captured graph; in a batch of 80 it is its own launch. The tolerance is picked so that the
+    oracle converges by it after 5 to 20 iterations (three tolerances, so that the last iteration
+    falls at different places of the four-iteration graphs); iterations, termination, steps exact,
+    cost 1e-7."""
+    w = _window(og, seed=61)
+    base = dict(max_num_iterations=25, function_tolerance=0.0, parameter_tolerance=0.0)
+    picks = []
+    for g in (3e3, 1e3, 3e2, 1e2, 3e1, 1e1, 3.0, 1.0, 0.3, 0.1, 3e-2, 1e-2, 3e-3, 1e-3, 1e-4, 1e-5, 1e-6):
+        w.reset()
+        so = oracle.solve(w.problem_ptr(), og.default_options(gradient_tolerance=g, **base))
+        if so["termination"] == "CONVERGENCE" and 5 <= so["num_iterations"] <= 20:
+            picks.append((g, so))
+        if len(picks) == 3:
+            break
+    assert picks, "no gradient tolerance ends the oracle's solve by its gradient test"
+    others = [_window(og, seed=700 + k) for k in range(n_batch - 1)]
+    for g, so in picks:
+        w.reset()
+        for o in others:
+            o.reset()
+        gpu_ctx.set_problems([w.problem] + [o.problem for o in others])
+        sg = gpu_ctx.solve(og.default_options(gradient_tolerance=g, **base), n_batch)[0]
+        for f in ("num_iterations", "termination", "num_successful_steps", "num_unsuccessful_steps"):
+            assert sg[f] == so[f], (f, g, sg, so)
+        parity(f"gradient-tolerance {g:g} termination ({'alone' if n_batch == 1 else 'batch of 80'}): final cost (rel)",
+               abs(sg["final_cost"] - so["final_cost"]) / so["final_cost"], 1e-7)
+
+
 def test_solve_is_deterministic(og, gpu_ctx):
     w = _window(og)
     opts = og.default_options(max_num_iterations=5)
