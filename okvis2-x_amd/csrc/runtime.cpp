@@ -2865,7 +2865,16 @@ int okvisgpu_plan_window(const okvisgpu_problem* p, int32_t nested_dissection, i
   try {
     HostBatch B;
     B.nd = nested_dissection != 0;
+#ifdef OKG_ANALYSE_TIMING
+    for (double& x : g_atime) x = 0.0;
+    g_alast = std::chrono::steady_clock::now();
+#endif
     analyse({p}, {}, B);
+#ifdef OKG_ANALYSE_TIMING
+    std::fprintf(stderr, "analyse ms:");
+    for (int i = 0; i < 11; ++i) std::fprintf(stderr, " [%d] %.3f", i, g_atime[i]);
+    std::fprintf(stderr, "\n");
+#endif
     const int T = B.tileT[0], fpad = B.win_fpad[0];
     const auto& nz = B.tileNz[0];
     std::vector<int> L, last;
