@@ -25,9 +25,11 @@ static __device__ unsigned long long g_cholClk[32];
 #define CHOL_CLK_REPORT(T)                                                                               \
   if (blockIdx.x == 0 && threadIdx.x == 0)                                                               \
     printf("CHOLCLK T=%d potrf %llu panel %llu update %llu bsub %llu | load %llu pfac %llu ptrail %llu " \
-           "dinv %llu subd %llu store %llu y %llu (x10ns)\n",                                            \
+           "dinv %llu subd %llu store %llu y %llu | sweep: wait %llu lookahead %llu chol8 %llu "         \
+           "publish %llu loop %llu (x10ns)\n",                                                            \
            (T), g_cholClk[0], g_cholClk[1], g_cholClk[2] + g_cholClk[11], g_cholClk[3], g_cholClk[4],    \
-           g_cholClk[5], g_cholClk[6], g_cholClk[7], g_cholClk[8], g_cholClk[9], g_cholClk[10]);
+           g_cholClk[5], g_cholClk[6], g_cholClk[7], g_cholClk[8], g_cholClk[9], g_cholClk[10],          \
+           g_cholClk[21], g_cholClk[22], g_cholClk[23], g_cholClk[24], g_cholClk[25]);
 #define BSUB_CLK_REPORT(T)                                                                               \
   if (blockIdx.x == 0 && threadIdx.x == 0)                                                               \
     printf("BSUBCLK T=%d init %llu steps %llu (x10ns)\n", (T), g_cholClk[12], g_cholClk[13]);
