@@ -159,6 +159,9 @@ constexpr int kImuFewChunkWindows = 2;
 #ifndef OKG_IMU_FEW_K
 #define OKG_IMU_FEW_K 16  // (build knob for A/B measurements)
 #endif
+#ifndef OKG_IMU_JAC_ROWS
+#define OKG_IMU_JAC_ROWS 1  // (build knob: 0 forms the Jacobian by columns)
+#endif
 #ifndef OKG_IMU_FREG
 #define OKG_IMU_FREG 1  // (build knob: 0 reads F_delta from LDS in both products of a step)
 #endif
@@ -952,8 +955,51 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
   if (live && l == 0) gmemw(P.imu_cost[lb])[f] = 0.5 * c2;
   __syncthreads();
   ICLK(4)
-  // J = U [F0 | F1]; lane l computes columns l and l + 16 of the 15 x 30 Jacobian. Column j of
-  // [F0 | F1] has at most three non-zero 3-blocks: (block row, staged block, sign, or identity).
+  // J = U [F0 | F1]. Column j of [F0 | F1] has at most three non-zero 3-blocks: (block row, staged
+  // block, sign, or identity); the table depends on j only.
+#if OKG_IMU_JAC_ROWS
+  // Lane l < 15 forms row l of J: U's row l in registers, the 30 columns unrolled (the column
+  // table a compile-time constant), the staged blocks read as LDS broadcasts; every entry is the
+  // same expression as in the column form (same bits), and a lane's 30 stores are contiguous.
+  if (live && l < 15) {
+    double u[15];
+#pragma unroll
+    for (int k = 0; k < 15; ++k) u[k] = sA[l * kS + k];
+#pragma unroll
+    for (int j = 0; j < 30; ++j) {
+      const bool right = j >= 15;
+      const int jj = right ? j - 15 : j, bj = jj / 3, c = jj % 3;
+      int nt = 0, trow[3] = {0, 0, 0}, tblk[3] = {0, 0, 0};
+      double tsc[3] = {0.0, 0.0, 0.0};
+      auto add = [&](int row, int blk, double sc) { trow[nt] = row; tblk[nt] = blk; tsc[nt] = sc; ++nt; };
+      if (!right) {
+        if (bj == 0) add(0, 0, 1.0);
+        else if (bj == 1) { add(0, 1, 1.0); add(3, 2, 1.0); add(6, 3, 1.0); }
+        else if (bj == 2) { add(0, 0, Dt); add(6, 0, 1.0); }
+        else if (bj == 3) { add(0, 4, 1.0); add(3, 5, 1.0); add(6, 6, 1.0); }
+        else { add(0, 7, -1.0); add(6, 8, -1.0); }
+      } else {
+        if (bj == 0) add(0, 0, -1.0);
+        else if (bj == 1) add(3, 9, 1.0);
+        else if (bj == 2) add(6, 0, -1.0);
+      }
+      const int idrow = (bj >= 3) ? 3 * bj + c : -1;
+      const double idv = right ? -1.0 : 1.0;
+      double acc = 0.0;
+      if (success) {
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+          if (t < nt) {
+            const double* Bk = sB + tblk[t] * 9;
+            acc += tsc[t] * (u[trow[t]] * Bk[0 * 3 + c] + u[trow[t] + 1] * Bk[1 * 3 + c] + u[trow[t] + 2] * Bk[2 * 3 + c]);
+          }
+        if (idrow >= 0) acc += idv * u[idrow];
+      }
+      lin[15 + l * 30 + j] = acc;
+    }
+  }
+#else
+  // (column form: lane l computes columns l and l + 16)
   if (live) {
     for (int pass = 0; pass < 2; ++pass) {
       const int j = l + 16 * pass;
@@ -991,6 +1037,7 @@ __device__ __forceinline__ void evalImuBlock(const DevProblem& P, int mode, int 
       }
     }
   }
+#endif
   ICLK(5)
   ICLK_END
 }
