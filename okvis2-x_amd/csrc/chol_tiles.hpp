@@ -46,7 +46,7 @@ struct TileSrc {
   int T;
   int64_t ld;
   __device__ __forceinline__ const double* at(int i, int j, int k) const {
-    return (fu[i * T + j] < k ? W : S) + (int64_t)i * kTile * ld + j * kTile;
+    return (gmem(fu)[i * T + j] < k ? W : S) + (int64_t)i * kTile * ld + j * kTile;
   }
 };
 __device__ __forceinline__ TileSrc tileSrc(const DevProblem& P, int w, int64_t ld) {
