@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B of non-temporal S-tile reads in the persistent Cholesky (libokvisgpu.so) against ordinary
 # loads (lib_nont.so): k_cholesky at 2,048 and 512 windows, the batched bench line, twice.
+# (the OKG_CHOL_NT switch lived in kernels_chol.hip for this A/B only; result: profiles/r06_chol_nt_ab.txt)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
