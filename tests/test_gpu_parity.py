@@ -255,12 +255,14 @@ def test_window_alone_vs_large_batch(og, gpu_ctx, parity, n_batch):
                float(np.abs(w.poses()[:, :3] - Pb[k][:, :3]).max()), 1e-8)
 
 
-@pytest.mark.parametrize("n_batch", [1, 80], ids=["alone", "batch80"])
+@pytest.mark.parametrize("n_batch", [1, 80, 300], ids=["alone", "batch80", "batch300"])
 def test_gradient_tolerance_termination(og, oracle, gpu_ctx, parity, n_batch):
     """The gradient test ends the solve at the oracle's iteration (TrustRegionMinimizer: max-norm of
     x - Plus(x, -g) <= gradient_tolerance after an accepted step). Alone (a quarter window per CU or
     less) the test runs inside the next iteration's assembly launch with one standalone test closing
-    each captured graph; in a batch of 80 it is its own launch. The tolerance is picked so that the
+    each captured graph; in a batch of 80 (one-stream graph) it is its own launch after the
+    linearisation; in a batch of 300 (the forked graph: more windows than CUs on MI355X) likewise,
+    after k_fgrad on the main stream. The tolerance is picked so that the
     oracle converges by it after 5 to 20 iterations (three tolerances, so that the last iteration
     falls at different places of the four-iteration graphs); iterations, termination, steps exact,
     cost 1e-7."""
@@ -284,7 +286,7 @@ def test_gradient_tolerance_termination(og, oracle, gpu_ctx, parity, n_batch):
         sg = gpu_ctx.solve(og.default_options(gradient_tolerance=g, **base), n_batch)[0]
         for f in ("num_iterations", "termination", "num_successful_steps", "num_unsuccessful_steps"):
             assert sg[f] == so[f], (f, g, sg, so)
-        parity(f"gradient-tolerance {g:g} termination ({'alone' if n_batch == 1 else 'batch of 80'}): final cost (rel)",
+        parity(f"gradient-tolerance {g:g} termination ({'alone' if n_batch == 1 else f'batch of {n_batch}'}): final cost (rel)",
                abs(sg["final_cost"] - so["final_cost"]) / so["final_cost"], 1e-7)
 
 
