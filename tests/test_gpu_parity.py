@@ -255,12 +255,13 @@ def test_window_alone_vs_large_batch(og, gpu_ctx, parity, n_batch):
                float(np.abs(w.poses()[:, :3] - Pb[k][:, :3]).max()), 1e-8)
 
 
-@pytest.mark.parametrize("n_batch", [1, 80, 300], ids=["alone", "batch80", "batch300"])
+@pytest.mark.parametrize("n_batch", [1, 8, 80, 300], ids=["alone", "batch8", "batch80", "batch300"])
 def test_gradient_tolerance_termination(og, oracle, gpu_ctx, parity, n_batch):
     """The gradient test ends the solve at the oracle's iteration (TrustRegionMinimizer: max-norm of
-    x - Plus(x, -g) <= gradient_tolerance after an accepted step). Alone (a quarter window per CU or
-    less) the test runs inside the next iteration's assembly launch with one standalone test closing
-    each captured graph; in a batch of 80 (one-stream graph) it is its own launch after the
+    x - Plus(x, -g) <= gradient_tolerance after an accepted step). Alone and in a batch of 8 (a
+    quarter window per CU or less) the test runs inside the next iteration's assembly launch with one
+    standalone test closing each captured graph; in a batch of 80 (one-stream graph) it is its own
+    launch after the
     linearisation; in a batch of 300 (the forked graph: more windows than CUs on MI355X) likewise,
     after k_fgrad on the main stream. The tolerance is picked so that the
     oracle converges by it after 5 to 20 iterations (three tolerances, so that the last iteration
