@@ -134,3 +134,29 @@ static __device__ unsigned long long g_pipeClk[16];
 #define PCLK(i, tid)
 #define PCLK_REPORT(T)
 #endif
+
+// ---- k_dogleg (-DOKG_DOGLEG_CLOCK): workgroup 0, thread 0 after an added workgroup barrier per
+// phase (the barriers are part of the clock build only); prints the per-call averages every 200 calls.
+#ifdef OKG_DOGLEG_CLOCK
+static __device__ unsigned long long g_dlClk[8], g_dlCalls;
+#define DLCLK_INIT unsigned long long dlclk = __builtin_amdgcn_s_memrealtime();
+#define DLCLK(i)                                                                \
+  __syncthreads();                                                              \
+  if (blockIdx.x == 0 && threadIdx.x == 0) {                                    \
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();            \
+    g_dlClk[i] += now - dlclk;                                                  \
+    dlclk = now;                                                                \
+  }
+#define DLCLK_END                                                                                        \
+  if (blockIdx.x == 0 && threadIdx.x == 0 && ++g_dlCalls == 200) {                                       \
+    printf("DLCLK per call (x10ns): state %.1f pass1 loads %.1f tree1 %.1f pass2 f %.1f pass2 lm %.1f " \
+           "tree2 %.1f\n", g_dlClk[0] / 200.0, g_dlClk[1] / 200.0, g_dlClk[2] / 200.0, g_dlClk[3] / 200.0, \
+           g_dlClk[4] / 200.0, g_dlClk[5] / 200.0);                                                      \
+    for (int i_ = 0; i_ < 8; ++i_) g_dlClk[i_] = 0;                                                      \
+    g_dlCalls = 0;                                                                                       \
+  }
+#else
+#define DLCLK_INIT
+#define DLCLK(i)
+#define DLCLK_END
+#endif

@@ -16,6 +16,7 @@
 #include <cfloat>
 
 #include "block_reduce.hpp"
+#include "dev_clock.hpp"
 #include "device_problem.hpp"
 #include "gradnorm.hpp"
 #include "jv_groups.hpp"
@@ -219,6 +220,7 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
   const int w = blockIdx.x;
   WinState& s = P.st[w];
   if (s.done) return;
+  DLCLK_INIT
   __shared__ double sh[6 * RB];
   __shared__ int sflag;
   const int t = threadIdx.x;
@@ -259,6 +261,7 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
   }
   __syncthreads();
   if (sflag) return;
+  DLCLK(0)
   const int foff = P.win_foff[w], fd = P.win_fdim[w];
   const int l0 = P.win_lm_range[2 * w], l1 = P.win_lm_range[2 * w + 1];
   // pass 1: norms (f-blocks here, landmarks as the landmark groups' sums of k_lm_backsub_jv)
@@ -284,8 +287,10 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
     double r6[6];
     double a3[3];
     jvPartials(P, w, t, RB, a3);
+    DLCLK(1)
     r6[0] = a3[0]; r6[1] = a3[1]; r6[2] = a3[2]; r6[3] = gg; r6[4] = nn; r6[5] = gn;
     blockSumN<RB, 6>(r6, sh);
+    DLCLK(2)
     gg = r6[3];
     nn = r6[4];
     gn = r6[5];
@@ -386,6 +391,7 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
       sn2 += (x[c] - yv) * (x[c] - yv);
     }
   }
+  DLCLK(3)
   struct LS { double x[4], dg[3], gn[3], dia[3], sl[3], g[3]; uint8_t f; };
   stridedBatched<RB, (RB >= 1024 ? 1 : 4)>(l0, l1,
                     [&](int l) {
@@ -417,6 +423,7 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
                       }
                       y[3] = v.x[3];
                     });
+  DLCLK(4)
   {
     double r3[3] = {sn2, dn2, jr};
     blockSumN<RB, 3>(r3, sh);
@@ -424,6 +431,8 @@ __global__ __launch_bounds__(RB) void k_dogleg(const DevProblem* __restrict__ Pp
     dn2 = r3[1];
     jr = r3[2];
   }
+  DLCLK(5)
+  DLCLK_END
   if (t != 0) return;
   s.dogleg_step_norm = (dcase == 1) ? gauss_newton_norm : (dcase == 2) ? radius : sqrt(dn2);
   s.step_norm = sqrt(sn2);
