@@ -1,5 +1,5 @@
-// dev_clock.hpp — development-only phase clocks of the three kernels whose phases were profiled
-// from the inside (k_cholesky / k_chol_bsub, k_eval_imu, k_lm_visit<1>). Off in every product build:
+// dev_clock.hpp — development-only phase clocks of the kernels whose phases were profiled
+// from the inside (k_cholesky / k_chol_bsub, k_eval_imu, k_lm_visit<1>, k_dogleg). Off in every product build:
 // each macro below expands to nothing unless its OKG_*_CLOCK switch is given on the compiler line
 // (make OPT="-O3 -DOKG_CHOL_CLOCK" etc.). The kernels only name the macros; the clock state and the
 // printf reports live here.
